@@ -1,0 +1,150 @@
+/* plvi_frontend.h — C-ABI of the MI355X-native PL-VI-ORBSLAM3 feature front end.
+ *
+ * Plain pointers and sizes only.  Each entry point replaces one reference
+ * interface (cited per function); the C++ drop-in classes in
+ * pl-vi-orbslam3_amd/host/ (ORBextractor, Lineextractor, ORBmatcher,
+ * LineMatcher) are thin wrappers over these calls, see INTEGRATION.md.
+ *
+ * Status codes: 0 = ok, negative = error (PLVI_E_*).  ORBextractor's
+ * "empty image -> -1" convention (src/ORBextractor.cc:1072-1073) is kept by
+ * plvi_orb_extract returning PLVI_E_EMPTY (-1).
+ *
+ * Threading: handles are independent and may be used from
+ * different host threads concurrently (each owns its device scratch and HIP
+ * stream); one handle is not re-entrant, exactly like the reference
+ * extractor whose operator() mutates mvImagePyramid.
+ */
+#ifndef PLVI_FRONTEND_H
+#define PLVI_FRONTEND_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  PLVI_OK = 0,
+  PLVI_E_EMPTY = -1,    /* empty image (ORBextractor.cc:1072) */
+  PLVI_E_BADARG = -2,   /* bad size / parameter / type */
+  PLVI_E_CAPACITY = -3, /* caller's output capacity too small (count still written) */
+  PLVI_E_HIP = -4,      /* HIP runtime failure */
+  PLVI_E_OVERFLOW = -5, /* internal fixed-capacity table overflowed on device */
+  PLVI_E_SIZE = -6,     /* descriptor row counts differ (LineMatcher.cpp:50-51) */
+};
+
+/* cv::KeyPoint layout (28 bytes): pt.x, pt.y, size, angle, response, octave, class_id. */
+typedef struct plvi_keypoint {
+  float x, y, size, angle, response;
+  int32_t octave, class_id;
+} plvi_keypoint;
+
+/* cv::line_descriptor::KeyLine layout (descriptor_custom.hpp:107-146). */
+typedef struct plvi_keyline {
+  float angle;
+  int32_t class_id;
+  int32_t octave;
+  float pt_x, pt_y;
+  float response;
+  float size;
+  float startPointX, startPointY, endPointX, endPointY;
+  float sPointInOctaveX, sPointInOctaveY, ePointInOctaveX, ePointInOctaveY;
+  float lineLength;
+  int32_t numOfPixels;
+} plvi_keyline;
+
+/* ------------------------------------------------------------------ ORB
+ * Replaces ORB_SLAM3::ORBextractor (include/ORBextractor.h:44-110,
+ * src/ORBextractor.cc:408-1177). */
+typedef struct plvi_orb_extractor plvi_orb_extractor;
+
+typedef struct plvi_orb_params {
+  int nfeatures;      /* ORBextractor(int nfeatures, ...) */
+  float scale_factor; /* float scaleFactor (stored as double, .h:97) */
+  int nlevels;
+  int ini_th_fast;
+  int min_th_fast;
+} plvi_orb_params;
+
+/* Create an extractor for frames of width x height, batches of up to
+ * max_batch frames, on HIP device `device`.  Replaces the constructor
+ * (ORBextractor.cc:408-468). */
+int plvi_orb_create(const plvi_orb_params* p, int width, int height, int max_batch, int device,
+                    plvi_orb_extractor** out);
+int plvi_orb_destroy(plvi_orb_extractor* h);
+
+/* One frame from host memory, synchronous: ORBextractor::operator()
+ * (ORBextractor.cc:1068-1150).  Keypoints are written in the reference's
+ * slot order (mono slots ascending from 0, vLappingArea slots from the back);
+ * descriptors are n x 32 bytes in the same row order.  *n = number of
+ * keypoints, *mono_index = return value of operator() (monoIndex).
+ * Returns PLVI_E_EMPTY for an empty image. */
+int plvi_orb_extract(plvi_orb_extractor* h, const uint8_t* img, int width, int height, size_t stride,
+                     int lap0, int lap1, plvi_keypoint* kps, uint8_t* desc, int cap, int* n, int* mono_index);
+
+/* Batched, device-resident variant: n_frames frames at d_frames (device
+ * pointer, frame f row r at d_frames + f*frame_stride + r*row_stride), all
+ * of the handle's width x height.  Asynchronous on `stream` (hipStream_t,
+ * NULL = the handle's own stream).  Results stay on the device: see
+ * plvi_orb_outputs. */
+int plvi_orb_extract_batch(plvi_orb_extractor* h, const uint8_t* d_frames, int n_frames, size_t frame_stride,
+                           size_t row_stride, int lap0, int lap1, void* stream);
+
+/* Device pointers to the last batch's outputs: keypoints [max_batch][cap],
+ * descriptors [max_batch][cap][32], counts [max_batch], mono [max_batch].
+ * *cap = per-frame keypoint capacity (sum of per-level octree capacities). */
+int plvi_orb_outputs(plvi_orb_extractor* h, plvi_keypoint** d_kps, uint8_t** d_desc, int** d_count, int** d_mono,
+                     int* cap);
+
+/* mvImagePyramid[level] of frame `frame` of the last call (lazy D2H copy).
+ * dst must hold w*h bytes; pass dst=NULL to query the size. */
+int plvi_orb_pyramid_level(plvi_orb_extractor* h, int frame, int level, uint8_t* dst, int* w, int* hgt);
+
+/* GetScaleFactors / GetInverseScaleFactors / GetScaleSigmaSquares /
+ * GetInverseScaleSigmaSquares (include/ORBextractor.h:62-82): nlevels floats each. */
+int plvi_orb_scale_tables(plvi_orb_extractor* h, float* scale, float* inv_scale, float* sigma2, float* inv_sigma2);
+
+/* Per-level feature quota (mnFeaturesPerLevel, ORBextractor.cc:433-444). */
+int plvi_orb_level_quota(plvi_orb_extractor* h, int* quota);
+
+/* Stage timing (HIP events on the launch stream) for bench.py's roofline:
+ * enable=1 resets and starts recording, 0 stops.  profile_read synchronises
+ * and returns per-stage milliseconds summed over the recorded runs (up to
+ * 512): [0] level build (resize+blur+FAST score), [1] cell NMS, [2] SAT,
+ * [3] octree, [4] node best, [5] orientation+rBRIEF, [6] output assembly. */
+int plvi_orb_profile(plvi_orb_extractor* h, int enable);
+int plvi_orb_profile_read(plvi_orb_extractor* h, float* stage_ms, int* runs);
+
+/* ------------------------------------------------------------------ Hamming
+ * ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:2350-2366) over a batch. */
+
+/* cv::BFMatcher(NORM_HAMMING).knnMatch(q, t, k=2) semantics (scan train rows
+ * ascending, strict-< insertion): for each query i, idx0/d0 = best train row
+ * and distance, idx1/d1 = second.  Missing entries are -1 / INT32_MAX.
+ * Batched over n_pairs independent (query,train) pairs; all pointers device.
+ * q: [n_pairs][nq_cap][32], t: [n_pairs][nt_cap][32]; nq/nt: per-pair counts
+ * (device int arrays).  Outputs [n_pairs][nq_cap]. */
+int plvi_hamming_knn2_batch(const uint8_t* d_q, const int* d_nq, int nq_cap, const uint8_t* d_t, const int* d_nt,
+                            int nt_cap, int n_pairs, int* d_idx0, int* d_d0, int* d_idx1, int* d_d1, void* stream);
+
+/* Host convenience wrapper (one pair, synchronous). */
+int plvi_hamming_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int* idx0, int* d0, int* idx1, int* d1);
+
+/* LineMatcher::matchNNR (src/LineMatcher.cpp:41-61): matches_12[i] = train
+ * index or -1; returns the number of matches (>=0) or an error code.
+ * Requires nt >= 2 (the reference indexes matches_[idx][1]). */
+int plvi_line_match_nnr(const uint8_t* desc1, int n1, const uint8_t* desc2, int n2, float nnr, int* matches_12);
+
+/* LineMatcher::match(desc1, desc2, nnr, matches_12) (LineMatcher.cpp:92-111):
+ * matchNNR both ways + mutual check. */
+int plvi_line_match(const uint8_t* desc1, int n1, const uint8_t* desc2, int n2, float nnr, int* matches_12);
+
+/* Device/library information for diagnostics. */
+const char* plvi_version(void);
+int plvi_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PLVI_FRONTEND_H */

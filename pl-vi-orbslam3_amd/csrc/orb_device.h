@@ -1,0 +1,37 @@
+// orb_device.h — device-side tables shared by the ORB kernels and the host
+// pipeline (orb.hip).  All geometry is precomputed on the host exactly as
+// ORBextractor does it (src/ORBextractor.cc:408-468, 771-785, 1156-1157).
+#pragma once
+#include <cstdint>
+
+namespace plvi {
+
+constexpr int kOrbMaxLevels = 16;
+constexpr int kOrbMaxRoots = 8;
+constexpr int kOrbCellMax = 64;  // max detection-window side (wCell+2 < 64)
+
+struct OrbLevelDev {
+    int w, h;
+    long long off;    // byte offset of this level's frame-0 plane in pyr/blur/score/cand
+    long long plane;  // bytes per frame plane (w*h)
+    int minB;         // EDGE_THRESHOLD-3 = 16
+    int rw, rh;       // relative region (maxBorder-minBorder)
+    int nCols, nRows, wCell, hCell;
+    long long satOff;    // int offset of this level's frame-0 SAT
+    long long satPlane;  // ints per frame SAT ((rw+1)*(rh+1))
+    int quota;           // mnFeaturesPerLevel
+    int nodeCap;         // octree output capacity (>= quota+3)
+    int kpOff;           // offset of this level in the per-frame level-keypoint table
+    float scale;         // mvScaleFactor
+    float size;          // (float)(int)(PATCH_SIZE*scale)
+    int nIni;
+    int rootGx[kOrbMaxRoots + 1];  // geometric root x: (int)(hX*i)
+    int rootB[kOrbMaxRoots + 1];   // membership: root i holds x in [rootB[i], rootB[i+1])
+};
+
+struct OrbCellDev {
+    int level;
+    int x0, y0, x1, y1;  // FAST detection window [x0,x1)x[y0,y1) in level coords
+};
+
+}  // namespace plvi

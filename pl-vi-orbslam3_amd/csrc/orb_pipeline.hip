@@ -1,0 +1,462 @@
+// orb_pipeline.hip — host orchestration of the ORB kernels and the ORB part
+// of the C-ABI (include/plvi_frontend.h).  Geometry is derived exactly as
+// ORBextractor does (src/ORBextractor.cc:408-468 ctor, :1152-1177 pyramid,
+// :763-878 cells/borders, :537-561 octree roots).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "orb_device.h"
+#include "plvi_common.h"
+#include "orb_kernels.hpp"
+
+namespace plvi {
+
+static inline int cv_round_h(float v) { return (int)lrintf(v); }
+static inline int cv_round_h(double v) { return (int)lrint(v); }
+static inline int cv_floor_h(float v) { int i = (int)v; return i - (i > v); }
+static inline int cv_ceil_h(float v) { int i = (int)v; return i + (i < v); }
+
+struct ResizeTab {
+    std::vector<int> xofs, yrow;
+    std::vector<short> xa, yb;
+    int xmax = 0;
+};
+
+// cv::resize INTER_LINEAR coefficient tables (imgproc/src/resize.cpp, 4.2).
+static ResizeTab make_resize_tab(int sw, int sh, int dw, int dh) {
+    ResizeTab t;
+    const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
+    t.xofs.resize(dw);
+    t.xa.resize(2 * dw);
+    t.xmax = dw;
+    for (int dx = 0; dx < dw; ++dx) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = cv_floor_h(fx);
+        fx -= sx;
+        if (sx < 0) { fx = 0; sx = 0; }
+        if (sx + 1 >= sw) {
+            t.xmax = std::min(t.xmax, dx);
+            if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+        }
+        t.xofs[dx] = sx;
+        t.xa[2 * dx] = (short)cv_round_h((1.f - fx) * 2048);
+        t.xa[2 * dx + 1] = (short)cv_round_h(fx * 2048);
+    }
+    t.yrow.resize(2 * dh);
+    t.yb.resize(2 * dh);
+    for (int dy = 0; dy < dh; ++dy) {
+        float fy = (float)((dy + 0.5) * scale_y - 0.5);
+        int sy = cv_floor_h(fy);
+        fy -= sy;
+        t.yrow[2 * dy] = std::min(std::max(sy, 0), sh - 1);
+        t.yrow[2 * dy + 1] = std::min(std::max(sy + 1, 0), sh - 1);
+        t.yb[2 * dy] = (short)cv_round_h((1.f - fy) * 2048);
+        t.yb[2 * dy + 1] = (short)cv_round_h(fy * 2048);
+    }
+    return t;
+}
+
+struct OrbPipeline {
+    plvi_orb_params prm{};
+    int W = 0, H = 0, Bcap = 0, device = 0, L = 0;
+    hipStream_t stream = nullptr;
+    std::vector<float> scale, invScale, sigma2, invSigma2;
+    std::vector<int> quota, umax;
+    std::vector<OrbLevelDev> lv;
+    std::vector<OrbCellDev> cells;
+    std::vector<ResizeTab> rtab;
+    int taps[7]{};
+    int kpCapFrame = 0, nodeCapMax = 0;
+    size_t pyrBytesFrameTotal = 0, satIntsFrameTotal = 0;
+    size_t lvOff0 = 0;  // (unused)
+    DevBuf d_lv, d_cells, d_tabs, pyr, blur, score, cand, sat, rects, rectCnt, lvkp, lvdesc, okp, odesc, ocount,
+        omono, err, staging;
+    std::vector<size_t> tabXofs, tabXa, tabYrow, tabYb;  // byte offsets in d_tabs per level
+    int lastFrames = 0;
+    // Stage timing with HIP events on the launch stream (bench.py roofline).
+    static constexpr int kStages = 7, kRing = 512;
+    bool prof = false;
+    int profRuns = 0;
+    std::vector<hipEvent_t> evs;  // kRing * (kStages+1)
+
+    ~OrbPipeline() {
+        for (auto e : evs) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    int profile(int on) {
+        if (on && evs.empty()) {
+            evs.resize((size_t)kRing * (kStages + 1));
+            for (auto& e : evs) PLVI_CHECK(hipEventCreate(&e));
+        }
+        prof = on != 0;
+        profRuns = 0;
+        return PLVI_OK;
+    }
+    void mark(int stage, hipStream_t st) {
+        if (prof && profRuns < kRing) (void)hipEventRecord(evs[(size_t)profRuns * (kStages + 1) + stage], st);
+    }
+    int profile_read(float* ms, int* runs) {
+        for (int k = 0; k < kStages; ++k) ms[k] = 0.f;
+        for (int r = 0; r < profRuns; ++r) {
+            PLVI_CHECK(hipEventSynchronize(evs[(size_t)r * (kStages + 1) + kStages]));
+            for (int k = 0; k < kStages; ++k) {
+                float t = 0.f;
+                PLVI_CHECK(hipEventElapsedTime(&t, evs[(size_t)r * (kStages + 1) + k],
+                                               evs[(size_t)r * (kStages + 1) + k + 1]));
+                ms[k] += t;
+            }
+        }
+        if (runs) *runs = profRuns;
+        return PLVI_OK;
+    }
+
+    int init(const plvi_orb_params* p, int width, int height, int max_batch, int dev) {
+        if (!p || width <= 0 || height <= 0 || max_batch <= 0 || p->nlevels <= 0 ||
+            p->nlevels > kOrbMaxLevels || p->nfeatures < 0 || !(p->scale_factor > 1.0f))
+            return PLVI_E_BADARG;
+        prm = *p;
+        W = width; H = height; Bcap = max_batch; device = dev; L = p->nlevels;
+        PLVI_CHECK(hipSetDevice(device));
+        PLVI_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        // ORBextractor ctor (ORBextractor.cc:413-444): scaleFactor is a double member.
+        const double sf = (double)p->scale_factor;
+        scale.assign(L, 1.f); sigma2.assign(L, 1.f);
+        for (int i = 1; i < L; ++i) {
+            scale[i] = (float)(scale[i - 1] * sf);
+            sigma2[i] = scale[i] * scale[i];
+        }
+        invScale.resize(L); invSigma2.resize(L);
+        for (int i = 0; i < L; ++i) { invScale[i] = 1.0f / scale[i]; invSigma2[i] = 1.0f / sigma2[i]; }
+        quota.assign(L, 0);
+        float factor = (float)(1.0f / sf);
+        float nDesired = p->nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)L));
+        int sum = 0;
+        for (int l = 0; l < L - 1; ++l) {
+            quota[l] = cv_round_h(nDesired);
+            sum += quota[l];
+            nDesired *= factor;
+        }
+        quota[L - 1] = std::max(p->nfeatures - sum, 0);
+        umax.assign(16, 0);
+        {
+            int v, v0, vmax = cv_floor_h(15 * std::sqrt(2.f) / 2 + 1);
+            int vmin = cv_ceil_h(15 * std::sqrt(2.f) / 2);
+            const double hp2 = 15 * 15;
+            for (v = 0; v <= vmax; ++v) umax[v] = cv_round_h(std::sqrt(hp2 - v * v));
+            for (v = 15, v0 = 0; v >= vmin; --v) {
+                while (umax[v0] == umax[v0 + 1]) ++v0;
+                umax[v] = v0;
+                ++v0;
+            }
+        }
+        // 7x7 sigma=2 fixed-point taps (error-diffused): [18,34,48,56,48,34,18]
+        const int t7[7] = {18, 34, 48, 56, 48, 34, 18};
+        std::memcpy(taps, t7, sizeof(taps));
+        // Levels
+        lv.resize(L);
+        rtab.resize(L);
+        size_t off = 0, satOff = 0;
+        int kpOff = 0;
+        nodeCapMax = 0;
+        for (int l = 0; l < L; ++l) {
+            OrbLevelDev& d = lv[l];
+            std::memset(&d, 0, sizeof(d));
+            d.w = cv_round_h((float)W * invScale[l]);
+            d.h = cv_round_h((float)H * invScale[l]);
+            d.plane = (long long)d.w * d.h;
+            d.off = (long long)off;
+            off += (size_t)d.plane * Bcap;
+            d.minB = 16;
+            const int maxBX = d.w - 16, maxBY = d.h - 16;
+            d.rw = maxBX - d.minB;
+            d.rh = maxBY - d.minB;
+            const float width = (float)d.rw, height = (float)d.rh;
+            d.nCols = (int)(width / 30.f);
+            d.nRows = (int)(height / 30.f);
+            if (d.nCols <= 0 || d.nRows <= 0) return PLVI_E_BADARG;
+            d.wCell = (int)std::ceil(width / d.nCols);
+            d.hCell = (int)std::ceil(height / d.nRows);
+            if (d.wCell + 6 > kOrbCellMax || d.hCell + 6 > kOrbCellMax) return PLVI_E_BADARG;
+            d.satPlane = (long long)(d.rw + 1) * (d.rh + 1);
+            d.satOff = (long long)satOff;
+            satOff += (size_t)d.satPlane * Bcap;
+            d.quota = quota[l];
+            d.scale = scale[l];
+            d.size = (float)(int)(31 * scale[l]);
+            // octree roots (ORBextractor.cc:541-567)
+            const int nIni = (int)std::round((float)(maxBX - d.minB) / (maxBY - d.minB));
+            if (nIni <= 0 || nIni > kOrbMaxRoots) return PLVI_E_BADARG;
+            d.nIni = nIni;
+            const float hX = (float)(maxBX - d.minB) / nIni;
+            for (int i = 0; i <= nIni; ++i) d.rootGx[i] = (int)(hX * (float)i);
+            // membership boundaries: root(x) = (int)(x / hX) for integer x
+            d.rootB[0] = 0;
+            for (int i = 1; i <= nIni; ++i) {
+                int b = d.rootB[i - 1];
+                while (b < d.rw && (int)((float)b / hX) < i) ++b;
+                d.rootB[i] = b;
+            }
+            d.rootB[nIni] = d.rw;
+            d.nodeCap = std::max(d.quota, 4 * nIni) + 8;
+            d.kpOff = kpOff;
+            kpOff += d.nodeCap;
+            nodeCapMax = std::max(nodeCapMax, d.nodeCap);
+            // cells (ORBextractor.cc:787-806): FAST detection windows
+            for (int i = 0; i < d.nRows; ++i) {
+                const float iniY = (float)(d.minB + i * d.hCell);
+                float maxY = iniY + d.hCell + 6;
+                if (iniY >= maxBY - 3) continue;
+                if (maxY > maxBY) maxY = (float)maxBY;
+                for (int j = 0; j < d.nCols; ++j) {
+                    const float iniX = (float)(d.minB + j * d.wCell);
+                    float maxX = iniX + d.wCell + 6;
+                    if (iniX >= maxBX - 6) continue;
+                    if (maxX > maxBX) maxX = (float)maxBX;
+                    OrbCellDev c;
+                    c.level = l;
+                    c.x0 = (int)iniX + 3; c.y0 = (int)iniY + 3;
+                    c.x1 = (int)maxX - 3; c.y1 = (int)maxY - 3;
+                    if (c.x1 > c.x0 && c.y1 > c.y0) cells.push_back(c);
+                }
+            }
+            if (l > 0) rtab[l] = make_resize_tab(lv[l - 1].w, lv[l - 1].h, d.w, d.h);
+        }
+        kpCapFrame = kpOff;
+        pyrBytesFrameTotal = off;
+        satIntsFrameTotal = satOff;
+        // device tables
+        if (d_lv.alloc(sizeof(OrbLevelDev) * L) || d_cells.alloc(sizeof(OrbCellDev) * cells.size()))
+            return PLVI_E_HIP;
+        PLVI_CHECK(hipMemcpy(d_lv.p, lv.data(), sizeof(OrbLevelDev) * L, hipMemcpyHostToDevice));
+        PLVI_CHECK(hipMemcpy(d_cells.p, cells.data(), sizeof(OrbCellDev) * cells.size(), hipMemcpyHostToDevice));
+        std::vector<uint8_t> tabs;
+        tabXofs.assign(L, 0); tabXa.assign(L, 0); tabYrow.assign(L, 0); tabYb.assign(L, 0);
+        auto put = [&](const void* src, size_t n) {
+            size_t o = (tabs.size() + 15) & ~size_t(15);
+            tabs.resize(o + n);
+            std::memcpy(tabs.data() + o, src, n);
+            return o;
+        };
+        for (int l = 1; l < L; ++l) {
+            tabXofs[l] = put(rtab[l].xofs.data(), rtab[l].xofs.size() * 4);
+            tabXa[l] = put(rtab[l].xa.data(), rtab[l].xa.size() * 2);
+            tabYrow[l] = put(rtab[l].yrow.data(), rtab[l].yrow.size() * 4);
+            tabYb[l] = put(rtab[l].yb.data(), rtab[l].yb.size() * 2);
+        }
+        if (tabs.empty()) tabs.resize(16);
+        if (d_tabs.alloc(tabs.size())) return PLVI_E_HIP;
+        PLVI_CHECK(hipMemcpy(d_tabs.p, tabs.data(), tabs.size(), hipMemcpyHostToDevice));
+        PLVI_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax.data(), 16 * sizeof(int)));
+        // work buffers
+        if (pyr.alloc(off) || blur.alloc(off) || score.alloc(off) || cand.alloc(off) ||
+            sat.alloc(satOff * sizeof(int)) || rects.alloc(sizeof(short4) * (size_t)nodeCapMax * L * Bcap) ||
+            rectCnt.alloc(sizeof(int) * L * Bcap) || lvkp.alloc(sizeof(float4) * (size_t)kpCapFrame * Bcap) ||
+            lvdesc.alloc((size_t)32 * kpCapFrame * Bcap) || okp.alloc(sizeof(plvi_keypoint) * (size_t)kpCapFrame * Bcap) ||
+            odesc.alloc((size_t)32 * kpCapFrame * Bcap) || ocount.alloc(sizeof(int) * Bcap) ||
+            omono.alloc(sizeof(int) * Bcap) || err.alloc(sizeof(int)) || staging.alloc((size_t)W * H))
+            return PLVI_E_HIP;
+        PLVI_CHECK(hipMemset(err.p, 0, sizeof(int)));
+        return PLVI_OK;
+    }
+
+    // The whole batch pipeline, asynchronous on `st`.
+    int run(const uint8_t* d_frames, int nf, size_t frame_stride, size_t row_stride, int lap0, int lap1,
+            hipStream_t st) {
+        if (nf <= 0 || nf > Bcap) return PLVI_E_BADARG;
+        if (!st) st = stream;
+        lastFrames = nf;
+        const int tmin = std::max(0, std::min(std::min(prm.ini_th_fast, prm.min_th_fast), 255));
+        const int t1 = std::max(0, std::min(prm.ini_th_fast, 255)), t2 = std::max(0, std::min(prm.min_th_fast, 255));
+        uint8_t* P = pyr.as<uint8_t>();
+        uint8_t* Bl = blur.as<uint8_t>();
+        uint8_t* Sc = score.as<uint8_t>();
+        uint8_t* Cd = cand.as<uint8_t>();
+        const uint8_t* T = d_tabs.as<uint8_t>();
+        mark(0, st);
+        // K1 per level
+        for (int l = 0; l < L; ++l) {
+            const OrbLevelDev& d = lv[l];
+            dim3 grid((d.w + kTWh - 1) / kTWh, (d.h + kTHh - 1) / kTHh, nf);
+            if (l == 0) {
+                hipLaunchKernelGGL(orb_level_kernel<false>, grid, dim3(256), 0, st, d_frames, frame_stride, row_stride,
+                                   P + d.off, Bl + d.off, Sc + d.off, d.w, d.h, (size_t)d.plane, nullptr, nullptr, 0,
+                                   nullptr, nullptr, taps[0], taps[1], taps[2], taps[3], tmin);
+            } else {
+                const OrbLevelDev& s = lv[l - 1];
+                hipLaunchKernelGGL(orb_level_kernel<true>, grid, dim3(256), 0, st, (const uint8_t*)(P + s.off),
+                                   (size_t)s.plane, (size_t)s.w, P + d.off, Bl + d.off, Sc + d.off, d.w, d.h,
+                                   (size_t)d.plane, (const int*)(T + tabXofs[l]), (const short*)(T + tabXa[l]),
+                                   rtab[l].xmax, (const int*)(T + tabYrow[l]), (const short*)(T + tabYb[l]), taps[0],
+                                   taps[1], taps[2], taps[3], tmin);
+            }
+        }
+        mark(1, st);
+        // K2 cell NMS -> candidate map (zeroed first: only detection windows are written)
+        PLVI_CHECK(hipMemsetAsync(Cd, 0, pyrBytesFrameTotal, st));
+        hipLaunchKernelGGL(orb_cell_nms_kernel, dim3((unsigned)cells.size(), nf), dim3(64), 0, st,
+                           d_cells.as<OrbCellDev>(), d_lv.as<OrbLevelDev>(), (const uint8_t*)Sc, Cd, t1, t2);
+        mark(2, st);
+        // K3 SAT
+        int maxRh = 0, maxRw = 0;
+        for (auto& d : lv) { maxRh = std::max(maxRh, d.rh); maxRw = std::max(maxRw, d.rw); }
+        hipLaunchKernelGGL(orb_sat_rows_kernel, dim3(maxRh + 1, L, nf), dim3(64), 0, st, d_lv.as<OrbLevelDev>(),
+                           (const uint8_t*)Cd, sat.as<int>());
+        hipLaunchKernelGGL(orb_sat_cols_kernel, dim3((maxRw + 1 + 255) / 256, L, nf), dim3(256), 0, st,
+                           d_lv.as<OrbLevelDev>(), sat.as<int>());
+        mark(3, st);
+        // K4 octree
+        const size_t smem = (size_t)nodeCapMax * (2 * 4 + 13 * 2 + 1) + 16;
+        hipLaunchKernelGGL(orb_octree_kernel, dim3(L, nf), dim3(64), smem, st, d_lv.as<OrbLevelDev>(),
+                           (const int*)sat.as<int>(), rects.as<short4>(), rectCnt.as<int>(), nodeCapMax, L,
+                           err.as<int>());
+        mark(4, st);
+        // K5 best per node
+        hipLaunchKernelGGL(orb_node_best_kernel, dim3(nodeCapMax, L, nf), dim3(64), 0, st, d_lv.as<OrbLevelDev>(),
+                           (const uint8_t*)Cd, (const short4*)rects.as<short4>(), (const int*)rectCnt.as<int>(),
+                           nodeCapMax, L, lvkp.as<float4>(), kpCapFrame);
+        mark(5, st);
+        // K6 orientation + rBRIEF
+        hipLaunchKernelGGL(orb_describe_kernel, dim3((kpCapFrame + 255) / 256, nf), dim3(256), 0, st,
+                           d_lv.as<OrbLevelDev>(), L, (const uint8_t*)P, (const uint8_t*)Bl,
+                           (const int*)rectCnt.as<int>(), lvkp.as<float4>(), lvdesc.as<uint8_t>(), kpCapFrame);
+        mark(6, st);
+        // K7 assemble
+        hipLaunchKernelGGL(orb_assemble_kernel, dim3(nf), dim3(256), 0, st, d_lv.as<OrbLevelDev>(), L,
+                           (const int*)rectCnt.as<int>(), (const float4*)lvkp.as<float4>(),
+                           (const uint8_t*)lvdesc.as<uint8_t>(), kpCapFrame, lap0, lap1, okp.as<plvi_keypoint>(),
+                           odesc.as<uint8_t>(), ocount.as<int>(), omono.as<int>());
+        mark(7, st);
+        if (prof && profRuns < kRing) ++profRuns;
+        PLVI_CHECK(hipGetLastError());
+        return PLVI_OK;
+    }
+
+    static constexpr int kTWh = 64, kTHh = 16;
+};
+
+}  // namespace plvi
+
+using plvi::OrbPipeline;
+
+struct plvi_orb_extractor {
+    OrbPipeline p;
+};
+
+extern "C" int plvi_orb_create(const plvi_orb_params* p, int width, int height, int max_batch, int device,
+                               plvi_orb_extractor** out) {
+    if (!out) return PLVI_E_BADARG;
+    *out = nullptr;
+    auto h = std::make_unique<plvi_orb_extractor>();
+    int rc = h->p.init(p, width, height, max_batch, device);
+    if (rc) return rc;
+    *out = h.release();
+    return PLVI_OK;
+}
+
+extern "C" int plvi_orb_destroy(plvi_orb_extractor* h) {
+    if (!h) return PLVI_E_BADARG;
+    (void)hipSetDevice(h->p.device);
+    (void)hipStreamSynchronize(h->p.stream);
+    delete h;
+    return PLVI_OK;
+}
+
+extern "C" int plvi_orb_extract_batch(plvi_orb_extractor* h, const uint8_t* d_frames, int n_frames,
+                                      size_t frame_stride, size_t row_stride, int lap0, int lap1, void* stream) {
+    if (!h || !d_frames) return PLVI_E_BADARG;
+    PLVI_CHECK(hipSetDevice(h->p.device));
+    return h->p.run(d_frames, n_frames, frame_stride, row_stride, lap0, lap1, (hipStream_t)stream);
+}
+
+extern "C" int plvi_orb_outputs(plvi_orb_extractor* h, plvi_keypoint** d_kps, uint8_t** d_desc, int** d_count,
+                                int** d_mono, int* cap) {
+    if (!h) return PLVI_E_BADARG;
+    if (d_kps) *d_kps = h->p.okp.as<plvi_keypoint>();
+    if (d_desc) *d_desc = h->p.odesc.as<uint8_t>();
+    if (d_count) *d_count = h->p.ocount.as<int>();
+    if (d_mono) *d_mono = h->p.omono.as<int>();
+    if (cap) *cap = h->p.kpCapFrame;
+    return PLVI_OK;
+}
+
+extern "C" int plvi_orb_extract(plvi_orb_extractor* h, const uint8_t* img, int width, int height, size_t stride,
+                                int lap0, int lap1, plvi_keypoint* kps, uint8_t* desc, int cap, int* n,
+                                int* mono_index) {
+    if (!h) return PLVI_E_BADARG;
+    if (n) *n = 0;
+    if (!img || width <= 0 || height <= 0) return PLVI_E_EMPTY;  // _image.empty() -> -1
+    OrbPipeline& P = h->p;
+    if (width != P.W || height != P.H) return PLVI_E_BADARG;
+    PLVI_CHECK(hipSetDevice(P.device));
+    PLVI_CHECK(hipMemcpy2DAsync(P.staging.p, (size_t)P.W, img, stride, (size_t)P.W, (size_t)P.H,
+                                hipMemcpyHostToDevice, P.stream));
+    int rc = P.run(P.staging.as<uint8_t>(), 1, (size_t)P.W * P.H, (size_t)P.W, lap0, lap1, P.stream);
+    if (rc) return rc;
+    int cnt = 0, mono = 0, errv = 0;
+    PLVI_CHECK(hipMemcpyAsync(&cnt, P.ocount.p, sizeof(int), hipMemcpyDeviceToHost, P.stream));
+    PLVI_CHECK(hipMemcpyAsync(&mono, P.omono.p, sizeof(int), hipMemcpyDeviceToHost, P.stream));
+    PLVI_CHECK(hipMemcpyAsync(&errv, P.err.p, sizeof(int), hipMemcpyDeviceToHost, P.stream));
+    PLVI_CHECK(hipStreamSynchronize(P.stream));
+    if (errv) {
+        PLVI_CHECK(hipMemset(P.err.p, 0, sizeof(int)));
+        return PLVI_E_OVERFLOW;
+    }
+    if (n) *n = cnt;
+    if (mono_index) *mono_index = mono;
+    if (cnt > cap) return PLVI_E_CAPACITY;
+    if (cnt > 0) {
+        if (kps) PLVI_CHECK(hipMemcpy(kps, P.okp.p, sizeof(plvi_keypoint) * cnt, hipMemcpyDeviceToHost));
+        if (desc) PLVI_CHECK(hipMemcpy(desc, P.odesc.p, (size_t)32 * cnt, hipMemcpyDeviceToHost));
+    }
+    return PLVI_OK;
+}
+
+extern "C" int plvi_orb_pyramid_level(plvi_orb_extractor* h, int frame, int level, uint8_t* dst, int* w, int* hgt) {
+    if (!h || level < 0 || level >= h->p.L || frame < 0 || frame >= h->p.Bcap) return PLVI_E_BADARG;
+    const auto& d = h->p.lv[level];
+    if (w) *w = d.w;
+    if (hgt) *hgt = d.h;
+    if (!dst) return PLVI_OK;
+    PLVI_CHECK(hipSetDevice(h->p.device));
+    PLVI_CHECK(hipStreamSynchronize(h->p.stream));
+    PLVI_CHECK(hipMemcpy(dst, h->p.pyr.as<uint8_t>() + d.off + (size_t)frame * d.plane, (size_t)d.plane,
+                         hipMemcpyDeviceToHost));
+    return PLVI_OK;
+}
+
+extern "C" int plvi_orb_scale_tables(plvi_orb_extractor* h, float* scale, float* inv_scale, float* sigma2,
+                                     float* inv_sigma2) {
+    if (!h) return PLVI_E_BADARG;
+    const auto& P = h->p;
+    for (int i = 0; i < P.L; ++i) {
+        if (scale) scale[i] = P.scale[i];
+        if (inv_scale) inv_scale[i] = P.invScale[i];
+        if (sigma2) sigma2[i] = P.sigma2[i];
+        if (inv_sigma2) inv_sigma2[i] = P.invSigma2[i];
+    }
+    return PLVI_OK;
+}
+
+extern "C" int plvi_orb_level_quota(plvi_orb_extractor* h, int* q) {
+    if (!h || !q) return PLVI_E_BADARG;
+    for (int i = 0; i < h->p.L; ++i) q[i] = h->p.quota[i];
+    return PLVI_OK;
+}
+
+extern "C" int plvi_orb_profile(plvi_orb_extractor* h, int enable) {
+    if (!h) return PLVI_E_BADARG;
+    PLVI_CHECK(hipSetDevice(h->p.device));
+    return h->p.profile(enable);
+}
+
+extern "C" int plvi_orb_profile_read(plvi_orb_extractor* h, float* stage_ms, int* runs) {
+    if (!h || !stage_ms) return PLVI_E_BADARG;
+    PLVI_CHECK(hipSetDevice(h->p.device));
+    return h->p.profile_read(stage_ms, runs);
+}

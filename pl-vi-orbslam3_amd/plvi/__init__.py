@@ -1,0 +1,261 @@
+"""plvi — Python host mirror of the MI355X front end's C-ABI.
+
+Thin ctypes layer over ``lib/libplvi_frontend.so`` (built from ``csrc/``).
+Class and method names follow the reference interfaces they replace:
+
+  ORBextractor  -> ORB_SLAM3::ORBextractor (include/ORBextractor.h:44-110)
+  LineMatcher   -> ORB_SLAM3::LineMatcher  (include/LineMatcher.h:88-107)
+  hamming_knn2  -> cv::BFMatcher(NORM_HAMMING).knnMatch(k=2) (LineMatcher.cpp:47-48)
+
+There is no CPU fallback: if the HIP library is missing or no GPU is
+visible, construction raises.  PyTorch is only used by bench.py for device
+memory and streams; this module needs numpy only.
+"""
+import ctypes
+import os
+import pathlib
+
+import numpy as np
+
+_PKG = pathlib.Path(__file__).resolve().parent.parent
+LIB_PATH = _PKG / "lib" / "libplvi_frontend.so"
+HEADER_PATH = _PKG.parent / "include" / "plvi_frontend.h"
+
+PLVI_OK = 0
+PLVI_E_EMPTY = -1
+PLVI_E_BADARG = -2
+PLVI_E_CAPACITY = -3
+PLVI_E_HIP = -4
+PLVI_E_OVERFLOW = -5
+PLVI_E_SIZE = -6
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+KEYLINE_DTYPE = np.dtype([("angle", "<f4"), ("class_id", "<i4"), ("octave", "<i4"), ("pt_x", "<f4"),
+                          ("pt_y", "<f4"), ("response", "<f4"), ("size", "<f4"), ("startPointX", "<f4"),
+                          ("startPointY", "<f4"), ("endPointX", "<f4"), ("endPointY", "<f4"),
+                          ("sPointInOctaveX", "<f4"), ("sPointInOctaveY", "<f4"), ("ePointInOctaveX", "<f4"),
+                          ("ePointInOctaveY", "<f4"), ("lineLength", "<f4"), ("numOfPixels", "<i4")])
+
+
+class PlviError(RuntimeError):
+    def __init__(self, code, what):
+        super().__init__(f"{what} failed with status {code}")
+        self.code = code
+
+
+class OrbParams(ctypes.Structure):
+    _fields_ = [("nfeatures", ctypes.c_int), ("scale_factor", ctypes.c_float), ("nlevels", ctypes.c_int),
+                ("ini_th_fast", ctypes.c_int), ("min_th_fast", ctypes.c_int)]
+
+
+_lib = None
+
+c_int_p = ctypes.POINTER(ctypes.c_int)
+c_void_pp = ctypes.POINTER(ctypes.c_void_p)
+
+
+def _declare(lib):
+    V, I, S, F, P = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_float, c_int_p
+    sig = {
+        "plvi_version": ([], ctypes.c_char_p),
+        "plvi_device_count": ([], I),
+        "plvi_orb_create": ([ctypes.POINTER(OrbParams), I, I, I, I, c_void_pp], I),
+        "plvi_orb_destroy": ([V], I),
+        "plvi_orb_extract": ([V, V, I, I, S, I, I, V, V, I, P, P], I),
+        "plvi_orb_extract_batch": ([V, V, I, S, S, I, I, V], I),
+        "plvi_orb_outputs": ([V, c_void_pp, c_void_pp, c_void_pp, c_void_pp, P], I),
+        "plvi_orb_pyramid_level": ([V, I, I, V, P, P], I),
+        "plvi_orb_scale_tables": ([V, V, V, V, V], I),
+        "plvi_orb_level_quota": ([V, V], I),
+        "plvi_orb_profile": ([V, I], I),
+        "plvi_orb_profile_read": ([V, V, P], I),
+        "plvi_hamming_knn2_batch": ([V, V, I, V, V, I, I, V, V, V, V, V], I),
+        "plvi_hamming_knn2": ([V, I, V, I, V, V, V, V], I),
+        "plvi_line_match_nnr": ([V, I, V, I, F, V], I),
+        "plvi_line_match": ([V, I, V, I, F, V], I),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    return lib
+
+
+def load():
+    """Load the HIP library (raises if it was not built: there is no fallback)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"{LIB_PATH} missing: build it with `make -C pl-vi-orbslam3_amd`")
+        _lib = _declare(ctypes.CDLL(str(LIB_PATH)))
+    return _lib
+
+
+def exported_symbols():
+    """Function names declared in include/plvi_frontend.h."""
+    import re
+    txt = HEADER_PATH.read_text()
+    return sorted(set(re.findall(r"\b(plvi_[a-z0-9_]+)\s*\(", txt)))
+
+
+def _check(rc, what):
+    if rc < 0:
+        raise PlviError(rc, what)
+    return rc
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+class ORBextractor:
+    """ORB_SLAM3::ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST).
+
+    ``extractor(image, mask, vLappingArea)`` returns ``(monoIndex, keypoints,
+    descriptors)`` like operator() (src/ORBextractor.cc:1068): keypoints is a
+    structured array in cv::KeyPoint layout, descriptors an N x 32 uint8 array.
+    An empty image returns ``(-1, empty, empty)``.
+    """
+
+    def __init__(self, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, width=640, height=480,
+                 max_batch=1, device=0):
+        self._lib = load()
+        self.params = OrbParams(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
+        self.width, self.height, self.max_batch = width, height, max_batch
+        self.nlevels = nlevels
+        h = ctypes.c_void_p()
+        _check(self._lib.plvi_orb_create(ctypes.byref(self.params), width, height, max_batch, device,
+                                         ctypes.byref(h)), "plvi_orb_create")
+        self._h = h
+        cap = ctypes.c_int()
+        self._lib.plvi_orb_outputs(self._h, None, None, None, None, ctypes.byref(cap))
+        self.kp_cap = cap.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.plvi_orb_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __call__(self, image, mask=None, vLappingArea=(0, 0)):
+        if image is None or image.size == 0:
+            return -1, np.zeros(0, KEYPOINT_DTYPE), np.zeros((0, 32), np.uint8)
+        image = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = image.shape
+        kps = np.zeros(self.kp_cap, KEYPOINT_DTYPE)
+        desc = np.zeros((self.kp_cap, 32), np.uint8)
+        n, mono = ctypes.c_int(), ctypes.c_int()
+        rc = self._lib.plvi_orb_extract(self._h, _ptr(image), w, h, w, int(vLappingArea[0]),
+                                        int(vLappingArea[1]), _ptr(kps), _ptr(desc), self.kp_cap,
+                                        ctypes.byref(n), ctypes.byref(mono))
+        _check(rc, "plvi_orb_extract")
+        return mono.value, kps[:n.value].copy(), desc[:n.value].copy()
+
+    # --- batched device path (bench / multi-frame) ---------------------------
+    def extract_batch(self, d_frames_ptr, n_frames, frame_stride, row_stride, lap=(0, 0), stream=None):
+        _check(self._lib.plvi_orb_extract_batch(self._h, ctypes.c_void_p(d_frames_ptr), n_frames, frame_stride,
+                                                row_stride, lap[0], lap[1], ctypes.c_void_p(stream or 0)),
+               "plvi_orb_extract_batch")
+
+    def outputs(self):
+        """Device pointers (kps, desc, count, mono) and per-frame capacity."""
+        kp, de, co, mo = (ctypes.c_void_p() for _ in range(4))
+        cap = ctypes.c_int()
+        _check(self._lib.plvi_orb_outputs(self._h, ctypes.byref(kp), ctypes.byref(de), ctypes.byref(co),
+                                          ctypes.byref(mo), ctypes.byref(cap)), "plvi_orb_outputs")
+        return kp.value, de.value, co.value, mo.value, cap.value
+
+    ORB_STAGES = ("level", "nms", "sat", "octree", "best", "describe", "assemble")
+
+    def profile(self, enable=True):
+        _check(self._lib.plvi_orb_profile(self._h, int(enable)), "plvi_orb_profile")
+
+    def profile_read(self):
+        ms = np.zeros(7, np.float32)
+        runs = ctypes.c_int()
+        _check(self._lib.plvi_orb_profile_read(self._h, _ptr(ms), ctypes.byref(runs)), "plvi_orb_profile_read")
+        return dict(zip(self.ORB_STAGES, ms.tolist())), runs.value
+
+    # --- reference getters ---------------------------------------------------
+    def _tables(self):
+        out = [np.zeros(self.nlevels, np.float32) for _ in range(4)]
+        _check(self._lib.plvi_orb_scale_tables(self._h, *[_ptr(a) for a in out]), "plvi_orb_scale_tables")
+        return out
+
+    def GetLevels(self):
+        return self.nlevels
+
+    def GetScaleFactor(self):
+        return float(np.float32(self.params.scale_factor))
+
+    def GetScaleFactors(self):
+        return self._tables()[0]
+
+    def GetInverseScaleFactors(self):
+        return self._tables()[1]
+
+    def GetScaleSigmaSquares(self):
+        return self._tables()[2]
+
+    def GetInverseScaleSigmaSquares(self):
+        return self._tables()[3]
+
+    def level_quota(self):
+        q = np.zeros(self.nlevels, np.int32)
+        _check(self._lib.plvi_orb_level_quota(self._h, _ptr(q)), "plvi_orb_level_quota")
+        return q
+
+    def pyramid_level(self, level, frame=0):
+        """mvImagePyramid[level] of the last call (lazy D2H)."""
+        w, h = ctypes.c_int(), ctypes.c_int()
+        _check(self._lib.plvi_orb_pyramid_level(self._h, frame, level, None, ctypes.byref(w), ctypes.byref(h)),
+               "plvi_orb_pyramid_level")
+        out = np.zeros((h.value, w.value), np.uint8)
+        _check(self._lib.plvi_orb_pyramid_level(self._h, frame, level, _ptr(out), None, None),
+               "plvi_orb_pyramid_level")
+        return out
+
+    @property
+    def mvImagePyramid(self):
+        return [self.pyramid_level(l) for l in range(self.nlevels)]
+
+
+def hamming_knn2(q, t):
+    """BFMatcher(NORM_HAMMING).knnMatch(q, t, 2) -> (idx0, d0, idx1, d1) arrays."""
+    lib = load()
+    q = np.ascontiguousarray(q, np.uint8)
+    t = np.ascontiguousarray(t, np.uint8)
+    nq, nt = q.shape[0], t.shape[0]
+    out = [np.zeros(nq, np.int32) for _ in range(4)]
+    _check(lib.plvi_hamming_knn2(_ptr(q), nq, _ptr(t), nt, *[_ptr(o) for o in out]), "plvi_hamming_knn2")
+    return tuple(out)
+
+
+class LineMatcher:
+    """ORB_SLAM3::LineMatcher static Hamming matchers (src/LineMatcher.cpp)."""
+
+    @staticmethod
+    def matchNNR(desc1, desc2, nnr):
+        lib = load()
+        d1 = np.ascontiguousarray(desc1, np.uint8)
+        d2 = np.ascontiguousarray(desc2, np.uint8)
+        m = np.full(d1.shape[0], -1, np.int32)
+        n = _check(lib.plvi_line_match_nnr(_ptr(d1), d1.shape[0], _ptr(d2), d2.shape[0], nnr, _ptr(m)),
+                   "plvi_line_match_nnr")
+        return n, m
+
+    @staticmethod
+    def match(desc1, desc2, nnr):
+        lib = load()
+        d1 = np.ascontiguousarray(desc1, np.uint8)
+        d2 = np.ascontiguousarray(desc2, np.uint8)
+        m = np.full(d1.shape[0], -1, np.int32)
+        n = _check(lib.plvi_line_match(_ptr(d1), d1.shape[0], _ptr(d2), d2.shape[0], nnr, _ptr(m)),
+                   "plvi_line_match")
+        return n, m

@@ -1,0 +1,109 @@
+"""Deterministic synthetic EuRoC-shaped frames.
+
+numpy PCG64(seed); W×H u8.  Background = bilinear upsample of an 8×6 grid
+U[60,190]; 40 filled rotated rectangles (intensity U[0,255]); 60 line
+segments (width 1–3 px, contrast >= 40); Gaussian noise sigma=2, rint, clip.
+The pair frame t+1 is frame t shifted by an integer (dx,dy) in [-3,3]^2
+plus fresh noise.  Gives thousands of FAST corners at th=20 and >=200 LSD
+segments per 640×480 frame.
+"""
+import numpy as np
+
+
+def _background(rng, w, h):
+    grid = rng.uniform(60, 190, size=(6, 8))
+    ys = np.linspace(0, 5, h)
+    xs = np.linspace(0, 7, w)
+    y0 = np.clip(np.floor(ys).astype(int), 0, 4)
+    x0 = np.clip(np.floor(xs).astype(int), 0, 6)
+    fy = (ys - y0)[:, None]
+    fx = (xs - x0)[None, :]
+    g00 = grid[y0][:, x0]
+    g01 = grid[y0][:, x0 + 1]
+    g10 = grid[y0 + 1][:, x0]
+    g11 = grid[y0 + 1][:, x0 + 1]
+    return (g00 * (1 - fy) * (1 - fx) + g01 * (1 - fy) * fx + g10 * fy * (1 - fx) + g11 * fy * fx)
+
+
+def _draw_rect(img, rng):
+    h, w = img.shape
+    cx, cy = rng.uniform(0, w), rng.uniform(0, h)
+    a, b = rng.uniform(8, w / 6), rng.uniform(8, h / 6)
+    th = rng.uniform(0, np.pi)
+    val = rng.uniform(0, 255)
+    r = int(np.ceil(np.hypot(a, b))) + 1
+    x0, x1 = max(int(cx) - r, 0), min(int(cx) + r + 1, w)
+    y0, y1 = max(int(cy) - r, 0), min(int(cy) + r + 1, h)
+    if x0 >= x1 or y0 >= y1:
+        return
+    yy, xx = np.mgrid[y0:y1, x0:x1]
+    dx, dy = xx - cx, yy - cy
+    u = dx * np.cos(th) + dy * np.sin(th)
+    v = -dx * np.sin(th) + dy * np.cos(th)
+    m = (np.abs(u) <= a) & (np.abs(v) <= b)
+    img[y0:y1, x0:x1][m] = val
+
+
+def _draw_line(img, rng):
+    h, w = img.shape
+    x0, y0 = rng.uniform(0, w), rng.uniform(0, h)
+    ang = rng.uniform(0, np.pi)
+    ln = rng.uniform(30, 250)
+    x1, y1 = x0 + ln * np.cos(ang), y0 + ln * np.sin(ang)
+    width = rng.uniform(1, 3)
+    bx0, bx1 = int(max(min(x0, x1) - 3, 0)), int(min(max(x0, x1) + 4, w))
+    by0, by1 = int(max(min(y0, y1) - 3, 0)), int(min(max(y0, y1) + 4, h))
+    if bx0 >= bx1 or by0 >= by1:
+        return
+    yy, xx = np.mgrid[by0:by1, bx0:bx1]
+    px, py = xx - x0, yy - y0
+    dx, dy = x1 - x0, y1 - y0
+    t = np.clip((px * dx + py * dy) / (dx * dx + dy * dy), 0, 1)
+    dist = np.hypot(px - t * dx, py - t * dy)
+    m = dist <= width / 2
+    region = img[by0:by1, bx0:bx1]
+    base = float(np.median(region)) if region.size else 128.0
+    c = rng.uniform(40, 120) * (1 if rng.uniform() < 0.5 else -1)
+    val = np.clip(base + c, 0, 255)
+    if abs(val - base) < 40:
+        val = np.clip(base - c, 0, 255)
+    region[m] = val
+
+
+def clean_frame(seed, w=640, h=480):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    img = _background(rng, w, h)
+    for _ in range(40):
+        _draw_rect(img, rng)
+    for _ in range(60):
+        _draw_line(img, rng)
+    return img, rng
+
+
+def _finish(img, rng):
+    noisy = img + rng.normal(0.0, 2.0, size=img.shape)
+    return np.clip(np.rint(noisy), 0, 255).astype(np.uint8)
+
+
+def frame(seed, w=640, h=480):
+    """One synthetic frame (u8 H×W)."""
+    img, rng = clean_frame(seed, w, h)
+    return _finish(img, rng)
+
+
+def frame_pair(seed, w=640, h=480):
+    """(frame t, frame t+1): t+1 = integer shift of t's clean image + fresh noise."""
+    img, rng = clean_frame(seed, w, h)
+    dx, dy = rng.integers(-3, 4, size=2)
+    shifted = np.roll(np.roll(img, int(dy), axis=0), int(dx), axis=1)
+    a = _finish(img, rng)
+    b = _finish(shifted, rng)
+    return a, b
+
+
+def batch(n, w=640, h=480, seed0=0):
+    """n frames with seeds seed0..seed0+n-1 as one contiguous (n,H,W) u8 array."""
+    out = np.empty((n, h, w), np.uint8)
+    for i in range(n):
+        out[i] = frame(seed0 + i, w, h)
+    return out

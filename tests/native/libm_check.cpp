@@ -1,0 +1,97 @@
+// tests/native/libm_check.cpp — exhaustive / sampled comparison of the
+// product's device math (pl-vi-orbslam3_amd/csrc/plvi_math.h, compiled here
+// as host code with the same IEEE operations) against the HOST glibc, which
+// is what the reference binary calls.  SURVEY.md B.3.
+//
+// usage: libm_check <mode> [lo_bits hi_bits]
+//   sincosf     : every float bit pattern in [lo,hi) (default: all 2^32)
+//   atan2f N    : N seeded random (y,x) pairs + edge grid
+//   lsdangles   : every float deg in [0,360]: float(cos/sin((double)deg*pi/180))
+// Prints "mismatches=<k> checked=<n>" and exits non-zero on any mismatch.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <thread>
+#include <vector>
+#include <atomic>
+
+#include "../../pl-vi-orbslam3_amd/csrc/plvi_math.h"
+
+static bool same(float a, float b) {
+    if (std::isnan(a) && std::isnan(b)) return true;
+    uint32_t x, y;
+    memcpy(&x, &a, 4); memcpy(&y, &b, 4);
+    return x == y;
+}
+
+int main(int argc, char** argv) {
+    const char* mode = argc > 1 ? argv[1] : "sincosf";
+    int nt = std::thread::hardware_concurrency();
+    if (nt > 16) nt = 16;
+    std::atomic<unsigned long long> bad{0}, checked{0};
+    std::vector<std::thread> th;
+    if (!strcmp(mode, "sincosf")) {
+        unsigned long long lo = argc > 2 ? strtoull(argv[2], 0, 0) : 0ull;
+        unsigned long long hi = argc > 3 ? strtoull(argv[3], 0, 0) : (1ull << 32);
+        for (int t = 0; t < nt; ++t)
+            th.emplace_back([&, t] {
+                unsigned long long b = 0, c = 0;
+                for (unsigned long long u = lo + t; u < hi; u += nt) {
+                    float x = plvi::u2f((uint32_t)u);
+                    if (!same(plvi::plvi_sinf(x), sinf(x))) { if (b < 5) fprintf(stderr, "sinf %a\n", x); ++b; }
+                    if (!same(plvi::plvi_cosf(x), cosf(x))) { if (b < 5) fprintf(stderr, "cosf %a\n", x); ++b; }
+                    ++c;
+                }
+                bad += b; checked += c;
+            });
+    } else if (!strcmp(mode, "atan2f")) {
+        long n = argc > 2 ? atol(argv[2]) : 100000000L;
+        for (int t = 0; t < nt; ++t)
+            th.emplace_back([&, t] {
+                std::mt19937_64 rng(1234 + t);
+                std::uniform_real_distribution<float> u(-800.f, 800.f);
+                std::uniform_int_distribution<uint32_t> bits;
+                unsigned long long b = 0, c = 0;
+                for (long i = t; i < n; i += nt) {
+                    float y, x;
+                    if (i % 3 == 0) { y = plvi::u2f(bits(rng)); x = plvi::u2f(bits(rng)); }
+                    else if (i % 3 == 1) { y = u(rng); x = u(rng); }
+                    else { y = (float)(int)u(rng) * 0.5f; x = (float)(int)u(rng) * 0.25f; }
+                    if (!same(plvi::plvi_atan2f(y, x), atan2f(y, x))) {
+                        if (b < 5) fprintf(stderr, "atan2f %a %a -> %a vs %a\n", y, x, plvi::plvi_atan2f(y, x), atan2f(y, x));
+                        ++b;
+                    }
+                    ++c;
+                }
+                bad += b; checked += c;
+            });
+    } else if (!strcmp(mode, "lsdangles")) {
+        const double D2R = M_PI / 180;
+        uint32_t hi = plvi::f2u(360.0f);
+        for (int t = 0; t < nt; ++t)
+            th.emplace_back([&, t] {
+                unsigned long long b = 0, c = 0;
+                for (uint32_t u = t; u <= hi; u += nt) {
+                    float deg = plvi::u2f(u);
+                    double a = (double)deg * D2R;
+                    // region_grow seed (lsd.cpp:648-649) and the float(angle)
+                    // path of :678-679 (cosf/sinf of float(a)).
+                    if (!same((float)plvi::plvi_cos(a), (float)std::cos(a))) { if (b < 5) fprintf(stderr, "cos %a\n", a); ++b; }
+                    if (!same((float)plvi::plvi_sin(a), (float)std::sin(a))) { if (b < 5) fprintf(stderr, "sin %a\n", a); ++b; }
+                    double na = -a;
+                    if (!same((float)plvi::plvi_cos(na), (float)std::cos(na))) ++b;
+                    if (!same((float)plvi::plvi_sin(na), (float)std::sin(na))) ++b;
+                    ++c;
+                }
+                bad += b; checked += c;
+            });
+    } else {
+        fprintf(stderr, "unknown mode\n");
+        return 2;
+    }
+    for (auto& x : th) x.join();
+    printf("mismatches=%llu checked=%llu\n", (unsigned long long)bad, (unsigned long long)checked);
+    return bad ? 1 : 0;
+}

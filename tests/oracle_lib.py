@@ -1,0 +1,161 @@
+"""ctypes loader for the CPU oracle (oracle/, test infrastructure only).
+
+Builds oracle/_build/liboracle.so with `make -C oracle` when missing.
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline use this.
+"""
+import ctypes
+import pathlib
+import subprocess
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+ORACLE_DIR = ROOT / "oracle"
+LIB = ORACLE_DIR / "_build" / "liboracle.so"
+
+
+class KP(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_float), ("y", ctypes.c_float), ("size", ctypes.c_float), ("angle", ctypes.c_float),
+                ("response", ctypes.c_float), ("octave", ctypes.c_int), ("class_id", ctypes.c_int)]
+
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", str(ORACLE_DIR)], check=True)
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    srcs = list(ORACLE_DIR.glob("*.cpp")) + list(ORACLE_DIR.glob("*.h")) + list(ORACLE_DIR.glob("*.inc"))
+    if not LIB.exists() or any(s.stat().st_mtime > LIB.stat().st_mtime for s in srcs):
+        build()
+    lib = ctypes.CDLL(str(LIB))
+    V, I, F, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_double
+    P = ctypes.POINTER(ctypes.c_int)
+    lib.oracle_orb_extract.argtypes = [V, I, I, I, I, F, I, I, I, I, I, V, V, I, P]
+    lib.oracle_orb_extract.restype = I
+    lib.oracle_orb_stage.argtypes = [V, I, I, I, F, I, I, I, I, V, V, P, P, V, I, P, V, I, P]
+    lib.oracle_orb_stage.restype = I
+    lib.oracle_orb_params.argtypes = [I, F, I, V, V, V]
+    lib.oracle_resize_u8.argtypes = [V, I, I, V, I, I]
+    lib.oracle_gaussian_blur_u8.argtypes = [V, I, I, I, D, V]
+    lib.oracle_gaussian_taps_u8.argtypes = [I, D, V]
+    lib.oracle_gaussian_kernel_f64.argtypes = [I, D, V]
+    lib.oracle_fast_atan2.argtypes = [F, F]
+    lib.oracle_fast_atan2.restype = F
+    lib.oracle_fast_score.argtypes = [V, I]
+    lib.oracle_fast_score.restype = I
+    _lib = lib
+    return lib
+
+
+def _p(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def orb_extract(img, nfeatures=1000, scale=1.2, nlevels=8, ini=20, mn=7, lap=(0, 0), cap=20000):
+    lib = load()
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    kps = np.zeros(cap, KEYPOINT_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    n = ctypes.c_int()
+    mono = lib.oracle_orb_extract(_p(img), w, h, w, nfeatures, scale, nlevels, ini, mn, lap[0], lap[1],
+                                  _p(kps), _p(desc), cap, ctypes.byref(n))
+    return mono, kps[:n.value].copy(), desc[:n.value].copy()
+
+
+def orb_stage(img, level, nfeatures=1000, scale=1.2, nlevels=8, ini=20, mn=7, cap=200000):
+    lib = load()
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    pyr = np.zeros(w * h, np.uint8)
+    blur = np.zeros(w * h, np.uint8)
+    lw, lh, nc, nl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    cand = np.zeros((cap, 3), np.float32)
+    lvk = np.zeros((cap, 4), np.float32)
+    rc = lib.oracle_orb_stage(_p(img), w, h, nfeatures, scale, nlevels, ini, mn, level, _p(pyr), _p(blur),
+                              ctypes.byref(lw), ctypes.byref(lh), _p(cand), cap, ctypes.byref(nc), _p(lvk), cap,
+                              ctypes.byref(nl))
+    assert rc == 0
+    n = lw.value * lh.value
+    return {"pyr": pyr[:n].reshape(lh.value, lw.value), "blur": blur[:n].reshape(lh.value, lw.value),
+            "cand": cand[:nc.value], "levelkps": lvk[:nl.value]}
+
+
+def resize(src, dw, dh):
+    lib = load()
+    src = np.ascontiguousarray(src, np.uint8)
+    out = np.zeros((dh, dw), np.uint8)
+    lib.oracle_resize_u8(_p(src), src.shape[1], src.shape[0], _p(out), dw, dh)
+    return out
+
+
+def gaussian_blur(src, ksize, sigma):
+    lib = load()
+    src = np.ascontiguousarray(src, np.uint8)
+    out = np.zeros_like(src)
+    lib.oracle_gaussian_blur_u8(_p(src), src.shape[1], src.shape[0], ksize, sigma, _p(out))
+    return out
+
+
+def gaussian_taps(ksize, sigma):
+    lib = load()
+    t = np.zeros(ksize, np.int32)
+    lib.oracle_gaussian_taps_u8(ksize, sigma, _p(t))
+    return t
+
+
+def gaussian_kernel_f64(ksize, sigma):
+    lib = load()
+    t = np.zeros(ksize, np.float64)
+    lib.oracle_gaussian_kernel_f64(ksize, sigma, _p(t))
+    return t
+
+
+def _declare_match(lib):
+    V, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    lib.oracle_knn2.argtypes = [V, I, V, I, V, V, V, V]
+    lib.oracle_match_nnr.argtypes = [V, I, V, I, F, V]
+    lib.oracle_match_nnr.restype = I
+    lib.oracle_match.argtypes = [V, I, V, I, F, V]
+    lib.oracle_match.restype = I
+    lib.oracle_descriptor_distance.argtypes = [V, V]
+    lib.oracle_line_descriptor_distance.argtypes = [V, V]
+
+
+def knn2(q, t):
+    lib = load()
+    _declare_match(lib)
+    q = np.ascontiguousarray(q, np.uint8)
+    t = np.ascontiguousarray(t, np.uint8)
+    out = [np.zeros(q.shape[0], np.int32) for _ in range(4)]
+    lib.oracle_knn2(_p(q), q.shape[0], _p(t), t.shape[0], *[_p(o) for o in out])
+    return tuple(out)
+
+
+def match_nnr(d1, d2, nnr):
+    lib = load()
+    _declare_match(lib)
+    d1 = np.ascontiguousarray(d1, np.uint8)
+    d2 = np.ascontiguousarray(d2, np.uint8)
+    m = np.zeros(d1.shape[0], np.int32)
+    n = lib.oracle_match_nnr(_p(d1), d1.shape[0], _p(d2), d2.shape[0], nnr, _p(m))
+    return n, m
+
+
+def match(d1, d2, nnr):
+    lib = load()
+    _declare_match(lib)
+    d1 = np.ascontiguousarray(d1, np.uint8)
+    d2 = np.ascontiguousarray(d2, np.uint8)
+    m = np.zeros(d1.shape[0], np.int32)
+    n = lib.oracle_match(_p(d1), d1.shape[0], _p(d2), d2.shape[0], nnr, _p(m))
+    return n, m

@@ -1,0 +1,40 @@
+"""The product's glibc-faithful math (csrc/plvi_math.h) vs the host glibc,
+exhaustively where the domain is finite."""
+import pathlib
+import subprocess
+
+import pytest
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+SRC = ROOT / "tests" / "native" / "libm_check.cpp"
+BIN = ROOT / "tests" / "native" / "_build" / "libm_check"
+
+
+@pytest.fixture(scope="module")
+def libm_check():
+    BIN.parent.mkdir(exist_ok=True)
+    hdr = ROOT / "pl-vi-orbslam3_amd" / "csrc" / "plvi_math.h"
+    if not BIN.exists() or BIN.stat().st_mtime < max(SRC.stat().st_mtime, hdr.stat().st_mtime):
+        subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-pthread", "-o",
+                        str(BIN), str(SRC), "-lm"], check=True)
+    return str(BIN)
+
+
+def _run(binp, *args):
+    r = subprocess.run([binp, *args], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches=0" in r.stdout
+    return r.stdout
+
+
+def test_sinf_cosf_every_float(libm_check):
+    out = _run(libm_check, "sincosf")          # all 2^32 bit patterns, both functions
+    assert "checked=4294967296" in out
+
+
+def test_lsd_double_cos_sin_every_float_angle(libm_check):
+    _run(libm_check, "lsdangles")              # float(cos/sin(deg*pi/180)) for every float deg in [0,360]
+
+
+def test_atan2f_sampled(libm_check):
+    _run(libm_check, "atan2f", "30000000")

@@ -1,0 +1,110 @@
+"""ORB parity: HIP path (through the C-ABI) vs the CPU oracle, bit-exact.
+
+Keypoints compare every cv::KeyPoint field bitwise (x, y, size, angle,
+response, octave, class_id) in the reference's slot order; descriptors
+byte-for-byte; monoIndex exactly."""
+import numpy as np
+import pytest
+
+import oracle_lib as ol
+import plvi
+from plvi import synth
+from util import real_frames
+
+pytestmark = pytest.mark.gpu
+
+
+def _assert_same(got, exp, tag):
+    mg, kg, dg = got
+    me, ke, de = exp
+    assert mg == me, f"{tag}: monoIndex {mg} != {me}"
+    assert len(kg) == len(ke), f"{tag}: n {len(kg)} != {len(ke)}"
+    for f in ke.dtype.names:
+        a, b = kg[f], ke[f]
+        bad = np.flatnonzero(a.view(np.uint32) != b.view(np.uint32)) if a.dtype.kind == "f" else np.flatnonzero(a != b)
+        assert bad.size == 0, f"{tag}: field {f} differs at {bad[:10]} got {a[bad[:5]]} exp {b[bad[:5]]}"
+    bad = np.flatnonzero((dg != de).any(axis=1))
+    assert bad.size == 0, f"{tag}: descriptors differ at rows {bad[:10]}"
+
+
+@pytest.fixture(scope="module")
+def orb640(plvi_lib):
+    return plvi.ORBextractor(1000, 1.2, 8, 20, 7, 640, 480, max_batch=8)
+
+
+@pytest.fixture(scope="module")
+def orb752(plvi_lib):
+    return plvi.ORBextractor(1000, 1.2, 8, 20, 7, 752, 480, max_batch=2)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
+def test_orb_synthetic_640(orb640, seed):
+    img = synth.frame(seed)
+    _assert_same(orb640(img, None, (0, 0)), ol.orb_extract(img), f"synth{seed}")
+
+
+def test_orb_pyramid_matches_oracle(orb640):
+    img = synth.frame(5)
+    orb640(img, None, (0, 0))
+    for level in range(8):
+        exp = ol.orb_stage(img, level)
+        got = orb640.pyramid_level(level)
+        assert np.array_equal(got, exp["pyr"]), f"level {level}"
+
+
+def test_orb_real_euroc_752(orb752):
+    fr = real_frames()
+    for k in ("euroc1", "euroc2"):
+        _assert_same(orb752(fr[k]), ol.orb_extract(fr[k]), k)
+
+
+def test_orb_real_rgb_640(orb640):
+    img = real_frames()["rgb1_gray"]
+    _assert_same(orb640(img), ol.orb_extract(img), "rgb1_gray")
+
+
+def test_orb_lapping_area_slots(orb640):
+    img = synth.frame(6)
+    for lap in [(0, 1000), (100, 300), (0, 0)]:
+        _assert_same(orb640(img, None, lap), ol.orb_extract(img, lap=lap), f"lap{lap}")
+
+
+def test_orb_ini_extractor_5000(plvi_lib):
+    ext = plvi.ORBextractor(5000, 1.2, 8, 20, 7, 640, 480)
+    img = synth.frame(7)
+    _assert_same(ext(img), ol.orb_extract(img, nfeatures=5000), "ini5000")
+
+
+def test_orb_flat_and_noise_edge_cases(orb640):
+    flat = np.full((480, 640), 128, np.uint8)
+    _assert_same(orb640(flat), ol.orb_extract(flat), "flat")
+    rng = np.random.default_rng(0)
+    noise = rng.integers(0, 256, size=(480, 640), dtype=np.uint8)
+    _assert_same(orb640(noise), ol.orb_extract(noise), "noise")
+
+
+def test_orb_empty_image_returns_minus_one(orb640):
+    mono, k, d = orb640(np.zeros((0, 0), np.uint8))
+    assert mono == -1 and len(k) == 0
+
+
+def test_orb_batch_equals_single(orb640):
+    import ctypes
+    torch = pytest.importorskip("torch")
+    frames = synth.batch(8, seed0=20)
+    d = torch.from_numpy(frames).cuda()
+    orb640.extract_batch(d.data_ptr(), 8, 640 * 480, 640)
+    torch.cuda.synchronize()
+    kp_p, de_p, co_p, mo_p, cap = orb640.outputs()
+    import plvi as P
+    lib = P.load()
+    cnt = np.zeros(8, np.int32); mono = np.zeros(8, np.int32)
+    kps = np.zeros(8 * cap, P.KEYPOINT_DTYPE); desc = np.zeros((8 * cap, 32), np.uint8)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipDeviceSynchronize()
+    for dst, src, n in [(cnt, co_p, 32), (mono, mo_p, 32), (kps, kp_p, kps.nbytes), (desc, de_p, desc.nbytes)]:
+        assert hip.hipMemcpy(ctypes.c_void_p(dst.ctypes.data), ctypes.c_void_p(src), ctypes.c_size_t(n), 2) == 0
+    for f in range(8):
+        exp = ol.orb_extract(frames[f])
+        got = (int(mono[f]), kps[f * cap:f * cap + cnt[f]], desc[f * cap:f * cap + cnt[f]])
+        _assert_same(got, exp, f"batch{f}")
