@@ -140,6 +140,14 @@ int plvi_line_match_nnr(const uint8_t* desc1, int n1, const uint8_t* desc2, int 
  * matchNNR both ways + mutual check. */
 int plvi_line_match(const uint8_t* desc1, int n1, const uint8_t* desc2, int n2, float nnr, int* matches_12);
 
+/* Device memory helpers for bindings that have no HIP runtime of their own
+ * (ctypes, JNI): thin wrappers over hipMalloc/hipFree/hipMemcpy on the
+ * current device.  kind: 1 = host->device, 2 = device->host, 3 = d->d. */
+int plvi_device_malloc(void** ptr, size_t bytes);
+int plvi_device_free(void* ptr);
+int plvi_memcpy(void* dst, const void* src, size_t bytes, int kind);
+int plvi_device_synchronize(void);
+
 /* Device/library information for diagnostics. */
 const char* plvi_version(void);
 int plvi_device_count(void);

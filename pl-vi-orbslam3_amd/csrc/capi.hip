@@ -10,3 +10,27 @@ extern "C" int plvi_device_count(void) {
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
 }
+
+extern "C" int plvi_device_malloc(void** ptr, size_t bytes) {
+    if (!ptr) return PLVI_E_BADARG;
+    PLVI_CHECK(hipMalloc(ptr, bytes));
+    return PLVI_OK;
+}
+
+extern "C" int plvi_device_free(void* ptr) {
+    PLVI_CHECK(hipFree(ptr));
+    return PLVI_OK;
+}
+
+extern "C" int plvi_memcpy(void* dst, const void* src, size_t bytes, int kind) {
+    const hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost
+                                                                         : hipMemcpyDeviceToDevice;
+    if (kind < 1 || kind > 3) return PLVI_E_BADARG;
+    PLVI_CHECK(hipMemcpy(dst, src, bytes, k));
+    return PLVI_OK;
+}
+
+extern "C" int plvi_device_synchronize(void) {
+    PLVI_CHECK(hipDeviceSynchronize());
+    return PLVI_OK;
+}

@@ -74,6 +74,10 @@ def _declare(lib):
         "plvi_hamming_knn2": ([V, I, V, I, V, V, V, V], I),
         "plvi_line_match_nnr": ([V, I, V, I, F, V], I),
         "plvi_line_match": ([V, I, V, I, F, V], I),
+        "plvi_device_malloc": ([c_void_pp, S], I),
+        "plvi_device_free": ([V], I),
+        "plvi_memcpy": ([V, V, S, I], I),
+        "plvi_device_synchronize": ([], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -97,6 +101,40 @@ def exported_symbols():
     import re
     txt = HEADER_PATH.read_text()
     return sorted(set(re.findall(r"\b(plvi_[a-z0-9_]+)\s*\(", txt)))
+
+
+class DeviceBuffer:
+    """hipMalloc'd buffer owned from Python (no torch needed)."""
+
+    def __init__(self, nbytes):
+        self._lib = load()
+        p = ctypes.c_void_p()
+        _check(self._lib.plvi_device_malloc(ctypes.byref(p), max(1, nbytes)), "plvi_device_malloc")
+        self.ptr, self.nbytes = p.value, nbytes
+
+    def upload(self, arr):
+        arr = np.ascontiguousarray(arr)
+        assert arr.nbytes <= self.nbytes
+        _check(self._lib.plvi_memcpy(ctypes.c_void_p(self.ptr), _ptr(arr), arr.nbytes, 1), "plvi_memcpy")
+
+    def download(self, arr, src_ptr=None):
+        _check(self._lib.plvi_memcpy(_ptr(arr), ctypes.c_void_p(src_ptr or self.ptr), arr.nbytes, 2),
+               "plvi_memcpy")
+        return arr
+
+    def __del__(self):
+        try:
+            if self.ptr:
+                self._lib.plvi_device_free(ctypes.c_void_p(self.ptr))
+                self.ptr = None
+        except Exception:
+            pass
+
+
+def download(ptr, arr):
+    """Copy device memory at `ptr` into numpy array `arr` (synchronous)."""
+    _check(load().plvi_memcpy(_ptr(arr), ctypes.c_void_p(ptr), arr.nbytes, 2), "plvi_memcpy")
+    return arr
 
 
 def _check(rc, what):

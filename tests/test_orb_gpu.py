@@ -89,21 +89,16 @@ def test_orb_empty_image_returns_minus_one(orb640):
 
 
 def test_orb_batch_equals_single(orb640):
-    import ctypes
-    torch = pytest.importorskip("torch")
     frames = synth.batch(8, seed0=20)
-    d = torch.from_numpy(frames).cuda()
-    orb640.extract_batch(d.data_ptr(), 8, 640 * 480, 640)
-    torch.cuda.synchronize()
+    buf = plvi.DeviceBuffer(frames.nbytes)
+    buf.upload(frames)
+    orb640.extract_batch(buf.ptr, 8, 640 * 480, 640)
+    plvi.load().plvi_device_synchronize()
     kp_p, de_p, co_p, mo_p, cap = orb640.outputs()
-    import plvi as P
-    lib = P.load()
-    cnt = np.zeros(8, np.int32); mono = np.zeros(8, np.int32)
-    kps = np.zeros(8 * cap, P.KEYPOINT_DTYPE); desc = np.zeros((8 * cap, 32), np.uint8)
-    hip = ctypes.CDLL("libamdhip64.so")
-    hip.hipDeviceSynchronize()
-    for dst, src, n in [(cnt, co_p, 32), (mono, mo_p, 32), (kps, kp_p, kps.nbytes), (desc, de_p, desc.nbytes)]:
-        assert hip.hipMemcpy(ctypes.c_void_p(dst.ctypes.data), ctypes.c_void_p(src), ctypes.c_size_t(n), 2) == 0
+    cnt = plvi.download(co_p, np.zeros(8, np.int32))
+    mono = plvi.download(mo_p, np.zeros(8, np.int32))
+    kps = plvi.download(kp_p, np.zeros(8 * cap, plvi.KEYPOINT_DTYPE))
+    desc = plvi.download(de_p, np.zeros((8 * cap, 32), np.uint8))
     for f in range(8):
         exp = ol.orb_extract(frames[f])
         got = (int(mono[f]), kps[f * cap:f * cap + cnt[f]], desc[f * cap:f * cap + cnt[f]])
