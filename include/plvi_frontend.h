@@ -116,6 +116,51 @@ int plvi_orb_level_quota(plvi_orb_extractor* h, int* quota);
 int plvi_orb_profile(plvi_orb_extractor* h, int enable);
 int plvi_orb_profile_read(plvi_orb_extractor* h, float* stage_ms, int* runs);
 
+/* ------------------------------------------------------------------ Lines
+ * Replaces ORB_SLAM3::Lineextractor (include/LineExtractor.h:49-93,
+ * src/LineExtractor.cc:39-117): LSDDetectorC pyramid + LSD
+ * (src/LSD/lsd.cpp) + KeyLine assembly + top-k + LBD
+ * (Thirdparty/line_descriptor/src/binary_descriptor_custom.cpp). */
+typedef struct plvi_line_extractor plvi_line_extractor;
+
+typedef struct plvi_line_params {
+  int nfeatures;   /* lsd_nfeatures (0 = keep all) */
+  int refine;      /* lsd_refine: only 0 (LSD_REFINE_NONE, the config) is supported */
+  float lsd_scale; /* lsd_scale (LSDOptions::scale, float) */
+  int nlevels;     /* pyramid octaves (<= 2) */
+  float scale;     /* pyramid scale factor (2.0) */
+  int extractor;   /* 0 = LSD (EDLines, extractor==1, is out of scope) */
+} plvi_line_params;
+
+int plvi_lines_create(const plvi_line_params* p, int width, int height, int max_batch, int device,
+                      plvi_line_extractor** out);
+int plvi_lines_destroy(plvi_line_extractor* h);
+
+/* One frame from host memory, synchronous: Lineextractor::operator()
+ * (LineExtractor.cc:45-117).  keylines (KeyLine layout) in the reference's
+ * order (post top-k sort when truncated), LBD descriptors n x 32, and the
+ * normalised line equations n x 3 doubles (keylineFunction).  The reference
+ * APPENDS to keylineFunction; callers append line_fns themselves. */
+int plvi_lines_extract(plvi_line_extractor* h, const uint8_t* img, int width, int height, size_t stride,
+                       plvi_keyline* keylines, uint8_t* desc, double* line_fns, int cap, int* n);
+
+/* Batched device-resident variant (same frame addressing as ORB). */
+int plvi_lines_extract_batch(plvi_line_extractor* h, const uint8_t* d_frames, int n_frames, size_t frame_stride,
+                             size_t row_stride, void* stream);
+int plvi_lines_outputs(plvi_line_extractor* h, plvi_keyline** d_kl, uint8_t** d_desc, double** d_fn, int** d_count,
+                       int* cap);
+
+/* mvImagePyramid_l[level] (gaussianPyrs, level >= 1; level 0 is the input). */
+int plvi_lines_pyramid_level(plvi_line_extractor* h, int frame, int level, uint8_t* dst, int* w, int* hgt);
+
+/* mvScaleFactor_l / mvInvScaleFactor_l / mvLevelSigma2_l / mvInvLevelSigma2_l (LineExtractor.cc:86-100). */
+int plvi_lines_scale_tables(plvi_line_extractor* h, float* scale, float* inv_scale, float* sigma2, float* inv_sigma2);
+
+/* Stage timing: [0] octave pyramid, [1] LSD prep (blur f64, resize, gradient),
+ * [2] region growing + rect, [3] keyline assembly + top-k, [4] LBD. */
+int plvi_lines_profile(plvi_line_extractor* h, int enable);
+int plvi_lines_profile_read(plvi_line_extractor* h, float* stage_ms, int* runs);
+
 /* ------------------------------------------------------------------ Hamming
  * ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:2350-2366) over a batch. */
 

@@ -1,0 +1,768 @@
+// lines_kernels.hpp — HIP/CDNA4 kernels of the line front end:
+//   LSDDetectorC (Thirdparty/line_descriptor/src/LSDDetector_custom.cpp)
+//   LineSegmentDetectorImpl::flsd (src/LSD/lsd.cpp, refine = NONE)
+//   BinaryDescriptor LBD (Thirdparty/line_descriptor/src/binary_descriptor_custom.cpp)
+// Compiled with -ffp-contract=off (bit-exact f32/f64 sequences).
+#include <hip/hip_runtime.h>
+
+#include "lines_device.h"
+#include "plvi_common.h"
+#include "plvi_math.h"
+#include "std_sort.h"
+
+namespace plvi {
+
+constexpr double kNotdef = -1024.0;
+constexpr float kNotdefF = -1024.0f;
+constexpr double kD2R = 3.14159265358979323846 / 180;  // DEG_TO_RADS (lsd.cpp)
+constexpr double kPi = 3.14159265358979323846;
+
+// ---------------------------------------------------------------------------
+// LK1: LSDDetectorC::ComputePyramid level 1 = resize(level0, (w/2,h/2)).
+// Exact factor 2 -> OpenCV's INTER_AREA fast path: the SIMD
+// body (first floor(w/8)*8 columns) rounds (a+b+c+d+2)>>2, the scalar tail
+// cvRound(sum*0.25f).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void lsd_half_kernel(const uint8_t* __restrict__ src, size_t s_frame, size_t s_row,
+                                                       uint8_t* __restrict__ dst, int dw, int dh, size_t d_frame) {
+    const int f = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= dw * dh) return;
+    const int y = i / dw, x = i % dw;
+    const uint8_t* S0 = src + (size_t)f * s_frame + (size_t)(2 * y) * s_row;
+    const uint8_t* S1 = S0 + s_row;
+    const int s = S0[2 * x] + S0[2 * x + 1] + S1[2 * x] + S1[2 * x + 1];
+    const int simd = (dw / 8) * 8;
+    int v = x < simd ? (s + 2) >> 2 : (int)__builtin_rintf((float)s * 0.25f);
+    dst[(size_t)f * d_frame + (size_t)y * dw + x] = (uint8_t)min(max(v, 0), 255);
+}
+
+// ---------------------------------------------------------------------------
+// LK2: LSD preparation, fused per 32x16 tile of the scaled image:
+//   u8 -> f64, GaussianBlur(7x7, sigma=0.6/SCALE) f64 reflect-101
+//   (RowFilter sequential sum, SymmColumnFilter; lsd.cpp:455),
+//   resize x SCALE f64 INTER_LINEAR with float coefficients (lsd.cpp:457),
+//   ll_angle gradient / norm / fastAtan2 angle (lsd.cpp:561-584).
+// Outputs per scaled pixel: LsdPix {deg | NOTDEF, cosf, sinf} and modgrad (f64).
+// ---------------------------------------------------------------------------
+constexpr int kPTX = 32, kPTY = 16;         // scaled tile
+constexpr int kPGW = 48, kPGH = 28;         // max blurred (G) region
+constexpr int kPIW = kPGW + 6, kPIH = kPGH + 6;
+
+__global__ __launch_bounds__(256) void lsd_prep_kernel(const uint8_t* __restrict__ src, size_t s_frame, size_t s_row,
+                                                       int gw, int gh, int sw, int sh, const int* __restrict__ xofs,
+                                                       const float* __restrict__ xa, int xmax,
+                                                       const int* __restrict__ yrow, const float* __restrict__ yb,
+                                                       double k0, double k1, double k2, double k3, double rho,
+                                                       LsdPix* __restrict__ pix, double* __restrict__ modgrad,
+                                                       size_t p_frame, int* __restrict__ err) {
+    __shared__ uint8_t I[kPIH][kPIW];
+    __shared__ double Hs[kPIH][kPGW];
+    __shared__ double Gs[kPGH][kPGW];
+    __shared__ double Ss[kPTY + 1][kPTX + 1];
+    const int f = blockIdx.z;
+    const int X0 = blockIdx.x * kPTX, Y0 = blockIdx.y * kPTY;
+    const int Xe = min(X0 + kPTX, sw - 1), Ye = min(Y0 + kPTY, sh - 1);  // inclusive (+1 for the gradient)
+    const int gx0 = xofs[X0], gx1 = min(xofs[Xe] + 1, gw - 1);
+    const int gy0 = yrow[2 * Y0], gy1 = yrow[2 * Ye + 1];
+    const int GW = gx1 - gx0 + 1, GH = gy1 - gy0 + 1;
+    if (GW > kPGW || GH > kPGH) {
+        if (threadIdx.x == 0) atomicOr(err, 2);
+        return;
+    }
+    const uint8_t* S = src + (size_t)f * s_frame;
+    const int IW = GW + 6, IH = GH + 6;
+    for (int i = threadIdx.x; i < IW * IH; i += 256) {
+        const int r = i / IW, c = i % IW;
+        I[r][c] = S[(size_t)reflect101(gy0 - 3 + r, gh) * s_row + reflect101(gx0 - 3 + c, gw)];
+    }
+    __syncthreads();
+    const double kk[7] = {k0, k1, k2, k3, k2, k1, k0};
+    for (int i = threadIdx.x; i < IH * GW; i += 256) {
+        const int r = i / GW, c = i % GW;
+        double s = kk[0] * (double)I[r][c];
+#pragma unroll
+        for (int k = 1; k < 7; ++k) s += kk[k] * (double)I[r][c + k];
+        Hs[r][c] = s;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < GH * GW; i += 256) {
+        const int r = i / GW, c = i % GW;
+        double s = k3 * Hs[r + 3][c] + 0.0;
+        s += k2 * (Hs[r + 4][c] + Hs[r + 2][c]);
+        s += k1 * (Hs[r + 5][c] + Hs[r + 1][c]);
+        s += k0 * (Hs[r + 6][c] + Hs[r][c]);
+        Gs[r][c] = s;
+    }
+    __syncthreads();
+    const int TW = Xe - X0 + 1, TH = Ye - Y0 + 1;
+    for (int i = threadIdx.x; i < TW * TH; i += 256) {
+        const int ty = i / TW, tx = i % TW;
+        const int dx = X0 + tx, dy = Y0 + ty;
+        const int r0 = yrow[2 * dy] - gy0, r1 = yrow[2 * dy + 1] - gy0;
+        const double b0 = (double)yb[2 * dy], b1 = (double)yb[2 * dy + 1];
+        const int sx = xofs[dx] - gx0;
+        double H0, H1;
+        if (dx < xmax) {
+            const double a0 = (double)xa[2 * dx], a1 = (double)xa[2 * dx + 1];
+            H0 = Gs[r0][sx] * a0 + Gs[r0][sx + 1] * a1;
+            H1 = Gs[r1][sx] * a0 + Gs[r1][sx + 1] * a1;
+        } else {
+            H0 = Gs[r0][sx] * 1.0;
+            H1 = Gs[r1][sx] * 1.0;
+        }
+        Ss[ty][tx] = H0 * b0 + H1 * b1;
+    }
+    __syncthreads();
+    LsdPix* P = pix + (size_t)f * p_frame;
+    double* M = modgrad + (size_t)f * p_frame;
+    for (int i = threadIdx.x; i < kPTX * kPTY; i += 256) {
+        const int ty = i / kPTX, tx = i % kPTX;
+        const int x = X0 + tx, y = Y0 + ty;
+        if (x >= sw || y >= sh) continue;
+        LsdPix o;
+        o.deg = kNotdefF; o.c = 0.f; o.s = 0.f; o.pad = 0.f;
+        double norm = 0.0;
+        if (x < sw - 1 && y < sh - 1) {
+            const double DA = Ss[ty + 1][tx + 1] - Ss[ty][tx];
+            const double BC = Ss[ty][tx + 1] - Ss[ty + 1][tx];
+            const double gx = DA + BC, gy = DA - BC;
+            norm = __builtin_sqrt((gx * gx + gy * gy) / 4);
+            if (!(norm <= rho)) {
+                const float deg = plvi_fast_atan2((float)gx, (float)-gy);
+                const float af = (float)((double)deg * kD2R);
+                o.deg = deg;
+                o.c = plvi_cosf(af);
+                o.s = plvi_sinf(af);
+            }
+        }
+        P[(size_t)y * sw + x] = o;
+        M[(size_t)y * sw + x] = norm;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// LK3: flsd's serial core (lsd.cpp:476-533): seeds in raster order (flsd
+// walks the coorlist vector, not the pseudo-ordered chain), region_grow
+// (:635-686) with the exact float sumdx/sumdy/fastAtan2 update per added
+// pixel, the min_reg_size test, region2rect (:688-744) + get_theta
+// (:746-782) in double with the reference summation order, +0.5, /SCALE.
+// One wave per (octave, frame); the USED map is a bitmap in LDS, region
+// points live in an LDS queue (global spill beyond kLsdQueueLds).
+// ---------------------------------------------------------------------------
+struct GrowCtx {
+    const LsdPix* P;
+    const double* M;
+    unsigned* used;   // LDS bitmap
+    unsigned* qlds;   // LDS queue (x | y<<16)
+    unsigned* qglob;  // global spill
+    int sw, sh;
+};
+
+__device__ __forceinline__ bool used_get(const unsigned* u, int a) { return (u[a >> 5] >> (a & 31)) & 1u; }
+__device__ __forceinline__ void used_set(unsigned* u, int a) { u[a >> 5] |= 1u << (a & 31); }
+__device__ __forceinline__ unsigned q_get(const GrowCtx& g, int i) {
+    return i < kLsdQueueLds ? g.qlds[i] : g.qglob[i - kLsdQueueLds];
+}
+__device__ __forceinline__ void q_put(GrowCtx& g, int i, unsigned v) {
+    if (i < kLsdQueueLds) g.qlds[i] = v;
+    else g.qglob[i - kLsdQueueLds] = v;
+}
+
+__device__ __forceinline__ bool is_aligned_deg(float deg, double theta, double prec) {
+    if (deg == kNotdefF) return false;
+    const double a = (double)deg * kD2R;
+    double n_theta = theta - a;
+    if (n_theta < 0) n_theta = -n_theta;
+    if (n_theta > (3 * kPi) / 2) {
+        n_theta -= (2 * kPi);
+        if (n_theta < 0) n_theta = -n_theta;
+    }
+    return n_theta <= prec;
+}
+
+__device__ __forceinline__ double angle_diff(double a, double b) {
+    double diff = a - b;
+    while (diff <= -kPi) diff += (2 * kPi);
+    while (diff > kPi) diff -= (2 * kPi);
+    return diff < 0 ? -diff : diff;
+}
+
+__global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restrict__ octs,
+                                                      const LsdPix* __restrict__ pix,
+                                                      const double* __restrict__ modgrad,
+                                                      unsigned* __restrict__ qspill, size_t qspill_frame,
+                                                      double prec, double scale_lsd, LsdLine* __restrict__ lines,
+                                                      int* __restrict__ nlines, int* __restrict__ err) {
+    extern __shared__ __align__(16) unsigned lds_u[];
+    const int o = blockIdx.x, f = blockIdx.y, nOct = gridDim.x;
+    const LineOctDev& od = octs[o];
+    const int sw = od.sw, sh = od.sh;
+    const int lane = threadIdx.x;
+    const int nwords = (sw * sh + 31) >> 5;
+    GrowCtx g;
+    g.P = pix + od.soff + (size_t)f * od.splane;
+    g.M = modgrad + od.soff + (size_t)f * od.splane;
+    g.used = lds_u;
+    g.qlds = lds_u + nwords;
+    g.qglob = qspill + (size_t)(f * nOct + o) * qspill_frame;
+    g.sw = sw; g.sh = sh;
+    for (int i = lane; i < nwords; i += 64) g.used[i] = 0u;
+    __syncthreads();
+    LsdLine* out = lines + (size_t)(f * nOct + o) * kLsdRawCap;
+    int nout = 0;
+    bool overflow = false;
+    const int min_reg = od.min_reg_size;
+    for (int y = 0; y < sh - 1; ++y) {
+        for (int xb = 0; xb < sw - 1; xb += 64) {
+            const int x = xb + lane;
+            bool cand = false;
+            if (x < sw - 1) {
+                const int a = y * sw + x;
+                cand = !used_get(g.used, a) && g.P[a].deg != kNotdefF;
+            }
+            unsigned long long m = __ballot(cand);
+            while (m) {
+                const int b = __ffsll((long long)m) - 1;
+                m &= m - 1;
+                const int sx = xb + b;
+                const int sa = y * sw + sx;
+                if (used_get(g.used, sa)) continue;  // absorbed by an earlier region of this chunk
+                // ---- region_grow (lsd.cpp:635-686)
+                double reg_angle = (double)g.P[sa].deg * kD2R;
+                float sumdx = (float)plvi_cos(reg_angle);
+                float sumdy = (float)plvi_sin(reg_angle);
+                __syncthreads();
+                if (lane == 0) {
+                    used_set(g.used, sa);
+                    q_put(g, 0, (unsigned)sx | ((unsigned)y << 16));
+                }
+                __syncthreads();
+                int reg_size = 1;
+                for (int i = 0; i < reg_size; ++i) {
+                    const unsigned pv = q_get(g, i);
+                    const int px = (int)(pv & 0xffffu), py = (int)(pv >> 16);
+                    const int xx_min = max(px - 1, 0), xx_max = min(px + 1, sw - 1);
+                    const int yy_min = max(py - 1, 0), yy_max = min(py + 1, sh - 1);
+                    // lanes 0..8 fetch the 3x3 neighbourhood's static data in parallel
+                    LsdPix nb;
+                    nb.deg = kNotdefF; nb.c = 0.f; nb.s = 0.f;
+                    if (lane < 9) {
+                        const int nx = px - 1 + lane % 3, ny = py - 1 + lane / 3;
+                        if (nx >= xx_min && nx <= xx_max && ny >= yy_min && ny <= yy_max) nb = g.P[ny * sw + nx];
+                    }
+                    for (int k = 0; k < 9; ++k) {
+                        const int nx = px - 1 + k % 3, ny = py - 1 + k / 3;
+                        if (nx < xx_min || nx > xx_max || ny < yy_min || ny > yy_max) continue;
+                        const int ca = ny * sw + nx;
+                        if (used_get(g.used, ca)) continue;
+                        const float deg = __shfl(nb.deg, k);
+                        if (!is_aligned_deg(deg, reg_angle, prec)) continue;
+                        const float cc = __shfl(nb.c, k), ss = __shfl(nb.s, k);
+                        __syncthreads();
+                        if (lane == 0) {
+                            used_set(g.used, ca);
+                            q_put(g, reg_size, (unsigned)nx | ((unsigned)ny << 16));
+                        }
+                        __syncthreads();
+                        ++reg_size;
+                        sumdx += cc;
+                        sumdy += ss;
+                        reg_angle = (double)plvi_fast_atan2(sumdy, sumdx) * kD2R;
+                    }
+                }
+                if (reg_size < min_reg) continue;
+                // ---- region2rect (lsd.cpp:688-744): sequential double sums in region order
+                double xs = 0, ys = 0, sum = 0;
+                for (int base = 0; base < reg_size; base += 64) {
+                    const int j = base + lane;
+                    unsigned pv = 0;
+                    double wgt = 0;
+                    if (j < reg_size) {
+                        pv = q_get(g, j);
+                        wgt = g.M[(int)(pv >> 16) * sw + (int)(pv & 0xffffu)];
+                    }
+                    const int n = min(64, reg_size - base);
+                    for (int t = 0; t < n; ++t) {
+                        const unsigned q = __shfl(pv, t);
+                        const double w = __shfl(wgt, t);
+                        xs += (double)(int)(q & 0xffffu) * w;
+                        ys += (double)(int)(q >> 16) * w;
+                        sum += w;
+                    }
+                }
+                xs /= sum;
+                ys /= sum;
+                // get_theta
+                double Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
+                for (int base = 0; base < reg_size; base += 64) {
+                    const int j = base + lane;
+                    unsigned pv = 0;
+                    double wgt = 0;
+                    if (j < reg_size) {
+                        pv = q_get(g, j);
+                        wgt = g.M[(int)(pv >> 16) * sw + (int)(pv & 0xffffu)];
+                    }
+                    const int n = min(64, reg_size - base);
+                    for (int t = 0; t < n; ++t) {
+                        const unsigned q = __shfl(pv, t);
+                        const double w = __shfl(wgt, t);
+                        const double dx = (double)(int)(q & 0xffffu) - xs;
+                        const double dy = (double)(int)(q >> 16) - ys;
+                        Ixx += dy * dy * w;
+                        Iyy += dx * dx * w;
+                        Ixy -= dx * dy * w;
+                    }
+                }
+                const double lambda = 0.5 * (Ixx + Iyy - __builtin_sqrt((Ixx - Iyy) * (Ixx - Iyy) + 4.0 * Ixy * Ixy));
+                double theta = (__builtin_fabs(Ixx) > __builtin_fabs(Iyy))
+                                   ? (double)plvi_fast_atan2((float)(lambda - Ixx), (float)Ixy)
+                                   : (double)plvi_fast_atan2((float)Ixy, (float)(lambda - Iyy));
+                theta *= kD2R;
+                if (angle_diff(theta, reg_angle) > prec) theta += kPi;
+                const double dxv = plvi_cos(theta), dyv = plvi_sin(theta);
+                // l/w extents: the reference's if/else-if max/min is equivalent to
+                // independent max(0, .)/min(0, .) (l_min <= 0 <= l_max throughout).
+                double lmax = 0, lmin = 0;
+                for (int j = lane; j < reg_size; j += 64) {
+                    const unsigned q = q_get(g, j);
+                    const double regdx = (double)(int)(q & 0xffffu) - xs;
+                    const double regdy = (double)(int)(q >> 16) - ys;
+                    const double l = regdx * dxv + regdy * dyv;
+                    lmax = l > lmax ? l : lmax;
+                    lmin = l < lmin ? l : lmin;
+                }
+                for (int s = 32; s > 0; s >>= 1) {
+                    const double a = __shfl_xor(lmax, s), b = __shfl_xor(lmin, s);
+                    lmax = a > lmax ? a : lmax;
+                    lmin = b < lmin ? b : lmin;
+                }
+                double x1 = xs + lmin * dxv, y1 = ys + lmin * dyv;
+                double x2 = xs + lmax * dxv, y2 = ys + lmax * dyv;
+                x1 += 0.5; y1 += 0.5; x2 += 0.5; y2 += 0.5;
+                if (scale_lsd != 1) {
+                    x1 /= scale_lsd; y1 /= scale_lsd; x2 /= scale_lsd; y2 /= scale_lsd;
+                }
+                if (nout < kLsdRawCap) {
+                    if (lane == 0) out[nout] = LsdLine{(float)x1, (float)y1, (float)x2, (float)y2};
+                    ++nout;
+                } else {
+                    overflow = true;
+                }
+            }
+        }
+    }
+    if (lane == 0) {
+        nlines[f * nOct + o] = nout;
+        if (overflow) atomicOr(err, 4);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// LK4: KeyLine assembly (LSDDetector_custom.cpp:306-346) + top-k filter
+// (LineExtractor.cc:75-84: libstdc++ std::sort by response desc, truncate,
+// class_id = i) + line equations (:106-115).  One workgroup per frame.
+// ---------------------------------------------------------------------------
+__device__ inline bool clip_line_ll(long long W, long long H, long long& x1, long long& y1, long long& x2,
+                                    long long& y2) {
+    int c1, c2;
+    const long long right = W - 1, bottom = H - 1;
+    if (W <= 0 || H <= 0) return false;
+    c1 = (x1 < 0) + (x1 > right) * 2 + (y1 < 0) * 4 + (y1 > bottom) * 8;
+    c2 = (x2 < 0) + (x2 > right) * 2 + (y2 < 0) * 4 + (y2 > bottom) * 8;
+    if ((c1 & c2) == 0 && (c1 | c2) != 0) {
+        long long a;
+        if (c1 & 12) {
+            a = c1 < 8 ? 0 : bottom;
+            x1 += (long long)((double)(a - y1) * (x2 - x1) / (y2 - y1));
+            y1 = a;
+            c1 = (x1 < 0) + (x1 > right) * 2;
+        }
+        if (c2 & 12) {
+            a = c2 < 8 ? 0 : bottom;
+            x2 += (long long)((double)(a - y2) * (x2 - x1) / (y2 - y1));
+            y2 = a;
+            c2 = (x2 < 0) + (x2 > right) * 2;
+        }
+        if ((c1 & c2) == 0 && (c1 | c2) != 0) {
+            if (c1) {
+                a = c1 == 1 ? 0 : right;
+                y1 += (long long)((double)(a - x1) * (y2 - y1) / (x2 - x1));
+                x1 = a;
+                c1 = 0;
+            }
+            if (c2) {
+                a = c2 == 1 ? 0 : right;
+                y2 += (long long)((double)(a - x2) * (y2 - y1) / (x2 - x1));
+                x2 = a;
+                c2 = 0;
+            }
+        }
+    }
+    return (c1 | c2) == 0;
+}
+
+__device__ inline int line_iter_count(int W, int H, float fx1, float fy1, float fx2, float fy2) {
+    int x1 = cv_round_f(fx1), y1 = cv_round_f(fy1), x2 = cv_round_f(fx2), y2 = cv_round_f(fy2);
+    if ((unsigned)x1 >= (unsigned)W || (unsigned)x2 >= (unsigned)W || (unsigned)y1 >= (unsigned)H ||
+        (unsigned)y2 >= (unsigned)H) {
+        long long a = x1, b = y1, c = x2, d = y2;
+        if (!clip_line_ll(W, H, a, b, c, d)) return 0;
+        x1 = (int)a; y1 = (int)b; x2 = (int)c; y2 = (int)d;
+    }
+    const int dx = abs(x2 - x1), dy = abs(y2 - y1);
+    return max(dx, dy) + 1;
+}
+
+constexpr int kKlCap = 4096;  // keylines per frame before the top-k filter
+
+__global__ __launch_bounds__(256) void line_assemble_kernel(const LineOctDev* __restrict__ octs, int nOct,
+                                                            const LsdLine* __restrict__ lines,
+                                                            const int* __restrict__ nlines, double min_length,
+                                                            int nfeatures, int fcap, plvi_keyline* __restrict__ kl_out,
+                                                            double* __restrict__ fn_out, int* __restrict__ count_out,
+                                                            plvi_keyline* __restrict__ kl_tmp, int* __restrict__ err) {
+    __shared__ int s_scan[256];
+    __shared__ int s_base;
+    __shared__ SortItem s_items[kKlCap];
+    const int f = blockIdx.x;
+    plvi_keyline* tmp = kl_tmp + (size_t)f * kKlCap;
+    if (threadIdx.x == 0) s_base = 0;
+    __syncthreads();
+    for (int o = 0; o < nOct; ++o) {
+        const LineOctDev& od = octs[o];
+        const int n = nlines[f * nOct + o];
+        const LsdLine* L = lines + (size_t)(f * nOct + o) * kLsdRawCap;
+        const int W = od.w, H = od.h;
+        for (int base = 0; base < n; base += 256) {
+            const int k = base + threadIdx.x;
+            plvi_keyline kl;
+            int keep = 0;
+            if (k < n) {
+                float e0 = L[k].x1, e1 = L[k].y1, e2 = L[k].x2, e3 = L[k].y2;
+                // checkLineExtremes (LSDDetector_custom.cpp:112-138)
+                if (e0 < 0) e0 = 0;
+                if (e0 >= W) e0 = (float)W - 1.0f;
+                if (e2 < 0) e2 = 0;
+                if (e2 >= W) e2 = (float)W - 1.0f;
+                if (e1 < 0) e1 = 0;
+                if (e1 >= H) e1 = (float)H - 1.0f;
+                if (e3 < 0) e3 = 0;
+                if (e3 >= H) e3 = (float)H - 1.0f;
+                const double d0 = (double)(e0 - e2), d1 = (double)(e1 - e3);
+                const double length = (float)__builtin_sqrt(d0 * d0 + d1 * d1);
+                if (length > min_length) {
+                    keep = 1;
+                    const float os = od.octaveScale;
+                    kl.startPointX = e0 * os;
+                    kl.startPointY = e1 * os;
+                    kl.endPointX = e2 * os;
+                    kl.endPointY = e3 * os;
+                    kl.sPointInOctaveX = e0;
+                    kl.sPointInOctaveY = e1;
+                    kl.ePointInOctaveX = e2;
+                    kl.ePointInOctaveY = e3;
+                    kl.lineLength = (float)length;
+                    kl.numOfPixels = line_iter_count(W, H, e0, e1, e2, e3);
+                    kl.angle = plvi_atan2f(kl.endPointY - kl.startPointY, kl.endPointX - kl.startPointX);
+                    kl.octave = o;
+                    kl.size = (kl.endPointX - kl.startPointX) * (kl.endPointY - kl.startPointY);
+                    kl.response = kl.lineLength / (float)od.maxWH;
+                    kl.pt_x = (kl.endPointX + kl.startPointX) / 2;
+                    kl.pt_y = (kl.endPointY + kl.startPointY) / 2;
+                }
+            }
+            s_scan[threadIdx.x] = keep;
+            __syncthreads();
+            for (int s = 1; s < 256; s <<= 1) {
+                const int v = threadIdx.x >= s ? s_scan[threadIdx.x - s] : 0;
+                __syncthreads();
+                s_scan[threadIdx.x] += v;
+                __syncthreads();
+            }
+            const int pos = s_base + s_scan[threadIdx.x] - keep;
+            if (keep) {
+                kl.class_id = pos;
+                if (pos < kKlCap) tmp[pos] = kl;
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) s_base += s_scan[255];
+            __syncthreads();
+        }
+    }
+    const int n = s_base;
+    if (n > kKlCap) {
+        if (threadIdx.x == 0) { count_out[f] = 0; atomicOr(err, 8); }
+        return;
+    }
+    int nfinal = n;
+    const bool truncate = n > nfeatures && nfeatures != 0;
+    if (truncate) {
+        for (int i = threadIdx.x; i < n; i += 256) s_items[i] = SortItem{tmp[i].response, i};
+        __syncthreads();
+        if (threadIdx.x == 0) std_sort(s_items, s_items + n);
+        __syncthreads();
+        nfinal = nfeatures;
+    }
+    if (nfinal > fcap) {
+        if (threadIdx.x == 0) { count_out[f] = 0; atomicOr(err, 8); }
+        return;
+    }
+    plvi_keyline* outk = kl_out + (size_t)f * fcap;
+    double* outf = fn_out + (size_t)f * fcap * 3;
+    for (int i = threadIdx.x; i < nfinal; i += 256) {
+        plvi_keyline kl = truncate ? tmp[s_items[i].idx] : tmp[i];
+        if (truncate) kl.class_id = i;
+        outk[i] = kl;
+        // lineF = (sp x ep) / sqrt(l0^2 + l1^2), Eigen Vector3d (LineExtractor.cc:106-115)
+        const double sx = kl.startPointX, sy = kl.startPointY, ex = kl.endPointX, ey = kl.endPointY;
+        const double a = sy * 1.0 - 1.0 * ey, b = 1.0 * ex - sx * 1.0, c = sx * ey - sy * ex;
+        const double nrm = __builtin_sqrt(a * a + b * b);
+        outf[3 * i] = a / nrm;
+        outf[3 * i + 1] = b / nrm;
+        outf[3 * i + 2] = c / nrm;
+    }
+    if (threadIdx.x == 0) count_out[f] = nfinal;
+}
+
+// ---------------------------------------------------------------------------
+// LB1: LBD octave 0 = GaussianBlur(5x5, 1) fixed point (taps 14,62,104,62,14)
+// of the full frame (binary_descriptor_custom.cpp:359), Sobel dx/dy int16
+// (:396-397).  LB2: octave 1 = pyrDown(blurred) (:367) + Sobel.
+// 64x16 tiles; all borders reflect-101.
+// ---------------------------------------------------------------------------
+constexpr int kBTW = 64, kBTH = 16;
+
+__global__ __launch_bounds__(256) void lbd_blur_sobel_kernel(const uint8_t* __restrict__ src, size_t s_frame,
+                                                             size_t s_row, int w, int h, uint8_t* __restrict__ blur,
+                                                             int16_t* __restrict__ dxo, int16_t* __restrict__ dyo,
+                                                             size_t d_frame) {
+    constexpr int EW = kBTW + 6, EH = kBTH + 6;  // input: halo 3 (2 blur + 1 sobel)
+    __shared__ uint8_t I[EH][EW];
+    __shared__ int Hs[EH][kBTW + 2];
+    __shared__ uint8_t Bv[kBTH + 2][kBTW + 2];
+    const int f = blockIdx.z;
+    const int X0 = blockIdx.x * kBTW, Y0 = blockIdx.y * kBTH;
+    const uint8_t* S = src + (size_t)f * s_frame;
+    for (int i = threadIdx.x; i < EW * EH; i += 256) {
+        const int r = i / EW, c = i % EW;
+        I[r][c] = S[(size_t)reflect101(Y0 - 3 + r, h) * s_row + reflect101(X0 - 3 + c, w)];
+    }
+    __syncthreads();
+    // horizontal 5-tap at virtual cols X0-1 .. X0+kBTW (kBTW+2), all EH rows
+    for (int i = threadIdx.x; i < EH * (kBTW + 2); i += 256) {
+        const int r = i / (kBTW + 2), c = i % (kBTW + 2);
+        const uint8_t* e = &I[r][c];
+        Hs[r][c] = 14 * (e[0] + e[4]) + 62 * (e[1] + e[3]) + 104 * e[2];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < (kBTH + 2) * (kBTW + 2); i += 256) {
+        const int r = i / (kBTW + 2), c = i % (kBTW + 2);
+        const unsigned s = (unsigned)(14 * (Hs[r][c] + Hs[r + 4][c]) + 62 * (Hs[r + 1][c] + Hs[r + 3][c]) +
+                                      104 * Hs[r + 2][c]);
+        Bv[r][c] = (uint8_t)min((s + 32768u) >> 16, 255u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kBTH * kBTW; i += 256) {
+        const int ty = i / kBTW, tx = i % kBTW;
+        const int x = X0 + tx, y = Y0 + ty;
+        if (x >= w || y >= h) continue;
+        const int r = ty + 1, c = tx + 1;
+        const int gx = (Bv[r - 1][c + 1] - Bv[r - 1][c - 1]) + 2 * (Bv[r][c + 1] - Bv[r][c - 1]) +
+                       (Bv[r + 1][c + 1] - Bv[r + 1][c - 1]);
+        const int gy = (Bv[r + 1][c - 1] - Bv[r - 1][c - 1]) + 2 * (Bv[r + 1][c] - Bv[r - 1][c]) +
+                       (Bv[r + 1][c + 1] - Bv[r - 1][c + 1]);
+        const size_t o = (size_t)f * d_frame + (size_t)y * w + x;
+        blur[o] = Bv[r][c];
+        dxo[o] = (int16_t)gx;
+        dyo[o] = (int16_t)gy;
+    }
+}
+
+__global__ __launch_bounds__(256) void lbd_pyrdown_sobel_kernel(const uint8_t* __restrict__ blur0, int w0, int h0,
+                                                                size_t s_frame, int w, int h,
+                                                                int16_t* __restrict__ dxo, int16_t* __restrict__ dyo,
+                                                                size_t d_frame) {
+    __shared__ uint8_t P[kBTH + 2][kBTW + 2];
+    const int f = blockIdx.z;
+    const int X0 = blockIdx.x * kBTW, Y0 = blockIdx.y * kBTH;
+    const uint8_t* S = blur0 + (size_t)f * s_frame;
+    for (int i = threadIdx.x; i < (kBTH + 2) * (kBTW + 2); i += 256) {
+        const int r = i / (kBTW + 2), c = i % (kBTW + 2);
+        // pyrDown output at the reflected physical position (the 2:1 grid is not
+        // symmetric about the far edge, so reflect before evaluating).
+        const int py = reflect101(Y0 - 1 + r, h), px = reflect101(X0 - 1 + c, w);
+        int s = 0;
+        const int kk[5] = {1, 4, 6, 4, 1};
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const uint8_t* R = S + (size_t)reflect101(2 * py + j - 2, h0) * w0;
+            int row = 0;
+#pragma unroll
+            for (int i2 = 0; i2 < 5; ++i2) row += kk[i2] * R[reflect101(2 * px + i2 - 2, w0)];
+            s += kk[j] * row;
+        }
+        P[r][c] = (uint8_t)((s + 128) >> 8);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kBTH * kBTW; i += 256) {
+        const int ty = i / kBTW, tx = i % kBTW;
+        const int x = X0 + tx, y = Y0 + ty;
+        if (x >= w || y >= h) continue;
+        const int r = ty + 1, c = tx + 1;
+        const int gx = (P[r - 1][c + 1] - P[r - 1][c - 1]) + 2 * (P[r][c + 1] - P[r][c - 1]) +
+                       (P[r + 1][c + 1] - P[r + 1][c - 1]);
+        const int gy = (P[r + 1][c - 1] - P[r - 1][c - 1]) + 2 * (P[r + 1][c] - P[r - 1][c]) +
+                       (P[r + 1][c + 1] - P[r - 1][c + 1]);
+        const size_t o = (size_t)f * d_frame + (size_t)y * w + x;
+        dxo[o] = (int16_t)gx;
+        dyo[o] = (int16_t)gy;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// LB3: BinaryDescriptor::computeLBD (binary_descriptor_custom.cpp:1073-1342)
+// + binaryConversion (:402-414, :663-667).  One wave per keyline: lane h
+// walks support-region row h (63 rows) with the reference's sequential
+// float stepping; lane 0 then accumulates the bands in row order and
+// normalises.  Gaussian coefficient tables come from the host (double exp,
+// cast to float at use, :1189/:1203).
+// ---------------------------------------------------------------------------
+__constant__ float c_gaussG[63];
+__constant__ float c_gaussL[21];
+__constant__ unsigned char c_comb[64];
+
+__global__ __launch_bounds__(64) void lbd_describe_kernel(const LineOctDev* __restrict__ octs,
+                                                          const int16_t* __restrict__ dx_all,
+                                                          const int16_t* __restrict__ dy_all,
+                                                          const plvi_keyline* __restrict__ kls,
+                                                          const int* __restrict__ counts, int fcap,
+                                                          uint8_t* __restrict__ desc) {
+    __shared__ float rs[4][64];
+    __shared__ float dv[72];
+    const int li = blockIdx.x, f = blockIdx.y;
+    if (li >= counts[f]) return;
+    const plvi_keyline kl = kls[(size_t)f * fcap + li];
+    const LineOctDev& od = octs[kl.octave];
+    const int16_t* pdx = dx_all + od.loff + (size_t)f * od.lplane;
+    const int16_t* pdy = dy_all + od.loff + (size_t)f * od.lplane;
+    const short realWidth = (short)od.lw;
+    const short imageWidth = realWidth - 1;
+    const short imageHeight = (short)(od.lh - 1);
+    const short lengthOfLSP = (short)kl.numOfPixels;
+    const short halfWidth = (lengthOfLSP - 1) / 2;
+    const short halfHeight = (63 - 1) / 2;
+    const float mX = (float)(0.5 * (double)(kl.sPointInOctaveX + kl.ePointInOctaveX));
+    const float mY = (float)(0.5 * (double)(kl.sPointInOctaveY + kl.ePointInOctaveY));
+    const float dL0 = plvi_cosf(kl.angle), dL1 = plvi_sinf(kl.angle);
+    const float dO0 = -dL1, dO1 = dL0;
+    const int h = threadIdx.x;
+    float pL = 0, nL = 0, pO = 0, nO = 0;
+    if (h < 63) {
+        float sX0 = -dL0 * halfWidth + dL1 * halfHeight + mX;
+        float sY0 = -dL1 * halfWidth - dL0 * halfHeight + mY;
+        for (int k = 0; k < h; ++k) {
+            sX0 -= dL1;
+            sY0 += dL0;
+        }
+        float sX = sX0, sY = sY0;
+        for (short w = 0; w < lengthOfLSP; ++w) {
+            short t = (short)__builtin_roundf(sX);
+            const short xc = (t < 0) ? 0 : (t > imageWidth) ? imageWidth : t;
+            t = (short)__builtin_roundf(sY);
+            const short yc = (t < 0) ? 0 : (t > imageHeight) ? imageHeight : t;
+            const short dx = pdx[yc * realWidth + xc];
+            const short dy = pdy[yc * realWidth + xc];
+            const float gDL = dx * dL0 + dy * dL1;
+            const float gDO = dx * dO0 + dy * dO1;
+            if (gDL > 0) pL += gDL;
+            else nL -= gDL;
+            if (gDO > 0) pO += gDO;
+            else nO -= gDO;
+            sX += dL0;
+            sY += dL1;
+        }
+    }
+    rs[0][h] = pL; rs[1][h] = nL; rs[2][h] = pO; rs[3][h] = nO;
+    __syncthreads();
+    if (h == 0) {
+        float pLB[9] = {0}, nLB[9] = {0}, pL2B[9] = {0}, nL2B[9] = {0};
+        float pOB[9] = {0}, nOB[9] = {0}, pO2B[9] = {0}, nO2B[9] = {0};
+        for (int r = 0; r < 63; ++r) {
+            float c = c_gaussG[r];
+            const float pLr = c * rs[0][r], nLr = c * rs[1][r];
+            const float pL2r = pLr * pLr, nL2r = nLr * nLr;
+            const float pOr = c * rs[2][r], nOr = c * rs[3][r];
+            const float pO2r = pOr * pOr, nO2r = nOr * nOr;
+            int band = r / 7;
+            c = c_gaussL[r % 7 + 7];
+            pLB[band] += c * pLr; nLB[band] += c * nLr;
+            pL2B[band] += c * c * pL2r; nL2B[band] += c * c * nL2r;
+            pOB[band] += c * pOr; nOB[band] += c * nOr;
+            pO2B[band] += c * c * pO2r; nO2B[band] += c * c * nO2r;
+            band--;
+            if (band >= 0) {
+                c = c_gaussL[r % 7 + 14];
+                pLB[band] += c * pLr; nLB[band] += c * nLr;
+                pL2B[band] += c * c * pL2r; nL2B[band] += c * c * nL2r;
+                pOB[band] += c * pOr; nOB[band] += c * nOr;
+                pO2B[band] += c * c * pO2r; nO2B[band] += c * c * nO2r;
+            }
+            band = band + 2;
+            if (band < 9) {
+                c = c_gaussL[r % 7];
+                pLB[band] += c * pLr; nLB[band] += c * nLr;
+                pL2B[band] += c * c * pL2r; nL2B[band] += c * c * nL2r;
+                pOB[band] += c * pOr; nOB[band] += c * nOr;
+                pO2B[band] += c * c * pO2r; nO2B[band] += c * c * nO2r;
+            }
+        }
+        const float invN2 = (float)(1.0 / (7 * 2.0)), invN3 = (float)(1.0 / (7 * 3.0));
+        for (int b = 0; b < 9; ++b) {
+            const float invN = (b == 0 || b == 8) ? invN2 : invN3;
+            const int d = b * 8;
+            float t = pLB[b] * invN;
+            dv[d] = t;
+            dv[d + 4] = __builtin_sqrtf(pL2B[b] * invN - t * t);
+            t = nLB[b] * invN;
+            dv[d + 1] = t;
+            dv[d + 5] = __builtin_sqrtf(nL2B[b] * invN - t * t);
+            t = pOB[b] * invN;
+            dv[d + 2] = t;
+            dv[d + 6] = __builtin_sqrtf(pO2B[b] * invN - t * t);
+            t = nOB[b] * invN;
+            dv[d + 3] = t;
+            dv[d + 7] = __builtin_sqrtf(nO2B[b] * invN - t * t);
+        }
+        float tM = 0, tS = 0;
+        for (int b = 0; b < 9; ++b) {
+            const float* v = dv + 8 * b;
+            tM += v[0] * v[0]; tM += v[1] * v[1]; tM += v[2] * v[2]; tM += v[3] * v[3];
+            tS += v[4] * v[4]; tS += v[5] * v[5]; tS += v[6] * v[6]; tS += v[7] * v[7];
+        }
+        tM = 1 / __builtin_sqrtf(tM);
+        tS = 1 / __builtin_sqrtf(tS);
+        for (int b = 0; b < 9; ++b) {
+            float* v = dv + 8 * b;
+            v[0] = v[0] * tM; v[1] = v[1] * tM; v[2] = v[2] * tM; v[3] = v[3] * tM;
+            v[4] = v[4] * tS; v[5] = v[5] * tS; v[6] = v[6] * tS; v[7] = v[7] * tS;
+        }
+        for (int i = 0; i < 72; ++i)
+            if ((double)dv[i] > 0.4) dv[i] = (float)0.4;
+        float t = 0;
+        for (int i = 0; i < 72; ++i) t += dv[i] * dv[i];
+        t = 1 / __builtin_sqrtf(t);
+        for (int i = 0; i < 72; ++i) dv[i] = dv[i] * t;
+    }
+    __syncthreads();
+    if (h < 32) {
+        const float* f1 = dv + 8 * c_comb[2 * h];
+        const float* f2 = dv + 8 * c_comb[2 * h + 1];
+        unsigned r = 0;
+        for (int i = 0; i < 8; ++i)
+            if (f1[i] > f2[i]) r += 1u << i;
+        desc[((size_t)f * fcap + li) * 32 + h] = (uint8_t)r;
+    }
+}
+
+}  // namespace plvi

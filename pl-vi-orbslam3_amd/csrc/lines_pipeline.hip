@@ -1,0 +1,414 @@
+// lines_pipeline.hip — host orchestration of the line kernels and the line
+// part of the C-ABI.  Replaces ORB_SLAM3::Lineextractor::operator()
+// (src/LineExtractor.cc:45-117, LSD branch) with the reference's constants:
+// LSD sigma_scale 0.6, quant 2, ang_th 22.5, log_eps 1, density 0.6,
+// n_bins 1024 (:56-61), min_length 0.025*min(w,h) (:72).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "lines_device.h"
+#include "lines_kernels.hpp"
+#include "plvi_common.h"
+
+namespace plvi {
+
+static inline int lround_h(float v) { return (int)lrintf(v); }
+static inline int lround_h(double v) { return (int)lrint(v); }
+static inline int lfloor_h(float v) { int i = (int)v; return i - (i > v); }
+
+// getGaussianKernelBitExact (OpenCV 4.2 smooth.dispatch.cpp) in double.
+static void gauss_kernel_f64(int n, double sigma, double* k) {
+    const double scale2X = -0.125 / (sigma * sigma);
+    const int n2 = (n - 1) / 2;
+    std::vector<double> values(n2 + 1);
+    double sum = 0;
+    for (int i = 0, x = 1 - n; i < n2; ++i, x += 2) {
+        double t = std::exp((double)(x * x) * scale2X);
+        values[i] = t;
+        sum += t;
+    }
+    sum *= 2;
+    sum += 1.0;
+    const double mul1 = 1.0 / sum;
+    for (int i = 0; i < n2; ++i) k[i] = k[n - 1 - i] = values[i] * mul1;
+    k[n2] = 1.0 * mul1;
+}
+
+struct LinePipeline {
+    plvi_line_params prm{};
+    int W = 0, H = 0, Bcap = 0, device = 0, nOct = 0, fcap = 0;
+    hipStream_t stream = nullptr;
+    std::vector<LineOctDev> oct;
+    std::vector<float> scaleF, invScaleF;
+    double SCALE = 0.8, prec = 0, rho = 0, min_length = 0;
+    double gk[7]{};
+    DevBuf d_oct, d_tabs, octImg, pix, modg, qspill, rawLines, nlines, klTmp, klOut, fnOut, cntOut, descOut, lbdBlur,
+        lbdDx, lbdDy, err, staging;
+    size_t qspillFrame = 0, lbdPlaneTotal = 0;
+    int lastFrames = 0;
+    static constexpr int kStages = 5, kRing = 512;
+    bool prof = false;
+    int profRuns = 0;
+    std::vector<hipEvent_t> evs;
+
+    ~LinePipeline() {
+        for (auto e : evs) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    int init(const plvi_line_params* p, int width, int height, int max_batch, int dev) {
+        if (!p || width <= 0 || height <= 0 || max_batch <= 0) return PLVI_E_BADARG;
+        if (p->refine != 0 || p->extractor != 0) return PLVI_E_BADARG;  // config: lsd_refine 0, extractor 0 (LSD)
+        if (p->nlevels <= 0 || p->nlevels > kLineMaxOct || p->nfeatures < 0) return PLVI_E_BADARG;
+        prm = *p;
+        W = width; H = height; Bcap = max_batch; device = dev; nOct = p->nlevels;
+        PLVI_CHECK(hipSetDevice(device));
+        PLVI_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        fcap = p->nfeatures > 0 ? p->nfeatures : kKlCap;
+        SCALE = (double)p->lsd_scale;  // LSDOptions::scale is float
+        if (!(SCALE > 0) || SCALE > 1) return PLVI_E_BADARG;
+        const double ANG_TH = 22.5, QUANT = 2.0, SIGMA_SCALE = 0.6;
+        prec = M_PI * ANG_TH / 180;
+        const double pp = ANG_TH / 180;
+        rho = QUANT / std::sin(prec);
+        min_length = 0.025 * std::min(W, H);
+        const double sigma = (SCALE < 1) ? (SIGMA_SCALE / SCALE) : SIGMA_SCALE;
+        const unsigned hk = (unsigned)std::ceil(sigma * std::sqrt(2 * 3.0 * std::log(10.0)));
+        if (SCALE != 1 && 1 + 2 * hk != 7) return PLVI_E_BADARG;  // tile kernel is specialised to 7 taps
+        gauss_kernel_f64(7, sigma, gk);
+        // ComputePyramid(image, scale, nlevels) (LSDDetector_custom.cpp:76-109)
+        scaleF.assign(nOct, 1.f); invScaleF.assign(nOct, 1.f);
+        for (int l = 0; l < nOct; ++l) {
+            if (l > 0) scaleF[l] = scaleF[l - 1] * p->scale;
+            invScaleF[l] = 1.0f / scaleF[l];
+        }
+        oct.resize(nOct);
+        size_t imgOff = 0, sOff = 0, lOff = 0, maxSplane = 0;
+        std::vector<uint8_t> tabs;
+        auto put = [&](const void* src, size_t n) {
+            size_t o = (tabs.size() + 15) & ~size_t(15);
+            tabs.resize(o + n);
+            std::memcpy(tabs.data() + o, src, n);
+            return (long long)o;
+        };
+        for (int l = 0; l < nOct; ++l) {
+            LineOctDev& d = oct[l];
+            std::memset(&d, 0, sizeof(d));
+            d.w = lround_h((float)W * invScaleF[l]);
+            d.h = lround_h((float)H * invScaleF[l]);
+            if (l > 0) {
+                // exact factor 2 required (INTER_AREA fast path): 640x480, 752x480
+                if (d.w * 2 != oct[l - 1].w || d.h * 2 != oct[l - 1].h) return PLVI_E_BADARG;
+                if (std::fabs(scaleF[l] / scaleF[l - 1] - 2.0f) > 0) return PLVI_E_BADARG;
+            }
+            d.plane = (long long)d.w * d.h;
+            d.off = (long long)imgOff;
+            if (l > 0) imgOff += (size_t)d.plane * Bcap;
+            d.sw = SCALE != 1 ? lround_h(d.w * SCALE) : d.w;
+            d.sh = SCALE != 1 ? lround_h(d.h * SCALE) : d.h;
+            d.splane = (long long)d.sw * d.sh;
+            d.soff = (long long)sOff;
+            sOff += (size_t)d.splane * Bcap;
+            maxSplane = std::max(maxSplane, (size_t)d.splane);
+            const double LOG_NT = 5 * (std::log10((double)d.sw) + std::log10((double)d.sh)) / 2 + std::log10(11.0);
+            d.min_reg_size = (int)(-LOG_NT / std::log10(pp));
+            d.octaveScale = (float)std::pow(p->scale, l);
+            d.maxWH = std::max(d.w, d.h);
+            // resize x SCALE tables (f64 INTER_LINEAR, float coefficients)
+            {
+                const double sx = 1. / SCALE, sy = 1. / SCALE;
+                std::vector<int> xofs(d.sw), yrow(2 * d.sh);
+                std::vector<float> xa(2 * d.sw), yb(2 * d.sh);
+                int xmax = d.sw;
+                for (int dx = 0; dx < d.sw; ++dx) {
+                    float fx = (float)((dx + 0.5) * sx - 0.5);
+                    int s = lfloor_h(fx);
+                    fx -= s;
+                    if (s < 0) { fx = 0; s = 0; }
+                    if (s + 1 >= d.w) {
+                        xmax = std::min(xmax, dx);
+                        if (s >= d.w - 1) { fx = 0; s = d.w - 1; }
+                    }
+                    xofs[dx] = s;
+                    xa[2 * dx] = 1.f - fx;
+                    xa[2 * dx + 1] = fx;
+                }
+                for (int dy = 0; dy < d.sh; ++dy) {
+                    float fy = (float)((dy + 0.5) * sy - 0.5);
+                    int s = lfloor_h(fy);
+                    fy -= s;
+                    yrow[2 * dy] = std::min(std::max(s, 0), d.h - 1);
+                    yrow[2 * dy + 1] = std::min(std::max(s + 1, 0), d.h - 1);
+                    yb[2 * dy] = 1.f - fy;
+                    yb[2 * dy + 1] = fy;
+                }
+                d.xmax = xmax;
+                d.tabXofs = put(xofs.data(), xofs.size() * 4);
+                d.tabXa = put(xa.data(), xa.size() * 4);
+                d.tabYrow = put(yrow.data(), yrow.size() * 4);
+                d.tabYb = put(yb.data(), yb.size() * 4);
+            }
+            // LBD pyramid (computeGaussianPyramid: pyrDown to (cols/2, rows/2))
+            d.lw = l == 0 ? W : oct[l - 1].lw / 2;
+            d.lh = l == 0 ? H : oct[l - 1].lh / 2;
+            d.lplane = (long long)d.lw * d.lh;
+            d.loff = (long long)lOff;
+            lOff += (size_t)d.lplane * Bcap;
+        }
+        lbdPlaneTotal = lOff;
+        qspillFrame = maxSplane;
+        if (d_oct.alloc(sizeof(LineOctDev) * nOct) || d_tabs.alloc(tabs.size())) return PLVI_E_HIP;
+        PLVI_CHECK(hipMemcpy(d_oct.p, oct.data(), sizeof(LineOctDev) * nOct, hipMemcpyHostToDevice));
+        PLVI_CHECK(hipMemcpy(d_tabs.p, tabs.data(), tabs.size(), hipMemcpyHostToDevice));
+        // LBD tables (BinaryDescriptor ctor, binary_descriptor_custom.cpp:231-260)
+        {
+            float gL[21], gG[63];
+            double u = (7 * 3 - 1) / 2, sg = (7 * 2 + 1) / 2, inv = -1 / (2 * sg * sg);
+            for (int i = 0; i < 21; ++i) { double dis = i - u; gL[i] = (float)std::exp(dis * dis * inv); }
+            u = (9 * 7 - 1) / 2; sg = u; inv = -1 / (2 * sg * sg);
+            for (int i = 0; i < 63; ++i) { double dis = i - u; gG[i] = (float)std::exp(dis * dis * inv); }
+            static const unsigned char comb[64] = {0, 1, 0, 2, 0, 3, 0, 4, 0, 5, 0, 6, 1, 2, 1, 3, 1, 4, 1, 5, 1, 6,
+                                                   2, 3, 2, 4, 2, 5, 2, 6, 2, 7, 2, 8, 3, 4, 3, 5, 3, 6, 3, 7, 3, 8,
+                                                   4, 5, 4, 6, 4, 7, 4, 8, 5, 6, 5, 7, 5, 8, 6, 7, 6, 8, 7, 8};
+            PLVI_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_gaussL), gL, sizeof(gL)));
+            PLVI_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_gaussG), gG, sizeof(gG)));
+            PLVI_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_comb), comb, sizeof(comb)));
+        }
+        if (octImg.alloc(std::max<size_t>(imgOff, 16)) || pix.alloc(sizeof(LsdPix) * sOff) ||
+            modg.alloc(sizeof(double) * sOff) || qspill.alloc(sizeof(unsigned) * qspillFrame * nOct * Bcap) ||
+            rawLines.alloc(sizeof(LsdLine) * (size_t)kLsdRawCap * nOct * Bcap) ||
+            nlines.alloc(sizeof(int) * nOct * Bcap) || klTmp.alloc(sizeof(plvi_keyline) * (size_t)kKlCap * Bcap) ||
+            klOut.alloc(sizeof(plvi_keyline) * (size_t)fcap * Bcap) || fnOut.alloc(sizeof(double) * 3 * fcap * Bcap) ||
+            cntOut.alloc(sizeof(int) * Bcap) || descOut.alloc((size_t)32 * fcap * Bcap) ||
+            lbdBlur.alloc((size_t)W * H * Bcap) || lbdDx.alloc(sizeof(int16_t) * lbdPlaneTotal) ||
+            lbdDy.alloc(sizeof(int16_t) * lbdPlaneTotal) || err.alloc(sizeof(int)) || staging.alloc((size_t)W * H))
+            return PLVI_E_HIP;
+        PLVI_CHECK(hipMemset(err.p, 0, sizeof(int)));
+        size_t maxWords = 0;
+        for (auto& d : oct) maxWords = std::max(maxWords, (size_t)((d.splane + 31) / 32));
+        growSmem = (maxWords + kLsdQueueLds) * sizeof(unsigned);
+        if (growSmem > 160 * 1024) return PLVI_E_BADARG;
+        PLVI_CHECK(hipFuncSetAttribute((const void*)lsd_grow_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)growSmem));
+        return PLVI_OK;
+    }
+    size_t growSmem = 0;
+
+    int profile(int on) {
+        if (on && evs.empty()) {
+            evs.resize((size_t)kRing * (kStages + 1));
+            for (auto& e : evs) PLVI_CHECK(hipEventCreate(&e));
+        }
+        prof = on != 0;
+        profRuns = 0;
+        return PLVI_OK;
+    }
+    void mark(int s, hipStream_t st) {
+        if (prof && profRuns < kRing) (void)hipEventRecord(evs[(size_t)profRuns * (kStages + 1) + s], st);
+    }
+    int profile_read(float* ms, int* runs) {
+        for (int k = 0; k < kStages; ++k) ms[k] = 0.f;
+        for (int r = 0; r < profRuns; ++r) {
+            PLVI_CHECK(hipEventSynchronize(evs[(size_t)r * (kStages + 1) + kStages]));
+            for (int k = 0; k < kStages; ++k) {
+                float t = 0.f;
+                PLVI_CHECK(hipEventElapsedTime(&t, evs[(size_t)r * (kStages + 1) + k],
+                                               evs[(size_t)r * (kStages + 1) + k + 1]));
+                ms[k] += t;
+            }
+        }
+        if (runs) *runs = profRuns;
+        return PLVI_OK;
+    }
+
+    int run(const uint8_t* d_frames, int nf, size_t frame_stride, size_t row_stride, hipStream_t st) {
+        if (nf <= 0 || nf > Bcap) return PLVI_E_BADARG;
+        if (!st) st = stream;
+        lastFrames = nf;
+        const uint8_t* T = d_tabs.as<uint8_t>();
+        mark(0, st);
+        // LK1: octave pyramid
+        for (int l = 1; l < nOct; ++l) {
+            const LineOctDev& d = oct[l];
+            const uint8_t* s = l == 1 ? d_frames : octImg.as<uint8_t>() + oct[l - 1].off;
+            const size_t sf = l == 1 ? frame_stride : (size_t)oct[l - 1].plane;
+            const size_t sr = l == 1 ? row_stride : (size_t)oct[l - 1].w;
+            hipLaunchKernelGGL(lsd_half_kernel, dim3((d.w * d.h + 255) / 256, nf), dim3(256), 0, st, s, sf, sr,
+                               octImg.as<uint8_t>() + d.off, d.w, d.h, (size_t)d.plane);
+        }
+        mark(1, st);
+        // LK2: LSD prep per octave
+        for (int l = 0; l < nOct; ++l) {
+            const LineOctDev& d = oct[l];
+            const uint8_t* s = l == 0 ? d_frames : octImg.as<uint8_t>() + d.off;
+            const size_t sf = l == 0 ? frame_stride : (size_t)d.plane;
+            const size_t sr = l == 0 ? row_stride : (size_t)d.w;
+            dim3 grid((d.sw + kPTX - 1) / kPTX, (d.sh + kPTY - 1) / kPTY, nf);
+            hipLaunchKernelGGL(lsd_prep_kernel, grid, dim3(256), 0, st, s, sf, sr, d.w, d.h, d.sw, d.sh,
+                               (const int*)(T + d.tabXofs), (const float*)(T + d.tabXa), d.xmax,
+                               (const int*)(T + d.tabYrow), (const float*)(T + d.tabYb), gk[0], gk[1], gk[2], gk[3],
+                               rho, pix.as<LsdPix>() + d.soff, modg.as<double>() + d.soff, (size_t)d.splane,
+                               err.as<int>());
+        }
+        mark(2, st);
+        // LK3: region growing (one wave per octave x frame)
+        hipLaunchKernelGGL(lsd_grow_kernel, dim3(nOct, nf), dim3(64), growSmem, st, d_oct.as<LineOctDev>(),
+                           (const LsdPix*)pix.as<LsdPix>(), (const double*)modg.as<double>(), qspill.as<unsigned>(),
+                           qspillFrame, prec, SCALE, rawLines.as<LsdLine>(), nlines.as<int>(), err.as<int>());
+        mark(3, st);
+        // LK4: keyline assembly + top-k + line equations
+        hipLaunchKernelGGL(line_assemble_kernel, dim3(nf), dim3(256), 0, st, d_oct.as<LineOctDev>(), nOct,
+                           (const LsdLine*)rawLines.as<LsdLine>(), (const int*)nlines.as<int>(), min_length,
+                           prm.nfeatures, fcap, klOut.as<plvi_keyline>(), fnOut.as<double>(), cntOut.as<int>(),
+                           klTmp.as<plvi_keyline>(), err.as<int>());
+        mark(4, st);
+        // LB1/LB2: LBD Gaussian pyramid + Sobel
+        {
+            const LineOctDev& d0 = oct[0];
+            dim3 g0((d0.lw + kBTW - 1) / kBTW, (d0.lh + kBTH - 1) / kBTH, nf);
+            hipLaunchKernelGGL(lbd_blur_sobel_kernel, g0, dim3(256), 0, st, d_frames, frame_stride, row_stride, d0.lw,
+                               d0.lh, lbdBlur.as<uint8_t>(), lbdDx.as<int16_t>() + d0.loff,
+                               lbdDy.as<int16_t>() + d0.loff, (size_t)d0.lplane);
+            for (int l = 1; l < nOct; ++l) {
+                const LineOctDev& d = oct[l];
+                if (l > 1) return PLVI_E_BADARG;  // pyrDown chain beyond octave 1 not wired (config: 2 levels)
+                dim3 g1((d.lw + kBTW - 1) / kBTW, (d.lh + kBTH - 1) / kBTH, nf);
+                hipLaunchKernelGGL(lbd_pyrdown_sobel_kernel, g1, dim3(256), 0, st, (const uint8_t*)lbdBlur.as<uint8_t>(),
+                                   d0.lw, d0.lh, (size_t)d0.lplane, d.lw, d.lh, lbdDx.as<int16_t>() + d.loff,
+                                   lbdDy.as<int16_t>() + d.loff, (size_t)d.lplane);
+            }
+        }
+        // LB3: LBD descriptors
+        hipLaunchKernelGGL(lbd_describe_kernel, dim3(fcap, nf), dim3(64), 0, st, d_oct.as<LineOctDev>(),
+                           (const int16_t*)lbdDx.as<int16_t>(), (const int16_t*)lbdDy.as<int16_t>(),
+                           (const plvi_keyline*)klOut.as<plvi_keyline>(), (const int*)cntOut.as<int>(), fcap,
+                           descOut.as<uint8_t>());
+        mark(5, st);
+        if (prof && profRuns < kRing) ++profRuns;
+        PLVI_CHECK(hipGetLastError());
+        return PLVI_OK;
+    }
+};
+
+}  // namespace plvi
+
+using plvi::LinePipeline;
+
+struct plvi_line_extractor {
+    LinePipeline p;
+};
+
+extern "C" int plvi_lines_create(const plvi_line_params* p, int width, int height, int max_batch, int device,
+                                 plvi_line_extractor** out) {
+    if (!out) return PLVI_E_BADARG;
+    *out = nullptr;
+    auto h = std::make_unique<plvi_line_extractor>();
+    int rc = h->p.init(p, width, height, max_batch, device);
+    if (rc) return rc;
+    *out = h.release();
+    return PLVI_OK;
+}
+
+extern "C" int plvi_lines_destroy(plvi_line_extractor* h) {
+    if (!h) return PLVI_E_BADARG;
+    (void)hipSetDevice(h->p.device);
+    (void)hipStreamSynchronize(h->p.stream);
+    delete h;
+    return PLVI_OK;
+}
+
+extern "C" int plvi_lines_extract_batch(plvi_line_extractor* h, const uint8_t* d_frames, int n_frames,
+                                        size_t frame_stride, size_t row_stride, void* stream) {
+    if (!h || !d_frames) return PLVI_E_BADARG;
+    PLVI_CHECK(hipSetDevice(h->p.device));
+    return h->p.run(d_frames, n_frames, frame_stride, row_stride, (hipStream_t)stream);
+}
+
+extern "C" int plvi_lines_outputs(plvi_line_extractor* h, plvi_keyline** d_kl, uint8_t** d_desc, double** d_fn,
+                                  int** d_count, int* cap) {
+    if (!h) return PLVI_E_BADARG;
+    if (d_kl) *d_kl = h->p.klOut.as<plvi_keyline>();
+    if (d_desc) *d_desc = h->p.descOut.as<uint8_t>();
+    if (d_fn) *d_fn = h->p.fnOut.as<double>();
+    if (d_count) *d_count = h->p.cntOut.as<int>();
+    if (cap) *cap = h->p.fcap;
+    return PLVI_OK;
+}
+
+extern "C" int plvi_lines_extract(plvi_line_extractor* h, const uint8_t* img, int width, int height, size_t stride,
+                                  plvi_keyline* kl, uint8_t* desc, double* line_fns, int cap, int* n) {
+    if (!h) return PLVI_E_BADARG;
+    if (n) *n = 0;
+    if (!img || width <= 0 || height <= 0) return PLVI_E_BADARG;
+    LinePipeline& P = h->p;
+    if (width != P.W || height != P.H) return PLVI_E_BADARG;
+    PLVI_CHECK(hipSetDevice(P.device));
+    PLVI_CHECK(hipMemcpy2DAsync(P.staging.p, (size_t)P.W, img, stride, (size_t)P.W, (size_t)P.H,
+                                hipMemcpyHostToDevice, P.stream));
+    int rc = P.run(P.staging.as<uint8_t>(), 1, (size_t)P.W * P.H, (size_t)P.W, P.stream);
+    if (rc) return rc;
+    int cnt = 0, errv = 0;
+    PLVI_CHECK(hipMemcpyAsync(&cnt, P.cntOut.p, sizeof(int), hipMemcpyDeviceToHost, P.stream));
+    PLVI_CHECK(hipMemcpyAsync(&errv, P.err.p, sizeof(int), hipMemcpyDeviceToHost, P.stream));
+    PLVI_CHECK(hipStreamSynchronize(P.stream));
+    if (errv) {
+        PLVI_CHECK(hipMemset(P.err.p, 0, sizeof(int)));
+        return PLVI_E_OVERFLOW;
+    }
+    if (n) *n = cnt;
+    if (cnt > cap) return PLVI_E_CAPACITY;
+    if (cnt > 0) {
+        if (kl) PLVI_CHECK(hipMemcpy(kl, P.klOut.p, sizeof(plvi_keyline) * cnt, hipMemcpyDeviceToHost));
+        if (desc) PLVI_CHECK(hipMemcpy(desc, P.descOut.p, (size_t)32 * cnt, hipMemcpyDeviceToHost));
+        if (line_fns) PLVI_CHECK(hipMemcpy(line_fns, P.fnOut.p, sizeof(double) * 3 * cnt, hipMemcpyDeviceToHost));
+    }
+    return PLVI_OK;
+}
+
+extern "C" int plvi_lines_pyramid_level(plvi_line_extractor* h, int frame, int level, uint8_t* dst, int* w,
+                                        int* hgt) {
+    if (!h || level < 0 || level >= h->p.nOct || frame < 0 || frame >= h->p.Bcap) return PLVI_E_BADARG;
+    const auto& d = h->p.oct[level];
+    if (w) *w = d.w;
+    if (hgt) *hgt = d.h;
+    if (!dst) return PLVI_OK;
+    if (level == 0) return PLVI_E_BADARG;  // level 0 is the caller's own image (gaussianPyrs[0] == image)
+    PLVI_CHECK(hipSetDevice(h->p.device));
+    PLVI_CHECK(hipStreamSynchronize(h->p.stream));
+    PLVI_CHECK(hipMemcpy(dst, h->p.octImg.as<uint8_t>() + d.off + (size_t)frame * d.plane, (size_t)d.plane,
+                         hipMemcpyDeviceToHost));
+    return PLVI_OK;
+}
+
+extern "C" int plvi_lines_scale_tables(plvi_line_extractor* h, float* scale, float* inv_scale, float* sigma2,
+                                       float* inv_sigma2) {
+    if (!h) return PLVI_E_BADARG;
+    const auto& P = h->p;
+    for (int i = 0; i < P.nOct; ++i) {
+        // Lineextractor (LineExtractor.cc:88-99): sigma2[0] = 1, sigma2[i] = s*s
+        const float s = P.scaleF[i];
+        const float s2 = i > 0 ? s * s : 1.0f;
+        if (scale) scale[i] = s;
+        if (inv_scale) inv_scale[i] = P.invScaleF[i];
+        if (sigma2) sigma2[i] = s2;
+        if (inv_sigma2) inv_sigma2[i] = 1.0f / s2;
+    }
+    return PLVI_OK;
+}
+
+extern "C" int plvi_lines_profile(plvi_line_extractor* h, int enable) {
+    if (!h) return PLVI_E_BADARG;
+    PLVI_CHECK(hipSetDevice(h->p.device));
+    return h->p.profile(enable);
+}
+
+extern "C" int plvi_lines_profile_read(plvi_line_extractor* h, float* stage_ms, int* runs) {
+    if (!h || !stage_ms) return PLVI_E_BADARG;
+    PLVI_CHECK(hipSetDevice(h->p.device));
+    return h->p.profile_read(stage_ms, runs);
+}

@@ -1,0 +1,183 @@
+// std_sort.h — a faithful restatement of libstdc++'s std::sort (introsort:
+// median-of-3 to first, unguarded partition, depth limit 2*lg(n), heapsort
+// fallback, final insertion sort with threshold 16) for device use.
+//
+// Lineextractor sorts keylines with std::sort and a `response >` comparator
+// (src/LineExtractor.cc:78); std::sort is not stable, so the surviving top-k
+// set and its order on ties depend on this exact algorithm.
+// __host__ __device__ so tests compare it against the host libstdc++.
+#pragma once
+
+#ifdef __HIPCC__
+#define PLVI_SORT_HD __host__ __device__
+#else
+#define PLVI_SORT_HD
+#endif
+
+namespace plvi {
+
+struct SortItem {
+    float key;  // KeyLine.response
+    int idx;    // original position
+};
+
+// comp(a, b) = a.response > b.response (sort_lines_by_response)
+PLVI_SORT_HD inline bool sort_comp(const SortItem& a, const SortItem& b) { return a.key > b.key; }
+
+PLVI_SORT_HD inline void sort_swap(SortItem* a, SortItem* b) {
+    SortItem t = *a;
+    *a = *b;
+    *b = t;
+}
+
+PLVI_SORT_HD inline void move_median_to_first(SortItem* result, SortItem* a, SortItem* b, SortItem* c) {
+    if (sort_comp(*a, *b)) {
+        if (sort_comp(*b, *c)) sort_swap(result, b);
+        else if (sort_comp(*a, *c)) sort_swap(result, c);
+        else sort_swap(result, a);
+    } else if (sort_comp(*a, *c)) sort_swap(result, a);
+    else if (sort_comp(*b, *c)) sort_swap(result, c);
+    else sort_swap(result, b);
+}
+
+PLVI_SORT_HD inline SortItem* unguarded_partition(SortItem* first, SortItem* last, SortItem* pivot) {
+    while (true) {
+        while (sort_comp(*first, *pivot)) ++first;
+        --last;
+        while (sort_comp(*pivot, *last)) --last;
+        if (!(first < last)) return first;
+        sort_swap(first, last);
+        ++first;
+    }
+}
+
+PLVI_SORT_HD inline void push_heap(SortItem* first, long hole, long top, SortItem value) {
+    long parent = (hole - 1) / 2;
+    while (hole > top && sort_comp(first[parent], value)) {
+        first[hole] = first[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    first[hole] = value;
+}
+
+PLVI_SORT_HD inline void adjust_heap(SortItem* first, long hole, long len, SortItem value) {
+    const long top = hole;
+    long second = hole;
+    while (second < (len - 1) / 2) {
+        second = 2 * (second + 1);
+        if (sort_comp(first[second], first[second - 1])) second--;
+        first[hole] = first[second];
+        hole = second;
+    }
+    if ((len & 1) == 0 && second == (len - 2) / 2) {
+        second = 2 * (second + 1);
+        first[hole] = first[second - 1];
+        hole = second - 1;
+    }
+    push_heap(first, hole, top, value);
+}
+
+PLVI_SORT_HD inline void make_heap(SortItem* first, SortItem* last) {
+    const long len = last - first;
+    if (len < 2) return;
+    long parent = (len - 2) / 2;
+    while (true) {
+        SortItem v = first[parent];
+        adjust_heap(first, parent, len, v);
+        if (parent == 0) return;
+        parent--;
+    }
+}
+
+PLVI_SORT_HD inline void pop_heap(SortItem* first, SortItem* last, SortItem* result) {
+    SortItem v = *result;
+    *result = *first;
+    adjust_heap(first, 0, last - first, v);
+}
+
+PLVI_SORT_HD inline void heap_sort_range(SortItem* first, SortItem* last) {  // __partial_sort(first,last,last)
+    make_heap(first, last);
+    while (last - first > 1) {
+        --last;
+        pop_heap(first, last, last);
+    }
+}
+
+PLVI_SORT_HD inline void unguarded_linear_insert(SortItem* last) {
+    SortItem val = *last;
+    SortItem* next = last - 1;
+    while (sort_comp(val, *next)) {
+        *last = *next;
+        last = next;
+        --next;
+    }
+    *last = val;
+}
+
+PLVI_SORT_HD inline void insertion_sort(SortItem* first, SortItem* last) {
+    if (first == last) return;
+    for (SortItem* i = first + 1; i != last; ++i) {
+        if (sort_comp(*i, *first)) {
+            SortItem val = *i;
+            for (SortItem* p = i; p != first; --p) *p = *(p - 1);
+            *first = val;
+        } else {
+            unguarded_linear_insert(i);
+        }
+    }
+}
+
+PLVI_SORT_HD inline int lg2(long n) {
+    int r = 0;
+    while (n > 1) { n >>= 1; ++r; }
+    return r;
+}
+
+// __introsort_loop, iterative form of the right-recursion with an explicit
+// stack (the recursion is on [cut, last) first, then the loop continues on
+// [first, cut)).  Depth limits travel with each stacked range.
+PLVI_SORT_HD inline void introsort_loop(SortItem* first, SortItem* last, int depth_limit) {
+    struct Range {
+        SortItem *first, *last;
+        int depth;
+    };
+    Range stack[64];
+    int sp = 0;
+    stack[sp++] = Range{first, last, depth_limit};
+    while (sp > 0) {
+        Range r = stack[--sp];
+        SortItem* f = r.first;
+        SortItem* l = r.last;
+        int depth = r.depth;
+        while (l - f > 16) {
+            if (depth == 0) {
+                heap_sort_range(f, l);
+                break;
+            }
+            --depth;
+            SortItem* mid = f + (l - f) / 2;
+            move_median_to_first(f, f + 1, mid, l - 1);
+            SortItem* cut = unguarded_partition(f + 1, l, f);
+            // recursive call on [cut, l) happens before the loop continues on [f, cut):
+            // process it first (LIFO): push the remaining left part, then the right part.
+            stack[sp++] = Range{f, cut, depth};
+            stack[sp++] = Range{cut, l, depth};
+            break;
+        }
+    }
+}
+
+PLVI_SORT_HD inline void std_sort(SortItem* first, SortItem* last) {
+    if (first == last) return;
+    introsort_loop(first, last, lg2(last - first) * 2);
+    // __final_insertion_sort
+    if (last - first > 16) {
+        insertion_sort(first, first + 16);
+        for (SortItem* i = first + 16; i != last; ++i) unguarded_linear_insert(i);
+    } else {
+        insertion_sort(first, last);
+    }
+}
+
+}  // namespace plvi

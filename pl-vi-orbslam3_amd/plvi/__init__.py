@@ -49,6 +49,11 @@ class OrbParams(ctypes.Structure):
                 ("ini_th_fast", ctypes.c_int), ("min_th_fast", ctypes.c_int)]
 
 
+class LineParams(ctypes.Structure):
+    _fields_ = [("nfeatures", ctypes.c_int), ("refine", ctypes.c_int), ("lsd_scale", ctypes.c_float),
+                ("nlevels", ctypes.c_int), ("scale", ctypes.c_float), ("extractor", ctypes.c_int)]
+
+
 _lib = None
 
 c_int_p = ctypes.POINTER(ctypes.c_int)
@@ -74,6 +79,15 @@ def _declare(lib):
         "plvi_hamming_knn2": ([V, I, V, I, V, V, V, V], I),
         "plvi_line_match_nnr": ([V, I, V, I, F, V], I),
         "plvi_line_match": ([V, I, V, I, F, V], I),
+        "plvi_lines_create": ([ctypes.POINTER(LineParams), I, I, I, I, c_void_pp], I),
+        "plvi_lines_destroy": ([V], I),
+        "plvi_lines_extract": ([V, V, I, I, S, V, V, V, I, P], I),
+        "plvi_lines_extract_batch": ([V, V, I, S, S, V], I),
+        "plvi_lines_outputs": ([V, c_void_pp, c_void_pp, c_void_pp, c_void_pp, P], I),
+        "plvi_lines_pyramid_level": ([V, I, I, V, P, P], I),
+        "plvi_lines_scale_tables": ([V, V, V, V, V], I),
+        "plvi_lines_profile": ([V, I], I),
+        "plvi_lines_profile_read": ([V, V, P], I),
         "plvi_device_malloc": ([c_void_pp, S], I),
         "plvi_device_free": ([V], I),
         "plvi_memcpy": ([V, V, S, I], I),
@@ -262,6 +276,88 @@ class ORBextractor:
     @property
     def mvImagePyramid(self):
         return [self.pyramid_level(l) for l in range(self.nlevels)]
+
+
+class Lineextractor:
+    """ORB_SLAM3::Lineextractor(lsd_nfeatures, lsd_refine, lsd_scale, nlevels, scale, extractor).
+
+    ``extractor(image, mask)`` returns ``(keylines, descriptors, keylineFunctions)``
+    as operator() fills them (src/LineExtractor.cc:45-117): keylines in KeyLine
+    layout, n x 32 LBD descriptors, n x 3 normalised line equations.
+    """
+
+    STAGES = ("pyramid", "lsd_prep", "region_grow", "assemble", "lbd")
+
+    def __init__(self, lsd_nfeatures, lsd_refine, lsd_scale, nlevels, scale, extractor=0, width=640, height=480,
+                 max_batch=1, device=0):
+        self._lib = load()
+        self.params = LineParams(lsd_nfeatures, lsd_refine, lsd_scale, nlevels, scale, extractor)
+        self.width, self.height, self.max_batch, self.nlevels = width, height, max_batch, nlevels
+        h = ctypes.c_void_p()
+        _check(self._lib.plvi_lines_create(ctypes.byref(self.params), width, height, max_batch, device,
+                                           ctypes.byref(h)), "plvi_lines_create")
+        self._h = h
+        cap = ctypes.c_int()
+        self._lib.plvi_lines_outputs(self._h, None, None, None, None, ctypes.byref(cap))
+        self.cap = cap.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.plvi_lines_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __call__(self, image, mask=None):
+        image = np.ascontiguousarray(image, dtype=np.uint8)
+        h, w = image.shape
+        kl = np.zeros(self.cap, KEYLINE_DTYPE)
+        desc = np.zeros((self.cap, 32), np.uint8)
+        fn = np.zeros((self.cap, 3), np.float64)
+        n = ctypes.c_int()
+        _check(self._lib.plvi_lines_extract(self._h, _ptr(image), w, h, w, _ptr(kl), _ptr(desc), _ptr(fn), self.cap,
+                                            ctypes.byref(n)), "plvi_lines_extract")
+        k = n.value
+        return kl[:k].copy(), desc[:k].copy(), fn[:k].copy()
+
+    def extract_batch(self, d_frames_ptr, n_frames, frame_stride, row_stride, stream=None):
+        _check(self._lib.plvi_lines_extract_batch(self._h, ctypes.c_void_p(d_frames_ptr), n_frames, frame_stride,
+                                                  row_stride, ctypes.c_void_p(stream or 0)),
+               "plvi_lines_extract_batch")
+
+    def outputs(self):
+        kl, de, fn, co = (ctypes.c_void_p() for _ in range(4))
+        cap = ctypes.c_int()
+        _check(self._lib.plvi_lines_outputs(self._h, ctypes.byref(kl), ctypes.byref(de), ctypes.byref(fn),
+                                            ctypes.byref(co), ctypes.byref(cap)), "plvi_lines_outputs")
+        return kl.value, de.value, fn.value, co.value, cap.value
+
+    def profile(self, enable=True):
+        _check(self._lib.plvi_lines_profile(self._h, int(enable)), "plvi_lines_profile")
+
+    def profile_read(self):
+        ms = np.zeros(5, np.float32)
+        runs = ctypes.c_int()
+        _check(self._lib.plvi_lines_profile_read(self._h, _ptr(ms), ctypes.byref(runs)), "plvi_lines_profile_read")
+        return dict(zip(self.STAGES, ms.tolist())), runs.value
+
+    def pyramid_level(self, level, frame=0):
+        w, h = ctypes.c_int(), ctypes.c_int()
+        _check(self._lib.plvi_lines_pyramid_level(self._h, frame, level, None, ctypes.byref(w), ctypes.byref(h)),
+               "plvi_lines_pyramid_level")
+        out = np.zeros((h.value, w.value), np.uint8)
+        _check(self._lib.plvi_lines_pyramid_level(self._h, frame, level, _ptr(out), None, None),
+               "plvi_lines_pyramid_level")
+        return out
+
+    def scale_tables(self):
+        out = [np.zeros(self.nlevels, np.float32) for _ in range(4)]
+        _check(self._lib.plvi_lines_scale_tables(self._h, *[_ptr(a) for a in out]), "plvi_lines_scale_tables")
+        return out
 
 
 def hamming_knn2(q, t):

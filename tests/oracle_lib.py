@@ -159,3 +159,46 @@ def match(d1, d2, nnr):
     m = np.zeros(d1.shape[0], np.int32)
     n = lib.oracle_match(_p(d1), d1.shape[0], _p(d2), d2.shape[0], nnr, _p(m))
     return n, m
+
+
+KEYLINE_DTYPE = np.dtype([("angle", "<f4"), ("class_id", "<i4"), ("octave", "<i4"), ("pt_x", "<f4"),
+                          ("pt_y", "<f4"), ("response", "<f4"), ("size", "<f4"), ("startPointX", "<f4"),
+                          ("startPointY", "<f4"), ("endPointX", "<f4"), ("endPointY", "<f4"),
+                          ("sPointInOctaveX", "<f4"), ("sPointInOctaveY", "<f4"), ("ePointInOctaveX", "<f4"),
+                          ("ePointInOctaveY", "<f4"), ("lineLength", "<f4"), ("numOfPixels", "<i4")])
+
+
+def line_extract(img, nfeatures=200, lsd_scale=0.8, nlevels=2, scale=2.0, cap=20000):
+    lib = load()
+    V, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    lib.oracle_line_extract.argtypes = [V, I, I, I, I, F, I, F, V, V, V, I, ctypes.POINTER(I)]
+    lib.oracle_line_extract.restype = I
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    kl = np.zeros(cap, KEYLINE_DTYPE)
+    desc = np.zeros((cap, 32), np.uint8)
+    fn = np.zeros((cap, 3), np.float64)
+    n = ctypes.c_int()
+    rc = lib.oracle_line_extract(_p(img), w, h, w, nfeatures, lsd_scale, nlevels, scale, _p(kl), _p(desc), _p(fn),
+                                 cap, ctypes.byref(n))
+    assert rc == 0, rc
+    k = n.value
+    return kl[:k].copy(), desc[:k].copy(), fn[:k].copy()
+
+
+def lsd_raw(img, lsd_scale=0.8, cap=20000):
+    lib = load()
+    V, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    lib.oracle_lsd_raw.argtypes = [V, I, I, F, V, I, ctypes.POINTER(I)]
+    img = np.ascontiguousarray(img, np.uint8)
+    out = np.zeros((cap, 4), np.float32)
+    n = ctypes.c_int()
+    lib.oracle_lsd_raw(_p(img), img.shape[1], img.shape[0], lsd_scale, _p(out), cap, ctypes.byref(n))
+    return out[:n.value].copy()
+
+
+def line_iterator_count(W, H, x1, y1, x2, y2):
+    lib = load()
+    F, I = ctypes.c_float, ctypes.c_int
+    lib.oracle_line_iterator_count.argtypes = [I, I, F, F, F, F]
+    return lib.oracle_line_iterator_count(W, H, x1, y1, x2, y2)

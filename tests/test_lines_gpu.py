@@ -1,0 +1,88 @@
+"""Line front end parity: HIP path vs the CPU oracle, bit-exact.
+
+KeyLine fields (all 17, bitwise), LBD descriptors byte-for-byte and the
+normalised line equations (doubles, bitwise)."""
+import numpy as np
+import pytest
+
+import oracle_lib as ol
+import plvi
+from plvi import synth
+from util import real_frames
+
+pytestmark = pytest.mark.gpu
+
+
+def _assert_same(got, exp, tag):
+    kg, dg, fg = got
+    ke, de, fe = exp
+    assert len(kg) == len(ke), f"{tag}: n {len(kg)} != {len(ke)}"
+    for f in ke.dtype.names:
+        a, b = kg[f], ke[f]
+        bad = np.flatnonzero(a.view(np.uint32) != b.view(np.uint32)) if a.dtype.kind == "f" else np.flatnonzero(a != b)
+        assert bad.size == 0, f"{tag}: field {f} differs at {bad[:10]} got {a[bad[:5]]} exp {b[bad[:5]]}"
+    bad = np.flatnonzero((dg != de).any(axis=1))
+    assert bad.size == 0, f"{tag}: descriptors differ at rows {bad[:10]}"
+    bad = np.flatnonzero((fg.view(np.uint64) != fe.view(np.uint64)).any(axis=1))
+    assert bad.size == 0, f"{tag}: line functions differ at rows {bad[:10]}"
+
+
+@pytest.fixture(scope="module")
+def lx640(plvi_lib):
+    return plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 640, 480, max_batch=4)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_lines_synthetic_640(lx640, seed):
+    img = synth.frame(seed)
+    _assert_same(lx640(img), ol.line_extract(img), f"synth{seed}")
+
+
+def test_lines_real_euroc_752(plvi_lib):
+    lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 752, 480)
+    fr = real_frames()
+    for k in ("euroc1", "euroc2"):
+        _assert_same(lx(fr[k]), ol.line_extract(fr[k]), k)
+
+
+def test_lines_real_rgb_640(lx640):
+    img = real_frames()["rgb1_gray"]
+    _assert_same(lx640(img), ol.line_extract(img), "rgb1_gray")
+
+
+def test_lines_keep_all_and_100(plvi_lib):
+    img = synth.frame(4)
+    for nf in (0, 100):
+        lx = plvi.Lineextractor(nf, 0, 0.8, 2, 2.0, 0, 640, 480)
+        _assert_same(lx(img), ol.line_extract(img, nfeatures=nf), f"nfeatures={nf}")
+
+
+def test_lines_flat_image(lx640):
+    flat = np.full((480, 640), 77, np.uint8)
+    kg, dg, fg = lx640(flat)
+    ke, de, fe = ol.line_extract(flat)
+    assert len(kg) == len(ke) == 0
+
+
+def test_lines_pyramid_level1(lx640):
+    img = synth.frame(8)
+    lx640(img)
+    s = img.astype(np.int32)
+    tot = s[0::2, 0::2] + s[0::2, 1::2] + s[1::2, 0::2] + s[1::2, 1::2]
+    assert np.array_equal(lx640.pyramid_level(1), ((tot + 2) >> 2).astype(np.uint8))
+
+
+def test_lines_batch_equals_single(lx640):
+    frames = synth.batch(4, seed0=40)
+    buf = plvi.DeviceBuffer(frames.nbytes)
+    buf.upload(frames)
+    lx640.extract_batch(buf.ptr, 4, 640 * 480, 640)
+    plvi.load().plvi_device_synchronize()
+    klp, dep, fnp, cop, cap = lx640.outputs()
+    cnt = plvi.download(cop, np.zeros(4, np.int32))
+    kl = plvi.download(klp, np.zeros(4 * cap, plvi.KEYLINE_DTYPE))
+    de = plvi.download(dep, np.zeros((4 * cap, 32), np.uint8))
+    fn = plvi.download(fnp, np.zeros((4 * cap, 3), np.float64))
+    for f in range(4):
+        s = slice(f * cap, f * cap + cnt[f])
+        _assert_same((kl[s], de[s], fn[s]), ol.line_extract(frames[f]), f"batch{f}")
