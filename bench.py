@@ -2,9 +2,11 @@
 
 A step = one pass of the hot path over one batch of B=64 synthetic 640x480
 frames already resident in HBM:
-  ORB extract (ORBextractor 1000/1.2/8/20/7, all kernels) on the batch, then
-  Hamming kNN-2 matching of every frame's descriptors against the previous
-  frame's (B-1 pairs, ~1000x1000 each).
+  ORB extract (ORBextractor 1000/1.2/8/20/7) on HIP stream A, concurrently
+  LSD + LBD line extract (Lineextractor 200/0/0.8/2/2.0) on HIP stream B,
+  then matching of every frame against the previous one (B-1 pairs):
+  ORB Hamming kNN-2 (~1000x1000) and LineMatcher::match (kNN-2 both ways,
+  ratio 0.9, mutual check).
 value = frames processed by all ranks / max-over-ranks wall time.
 
 Multi-GPU: one process per GPU (torchrun); each rank owns its own sequence of
@@ -53,26 +55,29 @@ def level_stage_bytes(w, h):
     return reads + writes
 
 
-def cpu_baseline(budget_s=10.0):
+def cpu_baseline(budget_s=15.0):
     import oracle_lib
     from plvi import synth
-    frames = [synth.frame(10_000 + i) for i in range(64)]
+    frames = [synth.frame(10_000 + i) for i in range(16)]
     n = 0
     prev = None
     t0 = time.perf_counter()
     while True:
         img = frames[n % len(frames)]
         _, k, d = oracle_lib.orb_extract(img)
+        kl, ld, fn = oracle_lib.line_extract(img)
         if prev is not None:
-            oracle_lib.knn2(d, prev)
-        prev = d
+            oracle_lib.knn2(d, prev[0])
+            if len(ld) >= 2 and len(prev[1]) >= 2:
+                oracle_lib.match(ld, prev[1], 0.9)
+        prev = (d, ld)
         n += 1
         if time.perf_counter() - t0 > budget_s and n >= 3:
             break
     el = time.perf_counter() - t0
     return {"value": n / el, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{n} synthetic 640x480 frames, ORB extract + kNN-2 vs previous frame, "
-                      f"single-thread CPU restatement (oracle/), {el:.1f}s"}
+            "sample": f"{n} synthetic 640x480 frames: ORB extract + LSD/LBD extract + ORB kNN-2 + LineMatcher::match "
+                      f"vs previous frame, single-thread CPU restatement (oracle/), {el:.1f}s"}
 
 
 def main():
@@ -102,40 +107,70 @@ def main():
     B, W, H = args.batch, 640, 480
     frames = torch.from_numpy(synth.batch(B, W, H, seed0=1_000_000 * rank)).to(f"cuda:{dev}")
     orb = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=B, device=dev)
+    lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=B, device=dev)
     kp_p, de_p, co_p, mo_p, cap = orb.outputs()
+    kl_p, lde_p, lfn_p, lco_p, lcap = lx.outputs()
     lib = plvi.load()
-    outs = [torch.empty((B - 1) * cap, dtype=torch.int32, device=f"cuda:{dev}") for _ in range(4)]
-    stream = torch.cuda.current_stream()
-    sp = stream.cuda_stream
+    i32 = dict(dtype=torch.int32, device=f"cuda:{dev}")
+    outs = [torch.empty((B - 1) * cap, **i32) for _ in range(4)]
+    lscratch = torch.empty(4 * (B - 1) * 2 * lcap, **i32)
+    lm12 = torch.empty((B - 1) * lcap, **i32)
+    lnm = torch.empty(B - 1, **i32)
+    sA = torch.cuda.current_stream()
+    sB = torch.cuda.Stream()
+    evA, evB = torch.cuda.Event(), torch.cuda.Event()
+
+    def run_orb():
+        orb.extract_batch(frames.data_ptr(), B, W * H, W, (0, 0), stream=sA.cuda_stream)
+
+    def run_lines():
+        lx.extract_batch(frames.data_ptr(), B, W * H, W, stream=sB.cuda_stream)
+
+    def run_match():
+        rc = lib.plvi_hamming_knn2_batch(de_p + cap * 32, co_p + 4, cap, de_p, co_p, cap, B - 1,
+                                         *[o.data_ptr() for o in outs], sA.cuda_stream)
+        rc |= lib.plvi_line_match_batch(lde_p + lcap * 32, lco_p + 4, lcap, lde_p, lco_p, lcap, B - 1, 0.9,
+                                        lscratch.data_ptr(), lm12.data_ptr(), lnm.data_ptr(), sA.cuda_stream)
+        if rc:
+            raise RuntimeError(f"match {rc}")
 
     def step():
-        orb.extract_batch(frames.data_ptr(), B, W * H, W, (0, 0), stream=sp)
-        rc = lib.plvi_hamming_knn2_batch(de_p + cap * 32, co_p + 4, cap, de_p, co_p, cap, B - 1,
-                                         *[o.data_ptr() for o in outs], sp)
-        if rc:
-            raise RuntimeError(f"knn2 {rc}")
+        evA.record(sA)
+        sB.wait_event(evA)       # lines start after the previous step's matching (buffer reuse)
+        run_lines()
+        run_orb()
+        evB.record(sB)
+        sA.wait_event(evB)
+        run_match()
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
 
-    # stage timing run (separate from the timed region: events add markers)
+    # stage timing run (separate from the timed region: events add markers).
+    # Each extractor runs alone here so its stage times are uncontended.
     orb.profile(True)
+    lx.profile(True)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    knn_ms = 0.0
+    match_ms = 0.0
     nprof = max(3, min(args.steps, 10))
     for _ in range(nprof):
-        orb.extract_batch(frames.data_ptr(), B, W * H, W, (0, 0), stream=sp)
-        ev0.record(stream)
-        lib.plvi_hamming_knn2_batch(de_p + cap * 32, co_p + 4, cap, de_p, co_p, cap, B - 1,
-                                    *[o.data_ptr() for o in outs], sp)
-        ev1.record(stream)
+        run_orb()
         torch.cuda.synchronize()
-        knn_ms += ev0.elapsed_time(ev1)
-    stage_ms, runs = orb.profile_read()
+        run_lines()
+        torch.cuda.synchronize()
+        ev0.record(sA)
+        run_match()
+        ev1.record(sA)
+        torch.cuda.synchronize()
+        match_ms += ev0.elapsed_time(ev1)
+    st_orb, runs = orb.profile_read()
+    st_lines, lruns = lx.profile_read()
     orb.profile(False)
-    stage_ms = {k: v / runs for k, v in stage_ms.items()}
-    stage_ms["knn2"] = knn_ms / nprof
+    lx.profile(False)
+    stage_ms = {f"orb.{k}": v / runs for k, v in st_orb.items()}
+    stage_ms.update({f"lines.{k}": v / lruns for k, v in st_lines.items()})
+    stage_ms["match"] = match_ms / nprof
 
     if world > 1:
         dist.barrier()
@@ -162,7 +197,7 @@ def main():
     dom = max(stage_ms, key=stage_ms.get)
     roof = {
         "bound": "hbm", "kernel": "orb_level_kernel (resize+blur7x7+FAST score, all 8 levels)",
-        "achieved": lvl_bytes / (stage_ms["level"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "achieved": lvl_bytes / (stage_ms["orb.level"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
         "traffic": None,
     }
     roof["frac"] = roof["achieved"] / roof["peak"]
@@ -170,8 +205,9 @@ def main():
         "metric": METRIC, "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-        "config": {"workload": "C1 ORB extract (1000 feats, 1.2, 8 levels, FAST 20/7) + ORB kNN-2 match vs "
-                               "previous frame; LSD/LBD not yet in the step (round 1)",
+        "config": {"workload": "C1+C2+C3: ORB extract (1000 feats, 1.2, 8 levels, FAST 20/7) || LSD+LBD "
+                               "(200 lines, scale 0.8, 2 octaves) on two HIP streams, then ORB kNN-2 + "
+                               "LineMatcher::match vs previous frame",
                    "batch": B, "width": W, "height": H, "parallelism": f"frames-sharded x{world}"},
         "roofline": roof,
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},

@@ -185,6 +185,15 @@ int plvi_line_match_nnr(const uint8_t* desc1, int n1, const uint8_t* desc2, int 
  * matchNNR both ways + mutual check. */
 int plvi_line_match(const uint8_t* desc1, int n1, const uint8_t* desc2, int n2, float nnr, int* matches_12);
 
+/* Batched LineMatcher::match on device descriptor tables: pair p matches
+ * desc1[p] (n1[p] rows, stride cap1) against desc2[p] (n2[p] rows, stride
+ * cap2).  d_scratch must hold 4*n_pairs*(cap1+cap2) ints.  Outputs
+ * matches_12 [n_pairs][cap1] and per-pair match counts.  Pairs with fewer
+ * than 2 rows on the train side produce no matches. */
+int plvi_line_match_batch(const uint8_t* d_desc1, const int* d_n1, int cap1, const uint8_t* d_desc2, const int* d_n2,
+                          int cap2, int n_pairs, float nnr, int* d_scratch, int* d_matches_12, int* d_nmatch,
+                          void* stream);
+
 /* Device memory helpers for bindings that have no HIP runtime of their own
  * (ctypes, JNI): thin wrappers over hipMalloc/hipFree/hipMemcpy on the
  * current device.  kind: 1 = host->device, 2 = device->host, 3 = d->d. */

@@ -67,6 +67,40 @@ __global__ __launch_bounds__(256) void hamming_knn2_kernel(const uint8_t* __rest
     }
 }
 
+// LineMatcher::match (LineMatcher.cpp:92-111) over a batch of pairs, given
+// the kNN-2 tables of both directions: ratio test (float, DMatch::distance)
+// then the mutual check.  One workgroup per pair.
+__global__ __launch_bounds__(256) void line_match_finish_kernel(const int* __restrict__ n1, const int* __restrict__ n2,
+                                                                int cap1, int cap2, const int* __restrict__ i0_12,
+                                                                const int* __restrict__ d0_12,
+                                                                const int* __restrict__ d1_12,
+                                                                const int* __restrict__ i0_21,
+                                                                const int* __restrict__ d0_21,
+                                                                const int* __restrict__ d1_21, float nnr,
+                                                                int* __restrict__ m12, int* __restrict__ nmatch) {
+    __shared__ int s_cnt;
+    const int p = blockIdx.x;
+    const int a = n1[p], b = n2[p];
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    int local = 0;
+    for (int i = threadIdx.x; i < a; i += 256) {
+        const size_t o = (size_t)p * cap1 + i;
+        int m = -1;
+        if (b >= 2 && (float)d0_12[o] < (float)d1_12[o] * nnr) m = i0_12[o];
+        if (m >= 0) {
+            const size_t q = (size_t)p * cap2 + m;
+            const int back = (a >= 2 && (float)d0_21[q] < (float)d1_21[q] * nnr) ? i0_21[q] : -1;
+            if (back != i) m = -1;
+        }
+        m12[o] = m;
+        local += m >= 0;
+    }
+    atomicAdd(&s_cnt, local);
+    __syncthreads();
+    if (threadIdx.x == 0) nmatch[p] = s_cnt;
+}
+
 int launch_knn2(const uint8_t* d_q, const int* d_nq, int nq_cap, const uint8_t* d_t, const int* d_nt, int nt_cap,
                 int n_pairs, int* i0, int* d0, int* i1, int* d1, hipStream_t st) {
     if (n_pairs <= 0 || nq_cap <= 0) return PLVI_OK;
@@ -137,6 +171,29 @@ extern "C" int plvi_hamming_knn2_batch(const uint8_t* d_q, const int* d_nq, int 
     if (!d_q || !d_t || !d_nq || !d_nt || nq_cap < 0 || nt_cap < 0 || n_pairs < 0) return PLVI_E_BADARG;
     return plvi::launch_knn2(d_q, d_nq, nq_cap, d_t, d_nt, nt_cap, n_pairs, d_idx0, d_d0, d_idx1, d_d1,
                              (hipStream_t)stream);
+}
+
+extern "C" int plvi_line_match_batch(const uint8_t* d_desc1, const int* d_n1, int cap1, const uint8_t* d_desc2,
+                                     const int* d_n2, int cap2, int n_pairs, float nnr, int* d_scratch,
+                                     int* d_matches_12, int* d_nmatch, void* stream) {
+    if (!d_desc1 || !d_desc2 || !d_n1 || !d_n2 || !d_scratch || !d_matches_12 || !d_nmatch || n_pairs < 0)
+        return PLVI_E_BADARG;
+    if (n_pairs == 0) return PLVI_OK;
+    hipStream_t st = (hipStream_t)stream;
+    int* s = d_scratch;
+    int *i0a = s, *d0a = s + (size_t)n_pairs * cap1, *i1a = s + 2 * (size_t)n_pairs * cap1,
+        *d1a = s + 3 * (size_t)n_pairs * cap1;
+    int* t = s + 4 * (size_t)n_pairs * cap1;
+    int *i0b = t, *d0b = t + (size_t)n_pairs * cap2, *i1b = t + 2 * (size_t)n_pairs * cap2,
+        *d1b = t + 3 * (size_t)n_pairs * cap2;
+    int rc = plvi::launch_knn2(d_desc1, d_n1, cap1, d_desc2, d_n2, cap2, n_pairs, i0a, d0a, i1a, d1a, st);
+    if (rc) return rc;
+    rc = plvi::launch_knn2(d_desc2, d_n2, cap2, d_desc1, d_n1, cap1, n_pairs, i0b, d0b, i1b, d1b, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(plvi::line_match_finish_kernel, dim3(n_pairs), dim3(256), 0, st, d_n1, d_n2, cap1, cap2, i0a,
+                       d0a, d1a, i0b, d0b, d1b, nnr, d_matches_12, d_nmatch);
+    PLVI_CHECK(hipGetLastError());
+    return PLVI_OK;
 }
 
 extern "C" int plvi_hamming_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, int* idx0, int* d0, int* idx1,

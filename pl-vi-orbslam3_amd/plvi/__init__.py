@@ -79,6 +79,7 @@ def _declare(lib):
         "plvi_hamming_knn2": ([V, I, V, I, V, V, V, V], I),
         "plvi_line_match_nnr": ([V, I, V, I, F, V], I),
         "plvi_line_match": ([V, I, V, I, F, V], I),
+        "plvi_line_match_batch": ([V, V, I, V, V, I, I, F, V, V, V, V], I),
         "plvi_lines_create": ([ctypes.POINTER(LineParams), I, I, I, I, c_void_pp], I),
         "plvi_lines_destroy": ([V], I),
         "plvi_lines_extract": ([V, V, I, I, S, V, V, V, I, P], I),

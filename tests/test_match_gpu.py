@@ -41,3 +41,34 @@ def test_line_match_nnr_and_mutual(plvi_lib):
         n, m = plvi.LineMatcher.match(q, t, nnr)
         ne, me = ol.match(q, t, nnr)
         assert n == ne and np.array_equal(m, me)
+
+
+def test_line_match_batch_device(plvi_lib):
+    rng = np.random.default_rng(21)
+    P, cap = 5, 64
+    d1 = np.zeros((P, cap, 32), np.uint8)
+    d2 = np.zeros((P, cap, 32), np.uint8)
+    n1 = np.array([64, 10, 2, 1, 40], np.int32)
+    n2 = np.array([60, 12, 5, 30, 0], np.int32)
+    for p in range(P):
+        q, t = near_duplicate_descriptors(rng, max(n2[p], 1), max(n1[p], 1), p_flip=0.05)
+        d1[p, :n1[p]] = q[:n1[p]]
+        d2[p, :n2[p]] = t[:n2[p]]
+    bufs = {k: plvi.DeviceBuffer(v.nbytes) for k, v in dict(d1=d1, d2=d2, n1=n1, n2=n2).items()}
+    for k, v in dict(d1=d1, d2=d2, n1=n1, n2=n2).items():
+        bufs[k].upload(v)
+    scratch = plvi.DeviceBuffer(4 * P * 2 * cap * 4)
+    m12 = plvi.DeviceBuffer(P * cap * 4)
+    nm = plvi.DeviceBuffer(P * 4)
+    rc = plvi.load().plvi_line_match_batch(bufs["d1"].ptr, bufs["n1"].ptr, cap, bufs["d2"].ptr, bufs["n2"].ptr, cap, P,
+                                           0.9, scratch.ptr, m12.ptr, nm.ptr, None)
+    assert rc == 0
+    plvi.load().plvi_device_synchronize()
+    got = m12.download(np.zeros((P, cap), np.int32))
+    cnt = nm.download(np.zeros(P, np.int32))
+    for p in range(P):
+        if n1[p] >= 2 and n2[p] >= 2:
+            ne, me = ol.match(d1[p, :n1[p]], d2[p, :n2[p]], 0.9)
+            assert cnt[p] == ne and np.array_equal(got[p, :n1[p]], me)
+        else:
+            assert cnt[p] == 0
