@@ -159,6 +159,10 @@ int plvi_lines_scale_tables(plvi_line_extractor* h, float* scale, float* inv_sca
 /* Stage timing: [0] octave pyramid, [1] LSD prep (blur f64, resize, gradient),
  * [2] region growing + rect, [3] keyline assembly + top-k, [4] LBD. */
 int plvi_lines_profile(plvi_line_extractor* h, int enable);
+/* Diagnostic cycle accounting inside the region-growing kernel (s_memtime):
+ * per (frame, octave) 16 uint64 = [total, pop-prep, commit rounds, rect,
+ * seeds, pops, commits, rect points, slow-path loads]; NULL disables. */
+int plvi_lines_debug_stats(plvi_line_extractor* h, unsigned long long* d_stats);
 int plvi_lines_profile_read(plvi_line_extractor* h, float* stage_ms, int* runs);
 
 /* ------------------------------------------------------------------ Hamming

@@ -43,7 +43,7 @@ __global__ __launch_bounds__(256) void lsd_half_kernel(const uint8_t* __restrict
 //   (RowFilter sequential sum, SymmColumnFilter; lsd.cpp:455),
 //   resize x SCALE f64 INTER_LINEAR with float coefficients (lsd.cpp:457),
 //   ll_angle gradient / norm / fastAtan2 angle (lsd.cpp:561-584).
-// Outputs per scaled pixel: LsdPix {deg | NOTDEF, cosf, sinf} and modgrad (f64).
+// Outputs per scaled pixel: angle in degrees (float, NOTDEF = -1024) and modgrad (f64).
 // ---------------------------------------------------------------------------
 constexpr int kPTX = 32, kPTY = 16;         // scaled tile
 constexpr int kPGW = 48, kPGH = 28;         // max blurred (G) region
@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256) void lsd_prep_kernel(const uint8_t* __restrict
                                                        const float* __restrict__ xa, int xmax,
                                                        const int* __restrict__ yrow, const float* __restrict__ yb,
                                                        double k0, double k1, double k2, double k3, double rho,
-                                                       LsdPix* __restrict__ pix, double* __restrict__ modgrad,
+                                                       float* __restrict__ pix, double* __restrict__ modgrad,
                                                        size_t p_frame, int* __restrict__ err) {
     __shared__ uint8_t I[kPIH][kPIW];
     __shared__ double Hs[kPIH][kPGW];
@@ -114,29 +114,22 @@ __global__ __launch_bounds__(256) void lsd_prep_kernel(const uint8_t* __restrict
         Ss[ty][tx] = H0 * b0 + H1 * b1;
     }
     __syncthreads();
-    LsdPix* P = pix + (size_t)f * p_frame;
+    float* P = pix + (size_t)f * p_frame;
     double* M = modgrad + (size_t)f * p_frame;
     for (int i = threadIdx.x; i < kPTX * kPTY; i += 256) {
         const int ty = i / kPTX, tx = i % kPTX;
         const int x = X0 + tx, y = Y0 + ty;
         if (x >= sw || y >= sh) continue;
-        LsdPix o;
-        o.deg = kNotdefF; o.c = 0.f; o.s = 0.f; o.pad = 0.f;
+        float deg = kNotdefF;
         double norm = 0.0;
         if (x < sw - 1 && y < sh - 1) {
             const double DA = Ss[ty + 1][tx + 1] - Ss[ty][tx];
             const double BC = Ss[ty][tx + 1] - Ss[ty + 1][tx];
             const double gx = DA + BC, gy = DA - BC;
             norm = __builtin_sqrt((gx * gx + gy * gy) / 4);
-            if (!(norm <= rho)) {
-                const float deg = plvi_fast_atan2((float)gx, (float)-gy);
-                const float af = (float)((double)deg * kD2R);
-                o.deg = deg;
-                o.c = plvi_cosf(af);
-                o.s = plvi_sinf(af);
-            }
+            if (!(norm <= rho)) deg = plvi_fast_atan2((float)gx, (float)-gy);
         }
-        P[(size_t)y * sw + x] = o;
+        P[(size_t)y * sw + x] = deg;
         M[(size_t)y * sw + x] = norm;
     }
 }
@@ -147,20 +140,35 @@ __global__ __launch_bounds__(256) void lsd_prep_kernel(const uint8_t* __restrict
 // (:635-686) with the exact float sumdx/sumdy/fastAtan2 update per added
 // pixel, the min_reg_size test, region2rect (:688-744) + get_theta
 // (:746-782) in double with the reference summation order, +0.5, /SCALE.
-// One wave per (octave, frame); the USED map is a bitmap in LDS, region
-// points live in an LDS queue (global spill beyond kLsdQueueLds).
+//
+// One wave per (octave, frame).  LDS holds the USED bitmap of the octave,
+// the region queue (global spill beyond kLsdQueueLds) and a sliding window
+// of R (power of two) rows of gradient angles starting at or above the row
+// before the current seed.  Seeds are visited in raster order, so every
+// defined pixel before the seed is already USED and a region only reaches
+// rows >= seed row; rows beyond the window are read from global memory.
+//
+// Speculative exact growth: the neighbour checks of up to 7 queued points
+// (63 lanes, the reference's scan order = lane order) are decided at once
+// against the current region angle; the exact angle sequence implied by the
+// speculated accepts is then computed (sequential float sums, parallel
+// fastAtan2) and every decision is re-evaluated against the angle it would
+// really see.  The consistent prefix is committed; the first inconsistent
+// lane is re-decided with the exact angle in the next round.  The result is
+// identical to the sequential algorithm.
 // ---------------------------------------------------------------------------
 struct GrowCtx {
-    const LsdPix* P;
+    const float* P;
     const double* M;
     unsigned* used;   // LDS bitmap
     unsigned* qlds;   // LDS queue (x | y<<16)
     unsigned* qglob;  // global spill
-    int sw, sh;
+    float* win;       // LDS angle window: R rows, ring indexed by row & (R-1)
+    int sw, sh, R, wb;
 };
 
 __device__ __forceinline__ bool used_get(const unsigned* u, int a) { return (u[a >> 5] >> (a & 31)) & 1u; }
-__device__ __forceinline__ void used_set(unsigned* u, int a) { u[a >> 5] |= 1u << (a & 31); }
+__device__ __forceinline__ void used_set(unsigned* u, int a) { atomicOr(&u[a >> 5], 1u << (a & 31)); }
 __device__ __forceinline__ unsigned q_get(const GrowCtx& g, int i) {
     return i < kLsdQueueLds ? g.qlds[i] : g.qglob[i - kLsdQueueLds];
 }
@@ -168,7 +176,13 @@ __device__ __forceinline__ void q_put(GrowCtx& g, int i, unsigned v) {
     if (i < kLsdQueueLds) g.qlds[i] = v;
     else g.qglob[i - kLsdQueueLds] = v;
 }
+__device__ __forceinline__ float deg_at(const GrowCtx& g, int x, int y) {
+    if (y < g.wb + g.R) return g.win[(y & (g.R - 1)) * g.sw + x];
+    return g.P[(size_t)y * g.sw + x];
+}
 
+// isAligned (lsd.cpp:1136-1152) with a = (double)deg * DEG_TO_RADS, exactly the
+// value ll_angle stored in angles_data.
 __device__ __forceinline__ bool is_aligned_deg(float deg, double theta, double prec) {
     if (deg == kNotdefF) return false;
     const double a = (double)deg * kD2R;
@@ -188,39 +202,101 @@ __device__ __forceinline__ double angle_diff(double a, double b) {
     return diff < 0 ? -diff : diff;
 }
 
+__device__ __forceinline__ int readlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double shfl_d(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __shfl((int)(b & 0xffffffff), src);
+    const int hi = __shfl((int)(b >> 32), src);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// Load image rows [r0, r1) of angles into their window slots.
+__device__ __forceinline__ void win_load_rows(GrowCtx& g, int r0, int r1, int lane) {
+    const int n = (r1 - r0) * g.sw;
+    const float* src = g.P + (size_t)r0 * g.sw;
+    int i = lane;
+    for (; i + 7 * 64 < n; i += 8 * 64) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = src[i + u * 64];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int j = i + u * 64, row = r0 + j / g.sw, x = j % g.sw;
+            g.win[(row & (g.R - 1)) * g.sw + x] = v[u];
+        }
+    }
+    for (; i < n; i += 64) {
+        const int row = r0 + i / g.sw, x = i % g.sw;
+        g.win[(row & (g.R - 1)) * g.sw + x] = src[i];
+    }
+}
+
 __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restrict__ octs,
-                                                      const LsdPix* __restrict__ pix,
+                                                      const float* __restrict__ pix,
                                                       const double* __restrict__ modgrad,
                                                       unsigned* __restrict__ qspill, size_t qspill_frame,
                                                       double prec, double scale_lsd, LsdLine* __restrict__ lines,
-                                                      int* __restrict__ nlines, int* __restrict__ err) {
+                                                      int* __restrict__ nlines, int* __restrict__ err, int winFloats,
+                                                      int wordsMax, unsigned long long* __restrict__ stats) {
     extern __shared__ __align__(16) unsigned lds_u[];
     const int o = blockIdx.x, f = blockIdx.y, nOct = gridDim.x;
     const LineOctDev& od = octs[o];
     const int sw = od.sw, sh = od.sh;
     const int lane = threadIdx.x;
     const int nwords = (sw * sh + 31) >> 5;
+    // rect staging (region coordinates + weights) shares the queue's LDS words
     GrowCtx g;
     g.P = pix + od.soff + (size_t)f * od.splane;
     g.M = modgrad + od.soff + (size_t)f * od.splane;
     g.used = lds_u;
-    g.qlds = lds_u + nwords;
+    g.qlds = lds_u + wordsMax;
+    g.win = reinterpret_cast<float*>(lds_u + wordsMax + kLsdQueueLds);
     g.qglob = qspill + (size_t)(f * nOct + o) * qspill_frame;
     g.sw = sw; g.sh = sh;
+    {
+        int r = 1;
+        while (r * 2 * sw <= winFloats && r * 2 <= 1024) r *= 2;  // power-of-two ring (host guarantees >= 4)
+        g.R = r;
+    }
+    g.wb = 0;
     for (int i = lane; i < nwords; i += 64) g.used[i] = 0u;
+    win_load_rows(g, 0, min(g.R, sh), lane);
     __syncthreads();
     LsdLine* out = lines + (size_t)(f * nOct + o) * kLsdRawCap;
     int nout = 0;
     bool overflow = false;
     const int min_reg = od.min_reg_size;
+    const int bp = lane / 9, bk = lane % 9;          // block point / neighbour index of this lane
+    const int kdx = bk % 3 - 1, kdy = bk / 3 - 1;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    // optional cycle accounting (diagnostic): [0] total [1] block setup [2] rounds [3] rect
+    // [4] seeds [5] blocks [6] rounds [7] rect points [8] commits
+    unsigned long long st_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const bool do_stats = stats != nullptr;
+    const unsigned long long t_begin = do_stats ? __builtin_amdgcn_s_memtime() : 0;
     for (int y = 0; y < sh - 1; ++y) {
+        // slide the window (half a window at a time) so it holds row y-1 and at
+        // least R/2 rows below it
+        const int half = g.R / 2;
+        if (y - 1 >= g.wb + half && g.wb + g.R < sh) {
+            const int r0 = g.wb + g.R, r1 = min(sh, r0 + half);
+            win_load_rows(g, r0, r1, lane);
+            g.wb += r1 - r0;
+            __syncthreads();
+        }
         for (int xb = 0; xb < sw - 1; xb += 64) {
             const int x = xb + lane;
             bool cand = false;
-            if (x < sw - 1) {
-                const int a = y * sw + x;
-                cand = !used_get(g.used, a) && g.P[a].deg != kNotdefF;
-            }
+            if (x < sw - 1) cand = !used_get(g.used, y * sw + x) && deg_at(g, x, y) != kNotdefF;
             unsigned long long m = __ballot(cand);
             while (m) {
                 const int b = __ffsll((long long)m) - 1;
@@ -229,89 +305,134 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                 const int sa = y * sw + sx;
                 if (used_get(g.used, sa)) continue;  // absorbed by an earlier region of this chunk
                 // ---- region_grow (lsd.cpp:635-686)
-                double reg_angle = (double)g.P[sa].deg * kD2R;
+                double reg_angle = (double)deg_at(g, sx, y) * kD2R;
                 float sumdx = (float)plvi_cos(reg_angle);
                 float sumdy = (float)plvi_sin(reg_angle);
-                __syncthreads();
                 if (lane == 0) {
                     used_set(g.used, sa);
-                    q_put(g, 0, (unsigned)sx | ((unsigned)y << 16));
+                    g.qlds[0] = (unsigned)sx | ((unsigned)y << 16);
                 }
                 __syncthreads();
+                if (do_stats) st_acc[4]++;
                 int reg_size = 1;
-                for (int i = 0; i < reg_size; ++i) {
-                    const unsigned pv = q_get(g, i);
+                for (int i = 0; i < reg_size;) {
+                    unsigned long long t0 = do_stats ? __builtin_amdgcn_s_memtime() : 0;
+                    const int nb = min(7, reg_size - i);
+                    const bool active = lane < 9 * nb;
+                    const unsigned pv = active ? q_get(g, i + bp) : 0u;
                     const int px = (int)(pv & 0xffffu), py = (int)(pv >> 16);
-                    const int xx_min = max(px - 1, 0), xx_max = min(px + 1, sw - 1);
-                    const int yy_min = max(py - 1, 0), yy_max = min(py + 1, sh - 1);
-                    // lanes 0..8 fetch the 3x3 neighbourhood's static data in parallel
-                    LsdPix nb;
-                    nb.deg = kNotdefF; nb.c = 0.f; nb.s = 0.f;
-                    if (lane < 9) {
-                        const int nx = px - 1 + lane % 3, ny = py - 1 + lane / 3;
-                        if (nx >= xx_min && nx <= xx_max && ny >= yy_min && ny <= yy_max) nb = g.P[ny * sw + nx];
+                    const int nx = px + kdx, ny = py + kdy;
+                    const bool valid = active && nx >= 0 && nx < sw && ny >= 0 && ny < sh;
+                    const int na = ny * sw + nx;
+                    const float deg = valid ? deg_at(g, nx, ny) : kNotdefF;
+                    // lanes of earlier block points that test the same pixel
+                    unsigned long long dup = 0;
+                    for (int p2 = 0; p2 < nb - 1; ++p2) {
+                        const unsigned q2 = (unsigned)readlane_i((int)pv, 9 * p2);
+                        const int ddx = nx - (int)(q2 & 0xffffu) + 1, ddy = ny - (int)(q2 >> 16) + 1;
+                        if (p2 < bp && ddx >= 0 && ddx <= 2 && ddy >= 0 && ddy <= 2)
+                            dup |= 1ull << (9 * p2 + ddy * 3 + ddx);
                     }
-                    for (int k = 0; k < 9; ++k) {
-                        const int nx = px - 1 + k % 3, ny = py - 1 + k / 3;
-                        if (nx < xx_min || nx > xx_max || ny < yy_min || ny > yy_max) continue;
-                        const int ca = ny * sw + nx;
-                        if (used_get(g.used, ca)) continue;
-                        const float deg = __shfl(nb.deg, k);
-                        if (!is_aligned_deg(deg, reg_angle, prec)) continue;
-                        const float cc = __shfl(nb.c, k), ss = __shfl(nb.s, k);
-                        __syncthreads();
-                        if (lane == 0) {
-                            used_set(g.used, ca);
-                            q_put(g, reg_size, (unsigned)nx | ((unsigned)ny << 16));
+                    const float af = (float)((double)deg * kD2R);
+                    const float cc = plvi_cosf(af), ss = plvi_sinf(af);
+                    unsigned long long t1 = 0;
+                    if (do_stats) { t1 = __builtin_amdgcn_s_memtime(); st_acc[1] += t1 - t0; st_acc[5]++; }
+                    int start = 0;
+                    while (start < 9 * nb) {
+                        if (do_stats) st_acc[6]++;
+                        const unsigned long long fromStart = ~0ull << start;
+                        const bool candl = lane >= start && valid && deg != kNotdefF && !used_get(g.used, na);
+                        const bool al = candl && is_aligned_deg(deg, reg_angle, prec);
+                        const bool acc = al && (dup & fromStart) == 0ull;
+                        const unsigned long long A = __ballot(acc);
+                        if (!A) break;  // no commit: every remaining decision is final
+                        // exact angle sequence of the speculated commits (sequential float sums)
+                        float sx2 = sumdx, sy2 = sumdy, pfx = 0.f, pfy = 0.f;
+                        int t = 0;
+                        for (unsigned long long mm = A; mm; mm &= mm - 1, ++t) {
+                            const int bl = __ffsll((long long)mm) - 1;
+                            sx2 += readlane_f(cc, bl);
+                            sy2 += readlane_f(ss, bl);
+                            if (lane == t) { pfx = sx2; pfy = sy2; }
+                        }
+                        const int mcount = t;
+                        const double th = lane < mcount ? (double)plvi_fast_atan2(pfy, pfx) * kD2R : 0.0;
+                        // verify every decision against the angle it really sees
+                        const int cl = __popcll(A & below);
+                        const double thl = shfl_d(th, cl > 0 ? cl - 1 : 0);
+                        const double theta_l = cl > 0 ? thl : reg_angle;
+                        const bool al2 = candl && (dup & A) == 0ull && is_aligned_deg(deg, theta_l, prec);
+                        const unsigned long long mism = __ballot(al2 != acc) & fromStart;
+                        unsigned long long C;
+                        int nc;
+                        if (!mism) {
+                            C = A;
+                            nc = mcount;
+                            start = 9 * nb;
+                        } else {
+                            const int ls = __ffsll((long long)mism) - 1;
+                            C = A & ((1ull << ls) - 1ull);
+                            nc = __popcll(C);
+                            start = ls;  // re-decided exactly next round
+                        }
+                        if (nc > 0) {
+                            if ((C >> lane) & 1ull) {
+                                used_set(g.used, na);
+                                q_put(g, reg_size + __popcll(C & below), (unsigned)nx | ((unsigned)ny << 16));
+                            }
+                            reg_size += nc;
+                            sumdx = readlane_f(pfx, nc - 1);
+                            sumdy = readlane_f(pfy, nc - 1);
+                            reg_angle = readlane_d(th, nc - 1);
+                            if (do_stats) st_acc[8] += nc;
                         }
                         __syncthreads();
-                        ++reg_size;
-                        sumdx += cc;
-                        sumdy += ss;
-                        reg_angle = (double)plvi_fast_atan2(sumdy, sumdx) * kD2R;
                     }
+                    if (do_stats) st_acc[2] += __builtin_amdgcn_s_memtime() - t1;
+                    i += nb;
                 }
                 if (reg_size < min_reg) continue;
-                // ---- region2rect (lsd.cpp:688-744): sequential double sums in region order
-                double xs = 0, ys = 0, sum = 0;
-                for (int base = 0; base < reg_size; base += 64) {
-                    const int j = base + lane;
-                    unsigned pv = 0;
-                    double wgt = 0;
-                    if (j < reg_size) {
-                        pv = q_get(g, j);
-                        wgt = g.M[(int)(pv >> 16) * sw + (int)(pv & 0xffffu)];
+                unsigned long long tr0 = do_stats ? __builtin_amdgcn_s_memtime() : 0;
+                if (do_stats) st_acc[7] += reg_size;
+                // ---- region2rect (lsd.cpp:688-744) + get_theta (:746-782):
+                // sequential double sums in region order by lane 0, the other
+                // lanes stage coordinates and weights
+                double xs = 0, ys = 0, sum = 0, Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
+                for (int pass = 0; pass < 2; ++pass) {
+                    for (int base = 0; base < reg_size; base += 64) {
+                        const int j = base + lane;
+                        unsigned pvj = 0;
+                        double wgt = 0;
+                        if (j < reg_size) {
+                            pvj = q_get(g, j);
+                            wgt = g.M[(int)(pvj >> 16) * sw + (int)(pvj & 0xffffu)];
+                        }
+                        const int n = min(64, reg_size - base);
+                        if (pass == 0) {
+#pragma unroll 4
+                            for (int t2 = 0; t2 < n; ++t2) {
+                                const unsigned q = (unsigned)readlane_i((int)pvj, t2);
+                                const double w = readlane_d(wgt, t2);
+                                xs += (double)(int)(q & 0xffffu) * w;
+                                ys += (double)(int)(q >> 16) * w;
+                                sum += w;
+                            }
+                        } else {
+#pragma unroll 4
+                            for (int t2 = 0; t2 < n; ++t2) {
+                                const unsigned q = (unsigned)readlane_i((int)pvj, t2);
+                                const double w = readlane_d(wgt, t2);
+                                const double dx = (double)(int)(q & 0xffffu) - xs;
+                                const double dy = (double)(int)(q >> 16) - ys;
+                                Ixx += dy * dy * w;
+                                Iyy += dx * dx * w;
+                                Ixy -= dx * dy * w;
+                            }
+                        }
                     }
-                    const int n = min(64, reg_size - base);
-                    for (int t = 0; t < n; ++t) {
-                        const unsigned q = __shfl(pv, t);
-                        const double w = __shfl(wgt, t);
-                        xs += (double)(int)(q & 0xffffu) * w;
-                        ys += (double)(int)(q >> 16) * w;
-                        sum += w;
-                    }
-                }
-                xs /= sum;
-                ys /= sum;
-                // get_theta
-                double Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
-                for (int base = 0; base < reg_size; base += 64) {
-                    const int j = base + lane;
-                    unsigned pv = 0;
-                    double wgt = 0;
-                    if (j < reg_size) {
-                        pv = q_get(g, j);
-                        wgt = g.M[(int)(pv >> 16) * sw + (int)(pv & 0xffffu)];
-                    }
-                    const int n = min(64, reg_size - base);
-                    for (int t = 0; t < n; ++t) {
-                        const unsigned q = __shfl(pv, t);
-                        const double w = __shfl(wgt, t);
-                        const double dx = (double)(int)(q & 0xffffu) - xs;
-                        const double dy = (double)(int)(q >> 16) - ys;
-                        Ixx += dy * dy * w;
-                        Iyy += dx * dx * w;
-                        Ixy -= dx * dy * w;
+                    if (pass == 0) {
+                        xs /= sum;
+                        ys /= sum;
                     }
                 }
                 const double lambda = 0.5 * (Ixx + Iyy - __builtin_sqrt((Ixx - Iyy) * (Ixx - Iyy) + 4.0 * Ixy * Ixy));
@@ -321,7 +442,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                 theta *= kD2R;
                 if (angle_diff(theta, reg_angle) > prec) theta += kPi;
                 const double dxv = plvi_cos(theta), dyv = plvi_sin(theta);
-                // l/w extents: the reference's if/else-if max/min is equivalent to
+                // l extents: the reference's if/else-if max/min is equivalent to
                 // independent max(0, .)/min(0, .) (l_min <= 0 <= l_max throughout).
                 double lmax = 0, lmin = 0;
                 for (int j = lane; j < reg_size; j += 64) {
@@ -333,9 +454,9 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                     lmin = l < lmin ? l : lmin;
                 }
                 for (int s = 32; s > 0; s >>= 1) {
-                    const double a = __shfl_xor(lmax, s), b = __shfl_xor(lmin, s);
+                    const double a = __shfl_xor(lmax, s), b2 = __shfl_xor(lmin, s);
                     lmax = a > lmax ? a : lmax;
-                    lmin = b < lmin ? b : lmin;
+                    lmin = b2 < lmin ? b2 : lmin;
                 }
                 double x1 = xs + lmin * dxv, y1 = ys + lmin * dyv;
                 double x2 = xs + lmax * dxv, y2 = ys + lmax * dyv;
@@ -349,12 +470,22 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                 } else {
                     overflow = true;
                 }
+                if (do_stats) st_acc[3] += __builtin_amdgcn_s_memtime() - tr0;
             }
         }
     }
     if (lane == 0) {
         nlines[f * nOct + o] = nout;
         if (overflow) atomicOr(err, 4);
+    }
+    if (do_stats) {
+        st_acc[0] = __builtin_amdgcn_s_memtime() - t_begin;
+        if (lane < 9) {
+            unsigned long long v = st_acc[0];
+            for (int q = 1; q < 9; ++q)
+                if (lane == q) v = st_acc[q];
+            stats[(size_t)(f * nOct + o) * 16 + lane] = v;
+        }
     }
 }
 

@@ -179,7 +179,7 @@ struct LinePipeline {
             PLVI_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_gaussG), gG, sizeof(gG)));
             PLVI_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_comb), comb, sizeof(comb)));
         }
-        if (octImg.alloc(std::max<size_t>(imgOff, 16)) || pix.alloc(sizeof(LsdPix) * sOff) ||
+        if (octImg.alloc(std::max<size_t>(imgOff, 16)) || pix.alloc(sizeof(float) * sOff) ||
             modg.alloc(sizeof(double) * sOff) || qspill.alloc(sizeof(unsigned) * qspillFrame * nOct * Bcap) ||
             rawLines.alloc(sizeof(LsdLine) * (size_t)kLsdRawCap * nOct * Bcap) ||
             nlines.alloc(sizeof(int) * nOct * Bcap) || klTmp.alloc(sizeof(plvi_keyline) * (size_t)kKlCap * Bcap) ||
@@ -189,15 +189,24 @@ struct LinePipeline {
             lbdDy.alloc(sizeof(int16_t) * lbdPlaneTotal) || err.alloc(sizeof(int)) || staging.alloc((size_t)W * H))
             return PLVI_E_HIP;
         PLVI_CHECK(hipMemset(err.p, 0, sizeof(int)));
-        size_t maxWords = 0;
-        for (auto& d : oct) maxWords = std::max(maxWords, (size_t)((d.splane + 31) / 32));
-        growSmem = (maxWords + kLsdQueueLds) * sizeof(unsigned);
-        if (growSmem > 160 * 1024) return PLVI_E_BADARG;
+        size_t maxWords = 0, maxSw = 0;
+        for (auto& d : oct) {
+            maxWords = std::max(maxWords, (size_t)((d.splane + 31) / 32));
+            maxSw = std::max(maxSw, (size_t)d.sw);
+        }
+        growWords = (int)maxWords;
+        const size_t budget = 160 * 1024 - 512;
+        const size_t fixed = (maxWords + kLsdQueueLds) * sizeof(unsigned);
+        if (fixed + 4 * 4 * maxSw > budget) return PLVI_E_BADARG;
+        growWinFloats = (int)((budget - fixed) / 4);
+        growSmem = fixed + (size_t)growWinFloats * 4;
         PLVI_CHECK(hipFuncSetAttribute((const void*)lsd_grow_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)growSmem));
         return PLVI_OK;
     }
     size_t growSmem = 0;
+    int growWords = 0, growWinFloats = 0;
+    unsigned long long* growStats = nullptr;  // diagnostic cycle counters (plvi_lines_debug_stats)
 
     int profile(int on) {
         if (on && evs.empty()) {
@@ -252,14 +261,15 @@ struct LinePipeline {
             hipLaunchKernelGGL(lsd_prep_kernel, grid, dim3(256), 0, st, s, sf, sr, d.w, d.h, d.sw, d.sh,
                                (const int*)(T + d.tabXofs), (const float*)(T + d.tabXa), d.xmax,
                                (const int*)(T + d.tabYrow), (const float*)(T + d.tabYb), gk[0], gk[1], gk[2], gk[3],
-                               rho, pix.as<LsdPix>() + d.soff, modg.as<double>() + d.soff, (size_t)d.splane,
+                               rho, pix.as<float>() + d.soff, modg.as<double>() + d.soff, (size_t)d.splane,
                                err.as<int>());
         }
         mark(2, st);
         // LK3: region growing (one wave per octave x frame)
         hipLaunchKernelGGL(lsd_grow_kernel, dim3(nOct, nf), dim3(64), growSmem, st, d_oct.as<LineOctDev>(),
-                           (const LsdPix*)pix.as<LsdPix>(), (const double*)modg.as<double>(), qspill.as<unsigned>(),
-                           qspillFrame, prec, SCALE, rawLines.as<LsdLine>(), nlines.as<int>(), err.as<int>());
+                           (const float*)pix.as<float>(), (const double*)modg.as<double>(), qspill.as<unsigned>(),
+                           qspillFrame, prec, SCALE, rawLines.as<LsdLine>(), nlines.as<int>(), err.as<int>(),
+                           growWinFloats, growWords, growStats);
         mark(3, st);
         // LK4: keyline assembly + top-k + line equations
         hipLaunchKernelGGL(line_assemble_kernel, dim3(nf), dim3(256), 0, st, d_oct.as<LineOctDev>(), nOct,
@@ -411,4 +421,12 @@ extern "C" int plvi_lines_profile_read(plvi_line_extractor* h, float* stage_ms, 
     if (!h || !stage_ms) return PLVI_E_BADARG;
     PLVI_CHECK(hipSetDevice(h->p.device));
     return h->p.profile_read(stage_ms, runs);
+}
+
+// Diagnostic: enable per-task cycle accounting of the region-growing kernel
+// into a caller-provided device buffer of n_frames*nlevels*16 uint64 (NULL disables).
+extern "C" int plvi_lines_debug_stats(plvi_line_extractor* h, unsigned long long* d_stats) {
+    if (!h) return PLVI_E_BADARG;
+    h->p.growStats = d_stats;
+    return PLVI_OK;
 }

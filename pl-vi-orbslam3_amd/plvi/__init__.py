@@ -89,6 +89,7 @@ def _declare(lib):
         "plvi_lines_scale_tables": ([V, V, V, V, V], I),
         "plvi_lines_profile": ([V, I], I),
         "plvi_lines_profile_read": ([V, V, P], I),
+        "plvi_lines_debug_stats": ([V, V], I),
         "plvi_device_malloc": ([c_void_pp, S], I),
         "plvi_device_free": ([V], I),
         "plvi_memcpy": ([V, V, S, I], I),
