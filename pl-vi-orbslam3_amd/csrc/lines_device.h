@@ -8,7 +8,7 @@ namespace plvi {
 
 constexpr int kLineMaxOct = 2;      // Lineextractor nlevels (config: 2)
 constexpr int kLsdRawCap = 8192;    // LSD segments per (frame, octave)
-constexpr int kLsdQueueLds = 4096;  // region points kept in LDS (rest spill to global)
+
 
 struct LineOctDev {
     int w, h;             // octave image (LSD input) dims

@@ -43,7 +43,8 @@ __global__ __launch_bounds__(256) void lsd_half_kernel(const uint8_t* __restrict
 //   (RowFilter sequential sum, SymmColumnFilter; lsd.cpp:455),
 //   resize x SCALE f64 INTER_LINEAR with float coefficients (lsd.cpp:457),
 //   ll_angle gradient / norm / fastAtan2 angle (lsd.cpp:561-584).
-// Outputs per scaled pixel: angle in degrees (float, NOTDEF = -1024) and modgrad (f64).
+// Outputs per scaled pixel: angle in degrees (float, NOTDEF = -1024), modgrad
+// (f64) and, for defined pixels, the seed direction (float cos, float sin).
 // ---------------------------------------------------------------------------
 constexpr int kPTX = 32, kPTY = 16;         // scaled tile
 constexpr int kPGW = 48, kPGH = 28;         // max blurred (G) region
@@ -55,7 +56,8 @@ __global__ __launch_bounds__(256) void lsd_prep_kernel(const uint8_t* __restrict
                                                        const int* __restrict__ yrow, const float* __restrict__ yb,
                                                        double k0, double k1, double k2, double k3, double rho,
                                                        float* __restrict__ pix, double* __restrict__ modgrad,
-                                                       size_t p_frame, int* __restrict__ err) {
+                                                       float2* __restrict__ seedcs, size_t p_frame,
+                                                       int* __restrict__ err) {
     __shared__ uint8_t I[kPIH][kPIW];
     __shared__ double Hs[kPIH][kPGW];
     __shared__ double Gs[kPGH][kPGW];
@@ -131,6 +133,11 @@ __global__ __launch_bounds__(256) void lsd_prep_kernel(const uint8_t* __restrict
         }
         P[(size_t)y * sw + x] = deg;
         M[(size_t)y * sw + x] = norm;
+        if (deg != kNotdefF) {
+            // region_grow's seed direction float(cos/sin(reg_angle)) (lsd.cpp:648-649)
+            const double a = (double)deg * kD2R;
+            seedcs[(size_t)f * p_frame + (size_t)y * sw + x] = make_float2((float)plvi_cos(a), (float)plvi_sin(a));
+        }
     }
 }
 
@@ -141,12 +148,14 @@ __global__ __launch_bounds__(256) void lsd_prep_kernel(const uint8_t* __restrict
 // pixel, the min_reg_size test, region2rect (:688-744) + get_theta
 // (:746-782) in double with the reference summation order, +0.5, /SCALE.
 //
-// One wave per (octave, frame).  LDS holds the USED bitmap of the octave,
-// the region queue (global spill beyond kLsdQueueLds) and a sliding window
-// of R (power of two) rows of gradient angles starting at or above the row
-// before the current seed.  Seeds are visited in raster order, so every
+// One wave per (octave, frame).  Seeds are visited in raster order, so every
 // defined pixel before the seed is already USED and a region only reaches
-// rows >= seed row; rows beyond the window are read from global memory.
+// rows >= seed row.  LDS therefore holds only a sliding window of R (power of
+// two) rows at or below the seed row: their gradient angles and USED bits.
+// Rows beyond the window are read from the angle plane and a global USED
+// bitmap (L2, bypassing L1), which the window picks up when it slides.  The
+// region queue lives in LDS up to QL entries and spills to global memory.
+// The footprint (~37 KB at R = 16) lets four waves share a CU.
 //
 // Speculative exact growth: the neighbour checks of up to 7 queued points
 // (63 lanes, the reference's scan order = lane order) are decided at once
@@ -158,23 +167,43 @@ __global__ __launch_bounds__(256) void lsd_prep_kernel(const uint8_t* __restrict
 // identical to the sequential algorithm.
 // ---------------------------------------------------------------------------
 struct GrowCtx {
-    const float* P;
-    const double* M;
-    unsigned* used;   // LDS bitmap
-    unsigned* qlds;   // LDS queue (x | y<<16)
-    unsigned* qglob;  // global spill
-    float* win;       // LDS angle window: R rows, ring indexed by row & (R-1)
-    int sw, sh, R, wb;
+    const float* P;   // angle plane (degrees, NOTDEF = -1024)
+    unsigned* gbits;  // global USED bitmap (rows at or beyond the window)
+    unsigned* bits;   // LDS USED ring: R rows x wpr words
+    unsigned* qlds;   // LDS region queue (x | y << 16), QL entries
+    unsigned* qglob;  // global queue spill
+    float* win;       // LDS angle ring: R rows x sw
+    int sw, sh, R, wpr, wb, QL, ys;  // ys = row of the current seed
 };
 
-__device__ __forceinline__ bool used_get(const unsigned* u, int a) { return (u[a >> 5] >> (a & 31)) & 1u; }
-__device__ __forceinline__ void used_set(unsigned* u, int a) { atomicOr(&u[a >> 5], 1u << (a & 31)); }
-__device__ __forceinline__ unsigned q_get(const GrowCtx& g, int i) {
-    return i < kLsdQueueLds ? g.qlds[i] : g.qglob[i - kLsdQueueLds];
+__device__ __forceinline__ unsigned gload_l2(unsigned* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void q_put(GrowCtx& g, int i, unsigned v) {
-    if (i < kLsdQueueLds) g.qlds[i] = v;
-    else g.qglob[i - kLsdQueueLds] = v;
+__device__ __forceinline__ void gstore_l2(unsigned* p, unsigned v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0); }
+
+// USED test.  Rows above the seed row hold only USED or NOTDEF pixels
+// (seeds are visited in raster order), so they read as USED.
+__device__ __forceinline__ bool used_get(const GrowCtx& g, int x, int y) {
+    if (y < g.ys) return true;
+    unsigned v;
+    if (y < g.wb + g.R) v = g.bits[(y & (g.R - 1)) * g.wpr + (x >> 5)];
+    else v = gload_l2(g.gbits + (size_t)y * g.wpr + (x >> 5));
+    return (v >> (x & 31)) & 1u;
+}
+__device__ __forceinline__ void used_set(const GrowCtx& g, int x, int y) {
+    const unsigned b = 1u << (x & 31);
+    if (y < g.wb + g.R) atomicOr(&g.bits[(y & (g.R - 1)) * g.wpr + (x >> 5)], b);
+    else __hip_atomic_fetch_or(g.gbits + (size_t)y * g.wpr + (x >> 5), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned q_get(const GrowCtx& g, int i) {
+    return i < g.QL ? g.qlds[i] : gload_l2(g.qglob + (i - g.QL));
+}
+__device__ __forceinline__ void q_put(const GrowCtx& g, int i, unsigned v) {
+    if (i < g.QL) g.qlds[i] = v;
+    else gstore_l2(g.qglob + (i - g.QL), v);
 }
 __device__ __forceinline__ float deg_at(const GrowCtx& g, int x, int y) {
     if (y < g.wb + g.R) return g.win[(y & (g.R - 1)) * g.sw + x];
@@ -219,8 +248,10 @@ __device__ __forceinline__ double shfl_d(double v, int src) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-// Load image rows [r0, r1) of angles into their window slots.
-__device__ __forceinline__ void win_load_rows(GrowCtx& g, int r0, int r1, int lane) {
+// Load image rows [r0, r1) into their window slots: angles from the angle
+// plane, USED bits from the global bitmap (set while the rows were beyond
+// the window).
+__device__ __forceinline__ void win_load_rows(const GrowCtx& g, int r0, int r1, int lane) {
     const int n = (r1 - r0) * g.sw;
     const float* src = g.P + (size_t)r0 * g.sw;
     int i = lane;
@@ -230,7 +261,7 @@ __device__ __forceinline__ void win_load_rows(GrowCtx& g, int r0, int r1, int la
         for (int u = 0; u < 8; ++u) v[u] = src[i + u * 64];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int j = i + u * 64, row = r0 + j / g.sw, x = j % g.sw;
+            const int j = i + u * 64, row = r0 + j / g.sw, x = j - (j / g.sw) * g.sw;
             g.win[(row & (g.R - 1)) * g.sw + x] = v[u];
         }
     }
@@ -238,92 +269,103 @@ __device__ __forceinline__ void win_load_rows(GrowCtx& g, int r0, int r1, int la
         const int row = r0 + i / g.sw, x = i % g.sw;
         g.win[(row & (g.R - 1)) * g.sw + x] = src[i];
     }
+    const int nw = (r1 - r0) * g.wpr;
+    for (int k = lane; k < nw; k += 64) {
+        const int row = r0 + k / g.wpr, w = k % g.wpr;
+        g.bits[(row & (g.R - 1)) * g.wpr + w] = gload_l2(g.gbits + (size_t)row * g.wpr + w);
+    }
 }
 
 __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restrict__ octs,
                                                       const float* __restrict__ pix,
                                                       const double* __restrict__ modgrad,
+                                                      const float2* __restrict__ seedcs,
+                                                      unsigned* __restrict__ gbits_all, size_t gbits_frame,
                                                       unsigned* __restrict__ qspill, size_t qspill_frame,
                                                       double prec, double scale_lsd, LsdLine* __restrict__ lines,
-                                                      int* __restrict__ nlines, int* __restrict__ err, int winFloats,
-                                                      int wordsMax, unsigned long long* __restrict__ stats) {
+                                                      int* __restrict__ nlines, int* __restrict__ err, int R, int QL,
+                                                      unsigned long long* __restrict__ stats) {
     extern __shared__ __align__(16) unsigned lds_u[];
     const int o = blockIdx.x, f = blockIdx.y, nOct = gridDim.x;
     const LineOctDev& od = octs[o];
     const int sw = od.sw, sh = od.sh;
     const int lane = threadIdx.x;
-    const int nwords = (sw * sh + 31) >> 5;
-    // rect staging (region coordinates + weights) shares the queue's LDS words
     GrowCtx g;
+    g.sw = sw; g.sh = sh; g.R = R; g.QL = QL;
+    g.wpr = (sw + 31) >> 5;
     g.P = pix + od.soff + (size_t)f * od.splane;
-    g.M = modgrad + od.soff + (size_t)f * od.splane;
-    g.used = lds_u;
-    g.qlds = lds_u + wordsMax;
-    g.win = reinterpret_cast<float*>(lds_u + wordsMax + kLsdQueueLds);
+    const double* M = modgrad + od.soff + (size_t)f * od.splane;
+    const float2* SC = seedcs + od.soff + (size_t)f * od.splane;
+    g.gbits = gbits_all + (size_t)(f * nOct + o) * gbits_frame;
     g.qglob = qspill + (size_t)(f * nOct + o) * qspill_frame;
-    g.sw = sw; g.sh = sh;
-    {
-        int r = 1;
-        while (r * 2 * sw <= winFloats && r * 2 <= 1024) r *= 2;  // power-of-two ring (host guarantees >= 4)
-        g.R = r;
-    }
+    // LDS: rect staging (64 x 3 doubles) | USED ring | queue | angle ring
+    double* rs = reinterpret_cast<double*>(lds_u);
+    g.bits = lds_u + 64 * 3 * 2;
+    g.qlds = g.bits + R * g.wpr;
+    g.win = reinterpret_cast<float*>(g.qlds + QL);
     g.wb = 0;
-    for (int i = lane; i < nwords; i += 64) g.used[i] = 0u;
-    win_load_rows(g, 0, min(g.R, sh), lane);
+    g.ys = 0;
+    for (int i = lane; i < sh * g.wpr; i += 64) g.gbits[i] = 0u;
+    vm_drain();
+    win_load_rows(g, 0, min(R, sh), lane);
+    vm_drain();
     __syncthreads();
     LsdLine* out = lines + (size_t)(f * nOct + o) * kLsdRawCap;
     int nout = 0;
     bool overflow = false;
     const int min_reg = od.min_reg_size;
-    const int bp = lane / 9, bk = lane % 9;          // block point / neighbour index of this lane
+    const int bp = lane / 9, bk = lane % 9;  // block point / neighbour index of this lane
     const int kdx = bk % 3 - 1, kdy = bk / 3 - 1;
     const unsigned long long below = (1ull << lane) - 1ull;
     // optional cycle accounting (diagnostic): [0] total [1] block setup [2] rounds [3] rect
     // [4] seeds [5] blocks [6] rounds [7] rect points [8] commits
-    unsigned long long st_acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long s_setup = 0, s_round = 0, s_rect = 0, n_seed = 0, n_block = 0, n_round = 0, n_rpt = 0,
+                       n_commit = 0;
     const bool do_stats = stats != nullptr;
     const unsigned long long t_begin = do_stats ? __builtin_amdgcn_s_memtime() : 0;
+    const int half = R / 2;
     for (int y = 0; y < sh - 1; ++y) {
-        // slide the window (half a window at a time) so it holds row y-1 and at
-        // least R/2 rows below it
-        const int half = g.R / 2;
-        if (y - 1 >= g.wb + half && g.wb + g.R < sh) {
-            const int r0 = g.wb + g.R, r1 = min(sh, r0 + half);
+        // slide the window by half its height once row y is past its middle;
+        // the rows leaving it are above y and never read again
+        while (y >= g.wb + half && g.wb + R < sh) {
+            const int r0 = g.wb + R, r1 = min(sh, r0 + half);
             win_load_rows(g, r0, r1, lane);
             g.wb += r1 - r0;
+            vm_drain();
             __syncthreads();
         }
+        g.ys = y;
         for (int xb = 0; xb < sw - 1; xb += 64) {
             const int x = xb + lane;
             bool cand = false;
-            if (x < sw - 1) cand = !used_get(g.used, y * sw + x) && deg_at(g, x, y) != kNotdefF;
+            if (x < sw - 1) cand = !used_get(g, x, y) && deg_at(g, x, y) != kNotdefF;
             unsigned long long m = __ballot(cand);
+            if (!m) continue;
+            const float2 scl = cand ? SC[(size_t)y * sw + x] : make_float2(0.f, 0.f);
             while (m) {
                 const int b = __ffsll((long long)m) - 1;
                 m &= m - 1;
                 const int sx = xb + b;
-                const int sa = y * sw + sx;
-                if (used_get(g.used, sa)) continue;  // absorbed by an earlier region of this chunk
+                if (used_get(g, sx, y)) continue;  // absorbed by an earlier region of this chunk
                 // ---- region_grow (lsd.cpp:635-686)
                 double reg_angle = (double)deg_at(g, sx, y) * kD2R;
-                float sumdx = (float)plvi_cos(reg_angle);
-                float sumdy = (float)plvi_sin(reg_angle);
+                float sumdx = readlane_f(scl.x, b);
+                float sumdy = readlane_f(scl.y, b);
                 if (lane == 0) {
-                    used_set(g.used, sa);
+                    used_set(g, sx, y);
                     g.qlds[0] = (unsigned)sx | ((unsigned)y << 16);
                 }
                 __syncthreads();
-                if (do_stats) st_acc[4]++;
+                if (do_stats) n_seed++;
                 int reg_size = 1;
                 for (int i = 0; i < reg_size;) {
-                    unsigned long long t0 = do_stats ? __builtin_amdgcn_s_memtime() : 0;
+                    const unsigned long long t0 = do_stats ? __builtin_amdgcn_s_memtime() : 0;
                     const int nb = min(7, reg_size - i);
                     const bool active = lane < 9 * nb;
                     const unsigned pv = active ? q_get(g, i + bp) : 0u;
                     const int px = (int)(pv & 0xffffu), py = (int)(pv >> 16);
                     const int nx = px + kdx, ny = py + kdy;
-                    const bool valid = active && nx >= 0 && nx < sw && ny >= 0 && ny < sh;
-                    const int na = ny * sw + nx;
+                    const bool valid = active && nx >= 0 && nx < sw && ny >= y && ny < sh;
                     const float deg = valid ? deg_at(g, nx, ny) : kNotdefF;
                     // lanes of earlier block points that test the same pixel
                     unsigned long long dup = 0;
@@ -333,15 +375,16 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                         if (p2 < bp && ddx >= 0 && ddx <= 2 && ddy >= 0 && ddy <= 2)
                             dup |= 1ull << (9 * p2 + ddy * 3 + ddx);
                     }
-                    const float af = (float)((double)deg * kD2R);
-                    const float cc = plvi_cosf(af), ss = plvi_sinf(af);
+                    // cos/sin(float(angle)) of lsd.cpp:678-679
+                    float cc, ss;
+                    plvi_sincosf_pos(deg == kNotdefF ? 0.f : (float)((double)deg * kD2R), &ss, &cc);
                     unsigned long long t1 = 0;
-                    if (do_stats) { t1 = __builtin_amdgcn_s_memtime(); st_acc[1] += t1 - t0; st_acc[5]++; }
+                    if (do_stats) { t1 = __builtin_amdgcn_s_memtime(); s_setup += t1 - t0; n_block++; }
                     int start = 0;
                     while (start < 9 * nb) {
-                        if (do_stats) st_acc[6]++;
+                        if (do_stats) n_round++;
                         const unsigned long long fromStart = ~0ull << start;
-                        const bool candl = lane >= start && valid && deg != kNotdefF && !used_get(g.used, na);
+                        const bool candl = lane >= start && deg != kNotdefF && !used_get(g, nx, ny);
                         const bool al = candl && is_aligned_deg(deg, reg_angle, prec);
                         const bool acc = al && (dup & fromStart) == 0ull;
                         const unsigned long long A = __ballot(acc);
@@ -359,8 +402,16 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                         const double th = lane < mcount ? (double)plvi_fast_atan2(pfy, pfx) * kD2R : 0.0;
                         // verify every decision against the angle it really sees
                         const int cl = __popcll(A & below);
-                        const double thl = shfl_d(th, cl > 0 ? cl - 1 : 0);
-                        const double theta_l = cl > 0 ? thl : reg_angle;
+                        double theta_l = reg_angle;
+                        if (mcount <= 6) {
+                            for (int k = 0; k < mcount; ++k) {
+                                const double v = readlane_d(th, k);
+                                if (cl == k + 1) theta_l = v;
+                            }
+                        } else {
+                            const double v = shfl_d(th, cl > 0 ? cl - 1 : 0);
+                            if (cl > 0) theta_l = v;
+                        }
                         const bool al2 = candl && (dup & A) == 0ull && is_aligned_deg(deg, theta_l, prec);
                         const unsigned long long mism = __ballot(al2 != acc) & fromStart;
                         unsigned long long C;
@@ -376,65 +427,76 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                             start = ls;  // re-decided exactly next round
                         }
                         if (nc > 0) {
-                            if ((C >> lane) & 1ull) {
-                                used_set(g.used, na);
+                            const bool mine = (C >> lane) & 1ull;
+                            if (mine) {
+                                used_set(g, nx, ny);
                                 q_put(g, reg_size + __popcll(C & below), (unsigned)nx | ((unsigned)ny << 16));
                             }
+                            // global USED bits / queue spill must land before they are read back
+                            if (__ballot(mine && ny >= g.wb + R) || reg_size + nc > QL) vm_drain();
                             reg_size += nc;
                             sumdx = readlane_f(pfx, nc - 1);
                             sumdy = readlane_f(pfy, nc - 1);
                             reg_angle = readlane_d(th, nc - 1);
-                            if (do_stats) st_acc[8] += nc;
+                            if (do_stats) n_commit += nc;
                         }
                         __syncthreads();
                     }
-                    if (do_stats) st_acc[2] += __builtin_amdgcn_s_memtime() - t1;
+                    if (do_stats) s_round += __builtin_amdgcn_s_memtime() - t1;
                     i += nb;
                 }
                 if (reg_size < min_reg) continue;
-                unsigned long long tr0 = do_stats ? __builtin_amdgcn_s_memtime() : 0;
-                if (do_stats) st_acc[7] += reg_size;
-                // ---- region2rect (lsd.cpp:688-744) + get_theta (:746-782):
-                // sequential double sums in region order by lane 0, the other
-                // lanes stage coordinates and weights
+                const unsigned long long tr0 = do_stats ? __builtin_amdgcn_s_memtime() : 0;
+                if (do_stats) n_rpt += reg_size;
+                // ---- region2rect (lsd.cpp:688-744) + get_theta (:746-782): the
+                // lanes form the per-point products, lane 0 adds them in region
+                // order (the reference's double summation order)
                 double xs = 0, ys = 0, sum = 0, Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
                 for (int pass = 0; pass < 2; ++pass) {
                     for (int base = 0; base < reg_size; base += 64) {
                         const int j = base + lane;
-                        unsigned pvj = 0;
-                        double wgt = 0;
                         if (j < reg_size) {
-                            pvj = q_get(g, j);
-                            wgt = g.M[(int)(pvj >> 16) * sw + (int)(pvj & 0xffffu)];
-                        }
-                        const int n = min(64, reg_size - base);
-                        if (pass == 0) {
-#pragma unroll 4
-                            for (int t2 = 0; t2 < n; ++t2) {
-                                const unsigned q = (unsigned)readlane_i((int)pvj, t2);
-                                const double w = readlane_d(wgt, t2);
-                                xs += (double)(int)(q & 0xffffu) * w;
-                                ys += (double)(int)(q >> 16) * w;
-                                sum += w;
-                            }
-                        } else {
-#pragma unroll 4
-                            for (int t2 = 0; t2 < n; ++t2) {
-                                const unsigned q = (unsigned)readlane_i((int)pvj, t2);
-                                const double w = readlane_d(wgt, t2);
-                                const double dx = (double)(int)(q & 0xffffu) - xs;
-                                const double dy = (double)(int)(q >> 16) - ys;
-                                Ixx += dy * dy * w;
-                                Iyy += dx * dx * w;
-                                Ixy -= dx * dy * w;
+                            const unsigned q = q_get(g, j);
+                            const double w = M[(int)(q >> 16) * sw + (int)(q & 0xffffu)];
+                            const double rx = (double)(int)(q & 0xffffu), ry = (double)(int)(q >> 16);
+                            if (pass == 0) {
+                                rs[lane] = rx * w;
+                                rs[64 + lane] = ry * w;
+                                rs[128 + lane] = w;
+                            } else {
+                                const double dx = rx - xs, dy = ry - ys;
+                                rs[lane] = dy * dy * w;
+                                rs[64 + lane] = dx * dx * w;
+                                rs[128 + lane] = dx * dy * w;
                             }
                         }
+                        __syncthreads();
+                        if (lane == 0) {
+                            const int n = min(64, reg_size - base);
+                            if (pass == 0) {
+                                for (int t2 = 0; t2 < n; ++t2) {
+                                    xs += rs[t2];
+                                    ys += rs[64 + t2];
+                                    sum += rs[128 + t2];
+                                }
+                            } else {
+                                for (int t2 = 0; t2 < n; ++t2) {
+                                    Ixx += rs[t2];
+                                    Iyy += rs[64 + t2];
+                                    Ixy -= rs[128 + t2];
+                                }
+                            }
+                        }
+                        __syncthreads();
                     }
                     if (pass == 0) {
-                        xs /= sum;
-                        ys /= sum;
+                        xs = readlane_d(xs, 0) / readlane_d(sum, 0);
+                        ys = readlane_d(ys, 0) / readlane_d(sum, 0);
                     }
                 }
+                Ixx = readlane_d(Ixx, 0);
+                Iyy = readlane_d(Iyy, 0);
+                Ixy = readlane_d(Ixy, 0);
                 const double lambda = 0.5 * (Ixx + Iyy - __builtin_sqrt((Ixx - Iyy) * (Ixx - Iyy) + 4.0 * Ixy * Ixy));
                 double theta = (__builtin_fabs(Ixx) > __builtin_fabs(Iyy))
                                    ? (double)plvi_fast_atan2((float)(lambda - Ixx), (float)Ixy)
@@ -470,7 +532,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                 } else {
                     overflow = true;
                 }
-                if (do_stats) st_acc[3] += __builtin_amdgcn_s_memtime() - tr0;
+                if (do_stats) s_rect += __builtin_amdgcn_s_memtime() - tr0;
             }
         }
     }
@@ -478,14 +540,11 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
         nlines[f * nOct + o] = nout;
         if (overflow) atomicOr(err, 4);
     }
-    if (do_stats) {
-        st_acc[0] = __builtin_amdgcn_s_memtime() - t_begin;
-        if (lane < 9) {
-            unsigned long long v = st_acc[0];
-            for (int q = 1; q < 9; ++q)
-                if (lane == q) v = st_acc[q];
-            stats[(size_t)(f * nOct + o) * 16 + lane] = v;
-        }
+    if (do_stats && lane == 0) {
+        unsigned long long* S = stats + (size_t)(f * nOct + o) * 16;
+        S[0] = __builtin_amdgcn_s_memtime() - t_begin;
+        S[1] = s_setup; S[2] = s_round; S[3] = s_rect; S[4] = n_seed;
+        S[5] = n_block; S[6] = n_round; S[7] = n_rpt; S[8] = n_commit;
     }
 }
 

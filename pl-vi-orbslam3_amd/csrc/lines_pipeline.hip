@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -47,9 +48,9 @@ struct LinePipeline {
     std::vector<float> scaleF, invScaleF;
     double SCALE = 0.8, prec = 0, rho = 0, min_length = 0;
     double gk[7]{};
-    DevBuf d_oct, d_tabs, octImg, pix, modg, qspill, rawLines, nlines, klTmp, klOut, fnOut, cntOut, descOut, lbdBlur,
+    DevBuf d_oct, d_tabs, octImg, pix, modg, seedcs, gbits, qspill, rawLines, nlines, klTmp, klOut, fnOut, cntOut, descOut, lbdBlur,
         lbdDx, lbdDy, err, staging;
-    size_t qspillFrame = 0, lbdPlaneTotal = 0;
+    size_t qspillFrame = 0, gbitsFrame = 0, lbdPlaneTotal = 0;
     int lastFrames = 0;
     static constexpr int kStages = 5, kRing = 512;
     bool prof = false;
@@ -162,6 +163,7 @@ struct LinePipeline {
         }
         lbdPlaneTotal = lOff;
         qspillFrame = maxSplane;
+        for (auto& d : oct) gbitsFrame = std::max(gbitsFrame, (size_t)d.sh * (size_t)((d.sw + 31) / 32));
         if (d_oct.alloc(sizeof(LineOctDev) * nOct) || d_tabs.alloc(tabs.size())) return PLVI_E_HIP;
         PLVI_CHECK(hipMemcpy(d_oct.p, oct.data(), sizeof(LineOctDev) * nOct, hipMemcpyHostToDevice));
         PLVI_CHECK(hipMemcpy(d_tabs.p, tabs.data(), tabs.size(), hipMemcpyHostToDevice));
@@ -180,7 +182,8 @@ struct LinePipeline {
             PLVI_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_comb), comb, sizeof(comb)));
         }
         if (octImg.alloc(std::max<size_t>(imgOff, 16)) || pix.alloc(sizeof(float) * sOff) ||
-            modg.alloc(sizeof(double) * sOff) || qspill.alloc(sizeof(unsigned) * qspillFrame * nOct * Bcap) ||
+            modg.alloc(sizeof(double) * sOff) || seedcs.alloc(sizeof(float2) * sOff) ||
+            gbits.alloc(sizeof(unsigned) * gbitsFrame * nOct * Bcap) || qspill.alloc(sizeof(unsigned) * qspillFrame * nOct * Bcap) ||
             rawLines.alloc(sizeof(LsdLine) * (size_t)kLsdRawCap * nOct * Bcap) ||
             nlines.alloc(sizeof(int) * nOct * Bcap) || klTmp.alloc(sizeof(plvi_keyline) * (size_t)kKlCap * Bcap) ||
             klOut.alloc(sizeof(plvi_keyline) * (size_t)fcap * Bcap) || fnOut.alloc(sizeof(double) * 3 * fcap * Bcap) ||
@@ -189,23 +192,26 @@ struct LinePipeline {
             lbdDy.alloc(sizeof(int16_t) * lbdPlaneTotal) || err.alloc(sizeof(int)) || staging.alloc((size_t)W * H))
             return PLVI_E_HIP;
         PLVI_CHECK(hipMemset(err.p, 0, sizeof(int)));
-        size_t maxWords = 0, maxSw = 0;
-        for (auto& d : oct) {
-            maxWords = std::max(maxWords, (size_t)((d.splane + 31) / 32));
-            maxSw = std::max(maxSw, (size_t)d.sw);
-        }
-        growWords = (int)maxWords;
-        const size_t budget = 160 * 1024 - 512;
-        const size_t fixed = (maxWords + kLsdQueueLds) * sizeof(unsigned);
-        if (fixed + 4 * 4 * maxSw > budget) return PLVI_E_BADARG;
-        growWinFloats = (int)((budget - fixed) / 4);
-        growSmem = fixed + (size_t)growWinFloats * 4;
+        // region-growing LDS: rect staging + R-row USED/angle window + queue,
+        // sized so that several waves share a CU (PLVI_GROW_LDS, default 40 KB)
+        size_t maxSw = 0;
+        for (auto& d : oct) maxSw = std::max(maxSw, (size_t)d.sw);
+        size_t budget = 40 * 1024;
+        if (const char* e = getenv("PLVI_GROW_LDS")) budget = (size_t)atol(e);
+        budget = std::min<size_t>(budget, 160 * 1024);
+        growQL = 1024;
+        const size_t fixed = 64 * 3 * sizeof(double) + (size_t)growQL * sizeof(unsigned);
+        const size_t perRow = maxSw * sizeof(float) + (maxSw + 31) / 32 * sizeof(unsigned);
+        growR = 4;
+        if (fixed + perRow * 4 > budget) return PLVI_E_BADARG;
+        while (growR * 2 <= 1024 && fixed + perRow * growR * 2 <= budget) growR *= 2;
+        growSmem = fixed + perRow * growR;
         PLVI_CHECK(hipFuncSetAttribute((const void*)lsd_grow_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)growSmem));
         return PLVI_OK;
     }
     size_t growSmem = 0;
-    int growWords = 0, growWinFloats = 0;
+    int growR = 0, growQL = 0;
     unsigned long long* growStats = nullptr;  // diagnostic cycle counters (plvi_lines_debug_stats)
 
     int profile(int on) {
@@ -261,15 +267,16 @@ struct LinePipeline {
             hipLaunchKernelGGL(lsd_prep_kernel, grid, dim3(256), 0, st, s, sf, sr, d.w, d.h, d.sw, d.sh,
                                (const int*)(T + d.tabXofs), (const float*)(T + d.tabXa), d.xmax,
                                (const int*)(T + d.tabYrow), (const float*)(T + d.tabYb), gk[0], gk[1], gk[2], gk[3],
-                               rho, pix.as<float>() + d.soff, modg.as<double>() + d.soff, (size_t)d.splane,
-                               err.as<int>());
+                               rho, pix.as<float>() + d.soff, modg.as<double>() + d.soff,
+                               seedcs.as<float2>() + d.soff, (size_t)d.splane, err.as<int>());
         }
         mark(2, st);
         // LK3: region growing (one wave per octave x frame)
         hipLaunchKernelGGL(lsd_grow_kernel, dim3(nOct, nf), dim3(64), growSmem, st, d_oct.as<LineOctDev>(),
-                           (const float*)pix.as<float>(), (const double*)modg.as<double>(), qspill.as<unsigned>(),
-                           qspillFrame, prec, SCALE, rawLines.as<LsdLine>(), nlines.as<int>(), err.as<int>(),
-                           growWinFloats, growWords, growStats);
+                           (const float*)pix.as<float>(), (const double*)modg.as<double>(),
+                           (const float2*)seedcs.as<float2>(), gbits.as<unsigned>(), gbitsFrame, qspill.as<unsigned>(),
+                           qspillFrame, prec, SCALE, rawLines.as<LsdLine>(), nlines.as<int>(), err.as<int>(), growR,
+                           growQL, growStats);
         mark(3, st);
         // LK4: keyline assembly + top-k + line equations
         hipLaunchKernelGGL(line_assemble_kernel, dim3(nf), dim3(256), 0, st, d_oct.as<LineOctDev>(), nOct,

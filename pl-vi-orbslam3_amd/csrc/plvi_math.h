@@ -151,6 +151,37 @@ PLVI_HD float plvi_cosf(float y) {
     return (y - y) / (y - y);
 }
 
+// sinf(y) and cosf(y) for 0 <= y < 120 without lane divergence (LSD feeds
+// float(deg * DEG_TO_RADS), deg in [0, 360)).  For y < pi/4 glibc's direct
+// branch equals the reduce_fast branch with n = 0 (x - 0*hpi == x exactly),
+// so one reduction serves both; the sine and cosine polynomials are both
+// evaluated once and selected by the quadrant parity.  Checked exhaustively
+// against plvi_sinf/plvi_cosf and glibc (tests/native/libm_check.cpp).
+PLVI_HD void plvi_sincosf_pos(float y, float* sp, float* cp) {
+    int n;
+    const double x = reduce_fast((double)y, &n);
+    const double sg = (n & 3) == 1 || (n & 3) == 2 ? -1.0 : 1.0;
+    const double neg = (n & 2) ? -1.0 : 1.0;
+    const double xs = x * sg, x2 = x * x;
+    // sine polynomial (s coefficients are not negated in table entry 1)
+    const double x3 = xs * x2;
+    const double s1 = fmad(x2, -0x1.994eb3774cf24p-13, 0x1.1107605230bc4p-7);
+    const double x7 = x3 * x2;
+    const double sv = fmad(x3, -0x1.555545995a603p-3, xs);
+    const float S = (float)fmad(x7, s1, sv);
+    // cosine polynomial (c coefficients negated in table entry 1)
+    const double x4 = x2 * x2;
+    const double c2 = fmad(x2, neg * 0x1.99343027bf8c3p-16, neg * -0x1.6c087e89a359dp-10);
+    const double c1 = fmad(x2, neg * -0x1.ffffffd0c621cp-2, neg * 0x1.0p+0);
+    const double x6 = x4 * x2;
+    const double cv = fmad(x4, neg * 0x1.55553e1068f19p-5, c1);
+    const float C = (float)fmad(x6, c2, cv);
+    float s = (n & 1) ? C : S, c = (n & 1) ? S : C;
+    if (abstop12(y) < abstop12(0x1p-12f)) { s = y; c = 1.0f; }
+    *sp = s;
+    *cp = c;
+}
+
 // ------------------------------------------------------------ fastAtan2
 PLVI_HD float plvi_fast_atan2(float y, float x) {
     const float k = (float)(180 / 3.1415926535897932384626433832795);

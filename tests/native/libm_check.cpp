@@ -87,6 +87,20 @@ int main(int argc, char** argv) {
                 }
                 bad += b; checked += c;
             });
+    } else if (!strcmp(mode, "sincospos")) {
+        // branch-free sincosf of region_grow (lsd.cpp:678-679): every float in [0, 120)
+        uint32_t hi = plvi::f2u(120.0f);
+        for (int t = 0; t < nt; ++t)
+            th.emplace_back([&, t] {
+                unsigned long long b = 0, c = 0;
+                for (uint32_t u = t; u < hi; u += nt) {
+                    float x = plvi::u2f(u), s, co;
+                    plvi::plvi_sincosf_pos(x, &s, &co);
+                    if (!same(s, sinf(x)) || !same(co, cosf(x))) { if (b < 5) fprintf(stderr, "sincospos %a\n", x); ++b; }
+                    ++c;
+                }
+                bad += b; checked += c;
+            });
     } else {
         fprintf(stderr, "unknown mode\n");
         return 2;

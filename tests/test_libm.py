@@ -38,3 +38,7 @@ def test_lsd_double_cos_sin_every_float_angle(libm_check):
 
 def test_atan2f_sampled(libm_check):
     _run(libm_check, "atan2f", "30000000")
+
+
+def test_branch_free_sincosf_every_float(libm_check):
+    _run(libm_check, "sincospos")              # plvi_sincosf_pos vs glibc sinf/cosf, every float in [0, 120)
