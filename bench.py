@@ -116,7 +116,8 @@ def main():
     lscratch = torch.empty(4 * (B - 1) * 2 * lcap, **i32)
     lm12 = torch.empty((B - 1) * lcap, **i32)
     lnm = torch.empty(B - 1, **i32)
-    sA = torch.cuda.current_stream()
+    # two non-default streams: the legacy null stream would serialise with both
+    sA = torch.cuda.Stream()
     sB = torch.cuda.Stream()
     evA, evB = torch.cuda.Event(), torch.cuda.Event()
 

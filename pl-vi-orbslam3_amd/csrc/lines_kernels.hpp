@@ -185,43 +185,48 @@ __device__ __forceinline__ void gstore_l2(unsigned* p, unsigned v) {
 __device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0); }
 
 // USED test.  Rows above the seed row hold only USED or NOTDEF pixels
-// (seeds are visited in raster order), so they read as USED.
+// (seeds are visited in raster order), so they read as USED.  The LDS read
+// is unconditional (row clamped into the window); rows beyond the window
+// (rare) take the global bitmap.
 __device__ __forceinline__ bool used_get(const GrowCtx& g, int x, int y) {
-    if (y < g.ys) return true;
-    unsigned v;
-    if (y < g.wb + g.R) v = g.bits[(y & (g.R - 1)) * g.wpr + (x >> 5)];
-    else v = gload_l2(g.gbits + (size_t)y * g.wpr + (x >> 5));
-    return (v >> (x & 31)) & 1u;
+    const bool inwin = y < g.wb + g.R;
+    const int yy = inwin ? y : g.wb;
+    unsigned v = g.bits[(yy & (g.R - 1)) * g.wpr + (x >> 5)];
+    if (__builtin_expect(!inwin, 0)) v = gload_l2(g.gbits + (size_t)y * g.wpr + (x >> 5));
+    return y < g.ys || ((v >> (x & 31)) & 1u);
 }
 __device__ __forceinline__ void used_set(const GrowCtx& g, int x, int y) {
     const unsigned b = 1u << (x & 31);
-    if (y < g.wb + g.R) atomicOr(&g.bits[(y & (g.R - 1)) * g.wpr + (x >> 5)], b);
+    if (__builtin_expect(y < g.wb + g.R, 1)) atomicOr(&g.bits[(y & (g.R - 1)) * g.wpr + (x >> 5)], b);
     else __hip_atomic_fetch_or(g.gbits + (size_t)y * g.wpr + (x >> 5), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ unsigned q_get(const GrowCtx& g, int i) {
-    return i < g.QL ? g.qlds[i] : gload_l2(g.qglob + (i - g.QL));
+    if (__builtin_expect(i < g.QL, 1)) return g.qlds[i];
+    return gload_l2(g.qglob + (i - g.QL));
 }
 __device__ __forceinline__ void q_put(const GrowCtx& g, int i, unsigned v) {
-    if (i < g.QL) g.qlds[i] = v;
+    if (__builtin_expect(i < g.QL, 1)) g.qlds[i] = v;
     else gstore_l2(g.qglob + (i - g.QL), v);
 }
 __device__ __forceinline__ float deg_at(const GrowCtx& g, int x, int y) {
-    if (y < g.wb + g.R) return g.win[(y & (g.R - 1)) * g.sw + x];
-    return g.P[(size_t)y * g.sw + x];
+    const bool inwin = y < g.wb + g.R;
+    const int yy = inwin ? y : g.wb;
+    float v = g.win[(yy & (g.R - 1)) * g.sw + x];
+    if (__builtin_expect(!inwin, 0)) v = g.P[(size_t)y * g.sw + x];
+    return v;
 }
 
 // isAligned (lsd.cpp:1136-1152) with a = (double)deg * DEG_TO_RADS, exactly the
 // value ll_angle stored in angles_data.
 __device__ __forceinline__ bool is_aligned_deg(float deg, double theta, double prec) {
-    if (deg == kNotdefF) return false;
+    // select form of the reference's branches (same operations, no divergence)
     const double a = (double)deg * kD2R;
-    double n_theta = theta - a;
-    if (n_theta < 0) n_theta = -n_theta;
-    if (n_theta > (3 * kPi) / 2) {
-        n_theta -= (2 * kPi);
-        if (n_theta < 0) n_theta = -n_theta;
-    }
-    return n_theta <= prec;
+    const double d = theta - a;
+    const double n0 = d < 0 ? -d : d;
+    const double d2 = n0 - (2 * kPi);
+    const double n1 = d2 < 0 ? -d2 : d2;
+    const double n_theta = n0 > (3 * kPi) / 2 ? n1 : n0;
+    return deg != kNotdefF && n_theta <= prec;
 }
 
 __device__ __forceinline__ double angle_diff(double a, double b) {
@@ -286,6 +291,9 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                                                       int* __restrict__ nlines, int* __restrict__ err, int R, int QL,
                                                       unsigned long long* __restrict__ stats) {
     extern __shared__ __align__(16) unsigned lds_u[];
+    // latency-bound serial chain: win the SIMD arbiter against co-resident
+    // throughput kernels (ORB / LBD on the other stream)
+    __builtin_amdgcn_s_setprio(3);
     const int o = blockIdx.x, f = blockIdx.y, nOct = gridDim.x;
     const LineOctDev& od = octs[o];
     const int sw = od.sw, sh = od.sh;
@@ -321,6 +329,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
     // [4] seeds [5] blocks [6] rounds [7] rect points [8] commits
     unsigned long long s_setup = 0, s_round = 0, s_rect = 0, n_seed = 0, n_block = 0, n_round = 0, n_rpt = 0,
                        n_commit = 0;
+    unsigned long long s_ph[4] = {0, 0, 0, 0};
     const bool do_stats = stats != nullptr;
     const unsigned long long t_begin = do_stats ? __builtin_amdgcn_s_memtime() : 0;
     const int half = R / 2;
@@ -382,12 +391,14 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                     if (do_stats) { t1 = __builtin_amdgcn_s_memtime(); s_setup += t1 - t0; n_block++; }
                     int start = 0;
                     while (start < 9 * nb) {
-                        if (do_stats) n_round++;
+                        unsigned long long r0t = 0;
+                        if (do_stats) { n_round++; r0t = __builtin_amdgcn_s_memtime(); }
                         const unsigned long long fromStart = ~0ull << start;
                         const bool candl = lane >= start && deg != kNotdefF && !used_get(g, nx, ny);
                         const bool al = candl && is_aligned_deg(deg, reg_angle, prec);
                         const bool acc = al && (dup & fromStart) == 0ull;
                         const unsigned long long A = __ballot(acc);
+                        if (do_stats) { const unsigned long long t = __builtin_amdgcn_s_memtime(); s_ph[0] += t - r0t; r0t = t; }
                         if (!A) break;  // no commit: every remaining decision is final
                         // exact angle sequence of the speculated commits (sequential float sums)
                         float sx2 = sumdx, sy2 = sumdy, pfx = 0.f, pfy = 0.f;
@@ -400,6 +411,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                         }
                         const int mcount = t;
                         const double th = lane < mcount ? (double)plvi_fast_atan2(pfy, pfx) * kD2R : 0.0;
+                        if (do_stats) { const unsigned long long t = __builtin_amdgcn_s_memtime(); s_ph[1] += t - r0t; r0t = t; }
                         // verify every decision against the angle it really sees
                         const int cl = __popcll(A & below);
                         double theta_l = reg_angle;
@@ -414,6 +426,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                         }
                         const bool al2 = candl && (dup & A) == 0ull && is_aligned_deg(deg, theta_l, prec);
                         const unsigned long long mism = __ballot(al2 != acc) & fromStart;
+                        if (do_stats) { const unsigned long long t = __builtin_amdgcn_s_memtime(); s_ph[2] += t - r0t; r0t = t; }
                         unsigned long long C;
                         int nc;
                         if (!mism) {
@@ -440,7 +453,8 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                             reg_angle = readlane_d(th, nc - 1);
                             if (do_stats) n_commit += nc;
                         }
-                        __syncthreads();
+                        __builtin_amdgcn_wave_barrier();
+                        if (do_stats) s_ph[3] += __builtin_amdgcn_s_memtime() - r0t;
                     }
                     if (do_stats) s_round += __builtin_amdgcn_s_memtime() - t1;
                     i += nb;
@@ -452,12 +466,18 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                 // lanes form the per-point products, lane 0 adds them in region
                 // order (the reference's double summation order)
                 double xs = 0, ys = 0, sum = 0, Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
+                unsigned q0 = 0;
+                double w0 = 0.0;
+                if (lane < reg_size) {
+                    q0 = q_get(g, lane);
+                    w0 = M[(int)(q0 >> 16) * sw + (int)(q0 & 0xffffu)];
+                }
                 for (int pass = 0; pass < 2; ++pass) {
                     for (int base = 0; base < reg_size; base += 64) {
                         const int j = base + lane;
                         if (j < reg_size) {
-                            const unsigned q = q_get(g, j);
-                            const double w = M[(int)(q >> 16) * sw + (int)(q & 0xffffu)];
+                            const unsigned q = base == 0 ? q0 : q_get(g, j);
+                            const double w = base == 0 ? w0 : M[(int)(q >> 16) * sw + (int)(q & 0xffffu)];
                             const double rx = (double)(int)(q & 0xffffu), ry = (double)(int)(q >> 16);
                             if (pass == 0) {
                                 rs[lane] = rx * w;
@@ -545,6 +565,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
         S[0] = __builtin_amdgcn_s_memtime() - t_begin;
         S[1] = s_setup; S[2] = s_round; S[3] = s_rect; S[4] = n_seed;
         S[5] = n_block; S[6] = n_round; S[7] = n_rpt; S[8] = n_commit;
+        S[9] = s_ph[0]; S[10] = s_ph[1]; S[11] = s_ph[2]; S[12] = s_ph[3];
     }
 }
 

@@ -199,7 +199,7 @@ struct LinePipeline {
         size_t budget = 40 * 1024;
         if (const char* e = getenv("PLVI_GROW_LDS")) budget = (size_t)atol(e);
         budget = std::min<size_t>(budget, 160 * 1024);
-        growQL = 1024;
+        growQL = budget >= 32 * 1024 ? 1024 : 256;
         const size_t fixed = 64 * 3 * sizeof(double) + (size_t)growQL * sizeof(unsigned);
         const size_t perRow = maxSw * sizeof(float) + (maxSw + 31) / 32 * sizeof(unsigned);
         growR = 4;

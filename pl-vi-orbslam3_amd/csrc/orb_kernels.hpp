@@ -468,59 +468,82 @@ __constant__ signed char c_pattern[1024] = {
 };
 __constant__ int c_umax[16];
 
+// One wave per keypoint (4 waves per workgroup, grid-stride over the slots):
+//  * IC_Angle moments: lanes 0..30 / 32..62 take the disc columns u=-15..15
+//    of rows v = 0..7 / 8..15, read straight from the level image (each row
+//    one coalesced 31-byte segment); integer sums, so any order is exact.
+//  * rBRIEF: the 37x37 neighbourhood of the blurred level (rotated pattern
+//    offsets are within +-18) is staged in LDS with row-coalesced loads;
+//    lane l evaluates tests l, l+64, l+128, l+192 and one ballot per 64
+//    tests yields 8 descriptor bytes directly (test j = byte j/8, bit j%8).
+constexpr int kDescR = 18, kDescP = 2 * kDescR + 1, kDescPitch = 40;
+
 __global__ __launch_bounds__(256) void orb_describe_kernel(const OrbLevelDev* __restrict__ lvs, int L,
                                                            const uint8_t* __restrict__ pyr,
                                                            const uint8_t* __restrict__ blur,
                                                            const int* __restrict__ rect_cnt,
                                                            float4* __restrict__ lvkp, uint8_t* __restrict__ lvdesc,
                                                            int kpCapFrame) {
+    __shared__ uint8_t patch[4][kDescP * kDescPitch];
     const int f = blockIdx.y;
-    const int slot = blockIdx.x * 256 + threadIdx.x;
-    if (slot >= kpCapFrame) return;
-    int l = 0;
-    while (l + 1 < L && slot >= lvs[l + 1].kpOff) ++l;
-    const OrbLevelDev& lv = lvs[l];
-    const int idx = slot - lv.kpOff;
-    if (idx >= rect_cnt[(size_t)f * L + l]) return;
-    float4 kp = lvkp[(size_t)f * kpCapFrame + slot];
-    const int cx = (int)kp.x, cy = (int)kp.y;  // integer-valued level coords
-    const uint8_t* I = pyr + lv.off + (size_t)f * lv.plane;
-    const int W = lv.w;
-    // IC_Angle
-    int m_01 = 0, m_10 = 0;
-    const uint8_t* center = I + (size_t)cy * W + cx;
-    for (int u = -15; u <= 15; ++u) m_10 += u * center[u];
-    for (int v = 1; v <= 15; ++v) {
-        int v_sum = 0;
-        const int d = c_umax[v];
-        for (int u = -d; u <= d; ++u) {
-            const int vp = center[u + v * W], vm = center[u - v * W];
-            v_sum += vp - vm;
-            m_10 += u * (vp + vm);
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint8_t* P = patch[wv];
+    const int half = lane >> 5, u = (lane & 31) - 15;
+    for (int slot = blockIdx.x * 4 + wv; slot < kpCapFrame; slot += gridDim.x * 4) {
+        int l = 0;
+        while (l + 1 < L && slot >= lvs[l + 1].kpOff) ++l;
+        const OrbLevelDev& lv = lvs[l];
+        const int idx = slot - lv.kpOff;
+        if (idx >= rect_cnt[(size_t)f * L + l]) continue;  // wave-uniform
+        float4 kp = lvkp[(size_t)f * kpCapFrame + slot];
+        const int cx = (int)kp.x, cy = (int)kp.y;  // integer-valued level coords
+        const int W = lv.w;
+        // ---- IC_Angle (ORBextractor.cc:75-102)
+        const uint8_t* center = pyr + lv.off + (size_t)f * lv.plane + (size_t)cy * W + cx;
+        int m_01 = 0, m_10 = 0;
+        if (u <= 15) {
+            if (half == 0) m_10 += u * center[u];
+            for (int v = half ? 8 : 1; v <= (half ? 15 : 7); ++v) {
+                const int d = c_umax[v];
+                if (u >= -d && u <= d) {
+                    const int vp = center[u + v * W], vm = center[u - v * W];
+                    m_01 += v * (vp - vm);
+                    m_10 += u * (vp + vm);
+                }
+            }
         }
-        m_01 += v * v_sum;
-    }
-    const float angle = plvi_fast_atan2((float)m_01, (float)m_10);
-    kp.w = angle;
-    lvkp[(size_t)f * kpCapFrame + slot] = kp;
-    // rBRIEF
-    const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
-    const float ang = angle * factorPI;
-    const float a = plvi_cosf(ang), b = plvi_sinf(ang);
-    const uint8_t* Bc = blur + lv.off + (size_t)f * lv.plane + (size_t)cy * W + cx;
-    uint8_t* out = lvdesc + ((size_t)f * kpCapFrame + slot) * 32;
-    for (int i = 0; i < 32; ++i) {
-        int val = 0;
+        for (int s2 = 32; s2 > 0; s2 >>= 1) {
+            m_01 += __shfl_xor(m_01, s2);
+            m_10 += __shfl_xor(m_10, s2);
+        }
+        const float angle = plvi_fast_atan2((float)m_01, (float)m_10);
+        if (lane == 0) {
+            kp.w = angle;
+            lvkp[(size_t)f * kpCapFrame + slot] = kp;
+        }
+        // ---- rBRIEF (computeOrbDescriptor, ORBextractor.cc:106-145)
+        const uint8_t* Bc = blur + lv.off + (size_t)f * lv.plane + (size_t)(cy - kDescR) * W + (cx - kDescR);
+        for (int i = lane; i < kDescP * kDescP; i += 64) {
+            const int r = i / kDescP, c = i - r * kDescP;
+            P[r * kDescPitch + c] = Bc[(size_t)r * W + c];
+        }
+        const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
+        const float ang = angle * factorPI;
+        const float a = plvi_cosf(ang), b = plvi_sinf(ang);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        uint64_t* out = reinterpret_cast<uint64_t*>(lvdesc + ((size_t)f * kpCapFrame + slot) * 32);
 #pragma unroll
-        for (int bit = 0; bit < 8; ++bit) {
-            const int p0 = 16 * i + 2 * bit, p1 = p0 + 1;
-            const float x0 = c_pattern[2 * p0], y0 = c_pattern[2 * p0 + 1];
-            const float x1 = c_pattern[2 * p1], y1 = c_pattern[2 * p1 + 1];
-            const int t0 = Bc[cv_round_f(x0 * b + y0 * a) * W + cv_round_f(x0 * a - y0 * b)];
-            const int t1 = Bc[cv_round_f(x1 * b + y1 * a) * W + cv_round_f(x1 * a - y1 * b)];
-            val |= (t0 < t1) << bit;
+        for (int k = 0; k < 4; ++k) {
+            const int j = lane + 64 * k;
+            const float x0 = c_pattern[4 * j], y0 = c_pattern[4 * j + 1];
+            const float x1 = c_pattern[4 * j + 2], y1 = c_pattern[4 * j + 3];
+            const int t0 = P[(cv_round_f(x0 * b + y0 * a) + kDescR) * kDescPitch + cv_round_f(x0 * a - y0 * b) + kDescR];
+            const int t1 = P[(cv_round_f(x1 * b + y1 * a) + kDescR) * kDescPitch + cv_round_f(x1 * a - y1 * b) + kDescR];
+            const unsigned long long m = __ballot(t0 < t1);
+            if (lane == 0) out[k] = m;
         }
-        out[i] = (uint8_t)val;
+        __builtin_amdgcn_wave_barrier();
     }
 }
 

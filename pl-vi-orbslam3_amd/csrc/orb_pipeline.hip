@@ -322,7 +322,7 @@ struct OrbPipeline {
                            nodeCapMax, L, lvkp.as<float4>(), kpCapFrame);
         mark(5, st);
         // K6 orientation + rBRIEF
-        hipLaunchKernelGGL(orb_describe_kernel, dim3((kpCapFrame + 255) / 256, nf), dim3(256), 0, st,
+        hipLaunchKernelGGL(orb_describe_kernel, dim3((kpCapFrame + 15) / 16, nf), dim3(256), 0, st,
                            d_lv.as<OrbLevelDev>(), L, (const uint8_t*)P, (const uint8_t*)Bl,
                            (const int*)rectCnt.as<int>(), lvkp.as<float4>(), lvdesc.as<uint8_t>(), kpCapFrame);
         mark(6, st);

@@ -189,16 +189,13 @@ PLVI_HD float plvi_fast_atan2(float y, float x) {
     const float p5 = 0.1555786518463281f * k, p7 = -0.04432655554792128f * k;
     const float eps = (float)2.2204460492503131e-16;
     float ax = __builtin_fabsf(x), ay = __builtin_fabsf(y);
-    float a, c, c2;
-    if (ax >= ay) {
-        c = ay / (ax + eps);
-        c2 = c * c;
-        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
-    } else {
-        c = ax / (ay + eps);
-        c2 = c * c;
-        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
-    }
+    // both branches of cv::fastAtan2 share one division and one polynomial
+    // (select form: no lane divergence, identical operations per branch)
+    const bool ge = ax >= ay;
+    const float c = (ge ? ay : ax) / ((ge ? ax : ay) + eps);
+    const float c2 = c * c;
+    const float pc = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    float a = ge ? pc : 90.f - pc;
     if (x < 0) a = 180.f - a;
     if (y < 0) a = 360.f - a;
     return a;

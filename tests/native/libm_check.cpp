@@ -7,6 +7,8 @@
 //   sincosf     : every float bit pattern in [lo,hi) (default: all 2^32)
 //   atan2f N    : N seeded random (y,x) pairs + edge grid
 //   lsdangles   : every float deg in [0,360]: float(cos/sin((double)deg*pi/180))
+//   sincospos   : branch-free sincosf vs glibc, every float in [0,120)
+//   fastatan2 N : device cv::fastAtan2 vs the oracle's restatement, N pairs + grid
 // Prints "mismatches=<k> checked=<n>" and exits non-zero on any mismatch.
 #include <cmath>
 #include <cstdio>
@@ -18,6 +20,7 @@
 #include <atomic>
 
 #include "../../pl-vi-orbslam3_amd/csrc/plvi_math.h"
+#include "../../oracle/cvprim.h"
 
 static bool same(float a, float b) {
     if (std::isnan(a) && std::isnan(b)) return true;
@@ -97,6 +100,27 @@ int main(int argc, char** argv) {
                     float x = plvi::u2f(u), s, co;
                     plvi::plvi_sincosf_pos(x, &s, &co);
                     if (!same(s, sinf(x)) || !same(co, cosf(x))) { if (b < 5) fprintf(stderr, "sincospos %a\n", x); ++b; }
+                    ++c;
+                }
+                bad += b; checked += c;
+            });
+    } else if (!strcmp(mode, "fastatan2")) {
+        long n = argc > 2 ? atol(argv[2]) : 100000000L;
+        for (int t = 0; t < nt; ++t)
+            th.emplace_back([&, t] {
+                std::mt19937_64 rng(99 + t);
+                std::uniform_real_distribution<float> u(-4.f, 4.f);
+                std::uniform_int_distribution<uint32_t> bits;
+                unsigned long long b = 0, c = 0;
+                for (long i = t; i < n; i += nt) {
+                    float y, x;
+                    if (i % 3 == 0) { y = plvi::u2f(bits(rng)); x = plvi::u2f(bits(rng)); }
+                    else if (i % 3 == 1) { y = u(rng); x = u(rng); }
+                    else { y = (float)((int)(i / 3) % 41 - 20); x = (float)((int)(i / 123) % 41 - 20); }
+                    if (!same(plvi::plvi_fast_atan2(y, x), oracle::fast_atan2(y, x))) {
+                        if (b < 5) fprintf(stderr, "fastatan2 %a %a\n", y, x);
+                        ++b;
+                    }
                     ++c;
                 }
                 bad += b; checked += c;

@@ -16,7 +16,7 @@ def libm_check():
     hdr = ROOT / "pl-vi-orbslam3_amd" / "csrc" / "plvi_math.h"
     if not BIN.exists() or BIN.stat().st_mtime < max(SRC.stat().st_mtime, hdr.stat().st_mtime):
         subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-pthread", "-o",
-                        str(BIN), str(SRC), "-lm"], check=True)
+                        str(BIN), str(SRC), str(ROOT / "oracle" / "cvprim.cpp"), "-lm"], check=True)
     return str(BIN)
 
 
@@ -42,3 +42,7 @@ def test_atan2f_sampled(libm_check):
 
 def test_branch_free_sincosf_every_float(libm_check):
     _run(libm_check, "sincospos")              # plvi_sincosf_pos vs glibc sinf/cosf, every float in [0, 120)
+
+
+def test_fast_atan2_select_form(libm_check):
+    _run(libm_check, "fastatan2", "30000000")  # branch-free device cv::fastAtan2 vs the oracle restatement
