@@ -198,6 +198,40 @@ int plvi_line_match_batch(const uint8_t* d_desc1, const int* d_n1, int cap1, con
                           int cap2, int n_pairs, float nnr, int* d_scratch, int* d_matches_12, int* d_nmatch,
                           void* stream);
 
+/* ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:2350-2366) or, with
+ * line_matcher_quirk != 0, LineMatcher::DescriptorDistance
+ * (src/LineMatcher.cpp:487-499: per-word count >> 25) of n row pairs
+ * (d_a[i], d_b[i]), 32 bytes each; device pointers, asynchronous. */
+int plvi_descriptor_distance_batch(const uint8_t* d_a, const uint8_t* d_b, int n, int line_matcher_quirk, int* d_out,
+                                   void* stream);
+
+/* ------------------------------------------------------------- SearchByBoW
+ * ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>&)
+ * (src/ORBmatcher.cc:269-471) with ComputeThreeMaxima (:2304-2345),
+ * monocular branch (F.Nleft == -1, no second camera).  FeatureVectors are
+ * CSR arrays sorted by node id: node[i], off[i]..off[i+1] into idx[] (the
+ * keypoint indices of node i in FeatureVector order).  kf_live[k] = the KF
+ * keypoint has a MapPoint that is not bad (evaluated by the caller).
+ * Angles: pKF->mvKeysUn[k].angle and F.mvKeys[i].angle.  Output
+ * match_kf[i] = KF keypoint index whose MapPoint goes to
+ * vpMapPointMatches[i], or -1.  Returns nmatches (>= 0) or an error. */
+int plvi_search_by_bow(float nnratio, int check_orientation, const uint8_t* kf_desc, const float* kf_angle,
+                       const uint8_t* kf_live, int kf_n, const int* kf_node, const int* kf_off, int kf_nnodes,
+                       const int* kf_idx, const uint8_t* f_desc, const float* f_angle, int f_n, const int* f_node,
+                       const int* f_off, int f_nnodes, const int* f_idx, int* match_kf);
+
+/* Batched device variant: pair p uses rows p*kf_cap / p*f_cap of the
+ * keypoint arrays, p*node_cap (node ids) and p*(node_cap+1) (offsets) of
+ * the CSR arrays, counts kf_nnodes[p], f_nnodes[p], f_n[p].  Outputs
+ * match_kf [n_pairs][f_cap], nmatches [n_pairs].  Needs
+ * 4*f_cap + 8*node_cap <= 65536 bytes of LDS. */
+int plvi_search_by_bow_batch(int n_pairs, float nnratio, int check_orientation, int kf_cap, int f_cap, int node_cap,
+                             const uint8_t* d_kf_desc, const float* d_kf_angle, const uint8_t* d_kf_live,
+                             const int* d_kf_node, const int* d_kf_off, const int* d_kf_nnodes, const int* d_kf_idx,
+                             const uint8_t* d_f_desc, const float* d_f_angle, const int* d_f_n, const int* d_f_node,
+                             const int* d_f_off, const int* d_f_nnodes, const int* d_f_idx, int* d_match_kf,
+                             int* d_nmatches, void* stream);
+
 /* Device memory helpers for bindings that have no HIP runtime of their own
  * (ctypes, JNI): thin wrappers over hipMalloc/hipFree/hipMemcpy on the
  * current device.  kind: 1 = host->device, 2 = device->host, 3 = d->d. */

@@ -6,7 +6,9 @@
 //   LineMatcher::DescriptorDistance src/LineMatcher.cpp:487-499 (>>25 quirk)
 //   BFMatcher::knnMatch(k=2)  OpenCV 4.2 batchDistance K-insertion
 //   LineMatcher::matchNNR / match  src/LineMatcher.cpp:41-111
+//   ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...)  src/ORBmatcher.cc:269-471
 #include <climits>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -76,4 +78,105 @@ extern "C" int oracle_match(const uint8_t* d1, int n1, const uint8_t* d2, int n2
         }
     }
     return matches;
+}
+
+// ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)
+// (src/ORBmatcher.cc:269-471) + ComputeThreeMaxima (:2304-2345), monocular
+// branch (F.Nleft == -1, no second camera).  The FeatureVectors
+// (std::map<NodeId, vector<unsigned>>) arrive as CSR arrays sorted by node
+// id; pMP != NULL && !pMP->isBad() arrives as kf_live[realIdxKF].  Output:
+// match_kf[iF] = KF keypoint index whose MapPoint the reference stores in
+// vpMapPointMatches[iF], or -1.  Returns nmatches.
+static int lower_bound_node(const int* ids, int lo, int hi, int key) {
+    while (lo < hi) {
+        int mid = (lo + hi) / 2;
+        if (ids[mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+extern "C" int oracle_search_by_bow(const uint8_t* kf_desc, const float* kf_angle, const uint8_t* kf_live,
+                                    const int* kf_node, const int* kf_off, int kf_nnodes, const int* kf_idx,
+                                    const uint8_t* f_desc, const float* f_angle, int f_n, const int* f_node,
+                                    const int* f_off, int f_nnodes, const int* f_idx, float nnratio,
+                                    int check_orientation, int* match_kf) {
+    const int TH_LOW = 50, HISTO_LENGTH = 30;
+    for (int i = 0; i < f_n; ++i) match_kf[i] = -1;
+    std::vector<std::vector<int>> rotHist(HISTO_LENGTH);
+    const float factor = 1.0f / HISTO_LENGTH;
+    int nmatches = 0;
+    int KFit = 0, Fit = 0;
+    while (KFit < kf_nnodes && Fit < f_nnodes) {
+        if (kf_node[KFit] == f_node[Fit]) {
+            for (int a = kf_off[KFit]; a < kf_off[KFit + 1]; ++a) {
+                const int realIdxKF = kf_idx[a];
+                if (!kf_live[realIdxKF]) continue;
+                const uint8_t* dKF = kf_desc + (size_t)realIdxKF * 32;
+                int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
+                for (int b = f_off[Fit]; b < f_off[Fit + 1]; ++b) {
+                    const int realIdxF = f_idx[b];
+                    if (match_kf[realIdxF] >= 0) continue;
+                    const int dist = descriptor_distance(dKF, f_desc + (size_t)realIdxF * 32, 24);
+                    if (dist < bestDist1) {
+                        bestDist2 = bestDist1;
+                        bestDist1 = dist;
+                        bestIdxF = realIdxF;
+                    } else if (dist < bestDist2) {
+                        bestDist2 = dist;
+                    }
+                }
+                if (bestDist1 <= TH_LOW) {
+                    if (static_cast<float>(bestDist1) < nnratio * static_cast<float>(bestDist2)) {
+                        match_kf[bestIdxF] = realIdxKF;
+                        if (check_orientation) {
+                            float rot = kf_angle[realIdxKF] - f_angle[bestIdxF];
+                            if (rot < 0.0) rot += 360.0f;
+                            int bin = (int)std::round(rot * factor);
+                            if (bin == HISTO_LENGTH) bin = 0;
+                            rotHist[bin].push_back(bestIdxF);
+                        }
+                        nmatches++;
+                    }
+                }
+            }
+            KFit++;
+            Fit++;
+        } else if (kf_node[KFit] < f_node[Fit]) {
+            KFit = lower_bound_node(kf_node, KFit, kf_nnodes, f_node[Fit]);
+        } else {
+            Fit = lower_bound_node(f_node, Fit, f_nnodes, kf_node[KFit]);
+        }
+    }
+    if (check_orientation) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        int max1 = 0, max2 = 0, max3 = 0;
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            const int s = (int)rotHist[i].size();
+            if (s > max1) {
+                max3 = max2; max2 = max1; max1 = s;
+                ind3 = ind2; ind2 = ind1; ind1 = i;
+            } else if (s > max2) {
+                max3 = max2; max2 = s;
+                ind3 = ind2; ind2 = i;
+            } else if (s > max3) {
+                max3 = s;
+                ind3 = i;
+            }
+        }
+        if (max2 < 0.1f * (float)max1) {
+            ind2 = -1;
+            ind3 = -1;
+        } else if (max3 < 0.1f * (float)max1) {
+            ind3 = -1;
+        }
+        for (int i = 0; i < HISTO_LENGTH; i++) {
+            if (i == ind1 || i == ind2 || i == ind3) continue;
+            for (size_t j = 0; j < rotHist[i].size(); j++) {
+                match_kf[rotHist[i][j]] = -1;
+                nmatches--;
+            }
+        }
+    }
+    return nmatches;
 }

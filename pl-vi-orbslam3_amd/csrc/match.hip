@@ -240,3 +240,35 @@ extern "C" int plvi_line_match(const uint8_t* desc1, int n1, const uint8_t* desc
     }
     return matches;
 }
+
+// ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:2350-2366, per-word
+// count >> 24 = popcount) and LineMatcher::DescriptorDistance
+// (src/LineMatcher.cpp:487-499, the >> 25 quirk: each word's count halved
+// and floored), over n row pairs (a[i], b[i]).
+namespace plvi {
+__global__ __launch_bounds__(256) void descriptor_distance_kernel(const uint8_t* __restrict__ a,
+                                                                  const uint8_t* __restrict__ b, int n, int shift,
+                                                                  int* __restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint4* pa = reinterpret_cast<const uint4*>(a + (size_t)i * 32);
+    const uint4* pb = reinterpret_cast<const uint4*>(b + (size_t)i * 32);
+    const uint4 a0 = pa[0], a1 = pa[1], b0 = pb[0], b1 = pb[1];
+    const unsigned w[8] = {a0.x ^ b0.x, a0.y ^ b0.y, a0.z ^ b0.z, a0.w ^ b0.w,
+                           a1.x ^ b1.x, a1.y ^ b1.y, a1.z ^ b1.z, a1.w ^ b1.w};
+    int d = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d += (int)((unsigned)__popc(w[k]) >> (shift - 24));
+    out[i] = d;
+}
+}  // namespace plvi
+
+extern "C" int plvi_descriptor_distance_batch(const uint8_t* d_a, const uint8_t* d_b, int n, int line_matcher_quirk,
+                                              int* d_out, void* stream) {
+    if (n < 0 || (n && (!d_a || !d_b || !d_out))) return PLVI_E_BADARG;
+    if (n == 0) return PLVI_OK;
+    hipLaunchKernelGGL(plvi::descriptor_distance_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       d_a, d_b, n, line_matcher_quirk ? 25 : 24, d_out);
+    PLVI_CHECK(hipGetLastError());
+    return PLVI_OK;
+}

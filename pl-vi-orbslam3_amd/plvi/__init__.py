@@ -5,6 +5,7 @@ Class and method names follow the reference interfaces they replace:
 
   ORBextractor  -> ORB_SLAM3::ORBextractor (include/ORBextractor.h:44-110)
   LineMatcher   -> ORB_SLAM3::LineMatcher  (include/LineMatcher.h:88-107)
+  ORBmatcher    -> ORB_SLAM3::ORBmatcher   (include/ORBmatcher.h:39-68): SearchByBoW, DescriptorDistance
   hamming_knn2  -> cv::BFMatcher(NORM_HAMMING).knnMatch(k=2) (LineMatcher.cpp:47-48)
 
 There is no CPU fallback: if the HIP library is missing or no GPU is
@@ -90,6 +91,9 @@ def _declare(lib):
         "plvi_lines_profile": ([V, I], I),
         "plvi_lines_profile_read": ([V, V, P], I),
         "plvi_lines_debug_stats": ([V, V], I),
+        "plvi_descriptor_distance_batch": ([V, V, I, I, V, V], I),
+        "plvi_search_by_bow": ([F, I, V, V, V, I, V, V, I, V, V, V, I, V, V, I, V, V], I),
+        "plvi_search_by_bow_batch": ([I, F, I, I, I, I, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V], I),
         "plvi_device_malloc": ([c_void_pp, S], I),
         "plvi_device_free": ([V], I),
         "plvi_memcpy": ([V, V, S, I], I),
@@ -395,3 +399,57 @@ class LineMatcher:
         n = _check(lib.plvi_line_match(_ptr(d1), d1.shape[0], _ptr(d2), d2.shape[0], nnr, _ptr(m)),
                    "plvi_line_match")
         return n, m
+
+
+def feature_vector_csr(fv):
+    """DBoW2::FeatureVector (std::map<NodeId, vector<unsigned>>) as given by a
+    dict {node_id: [keypoint indices]} -> (node ids ascending, offsets, indices)."""
+    nodes = np.array(sorted(fv), dtype=np.int32)
+    off = np.zeros(len(nodes) + 1, np.int32)
+    idx = []
+    for i, n in enumerate(nodes):
+        idx.extend(fv[int(n)])
+        off[i + 1] = len(idx)
+    return nodes, off, np.array(idx, dtype=np.int32)
+
+
+class ORBmatcher:
+    """ORB_SLAM3::ORBmatcher(nnratio=0.6, checkOri=true) (include/ORBmatcher.h:39-68)."""
+
+    def __init__(self, nnratio=0.6, checkOri=True):
+        self._lib = load()
+        self.nnratio = float(nnratio)
+        self.check_orientation = bool(checkOri)
+
+    def SearchByBoW(self, kf_desc, kf_angle, kf_live, kf_featvec, f_desc, f_angle, f_featvec):
+        """SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&) (src/ORBmatcher.cc:269-471).
+        Returns (nmatches, match_kf) with match_kf[iF] = KF keypoint index or -1."""
+        kd = np.ascontiguousarray(kf_desc, np.uint8)
+        ka = np.ascontiguousarray(kf_angle, np.float32)
+        kl = np.ascontiguousarray(kf_live, np.uint8)
+        fd = np.ascontiguousarray(f_desc, np.uint8)
+        fa = np.ascontiguousarray(f_angle, np.float32)
+        kn, ko, ki = feature_vector_csr(kf_featvec)
+        fn, fo, fi = feature_vector_csr(f_featvec)
+        out = np.full(max(len(fd), 1), -1, np.int32)
+        n = _check(self._lib.plvi_search_by_bow(self.nnratio, int(self.check_orientation), _ptr(kd), _ptr(ka),
+                                                _ptr(kl), len(kd), _ptr(kn), _ptr(ko), len(kn), _ptr(ki), _ptr(fd),
+                                                _ptr(fa), len(fd), _ptr(fn), _ptr(fo), len(fn), _ptr(fi), _ptr(out)),
+                   "plvi_search_by_bow")
+        return n, out[:len(fd)]
+
+    @staticmethod
+    def DescriptorDistance(a, b, line_matcher_quirk=False):
+        """Row-wise distances of two n x 32 descriptor tables on the GPU."""
+        a = np.ascontiguousarray(a, np.uint8).reshape(-1, 32)
+        b = np.ascontiguousarray(b, np.uint8).reshape(-1, 32)
+        n = a.shape[0]
+        lib = load()
+        da, db, do = DeviceBuffer(max(a.nbytes, 32)), DeviceBuffer(max(b.nbytes, 32)), DeviceBuffer(max(4 * n, 4))
+        da.upload(a)
+        db.upload(b)
+        _check(lib.plvi_descriptor_distance_batch(ctypes.c_void_p(da.ptr), ctypes.c_void_p(db.ptr), n,
+                                                  int(line_matcher_quirk), ctypes.c_void_p(do.ptr), None),
+               "plvi_descriptor_distance_batch")
+        lib.plvi_device_synchronize()
+        return do.download(np.zeros(n, np.int32))

@@ -50,6 +50,12 @@ def load():
     lib.oracle_gaussian_kernel_f64.argtypes = [I, D, V]
     lib.oracle_fast_atan2.argtypes = [F, F]
     lib.oracle_fast_atan2.restype = F
+    lib.oracle_search_by_bow.argtypes = [V, V, V, V, V, I, V, V, V, I, V, V, I, V, F, I, V]
+    lib.oracle_search_by_bow.restype = I
+    lib.oracle_descriptor_distance.argtypes = [V, V]
+    lib.oracle_descriptor_distance.restype = I
+    lib.oracle_line_descriptor_distance.argtypes = [V, V]
+    lib.oracle_line_descriptor_distance.restype = I
     lib.oracle_fast_score.argtypes = [V, I]
     lib.oracle_fast_score.restype = I
     _lib = lib
@@ -202,3 +208,25 @@ def line_iterator_count(W, H, x1, y1, x2, y2):
     F, I = ctypes.c_float, ctypes.c_int
     lib.oracle_line_iterator_count.argtypes = [I, I, F, F, F, F]
     return lib.oracle_line_iterator_count(W, H, x1, y1, x2, y2)
+
+
+def search_by_bow(kf_desc, kf_angle, kf_live, kf_fv, f_desc, f_angle, f_fv, nnratio, check_orientation=True):
+    """ORBmatcher::SearchByBoW restatement; fv = dict {node: [indices]}."""
+    lib = load()
+    def csr(fv):
+        nodes = np.array(sorted(fv), dtype=np.int32)
+        off = np.zeros(len(nodes) + 1, np.int32)
+        idx = []
+        for i, n in enumerate(nodes):
+            idx.extend(fv[int(n)])
+            off[i + 1] = len(idx)
+        return nodes, off, np.array(idx if idx else [0], dtype=np.int32)
+    kn, ko, ki = csr(kf_fv)
+    fn, fo, fi = csr(f_fv)
+    kd = np.ascontiguousarray(kf_desc, np.uint8); ka = np.ascontiguousarray(kf_angle, np.float32)
+    kl = np.ascontiguousarray(kf_live, np.uint8); fd = np.ascontiguousarray(f_desc, np.uint8)
+    fa = np.ascontiguousarray(f_angle, np.float32)
+    out = np.full(max(len(fd), 1), -1, np.int32)
+    n = lib.oracle_search_by_bow(_p(kd), _p(ka), _p(kl), _p(kn), _p(ko), len(kn), _p(ki), _p(fd), _p(fa), len(fd),
+                                 _p(fn), _p(fo), len(fn), _p(fi), float(nnratio), int(check_orientation), _p(out))
+    return n, out[:len(fd)]
