@@ -232,6 +232,34 @@ int plvi_search_by_bow_batch(int n_pairs, float nnratio, int check_orientation, 
                              const int* d_f_off, const int* d_f_nnodes, const int* d_f_idx, int* d_match_kf,
                              int* d_nmatches, void* stream);
 
+/* ------------------------------------------------------------- matchGrid
+ * LineMatcher::matchGrid(lines1, desc1, grid, desc2, directions2, w,
+ * matches_12) (src/LineMatcher.cpp:191-272) with GridStructure::get
+ * (src/gridStructure.cpp:64-75).  lines1: n1 x 4 ints (sp.x, sp.y, ep.x,
+ * ep.y) = the line_2d grid coordinates (pair<int,int>, Frame.cc:1424-1427);
+ * grid: CSR over grid_cols x grid_rows cells, cell (x, y) = x*grid_rows + y,
+ * cell_off[ncell+1], cell_idx[] in std::list order; directions2: n2 x 2
+ * doubles; window = GridWindow{width(w0, w1), height(h0, h1)}.
+ * libstdcxx_range_hint selects the std::unordered_set range-insert rehash
+ * rule that orders the candidates (1: GCC <= 10, the reference's Ubuntu
+ * 20.04 toolchain; 0: GCC >= 11).  matches_12 is fully written (-1 = no
+ * match).  Returns the match count or an error (n1, n2 <= 2048). */
+int plvi_line_match_grid(const int* lines1, const uint8_t* desc1, int n1, int grid_cols, int grid_rows,
+                         const int* cell_off, const int* cell_idx, const uint8_t* desc2, const double* directions2,
+                         int n2, int win_w0, int win_w1, int win_h0, int win_h1, int libstdcxx_range_hint,
+                         int* matches_12);
+
+/* Batched device variant: pair p uses lines1 + p*cap1*4, desc1 + p*cap1*32,
+ * cell_off + p*(ncell+1), cell_idx + p*idx_cap, desc2 + p*cap2*32,
+ * directions2 + p*cap2*2, counts n1[p], n2[p].  Outputs matches_12
+ * [n_pairs][cap1], nmatches [n_pairs]; *d_err |= 1 when a candidate set
+ * exceeds 1024 lines. */
+int plvi_line_match_grid_batch(int n_pairs, const int* d_lines1, const uint8_t* d_desc1, const int* d_n1, int cap1,
+                               int grid_cols, int grid_rows, const int* d_cell_off, const int* d_cell_idx,
+                               int idx_cap, const uint8_t* d_desc2, const double* d_directions2, const int* d_n2,
+                               int cap2, int win_w0, int win_w1, int win_h0, int win_h1, int libstdcxx_range_hint,
+                               int* d_matches_12, int* d_nmatches, int* d_err, void* stream);
+
 /* Device memory helpers for bindings that have no HIP runtime of their own
  * (ctypes, JNI): thin wrappers over hipMalloc/hipFree/hipMemcpy on the
  * current device.  kind: 1 = host->device, 2 = device->host, 3 = d->d. */

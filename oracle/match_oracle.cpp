@@ -7,6 +7,7 @@
 //   BFMatcher::knnMatch(k=2)  OpenCV 4.2 batchDistance K-insertion
 //   LineMatcher::matchNNR / match  src/LineMatcher.cpp:41-111
 //   ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...)  src/ORBmatcher.cc:269-471
+//   LineMatcher::matchGrid  src/LineMatcher.cpp:191-272 (+ gridStructure.cpp:64-75)
 #include <climits>
 #include <cmath>
 #include <cstdint>
@@ -179,4 +180,78 @@ extern "C" int oracle_search_by_bow(const uint8_t* kf_desc, const float* kf_angl
         }
     }
     return nmatches;
+}
+
+// LineMatcher::matchGrid (src/LineMatcher.cpp:191-272) with
+// GridStructure::get (src/gridStructure.cpp:64-75): literal restatement on
+// std::list cells and std::unordered_set<int> candidates (the host
+// libstdc++ decides the candidate iteration order, as the reference's
+// does).  lines1[i] = (sp.x, sp.y, ep.x, ep.y) as line_2d = pair<pair<int,int>>
+// (coordinates already truncated to grid cells by the caller, Frame.cc:1424-1427);
+// the grid is CSR over cells (x * rows + y) in list order.
+#include <list>
+#include <limits>
+#include <unordered_set>
+extern "C" int oracle_match_grid(const int* lines1, const uint8_t* desc1, int n1, int cols, int rows,
+                                 const int* cell_off, const int* cell_idx, const uint8_t* desc2,
+                                 const double* directions2, int n2, int w0, int w1, int h0, int h1,
+                                 int* matches_12) {
+    std::vector<std::vector<std::list<int>>> grid(cols, std::vector<std::list<int>>(rows));
+    for (int x = 0; x < cols; ++x)
+        for (int y = 0; y < rows; ++y)
+            for (int k = cell_off[x * rows + y]; k < cell_off[x * rows + y + 1]; ++k) grid[x][y].push_back(cell_idx[k]);
+    auto get = [&](int x, int y, std::unordered_set<int>& indices) {
+        int min_x = std::max(0, x - w0);
+        int max_x = std::min(cols, x + w1 + 1);
+        int min_y = std::max(0, y - h0);
+        int max_y = std::min(rows, y + h1 + 1);
+        for (int x_ = min_x; x_ < max_x; ++x_)
+            for (int y_ = min_y; y_ < max_y; ++y_) indices.insert(grid[x_][y_].begin(), grid[x_][y_].end());
+    };
+    const double lineSimTh = 0.75, minRatio12L = 0.9;
+    int matches = 0;
+    for (int i = 0; i < n1; ++i) matches_12[i] = -1;
+    std::vector<int> matches_21(n2, -1), distances(n2, std::numeric_limits<int>::max());
+    for (int i1 = 0; i1 < n1; ++i1) {
+        int best_d = std::numeric_limits<int>::max(), best_d2 = std::numeric_limits<int>::max(), best_idx = -1;
+        const int spx = lines1[4 * i1], spy = lines1[4 * i1 + 1], epx = lines1[4 * i1 + 2], epy = lines1[4 * i1 + 3];
+        double vx = (double)(epx - spx), vy = (double)(epy - spy);
+        const double magnitude = std::sqrt(vx * vx + vy * vy);
+        vx /= magnitude;
+        vy /= magnitude;
+        std::unordered_set<int> candidates;
+        get(spx, spy, candidates);
+        get(epx, epy, candidates);
+        if (candidates.empty()) continue;
+        for (const int& i2 : candidates) {
+            if (i2 < 0 || i2 >= n2) continue;
+            if (std::abs(vx * directions2[2 * i2] + vy * directions2[2 * i2 + 1]) < lineSimTh) continue;
+            const int d = descriptor_distance(desc1 + (size_t)i1 * 32, desc2 + (size_t)i2 * 32, 24);
+            if (d < distances[i2]) {
+                distances[i2] = d;
+                matches_21[i2] = i1;
+            } else {
+                continue;
+            }
+            if (d < best_d) {
+                best_d2 = best_d;
+                best_d = d;
+                best_idx = i2;
+            } else if (d < best_d2) {
+                best_d2 = d;
+            }
+        }
+        if (best_d < best_d2 * minRatio12L) {
+            matches_12[i1] = best_idx;
+            matches++;
+        }
+    }
+    for (int i1 = 0; i1 < n1; ++i1) {
+        int& i2 = matches_12[i1];
+        if (i2 >= 0 && matches_21[i2] != i1) {
+            i2 = -1;
+            matches--;
+        }
+    }
+    return matches;
 }

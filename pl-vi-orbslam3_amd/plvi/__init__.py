@@ -94,6 +94,8 @@ def _declare(lib):
         "plvi_descriptor_distance_batch": ([V, V, I, I, V, V], I),
         "plvi_search_by_bow": ([F, I, V, V, V, I, V, V, I, V, V, V, I, V, V, I, V, V], I),
         "plvi_search_by_bow_batch": ([I, F, I, I, I, I, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V], I),
+        "plvi_line_match_grid": ([V, V, I, I, I, V, V, V, V, I, I, I, I, I, I, V], I),
+        "plvi_line_match_grid_batch": ([I, V, V, V, I, I, I, V, V, I, V, V, V, I, I, I, I, I, I, V, V, V, V], I),
         "plvi_device_malloc": ([c_void_pp, S], I),
         "plvi_device_free": ([V], I),
         "plvi_memcpy": ([V, V, S, I], I),
@@ -377,6 +379,18 @@ def hamming_knn2(q, t):
     return tuple(out)
 
 
+def grid_csr(grid):
+    """GridStructure (grid[x][y] = list of indices) -> (cols, rows, cell_off, cell_idx)."""
+    cols, rows = len(grid), len(grid[0])
+    off = np.zeros(cols * rows + 1, np.int32)
+    idx = []
+    for x in range(cols):
+        for y in range(rows):
+            idx.extend(grid[x][y])
+            off[x * rows + y + 1] = len(idx)
+    return cols, rows, off, np.array(idx if idx else [0], np.int32)
+
+
 class LineMatcher:
     """ORB_SLAM3::LineMatcher static Hamming matchers (src/LineMatcher.cpp)."""
 
@@ -399,6 +413,24 @@ class LineMatcher:
         n = _check(lib.plvi_line_match(_ptr(d1), d1.shape[0], _ptr(d2), d2.shape[0], nnr, _ptr(m)),
                    "plvi_line_match")
         return n, m
+
+    @staticmethod
+    def matchGrid(lines1, desc1, grid, desc2, directions2, window=((7, 0), (2, 2)), range_hint=1):
+        """LineMatcher::matchGrid (src/LineMatcher.cpp:191-272).  lines1: n1 x 4 ints (line_2d grid coords),
+        grid: grid[x][y] lists of right-line indices, directions2: n2 x 2.  range_hint: 1 = libstdc++ <= GCC 10
+        candidate order (the reference's toolchain), 0 = GCC >= 11.  Returns (nmatches, matches_12)."""
+        lib = load()
+        l1 = np.ascontiguousarray(lines1, np.int32).reshape(-1, 4)
+        d1 = np.ascontiguousarray(desc1, np.uint8).reshape(-1, 32)
+        d2 = np.ascontiguousarray(desc2, np.uint8).reshape(-1, 32)
+        v2 = np.ascontiguousarray(directions2, np.float64).reshape(-1, 2)
+        cols, rows, off, idx = grid_csr(grid)
+        m = np.full(max(len(l1), 1), -1, np.int32)
+        (w0, w1), (h0, h1) = window
+        n = _check(lib.plvi_line_match_grid(_ptr(l1), _ptr(d1), len(l1), cols, rows, _ptr(off), _ptr(idx), _ptr(d2),
+                                            _ptr(v2), len(d2), w0, w1, h0, h1, int(range_hint), _ptr(m)),
+                   "plvi_line_match_grid")
+        return n, m[:len(l1)]
 
 
 def feature_vector_csr(fv):

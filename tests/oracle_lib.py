@@ -56,6 +56,8 @@ def load():
     lib.oracle_descriptor_distance.restype = I
     lib.oracle_line_descriptor_distance.argtypes = [V, V]
     lib.oracle_line_descriptor_distance.restype = I
+    lib.oracle_match_grid.argtypes = [V, V, I, I, I, V, V, V, V, I, I, I, I, I, V]
+    lib.oracle_match_grid.restype = I
     lib.oracle_fast_score.argtypes = [V, I]
     lib.oracle_fast_score.restype = I
     _lib = lib
@@ -230,3 +232,25 @@ def search_by_bow(kf_desc, kf_angle, kf_live, kf_fv, f_desc, f_angle, f_fv, nnra
     n = lib.oracle_search_by_bow(_p(kd), _p(ka), _p(kl), _p(kn), _p(ko), len(kn), _p(ki), _p(fd), _p(fa), len(fd),
                                  _p(fn), _p(fo), len(fn), _p(fi), float(nnratio), int(check_orientation), _p(out))
     return n, out[:len(fd)]
+
+
+def match_grid(lines1, desc1, grid, desc2, directions2, window=((7, 0), (2, 2))):
+    """LineMatcher::matchGrid restatement (real std::unordered_set of the host libstdc++)."""
+    lib = load()
+    cols, rows = len(grid), len(grid[0])
+    off = np.zeros(cols * rows + 1, np.int32)
+    idx = []
+    for x in range(cols):
+        for y in range(rows):
+            idx.extend(grid[x][y])
+            off[x * rows + y + 1] = len(idx)
+    idx = np.array(idx if idx else [0], np.int32)
+    l1 = np.ascontiguousarray(lines1, np.int32).reshape(-1, 4)
+    d1 = np.ascontiguousarray(desc1, np.uint8).reshape(-1, 32)
+    d2 = np.ascontiguousarray(desc2, np.uint8).reshape(-1, 32)
+    v2 = np.ascontiguousarray(directions2, np.float64).reshape(-1, 2)
+    m = np.full(max(len(l1), 1), -1, np.int32)
+    (w0, w1), (h0, h1) = window
+    n = lib.oracle_match_grid(_p(l1), _p(d1), len(l1), cols, rows, _p(off), _p(idx), _p(d2), _p(v2), len(d2),
+                              w0, w1, h0, h1, _p(m))
+    return n, m[:len(l1)]

@@ -56,3 +56,65 @@ def bow_case(seed, n_kf=1000, n_f=1000, n_nodes=100, zipf=1.2, live=0.7, dup=0.6
             d.setdefault(int(n), []).append(i)
         return d
     return kf_desc, kf_angle, kf_live, fv(kf_node), f_desc, f_angle, fv(f_node)
+
+
+def line_iterator(x1, y1, x2, y2):
+    """ORB_SLAM3::LineIterator (src/LineIterator.cpp:31-73): Bresenham on doubles."""
+    steep = abs(y2 - y1) > abs(x2 - x1)
+    if steep:
+        x1, y1, x2, y2 = y1, x1, y2, x2
+    if x1 > x2:
+        x1, x2, y1, y2 = x2, x1, y2, y1
+    dx, dy = x2 - x1, abs(y2 - y1)
+    error = dx / 2.0
+    ystep = 1 if y1 < y2 else -1
+    x, y, maxX = int(x1), int(y1), int(x2)
+    out = []
+    while x <= maxX:
+        out.append((y, x) if steep else (x, y))
+        error -= dy
+        if error < 0:
+            y += ystep
+            error += dx
+        x += 1
+    return out
+
+
+def stereo_line_case(seed, n=220, W=640, H=480, cols=64, rows=48, ties=True):
+    """Synthetic stereo line set shaped like Frame::ComputeStereoMatches_Lines
+    (src/Frame.cc:1408-1451): right lines rasterised into the 64x48 grid with
+    LineIterator, normalised directions, left lines = right lines shifted by a
+    disparity with noisy descriptors.  Returns (lines1 int n1x4, desc1, grid,
+    desc2, directions2)."""
+    rng = np.random.default_rng(seed)
+    inv_w, inv_h = cols / W, rows / H
+    sp = np.stack([rng.uniform(0, W - 1, n), rng.uniform(0, H - 1, n)], 1)
+    ang = rng.uniform(0, np.pi, n)
+    ln = rng.uniform(5, 160, n)
+    ep = np.clip(sp + np.stack([np.cos(ang), np.sin(ang)], 1) * ln[:, None], 0, [W - 1, H - 1])
+    desc2 = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    if ties:  # duplicated right lines/descriptors produce distance ties
+        k = n // 10
+        desc2[-k:] = desc2[:k]
+        sp[-k:] = sp[:k] + rng.normal(0, 2, (k, 2))
+        ep[-k:] = ep[:k] + rng.normal(0, 2, (k, 2))
+    grid = [[[] for _ in range(rows)] for _ in range(cols)]
+    dirs = np.zeros((n, 2))
+    for i in range(n):
+        v = ((ep[i, 0] - sp[i, 0]) * inv_w, (ep[i, 1] - sp[i, 1]) * inv_h)
+        m = np.sqrt(v[0] * v[0] + v[1] * v[1])
+        dirs[i] = (v[0] / m, v[1] / m)
+        for (x, y) in line_iterator(sp[i, 0] * inv_w, sp[i, 1] * inv_h, ep[i, 0] * inv_w, ep[i, 1] * inv_h):
+            if 0 <= x < cols and 0 <= y < rows:
+                grid[x][y].append(i)
+    n1 = int(n * 0.9)
+    src = rng.permutation(n)[:n1]
+    disp = rng.uniform(2, 40, n1)
+    s1 = sp[src] + np.stack([disp, np.zeros(n1)], 1)
+    e1 = ep[src] + np.stack([disp, np.zeros(n1)], 1)
+    bits = np.unpackbits(desc2[src], axis=1)
+    bits ^= (rng.random(bits.shape) < 0.1).astype(np.uint8)
+    desc1 = np.packbits(bits, axis=1)
+    lines1 = np.stack([(s1[:, 0] * inv_w).astype(np.int64), (s1[:, 1] * inv_h).astype(np.int64),
+                       (e1[:, 0] * inv_w).astype(np.int64), (e1[:, 1] * inv_h).astype(np.int64)], 1).astype(np.int32)
+    return lines1, desc1, grid, desc2, dirs
