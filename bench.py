@@ -90,22 +90,20 @@ def main():
     args = ap.parse_args()
 
     import torch
-    import torch.distributed as dist
     import plvi
+    from plvi import dist as pdist
     from plvi import synth
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = pdist.env()
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        pdist.init("nccl", torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
 
     B, W, H = args.batch, 640, 480
-    frames = torch.from_numpy(synth.batch(B, W, H, seed0=1_000_000 * rank)).to(f"cuda:{dev}")
+    frames = torch.from_numpy(synth.batch(B, W, H, seed0=pdist.shard_seed(rank))).to(f"cuda:{dev}")
     orb = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=B, device=dev)
     lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=B, device=dev)
     kp_p, de_p, co_p, mo_p, cap = orb.outputs()
@@ -173,20 +171,14 @@ def main():
     stage_ms.update({f"lines.{k}": v / lruns for k, v in st_lines.items()})
     stage_ms["match"] = match_ms / nprof
 
-    if world > 1:
-        dist.barrier()
+    pdist.barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{dev}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    pdist.barrier(world)
+    el = pdist.max_over_ranks(time.perf_counter() - t0, world, f"cuda:{dev}")
 
     frames_total = B * args.steps * world
     value = frames_total / el
@@ -219,6 +211,7 @@ def main():
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
+        import torch.distributed as dist
         dist.destroy_process_group()
 
 

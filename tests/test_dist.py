@@ -1,0 +1,48 @@
+"""Multi-process path of the bench (plvi.dist) with the gloo backend on CPU,
+world size 2: rank-sharded frame sequences (no data-path collective), the
+max-over-ranks wall time and the whole-job frame count."""
+import os
+import socket
+
+import numpy as np
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    from plvi import dist as pdist
+    from plvi import synth
+    w, r, _ = pdist.env()
+    pdist.init("gloo")
+    frames = synth.batch(2, 64, 48, seed0=pdist.shard_seed(r))
+    pdist.barrier(w)
+    el = pdist.max_over_ranks(0.5 + r, w)
+    total = pdist.sum_over_ranks(frames.shape[0], w)
+    q.put((r, el, total, int(frames.astype(np.int64).sum())))
+    import torch.distributed as dist
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_sharding_and_max_time():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [o[1] for o in out] == [1.5, 1.5]       # slowest rank's time on every rank
+    assert [o[2] for o in out] == [4, 4]           # whole-job frame count
+    assert out[0][3] != out[1][3]                  # each rank owns different frames
