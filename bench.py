@@ -1,9 +1,10 @@
 """bench.py — throughput of the MI355X feature front end (BASELINE.json metric).
 
-A step = one pass of the hot path over one batch of B=64 synthetic 640x480
-frames already resident in HBM:
-  ORB extract (ORBextractor 1000/1.2/8/20/7) on HIP stream A, concurrently
-  LSD + LBD line extract (Lineextractor 200/0/0.8/2/2.0) on HIP stream B,
+A step = one pass of the hot path over one batch of B synthetic 640x480
+frames already resident in HBM (default B=1024 frames in flight per GPU):
+  ORB extract (ORBextractor 1000/1.2/8/20/7) and LSD + LBD line extract
+  (Lineextractor 200/0/0.8/2/2.0) as one schedule (plvi_frame_extract_batch:
+  region growing concurrent with the ORB pipeline and the LBD Sobel pyramid),
   then matching of every frame against the previous one (B-1 pairs):
   ORB Hamming kNN-2 (~1000x1000) and LineMatcher::match (kNN-2 both ways,
   ratio 0.9, mutual check).
@@ -85,7 +86,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=512)
+    ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -114,16 +115,10 @@ def main():
     lscratch = torch.empty(4 * (B - 1) * 2 * lcap, **i32)
     lm12 = torch.empty((B - 1) * lcap, **i32)
     lnm = torch.empty(B - 1, **i32)
-    # two non-default streams: the legacy null stream would serialise with both
-    sA = torch.cuda.Stream()
-    sB = torch.cuda.Stream()
-    evA, evB = torch.cuda.Event(), torch.cuda.Event()
+    sA = torch.cuda.Stream()  # non-default: the legacy null stream would serialise
 
     def run_orb():
         orb.extract_batch(frames.data_ptr(), B, W * H, W, (0, 0), stream=sA.cuda_stream)
-
-    def run_lines():
-        lx.extract_batch(frames.data_ptr(), B, W * H, W, stream=sB.cuda_stream)
 
     def run_match():
         rc = lib.plvi_hamming_knn2_batch(de_p + cap * 32, co_p + 4, cap, de_p, co_p, cap, B - 1,
@@ -134,12 +129,9 @@ def main():
             raise RuntimeError(f"match {rc}")
 
     def step():
-        evA.record(sA)
-        sB.wait_event(evA)       # lines start after the previous step's matching (buffer reuse)
-        run_lines()
-        run_orb()
-        evB.record(sB)
-        sA.wait_event(evB)
+        # Frame::Frame: ORB || lines as one schedule (region growing overlapped
+        # with the ORB pipeline and the LBD Sobel pyramid), then matching
+        plvi.frame_extract_batch(orb, lx, frames.data_ptr(), B, W * H, W, (0, 0), stream=sA.cuda_stream)
         run_match()
 
     for _ in range(args.warmup):
@@ -156,7 +148,7 @@ def main():
     for _ in range(nprof):
         run_orb()
         torch.cuda.synchronize()
-        run_lines()
+        lx.extract_batch(frames.data_ptr(), B, W * H, W, stream=sA.cuda_stream)
         torch.cuda.synchronize()
         ev0.record(sA)
         run_match()

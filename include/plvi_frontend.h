@@ -260,6 +260,16 @@ int plvi_line_match_grid_batch(int n_pairs, const int* d_lines1, const uint8_t* 
                                int cap2, int win_w0, int win_w1, int win_h0, int win_h1, int libstdcxx_range_hint,
                                int* d_matches_12, int* d_nmatches, int* d_err, void* stream);
 
+/* ------------------------------------------------------------ Frame level
+ * Frame::Frame's extraction (src/Frame.cc:537-641, ExtractORB/ExtractLine
+ * :677-692): the ORB and line extractors on the same batch of frames, run
+ * as one schedule (LSD prep, then region growing concurrent with the ORB
+ * pipeline and the LBD Sobel pyramid on the handles' own streams).
+ * Asynchronous with respect to `stream`, which it joins at the end; the
+ * results are read with plvi_orb_outputs / plvi_lines_outputs. */
+int plvi_frame_extract_batch(plvi_orb_extractor* orb, plvi_line_extractor* lines, const uint8_t* d_frames,
+                             int n_frames, size_t frame_stride, size_t row_stride, int lap0, int lap1, void* stream);
+
 /* Device memory helpers for bindings that have no HIP runtime of their own
  * (ctypes, JNI): thin wrappers over hipMalloc/hipFree/hipMemcpy on the
  * current device.  kind: 1 = host->device, 2 = device->host, 3 = d->d. */

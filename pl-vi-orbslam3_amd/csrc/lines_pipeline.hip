@@ -44,6 +44,8 @@ struct LinePipeline {
     plvi_line_params prm{};
     int W = 0, H = 0, Bcap = 0, device = 0, nOct = 0, fcap = 0;
     hipStream_t stream = nullptr;
+    hipStream_t aux[2] = {nullptr, nullptr};  // frame mode: ORB and LBD-Sobel streams
+    hipEvent_t evFork = nullptr, evPrep = nullptr, evSobel = nullptr, evOrb = nullptr;
     std::vector<LineOctDev> oct;
     std::vector<float> scaleF, invScaleF;
     double SCALE = 0.8, prec = 0, rho = 0, min_length = 0;
@@ -59,6 +61,10 @@ struct LinePipeline {
 
     ~LinePipeline() {
         for (auto e : evs) (void)hipEventDestroy(e);
+        for (auto e : {evFork, evPrep, evSobel, evOrb})
+            if (e) (void)hipEventDestroy(e);
+        for (auto a : aux)
+            if (a) (void)hipStreamDestroy(a);
         if (stream) (void)hipStreamDestroy(stream);
     }
 
@@ -70,6 +76,9 @@ struct LinePipeline {
         W = width; H = height; Bcap = max_batch; device = dev; nOct = p->nlevels;
         PLVI_CHECK(hipSetDevice(device));
         PLVI_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        for (auto& a : aux) PLVI_CHECK(hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
+        for (auto* e : {&evFork, &evPrep, &evSobel, &evOrb})
+            PLVI_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         fcap = p->nfeatures > 0 ? p->nfeatures : kKlCap;
         SCALE = (double)p->lsd_scale;  // LSDOptions::scale is float
         if (!(SCALE > 0) || SCALE > 1) return PLVI_E_BADARG;
@@ -193,17 +202,19 @@ struct LinePipeline {
             return PLVI_E_HIP;
         PLVI_CHECK(hipMemset(err.p, 0, sizeof(int)));
         // region-growing LDS: rect staging + R-row USED/angle window + queue,
-        // sized so that several waves share a CU (PLVI_GROW_LDS, default 40 KB)
+        // sized so that several waves share a CU and leave LDS to the kernels that
+        // run concurrently (PLVI_GROW_LDS, default 12 KB: R = 4 rows)
         size_t maxSw = 0;
         for (auto& d : oct) maxSw = std::max(maxSw, (size_t)d.sw);
-        size_t budget = 40 * 1024;
+        size_t budget = 12 * 1024;
         if (const char* e = getenv("PLVI_GROW_LDS")) budget = (size_t)atol(e);
         budget = std::min<size_t>(budget, 160 * 1024);
         growQL = budget >= 32 * 1024 ? 1024 : 256;
         const size_t fixed = 64 * 3 * sizeof(double) + (size_t)growQL * sizeof(unsigned);
         const size_t perRow = maxSw * sizeof(float) + (maxSw + 31) / 32 * sizeof(unsigned);
         growR = 4;
-        if (fixed + perRow * 4 > budget) return PLVI_E_BADARG;
+        budget = std::max(budget, fixed + perRow * 4);  // at least a 4-row window (wide frames)
+        if (budget > 160 * 1024) return PLVI_E_BADARG;
         while (growR * 2 <= 1024 && fixed + perRow * growR * 2 <= budget) growR *= 2;
         growSmem = fixed + perRow * growR;
         PLVI_CHECK(hipFuncSetAttribute((const void*)lsd_grow_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -241,13 +252,9 @@ struct LinePipeline {
         return PLVI_OK;
     }
 
-    int run(const uint8_t* d_frames, int nf, size_t frame_stride, size_t row_stride, hipStream_t st) {
-        if (nf <= 0 || nf > Bcap) return PLVI_E_BADARG;
-        if (!st) st = stream;
-        lastFrames = nf;
+    // Phase A: octave pyramid + LSD prep (LK1, LK2).
+    void launch_prep(const uint8_t* d_frames, int nf, size_t frame_stride, size_t row_stride, hipStream_t st) {
         const uint8_t* T = d_tabs.as<uint8_t>();
-        mark(0, st);
-        // LK1: octave pyramid
         for (int l = 1; l < nOct; ++l) {
             const LineOctDev& d = oct[l];
             const uint8_t* s = l == 1 ? d_frames : octImg.as<uint8_t>() + oct[l - 1].off;
@@ -257,7 +264,6 @@ struct LinePipeline {
                                octImg.as<uint8_t>() + d.off, d.w, d.h, (size_t)d.plane);
         }
         mark(1, st);
-        // LK2: LSD prep per octave
         for (int l = 0; l < nOct; ++l) {
             const LineOctDev& d = oct[l];
             const uint8_t* s = l == 0 ? d_frames : octImg.as<uint8_t>() + d.off;
@@ -271,44 +277,92 @@ struct LinePipeline {
                                seedcs.as<float2>() + d.soff, (size_t)d.splane, err.as<int>());
         }
         mark(2, st);
-        // LK3: region growing (one wave per octave x frame)
+    }
+
+    // Phase B: region growing (LK3) + keyline assembly / top-k (LK4).
+    void launch_grow_assemble(int nf, hipStream_t st) {
         hipLaunchKernelGGL(lsd_grow_kernel, dim3(nOct, nf), dim3(64), growSmem, st, d_oct.as<LineOctDev>(),
                            (const float*)pix.as<float>(), (const double*)modg.as<double>(),
                            (const float2*)seedcs.as<float2>(), gbits.as<unsigned>(), gbitsFrame, qspill.as<unsigned>(),
                            qspillFrame, prec, SCALE, rawLines.as<LsdLine>(), nlines.as<int>(), err.as<int>(), growR,
                            growQL, growStats);
         mark(3, st);
-        // LK4: keyline assembly + top-k + line equations
         hipLaunchKernelGGL(line_assemble_kernel, dim3(nf), dim3(256), 0, st, d_oct.as<LineOctDev>(), nOct,
                            (const LsdLine*)rawLines.as<LsdLine>(), (const int*)nlines.as<int>(), min_length,
                            prm.nfeatures, fcap, klOut.as<plvi_keyline>(), fnOut.as<double>(), cntOut.as<int>(),
                            klTmp.as<plvi_keyline>(), err.as<int>());
         mark(4, st);
-        // LB1/LB2: LBD Gaussian pyramid + Sobel
-        {
-            const LineOctDev& d0 = oct[0];
-            dim3 g0((d0.lw + kBTW - 1) / kBTW, (d0.lh + kBTH - 1) / kBTH, nf);
-            hipLaunchKernelGGL(lbd_blur_sobel_kernel, g0, dim3(256), 0, st, d_frames, frame_stride, row_stride, d0.lw,
-                               d0.lh, lbdBlur.as<uint8_t>(), lbdDx.as<int16_t>() + d0.loff,
-                               lbdDy.as<int16_t>() + d0.loff, (size_t)d0.lplane);
-            for (int l = 1; l < nOct; ++l) {
-                const LineOctDev& d = oct[l];
-                if (l > 1) return PLVI_E_BADARG;  // pyrDown chain beyond octave 1 not wired (config: 2 levels)
-                dim3 g1((d.lw + kBTW - 1) / kBTW, (d.lh + kBTH - 1) / kBTH, nf);
-                hipLaunchKernelGGL(lbd_pyrdown_sobel_kernel, g1, dim3(256), 0, st, (const uint8_t*)lbdBlur.as<uint8_t>(),
-                                   d0.lw, d0.lh, (size_t)d0.lplane, d.lw, d.lh, lbdDx.as<int16_t>() + d.loff,
-                                   lbdDy.as<int16_t>() + d.loff, (size_t)d.lplane);
-            }
+    }
+
+    // LB1/LB2: LBD Gaussian pyramid + Sobel (depends on the frames only).
+    int launch_sobel(const uint8_t* d_frames, int nf, size_t frame_stride, size_t row_stride, hipStream_t st) {
+        const LineOctDev& d0 = oct[0];
+        dim3 g0((d0.lw + kBTW - 1) / kBTW, (d0.lh + kBTH - 1) / kBTH, nf);
+        hipLaunchKernelGGL(lbd_blur_sobel_kernel, g0, dim3(256), 0, st, d_frames, frame_stride, row_stride, d0.lw,
+                           d0.lh, lbdBlur.as<uint8_t>(), lbdDx.as<int16_t>() + d0.loff, lbdDy.as<int16_t>() + d0.loff,
+                           (size_t)d0.lplane);
+        for (int l = 1; l < nOct; ++l) {
+            const LineOctDev& d = oct[l];
+            if (l > 1) return PLVI_E_BADARG;  // pyrDown chain beyond octave 1 not wired (config: 2 levels)
+            dim3 g1((d.lw + kBTW - 1) / kBTW, (d.lh + kBTH - 1) / kBTH, nf);
+            hipLaunchKernelGGL(lbd_pyrdown_sobel_kernel, g1, dim3(256), 0, st, (const uint8_t*)lbdBlur.as<uint8_t>(),
+                               d0.lw, d0.lh, (size_t)d0.lplane, d.lw, d.lh, lbdDx.as<int16_t>() + d.loff,
+                               lbdDy.as<int16_t>() + d.loff, (size_t)d.lplane);
         }
-        // LB3: LBD descriptors
+        return PLVI_OK;
+    }
+
+    // LB3: LBD descriptors of the assembled keylines.
+    void launch_describe(int nf, hipStream_t st) {
         hipLaunchKernelGGL(lbd_describe_kernel, dim3(fcap, nf), dim3(64), 0, st, d_oct.as<LineOctDev>(),
                            (const int16_t*)lbdDx.as<int16_t>(), (const int16_t*)lbdDy.as<int16_t>(),
                            (const plvi_keyline*)klOut.as<plvi_keyline>(), (const int*)cntOut.as<int>(), fcap,
                            descOut.as<uint8_t>());
         mark(5, st);
+    }
+
+    int run(const uint8_t* d_frames, int nf, size_t frame_stride, size_t row_stride, hipStream_t st) {
+        if (nf <= 0 || nf > Bcap) return PLVI_E_BADARG;
+        if (!st) st = stream;
+        lastFrames = nf;
+        mark(0, st);
+        launch_prep(d_frames, nf, frame_stride, row_stride, st);
+        launch_grow_assemble(nf, st);
+        int rc = launch_sobel(d_frames, nf, frame_stride, row_stride, st);
+        if (rc) return rc;
+        launch_describe(nf, st);
         if (prof && profRuns < kRing) ++profRuns;
         PLVI_CHECK(hipGetLastError());
         return PLVI_OK;
+    }
+
+    // Frame::Frame's two extractor threads (Frame.cc:558-561) as one
+    // schedule: the latency-bound region growing runs while the ORB
+    // extractor and the LBD Sobel pyramid fill the machine on two more
+    // streams; everything joins back on `st`.
+    int run_with_orb(const uint8_t* d_frames, int nf, size_t frame_stride, size_t row_stride, hipStream_t st,
+                     plvi_orb_extractor* orb, int lap0, int lap1) {
+        if (nf <= 0 || nf > Bcap) return PLVI_E_BADARG;
+        if (!st) st = stream;
+        lastFrames = nf;
+        const bool p0 = prof;
+        prof = false;  // stage events are meaningless across streams
+        PLVI_CHECK(hipEventRecord(evFork, st));
+        launch_prep(d_frames, nf, frame_stride, row_stride, st);
+        PLVI_CHECK(hipEventRecord(evPrep, st));
+        PLVI_CHECK(hipStreamWaitEvent(aux[0], evPrep, 0));
+        int rc = plvi_orb_extract_batch(orb, d_frames, nf, frame_stride, row_stride, lap0, lap1, aux[0]);
+        PLVI_CHECK(hipEventRecord(evOrb, aux[0]));
+        PLVI_CHECK(hipStreamWaitEvent(aux[1], evPrep, 0));
+        if (!rc) rc = launch_sobel(d_frames, nf, frame_stride, row_stride, aux[1]);
+        PLVI_CHECK(hipEventRecord(evSobel, aux[1]));
+        launch_grow_assemble(nf, st);
+        PLVI_CHECK(hipStreamWaitEvent(st, evSobel, 0));
+        launch_describe(nf, st);
+        PLVI_CHECK(hipStreamWaitEvent(st, evOrb, 0));
+        prof = p0;
+        PLVI_CHECK(hipGetLastError());
+        return rc;
     }
 };
 
@@ -344,6 +398,14 @@ extern "C" int plvi_lines_extract_batch(plvi_line_extractor* h, const uint8_t* d
     if (!h || !d_frames) return PLVI_E_BADARG;
     PLVI_CHECK(hipSetDevice(h->p.device));
     return h->p.run(d_frames, n_frames, frame_stride, row_stride, (hipStream_t)stream);
+}
+
+extern "C" int plvi_frame_extract_batch(plvi_orb_extractor* orb, plvi_line_extractor* lines, const uint8_t* d_frames,
+                                        int n_frames, size_t frame_stride, size_t row_stride, int lap0, int lap1,
+                                        void* stream) {
+    if (!orb || !lines || !d_frames) return PLVI_E_BADARG;
+    PLVI_CHECK(hipSetDevice(lines->p.device));
+    return lines->p.run_with_orb(d_frames, n_frames, frame_stride, row_stride, (hipStream_t)stream, orb, lap0, lap1);
 }
 
 extern "C" int plvi_lines_outputs(plvi_line_extractor* h, plvi_keyline** d_kl, uint8_t** d_desc, double** d_fn,

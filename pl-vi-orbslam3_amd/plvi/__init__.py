@@ -96,6 +96,7 @@ def _declare(lib):
         "plvi_search_by_bow_batch": ([I, F, I, I, I, I, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V], I),
         "plvi_line_match_grid": ([V, V, I, I, I, V, V, V, V, I, I, I, I, I, I, V], I),
         "plvi_line_match_grid_batch": ([I, V, V, V, I, I, I, V, V, I, V, V, V, I, I, I, I, I, I, V, V, V, V], I),
+        "plvi_frame_extract_batch": ([V, V, V, I, S, S, I, I, V], I),
         "plvi_device_malloc": ([c_void_pp, S], I),
         "plvi_device_free": ([V], I),
         "plvi_memcpy": ([V, V, S, I], I),
@@ -485,3 +486,11 @@ class ORBmatcher:
                "plvi_descriptor_distance_batch")
         lib.plvi_device_synchronize()
         return do.download(np.zeros(n, np.int32))
+
+
+def frame_extract_batch(orb, lines, d_frames_ptr, n_frames, frame_stride, row_stride, lap=(0, 0), stream=None):
+    """Frame::Frame's ORB + line extraction of a device batch as one schedule
+    (plvi_frame_extract_batch); results via orb.outputs() / lines.outputs()."""
+    _check(load().plvi_frame_extract_batch(orb._h, lines._h, ctypes.c_void_p(d_frames_ptr), n_frames, frame_stride,
+                                           row_stride, lap[0], lap[1], ctypes.c_void_p(stream or 0)),
+           "plvi_frame_extract_batch")

@@ -1,0 +1,50 @@
+"""plvi_frame_extract_batch (Frame::Frame's ORB + line extraction as one
+multi-stream schedule, src/Frame.cc:537-692) gives exactly the results of
+the two extractors run on their own, which the other GPU tests pin to the
+oracle; spot-checked against the oracle too."""
+import numpy as np
+import pytest
+
+import oracle_lib as ol
+import plvi
+from plvi import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _orb_out(orb, n):
+    kp, de, co, mo, cap = orb.outputs()
+    cnt = plvi.download(co, np.zeros(n, np.int32))
+    return cnt, plvi.download(kp, np.zeros(n * cap, plvi.KEYPOINT_DTYPE)), \
+        plvi.download(de, np.zeros((n * cap, 32), np.uint8)), cap
+
+
+def _line_out(lx, n):
+    kl, de, fn, co, cap = lx.outputs()
+    cnt = plvi.download(co, np.zeros(n, np.int32))
+    return cnt, plvi.download(kl, np.zeros(n * cap, plvi.KEYLINE_DTYPE)), \
+        plvi.download(de, np.zeros((n * cap, 32), np.uint8)), cap
+
+
+def test_frame_extract_equals_separate_extractors():
+    n = 6
+    frames = synth.batch(n, seed0=77)
+    buf = plvi.DeviceBuffer(frames.nbytes)
+    buf.upload(frames)
+    lib = plvi.load()
+    orb = plvi.ORBextractor(1000, 1.2, 8, 20, 7, 640, 480, max_batch=n)
+    lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 640, 480, max_batch=n)
+    orb.extract_batch(buf.ptr, n, 640 * 480, 640)
+    lx.extract_batch(buf.ptr, n, 640 * 480, 640)
+    lib.plvi_device_synchronize()
+    ref_o, ref_l = _orb_out(orb, n), _line_out(lx, n)
+    plvi.frame_extract_batch(orb, lx, buf.ptr, n, 640 * 480, 640)
+    lib.plvi_device_synchronize()
+    got_o, got_l = _orb_out(orb, n), _line_out(lx, n)
+    for a, b in zip(ref_o[:3] + ref_l[:3], got_o[:3] + got_l[:3]):
+        np.testing.assert_array_equal(a.view(np.uint8), b.view(np.uint8))
+    # and frame 0 against the oracle
+    cnt, kps, desc, cap = got_o
+    mono, okps, odesc = ol.orb_extract(frames[0])
+    assert cnt[0] == len(okps)
+    np.testing.assert_array_equal(desc[:cnt[0]], odesc)
