@@ -88,6 +88,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-bow", action="store_true", help="skip the DBoW2 transform stage timing")
     args = ap.parse_args()
 
     import torch
@@ -159,9 +160,37 @@ def main():
     st_lines, lruns = lx.profile_read()
     orb.profile(False)
     lx.profile(False)
+    # DBoW2 transform (Frame::ComputeBoW) of the batch's ORB
+    # descriptors on a k=10, L=6 synthetic vocabulary (ORBvoc.txt's shape);
+    # timed separately: the reference runs it for keyframes / relocalisation,
+    # not inside the per-frame extract+match step.
+    bow_ms = None
+    if not args.no_bow:
+        pv = synth.vocabulary(10, 6, seed=1)
+        voc = plvi.ORBVocabulary.from_nodes(10, 6, 0, 0, *pv, device=dev)
+        bo = {k: torch.empty(B * (cap + 1) * sz, dtype=torch.uint8, device=f"cuda:{dev}")
+              for k, sz in (("bw", 4), ("bv", 8), ("bn", 4), ("fn", 4), ("fo", 4), ("fi", 4), ("fc", 4))}
+
+        def run_bow():
+            rc = lib.plvi_vocab_transform_batch(voc._h, de_p, co_p, cap, B, 4, *[bo[k].data_ptr() for k in
+                                                ("bw", "bv", "bn", "fn", "fo", "fi", "fc")], None, None,
+                                                sA.cuda_stream)
+            if rc:
+                raise RuntimeError(f"bow {rc}")
+        run_orb()
+        run_bow()
+        torch.cuda.synchronize()
+        ev0.record(sA)
+        for _ in range(nprof):
+            run_bow()
+        ev1.record(sA)
+        torch.cuda.synchronize()
+        bow_ms = ev0.elapsed_time(ev1) / nprof
     stage_ms = {f"orb.{k}": v / runs for k, v in st_orb.items()}
     stage_ms.update({f"lines.{k}": v / lruns for k, v in st_lines.items()})
     stage_ms["match"] = match_ms / nprof
+    if bow_ms is not None:
+        stage_ms["bow.transform"] = bow_ms
 
     pdist.barrier(world)
     torch.cuda.synchronize()
@@ -179,7 +208,7 @@ def main():
     # roofline: dominant stage
     lvl_bytes = level_stage_bytes(W, H) * B
     knn_ops = (B - 1) * 1000 * 1000 * 16  # 8 x (xor + popcount) per descriptor pair
-    dom = max(stage_ms, key=stage_ms.get)
+    dom = max((k for k in stage_ms if k != "bow.transform"), key=stage_ms.get)
     roof = {
         "bound": "hbm", "kernel": "orb_level_kernel (resize+blur7x7+FAST score, all 8 levels)",
         "achieved": lvl_bytes / (stage_ms["orb.level"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",

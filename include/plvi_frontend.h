@@ -1,9 +1,10 @@
 /* plvi_frontend.h — C-ABI of the MI355X-native PL-VI-ORBSLAM3 feature front end.
  *
  * Plain pointers and sizes only.  Each entry point replaces one reference
- * interface (cited per function); the C++ drop-in classes in
- * pl-vi-orbslam3_amd/host/ (ORBextractor, Lineextractor, ORBmatcher,
- * LineMatcher) are thin wrappers over these calls, see INTEGRATION.md.
+ * interface (cited per function); INTEGRATION.md gives the C++ shim bodies
+ * a maintainer drops into the reference classes (ORBextractor,
+ * Lineextractor, ORBmatcher, LineMatcher, ORBVocabulary), and
+ * pl-vi-orbslam3_amd/plvi/ is the Python (ctypes) mirror.
  *
  * Status codes: 0 = ok, negative = error (PLVI_E_*).  ORBextractor's
  * "empty image -> -1" convention (src/ORBextractor.cc:1072-1073) is kept by
@@ -259,6 +260,54 @@ int plvi_line_match_grid_batch(int n_pairs, const int* d_lines1, const uint8_t* 
                                int idx_cap, const uint8_t* d_desc2, const double* d_directions2, const int* d_n2,
                                int cap2, int win_w0, int win_w1, int win_h0, int win_h1, int libstdcxx_range_hint,
                                int* d_matches_12, int* d_nmatches, int* d_err, void* stream);
+
+/* ------------------------------------------------------------- Vocabulary
+ * DBoW2::TemplatedVocabulary<FORB::TDescriptor, FORB>
+ * (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h), the ORB vocabulary of
+ * Frame::ComputeBoW (src/Frame.cc:1115-1122) and KeyFrame::ComputeBoW
+ * (src/KeyFrame.cc:111).  Node ids and word ids follow the reference's
+ * loader (node i = i-th line after the header, word ids in leaf order). */
+typedef struct plvi_vocabulary plvi_vocabulary;
+
+/* loadFromTextFile (TemplatedVocabulary.h:1338-1424; System.cc:84).
+ * emulate_tail != 0 reproduces the loader's extra node read from the empty
+ * tail after the file's final newline (a weight-0 leaf child of the root,
+ * descriptor zero here, uninitialised in the reference). */
+int plvi_vocab_load_text(const char* path, int emulate_tail, int device, plvi_vocabulary** out);
+
+/* Build from a node table (row i = node i+1 in file order; parent[i] < i+1):
+ * the structure loadFromTextFile would produce from the same lines. */
+int plvi_vocab_create(int k, int L, int scoring, int weighting, int n_nodes, const int* parent,
+                      const uint8_t* is_leaf, const uint8_t* desc, const double* weight, int device,
+                      plvi_vocabulary** out);
+int plvi_vocab_destroy(plvi_vocabulary* h);
+
+/* info[6] = k, L, scoring, weighting, node count (incl. root), word count. */
+int plvi_vocab_info(plvi_vocabulary* h, int* info);
+
+/* transform(features, BowVector&, FeatureVector&, levelsup)
+ * (TemplatedVocabulary.h:1126-1194) for one frame from host memory:
+ * BowVector (std::map<WordId, WordValue>) as bow_word/bow_value in map order,
+ * FeatureVector (std::map<NodeId, vector<unsigned>>) as CSR fv_node[i],
+ * fv_idx[fv_off[i] .. fv_off[i+1]) in map order.  Arrays hold n entries
+ * (fv_off n + 1). */
+int plvi_vocab_transform(plvi_vocabulary* h, const uint8_t* desc, int n, int levelsup, unsigned* bow_word,
+                         double* bow_value, int* bow_n, unsigned* fv_node, int* fv_off, unsigned* fv_idx,
+                         int* fv_n);
+
+/* Per-descriptor descent (transform(feature, word_id, weight, &nid, levelsup),
+ * :1217-1259): word id and the node at level L - levelsup. */
+int plvi_vocab_transform_features(plvi_vocabulary* h, const uint8_t* desc, int n, int levelsup, unsigned* word,
+                                  unsigned* nid);
+
+/* Batched device variant over n_frames descriptor tables [n_frames][cap][32]
+ * with counts d_count (e.g. plvi_orb_outputs): outputs [n_frames][cap]
+ * (fv_off [n_frames][cap+1]) and per-frame counts.  d_feat_word/d_feat_nid
+ * (nullable) receive the per-descriptor descent.  Asynchronous. */
+int plvi_vocab_transform_batch(plvi_vocabulary* h, const uint8_t* d_desc, const int* d_count, int cap, int n_frames,
+                               int levelsup, unsigned* d_bow_word, double* d_bow_value, int* d_bow_n,
+                               unsigned* d_fv_node, int* d_fv_off, unsigned* d_fv_idx, int* d_fv_n,
+                               unsigned* d_feat_word, unsigned* d_feat_nid, void* stream);
 
 /* ------------------------------------------------------------ Frame level
  * Frame::Frame's extraction (src/Frame.cc:537-641, ExtractORB/ExtractLine

@@ -7,6 +7,8 @@ Class and method names follow the reference interfaces they replace:
   LineMatcher   -> ORB_SLAM3::LineMatcher  (include/LineMatcher.h:88-107)
   ORBmatcher    -> ORB_SLAM3::ORBmatcher   (include/ORBmatcher.h:39-68): SearchByBoW, DescriptorDistance
   hamming_knn2  -> cv::BFMatcher(NORM_HAMMING).knnMatch(k=2) (LineMatcher.cpp:47-48)
+  ORBVocabulary -> DBoW2::TemplatedVocabulary<FORB> (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h):
+                   loadFromTextFile, transform(features, BowVector&, FeatureVector&, levelsup)
 
 There is no CPU fallback: if the HIP library is missing or no GPU is
 visible, construction raises.  PyTorch is only used by bench.py for device
@@ -97,6 +99,13 @@ def _declare(lib):
         "plvi_line_match_grid": ([V, V, I, I, I, V, V, V, V, I, I, I, I, I, I, V], I),
         "plvi_line_match_grid_batch": ([I, V, V, V, I, I, I, V, V, I, V, V, V, I, I, I, I, I, I, V, V, V, V], I),
         "plvi_frame_extract_batch": ([V, V, V, I, S, S, I, I, V], I),
+        "plvi_vocab_load_text": ([ctypes.c_char_p, I, I, c_void_pp], I),
+        "plvi_vocab_create": ([I, I, I, I, I, V, V, V, V, I, c_void_pp], I),
+        "plvi_vocab_destroy": ([V], I),
+        "plvi_vocab_info": ([V, V], I),
+        "plvi_vocab_transform": ([V, V, I, I, V, V, P, V, V, V, P], I),
+        "plvi_vocab_transform_features": ([V, V, I, I, V, V], I),
+        "plvi_vocab_transform_batch": ([V, V, V, I, I, I, V, V, V, V, V, V, V, V, V, V], I),
         "plvi_device_malloc": ([c_void_pp, S], I),
         "plvi_device_free": ([V], I),
         "plvi_memcpy": ([V, V, S, I], I),
@@ -494,3 +503,82 @@ def frame_extract_batch(orb, lines, d_frames_ptr, n_frames, frame_stride, row_st
     _check(load().plvi_frame_extract_batch(orb._h, lines._h, ctypes.c_void_p(d_frames_ptr), n_frames, frame_stride,
                                            row_stride, lap[0], lap[1], ctypes.c_void_p(stream or 0)),
            "plvi_frame_extract_batch")
+
+
+class ORBVocabulary:
+    """DBoW2::TemplatedVocabulary<FORB::TDescriptor, FORB> (ORBVocabulary.h) on the GPU.
+
+    ``ORBVocabulary.loadFromTextFile(path)`` mirrors the reference loader
+    (TemplatedVocabulary.h:1338-1424); ``ORBVocabulary.from_nodes(...)`` builds
+    the same structure from a node table.  ``transform(desc, levelsup)``
+    returns ``(BowVector, FeatureVector)`` as dicts {word: value} and
+    {node: [feature indices]} in std::map (ascending key) order
+    (TemplatedVocabulary.h:1126-1194).
+    """
+
+    def __init__(self, handle):
+        self._lib = load()
+        self._h = handle
+        info = np.zeros(6, np.int32)
+        _check(self._lib.plvi_vocab_info(self._h, _ptr(info)), "plvi_vocab_info")
+        self.k, self.L, self.scoring, self.weighting, self.n_nodes, self.n_words = (int(x) for x in info)
+
+    @classmethod
+    def loadFromTextFile(cls, path, emulate_tail=True, device=0):
+        h = ctypes.c_void_p()
+        _check(load().plvi_vocab_load_text(str(path).encode(), int(emulate_tail), device, ctypes.byref(h)),
+               "plvi_vocab_load_text")
+        return cls(h)
+
+    @classmethod
+    def from_nodes(cls, k, L, scoring, weighting, parent, is_leaf, desc, weight, device=0):
+        parent = np.ascontiguousarray(parent, np.int32)
+        is_leaf = np.ascontiguousarray(is_leaf, np.uint8)
+        desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        weight = np.ascontiguousarray(weight, np.float64)
+        h = ctypes.c_void_p()
+        _check(load().plvi_vocab_create(k, L, scoring, weighting, len(parent), _ptr(parent), _ptr(is_leaf),
+                                        _ptr(desc), _ptr(weight), device, ctypes.byref(h)), "plvi_vocab_create")
+        return cls(h)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.plvi_vocab_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def empty(self):
+        return self.n_words == 0
+
+    def transform_arrays(self, desc, levelsup=4):
+        """Raw CSR form: (bow_word, bow_value, fv_node, fv_off, fv_idx)."""
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = d.shape[0]
+        m = max(n, 1)
+        bw, bv = np.zeros(m, np.uint32), np.zeros(m, np.float64)
+        fn, fo, fi = np.zeros(m, np.uint32), np.zeros(m + 1, np.int32), np.zeros(m, np.uint32)
+        nb, nf = ctypes.c_int(), ctypes.c_int()
+        _check(self._lib.plvi_vocab_transform(self._h, _ptr(d), n, levelsup, _ptr(bw), _ptr(bv), ctypes.byref(nb),
+                                              _ptr(fn), _ptr(fo), _ptr(fi), ctypes.byref(nf)), "plvi_vocab_transform")
+        nb, nf = nb.value, nf.value
+        return bw[:nb], bv[:nb], fn[:nf], fo[:nf + 1], fi[:fo[nf]]
+
+    def transform(self, desc, levelsup=4):
+        bw, bv, fn, fo, fi = self.transform_arrays(desc, levelsup)
+        bow = {int(w): float(v) for w, v in zip(bw, bv)}
+        fv = {int(fn[i]): [int(x) for x in fi[fo[i]:fo[i + 1]]] for i in range(len(fn))}
+        return bow, fv
+
+    def transform_features(self, desc, levelsup=4):
+        """Per-descriptor (word ids, node ids at level L - levelsup)."""
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = d.shape[0]
+        w, ni = np.zeros(max(n, 1), np.uint32), np.zeros(max(n, 1), np.uint32)
+        _check(self._lib.plvi_vocab_transform_features(self._h, _ptr(d), n, levelsup, _ptr(w), _ptr(ni)),
+               "plvi_vocab_transform_features")
+        return w[:n], ni[:n]

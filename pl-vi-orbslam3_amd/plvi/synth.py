@@ -107,3 +107,99 @@ def batch(n, w=640, h=480, seed0=0):
     for i in range(n):
         out[i] = frame(seed0 + i, w, h)
     return out
+
+
+# ---------------------------------------------------------------- vocabulary
+# Seeded synthetic DBoW2 ORB vocabulary in the reference's node-table form
+# (the real Vocabulary/ORBvoc.txt is a missing blob).
+# Children of a node are consecutive in file order, as the kmeans builder
+# creates them; descriptors of a child = its parent's with random bit flips,
+# so descending the tree is meaningful; leaves carry idf-like weights with
+# ~2 % stopped words (weight 0).
+
+def _flip_mask(rng, n, ands):
+    """n x 32 random bytes whose bits are set with probability 2^-ands."""
+    m = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    for _ in range(ands - 1):
+        m &= rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    return m
+
+
+def vocabulary(k=10, L=6, seed=0):
+    """Full k-ary tree of depth L in breadth-first file order.
+    Returns (parent, is_leaf, desc, weight) for nodes 1..n."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    parents, leaves, descs, weights = [], [], [], []
+    prev_ids = np.zeros(1, np.int64)
+    prev_desc = np.zeros((1, 32), np.uint8)
+    next_id = 1
+    for d in range(1, L + 1):
+        cnt = len(prev_ids) * k
+        par = np.repeat(prev_ids, k)
+        if d == 1:
+            de = rng.integers(0, 256, (cnt, 32), dtype=np.uint8)
+        else:
+            de = np.repeat(prev_desc, k, axis=0) ^ _flip_mask(rng, cnt, min(d, 5))
+        ids = np.arange(next_id, next_id + cnt, dtype=np.int64)
+        next_id += cnt
+        leaf = d == L
+        w = np.zeros(cnt)
+        if leaf:
+            w = rng.uniform(0.5, 9.0, cnt)
+            w[rng.uniform(size=cnt) < 0.02] = 0.0
+        parents.append(par)
+        leaves.append(np.full(cnt, leaf, np.uint8))
+        descs.append(de)
+        weights.append(w)
+        prev_ids, prev_desc = ids, de
+    return (np.concatenate(parents).astype(np.int32), np.concatenate(leaves), np.concatenate(descs),
+            np.concatenate(weights))
+
+
+def vocabulary_irregular(k=6, L=4, seed=0):
+    """Small irregular tree in the kmeans builder's file order (children of a
+    node consecutive, recursion depth first): branching 1..k, early leaves,
+    duplicate child descriptors (ties), stopped words."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    parent, leaf, desc, weight = [], [], [], []
+
+    def emit(pid, d, pdesc):
+        nc = int(rng.integers(1, k + 1))
+        first = len(parent) + 1
+        kids = []
+        for c in range(nc):
+            if d == 1:
+                de = rng.integers(0, 256, 32, dtype=np.uint8)
+            elif c > 0 and rng.uniform() < 0.1:
+                de = desc[kids[-1] - 1].copy()  # exact tie with the previous sibling
+            else:
+                de = pdesc ^ _flip_mask(rng, 1, 3)[0]
+            is_leaf = d == L or (d >= 2 and rng.uniform() < 0.15)
+            parent.append(pid)
+            leaf.append(1 if is_leaf else 0)
+            desc.append(de)
+            weight.append(0.0 if (not is_leaf or rng.uniform() < 0.05) else float(rng.uniform(0.1, 5.0)))
+            kids.append(first + c)
+        for c, nid in enumerate(kids):
+            if not leaf[nid - 1]:
+                emit(nid, d + 1, desc[nid - 1])
+
+    emit(0, 1, None)
+    return (np.array(parent, np.int32), np.array(leaf, np.uint8), np.array(desc, np.uint8).reshape(-1, 32),
+            np.array(weight, np.float64))
+
+
+def vocabulary_text(k, L, scoring, weighting, parent, is_leaf, desc, weight):
+    """saveToTextFile (TemplatedVocabulary.h:1429-1449) formatting."""
+    lines = [f"{k} {L}  {scoring} {weighting}"]
+    for p, lf, d, w in zip(parent, is_leaf, desc, weight):
+        lines.append(f"{int(p)} {int(lf)} " + " ".join(str(int(x)) for x in d) + f"  {w:.6g}")
+    return "\n".join(lines) + "\n"
+
+
+def vocab_features(parent, is_leaf, desc, n, seed=0, flips=3):
+    """n query descriptors near random leaves (bit flips with probability 2^-flips)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    leaves = np.nonzero(is_leaf)[0]
+    pick = rng.choice(leaves, n)
+    return desc[pick] ^ _flip_mask(rng, n, flips)

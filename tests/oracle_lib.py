@@ -254,3 +254,75 @@ def match_grid(lines1, desc1, grid, desc2, directions2, window=((7, 0), (2, 2)))
     n = lib.oracle_match_grid(_p(l1), _p(d1), len(l1), cols, rows, _p(off), _p(idx), _p(d2), _p(v2), len(d2),
                               w0, w1, h0, h1, _p(m))
     return n, m[:len(l1)]
+
+
+def _declare_vocab(lib):
+    V, I = ctypes.c_void_p, ctypes.c_int
+    lib.oracle_vocab_load.argtypes = [ctypes.c_char_p, I]
+    lib.oracle_vocab_load.restype = V
+    lib.oracle_vocab_create.argtypes = [I, I, I, I, I, V, V, V, V]
+    lib.oracle_vocab_create.restype = V
+    lib.oracle_vocab_free.argtypes = [V]
+    lib.oracle_vocab_info.argtypes = [V, V]
+    lib.oracle_vocab_nodes.argtypes = [V, V, V, V, V, V, V]
+    lib.oracle_vocab_transform.argtypes = [V, V, I, I, V, V, V, V, V, V, V, V, V, V]
+
+
+class Vocab:
+    """DBoW2 TemplatedVocabulary restatement (oracle/bow_oracle.cpp)."""
+
+    def __init__(self, handle):
+        self.lib = load()
+        _declare_vocab(self.lib)
+        if not handle:
+            raise ValueError("oracle vocabulary load failed")
+        self.h = handle
+        info = np.zeros(6, np.int32)
+        self.lib.oracle_vocab_info(self.h, _p(info))
+        self.k, self.L, self.scoring, self.weighting, self.n_nodes, self.n_words = (int(x) for x in info)
+
+    @classmethod
+    def load_text(cls, path, emulate_tail=True):
+        lib = load()
+        _declare_vocab(lib)
+        return cls(lib.oracle_vocab_load(str(path).encode(), int(emulate_tail)))
+
+    @classmethod
+    def create(cls, k, L, scoring, weighting, parent, is_leaf, desc, weight):
+        lib = load()
+        _declare_vocab(lib)
+        parent = np.ascontiguousarray(parent, np.int32); is_leaf = np.ascontiguousarray(is_leaf, np.uint8)
+        desc = np.ascontiguousarray(desc, np.uint8); weight = np.ascontiguousarray(weight, np.float64)
+        h = lib.oracle_vocab_create(k, L, scoring, weighting, len(parent), _p(parent), _p(is_leaf), _p(desc),
+                                    _p(weight))
+        v = cls(h)
+        v._keep = (parent, is_leaf, desc, weight)
+        return v
+
+    def __del__(self):
+        try:
+            self.lib.oracle_vocab_free(self.h)
+        except Exception:
+            pass
+
+    def nodes(self):
+        n = self.n_nodes
+        parent, nchild = np.zeros(n, np.int32), np.zeros(n, np.int32)
+        word, weight = np.zeros(n, np.uint32), np.zeros(n, np.float64)
+        desc, children = np.zeros((n, 32), np.uint8), np.zeros(max(n, 1), np.int32)
+        self.lib.oracle_vocab_nodes(self.h, _p(parent), _p(nchild), _p(word), _p(weight), _p(desc), _p(children))
+        return parent, nchild, word, weight, desc
+
+    def transform(self, desc, levelsup=4):
+        """-> (bow_word, bow_value, fv_node, fv_off, fv_idx, feat_word, feat_w, feat_nid)."""
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        n = d.shape[0]
+        m = max(n, 1)
+        bw, bv = np.zeros(m, np.uint32), np.zeros(m, np.float64)
+        fn, fo, fi = np.zeros(m, np.uint32), np.zeros(m + 1, np.int32), np.zeros(m, np.uint32)
+        fw, fwt, fni = np.zeros(m, np.uint32), np.zeros(m, np.float64), np.zeros(m, np.uint32)
+        nb, nf = ctypes.c_int(), ctypes.c_int()
+        self.lib.oracle_vocab_transform(self.h, _p(d), n, levelsup, _p(bw), _p(bv), ctypes.byref(nb), _p(fn), _p(fo),
+                                        _p(fi), ctypes.byref(nf), _p(fw), _p(fwt), _p(fni))
+        nb, nf = nb.value, nf.value
+        return bw[:nb], bv[:nb], fn[:nf], fo[:nf + 1], fi[:fo[nf]], fw[:n], fwt[:n], fni[:n]

@@ -1,24 +1,36 @@
 #!/bin/bash
-# One gpurun session: GPU tests, bench, rocprof kernel-trace stats.
+# One gpurun session: GPU tests, bench, rocprof kernel-trace stats, PMC passes.
 # Every GPU step has its own time limit; a fault/abort/timeout ends the session.
+# Knobs: SKIP_TESTS, SKIP_BENCH, SKIP_PROF, SKIP_PMC, PYTEST_ARGS, BENCH_ARGS, PROF_ARGS.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
 mkdir -p $OUT
 cd $R
-fatal() { case $1 in 124|134|137|139) echo "FATAL exit $1 in $2 — stopping"; exit $1;; esac; }
+fatal() { case $1 in 0) ;; 124|134|137|139) echo "FATAL exit $1 in $2 — stopping"; exit $1;; *) [ "${3:-}" = hard ] && { echo "exit $1 in $2 — stopping"; exit $1; };; esac; }
 
-echo "== tests"
-timeout -k 10 ${TEST_T:-900} python -m pytest tests -m gpu -q --maxfail=8 ${PYTEST_ARGS:-} > $OUT/gpu_tests.log 2>&1
-rc=$?; tail -30 $OUT/gpu_tests.log; fatal $rc tests
-[ "${SKIP_BENCH:-0}" = 1 ] && exit 0
-echo "== bench"
-timeout -k 10 ${BENCH_T:-400} python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err
-rc=$?; cat $OUT/bench.json; tail -5 $OUT/bench.err; fatal $rc bench
-[ "${SKIP_PROF:-0}" = 1 ] && exit 0
-echo "== rocprof"
+if [ "${SKIP_TESTS:-0}" != 1 ]; then
+  echo "== tests"
+  timeout -k 10 ${TEST_T:-900} python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread --maxfail=8 ${PYTEST_ARGS:-} > $OUT/gpu_tests.log 2>&1
+  rc=$?; grep -E "passed|failed|error" $OUT/gpu_tests.log | tail -15; fatal $rc tests
+fi
+if [ "${SKIP_BENCH:-0}" != 1 ]; then
+  echo "== bench"
+  timeout -k 10 ${BENCH_T:-400} python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/bench.err
+  rc=$?; cat $OUT/bench.json; tail -5 $OUT/bench.err; fatal $rc bench hard
+fi
+PARGS=${PROF_ARGS:---steps 3 --warmup 1 --no-cpu-baseline}
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 ${PROF_T:-400} rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline > $OUT/prof.log 2>&1
-rc=$?; tail -3 $OUT/prof.log; fatal $rc rocprof
-find $OUT/prof -name "*stats*" | head
+if [ "${SKIP_PROF:-0}" != 1 ]; then
+  echo "== rocprof stats"
+  timeout -k 10 ${PROF_T:-400} rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py $PARGS > $OUT/prof.log 2>&1
+  rc=$?; tail -3 $OUT/prof.log; fatal $rc rocprof hard
+fi
+if [ "${SKIP_PMC:-0}" != 1 ]; then
+  for c in FETCH_SIZE WRITE_SIZE; do
+    echo "== pmc $c"
+    timeout -s KILL ${PMC_T:-240} rocprofv3 --pmc $c -d $OUT/pmc_$c -o run --output-format csv -- python3 $R/bench.py $PARGS > $OUT/pmc_$c.log 2>&1
+    rc=$?; tail -2 $OUT/pmc_$c.log; fatal $rc pmc_$c hard
+  done
+fi
 exit 0
