@@ -29,6 +29,12 @@ struct OrbLevelDev {
     int rootB[kOrbMaxRoots + 1];   // membership: root i holds x in [rootB[i], rootB[i+1])
 };
 
+// One column strip of a level for the blur + FAST kernel: output columns
+// [x0, x0 + 58) (64 lanes minus a 3-px halo each side), rows [y0, y1).
+struct OrbStripDev {
+    int level, x0, y0, y1;
+};
+
 struct OrbCellDev {
     int level;
     int x0, y0, x1, y1;  // FAST detection window [x0,x1)x[y0,y1) in level coords

@@ -69,12 +69,13 @@ struct OrbPipeline {
     std::vector<int> quota, umax;
     std::vector<OrbLevelDev> lv;
     std::vector<OrbCellDev> cells;
+    std::vector<OrbStripDev> strips;
     std::vector<ResizeTab> rtab;
     int taps[7]{};
     int kpCapFrame = 0, nodeCapMax = 0;
     size_t pyrBytesFrameTotal = 0, satIntsFrameTotal = 0;
     size_t lvOff0 = 0;  // (unused)
-    DevBuf d_lv, d_cells, d_tabs, pyr, blur, score, cand, sat, rects, rectCnt, lvkp, lvdesc, okp, odesc, ocount,
+    DevBuf d_lv, d_cells, d_strips, d_tabs, pyr, blur, score, cand, sat, rects, rectCnt, lvkp, lvdesc, okp, odesc, ocount,
         omono, err, staging;
     std::vector<size_t> tabXofs, tabXa, tabYrow, tabYb;  // byte offsets in d_tabs per level
     int lastFrames = 0;
@@ -226,13 +227,20 @@ struct OrbPipeline {
                 }
             }
             if (l > 0) rtab[l] = make_resize_tab(lv[l - 1].w, lv[l - 1].h, d.w, d.h);
+            // column strips of the blur + FAST kernel (candidate queue packs rows in 10 bits)
+            if (d.h >= 1024) return PLVI_E_BADARG;
+            for (int y0 = 0; y0 < d.h; y0 += kStripRows)
+                for (int x0 = 0; x0 < d.w; x0 += kStripOut)
+                    strips.push_back(OrbStripDev{l, x0, y0, std::min(y0 + kStripRows, d.h)});
         }
         kpCapFrame = kpOff;
         pyrBytesFrameTotal = off;
         satIntsFrameTotal = satOff;
         // device tables
-        if (d_lv.alloc(sizeof(OrbLevelDev) * L) || d_cells.alloc(sizeof(OrbCellDev) * cells.size()))
+        if (d_lv.alloc(sizeof(OrbLevelDev) * L) || d_cells.alloc(sizeof(OrbCellDev) * cells.size()) ||
+            d_strips.alloc(sizeof(OrbStripDev) * strips.size()))
             return PLVI_E_HIP;
+        PLVI_CHECK(hipMemcpy(d_strips.p, strips.data(), sizeof(OrbStripDev) * strips.size(), hipMemcpyHostToDevice));
         PLVI_CHECK(hipMemcpy(d_lv.p, lv.data(), sizeof(OrbLevelDev) * L, hipMemcpyHostToDevice));
         PLVI_CHECK(hipMemcpy(d_cells.p, cells.data(), sizeof(OrbCellDev) * cells.size(), hipMemcpyHostToDevice));
         std::vector<uint8_t> tabs;
@@ -279,23 +287,22 @@ struct OrbPipeline {
         uint8_t* Cd = cand.as<uint8_t>();
         const uint8_t* T = d_tabs.as<uint8_t>();
         mark(0, st);
-        // K1 per level
-        for (int l = 0; l < L; ++l) {
+        // K1a: the pyramid (ComputePyramid, chained resize: level l from l-1;
+        // level 1 reads the caller's frames directly)
+        for (int l = 1; l < L; ++l) {
             const OrbLevelDev& d = lv[l];
-            dim3 grid((d.w + kTWh - 1) / kTWh, (d.h + kTHh - 1) / kTHh, nf);
-            if (l == 0) {
-                hipLaunchKernelGGL(orb_level_kernel<false>, grid, dim3(256), 0, st, d_frames, frame_stride, row_stride,
-                                   P + d.off, Bl + d.off, Sc + d.off, d.w, d.h, (size_t)d.plane, nullptr, nullptr, 0,
-                                   nullptr, nullptr, taps[0], taps[1], taps[2], taps[3], tmin);
-            } else {
-                const OrbLevelDev& s = lv[l - 1];
-                hipLaunchKernelGGL(orb_level_kernel<true>, grid, dim3(256), 0, st, (const uint8_t*)(P + s.off),
-                                   (size_t)s.plane, (size_t)s.w, P + d.off, Bl + d.off, Sc + d.off, d.w, d.h,
-                                   (size_t)d.plane, (const int*)(T + tabXofs[l]), (const short*)(T + tabXa[l]),
-                                   rtab[l].xmax, (const int*)(T + tabYrow[l]), (const short*)(T + tabYb[l]), taps[0],
-                                   taps[1], taps[2], taps[3], tmin);
-            }
+            const OrbLevelDev& s = lv[l - 1];
+            dim3 grid((d.w + 63) / 64, (d.h + 3) / 4, nf);
+            const uint8_t* sp = l == 1 ? d_frames : (const uint8_t*)(P + s.off);
+            const size_t sf = l == 1 ? frame_stride : (size_t)s.plane, sr = l == 1 ? row_stride : (size_t)s.w;
+            hipLaunchKernelGGL(orb_resize_kernel, grid, dim3(256), 0, st, sp, sf, sr, P + d.off, d.w, d.h,
+                               (size_t)d.plane, (const int*)(T + tabXofs[l]), (const short*)(T + tabXa[l]),
+                               rtab[l].xmax, (const int*)(T + tabYrow[l]), (const short*)(T + tabYb[l]));
         }
+        // K1b: blur + FAST score of every level (level 0 also copies the frame into its plane)
+        hipLaunchKernelGGL(orb_blur_fast_kernel, dim3((unsigned)strips.size(), nf), dim3(64), 0, st,
+                           d_lv.as<OrbLevelDev>(), d_strips.as<OrbStripDev>(), d_frames, frame_stride, row_stride, P,
+                           Bl, Sc, taps[0], taps[1], taps[2], taps[3], tmin);
         mark(1, st);
         // K2 cell NMS -> candidate map (zeroed first: only detection windows are written)
         PLVI_CHECK(hipMemsetAsync(Cd, 0, pyrBytesFrameTotal, st));
@@ -337,7 +344,6 @@ struct OrbPipeline {
         return PLVI_OK;
     }
 
-    static constexpr int kTWh = 64, kTHh = 16;
 };
 
 }  // namespace plvi

@@ -27,6 +27,33 @@ __host__ __device__ inline int reflect101(int p, int len) {
     return p;
 }
 
+// Global -> LDS staging of an h x w byte block by NT cooperating threads
+// (thread t of NT), 8 loads in flight per thread: a plain element loop would
+// wait for every load before its LDS store (one memory latency per element).
+// Row/column from the flat index with an exact multiply-high division
+// (m = ceil(2^32 / w) is exact for i < 2^32 / w).
+template <int NT>
+__device__ __forceinline__ void stage_bytes(uint8_t* __restrict__ dst, int dst_pitch, const uint8_t* __restrict__ src,
+                                            size_t src_pitch, int w, int h, int t) {
+    const int n = w * h;
+    const unsigned m = (unsigned)(0xFFFFFFFFull / (unsigned)w) + 1u;
+    for (int i0 = 0; i0 < n; i0 += 8 * NT) {
+        uint8_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = i0 + t + k * NT;
+            const int r = (int)__umulhi((unsigned)i, m), c = i - r * w;
+            v[k] = i < n ? src[(size_t)r * src_pitch + c] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = i0 + t + k * NT;
+            const int r = (int)__umulhi((unsigned)i, m), c = i - r * w;
+            if (i < n) dst[r * dst_pitch + c] = v[k];
+        }
+    }
+}
+
 // A device allocation owned by a pipeline (freed in the destructor).
 struct DevBuf {
     void* p = nullptr;
