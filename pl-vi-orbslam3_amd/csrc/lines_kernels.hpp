@@ -281,6 +281,7 @@ __device__ __forceinline__ void win_load_rows(const GrowCtx& g, int r0, int r1, 
     }
 }
 
+template <bool STATS>
 __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restrict__ octs,
                                                       const float* __restrict__ pix,
                                                       const double* __restrict__ modgrad,
@@ -330,7 +331,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
     unsigned long long s_setup = 0, s_round = 0, s_rect = 0, n_seed = 0, n_block = 0, n_round = 0, n_rpt = 0,
                        n_commit = 0;
     unsigned long long s_ph[4] = {0, 0, 0, 0};
-    const bool do_stats = stats != nullptr;
+    constexpr bool do_stats = STATS;  // diagnostic variant only (keeps SGPRs free in the product kernel)
     const unsigned long long t_begin = do_stats ? __builtin_amdgcn_s_memtime() : 0;
     const int half = R / 2;
     for (int y = 0; y < sh - 1; ++y) {
@@ -746,8 +747,7 @@ constexpr int kBTW = 64, kBTH = 16;
 
 __global__ __launch_bounds__(256) void lbd_blur_sobel_kernel(const uint8_t* __restrict__ src, size_t s_frame,
                                                              size_t s_row, int w, int h, uint8_t* __restrict__ blur,
-                                                             int16_t* __restrict__ dxo, int16_t* __restrict__ dyo,
-                                                             size_t d_frame) {
+                                                             short2* __restrict__ go, size_t d_frame) {
     constexpr int EW = kBTW + 6, EH = kBTH + 6;  // input: halo 3 (2 blur + 1 sobel)
     __shared__ uint8_t I[EH][EW];
     __shared__ int Hs[EH][kBTW + 2];
@@ -785,15 +785,13 @@ __global__ __launch_bounds__(256) void lbd_blur_sobel_kernel(const uint8_t* __re
                        (Bv[r + 1][c + 1] - Bv[r - 1][c + 1]);
         const size_t o = (size_t)f * d_frame + (size_t)y * w + x;
         blur[o] = Bv[r][c];
-        dxo[o] = (int16_t)gx;
-        dyo[o] = (int16_t)gy;
+        go[o] = make_short2((short)gx, (short)gy);
     }
 }
 
 __global__ __launch_bounds__(256) void lbd_pyrdown_sobel_kernel(const uint8_t* __restrict__ blur0, int w0, int h0,
                                                                 size_t s_frame, int w, int h,
-                                                                int16_t* __restrict__ dxo, int16_t* __restrict__ dyo,
-                                                                size_t d_frame) {
+                                                                short2* __restrict__ go, size_t d_frame) {
     __shared__ uint8_t P[kBTH + 2][kBTW + 2];
     const int f = blockIdx.z;
     const int X0 = blockIdx.x * kBTW, Y0 = blockIdx.y * kBTH;
@@ -826,8 +824,7 @@ __global__ __launch_bounds__(256) void lbd_pyrdown_sobel_kernel(const uint8_t* _
         const int gy = (P[r + 1][c - 1] - P[r - 1][c - 1]) + 2 * (P[r + 1][c] - P[r - 1][c]) +
                        (P[r + 1][c + 1] - P[r - 1][c + 1]);
         const size_t o = (size_t)f * d_frame + (size_t)y * w + x;
-        dxo[o] = (int16_t)gx;
-        dyo[o] = (int16_t)gy;
+        go[o] = make_short2((short)gx, (short)gy);
     }
 }
 
@@ -844,19 +841,18 @@ __constant__ float c_gaussL[21];
 __constant__ unsigned char c_comb[64];
 
 __global__ __launch_bounds__(64) void lbd_describe_kernel(const LineOctDev* __restrict__ octs,
-                                                          const int16_t* __restrict__ dx_all,
-                                                          const int16_t* __restrict__ dy_all,
+                                                          const short2* __restrict__ g_all,
                                                           const plvi_keyline* __restrict__ kls,
                                                           const int* __restrict__ counts, int fcap,
                                                           uint8_t* __restrict__ desc) {
-    __shared__ float rs[4][64];
+    __shared__ float rq[8][64];
+    __shared__ float bs[72];
     __shared__ float dv[72];
     const int li = blockIdx.x, f = blockIdx.y;
     if (li >= counts[f]) return;
     const plvi_keyline kl = kls[(size_t)f * fcap + li];
     const LineOctDev& od = octs[kl.octave];
-    const int16_t* pdx = dx_all + od.loff + (size_t)f * od.lplane;
-    const int16_t* pdy = dy_all + od.loff + (size_t)f * od.lplane;
+    const short2* pg = g_all + od.loff + (size_t)f * od.lplane;  // (dx, dy) interleaved
     const short realWidth = (short)od.lw;
     const short imageWidth = realWidth - 1;
     const short imageHeight = (short)(od.lh - 1);
@@ -877,94 +873,97 @@ __global__ __launch_bounds__(64) void lbd_describe_kernel(const LineOctDev* __re
             sY0 += dL0;
         }
         float sX = sX0, sY = sY0;
-        for (short w = 0; w < lengthOfLSP; ++w) {
-            short t = (short)__builtin_roundf(sX);
-            const short xc = (t < 0) ? 0 : (t > imageWidth) ? imageWidth : t;
-            t = (short)__builtin_roundf(sY);
-            const short yc = (t < 0) ? 0 : (t > imageHeight) ? imageHeight : t;
-            const short dx = pdx[yc * realWidth + xc];
-            const short dy = pdy[yc * realWidth + xc];
-            const float gDL = dx * dL0 + dy * dL1;
-            const float gDO = dx * dO0 + dy * dO1;
-            if (gDL > 0) pL += gDL;
-            else nL -= gDL;
-            if (gDO > 0) pO += gDO;
-            else nO -= gDO;
-            sX += dL0;
-            sY += dL1;
+        // samples in batches of 8: the coordinate sequence (sequential float
+        // steps) and the sums stay in reference order; the 8 gathers are in
+        // flight together
+        for (int w0 = 0; w0 < lengthOfLSP; w0 += 8) {
+            int idx[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                short t = (short)__builtin_roundf(sX);
+                const short xc = (t < 0) ? 0 : (t > imageWidth) ? imageWidth : t;
+                t = (short)__builtin_roundf(sY);
+                const short yc = (t < 0) ? 0 : (t > imageHeight) ? imageHeight : t;
+                idx[k] = yc * realWidth + xc;
+                sX += dL0;
+                sY += dL1;
+            }
+            short2 g[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) g[k] = w0 + k < lengthOfLSP ? pg[idx[k]] : make_short2(0, 0);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                if (w0 + k >= lengthOfLSP) break;
+                const short dx = g[k].x, dy = g[k].y;
+                const float gDL = dx * dL0 + dy * dL1;
+                const float gDO = dx * dO0 + dy * dO1;
+                if (gDL > 0) pL += gDL;
+                else nL -= gDL;
+                if (gDO > 0) pO += gDO;
+                else nO -= gDO;
+            }
         }
     }
-    rs[0][h] = pL; rs[1][h] = nL; rs[2][h] = pO; rs[3][h] = nO;
+    // row sums scaled by gaussCoefG_ (:1189-1197), per row lane
+    if (h < 63) {
+        const float c = c_gaussG[h];
+        const float pLr = c * pL, nLr = c * nL, pOr = c * pO, nOr = c * nO;
+        rq[0][h] = pLr; rq[1][h] = nLr; rq[2][h] = pLr * pLr; rq[3][h] = nLr * nLr;
+        rq[4][h] = pOr; rq[5][h] = nOr; rq[6][h] = pOr * pOr; rq[7][h] = nOr * nOr;
+    }
     __syncthreads();
+    // band sums (:1202-1241): accumulator (band b, quantity q) takes the rows of
+    // bands b-1, b, b+1 in row order, exactly the reference's += sequence for it
+    for (int a = h; a < 72; a += 64) {
+        const int b = a >> 3, q = a & 7;
+        const bool sq = (q & 2) != 0;
+        float acc = 0.f;
+        const int r0 = max(0, 7 * (b - 1)), r1 = min(62, 7 * (b + 2) - 1);
+        for (int r = r0; r <= r1; ++r) {
+            const int j = r / 7, m = r - 7 * j;
+            const float c = j == b ? c_gaussL[m + 7] : j == b + 1 ? c_gaussL[m + 14] : c_gaussL[m];
+            const float x = rq[q][r];
+            acc += sq ? c * c * x : c * x;
+        }
+        bs[a] = acc;
+    }
+    __syncthreads();
+    if (h < 36) {  // mean / std per band (:1254-1281)
+        const int b = h >> 2, k = h & 3;
+        const int qs = (k < 2 ? 0 : 4) + (k & 1);
+        const float invN = (b == 0 || b == 8) ? (float)(1.0 / (7 * 2.0)) : (float)(1.0 / (7 * 3.0));
+        const float t = bs[8 * b + qs] * invN;
+        dv[8 * b + k] = t;
+        dv[8 * b + 4 + k] = __builtin_sqrtf(bs[8 * b + qs + 2] * invN - t * t);
+    }
+    __syncthreads();
+    // normalisation (:1283-1330): the three sums stay sequential (lane 0),
+    // the element-wise scaling and the 0.4 clip run on all lanes
+    __shared__ float s_t[3];
     if (h == 0) {
-        float pLB[9] = {0}, nLB[9] = {0}, pL2B[9] = {0}, nL2B[9] = {0};
-        float pOB[9] = {0}, nOB[9] = {0}, pO2B[9] = {0}, nO2B[9] = {0};
-        for (int r = 0; r < 63; ++r) {
-            float c = c_gaussG[r];
-            const float pLr = c * rs[0][r], nLr = c * rs[1][r];
-            const float pL2r = pLr * pLr, nL2r = nLr * nLr;
-            const float pOr = c * rs[2][r], nOr = c * rs[3][r];
-            const float pO2r = pOr * pOr, nO2r = nOr * nOr;
-            int band = r / 7;
-            c = c_gaussL[r % 7 + 7];
-            pLB[band] += c * pLr; nLB[band] += c * nLr;
-            pL2B[band] += c * c * pL2r; nL2B[band] += c * c * nL2r;
-            pOB[band] += c * pOr; nOB[band] += c * nOr;
-            pO2B[band] += c * c * pO2r; nO2B[band] += c * c * nO2r;
-            band--;
-            if (band >= 0) {
-                c = c_gaussL[r % 7 + 14];
-                pLB[band] += c * pLr; nLB[band] += c * nLr;
-                pL2B[band] += c * c * pL2r; nL2B[band] += c * c * nL2r;
-                pOB[band] += c * pOr; nOB[band] += c * nOr;
-                pO2B[band] += c * c * pO2r; nO2B[band] += c * c * nO2r;
-            }
-            band = band + 2;
-            if (band < 9) {
-                c = c_gaussL[r % 7];
-                pLB[band] += c * pLr; nLB[band] += c * nLr;
-                pL2B[band] += c * c * pL2r; nL2B[band] += c * c * nL2r;
-                pOB[band] += c * pOr; nOB[band] += c * nOr;
-                pO2B[band] += c * c * pO2r; nO2B[band] += c * c * nO2r;
-            }
-        }
-        const float invN2 = (float)(1.0 / (7 * 2.0)), invN3 = (float)(1.0 / (7 * 3.0));
-        for (int b = 0; b < 9; ++b) {
-            const float invN = (b == 0 || b == 8) ? invN2 : invN3;
-            const int d = b * 8;
-            float t = pLB[b] * invN;
-            dv[d] = t;
-            dv[d + 4] = __builtin_sqrtf(pL2B[b] * invN - t * t);
-            t = nLB[b] * invN;
-            dv[d + 1] = t;
-            dv[d + 5] = __builtin_sqrtf(nL2B[b] * invN - t * t);
-            t = pOB[b] * invN;
-            dv[d + 2] = t;
-            dv[d + 6] = __builtin_sqrtf(pO2B[b] * invN - t * t);
-            t = nOB[b] * invN;
-            dv[d + 3] = t;
-            dv[d + 7] = __builtin_sqrtf(nO2B[b] * invN - t * t);
-        }
         float tM = 0, tS = 0;
         for (int b = 0; b < 9; ++b) {
             const float* v = dv + 8 * b;
             tM += v[0] * v[0]; tM += v[1] * v[1]; tM += v[2] * v[2]; tM += v[3] * v[3];
             tS += v[4] * v[4]; tS += v[5] * v[5]; tS += v[6] * v[6]; tS += v[7] * v[7];
         }
-        tM = 1 / __builtin_sqrtf(tM);
-        tS = 1 / __builtin_sqrtf(tS);
-        for (int b = 0; b < 9; ++b) {
-            float* v = dv + 8 * b;
-            v[0] = v[0] * tM; v[1] = v[1] * tM; v[2] = v[2] * tM; v[3] = v[3] * tM;
-            v[4] = v[4] * tS; v[5] = v[5] * tS; v[6] = v[6] * tS; v[7] = v[7] * tS;
-        }
-        for (int i = 0; i < 72; ++i)
-            if ((double)dv[i] > 0.4) dv[i] = (float)0.4;
+        s_t[0] = 1 / __builtin_sqrtf(tM);
+        s_t[1] = 1 / __builtin_sqrtf(tS);
+    }
+    __syncthreads();
+    for (int i = h; i < 72; i += 64) {
+        float v = dv[i] * ((i & 7) < 4 ? s_t[0] : s_t[1]);
+        if ((double)v > 0.4) v = (float)0.4;
+        dv[i] = v;
+    }
+    __syncthreads();
+    if (h == 0) {
         float t = 0;
         for (int i = 0; i < 72; ++i) t += dv[i] * dv[i];
-        t = 1 / __builtin_sqrtf(t);
-        for (int i = 0; i < 72; ++i) dv[i] = dv[i] * t;
+        s_t[2] = 1 / __builtin_sqrtf(t);
     }
+    __syncthreads();
+    for (int i = h; i < 72; i += 64) dv[i] = dv[i] * s_t[2];
     __syncthreads();
     if (h < 32) {
         const float* f1 = dv + 8 * c_comb[2 * h];

@@ -51,7 +51,7 @@ struct LinePipeline {
     double SCALE = 0.8, prec = 0, rho = 0, min_length = 0;
     double gk[7]{};
     DevBuf d_oct, d_tabs, octImg, pix, modg, seedcs, gbits, qspill, rawLines, nlines, klTmp, klOut, fnOut, cntOut, descOut, lbdBlur,
-        lbdDx, lbdDy, err, staging;
+        lbdG, err, staging;
     size_t qspillFrame = 0, gbitsFrame = 0, lbdPlaneTotal = 0;
     int lastFrames = 0;
     static constexpr int kStages = 5, kRing = 512;
@@ -197,8 +197,8 @@ struct LinePipeline {
             nlines.alloc(sizeof(int) * nOct * Bcap) || klTmp.alloc(sizeof(plvi_keyline) * (size_t)kKlCap * Bcap) ||
             klOut.alloc(sizeof(plvi_keyline) * (size_t)fcap * Bcap) || fnOut.alloc(sizeof(double) * 3 * fcap * Bcap) ||
             cntOut.alloc(sizeof(int) * Bcap) || descOut.alloc((size_t)32 * fcap * Bcap) ||
-            lbdBlur.alloc((size_t)W * H * Bcap) || lbdDx.alloc(sizeof(int16_t) * lbdPlaneTotal) ||
-            lbdDy.alloc(sizeof(int16_t) * lbdPlaneTotal) || err.alloc(sizeof(int)) || staging.alloc((size_t)W * H))
+            lbdBlur.alloc((size_t)W * H * Bcap) || lbdG.alloc(sizeof(short2) * lbdPlaneTotal) ||
+            err.alloc(sizeof(int)) || staging.alloc((size_t)W * H))
             return PLVI_E_HIP;
         PLVI_CHECK(hipMemset(err.p, 0, sizeof(int)));
         // region-growing LDS: rect staging + R-row USED/angle window + queue,
@@ -217,8 +217,8 @@ struct LinePipeline {
         if (budget > 160 * 1024) return PLVI_E_BADARG;
         while (growR * 2 <= 1024 && fixed + perRow * growR * 2 <= budget) growR *= 2;
         growSmem = fixed + perRow * growR;
-        PLVI_CHECK(hipFuncSetAttribute((const void*)lsd_grow_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)growSmem));
+        for (const void* k : {(const void*)lsd_grow_kernel<false>, (const void*)lsd_grow_kernel<true>})
+            PLVI_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)growSmem));
         return PLVI_OK;
     }
     size_t growSmem = 0;
@@ -281,7 +281,8 @@ struct LinePipeline {
 
     // Phase B: region growing (LK3) + keyline assembly / top-k (LK4).
     void launch_grow_assemble(int nf, hipStream_t st) {
-        hipLaunchKernelGGL(lsd_grow_kernel, dim3(nOct, nf), dim3(64), growSmem, st, d_oct.as<LineOctDev>(),
+        auto growK = growStats ? lsd_grow_kernel<true> : lsd_grow_kernel<false>;
+        hipLaunchKernelGGL(growK, dim3(nOct, nf), dim3(64), growSmem, st, d_oct.as<LineOctDev>(),
                            (const float*)pix.as<float>(), (const double*)modg.as<double>(),
                            (const float2*)seedcs.as<float2>(), gbits.as<unsigned>(), gbitsFrame, qspill.as<unsigned>(),
                            qspillFrame, prec, SCALE, rawLines.as<LsdLine>(), nlines.as<int>(), err.as<int>(), growR,
@@ -299,15 +300,14 @@ struct LinePipeline {
         const LineOctDev& d0 = oct[0];
         dim3 g0((d0.lw + kBTW - 1) / kBTW, (d0.lh + kBTH - 1) / kBTH, nf);
         hipLaunchKernelGGL(lbd_blur_sobel_kernel, g0, dim3(256), 0, st, d_frames, frame_stride, row_stride, d0.lw,
-                           d0.lh, lbdBlur.as<uint8_t>(), lbdDx.as<int16_t>() + d0.loff, lbdDy.as<int16_t>() + d0.loff,
-                           (size_t)d0.lplane);
+                           d0.lh, lbdBlur.as<uint8_t>(), lbdG.as<short2>() + d0.loff, (size_t)d0.lplane);
         for (int l = 1; l < nOct; ++l) {
             const LineOctDev& d = oct[l];
             if (l > 1) return PLVI_E_BADARG;  // pyrDown chain beyond octave 1 not wired (config: 2 levels)
             dim3 g1((d.lw + kBTW - 1) / kBTW, (d.lh + kBTH - 1) / kBTH, nf);
             hipLaunchKernelGGL(lbd_pyrdown_sobel_kernel, g1, dim3(256), 0, st, (const uint8_t*)lbdBlur.as<uint8_t>(),
-                               d0.lw, d0.lh, (size_t)d0.lplane, d.lw, d.lh, lbdDx.as<int16_t>() + d.loff,
-                               lbdDy.as<int16_t>() + d.loff, (size_t)d.lplane);
+                               d0.lw, d0.lh, (size_t)d0.lplane, d.lw, d.lh, lbdG.as<short2>() + d.loff,
+                               (size_t)d.lplane);
         }
         return PLVI_OK;
     }
@@ -315,7 +315,7 @@ struct LinePipeline {
     // LB3: LBD descriptors of the assembled keylines.
     void launch_describe(int nf, hipStream_t st) {
         hipLaunchKernelGGL(lbd_describe_kernel, dim3(fcap, nf), dim3(64), 0, st, d_oct.as<LineOctDev>(),
-                           (const int16_t*)lbdDx.as<int16_t>(), (const int16_t*)lbdDy.as<int16_t>(),
+                           (const short2*)lbdG.as<short2>(),
                            (const plvi_keyline*)klOut.as<plvi_keyline>(), (const int*)cntOut.as<int>(), fcap,
                            descOut.as<uint8_t>());
         mark(5, st);
