@@ -166,13 +166,18 @@ __global__ __launch_bounds__(256) void lsd_prep_kernel(const uint8_t* __restrict
 // lane is re-decided with the exact angle in the next round.  The result is
 // identical to the sequential algorithm.
 // ---------------------------------------------------------------------------
+// LDS pointers carry address space 3 so every access is a ds_* instruction
+// (a generic pointer turns them into flat accesses that wait on vmcnt too).
+typedef unsigned __attribute__((address_space(3))) lds_u32;
+typedef float __attribute__((address_space(3))) lds_f32;
+
 struct GrowCtx {
     const float* P;   // angle plane (degrees, NOTDEF = -1024)
     unsigned* gbits;  // global USED bitmap (rows at or beyond the window)
-    unsigned* bits;   // LDS USED ring: R rows x wpr words
-    unsigned* qlds;   // LDS region queue (x | y << 16), QL entries
+    lds_u32* bits;    // LDS USED ring: R rows x wpr words
+    lds_u32* qlds;    // LDS region queue (x | y << 16), QL entries
     unsigned* qglob;  // global queue spill
-    float* win;       // LDS angle ring: R rows x sw
+    lds_f32* win;     // LDS angle ring: R rows x sw
     int sw, sh, R, wpr, wb, QL, ys;  // ys = row of the current seed
 };
 
@@ -197,7 +202,8 @@ __device__ __forceinline__ bool used_get(const GrowCtx& g, int x, int y) {
 }
 __device__ __forceinline__ void used_set(const GrowCtx& g, int x, int y) {
     const unsigned b = 1u << (x & 31);
-    if (__builtin_expect(y < g.wb + g.R, 1)) atomicOr(&g.bits[(y & (g.R - 1)) * g.wpr + (x >> 5)], b);
+    if (__builtin_expect(y < g.wb + g.R, 1))
+        __atomic_fetch_or(&g.bits[(y & (g.R - 1)) * g.wpr + (x >> 5)], b, __ATOMIC_RELAXED);  // ds_or_b32
     else __hip_atomic_fetch_or(g.gbits + (size_t)y * g.wpr + (x >> 5), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ unsigned q_get(const GrowCtx& g, int i) {
@@ -309,9 +315,9 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
     g.qglob = qspill + (size_t)(f * nOct + o) * qspill_frame;
     // LDS: rect staging (64 x 3 doubles) | USED ring | queue | angle ring
     double* rs = reinterpret_cast<double*>(lds_u);
-    g.bits = lds_u + 64 * 3 * 2;
+    g.bits = (lds_u32*)(lds_u + 64 * 3 * 2);
     g.qlds = g.bits + R * g.wpr;
-    g.win = reinterpret_cast<float*>(g.qlds + QL);
+    g.win = (lds_f32*)(g.qlds + QL);
     g.wb = 0;
     g.ys = 0;
     for (int i = lane; i < sh * g.wpr; i += 64) g.gbits[i] = 0u;

@@ -510,33 +510,46 @@ __global__ __launch_bounds__(64) void orb_cell_nms_kernel(const OrbCellDev* __re
 // region [minB, minB+rw) x [minB, minB+rh).  SAT[y][x] = #candidates in
 // [0,x) x [0,y) (relative coords), (rw+1) x (rh+1).
 // ---------------------------------------------------------------------------
+constexpr int kSatRowsPerWave = 8;
+
+// Row prefix counts, kSatRowsPerWave rows per wave (their loads in flight together).
 __global__ __launch_bounds__(64) void orb_sat_rows_kernel(const OrbLevelDev* __restrict__ lvs,
                                                           const uint8_t* __restrict__ cand, int* __restrict__ sat) {
-    const int y = blockIdx.x, l = blockIdx.y, f = blockIdx.z;
+    const int l = blockIdx.y, f = blockIdx.z;
     const OrbLevelDev& L = lvs[l];
-    if (y > L.rh) return;
-    int* row = sat + L.satOff + (size_t)f * L.satPlane + (size_t)y * (L.rw + 1);
+    const int yb = blockIdx.x * kSatRowsPerWave;
+    if (yb > L.rh) return;
+    int* base = sat + L.satOff + (size_t)f * L.satPlane;
+    const uint8_t* C0 = cand + L.off + (size_t)f * L.plane + (size_t)L.minB * L.w + L.minB;
     const int lane = threadIdx.x;
-    if (y == 0) {
-        for (int x = lane; x <= L.rw; x += 64) row[x] = 0;
-        return;
-    }
-    const uint8_t* C = cand + L.off + (size_t)f * L.plane + (size_t)(L.minB + y - 1) * L.w + L.minB;
-    if (lane == 0) row[0] = 0;
-    int carry = 0;
+    int carry[kSatRowsPerWave];
+#pragma unroll
+    for (int k = 0; k < kSatRowsPerWave; ++k) carry[k] = 0;
     for (int x0 = 0; x0 < L.rw; x0 += 64) {
         const int x = x0 + lane;
-        int v = (x < L.rw && C[x] != 0) ? 1 : 0;
+        int v[kSatRowsPerWave];
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int n = __shfl_up(v, o);
-            if (lane >= o) v += n;
+        for (int k = 0; k < kSatRowsPerWave; ++k) {
+            const int y = yb + k;  // SAT row y counts image row y-1 of the region
+            v[k] = (y >= 1 && y <= L.rh && x < L.rw) ? (C0[(size_t)(y - 1) * L.w + x] != 0) : 0;
         }
-        if (x < L.rw) row[x + 1] = carry + v;
-        carry += __shfl(v, 63);
+#pragma unroll
+        for (int k = 0; k < kSatRowsPerWave; ++k) {
+            int t = v[k];
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int nb = __shfl_up(t, o);
+                if (lane >= o) t += nb;
+            }
+            const int y = yb + k;
+            if (y <= L.rh && x < L.rw) base[(size_t)y * (L.rw + 1) + x + 1] = carry[k] + t;
+            carry[k] += __shfl(t, 63);
+        }
     }
+    if (lane < kSatRowsPerWave && yb + lane <= L.rh) base[(size_t)(yb + lane) * (L.rw + 1)] = 0;
 }
 
+// Column prefix, one thread per column, 16 rows' loads in flight.
 __global__ __launch_bounds__(256) void orb_sat_cols_kernel(const OrbLevelDev* __restrict__ lvs,
                                                            int* __restrict__ sat) {
     const int l = blockIdx.y, f = blockIdx.z;
@@ -547,13 +560,15 @@ __global__ __launch_bounds__(256) void orb_sat_cols_kernel(const OrbLevelDev* __
     int* col = sat + L.satOff + (size_t)f * L.satPlane + x;
     int acc = 0;
     int y = 1;
-    for (; y + 4 <= L.rh + 1; y += 4) {
-        const int a = col[(size_t)y * st], b = col[(size_t)(y + 1) * st], c = col[(size_t)(y + 2) * st],
-                  d = col[(size_t)(y + 3) * st];
-        acc += a; col[(size_t)y * st] = acc;
-        acc += b; col[(size_t)(y + 1) * st] = acc;
-        acc += c; col[(size_t)(y + 2) * st] = acc;
-        acc += d; col[(size_t)(y + 3) * st] = acc;
+    for (; y + 16 <= L.rh + 1; y += 16) {
+        int v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = col[(size_t)(y + k) * st];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            acc += v[k];
+            col[(size_t)(y + k) * st] = acc;
+        }
     }
     for (; y <= L.rh; ++y) {
         acc += col[(size_t)y * st];
@@ -577,16 +592,21 @@ struct OctNodes {
     short *mx0, *my0, *mx1, *my1;  // membership rectangle (half-open)
     int *cnt, *seq;
     short *nxt, *prv, *freel;
-    short *vsz, *vprev;
+    short *vsz, *vprev, *todo;
+    int* ccnt;                     // [C][4] key counts of the four children (prefetched)
     unsigned char* nomore;
 };
 
+// The whole wave executes the list algorithm in lockstep (identical values in
+// every lane, identical LDS writes), so that the SAT counts of every split a
+// phase will perform are gathered first by all lanes in parallel: the
+// children of a node depend only on the node, not on the list order.
 __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __restrict__ lvs,
                                                         const int* __restrict__ sat, short4* __restrict__ out_rect,
                                                         int* __restrict__ out_cnt, int nodeCapMax, int L,
                                                         int* __restrict__ err) {
     extern __shared__ __align__(16) unsigned char smem[];
-    const int l = blockIdx.x, f = blockIdx.y;
+    const int l = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
     const OrbLevelDev& lv = lvs[l];
     const int C = nodeCapMax;
     OctNodes n;
@@ -594,22 +614,54 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
         int* ip = reinterpret_cast<int*>(smem);
         n.cnt = ip; ip += C;
         n.seq = ip; ip += C;
+        n.ccnt = ip; ip += 4 * C;
         short* sp = reinterpret_cast<short*>(ip);
         n.gx0 = sp; sp += C; n.gy0 = sp; sp += C; n.gx1 = sp; sp += C; n.gy1 = sp; sp += C;
         n.mx0 = sp; sp += C; n.my0 = sp; sp += C; n.mx1 = sp; sp += C; n.my1 = sp; sp += C;
         n.nxt = sp; sp += C; n.prv = sp; sp += C; n.freel = sp; sp += C;
-        n.vsz = sp; sp += C; n.vprev = sp; sp += C;
+        n.vsz = sp; sp += C; n.vprev = sp; sp += C; n.todo = sp; sp += C;
         n.nomore = reinterpret_cast<unsigned char*>(sp);
     }
-    if (threadIdx.x != 0) return;
-
     const int* S = sat + lv.satOff + (size_t)f * lv.satPlane;
     const int st = lv.rw + 1, RW = lv.rw, RH = lv.rh;
+    auto sat_at = [&](int x, int y) -> int {
+        x = max(0, min(x, RW));
+        y = max(0, min(y, RH));
+        return S[y * st + x];
+    };
     auto count = [&](int x0, int y0, int x1, int y1) -> int {
         x0 = max(0, min(x0, RW)); x1 = max(0, min(x1, RW));
         y0 = max(0, min(y0, RH)); y1 = max(0, min(y1, RH));
         if (x0 >= x1 || y0 >= y1) return 0;
         return S[y1 * st + x1] - S[y0 * st + x1] - S[y1 * st + x0] + S[y0 * st + x0];
+    };
+    // children counts of nodes ids[0..k): lanes in parallel, 16 SAT loads each in flight
+    auto prefetch = [&](const short* ids, int k) {
+        __syncthreads();
+        for (int i = lane; i < k; i += 64) {
+            const int p = ids[i];
+            const int x0 = n.gx0[p], y0 = n.gy0[p], x1 = n.gx1[p], y1 = n.gy1[p];
+            const int midX = x0 + (int)ceilf((float)(x1 - x0) / 2), midY = y0 + (int)ceilf((float)(y1 - y0) / 2);
+            const int mx0 = n.mx0[p], my0 = n.my0[p], mx1 = n.mx1[p], my1 = n.my1[p];
+            const int xs[4] = {mx0, min(mx1, midX), max(mx0, midX), mx1};
+            const int ys[4] = {my0, min(my1, midY), max(my0, midY), my1};
+            int v[4][4];
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) v[a][b] = sat_at(xs[b], ys[a]);
+            // child q: x range (xs[0],xs[1]) or (xs[2],xs[3]); y range likewise
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int xa = (q & 1) ? 2 : 0, ya = (q & 2) ? 2 : 0;
+                const int cx0 = max(0, min(xs[xa], RW)), cx1 = max(0, min(xs[xa + 1], RW));
+                const int cy0 = max(0, min(ys[ya], RH)), cy1 = max(0, min(ys[ya + 1], RH));
+                n.ccnt[4 * p + q] = (cx0 >= cx1 || cy0 >= cy1)
+                                        ? 0
+                                        : v[ya + 1][xa + 1] - v[ya][xa + 1] - v[ya + 1][xa] + v[ya][xa];
+            }
+        }
+        __syncthreads();
     };
     const int N = lv.quota;
     int nfree = 0;
@@ -654,13 +706,16 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
         const int halfX = (int)ceilf((float)(x1 - x0) / 2), halfY = (int)ceilf((float)(y1 - y0) / 2);
         const int midX = x0 + halfX, midY = y0 + halfY;
         const int mx0 = n.mx0[p], my0 = n.my0[p], mx1 = n.mx1[p], my1 = n.my1[p];
+        int cc[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cc[q] = n.ccnt[4 * p + q];
         for (int q = 0; q < 4; ++q) {
             int cx0, cy0, cx1, cy1, bx0, by0, bx1, by1;
             if (q == 0) { cx0 = x0; cy0 = y0; cx1 = midX; cy1 = midY; bx0 = mx0; by0 = my0; bx1 = min(mx1, midX); by1 = min(my1, midY); }
             else if (q == 1) { cx0 = midX; cy0 = y0; cx1 = x1; cy1 = midY; bx0 = max(mx0, midX); by0 = my0; bx1 = mx1; by1 = min(my1, midY); }
             else if (q == 2) { cx0 = x0; cy0 = midY; cx1 = midX; cy1 = y1; bx0 = mx0; by0 = max(my0, midY); bx1 = min(mx1, midX); by1 = my1; }
             else { cx0 = midX; cy0 = midY; cx1 = x1; cy1 = y1; bx0 = max(mx0, midX); by0 = max(my0, midY); bx1 = mx1; by1 = my1; }
-            const int c = count(bx0, by0, bx1, by1);
+            const int c = cc[q];
             if (c == 0) continue;
             const int k = alloc();
             if (k < 0) return;
@@ -679,14 +734,16 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
         int prevSize = size;
         int nToExpand = 0;
         nv = 0;
-        for (int it = head; it >= 0;) {
-            const int next = n.nxt[it];
-            if (!n.nomore[it]) {
-                split(it, &nToExpand);
-                if (overflow) break;
-                unlink(it);
-            }
-            it = next;
+        // the nodes this pass splits: every node without bNoMore, in list order
+        int nt = 0;
+        for (int it = head; it >= 0; it = n.nxt[it])
+            if (!n.nomore[it]) n.todo[nt++] = (short)it;
+        prefetch(n.todo, nt);
+        for (int t = 0; t < nt && !overflow; ++t) {
+            const int it = n.todo[t];
+            split(it, &nToExpand);
+            if (overflow) break;
+            unlink(it);
         }
         if (overflow) break;
         if (size >= N || size == prevSize) {
@@ -711,6 +768,7 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
                     }
                     n.vprev[j + 1] = v;
                 }
+                prefetch(n.vprev, np);
                 for (int j = np - 1; j >= 0; --j) {
                     const int p = n.vprev[j];
                     split(p, nullptr);
@@ -726,12 +784,15 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
     int cntOut = 0;
     if (!overflow) {
         for (int it = head; it >= 0 && cntOut < lv.nodeCap; it = n.nxt[it]) {
-            R[cntOut++] = make_short4(n.mx0[it], n.my0[it], n.mx1[it], n.my1[it]);
+            if (lane == 0) R[cntOut] = make_short4(n.mx0[it], n.my0[it], n.mx1[it], n.my1[it]);
+            ++cntOut;
         }
         if (size > lv.nodeCap) overflow = true;
     }
-    out_cnt[(size_t)f * L + l] = overflow ? 0 : cntOut;
-    if (overflow) atomicOr(err, 1);
+    if (lane == 0) {
+        out_cnt[(size_t)f * L + l] = overflow ? 0 : cntOut;
+        if (overflow) atomicOr(err, 1);
+    }
 }
 
 // ---------------------------------------------------------------------------

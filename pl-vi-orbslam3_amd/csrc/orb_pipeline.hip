@@ -312,13 +312,14 @@ struct OrbPipeline {
         // K3 SAT
         int maxRh = 0, maxRw = 0;
         for (auto& d : lv) { maxRh = std::max(maxRh, d.rh); maxRw = std::max(maxRw, d.rw); }
-        hipLaunchKernelGGL(orb_sat_rows_kernel, dim3(maxRh + 1, L, nf), dim3(64), 0, st, d_lv.as<OrbLevelDev>(),
+        hipLaunchKernelGGL(orb_sat_rows_kernel, dim3((maxRh + kSatRowsPerWave) / kSatRowsPerWave, L, nf), dim3(64), 0,
+                           st, d_lv.as<OrbLevelDev>(),
                            (const uint8_t*)Cd, sat.as<int>());
         hipLaunchKernelGGL(orb_sat_cols_kernel, dim3((maxRw + 1 + 255) / 256, L, nf), dim3(256), 0, st,
                            d_lv.as<OrbLevelDev>(), sat.as<int>());
         mark(3, st);
         // K4 octree
-        const size_t smem = (size_t)nodeCapMax * (2 * 4 + 13 * 2 + 1) + 16;
+        const size_t smem = (size_t)nodeCapMax * (6 * 4 + 14 * 2 + 1) + 16;
         hipLaunchKernelGGL(orb_octree_kernel, dim3(L, nf), dim3(64), smem, st, d_lv.as<OrbLevelDev>(),
                            (const int*)sat.as<int>(), rects.as<short4>(), rectCnt.as<int>(), nodeCapMax, L,
                            err.as<int>());
