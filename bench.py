@@ -45,15 +45,27 @@ def level_dims(w, h, nlevels=8, sf=1.2):
     return dims
 
 
-def level_stage_bytes(w, h):
-    """Algorithmic bytes/frame of the fused level kernel: read the level's
-    source (input frame at l=0, level l-1 otherwise) once, write the level
-    image, its 7x7 blur and its FAST score map once (u8)."""
-    d = level_dims(w, h)
-    planes = [a * b for a, b in d]
-    reads = w * h + sum(planes[:-1])
-    writes = 3 * sum(planes)
-    return reads + writes
+def blur_fast_bytes(w, h):
+    """Algorithmic bytes/frame of orb_blur_fast_kernel (one launch covers all
+    8 levels): read every level image once (level 0 = the input frame), write
+    its 7x7 blur and FAST score planes once, and level 0's pyramid copy (u8)."""
+    planes = [a * b for a, b in level_dims(w, h)]
+    return sum(planes) + 2 * sum(planes) + planes[0]
+
+
+def committed_traffic(batch):
+    """HBM bytes per launch of the roofline kernel from the committed PMC
+    passes (profiles/*/pmc_traffic.json, tools/pmc_traffic.py), when they were
+    taken at this batch size; else None."""
+    best = None
+    for f in sorted(ROOT.glob("profiles/*/pmc_traffic.json")):
+        try:
+            d = json.loads(f.read_text())
+        except ValueError:
+            continue
+        if d.get("batch") == batch and d.get("kernel") == "orb_blur_fast_kernel":
+            best = d
+    return None if best is None else best["bytes_per_launch"]
 
 
 def cpu_baseline(budget_s=15.0):
@@ -89,6 +101,8 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-bow", action="store_true", help="skip the DBoW2 transform stage timing")
+    ap.add_argument("--gather", action="store_true",
+                    help="BASELINE C4: all-gather every step's per-frame ORB/line tables over RCCL (timed)")
     args = ap.parse_args()
 
     import torch
@@ -107,6 +121,7 @@ def main():
     B, W, H = args.batch, 640, 480
     frames = torch.from_numpy(synth.batch(B, W, H, seed0=pdist.shard_seed(rank))).to(f"cuda:{dev}")
     orb = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=B, device=dev)
+    orb.kernel_timing(True)  # event pair around every roofline-kernel launch of this process
     lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=B, device=dev)
     kp_p, de_p, co_p, mo_p, cap = orb.outputs()
     kl_p, lde_p, lfn_p, lco_p, lcap = lx.outputs()
@@ -129,11 +144,26 @@ def main():
         if rc:
             raise RuntimeError(f"match {rc}")
 
+    # C4 (--gather): per-frame tables staged into torch tensors on sA, then one
+    # all_gather per table over RCCL (plvi.dist.gather_tables)
+    tab_src = [(co_p, 4 * B), (kp_p, 28 * cap * B), (de_p, 32 * cap * B), (lco_p, 4 * B), (kl_p, 68 * lcap * B),
+               (lde_p, 32 * lcap * B)]
+    tabs = [torch.empty(n, dtype=torch.uint8, device=f"cuda:{dev}") for _, n in tab_src] if args.gather else []
+
+    def run_gather():
+        for (src, n), t in zip(tab_src, tabs):
+            if lib.plvi_memcpy_async(t.data_ptr(), src, n, 3, sA.cuda_stream):
+                raise RuntimeError("gather copy")
+        with torch.cuda.stream(sA):
+            pdist.gather_tables(tabs, world)
+
     def step():
         # Frame::Frame: ORB || lines as one schedule (region growing overlapped
         # with the ORB pipeline and the LBD Sobel pyramid), then matching
         plvi.frame_extract_batch(orb, lx, frames.data_ptr(), B, W * H, W, (0, 0), stream=sA.cuda_stream)
         run_match()
+        if args.gather:
+            run_gather()
 
     for _ in range(args.warmup):
         step()
@@ -205,14 +235,17 @@ def main():
     value = frames_total / el
     ms_step = el / args.steps * 1e3
 
-    # roofline: dominant stage
-    lvl_bytes = level_stage_bytes(W, H) * B
-    knn_ops = (B - 1) * 1000 * 1000 * 16  # 8 x (xor + popcount) per descriptor pair
+    # roofline: the dominant HBM-streaming kernel, averaged over every launch
+    # of this process (warmup, stage runs, timed steps) = what rocprofv3
+    # --stats averages for the same command
+    ktot, kn = orb.kernel_timing_read()
+    kavg_ms = ktot / max(kn, 1)
+    bf_bytes = blur_fast_bytes(W, H) * B
     dom = max((k for k in stage_ms if k != "bow.transform"), key=stage_ms.get)
     roof = {
-        "bound": "hbm", "kernel": "orb_level_kernel (resize+blur7x7+FAST score, all 8 levels)",
-        "achieved": lvl_bytes / (stage_ms["orb.level"] * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "traffic": None,
+        "bound": "hbm", "kernel": "orb_blur_fast_kernel (7x7 blur + FAST score, all 8 levels, one launch)",
+        "achieved": bf_bytes / (kavg_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "traffic": committed_traffic(B), "bytes_per_launch": bf_bytes, "avg_launch_ms": kavg_ms, "launches": kn,
     }
     roof["frac"] = roof["achieved"] / roof["peak"]
     result = {
@@ -222,7 +255,8 @@ def main():
         "config": {"workload": "C1+C2+C3: ORB extract (1000 feats, 1.2, 8 levels, FAST 20/7) || LSD+LBD "
                                "(200 lines, scale 0.8, 2 octaves) on two HIP streams, then ORB kNN-2 + "
                                "LineMatcher::match vs previous frame",
-                   "batch": B, "width": W, "height": H, "parallelism": f"frames-sharded x{world}"},
+                   "batch": B, "width": W, "height": H, "parallelism": f"frames-sharded x{world}",
+                   "gather": bool(args.gather)},
         "roofline": roof,
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "dominant_stage": dom,

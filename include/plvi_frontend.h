@@ -117,6 +117,13 @@ int plvi_orb_level_quota(plvi_orb_extractor* h, int* quota);
 int plvi_orb_profile(plvi_orb_extractor* h, int enable);
 int plvi_orb_profile_read(plvi_orb_extractor* h, float* stage_ms, int* runs);
 
+/* Per-launch timing of the pyramid blur + FAST kernel (bench.py's roofline
+ * kernel): enable=1 resets and records an event pair around every launch on
+ * its launch stream (up to 4096 launches); read synchronises and returns the
+ * summed milliseconds and the launch count. */
+int plvi_orb_kernel_timing(plvi_orb_extractor* h, int enable);
+int plvi_orb_kernel_timing_read(plvi_orb_extractor* h, float* total_ms, int* launches);
+
 /* ------------------------------------------------------------------ Lines
  * Replaces ORB_SLAM3::Lineextractor (include/LineExtractor.h:49-93,
  * src/LineExtractor.cc:39-117): LSDDetectorC pyramid + LSD
@@ -325,6 +332,8 @@ int plvi_frame_extract_batch(plvi_orb_extractor* orb, plvi_line_extractor* lines
 int plvi_device_malloc(void** ptr, size_t bytes);
 int plvi_device_free(void* ptr);
 int plvi_memcpy(void* dst, const void* src, size_t bytes, int kind);
+/* Same, asynchronous on `stream` (hipStream_t). */
+int plvi_memcpy_async(void* dst, const void* src, size_t bytes, int kind, void* stream);
 int plvi_device_synchronize(void);
 
 /* Device/library information for diagnostics. */

@@ -30,6 +30,14 @@ extern "C" int plvi_memcpy(void* dst, const void* src, size_t bytes, int kind) {
     return PLVI_OK;
 }
 
+extern "C" int plvi_memcpy_async(void* dst, const void* src, size_t bytes, int kind, void* stream) {
+    const hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost
+                                                                         : hipMemcpyDeviceToDevice;
+    if (kind < 1 || kind > 3) return PLVI_E_BADARG;
+    PLVI_CHECK(hipMemcpyAsync(dst, src, bytes, k, (hipStream_t)stream));
+    return PLVI_OK;
+}
+
 extern "C" int plvi_device_synchronize(void) {
     PLVI_CHECK(hipDeviceSynchronize());
     return PLVI_OK;

@@ -87,7 +87,36 @@ struct OrbPipeline {
 
     ~OrbPipeline() {
         for (auto e : evs) (void)hipEventDestroy(e);
+        for (auto e : kev) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    // Per-launch timing of the blur + FAST kernel (bench.py's roofline kernel):
+    // an event pair on the launch stream around every launch while enabled.
+    static constexpr int kKRing = 4096;
+    bool ktime = false;
+    int kn = 0;
+    std::vector<hipEvent_t> kev;
+    int ktiming(int on) {
+        if (on && kev.empty()) {
+            kev.resize(2 * kKRing);
+            for (auto& e : kev) PLVI_CHECK(hipEventCreate(&e));
+        }
+        ktime = on != 0;
+        if (on) kn = 0;
+        return PLVI_OK;
+    }
+    int ktiming_read(float* total_ms, int* launches) {
+        float tot = 0.f;
+        for (int i = 0; i < kn; ++i) {
+            PLVI_CHECK(hipEventSynchronize(kev[2 * i + 1]));
+            float t = 0.f;
+            PLVI_CHECK(hipEventElapsedTime(&t, kev[2 * i], kev[2 * i + 1]));
+            tot += t;
+        }
+        if (total_ms) *total_ms = tot;
+        if (launches) *launches = kn;
+        return PLVI_OK;
     }
 
     int profile(int on) {
@@ -300,9 +329,15 @@ struct OrbPipeline {
                                rtab[l].xmax, (const int*)(T + tabYrow[l]), (const short*)(T + tabYb[l]));
         }
         // K1b: blur + FAST score of every level (level 0 also copies the frame into its plane)
+        const bool kt = ktime && kn < kKRing;
+        if (kt) PLVI_CHECK(hipEventRecord(kev[2 * kn], st));
         hipLaunchKernelGGL(orb_blur_fast_kernel, dim3((unsigned)strips.size(), nf), dim3(64), 0, st,
                            d_lv.as<OrbLevelDev>(), d_strips.as<OrbStripDev>(), d_frames, frame_stride, row_stride, P,
                            Bl, Sc, taps[0], taps[1], taps[2], taps[3], tmin);
+        if (kt) {
+            PLVI_CHECK(hipEventRecord(kev[2 * kn + 1], st));
+            ++kn;
+        }
         mark(1, st);
         // K2 cell NMS -> candidate map (zeroed first: only detection windows are written)
         PLVI_CHECK(hipMemsetAsync(Cd, 0, pyrBytesFrameTotal, st));
@@ -466,4 +501,16 @@ extern "C" int plvi_orb_profile_read(plvi_orb_extractor* h, float* stage_ms, int
     if (!h || !stage_ms) return PLVI_E_BADARG;
     PLVI_CHECK(hipSetDevice(h->p.device));
     return h->p.profile_read(stage_ms, runs);
+}
+
+extern "C" int plvi_orb_kernel_timing(plvi_orb_extractor* h, int enable) {
+    if (!h) return PLVI_E_BADARG;
+    PLVI_CHECK(hipSetDevice(h->p.device));
+    return h->p.ktiming(enable);
+}
+
+extern "C" int plvi_orb_kernel_timing_read(plvi_orb_extractor* h, float* total_ms, int* launches) {
+    if (!h) return PLVI_E_BADARG;
+    PLVI_CHECK(hipSetDevice(h->p.device));
+    return h->p.ktiming_read(total_ms, launches);
 }

@@ -78,6 +78,8 @@ def _declare(lib):
         "plvi_orb_level_quota": ([V, V], I),
         "plvi_orb_profile": ([V, I], I),
         "plvi_orb_profile_read": ([V, V, P], I),
+        "plvi_orb_kernel_timing": ([V, I], I),
+        "plvi_orb_kernel_timing_read": ([V, V, P], I),
         "plvi_hamming_knn2_batch": ([V, V, I, V, V, I, I, V, V, V, V, V], I),
         "plvi_hamming_knn2": ([V, I, V, I, V, V, V, V], I),
         "plvi_line_match_nnr": ([V, I, V, I, F, V], I),
@@ -109,6 +111,7 @@ def _declare(lib):
         "plvi_device_malloc": ([c_void_pp, S], I),
         "plvi_device_free": ([V], I),
         "plvi_memcpy": ([V, V, S, I], I),
+        "plvi_memcpy_async": ([V, V, S, I, V], I),
         "plvi_device_synchronize": ([], I),
     }
     for name, (args, res) in sig.items():
@@ -251,6 +254,17 @@ class ORBextractor:
         runs = ctypes.c_int()
         _check(self._lib.plvi_orb_profile_read(self._h, _ptr(ms), ctypes.byref(runs)), "plvi_orb_profile_read")
         return dict(zip(self.ORB_STAGES, ms.tolist())), runs.value
+
+    def kernel_timing(self, enable=True):
+        """Event pair around every blur + FAST kernel launch (roofline kernel)."""
+        _check(self._lib.plvi_orb_kernel_timing(self._h, int(enable)), "plvi_orb_kernel_timing")
+
+    def kernel_timing_read(self):
+        tot = ctypes.c_float()
+        n = ctypes.c_int()
+        _check(self._lib.plvi_orb_kernel_timing_read(self._h, ctypes.byref(tot), ctypes.byref(n)),
+               "plvi_orb_kernel_timing_read")
+        return tot.value, n.value
 
     # --- reference getters ---------------------------------------------------
     def _tables(self):

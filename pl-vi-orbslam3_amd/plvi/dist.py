@@ -50,3 +50,27 @@ def sum_over_ranks(value, world, device="cpu"):
     t = torch.tensor([int(value)], dtype=torch.int64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return int(t.item())
+
+
+def gather_tables(tables, world):
+    """SURVEY §8e / BASELINE C4: collect every rank's fixed-capacity per-frame
+    tables (e.g. counts [B], keypoints [B, cap, 28 B], descriptors
+    [B, cap, 32]) on every rank, rank-major — one all_gather_into_tensor per
+    table (RCCL over xGMI on GPUs, gloo on CPU).  Tables are byte tensors of
+    identical shape on all ranks; returns a list of [world, *shape] tensors.
+    Not on the extract+match data path: frames are independent per rank."""
+    import torch
+    import torch.distributed as dist
+    out = []
+    for t in tables:
+        t = t.contiguous()
+        if world == 1:
+            out.append(t.unsqueeze(0).clone())
+            continue
+        g = torch.empty((world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        if t.device.type == "cpu":  # gloo has no all_gather_into_tensor
+            dist.all_gather(list(g.unbind(0)), t)
+        else:
+            dist.all_gather_into_tensor(g, t)
+        out.append(g)
+    return out

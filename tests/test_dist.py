@@ -27,7 +27,13 @@ def _worker(rank, world, port, q):
     pdist.barrier(w)
     el = pdist.max_over_ranks(0.5 + r, w)
     total = pdist.sum_over_ranks(frames.shape[0], w)
-    q.put((r, el, total, int(frames.astype(np.int64).sum())))
+    import torch
+    counts = torch.tensor([10 * r + 1, 10 * r + 2], dtype=torch.int32)
+    desc = torch.full((2, 5, 32), r + 7, dtype=torch.uint8)
+    gc, gd = pdist.gather_tables([counts, desc], w)
+    ok = (gc.tolist() == [[1, 2], [11, 12]] and gd.shape == (2, 2, 5, 32) and int(gd[0].max()) == 7
+          and int(gd[1].min()) == 8)
+    q.put((r, el, total, int(frames.astype(np.int64).sum()), ok))
     import torch.distributed as dist
     dist.destroy_process_group()
 
@@ -46,3 +52,4 @@ def test_gloo_world2_sharding_and_max_time():
     assert [o[1] for o in out] == [1.5, 1.5]       # slowest rank's time on every rank
     assert [o[2] for o in out] == [4, 4]           # whole-job frame count
     assert out[0][3] != out[1][3]                  # each rank owns different frames
+    assert all(o[4] for o in out)                  # per-frame tables gathered rank-major on every rank

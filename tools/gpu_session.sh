@@ -23,7 +23,8 @@ PARGS=${PROF_ARGS:---steps 3 --warmup 1 --no-cpu-baseline}
 cd /tmp && export TMPDIR=/tmp
 if [ "${SKIP_PROF:-0}" != 1 ]; then
   echo "== rocprof stats"
-  timeout -k 10 ${PROF_T:-400} rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py $PARGS > $OUT/prof.log 2>&1
+  # the bench command itself (default arguments unless STATS_ARGS is set)
+  timeout -k 10 ${PROF_T:-400} rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py ${STATS_ARGS:-} > $OUT/prof.log 2>&1
   rc=$?; tail -3 $OUT/prof.log; fatal $rc rocprof hard
 fi
 if [ "${SKIP_PMC:-0}" != 1 ]; then
