@@ -18,6 +18,7 @@ Also reported: roofline of the dominant kernel stage (HIP events on the
 launch stream), and the CPU oracle timed on a bounded sample (rank 0, N=1).
 """
 import argparse
+import ctypes
 import json
 import os
 import pathlib
@@ -101,6 +102,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-bow", action="store_true", help="skip the DBoW2 transform stage timing")
+    ap.add_argument("--no-proj", action="store_true", help="skip the SearchByProjection stage timing")
     ap.add_argument("--gather", action="store_true",
                     help="BASELINE C4: all-gather every step's per-frame ORB/line tables over RCCL (timed)")
     args = ap.parse_args()
@@ -216,11 +218,57 @@ def main():
         ev1.record(sA)
         torch.cuda.synchronize()
         bow_ms = ev0.elapsed_time(ev1) / nprof
+    # SearchByProjection (Tracking::TrackWithMotionModel):
+    # AssignFeaturesToGrid of the batch, then frame t vs frame t-1's keypoints
+    # as MapPoints (identity motion, depth 5, their own descriptors), th = 15
+    proj_ms = None
+    if not args.no_proj:
+        gp = plvi.GridParams(0.0, 0.0, *[float(x) for x in plvi.grid_geometry(W, H)[4:]])
+        cell_off = torch.empty(B * 3073, dtype=torch.int32, device=f"cuda:{dev}")
+        cell_idx = torch.empty(B * cap, dtype=torch.int32, device=f"cuda:{dev}")
+        kpt = torch.empty(B * cap * 7, dtype=torch.float32, device=f"cuda:{dev}")
+        lib.plvi_memcpy_async(kpt.data_ptr(), kp_p, B * cap * 28, 3, sA.cuda_stream)
+        torch.cuda.synchronize()
+        kv = kpt.view(B, cap, 7)
+        fx, fy, cx, cy, z = 458.654, 457.296, 367.215, 248.375, 5.0
+        x3 = torch.stack([(kv[..., 0] - cx) * z / fx, (kv[..., 1] - cy) * z / fy,
+                          torch.full_like(kv[..., 0], z)], -1).contiguous()
+        loct = kv[..., 5].view(torch.int32).contiguous()
+        lang = kv[..., 3].contiguous()
+        lflags = torch.full((B * cap,), 3, dtype=torch.uint8, device=f"cuda:{dev}")
+        pp = plvi.ProjParams()
+        pp.fx, pp.fy, pp.cx, pp.cy, pp.mbf, pp.th = fx, fy, cx, cy, 40.0, 15.0
+        geo = plvi.grid_geometry(W, H)
+        pp.min_x, pp.max_x, pp.min_y, pp.max_y, pp.inv_w, pp.inv_h = [float(x) for x in geo]
+        pp.check_orientation, pp.nlevels = 1, 8
+        for i, sfac in enumerate(orb.GetScaleFactors()):
+            pp.scale_factors[i] = float(sfac)
+        pm = torch.empty((B - 1) * cap, dtype=torch.int32, device=f"cuda:{dev}")
+        pn = torch.empty(B, dtype=torch.int32, device=f"cuda:{dev}")
+
+        def run_proj():
+            plvi.assign_grid_batch(kp_p, co_p, cap, B, gp, cell_off.data_ptr(), cell_idx.data_ptr(), sA.cuda_stream)
+            rc = lib.plvi_search_by_projection_batch(
+                B - 1, ctypes.byref(pp), kp_p + 28 * cap, de_p + 32 * cap, co_p + 4, cap, None, None,
+                cell_off.data_ptr() + 4 * 3073, cell_idx.data_ptr() + 4 * cap, x3.data_ptr(), loct.data_ptr(),
+                lang.data_ptr(), de_p, lflags.data_ptr(), co_p, cap, pm.data_ptr(), pn.data_ptr(), sA.cuda_stream)
+            if rc:
+                raise RuntimeError(f"projection {rc}")
+        run_proj()
+        torch.cuda.synchronize()
+        ev0.record(sA)
+        for _ in range(nprof):
+            run_proj()
+        ev1.record(sA)
+        torch.cuda.synchronize()
+        proj_ms = ev0.elapsed_time(ev1) / nprof
     stage_ms = {f"orb.{k}": v / runs for k, v in st_orb.items()}
     stage_ms.update({f"lines.{k}": v / lruns for k, v in st_lines.items()})
     stage_ms["match"] = match_ms / nprof
     if bow_ms is not None:
         stage_ms["bow.transform"] = bow_ms
+    if proj_ms is not None:
+        stage_ms["proj.grid+search"] = proj_ms
 
     pdist.barrier(world)
     torch.cuda.synchronize()
@@ -241,7 +289,7 @@ def main():
     ktot, kn = orb.kernel_timing_read()
     kavg_ms = ktot / max(kn, 1)
     bf_bytes = blur_fast_bytes(W, H) * B
-    dom = max((k for k in stage_ms if k != "bow.transform"), key=stage_ms.get)
+    dom = max((k for k in stage_ms if k not in ("bow.transform", "proj.grid+search")), key=stage_ms.get)
     roof = {
         "bound": "hbm", "kernel": "orb_blur_fast_kernel (7x7 blur + FAST score, all 8 levels, one launch)",
         "achieved": bf_bytes / (kavg_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -316,6 +316,65 @@ int plvi_vocab_transform_batch(plvi_vocabulary* h, const uint8_t* d_desc, const 
                                unsigned* d_fv_node, int* d_fv_off, unsigned* d_fv_idx, int* d_fv_n,
                                unsigned* d_feat_word, unsigned* d_feat_nid, void* stream);
 
+/* ------------------------------------------------------ SearchByProjection
+ * The steady-state frame-to-frame ORB matcher of Tracking::TrackWithMotionModel
+ * (src/Tracking.cc:3957): Frame::AssignFeaturesToGrid (src/Frame.cc:644-675),
+ * Frame::GetFeaturesInArea (:1006-1075) and
+ * ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono)
+ * (src/ORBmatcher.cc:1962-2178, single camera: Nleft == -1). */
+
+/* Frame grid geometry: mnMinX, mnMinY, mfGridElementWidthInv/HeightInv
+ * (Frame.cc:156-157); the grid is FRAME_GRID_COLS x ROWS = 64 x 48. */
+typedef struct plvi_grid_params {
+  float min_x, min_y, inv_w, inv_h;
+} plvi_grid_params;
+
+/* AssignFeaturesToGrid of n_frames keypoint tables [n_frames][cap]
+ * (mvKeysUn; counts d_count) as CSR: cell (ix, iy) = ix*48 + iy lists its
+ * keypoints at d_cell_idx[f*cap + d_cell_off[f*3073 + cell] ...] in index
+ * order (= mGrid[ix][iy]).  cap <= 8192.  Asynchronous. */
+int plvi_assign_grid_batch(const plvi_keypoint* d_kps, const int* d_count, int cap, int n_frames,
+                           const plvi_grid_params* gp, int* d_cell_off, int* d_cell_idx, void* stream);
+
+typedef struct plvi_proj_params {
+  float fx, fy, cx, cy;            /* Pinhole mvParameters (CameraModels/Pinhole.cpp:30-33) */
+  float mbf;                       /* CurrentFrame.mbf (mvuRight check, :2041-2047) */
+  float th;                        /* window radius at octave 0 (radius = th * mvScaleFactors[octave]) */
+  float min_x, max_x, min_y, max_y; /* mnMinX, mnMaxX, mnMinY, mnMaxY */
+  float inv_w, inv_h;              /* mfGridElementWidthInv / HeightInv */
+  int forward, backward;           /* bForward / bBackward (:1982-1983; both 0 for bMono) */
+  int check_orientation;           /* mbCheckOrientation */
+  int nlevels;
+  float scale_factors[16];         /* CurrentFrame.mvScaleFactors */
+} plvi_proj_params;
+
+/* Batched SearchByProjection over n_pairs (CurrentFrame, LastFrame) pairs.
+ * Current frame p: keypoints/descriptors [p][cur_cap] (mvKeysUn, counts
+ * d_cur_n), grid CSR from plvi_assign_grid_batch, blocked[i2] =
+ * mvpMapPoints[i2] && Observations() > 0 on entry (NULL = none), mvuRight
+ * (NULL = none).  Last frame p: [p][last_cap] x3Dc = Rcw*x3Dw + tcw of the
+ * point's MapPoint (3 floats), octave (mvKeys[i].octave), angle
+ * (mvKeysUn[i].angle), MapPoint descriptor (32 B), flags bit0 = has a
+ * MapPoint and is not an outlier, bit1 = that MapPoint's Observations() > 0.
+ * Output match [p][cur_cap]: LastFrame index whose MapPoint
+ * mvpMapPoints[i2] holds on return, -2 = set to NULL by the rotation filter,
+ * -1 = untouched; nmatches [p] = the return value.  cur_cap, last_cap <= 65535
+ * and the LDS footprint (~19 B per current + 8 B per last keypoint + 12 KB)
+ * <= 160 KB. */
+int plvi_search_by_projection_batch(int n_pairs, const plvi_proj_params* p, const plvi_keypoint* d_cur_kps,
+                                    const uint8_t* d_cur_desc, const int* d_cur_n, int cur_cap,
+                                    const uint8_t* d_cur_blocked, const float* d_cur_uright, const int* d_cell_off,
+                                    const int* d_cell_idx, const float* d_x3dc, const int* d_last_octave,
+                                    const float* d_last_angle, const uint8_t* d_mp_desc, const uint8_t* d_last_flags,
+                                    const int* d_last_n, int last_cap, int* d_match, int* d_nmatches, void* stream);
+
+/* One pair from host memory, synchronous (grid built on the device).
+ * Returns nmatches (>= 0) or an error. */
+int plvi_search_by_projection(const plvi_proj_params* p, const plvi_keypoint* cur_kps, const uint8_t* cur_desc,
+                              int n_cur, const uint8_t* cur_blocked, const float* cur_uright, const float* x3dc,
+                              const int* last_octave, const float* last_angle, const uint8_t* mp_desc,
+                              const uint8_t* last_flags, int n_last, int* match);
+
 /* ------------------------------------------------------------ Frame level
  * Frame::Frame's extraction (src/Frame.cc:537-641, ExtractORB/ExtractLine
  * :677-692): the ORB and line extractors on the same batch of frames, run

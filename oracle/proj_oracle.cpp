@@ -1,0 +1,231 @@
+// oracle/proj_oracle.cpp — TEST INFRASTRUCTURE ONLY.
+//
+// CPU restatement of the steady-state frame-to-frame ORB matcher and the grid
+// it searches ("parity unpinned": no reference test pins them):
+//   Frame::AssignFeaturesToGrid      src/Frame.cc:644-675
+//   Frame::PosInGrid                 src/Frame.cc:1077-1087
+//   Frame::GetFeaturesInArea         src/Frame.cc:1006-1075
+//   ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono)
+//                                    src/ORBmatcher.cc:1962-2178 (Nleft == -1 branch)
+//   ORBmatcher::ComputeThreeMaxima   src/ORBmatcher.cc:2304-2345
+//   Pinhole::project                 src/CameraModels/Pinhole.cpp:30-39
+// The pose product x3Dc = Rcw*x3Dw + tcw (cv::Mat) is an input: it is taken
+// from the caller, as the drop-in shim keeps it on the host.
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+namespace {
+
+constexpr int kCols = 64, kRows = 48;  // FRAME_GRID_COLS / FRAME_GRID_ROWS (include/Frame.h:47-48)
+constexpr int kThHigh = 100, kHisto = 30;
+
+struct Kp {
+    float x, y;
+    int octave;
+    float angle;
+};
+
+struct Grid {
+    std::vector<size_t> cell[kCols][kRows];
+};
+
+int dist256(const uint8_t* a, const uint8_t* b) {
+    int d = 0;
+    for (int i = 0; i < 8; ++i) {
+        int32_t pa, pb;
+        std::memcpy(&pa, a + 4 * i, 4);
+        std::memcpy(&pb, b + 4 * i, 4);
+        unsigned v = (unsigned)(pa ^ pb);
+        v = v - ((v >> 1) & 0x55555555);
+        v = (v & 0x33333333) + ((v >> 2) & 0x33333333);
+        d += (((v + (v >> 4)) & 0xF0F0F0F) * 0x1010101) >> 24;
+    }
+    return d;
+}
+
+bool pos_in_grid(const Kp& kp, float minX, float minY, float invW, float invH, int& px, int& py) {
+    px = (int)std::round((kp.x - minX) * invW);  // std::round(float)
+    py = (int)std::round((kp.y - minY) * invH);
+    return !(px < 0 || px >= kCols || py < 0 || py >= kRows);
+}
+
+void assign_grid(const std::vector<Kp>& kps, float minX, float minY, float invW, float invH, Grid& g) {
+    for (int i = 0; i < (int)kps.size(); ++i) {
+        int px, py;
+        if (pos_in_grid(kps[i], minX, minY, invW, invH, px, py)) g.cell[px][py].push_back(i);
+    }
+}
+
+std::vector<size_t> features_in_area(const Grid& g, const std::vector<Kp>& kps, float minX, float minY, float invW,
+                                     float invH, const float& x, const float& y, const float& r, int minLevel,
+                                     int maxLevel) {
+    std::vector<size_t> v;
+    const float factorX = r, factorY = r;
+    const int nMinCellX = std::max(0, (int)std::floor((x - minX - factorX) * invW));
+    if (nMinCellX >= kCols) return v;
+    const int nMaxCellX = std::min(kCols - 1, (int)std::ceil((x - minX + factorX) * invW));
+    if (nMaxCellX < 0) return v;
+    const int nMinCellY = std::max(0, (int)std::floor((y - minY - factorY) * invH));
+    if (nMinCellY >= kRows) return v;
+    const int nMaxCellY = std::min(kRows - 1, (int)std::ceil((y - minY + factorY) * invH));
+    if (nMaxCellY < 0) return v;
+    const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+    for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
+        for (int iy = nMinCellY; iy <= nMaxCellY; iy++) {
+            const std::vector<size_t>& vCell = g.cell[ix][iy];
+            for (size_t j = 0; j < vCell.size(); j++) {
+                const Kp& kp = kps[vCell[j]];
+                if (bCheckLevels) {
+                    if (kp.octave < minLevel) continue;
+                    if (maxLevel >= 0 && kp.octave > maxLevel) continue;
+                }
+                const float distx = kp.x - x, disty = kp.y - y;
+                if (std::fabs(distx) < factorX && std::fabs(disty) < factorY) v.push_back(vCell[j]);
+            }
+        }
+    return v;
+}
+
+void three_maxima(const std::vector<int>* histo, int L, int& ind1, int& ind2, int& ind3) {
+    int max1 = 0, max2 = 0, max3 = 0;
+    for (int i = 0; i < L; i++) {
+        const int s = (int)histo[i].size();
+        if (s > max1) {
+            max3 = max2; max2 = max1; max1 = s;
+            ind3 = ind2; ind2 = ind1; ind1 = i;
+        } else if (s > max2) {
+            max3 = max2; max2 = s;
+            ind3 = ind2; ind2 = i;
+        } else if (s > max3) {
+            max3 = s;
+            ind3 = i;
+        }
+    }
+    if (max2 < 0.1f * (float)max1) {
+        ind2 = -1;
+        ind3 = -1;
+    } else if (max3 < 0.1f * (float)max1) {
+        ind3 = -1;
+    }
+}
+
+std::vector<Kp> make_kps(int n, const float* x, const float* y, const int* oct, const float* ang) {
+    std::vector<Kp> k(n);
+    for (int i = 0; i < n; ++i) k[i] = Kp{x[i], y[i], oct ? oct[i] : 0, ang ? ang[i] : 0.f};
+    return k;
+}
+
+}  // namespace
+
+// AssignFeaturesToGrid as CSR: cell (ix, iy) = ix*48 + iy, cell_off[3073].
+extern "C" int oracle_assign_grid(const float* x, const float* y, int n, float minX, float minY, float invW,
+                                  float invH, int* cell_off, int* cell_idx) {
+    Grid g;
+    assign_grid(make_kps(n, x, y, nullptr, nullptr), minX, minY, invW, invH, g);
+    int c = 0;
+    cell_off[0] = 0;
+    for (int ix = 0; ix < kCols; ++ix)
+        for (int iy = 0; iy < kRows; ++iy) {
+            for (size_t j : g.cell[ix][iy]) cell_idx[c++] = (int)j;
+            cell_off[ix * kRows + iy + 1] = c;
+        }
+    return c;
+}
+
+// GetFeaturesInArea on a grid built from the same keypoints; returns the count.
+extern "C" int oracle_features_in_area(const float* kx, const float* ky, const int* oct, int n, float minX,
+                                       float minY, float invW, float invH, float x, float y, float r, int minLevel,
+                                       int maxLevel, int* out) {
+    const std::vector<Kp> kps = make_kps(n, kx, ky, oct, nullptr);
+    Grid g;
+    assign_grid(kps, minX, minY, invW, invH, g);
+    const std::vector<size_t> v = features_in_area(g, kps, minX, minY, invW, invH, x, y, r, minLevel, maxLevel);
+    for (size_t i = 0; i < v.size(); ++i) out[i] = (int)v[i];
+    return (int)v.size();
+}
+
+// SearchByProjection(CurrentFrame, LastFrame, th, bMono), Nleft == -1.
+//  cur_*: CurrentFrame.mvKeysUn (x, y, octave, angle), mDescriptors, blocked[i2]
+//         = mvpMapPoints[i2] && Observations() > 0 on entry, mvuRight (or NULL).
+//  last_*: per LastFrame point i: flags bit0 = has a MapPoint and not an
+//         outlier, bit1 = that MapPoint's Observations() > 0; x3Dc = Rcw*x3Dw+tcw;
+//         octave = LastFrame.mvKeys[i].octave, angle = mvKeysUn[i].angle;
+//         mp_desc = pMP->GetDescriptor().
+//  out: match[i2] = LastFrame index whose MapPoint mvpMapPoints[i2] holds on
+//       return, -2 = set to NULL by the rotation filter, -1 = untouched.
+extern "C" int oracle_search_by_projection(
+    int n_cur, const float* cx_, const float* cy_, const int* coct, const float* cang, const uint8_t* cdesc,
+    const uint8_t* cblocked, const float* curight, float minX, float maxX, float minY, float maxY, float invW,
+    float invH, const float* scale_factors, float fx, float fy, float cxp, float cyp, float mbf, int n_last,
+    const uint8_t* lflags, const float* x3dc, const int* loct, const float* lang, const uint8_t* mpdesc, float th,
+    int bForward, int bBackward, int check_ori, int* match) {
+    const std::vector<Kp> kps = make_kps(n_cur, cx_, cy_, coct, cang);
+    Grid g;
+    assign_grid(kps, minX, minY, invW, invH, g);
+    std::vector<int> mp(n_cur, -1);          // index of the LastFrame point whose MapPoint is stored
+    std::vector<char> blocked(cblocked, cblocked + n_cur);  // mvpMapPoints[i2] && Observations()>0
+    std::vector<int> rotHist[kHisto];
+    const float factor = 1.0f / kHisto;
+    int nmatches = 0;
+    for (int i = 0; i < n_last; i++) {
+        if (!(lflags[i] & 1)) continue;
+        const float xc = x3dc[3 * i], yc = x3dc[3 * i + 1], zc = x3dc[3 * i + 2];
+        const float invzc = 1.0 / zc;
+        if (invzc < 0) continue;
+        const float u = fx * xc / zc + cxp, v = fy * yc / zc + cyp;
+        if (u < minX || u > maxX) continue;
+        if (v < minY || v > maxY) continue;
+        const int nLastOctave = loct[i];
+        const float radius = th * scale_factors[nLastOctave];
+        std::vector<size_t> vIndices2;
+        if (bForward)
+            vIndices2 = features_in_area(g, kps, minX, minY, invW, invH, u, v, radius, nLastOctave, -1);
+        else if (bBackward)
+            vIndices2 = features_in_area(g, kps, minX, minY, invW, invH, u, v, radius, 0, nLastOctave);
+        else
+            vIndices2 = features_in_area(g, kps, minX, minY, invW, invH, u, v, radius, nLastOctave - 1,
+                                         nLastOctave + 1);
+        if (vIndices2.empty()) continue;
+        int bestDist = 256, bestIdx2 = -1;
+        for (size_t i2 : vIndices2) {
+            if (blocked[i2]) continue;
+            if (curight && curight[i2] > 0) {
+                const float ur = u - mbf * invzc;
+                const float er = std::fabs(ur - curight[i2]);
+                if (er > radius) continue;
+            }
+            const int dist = dist256(mpdesc + 32 * (size_t)i, cdesc + 32 * i2);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx2 = (int)i2;
+            }
+        }
+        if (bestDist <= kThHigh) {
+            mp[bestIdx2] = i;
+            blocked[bestIdx2] = (lflags[i] & 2) ? 1 : 0;  // the stored MapPoint's Observations() > 0
+            nmatches++;
+            if (check_ori) {
+                float rot = lang[i] - kps[bestIdx2].angle;
+                if (rot < 0.0) rot += 360.0f;
+                int bin = (int)std::round(rot * factor);
+                if (bin == kHisto) bin = 0;
+                rotHist[bin].push_back(bestIdx2);
+            }
+        }
+    }
+    std::vector<char> nulled(n_cur, 0);
+    if (check_ori) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        three_maxima(rotHist, kHisto, ind1, ind2, ind3);
+        for (int b = 0; b < kHisto; b++)
+            if (b != ind1 && b != ind2 && b != ind3)
+                for (int idx : rotHist[b]) {
+                    nulled[idx] = 1;
+                    nmatches--;
+                }
+    }
+    for (int i2 = 0; i2 < n_cur; ++i2) match[i2] = nulled[i2] ? -2 : mp[i2];
+    return nmatches;
+}

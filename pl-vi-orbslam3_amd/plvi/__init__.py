@@ -47,6 +47,29 @@ class PlviError(RuntimeError):
         self.code = code
 
 
+class GridParams(ctypes.Structure):
+    """plvi_grid_params: mnMinX, mnMinY, mfGridElementWidthInv, mfGridElementHeightInv."""
+    _fields_ = [("min_x", ctypes.c_float), ("min_y", ctypes.c_float), ("inv_w", ctypes.c_float),
+                ("inv_h", ctypes.c_float)]
+
+
+class ProjParams(ctypes.Structure):
+    """plvi_proj_params (include/plvi_frontend.h)."""
+    _fields_ = [("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
+                ("mbf", ctypes.c_float), ("th", ctypes.c_float), ("min_x", ctypes.c_float),
+                ("max_x", ctypes.c_float), ("min_y", ctypes.c_float), ("max_y", ctypes.c_float),
+                ("inv_w", ctypes.c_float), ("inv_h", ctypes.c_float), ("forward", ctypes.c_int),
+                ("backward", ctypes.c_int), ("check_orientation", ctypes.c_int), ("nlevels", ctypes.c_int),
+                ("scale_factors", ctypes.c_float * 16)]
+
+
+def grid_geometry(width, height):
+    """Frame ctor grid geometry without distortion (mnMinX = 0, mnMaxX = cols, ...;
+    Frame.cc:156-157): (min_x, max_x, min_y, max_y, inv_w, inv_h) as float32."""
+    f = np.float32
+    return (f(0), f(width), f(0), f(height), f(64) / (f(width) - f(0)), f(48) / (f(height) - f(0)))
+
+
 class OrbParams(ctypes.Structure):
     _fields_ = [("nfeatures", ctypes.c_int), ("scale_factor", ctypes.c_float), ("nlevels", ctypes.c_int),
                 ("ini_th_fast", ctypes.c_int), ("min_th_fast", ctypes.c_int)]
@@ -101,6 +124,9 @@ def _declare(lib):
         "plvi_line_match_grid": ([V, V, I, I, I, V, V, V, V, I, I, I, I, I, I, V], I),
         "plvi_line_match_grid_batch": ([I, V, V, V, I, I, I, V, V, I, V, V, V, I, I, I, I, I, I, V, V, V, V], I),
         "plvi_frame_extract_batch": ([V, V, V, I, S, S, I, I, V], I),
+        "plvi_assign_grid_batch": ([V, V, I, I, V, V, V, V], I),
+        "plvi_search_by_projection_batch": ([I, V, V, V, V, I, V, V, V, V, V, V, V, V, V, V, I, V, V, V], I),
+        "plvi_search_by_projection": ([V, V, V, I, V, V, V, V, V, V, V, I, V], I),
         "plvi_vocab_load_text": ([ctypes.c_char_p, I, I, c_void_pp], I),
         "plvi_vocab_create": ([I, I, I, I, I, V, V, V, V, I, c_void_pp], I),
         "plvi_vocab_destroy": ([V], I),
@@ -494,6 +520,31 @@ class ORBmatcher:
                    "plvi_search_by_bow")
         return n, out[:len(fd)]
 
+    def SearchByProjection(self, params, cur_kps, cur_desc, last_x3dc, last_octave, last_angle, mp_desc,
+                           last_flags, cur_blocked=None, cur_uright=None):
+        """SearchByProjection(CurrentFrame, LastFrame, th, bMono) (src/ORBmatcher.cc:1962-2178) with
+        mbCheckOrientation = checkOri of this matcher.  params: ProjParams (th, camera, grid, bounds,
+        scale factors); cur_kps: mvKeysUn (KEYPOINT_DTYPE); last_*: see include/plvi_frontend.h.
+        Returns (nmatches, match) with match[i2] = LastFrame index, -2 (nulled) or -1 (untouched)."""
+        params.check_orientation = int(self.check_orientation)
+        ck = np.ascontiguousarray(cur_kps).view(KEYPOINT_DTYPE)
+        cd = np.ascontiguousarray(cur_desc, np.uint8).reshape(-1, 32)
+        n = len(ck)
+        x3 = np.ascontiguousarray(last_x3dc, np.float32).reshape(-1, 3)
+        lo = np.ascontiguousarray(last_octave, np.int32)
+        la = np.ascontiguousarray(last_angle, np.float32)
+        md = np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32)
+        lf = np.ascontiguousarray(last_flags, np.uint8)
+        cb = None if cur_blocked is None else np.ascontiguousarray(cur_blocked, np.uint8)
+        cu = None if cur_uright is None else np.ascontiguousarray(cur_uright, np.float32)
+        out = np.full(max(n, 1), -1, np.int32)
+        nm = _check(self._lib.plvi_search_by_projection(ctypes.byref(params), _ptr(ck), _ptr(cd), n,
+                                                        None if cb is None else _ptr(cb),
+                                                        None if cu is None else _ptr(cu), _ptr(x3), _ptr(lo),
+                                                        _ptr(la), _ptr(md), _ptr(lf), len(lf), _ptr(out)),
+                    "plvi_search_by_projection")
+        return nm, out[:n]
+
     @staticmethod
     def DescriptorDistance(a, b, line_matcher_quirk=False):
         """Row-wise distances of two n x 32 descriptor tables on the GPU."""
@@ -596,3 +647,11 @@ class ORBVocabulary:
         _check(self._lib.plvi_vocab_transform_features(self._h, _ptr(d), n, levelsup, _ptr(w), _ptr(ni)),
                "plvi_vocab_transform_features")
         return w[:n], ni[:n]
+
+
+def assign_grid_batch(d_kps, d_count, cap, n_frames, grid, d_cell_off, d_cell_idx, stream=None):
+    """Frame::AssignFeaturesToGrid (src/Frame.cc:644-675) of device keypoint tables -> CSR grids."""
+    _check(load().plvi_assign_grid_batch(ctypes.c_void_p(d_kps), ctypes.c_void_p(d_count), cap, n_frames,
+                                         ctypes.byref(grid), ctypes.c_void_p(d_cell_off),
+                                         ctypes.c_void_p(d_cell_idx), ctypes.c_void_p(stream or 0)),
+           "plvi_assign_grid_batch")

@@ -326,3 +326,58 @@ class Vocab:
                                         _p(fi), ctypes.byref(nf), _p(fw), _p(fwt), _p(fni))
         nb, nf = nb.value, nf.value
         return bw[:nb], bv[:nb], fn[:nf], fo[:nf + 1], fi[:fo[nf]], fw[:n], fwt[:n], fni[:n]
+
+
+def assign_grid(kx, ky, grid):
+    """Frame::AssignFeaturesToGrid restatement -> (cell_off[3073], cell_idx)."""
+    lib = load()
+    V, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    lib.oracle_assign_grid.argtypes = [V, V, I, F, F, F, F, V, V]
+    lib.oracle_assign_grid.restype = I
+    kx = np.ascontiguousarray(kx, np.float32); ky = np.ascontiguousarray(ky, np.float32)
+    off = np.zeros(64 * 48 + 1, np.int32); idx = np.zeros(max(len(kx), 1), np.int32)
+    min_x, max_x, min_y, max_y, inv_w, inv_h = grid
+    m = lib.oracle_assign_grid(_p(kx), _p(ky), len(kx), min_x, min_y, inv_w, inv_h, _p(off), _p(idx))
+    return off, idx[:m]
+
+
+def features_in_area(kx, ky, oct_, grid, x, y, r, min_level, max_level):
+    lib = load()
+    V, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    lib.oracle_features_in_area.argtypes = [V, V, V, I, F, F, F, F, F, F, F, I, I, V]
+    lib.oracle_features_in_area.restype = I
+    kx = np.ascontiguousarray(kx, np.float32); ky = np.ascontiguousarray(ky, np.float32)
+    oc = np.ascontiguousarray(oct_, np.int32)
+    out = np.zeros(max(len(kx), 1), np.int32)
+    min_x, max_x, min_y, max_y, inv_w, inv_h = grid
+    n = lib.oracle_features_in_area(_p(kx), _p(ky), _p(oc), len(kx), min_x, min_y, inv_w, inv_h, x, y, r,
+                                    min_level, max_level, _p(out))
+    return out[:n]
+
+
+def search_by_projection(case, th, forward=0, backward=0, check_ori=1):
+    """ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono) restatement -> (nmatches, match)."""
+    lib = load()
+    V, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    lib.oracle_search_by_projection.argtypes = [I, V, V, V, V, V, V, V, F, F, F, F, F, F, V, F, F, F, F, F, I, V,
+                                                V, V, V, V, F, I, I, I, V]
+    lib.oracle_search_by_projection.restype = I
+    c = case
+    k = c["cur_kps"]
+    kx = np.ascontiguousarray(k["x"], np.float32); ky = np.ascontiguousarray(k["y"], np.float32)
+    ko = np.ascontiguousarray(k["octave"], np.int32); ka = np.ascontiguousarray(k["angle"], np.float32)
+    cd = np.ascontiguousarray(c["cur_desc"], np.uint8)
+    cb = np.ascontiguousarray(c["cur_blocked"], np.uint8)
+    cu = None if c.get("cur_uright") is None else np.ascontiguousarray(c["cur_uright"], np.float32)
+    min_x, max_x, min_y, max_y, inv_w, inv_h = c["grid"]
+    sf = np.ascontiguousarray(c["scale_factors"], np.float32)
+    x3 = np.ascontiguousarray(c["x3dc"], np.float32); lf = np.ascontiguousarray(c["flags"], np.uint8)
+    lo = np.ascontiguousarray(c["last_octave"], np.int32); la = np.ascontiguousarray(c["last_angle"], np.float32)
+    md = np.ascontiguousarray(c["mp_desc"], np.uint8)
+    fx, fy, cx, cy, mbf = c["camera"]
+    out = np.full(max(len(kx), 1), -1, np.int32)
+    n = lib.oracle_search_by_projection(len(kx), _p(kx), _p(ky), _p(ko), _p(ka), _p(cd), _p(cb),
+                                        None if cu is None else _p(cu), min_x, max_x, min_y, max_y, inv_w, inv_h,
+                                        _p(sf), fx, fy, cx, cy, mbf, len(lf), _p(lf), _p(x3), _p(lo), _p(la), _p(md),
+                                        th, forward, backward, check_ori, _p(out))
+    return n, out[:len(kx)]

@@ -118,3 +118,67 @@ def stereo_line_case(seed, n=220, W=640, H=480, cols=64, rows=48, ties=True):
     lines1 = np.stack([(s1[:, 0] * inv_w).astype(np.int64), (s1[:, 1] * inv_h).astype(np.int64),
                        (e1[:, 0] * inv_w).astype(np.int64), (e1[:, 1] * inv_h).astype(np.int64)], 1).astype(np.int32)
     return lines1, desc1, grid, desc2, dirs
+
+
+def orb_scale_factors(n=8, sf=1.2):
+    """ORBextractor mvScaleFactor (float cumulative, ORBextractor.cc:415-420)."""
+    s = [np.float32(1.0)]
+    for _ in range(1, n):
+        s.append(np.float32(np.float64(s[-1]) * np.float64(np.float32(sf))))
+    return np.array(s + [np.float32(0)] * (16 - n), np.float32)
+
+
+def projection_case(seed, n_cur=1000, n_last=900, W=752, H=480, uright=False, dup=0.05):
+    """Synthetic SearchByProjection input: current-frame
+    keypoints (mvKeysUn) with descriptors; LastFrame MapPoints whose camera-
+    frame positions project near a current keypoint (70 %) or anywhere (30 %),
+    descriptors = the keypoint's with ~5 % bit flips (or random), a global
+    rotation of 10 degrees; some points invalid / behind the camera / with
+    Observations() == 0, some current keypoints pre-blocked, `dup` of the
+    last points aimed at the same keypoint as another (assignment conflicts)."""
+    from plvi import KEYPOINT_DTYPE, grid_geometry
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = np.float32(458.654), np.float32(457.296), np.float32(367.215), np.float32(248.375)
+    kps = np.zeros(n_cur, KEYPOINT_DTYPE)
+    kps["x"] = rng.uniform(-4, W + 4, n_cur).astype(np.float32)
+    kps["y"] = rng.uniform(-4, H + 4, n_cur).astype(np.float32)
+    kps["octave"] = np.minimum(rng.geometric(0.35, n_cur) - 1, 7)
+    kps["angle"] = rng.uniform(0, 360, n_cur).astype(np.float32)
+    kps["size"] = 31
+    kps["class_id"] = -1
+    desc = rng.integers(0, 256, (n_cur, 32), dtype=np.uint8)
+    near = rng.random(n_last) < 0.7
+    src = rng.integers(0, n_cur, n_last)
+    ndup = int(dup * n_last)
+    src[:ndup] = src[ndup:2 * ndup]
+    u = np.where(near, kps["x"][src] + rng.normal(0, 2.0, n_last), rng.uniform(0, W, n_last))
+    v = np.where(near, kps["y"][src] + rng.normal(0, 2.0, n_last), rng.uniform(0, H, n_last))
+    z = rng.uniform(1.0, 20.0, n_last)
+    z[rng.random(n_last) < 0.02] *= -1
+    x3 = np.stack([(u - cx) * z / fx, (v - cy) * z / fy, z], 1).astype(np.float32)
+    oct_ = np.clip(np.where(near, kps["octave"][src] + rng.integers(-1, 2, n_last), rng.integers(0, 8, n_last)), 0, 7)
+    bits = np.unpackbits(desc[src], axis=1)
+    bits ^= (rng.random(bits.shape) < 0.05).astype(np.uint8)
+    mp = np.where(near[:, None], np.packbits(bits, axis=1), rng.integers(0, 256, (n_last, 32), dtype=np.uint8))
+    ang = np.mod(kps["angle"][src] + 10 + rng.normal(0, 5, n_last), 360).astype(np.float32)
+    flags = ((rng.random(n_last) < 0.92).astype(np.uint8) | ((rng.random(n_last) < 0.85).astype(np.uint8) << 1))
+    case = {"cur_kps": kps, "cur_desc": desc, "cur_blocked": (rng.random(n_cur) < 0.05).astype(np.uint8),
+            "cur_uright": None, "grid": grid_geometry(W, H), "scale_factors": orb_scale_factors(),
+            "x3dc": x3, "flags": flags, "last_octave": oct_.astype(np.int32), "last_angle": ang,
+            "mp_desc": mp.astype(np.uint8), "camera": (fx, fy, cx, cy, np.float32(40.0))}
+    if uright:
+        ur = np.where(rng.random(n_cur) < 0.6, kps["x"] - rng.uniform(0, 30, n_cur), -1).astype(np.float32)
+        case["cur_uright"] = ur
+    return case
+
+
+def proj_params(case, th, forward=0, backward=0):
+    import plvi
+    p = plvi.ProjParams()
+    fx, fy, cx, cy, mbf = case["camera"]
+    p.fx, p.fy, p.cx, p.cy, p.mbf, p.th = fx, fy, cx, cy, mbf, th
+    (p.min_x, p.max_x, p.min_y, p.max_y, p.inv_w, p.inv_h) = case["grid"]
+    p.forward, p.backward, p.nlevels = forward, backward, 8
+    for i, s in enumerate(case["scale_factors"]):
+        p.scale_factors[i] = s
+    return p
