@@ -316,6 +316,29 @@ int plvi_vocab_transform_batch(plvi_vocabulary* h, const uint8_t* d_desc, const 
                                unsigned* d_fv_node, int* d_fv_off, unsigned* d_fv_idx, int* d_fv_n,
                                unsigned* d_feat_word, unsigned* d_feat_nid, void* stream);
 
+/* ----------------------------------------------------------- Undistortion
+ * Frame::UndistortKeyPoints (src/Frame.cc:1124-1157), UndistortKeyLines
+ * (:1159-1197) and ComputeImageBounds (:1199-1226) = cv::undistortPoints
+ * (OpenCV 4.2, 5 iterations, R = I, P = K).  mDistCoef[0] == 0 copies the
+ * points unchanged, as the reference does. */
+typedef struct plvi_camera {
+  float fx, fy, cx, cy; /* mK */
+  float dist[5];        /* mDistCoef: k1, k2, p1, p2[, k3] */
+  int ndist;            /* 4 or 5 */
+} plvi_camera;
+
+/* n points (x, y float pairs, device), asynchronous. */
+int plvi_undistort_points(const plvi_camera* cam, const float* d_xy, int n, float* d_out, void* stream);
+/* mvKeysUn of keypoint tables [n_frames][cap] (counts d_count): each
+ * keypoint copied with its pt undistorted. */
+int plvi_undistort_keypoints_batch(const plvi_camera* cam, const plvi_keypoint* d_kps, const int* d_count, int cap,
+                                   int n_frames, plvi_keypoint* d_out, void* stream);
+/* Undistorted keyline endpoints [n_frames][cap][4] = startX, startY, endX, endY. */
+int plvi_undistort_keylines_batch(const plvi_camera* cam, const plvi_keyline* d_kl, const int* d_count, int cap,
+                                  int n_frames, float* d_endpoints, void* stream);
+/* mnMinX, mnMaxX, mnMinY, mnMaxY (synchronous). */
+int plvi_image_bounds(const plvi_camera* cam, int cols, int rows, float* bounds);
+
 /* ------------------------------------------------------ SearchByProjection
  * The steady-state frame-to-frame ORB matcher of Tracking::TrackWithMotionModel
  * (src/Tracking.cc:3957): Frame::AssignFeaturesToGrid (src/Frame.cc:644-675),

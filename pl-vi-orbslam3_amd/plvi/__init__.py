@@ -53,6 +53,41 @@ class GridParams(ctypes.Structure):
                 ("inv_h", ctypes.c_float)]
 
 
+class Camera(ctypes.Structure):
+    """plvi_camera: mK (fx, fy, cx, cy) and mDistCoef (k1, k2, p1, p2[, k3])."""
+    _fields_ = [("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
+                ("dist", ctypes.c_float * 5), ("ndist", ctypes.c_int)]
+
+    @classmethod
+    def make(cls, fx, fy, cx, cy, dist):
+        c = cls()
+        c.fx, c.fy, c.cx, c.cy = fx, fy, cx, cy
+        for i, d in enumerate(dist):
+            c.dist[i] = d
+        c.ndist = len(dist)
+        return c
+
+
+def undistort_points(cam, xy):
+    """cv::undistortPoints as Frame::UndistortKeyPoints calls it (src/Frame.cc:1124-1157): n x 2 float32."""
+    xy = np.ascontiguousarray(xy, np.float32).reshape(-1, 2)
+    n = xy.shape[0]
+    lib = load()
+    d_in, d_out = DeviceBuffer(max(xy.nbytes, 8)), DeviceBuffer(max(xy.nbytes, 8))
+    d_in.upload(xy)
+    _check(lib.plvi_undistort_points(ctypes.byref(cam), ctypes.c_void_p(d_in.ptr), n, ctypes.c_void_p(d_out.ptr),
+                                     None), "plvi_undistort_points")
+    lib.plvi_device_synchronize()
+    return d_out.download(np.zeros((n, 2), np.float32))
+
+
+def image_bounds(cam, cols, rows):
+    """Frame::ComputeImageBounds (src/Frame.cc:1199-1226): (mnMinX, mnMaxX, mnMinY, mnMaxY)."""
+    b = np.zeros(4, np.float32)
+    _check(load().plvi_image_bounds(ctypes.byref(cam), cols, rows, _ptr(b)), "plvi_image_bounds")
+    return b
+
+
 class ProjParams(ctypes.Structure):
     """plvi_proj_params (include/plvi_frontend.h)."""
     _fields_ = [("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
@@ -125,6 +160,10 @@ def _declare(lib):
         "plvi_line_match_grid_batch": ([I, V, V, V, I, I, I, V, V, I, V, V, V, I, I, I, I, I, I, V, V, V, V], I),
         "plvi_frame_extract_batch": ([V, V, V, I, S, S, I, I, V], I),
         "plvi_assign_grid_batch": ([V, V, I, I, V, V, V, V], I),
+        "plvi_undistort_points": ([V, V, I, V, V], I),
+        "plvi_undistort_keypoints_batch": ([V, V, V, I, I, V, V], I),
+        "plvi_undistort_keylines_batch": ([V, V, V, I, I, V, V], I),
+        "plvi_image_bounds": ([V, I, I, V], I),
         "plvi_search_by_projection_batch": ([I, V, V, V, V, I, V, V, V, V, V, V, V, V, V, V, I, V, V, V], I),
         "plvi_search_by_projection": ([V, V, V, I, V, V, V, V, V, V, V, I, V], I),
         "plvi_vocab_load_text": ([ctypes.c_char_p, I, I, c_void_pp], I),

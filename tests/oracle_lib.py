@@ -381,3 +381,24 @@ def search_by_projection(case, th, forward=0, backward=0, check_ori=1):
                                         _p(sf), fx, fy, cx, cy, mbf, len(lf), _p(lf), _p(x3), _p(lo), _p(la), _p(md),
                                         th, forward, backward, check_ori, _p(out))
     return n, out[:len(kx)]
+
+
+def undistort_points(K4, dist, xy):
+    lib = load()
+    V, I = ctypes.c_void_p, ctypes.c_int
+    lib.oracle_undistort_points.argtypes = [V, V, I, V, I, V]
+    K = np.ascontiguousarray(K4, np.float32); d = np.ascontiguousarray(dist, np.float32)
+    xy = np.ascontiguousarray(xy, np.float32).reshape(-1, 2)
+    out = np.zeros_like(xy)
+    lib.oracle_undistort_points(_p(K), _p(d), len(d), _p(xy), xy.shape[0], _p(out))
+    return out
+
+
+def image_bounds(K4, dist, cols, rows):
+    lib = load()
+    V, I = ctypes.c_void_p, ctypes.c_int
+    lib.oracle_image_bounds.argtypes = [V, V, I, I, I, V]
+    K = np.ascontiguousarray(K4, np.float32); d = np.ascontiguousarray(dist, np.float32)
+    b = np.zeros(4, np.float32)
+    lib.oracle_image_bounds(_p(K), _p(d), len(d), cols, rows, _p(b))
+    return b
