@@ -1,7 +1,7 @@
 """bench.py — throughput of the MI355X feature front end (BASELINE.json metric).
 
 A step = one pass of the hot path over one batch of B synthetic 640x480
-frames already resident in HBM (default B=1024 frames in flight per GPU):
+frames already resident in HBM (default B=1536 frames in flight per GPU):
   ORB extract (ORBextractor 1000/1.2/8/20/7) and LSD + LBD line extract
   (Lineextractor 200/0/0.8/2/2.0) as one schedule (plvi_frame_extract_batch:
   region growing concurrent with the ORB pipeline and the LBD Sobel pyramid),
@@ -99,7 +99,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--batch", type=int, default=1536)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-bow", action="store_true", help="skip the DBoW2 transform stage timing")
     ap.add_argument("--no-proj", action="store_true", help="skip the SearchByProjection stage timing")

@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256) void lsd_prep_kernel(const uint8_t* __restrict
                                                        const int* __restrict__ yrow, const float* __restrict__ yb,
                                                        double k0, double k1, double k2, double k3, double rho,
                                                        float* __restrict__ pix, double* __restrict__ modgrad,
-                                                       float2* __restrict__ seedcs, size_t p_frame,
+                                                       float4* __restrict__ seedcs, size_t p_frame,
                                                        int* __restrict__ err) {
     __shared__ uint8_t I[kPIH][kPIW];
     __shared__ double Hs[kPIH][kPGW];
@@ -135,8 +135,12 @@ __global__ __launch_bounds__(256) void lsd_prep_kernel(const uint8_t* __restrict
         M[(size_t)y * sw + x] = norm;
         if (deg != kNotdefF) {
             // region_grow's seed direction float(cos/sin(reg_angle)) (lsd.cpp:648-649)
+            // and the per-pixel cos/sin(float(angle)) of its sums (:678-679)
             const double a = (double)deg * kD2R;
-            seedcs[(size_t)f * p_frame + (size_t)y * sw + x] = make_float2((float)plvi_cos(a), (float)plvi_sin(a));
+            float ps, pc;
+            plvi_sincosf_pos((float)a, &ps, &pc);
+            seedcs[(size_t)f * p_frame + (size_t)y * sw + x] =
+                make_float4((float)plvi_cos(a), (float)plvi_sin(a), pc, ps);
         }
     }
 }
@@ -291,7 +295,7 @@ template <bool STATS>
 __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restrict__ octs,
                                                       const float* __restrict__ pix,
                                                       const double* __restrict__ modgrad,
-                                                      const float2* __restrict__ seedcs,
+                                                      const float4* __restrict__ seedcs,
                                                       unsigned* __restrict__ gbits_all, size_t gbits_frame,
                                                       unsigned* __restrict__ qspill, size_t qspill_frame,
                                                       double prec, double scale_lsd, LsdLine* __restrict__ lines,
@@ -310,7 +314,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
     g.wpr = (sw + 31) >> 5;
     g.P = pix + od.soff + (size_t)f * od.splane;
     const double* M = modgrad + od.soff + (size_t)f * od.splane;
-    const float2* SC = seedcs + od.soff + (size_t)f * od.splane;
+    const float4* SC = seedcs + od.soff + (size_t)f * od.splane;
     g.gbits = gbits_all + (size_t)(f * nOct + o) * gbits_frame;
     g.qglob = qspill + (size_t)(f * nOct + o) * qspill_frame;
     // LDS: rect staging (64 x 3 doubles) | USED ring | queue | angle ring
@@ -357,7 +361,8 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
             if (x < sw - 1) cand = !used_get(g, x, y) && deg_at(g, x, y) != kNotdefF;
             unsigned long long m = __ballot(cand);
             if (!m) continue;
-            const float2 scl = cand ? SC[(size_t)y * sw + x] : make_float2(0.f, 0.f);
+            const float2 scl = cand ? make_float2(SC[(size_t)y * sw + x].x, SC[(size_t)y * sw + x].y)
+                                    : make_float2(0.f, 0.f);
             while (m) {
                 const int b = __ffsll((long long)m) - 1;
                 m &= m - 1;
@@ -391,9 +396,13 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                         if (p2 < bp && ddx >= 0 && ddx <= 2 && ddy >= 0 && ddy <= 2)
                             dup |= 1ull << (9 * p2 + ddy * 3 + ddx);
                     }
-                    // cos/sin(float(angle)) of lsd.cpp:678-679
-                    float cc, ss;
-                    plvi_sincosf_pos(deg == kNotdefF ? 0.f : (float)((double)deg * kD2R), &ss, &cc);
+                    // cos/sin(float(angle)) of lsd.cpp:678-679, precomputed by lsd_prep_kernel
+                    float cc = 0.f, ss = 0.f;
+                    if (deg != kNotdefF) {
+                        const float4 cs4 = SC[(size_t)ny * sw + nx];
+                        cc = cs4.z;
+                        ss = cs4.w;
+                    }
                     unsigned long long t1 = 0;
                     if (do_stats) { t1 = __builtin_amdgcn_s_memtime(); s_setup += t1 - t0; n_block++; }
                     int start = 0;

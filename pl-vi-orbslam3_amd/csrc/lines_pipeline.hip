@@ -45,7 +45,9 @@ struct LinePipeline {
     int W = 0, H = 0, Bcap = 0, device = 0, nOct = 0, fcap = 0;
     hipStream_t stream = nullptr;
     hipStream_t aux[2] = {nullptr, nullptr};  // frame mode: ORB and LBD-Sobel streams
-    hipEvent_t evFork = nullptr, evPrep = nullptr, evSobel = nullptr, evOrb = nullptr;
+    hipEvent_t evFork = nullptr, evPrep = nullptr, evSobel = nullptr, evOrb = nullptr, evCrit = nullptr;
+    hipStream_t critStream = nullptr;  // frame schedule: prep -> grow -> describe
+    bool orbAfterPrep = true;
     std::vector<LineOctDev> oct;
     std::vector<float> scaleF, invScaleF;
     double SCALE = 0.8, prec = 0, rho = 0, min_length = 0;
@@ -61,8 +63,9 @@ struct LinePipeline {
 
     ~LinePipeline() {
         for (auto e : evs) (void)hipEventDestroy(e);
-        for (auto e : {evFork, evPrep, evSobel, evOrb})
+        for (auto e : {evFork, evPrep, evSobel, evOrb, evCrit})
             if (e) (void)hipEventDestroy(e);
+        if (critStream) (void)hipStreamDestroy(critStream);
         for (auto a : aux)
             if (a) (void)hipStreamDestroy(a);
         if (stream) (void)hipStreamDestroy(stream);
@@ -76,8 +79,19 @@ struct LinePipeline {
         W = width; H = height; Bcap = max_batch; device = dev; nOct = p->nlevels;
         PLVI_CHECK(hipSetDevice(device));
         PLVI_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-        for (auto& a : aux) PLVI_CHECK(hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
-        for (auto* e : {&evFork, &evPrep, &evSobel, &evOrb})
+        {
+            // frame schedule streams: PLVI_STREAM_PRIO=1 (default) puts the critical
+            // path on the greatest priority and ORB / Sobel on the least
+            int least = 0, greatest = 0;
+            PLVI_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+            const char* e1 = getenv("PLVI_STREAM_PRIO");
+            const bool prio = !e1 || atoi(e1) != 0;
+            const char* e2 = getenv("PLVI_ORB_AFTER_PREP");
+            orbAfterPrep = !e2 || atoi(e2) != 0;
+            for (auto& a : aux) PLVI_CHECK(hipStreamCreateWithPriority(&a, hipStreamNonBlocking, prio ? least : 0));
+            if (prio) PLVI_CHECK(hipStreamCreateWithPriority(&critStream, hipStreamNonBlocking, greatest));
+        }
+        for (auto* e : {&evFork, &evPrep, &evSobel, &evOrb, &evCrit})
             PLVI_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         fcap = p->nfeatures > 0 ? p->nfeatures : kKlCap;
         SCALE = (double)p->lsd_scale;  // LSDOptions::scale is float
@@ -191,7 +205,7 @@ struct LinePipeline {
             PLVI_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_comb), comb, sizeof(comb)));
         }
         if (octImg.alloc(std::max<size_t>(imgOff, 16)) || pix.alloc(sizeof(float) * sOff) ||
-            modg.alloc(sizeof(double) * sOff) || seedcs.alloc(sizeof(float2) * sOff) ||
+            modg.alloc(sizeof(double) * sOff) || seedcs.alloc(sizeof(float4) * sOff) ||
             gbits.alloc(sizeof(unsigned) * gbitsFrame * nOct * Bcap) || qspill.alloc(sizeof(unsigned) * qspillFrame * nOct * Bcap) ||
             rawLines.alloc(sizeof(LsdLine) * (size_t)kLsdRawCap * nOct * Bcap) ||
             nlines.alloc(sizeof(int) * nOct * Bcap) || klTmp.alloc(sizeof(plvi_keyline) * (size_t)kKlCap * Bcap) ||
@@ -274,7 +288,7 @@ struct LinePipeline {
                                (const int*)(T + d.tabXofs), (const float*)(T + d.tabXa), d.xmax,
                                (const int*)(T + d.tabYrow), (const float*)(T + d.tabYb), gk[0], gk[1], gk[2], gk[3],
                                rho, pix.as<float>() + d.soff, modg.as<double>() + d.soff,
-                               seedcs.as<float2>() + d.soff, (size_t)d.splane, err.as<int>());
+                               seedcs.as<float4>() + d.soff, (size_t)d.splane, err.as<int>());
         }
         mark(2, st);
     }
@@ -284,7 +298,7 @@ struct LinePipeline {
         auto growK = growStats ? lsd_grow_kernel<true> : lsd_grow_kernel<false>;
         hipLaunchKernelGGL(growK, dim3(nOct, nf), dim3(64), growSmem, st, d_oct.as<LineOctDev>(),
                            (const float*)pix.as<float>(), (const double*)modg.as<double>(),
-                           (const float2*)seedcs.as<float2>(), gbits.as<unsigned>(), gbitsFrame, qspill.as<unsigned>(),
+                           (const float4*)seedcs.as<float4>(), gbits.as<unsigned>(), gbitsFrame, qspill.as<unsigned>(),
                            qspillFrame, prec, SCALE, rawLines.as<LsdLine>(), nlines.as<int>(), err.as<int>(), growR,
                            growQL, growStats);
         mark(3, st);
@@ -347,18 +361,28 @@ struct LinePipeline {
         lastFrames = nf;
         const bool p0 = prof;
         prof = false;  // stage events are meaningless across streams
+        // the critical path (prep -> region growing -> LBD describe) runs on
+        // the high-priority stream `crit`; ORB and the Sobel pyramid on the
+        // low-priority aux streams, started after prep (orbAfterPrep) or at once
+        hipStream_t crit = critStream ? critStream : st;
         PLVI_CHECK(hipEventRecord(evFork, st));
-        launch_prep(d_frames, nf, frame_stride, row_stride, st);
-        PLVI_CHECK(hipEventRecord(evPrep, st));
-        PLVI_CHECK(hipStreamWaitEvent(aux[0], evPrep, 0));
+        if (crit != st) PLVI_CHECK(hipStreamWaitEvent(crit, evFork, 0));
+        launch_prep(d_frames, nf, frame_stride, row_stride, crit);
+        PLVI_CHECK(hipEventRecord(evPrep, crit));
+        hipEvent_t auxStart = orbAfterPrep ? evPrep : evFork;
+        PLVI_CHECK(hipStreamWaitEvent(aux[0], auxStart, 0));
         int rc = plvi_orb_extract_batch(orb, d_frames, nf, frame_stride, row_stride, lap0, lap1, aux[0]);
         PLVI_CHECK(hipEventRecord(evOrb, aux[0]));
-        PLVI_CHECK(hipStreamWaitEvent(aux[1], evPrep, 0));
+        PLVI_CHECK(hipStreamWaitEvent(aux[1], auxStart, 0));
         if (!rc) rc = launch_sobel(d_frames, nf, frame_stride, row_stride, aux[1]);
         PLVI_CHECK(hipEventRecord(evSobel, aux[1]));
-        launch_grow_assemble(nf, st);
-        PLVI_CHECK(hipStreamWaitEvent(st, evSobel, 0));
-        launch_describe(nf, st);
+        launch_grow_assemble(nf, crit);
+        PLVI_CHECK(hipStreamWaitEvent(crit, evSobel, 0));
+        launch_describe(nf, crit);
+        if (crit != st) {
+            PLVI_CHECK(hipEventRecord(evCrit, crit));
+            PLVI_CHECK(hipStreamWaitEvent(st, evCrit, 0));
+        }
         PLVI_CHECK(hipStreamWaitEvent(st, evOrb, 0));
         prof = p0;
         PLVI_CHECK(hipGetLastError());
