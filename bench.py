@@ -192,6 +192,20 @@ def main():
     st_lines, lruns = lx.profile_read()
     orb.profile(False)
     lx.profile(False)
+    # ORB-only, LSD+LBD-only and match-only throughput, each part
+    # alone on the chip (no stage events), nprof back-to-back batches
+    def part_fps(fn):
+        fn()
+        torch.cuda.synchronize()
+        ev0.record(sA)
+        for _ in range(nprof):
+            fn()
+        ev1.record(sA)
+        torch.cuda.synchronize()
+        return B * nprof / (ev0.elapsed_time(ev1) * 1e-3)
+    parts = {"orb_only": part_fps(run_orb),
+             "lines_only": part_fps(lambda: lx.extract_batch(frames.data_ptr(), B, W * H, W, stream=sA.cuda_stream)),
+             "match_only": part_fps(run_match)}
     # DBoW2 transform (Frame::ComputeBoW) of the batch's ORB
     # descriptors on a k=10, L=6 synthetic vocabulary (ORBvoc.txt's shape);
     # timed separately: the reference runs it for keyframes / relocalisation,
@@ -308,6 +322,7 @@ def main():
         "roofline": roof,
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "dominant_stage": dom,
+        "part_fps": {k: round(v, 1) for k, v in parts.items()},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline()

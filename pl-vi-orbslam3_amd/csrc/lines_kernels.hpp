@@ -139,8 +139,9 @@ __global__ __launch_bounds__(256) void lsd_prep_kernel(const uint8_t* __restrict
             const double a = (double)deg * kD2R;
             float ps, pc;
             plvi_sincosf_pos((float)a, &ps, &pc);
-            seedcs[(size_t)f * p_frame + (size_t)y * sw + x] =
-                make_float4((float)plvi_cos(a), (float)plvi_sin(a), pc, ps);
+            double ds, dc;
+            plvi_sincos(a, &ds, &dc);
+            seedcs[(size_t)f * p_frame + (size_t)y * sw + x] = make_float4((float)dc, (float)ds, pc, ps);
         }
     }
 }
@@ -396,9 +397,11 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                         if (p2 < bp && ddx >= 0 && ddx <= 2 && ddy >= 0 && ddy <= 2)
                             dup |= 1ull << (9 * p2 + ddy * 3 + ddx);
                     }
-                    // cos/sin(float(angle)) of lsd.cpp:678-679, precomputed by lsd_prep_kernel
+                    // cos/sin(float(angle)) of lsd.cpp:678-679
                     float cc = 0.f, ss = 0.f;
                     if (deg != kNotdefF) {
+                        // precomputed by lsd_prep_kernel (computing them here costs
+                        // more VALU issue than the load's latency)
                         const float4 cs4 = SC[(size_t)ny * sw + nx];
                         cc = cs4.z;
                         ss = cs4.w;

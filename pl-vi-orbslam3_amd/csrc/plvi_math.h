@@ -375,6 +375,17 @@ PLVI_HD double plvi_cos(double x) {
     }
 }
 
+// sin and cos of one argument together: one argument reduction, both kernels,
+// quadrant by selects (no divergence across lanes with different quadrants).
+// Bitwise equal to plvi_sin / plvi_cos.
+PLVI_HD void plvi_sincos(double x, double* s, double* c) {
+    double y0, y1;
+    const int n = rem_pio2(x, &y0, &y1) & 3;
+    const double ks = k_sin(y0, y1, 1), kc = k_cos(y0, y1);
+    *s = n == 0 ? ks : n == 1 ? kc : n == 2 ? -ks : -kc;
+    *c = n == 0 ? kc : n == 1 ? -ks : n == 2 ? -kc : ks;
+}
+
 // cvRound (round half to even) and roundf (half away from zero).
 PLVI_HD int cv_round_f(float v) { return (int)__builtin_rintf(v); }
 PLVI_HD int cv_round_d(double v) { return (int)__builtin_rint(v); }

@@ -21,7 +21,8 @@ import pathlib
 import numpy as np
 
 _PKG = pathlib.Path(__file__).resolve().parent.parent
-LIB_PATH = _PKG / "lib" / "libplvi_frontend.so"
+# PLVI_LIB: an alternative build of the same library (A/B experiments, tools/build_variant.sh)
+LIB_PATH = pathlib.Path(os.environ["PLVI_LIB"]) if os.environ.get("PLVI_LIB") else _PKG / "lib" / "libplvi_frontend.so"
 HEADER_PATH = _PKG.parent / "include" / "plvi_frontend.h"
 
 PLVI_OK = 0
