@@ -103,6 +103,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-bow", action="store_true", help="skip the DBoW2 transform stage timing")
     ap.add_argument("--no-proj", action="store_true", help="skip the SearchByProjection stage timing")
+    ap.add_argument("--no-stereo", action="store_true", help="skip the rectified-stereo stage timing")
     ap.add_argument("--gather", action="store_true",
                     help="BASELINE C4: all-gather every step's per-frame ORB/line tables over RCCL (timed)")
     args = ap.parse_args()
@@ -276,6 +277,57 @@ def main():
         ev1.record(sA)
         torch.cuda.synchronize()
         proj_ms = ev0.elapsed_time(ev1) / nprof
+    # Stereo (Frame::ComputeStereoMatches / ComputeStereoMatches_Lines, SURVEY
+    # §8f rank 4) on S synthetic rectified pairs extracted by a second set of
+    # handles (left = own, right = the pair's other image); timed per S pairs
+    stereo_ms = None
+    if not args.no_stereo:
+        S = min(B, 256)
+        pairs = [synth.stereo_pair(pdist.shard_seed(rank) + 10 ** 5 + i, W, H) for i in range(S)]
+        sl = torch.from_numpy(np.stack([p[0] for p in pairs])).to(f"cuda:{dev}")
+        sr = torch.from_numpy(np.stack([p[1] for p in pairs])).to(f"cuda:{dev}")
+        o_l = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=S, device=dev)
+        o_r = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=S, device=dev)
+        l_l = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=S, device=dev)
+        l_r = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=S, device=dev)
+        for e, fr in ((o_l, sl), (o_r, sr), (l_l, sl), (l_r, sr)):
+            e.extract_batch(fr.data_ptr(), S, W * H, W, stream=sA.cuda_stream)
+        torch.cuda.synchronize()
+        scap = o_l.kp_cap
+        st_f = torch.empty(2 * S * scap, dtype=torch.float32, device=f"cuda:{dev}")
+        st_i = torch.zeros(S + 1, **i32)
+        a_kl, a_de, _, a_co, a_cap = l_l.outputs()
+        b_kl, b_de, _, b_co, b_cap = l_r.outputs()
+        idx_cap = 32768
+        sbytes = plvi.stereo_lines_scratch_bytes(S, a_cap, b_cap, idx_cap)
+        s_scr = torch.empty(sbytes, dtype=torch.uint8, device=f"cuda:{dev}")
+        s_lo = torch.empty(S * a_cap * 11, dtype=torch.float64, device=f"cuda:{dev}")
+        lo = s_lo.data_ptr()
+        mbf_, mb_ = 47.90639384423901, 0.11
+
+        def run_stereo_orb():
+            plvi.stereo_match_batch(o_l, o_r, S, mb_, mbf_, st_f.data_ptr(), st_f.data_ptr() + 4 * S * scap,
+                                    st_i.data_ptr(), st_i.data_ptr() + 4 * S, stream=sA.cuda_stream)
+
+        def run_stereo_lines():
+            plvi.stereo_lines_batch(S, a_kl, a_de, a_co, a_cap, b_kl, b_de, b_co, b_cap, None, W, H, mbf_, 1,
+                                    idx_cap, s_scr.data_ptr(), sbytes, lo, lo + 4 * S * a_cap,
+                                    lo + 12 * S * a_cap, lo + 20 * S * a_cap, lo + 44 * S * a_cap,
+                                    st_i.data_ptr() + 4 * S, stream=sA.cuda_stream)
+        stereo_ms = {}
+        for name, fn in (("stereo.orb", run_stereo_orb), ("stereo.lines", run_stereo_lines)):
+            fn()
+            torch.cuda.synchronize()
+            ev0.record(sA)
+            for _ in range(nprof):
+                fn()
+            ev1.record(sA)
+            torch.cuda.synchronize()
+            stereo_ms[name] = ev0.elapsed_time(ev1) / nprof
+        if int(st_i[S].item()) != 0:
+            raise RuntimeError(f"stereo err {int(st_i[S].item())}")
+        stereo_ms["stereo.pairs"] = S
+        del o_l, o_r, l_l, l_r
     stage_ms = {f"orb.{k}": v / runs for k, v in st_orb.items()}
     stage_ms.update({f"lines.{k}": v / lruns for k, v in st_lines.items()})
     stage_ms["match"] = match_ms / nprof
@@ -283,6 +335,9 @@ def main():
         stage_ms["bow.transform"] = bow_ms
     if proj_ms is not None:
         stage_ms["proj.grid+search"] = proj_ms
+    side = ("bow.transform", "proj.grid+search", "stereo.orb", "stereo.lines", "stereo.pairs")
+    if stereo_ms is not None:
+        stage_ms.update(stereo_ms)
 
     pdist.barrier(world)
     torch.cuda.synchronize()
@@ -303,7 +358,7 @@ def main():
     ktot, kn = orb.kernel_timing_read()
     kavg_ms = ktot / max(kn, 1)
     bf_bytes = blur_fast_bytes(W, H) * B
-    dom = max((k for k in stage_ms if k not in ("bow.transform", "proj.grid+search")), key=stage_ms.get)
+    dom = max((k for k in stage_ms if k not in side), key=stage_ms.get)
     roof = {
         "bound": "hbm", "kernel": "orb_blur_fast_kernel (7x7 blur + FAST score, all 8 levels, one launch)",
         "achieved": bf_bytes / (kavg_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",

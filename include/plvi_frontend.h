@@ -102,6 +102,15 @@ int plvi_orb_outputs(plvi_orb_extractor* h, plvi_keypoint** d_kps, uint8_t** d_d
  * dst must hold w*h bytes; pass dst=NULL to query the size. */
 int plvi_orb_pyramid_level(plvi_orb_extractor* h, int frame, int level, uint8_t* dst, int* w, int* hgt);
 
+/* Device view of mvImagePyramid (include/ORBextractor.h:84, read by
+ * Frame::ComputeStereoMatches, src/Frame.cc:1235,1325,1344): level `level`
+ * of frame f is the w x hgt u8 image (row stride w) at
+ * *d_frame0 + f * *frame_stride, valid after the last extraction on the
+ * handle's stream.  level = -1 only reports *nlevels.  Any out pointer may
+ * be NULL. */
+int plvi_orb_pyramid_device(plvi_orb_extractor* h, int level, const uint8_t** d_frame0, size_t* frame_stride, int* w,
+                            int* hgt, int* nlevels);
+
 /* GetScaleFactors / GetInverseScaleFactors / GetScaleSigmaSquares /
  * GetInverseScaleSigmaSquares (include/ORBextractor.h:62-82): nlevels floats each. */
 int plvi_orb_scale_tables(plvi_orb_extractor* h, float* scale, float* inv_scale, float* sigma2, float* inv_sigma2);
@@ -397,6 +406,58 @@ int plvi_search_by_projection(const plvi_proj_params* p, const plvi_keypoint* cu
                               int n_cur, const uint8_t* cur_blocked, const float* cur_uright, const float* x3dc,
                               const int* last_octave, const float* last_angle, const uint8_t* mp_desc,
                               const uint8_t* last_flags, int n_last, int* match);
+
+/* ---------------------------------------------------------------- Stereo
+ * Rectified stereo of the stereo Frame constructors (src/Frame.cc:95-140,
+ * :225-300). */
+
+/* Frame::ComputeStereoMatches (src/Frame.cc:1228-1406) for n_frames pairs
+ * extracted by two ORB handles of the same geometry (mpORBextractorLeft /
+ * Right, vLappingArea {0,0}): keypoints, descriptors and mvImagePyramid are
+ * read on the device.  mb / mbf: Frame::mb, mbf.  Outputs mvuRight /
+ * mvDepth [n_frames][cap] (cap of plvi_orb_outputs, -1 = no depth),
+ * d_nstereo [n_frames] = left keypoints with a depth; *d_err |= 1 when a
+ * right keypoint's row band leaves the image (the reference indexes
+ * vRowIndices out of range), |= 2 when an SAD window leaves its level (the
+ * reference's rowRange/colRange assert).  Asynchronous on `stream`. */
+int plvi_stereo_match_batch(plvi_orb_extractor* left, plvi_orb_extractor* right, int n_frames, float mb, float mbf,
+                            float* d_uright, float* d_depth, int* d_nstereo, int* d_err, void* stream);
+
+/* One pair from host memory, synchronous.  Pyramids: level l of each side
+ * at pyr + lvl_off[l], lvl_w[l] x lvl_h[l] (row stride lvl_w[l]); scale /
+ * inv_scale = mvScaleFactors / mvInvScaleFactors.  Returns the number of
+ * left keypoints with a depth, or an error (PLVI_E_OVERFLOW for the
+ * reference's out-of-range cases above). */
+int plvi_stereo_match(const plvi_keypoint* kpsL, const uint8_t* descL, int nL, const plvi_keypoint* kpsR,
+                      const uint8_t* descR, int nR, int nlevels, const float* scale, const float* inv_scale,
+                      const uint8_t* pyrL, const uint8_t* pyrR, const long long* lvl_off, const int* lvl_w,
+                      const int* lvl_h, float mb, float mbf, float* uright, float* depth);
+
+/* Frame::ComputeStereoMatches_Lines (src/Frame.cc:1408-1492): GridStructure
+ * of the right lines (getLineCoords, src/gridStructure.cpp:32-40), the
+ * line_2d coordinates and directions, LineMatcher::matchGrid with the
+ * stereo window {width (7,0), height (2,2)}, then the endpoint disparities
+ * (lineSegmentOverlapStereo :1494-1529, filterLineSegmentDisparity
+ * :1531-1542) and mvle_l from mvKeysUn_Line (d_klUn; NULL = the left
+ * keylines).  Per pair p: keylines/descriptors at p*cap, counts n[p].
+ * Outputs matches_12 [n][capL], mvDisparity_l / mvDepth_l [n][capL][2]
+ * floats (-1 = none), mvle_l [n][capL][3] doubles (0 when either side has
+ * no lines, as the reference returns before computing it), d_nstereo [n].
+ * d_scratch: plvi_stereo_lines_scratch_bytes(n, capL, capR, idx_cap) bytes;
+ * idx_cap bounds the grid entries of one frame (*d_err |= 4 if exceeded).
+ * Asynchronous on `stream`. */
+size_t plvi_stereo_lines_scratch_bytes(int n_frames, int capL, int capR, int idx_cap);
+int plvi_stereo_lines_batch(int n_frames, const plvi_keyline* d_klL, const uint8_t* d_descL, const int* d_nL, int capL,
+                            const plvi_keyline* d_klR, const uint8_t* d_descR, const int* d_nR, int capR,
+                            const plvi_keyline* d_klUn, int width, int height, float mbf, int libstdcxx_range_hint,
+                            int idx_cap, void* d_scratch, size_t scratch_bytes, int* d_matches_12, float* d_disparity,
+                            float* d_depth, double* d_le, int* d_nstereo, int* d_err, void* stream);
+
+/* One pair from host memory, synchronous (n <= 2048 lines per side).
+ * Returns the number of lines with a depth, or an error. */
+int plvi_stereo_lines(const plvi_keyline* klL, const uint8_t* descL, int nL, const plvi_keyline* klR,
+                      const uint8_t* descR, int nR, const plvi_keyline* klUn, int width, int height, float mbf,
+                      int libstdcxx_range_hint, int* matches_12, float* disparity, float* depth, double* le);
 
 /* ------------------------------------------------------------ Frame level
  * Frame::Frame's extraction (src/Frame.cc:537-641, ExtractORB/ExtractLine

@@ -472,6 +472,19 @@ extern "C" int plvi_orb_pyramid_level(plvi_orb_extractor* h, int frame, int leve
     return PLVI_OK;
 }
 
+extern "C" int plvi_orb_pyramid_device(plvi_orb_extractor* h, int level, const uint8_t** d_frame0,
+                                       size_t* frame_stride, int* w, int* hgt, int* nlevels) {
+    if (!h || level < -1 || level >= h->p.L) return PLVI_E_BADARG;
+    if (nlevels) *nlevels = h->p.L;
+    if (level < 0) return PLVI_OK;
+    const auto& d = h->p.lv[level];
+    if (d_frame0) *d_frame0 = h->p.pyr.as<uint8_t>() + d.off;
+    if (frame_stride) *frame_stride = (size_t)d.plane;
+    if (w) *w = d.w;
+    if (hgt) *hgt = d.h;
+    return PLVI_OK;
+}
+
 extern "C" int plvi_orb_scale_tables(plvi_orb_extractor* h, float* scale, float* inv_scale, float* sigma2,
                                      float* inv_sigma2) {
     if (!h) return PLVI_E_BADARG;

@@ -133,6 +133,7 @@ def _declare(lib):
         "plvi_orb_extract_batch": ([V, V, I, S, S, I, I, V], I),
         "plvi_orb_outputs": ([V, c_void_pp, c_void_pp, c_void_pp, c_void_pp, P], I),
         "plvi_orb_pyramid_level": ([V, I, I, V, P, P], I),
+        "plvi_orb_pyramid_device": ([V, I, c_void_pp, ctypes.POINTER(S), P, P, P], I),
         "plvi_orb_scale_tables": ([V, V, V, V, V], I),
         "plvi_orb_level_quota": ([V, V], I),
         "plvi_orb_profile": ([V, I], I),
@@ -174,6 +175,11 @@ def _declare(lib):
         "plvi_vocab_transform": ([V, V, I, I, V, V, P, V, V, V, P], I),
         "plvi_vocab_transform_features": ([V, V, I, I, V, V], I),
         "plvi_vocab_transform_batch": ([V, V, V, I, I, I, V, V, V, V, V, V, V, V, V, V], I),
+        "plvi_stereo_match_batch": ([V, V, I, F, F, V, V, V, V, V], I),
+        "plvi_stereo_match": ([V, V, I, V, V, I, I, V, V, V, V, V, V, V, F, F, V, V], I),
+        "plvi_stereo_lines_scratch_bytes": ([I, I, I, I], S),
+        "plvi_stereo_lines_batch": ([I, V, V, V, I, V, V, V, I, V, I, I, F, I, I, V, S, V, V, V, V, V, V, V], I),
+        "plvi_stereo_lines": ([V, V, I, V, V, I, V, I, I, F, I, V, V, V, V], I),
         "plvi_device_malloc": ([c_void_pp, S], I),
         "plvi_device_free": ([V], I),
         "plvi_memcpy": ([V, V, S, I], I),
@@ -374,6 +380,14 @@ class ORBextractor:
     @property
     def mvImagePyramid(self):
         return [self.pyramid_level(l) for l in range(self.nlevels)]
+
+    def pyramid_device(self, level):
+        """Device view of mvImagePyramid[level]: (frame-0 pointer, frame stride, w, h)."""
+        p, fs = ctypes.c_void_p(), ctypes.c_size_t()
+        w, h = ctypes.c_int(), ctypes.c_int()
+        _check(self._lib.plvi_orb_pyramid_device(self._h, level, ctypes.byref(p), ctypes.byref(fs), ctypes.byref(w),
+                                                 ctypes.byref(h), None), "plvi_orb_pyramid_device")
+        return p.value, fs.value, w.value, h.value
 
 
 class Lineextractor:
@@ -695,3 +709,85 @@ def assign_grid_batch(d_kps, d_count, cap, n_frames, grid, d_cell_off, d_cell_id
                                          ctypes.byref(grid), ctypes.c_void_p(d_cell_off),
                                          ctypes.c_void_p(d_cell_idx), ctypes.c_void_p(stream or 0)),
            "plvi_assign_grid_batch")
+
+
+# ----------------------------------------------------------------- stereo
+def pack_pyramid(levels):
+    """mvImagePyramid (list of 2-D uint8 arrays) -> (concatenated bytes, offsets, widths, heights)."""
+    off = np.zeros(len(levels), np.int64)
+    o = 0
+    for i, lv in enumerate(levels):
+        off[i] = o
+        o += lv.size
+    buf = np.concatenate([np.ascontiguousarray(lv, np.uint8).ravel() for lv in levels])
+    w = np.array([lv.shape[1] for lv in levels], np.int32)
+    h = np.array([lv.shape[0] for lv in levels], np.int32)
+    return buf, off, w, h
+
+
+def ComputeStereoMatches(kpsL, descL, kpsR, descR, pyrL, pyrR, scale_factors, inv_scale_factors, mb, mbf):
+    """Frame::ComputeStereoMatches (src/Frame.cc:1228-1406) for one rectified pair.  kps*: mvKeys /
+    mvKeysRight (KEYPOINT_DTYPE), pyr*: mvImagePyramid of the left / right extractor.  Returns
+    (nstereo, mvuRight, mvDepth)."""
+    lib = load()
+    kl = np.ascontiguousarray(kpsL).view(KEYPOINT_DTYPE)
+    kr = np.ascontiguousarray(kpsR).view(KEYPOINT_DTYPE)
+    dl = np.ascontiguousarray(descL, np.uint8).reshape(-1, 32)
+    dr = np.ascontiguousarray(descR, np.uint8).reshape(-1, 32)
+    bl, off, w, h = pack_pyramid(pyrL)
+    br, off2, w2, h2 = pack_pyramid(pyrR)
+    if not (np.array_equal(off, off2) and np.array_equal(w, w2) and np.array_equal(h, h2)):
+        raise ValueError("left and right pyramids differ in geometry")
+    sc = np.ascontiguousarray(scale_factors, np.float32)
+    inv = np.ascontiguousarray(inv_scale_factors, np.float32)
+    n = len(kl)
+    ur = np.full(max(n, 1), -1, np.float32)
+    dp = np.full(max(n, 1), -1, np.float32)
+    k = _check(lib.plvi_stereo_match(_ptr(kl), _ptr(dl), n, _ptr(kr), _ptr(dr), len(kr), len(pyrL), _ptr(sc),
+                                     _ptr(inv), _ptr(bl), _ptr(br), _ptr(off), _ptr(w), _ptr(h), float(mb),
+                                     float(mbf), _ptr(ur), _ptr(dp)), "plvi_stereo_match")
+    return k, ur[:n], dp[:n]
+
+
+def stereo_match_batch(left, right, n_frames, mb, mbf, d_uright, d_depth, d_nstereo, d_err, stream=None):
+    """plvi_stereo_match_batch on two ORBextractor handles (device outputs, asynchronous)."""
+    _check(load().plvi_stereo_match_batch(left._h, right._h, n_frames, float(mb), float(mbf),
+                                          ctypes.c_void_p(d_uright), ctypes.c_void_p(d_depth),
+                                          ctypes.c_void_p(d_nstereo), ctypes.c_void_p(d_err),
+                                          ctypes.c_void_p(stream or 0)), "plvi_stereo_match_batch")
+
+
+def ComputeStereoMatches_Lines(klL, descL, klR, descR, klUn, width, height, mbf, range_hint=1):
+    """Frame::ComputeStereoMatches_Lines (src/Frame.cc:1408-1492) for one pair: mvKeys_Line, mvKeysRight_Line,
+    mvKeysUn_Line (KEYLINE_DTYPE), LBD descriptors.  Returns (nstereo, matches_12, mvDisparity_l (n x 2),
+    mvDepth_l (n x 2), mvle_l (n x 3))."""
+    lib = load()
+    a = np.ascontiguousarray(klL).view(KEYLINE_DTYPE)
+    b = np.ascontiguousarray(klR).view(KEYLINE_DTYPE)
+    u = a if klUn is None else np.ascontiguousarray(klUn).view(KEYLINE_DTYPE)
+    dl = np.ascontiguousarray(descL, np.uint8).reshape(-1, 32)
+    dr = np.ascontiguousarray(descR, np.uint8).reshape(-1, 32)
+    n = len(a)
+    m = np.full(max(n, 1), -1, np.int32)
+    disp = np.full((max(n, 1), 2), -1, np.float32)
+    dep = np.full((max(n, 1), 2), -1, np.float32)
+    le = np.zeros((max(n, 1), 3), np.float64)
+    k = _check(lib.plvi_stereo_lines(_ptr(a), _ptr(dl), n, _ptr(b), _ptr(dr), len(b), _ptr(u), int(width),
+                                     int(height), float(mbf), int(range_hint), _ptr(m), _ptr(disp), _ptr(dep),
+                                     _ptr(le)), "plvi_stereo_lines")
+    return k, m[:n], disp[:n], dep[:n], le[:n]
+
+
+def stereo_lines_scratch_bytes(n_frames, capL, capR, idx_cap):
+    return load().plvi_stereo_lines_scratch_bytes(n_frames, capL, capR, idx_cap)
+
+
+def stereo_lines_batch(n_frames, d_klL, d_descL, d_nL, capL, d_klR, d_descR, d_nR, capR, d_klUn, width, height,
+                       mbf, range_hint, idx_cap, d_scratch, scratch_bytes, d_m12, d_disp, d_depth, d_le, d_nstereo,
+                       d_err, stream=None):
+    """plvi_stereo_lines_batch on device keyline tables (asynchronous)."""
+    V = ctypes.c_void_p
+    _check(load().plvi_stereo_lines_batch(n_frames, V(d_klL), V(d_descL), V(d_nL), capL, V(d_klR), V(d_descR),
+                                          V(d_nR), capR, V(d_klUn or 0), width, height, float(mbf), range_hint,
+                                          idx_cap, V(d_scratch), scratch_bytes, V(d_m12), V(d_disp), V(d_depth),
+                                          V(d_le), V(d_nstereo), V(d_err), V(stream or 0)), "plvi_stereo_lines_batch")

@@ -101,6 +101,19 @@ def frame_pair(seed, w=640, h=480):
     return a, b
 
 
+def stereo_pair(seed, w=640, h=480):
+    """Rectified stereo pair (left, right, (d_top, d_bottom)): one clean image of width w + 64 seen by the
+    left camera at columns [0, w) and by the right camera shifted by an integer disparity, d_top for the upper
+    half of the rows and d_bottom for the lower half (two depth planes), each side with its own noise."""
+    img, rng = clean_frame(seed, w + 64, h)
+    d0, d1 = (int(v) for v in rng.integers(4, 60, size=2))
+    left = img[:, :w]
+    right = np.empty((h, w))
+    right[: h // 2] = img[: h // 2, d0:d0 + w]
+    right[h // 2:] = img[h // 2:, d1:d1 + w]
+    return _finish(left, rng), _finish(right, rng), (d0, d1)
+
+
 def batch(n, w=640, h=480, seed0=0):
     """n frames with seeds seed0..seed0+n-1 as one contiguous (n,H,W) u8 array."""
     out = np.empty((n, h, w), np.uint8)

@@ -402,3 +402,63 @@ def image_bounds(K4, dist, cols, rows):
     b = np.zeros(4, np.float32)
     lib.oracle_image_bounds(_p(K), _p(d), len(d), cols, rows, _p(b))
     return b
+
+
+def orb_pyramid(img, nfeatures=1000, scale=1.2, nlevels=8):
+    """mvImagePyramid of the oracle extractor (list of uint8 levels)."""
+    img = np.ascontiguousarray(img, np.uint8)
+    out = []
+    for level in range(nlevels):
+        lvl = orb_stage(img, level, nfeatures, scale, nlevels)["pyr"]
+        out.append(lvl)
+    return out
+
+
+def stereo_match(kpsL, descL, kpsR, descR, pyrL, pyrR, scale, inv_scale, mb, mbf):
+    """Frame::ComputeStereoMatches restatement -> (nstereo, mvuRight, mvDepth)."""
+    lib = load()
+    V, F, I = ctypes.c_void_p, ctypes.c_float, ctypes.c_int
+    lib.oracle_stereo_match.argtypes = [V, V, I, V, V, I, V, V, V, V, V, V, V, F, F, V, V]
+    lib.oracle_stereo_match.restype = I
+    kl = np.ascontiguousarray(kpsL).view(KEYPOINT_DTYPE)
+    kr = np.ascontiguousarray(kpsR).view(KEYPOINT_DTYPE)
+    dl = np.ascontiguousarray(descL, np.uint8)
+    dr = np.ascontiguousarray(descR, np.uint8)
+    off = np.cumsum([0] + [lv.size for lv in pyrL[:-1]]).astype(np.int64)
+    bl = np.concatenate([lv.ravel() for lv in pyrL])
+    br = np.concatenate([lv.ravel() for lv in pyrR])
+    w = np.array([lv.shape[1] for lv in pyrL], np.int32)
+    h = np.array([lv.shape[0] for lv in pyrL], np.int32)
+    sc = np.ascontiguousarray(scale, np.float32)
+    inv = np.ascontiguousarray(inv_scale, np.float32)
+    n = len(kl)
+    ur = np.zeros(max(n, 1), np.float32)
+    dp = np.zeros(max(n, 1), np.float32)
+    k = lib.oracle_stereo_match(_p(kl), _p(dl), n, _p(kr), _p(dr), len(kr), _p(bl), _p(br), _p(off), _p(w), _p(h),
+                                _p(sc), _p(inv), mb, mbf, _p(ur), _p(dp))
+    return k, ur[:n], dp[:n]
+
+
+def stereo_lines(klL, descL, klR, descR, klUn, width, height, mbf):
+    """Frame::ComputeStereoMatches_Lines restatement -> (nstereo, matches, disparity, depth, le)."""
+    lib = load()
+    V, F, I = ctypes.c_void_p, ctypes.c_float, ctypes.c_int
+    lib.oracle_stereo_lines.argtypes = [V, V, I, V, V, I, V, I, I, F, V, V, V, V]
+    lib.oracle_stereo_lines.restype = I
+
+    def pts(k):
+        k = np.ascontiguousarray(k).view(KEYLINE_DTYPE)
+        return np.ascontiguousarray(np.stack([k["startPointX"], k["startPointY"], k["endPointX"], k["endPointY"]],
+                                             1).astype(np.float32))
+    a, b = pts(klL), pts(klR)
+    u = a if klUn is None else pts(klUn)
+    n = len(a)
+    dl = np.ascontiguousarray(descL, np.uint8)
+    dr = np.ascontiguousarray(descR, np.uint8)
+    m = np.zeros(max(n, 1), np.int32)
+    disp = np.zeros((max(n, 1), 2), np.float32)
+    dep = np.zeros((max(n, 1), 2), np.float32)
+    le = np.zeros((max(n, 1), 3), np.float64)
+    k = lib.oracle_stereo_lines(_p(a), _p(dl), n, _p(b), _p(dr), len(b), _p(u), width, height, mbf, _p(m), _p(disp),
+                                _p(dep), _p(le))
+    return k, m[:n], disp[:n], dep[:n], le[:n]
