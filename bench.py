@@ -99,7 +99,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=1536)
+    ap.add_argument("--batch", type=int, default=3072)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-bow", action="store_true", help="skip the DBoW2 transform stage timing")
     ap.add_argument("--no-proj", action="store_true", help="skip the SearchByProjection stage timing")

@@ -32,6 +32,13 @@ struct LsdLine {
     float x1, y1, x2, y2;
 };
 
+// A region kept by region growing: its points (x | y << 16, queue order) at
+// [start, start + n) of the task's point list, and its final reg_angle.
+struct LsdRegion {
+    int start, n;
+    double angle;
+};
+
 // Per-pixel static data for region growing: fastAtan2 angle in degrees
 // (float; NOTDEF encoded as -1024), and cosf/sinf of float(angle rad)
 // exactly as region_grow computes them (lsd.cpp:678-679).

@@ -299,8 +299,9 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                                                       const float4* __restrict__ seedcs,
                                                       unsigned* __restrict__ gbits_all, size_t gbits_frame,
                                                       unsigned* __restrict__ qspill, size_t qspill_frame,
-                                                      double prec, double scale_lsd, LsdLine* __restrict__ lines,
-                                                      int* __restrict__ nlines, int* __restrict__ err, int R, int QL,
+                                                      double prec, LsdRegion* __restrict__ regs, unsigned* __restrict__ regpts,
+                                                      size_t regpts_frame, int* __restrict__ nlines,
+                                                      int* __restrict__ err, int R, int QL,
                                                       unsigned long long* __restrict__ stats) {
     extern __shared__ __align__(16) unsigned lds_u[];
     // latency-bound serial chain: win the SIMD arbiter against co-resident
@@ -314,13 +315,14 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
     g.sw = sw; g.sh = sh; g.R = R; g.QL = QL;
     g.wpr = (sw + 31) >> 5;
     g.P = pix + od.soff + (size_t)f * od.splane;
-    const double* M = modgrad + od.soff + (size_t)f * od.splane;
     const float4* SC = seedcs + od.soff + (size_t)f * od.splane;
+    LsdRegion* outR = regs + (size_t)(f * nOct + o) * kLsdRawCap;
+    unsigned* outP = regpts + (size_t)(f * nOct + o) * regpts_frame;
+    int npts = 0;
     g.gbits = gbits_all + (size_t)(f * nOct + o) * gbits_frame;
     g.qglob = qspill + (size_t)(f * nOct + o) * qspill_frame;
-    // LDS: rect staging (64 x 3 doubles) | USED ring | queue | angle ring
-    double* rs = reinterpret_cast<double*>(lds_u);
-    g.bits = (lds_u32*)(lds_u + 64 * 3 * 2);
+    // LDS: USED ring | queue | angle ring
+    g.bits = (lds_u32*)lds_u;
     g.qlds = g.bits + R * g.wpr;
     g.win = (lds_f32*)(g.qlds + QL);
     g.wb = 0;
@@ -330,7 +332,6 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
     win_load_rows(g, 0, min(R, sh), lane);
     vm_drain();
     __syncthreads();
-    LsdLine* out = lines + (size_t)(f * nOct + o) * kLsdRawCap;
     int nout = 0;
     bool overflow = false;
     const int min_reg = od.min_reg_size;
@@ -481,92 +482,12 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                 if (reg_size < min_reg) continue;
                 const unsigned long long tr0 = do_stats ? __builtin_amdgcn_s_memtime() : 0;
                 if (do_stats) n_rpt += reg_size;
-                // ---- region2rect (lsd.cpp:688-744) + get_theta (:746-782): the
-                // lanes form the per-point products, lane 0 adds them in region
-                // order (the reference's double summation order)
-                double xs = 0, ys = 0, sum = 0, Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
-                unsigned q0 = 0;
-                double w0 = 0.0;
-                if (lane < reg_size) {
-                    q0 = q_get(g, lane);
-                    w0 = M[(int)(q0 >> 16) * sw + (int)(q0 & 0xffffu)];
-                }
-                for (int pass = 0; pass < 2; ++pass) {
-                    for (int base = 0; base < reg_size; base += 64) {
-                        const int j = base + lane;
-                        if (j < reg_size) {
-                            const unsigned q = base == 0 ? q0 : q_get(g, j);
-                            const double w = base == 0 ? w0 : M[(int)(q >> 16) * sw + (int)(q & 0xffffu)];
-                            const double rx = (double)(int)(q & 0xffffu), ry = (double)(int)(q >> 16);
-                            if (pass == 0) {
-                                rs[lane] = rx * w;
-                                rs[64 + lane] = ry * w;
-                                rs[128 + lane] = w;
-                            } else {
-                                const double dx = rx - xs, dy = ry - ys;
-                                rs[lane] = dy * dy * w;
-                                rs[64 + lane] = dx * dx * w;
-                                rs[128 + lane] = dx * dy * w;
-                            }
-                        }
-                        __syncthreads();
-                        if (lane == 0) {
-                            const int n = min(64, reg_size - base);
-                            if (pass == 0) {
-                                for (int t2 = 0; t2 < n; ++t2) {
-                                    xs += rs[t2];
-                                    ys += rs[64 + t2];
-                                    sum += rs[128 + t2];
-                                }
-                            } else {
-                                for (int t2 = 0; t2 < n; ++t2) {
-                                    Ixx += rs[t2];
-                                    Iyy += rs[64 + t2];
-                                    Ixy -= rs[128 + t2];
-                                }
-                            }
-                        }
-                        __syncthreads();
-                    }
-                    if (pass == 0) {
-                        xs = readlane_d(xs, 0) / readlane_d(sum, 0);
-                        ys = readlane_d(ys, 0) / readlane_d(sum, 0);
-                    }
-                }
-                Ixx = readlane_d(Ixx, 0);
-                Iyy = readlane_d(Iyy, 0);
-                Ixy = readlane_d(Ixy, 0);
-                const double lambda = 0.5 * (Ixx + Iyy - __builtin_sqrt((Ixx - Iyy) * (Ixx - Iyy) + 4.0 * Ixy * Ixy));
-                double theta = (__builtin_fabs(Ixx) > __builtin_fabs(Iyy))
-                                   ? (double)plvi_fast_atan2((float)(lambda - Ixx), (float)Ixy)
-                                   : (double)plvi_fast_atan2((float)Ixy, (float)(lambda - Iyy));
-                theta *= kD2R;
-                if (angle_diff(theta, reg_angle) > prec) theta += kPi;
-                const double dxv = plvi_cos(theta), dyv = plvi_sin(theta);
-                // l extents: the reference's if/else-if max/min is equivalent to
-                // independent max(0, .)/min(0, .) (l_min <= 0 <= l_max throughout).
-                double lmax = 0, lmin = 0;
-                for (int j = lane; j < reg_size; j += 64) {
-                    const unsigned q = q_get(g, j);
-                    const double regdx = (double)(int)(q & 0xffffu) - xs;
-                    const double regdy = (double)(int)(q >> 16) - ys;
-                    const double l = regdx * dxv + regdy * dyv;
-                    lmax = l > lmax ? l : lmax;
-                    lmin = l < lmin ? l : lmin;
-                }
-                for (int s = 32; s > 0; s >>= 1) {
-                    const double a = __shfl_xor(lmax, s), b2 = __shfl_xor(lmin, s);
-                    lmax = a > lmax ? a : lmax;
-                    lmin = b2 < lmin ? b2 : lmin;
-                }
-                double x1 = xs + lmin * dxv, y1 = ys + lmin * dyv;
-                double x2 = xs + lmax * dxv, y2 = ys + lmax * dyv;
-                x1 += 0.5; y1 += 0.5; x2 += 0.5; y2 += 0.5;
-                if (scale_lsd != 1) {
-                    x1 /= scale_lsd; y1 /= scale_lsd; x2 /= scale_lsd; y2 /= scale_lsd;
-                }
+                // region2rect runs in lsd_rect_kernel (one lane per region): hand
+                // over the region's points in queue order and its angle
                 if (nout < kLsdRawCap) {
-                    if (lane == 0) out[nout] = LsdLine{(float)x1, (float)y1, (float)x2, (float)y2};
+                    for (int j = lane; j < reg_size; j += 64) outP[npts + j] = q_get(g, j);
+                    if (lane == 0) outR[nout] = LsdRegion{npts, reg_size, reg_angle};
+                    npts += reg_size;
                     ++nout;
                 } else {
                     overflow = true;
@@ -585,6 +506,78 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
         S[1] = s_setup; S[2] = s_round; S[3] = s_rect; S[4] = n_seed;
         S[5] = n_block; S[6] = n_round; S[7] = n_rpt; S[8] = n_commit;
         S[9] = s_ph[0]; S[10] = s_ph[1]; S[11] = s_ph[2]; S[12] = s_ph[3];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// LK3b: region2rect (lsd.cpp:688-744) + get_theta (:746-782) of every region
+// lsd_grow_kernel kept (reg_size >= min_reg_size), one lane per region.  The
+// weighted centroid / inertia sums run sequentially in region order as in the
+// reference (double, no contraction); the l extents are order-free max/min.
+// Emits the Vec4f of flsd (:506-518) at the region's index.
+// ---------------------------------------------------------------------------
+constexpr int kRectBlocks = 8;  // 64-lane blocks per (octave, frame); lanes stride over the regions
+
+__global__ __launch_bounds__(64) void lsd_rect_kernel(const LineOctDev* __restrict__ octs,
+                                                      const double* __restrict__ modgrad,
+                                                      const LsdRegion* __restrict__ regs,
+                                                      const unsigned* __restrict__ regpts, size_t regpts_frame,
+                                                      const int* __restrict__ nlines, double prec, double scale_lsd,
+                                                      LsdLine* __restrict__ lines) {
+    const int o = blockIdx.y, f = blockIdx.z, nOct = gridDim.y;
+    const int task = f * nOct + o;
+    const int n = min(nlines[task], kLsdRawCap);
+    const LineOctDev& od = octs[o];
+    const int sw = od.sw;
+    const double* M = modgrad + od.soff + (size_t)f * od.splane;
+    const unsigned* P = regpts + (size_t)task * regpts_frame;
+    for (int k = blockIdx.x * 64 + threadIdx.x; k < n; k += gridDim.x * 64) {
+        const LsdRegion r = regs[(size_t)task * kLsdRawCap + k];
+        const unsigned* q = P + r.start;
+        double xs = 0, ys = 0, sum = 0;
+        for (int j = 0; j < r.n; ++j) {
+            const unsigned v = q[j];
+            const int x = (int)(v & 0xffffu), y = (int)(v >> 16);
+            const double w = M[(size_t)y * sw + x];
+            xs += (double)x * w;
+            ys += (double)y * w;
+            sum += w;
+        }
+        xs /= sum;
+        ys /= sum;
+        double Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
+        for (int j = 0; j < r.n; ++j) {
+            const unsigned v = q[j];
+            const int x = (int)(v & 0xffffu), y = (int)(v >> 16);
+            const double w = M[(size_t)y * sw + x];
+            const double dx = (double)x - xs, dy = (double)y - ys;
+            Ixx += dy * dy * w;
+            Iyy += dx * dx * w;
+            Ixy -= dx * dy * w;
+        }
+        const double lambda = 0.5 * (Ixx + Iyy - __builtin_sqrt((Ixx - Iyy) * (Ixx - Iyy) + 4.0 * Ixy * Ixy));
+        double theta = (__builtin_fabs(Ixx) > __builtin_fabs(Iyy))
+                           ? (double)plvi_fast_atan2((float)(lambda - Ixx), (float)Ixy)
+                           : (double)plvi_fast_atan2((float)Ixy, (float)(lambda - Iyy));
+        theta *= kD2R;
+        if (angle_diff(theta, r.angle) > prec) theta += kPi;
+        const double dxv = plvi_cos(theta), dyv = plvi_sin(theta);
+        // l extents: the reference's if/else-if max/min is equivalent to
+        // independent max(0, .)/min(0, .) (l_min <= 0 <= l_max throughout).
+        double lmax = 0, lmin = 0;
+        for (int j = 0; j < r.n; ++j) {
+            const unsigned v = q[j];
+            const double l = ((double)(int)(v & 0xffffu) - xs) * dxv + ((double)(int)(v >> 16) - ys) * dyv;
+            lmax = l > lmax ? l : lmax;
+            lmin = l < lmin ? l : lmin;
+        }
+        double x1 = xs + lmin * dxv, y1 = ys + lmin * dyv;
+        double x2 = xs + lmax * dxv, y2 = ys + lmax * dyv;
+        x1 += 0.5; y1 += 0.5; x2 += 0.5; y2 += 0.5;
+        if (scale_lsd != 1) {
+            x1 /= scale_lsd; y1 /= scale_lsd; x2 /= scale_lsd; y2 /= scale_lsd;
+        }
+        lines[(size_t)task * kLsdRawCap + k] = LsdLine{(float)x1, (float)y1, (float)x2, (float)y2};
     }
 }
 
@@ -994,3 +987,5 @@ __global__ __launch_bounds__(64) void lbd_describe_kernel(const LineOctDev* __re
 }
 
 }  // namespace plvi
+
+#include "lsd_grow2.hpp"

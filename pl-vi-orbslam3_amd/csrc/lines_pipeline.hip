@@ -52,7 +52,7 @@ struct LinePipeline {
     std::vector<float> scaleF, invScaleF;
     double SCALE = 0.8, prec = 0, rho = 0, min_length = 0;
     double gk[7]{};
-    DevBuf d_oct, d_tabs, octImg, pix, modg, seedcs, gbits, qspill, rawLines, nlines, klTmp, klOut, fnOut, cntOut, descOut, lbdBlur,
+    DevBuf d_oct, d_tabs, octImg, pix, modg, seedcs, gbits, qspill, regs, regpts, rawLines, nlines, klTmp, klOut, fnOut, cntOut, descOut, lbdBlur,
         lbdG, err, staging;
     size_t qspillFrame = 0, gbitsFrame = 0, lbdPlaneTotal = 0;
     int lastFrames = 0;
@@ -208,6 +208,8 @@ struct LinePipeline {
             modg.alloc(sizeof(double) * sOff) || seedcs.alloc(sizeof(float4) * sOff) ||
             gbits.alloc(sizeof(unsigned) * gbitsFrame * nOct * Bcap) || qspill.alloc(sizeof(unsigned) * qspillFrame * nOct * Bcap) ||
             rawLines.alloc(sizeof(LsdLine) * (size_t)kLsdRawCap * nOct * Bcap) ||
+            regs.alloc(sizeof(LsdRegion) * (size_t)kLsdRawCap * nOct * Bcap) ||
+            regpts.alloc(sizeof(unsigned) * qspillFrame * nOct * Bcap) ||
             nlines.alloc(sizeof(int) * nOct * Bcap) || klTmp.alloc(sizeof(plvi_keyline) * (size_t)kKlCap * Bcap) ||
             klOut.alloc(sizeof(plvi_keyline) * (size_t)fcap * Bcap) || fnOut.alloc(sizeof(double) * 3 * fcap * Bcap) ||
             cntOut.alloc(sizeof(int) * Bcap) || descOut.alloc((size_t)32 * fcap * Bcap) ||
@@ -224,19 +226,23 @@ struct LinePipeline {
         if (const char* e = getenv("PLVI_GROW_LDS")) budget = (size_t)atol(e);
         budget = std::min<size_t>(budget, 160 * 1024);
         growQL = budget >= 32 * 1024 ? 1024 : 256;
-        const size_t fixed = 64 * 3 * sizeof(double) + (size_t)growQL * sizeof(unsigned);
+        const size_t fixed = (size_t)growQL * sizeof(unsigned);
         const size_t perRow = maxSw * sizeof(float) + (maxSw + 31) / 32 * sizeof(unsigned);
-        growR = 4;
-        budget = std::max(budget, fixed + perRow * 4);  // at least a 4-row window (wide frames)
+        growR = 2;
+        budget = std::max(budget, fixed + perRow * 2);  // at least a 2-row window
         if (budget > 160 * 1024) return PLVI_E_BADARG;
         while (growR * 2 <= 1024 && fixed + perRow * growR * 2 <= budget) growR *= 2;
         growSmem = fixed + perRow * growR;
         for (const void* k : {(const void*)lsd_grow_kernel<false>, (const void*)lsd_grow_kernel<true>})
             PLVI_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)growSmem));
+        PLVI_CHECK(hipFuncSetAttribute((const void*)lsd_grow2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)(2 * growSmem)));
+        // PLVI_GROW_PACK: tasks per region-growing wave (1 = lsd_grow_kernel, default; 2 = lsd_grow2_kernel)
+        if (const char* e = getenv("PLVI_GROW_PACK")) growPack = atoi(e) == 2 ? 2 : 1;
         return PLVI_OK;
     }
     size_t growSmem = 0;
-    int growR = 0, growQL = 0;
+    int growR = 0, growQL = 0, growPack = 1;
     unsigned long long* growStats = nullptr;  // diagnostic cycle counters (plvi_lines_debug_stats)
 
     int profile(int on) {
@@ -295,12 +301,24 @@ struct LinePipeline {
 
     // Phase B: region growing (LK3) + keyline assembly / top-k (LK4).
     void launch_grow_assemble(int nf, hipStream_t st) {
-        auto growK = growStats ? lsd_grow_kernel<true> : lsd_grow_kernel<false>;
-        hipLaunchKernelGGL(growK, dim3(nOct, nf), dim3(64), growSmem, st, d_oct.as<LineOctDev>(),
-                           (const float*)pix.as<float>(), (const double*)modg.as<double>(),
-                           (const float4*)seedcs.as<float4>(), gbits.as<unsigned>(), gbitsFrame, qspill.as<unsigned>(),
-                           qspillFrame, prec, SCALE, rawLines.as<LsdLine>(), nlines.as<int>(), err.as<int>(), growR,
-                           growQL, growStats);
+        if (growPack == 2 && !growStats) {
+            hipLaunchKernelGGL(lsd_grow2_kernel, dim3(nOct, (nf + 1) / 2), dim3(64), 2 * growSmem, st,
+                               d_oct.as<LineOctDev>(), (const float*)pix.as<float>(),
+                               (const float4*)seedcs.as<float4>(), gbits.as<unsigned>(), gbitsFrame,
+                               qspill.as<unsigned>(), qspillFrame, prec, regs.as<LsdRegion>(), regpts.as<unsigned>(),
+                               qspillFrame, nlines.as<int>(), err.as<int>(), growR, growQL, nf, (int)(growSmem / 4));
+        } else {
+            auto growK = growStats ? lsd_grow_kernel<true> : lsd_grow_kernel<false>;
+            hipLaunchKernelGGL(growK, dim3(nOct, nf), dim3(64), growSmem, st, d_oct.as<LineOctDev>(),
+                               (const float*)pix.as<float>(), (const double*)modg.as<double>(),
+                               (const float4*)seedcs.as<float4>(), gbits.as<unsigned>(), gbitsFrame,
+                               qspill.as<unsigned>(), qspillFrame, prec, regs.as<LsdRegion>(), regpts.as<unsigned>(),
+                               qspillFrame, nlines.as<int>(), err.as<int>(), growR, growQL, growStats);
+        }
+        hipLaunchKernelGGL(lsd_rect_kernel, dim3(kRectBlocks, nOct, nf), dim3(64), 0, st, d_oct.as<LineOctDev>(),
+                           (const double*)modg.as<double>(), (const LsdRegion*)regs.as<LsdRegion>(),
+                           (const unsigned*)regpts.as<unsigned>(), qspillFrame, (const int*)nlines.as<int>(), prec,
+                           SCALE, rawLines.as<LsdLine>());
         mark(3, st);
         hipLaunchKernelGGL(line_assemble_kernel, dim3(nf), dim3(256), 0, st, d_oct.as<LineOctDev>(), nOct,
                            (const LsdLine*)rawLines.as<LsdLine>(), (const int*)nlines.as<int>(), min_length,
