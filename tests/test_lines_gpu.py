@@ -86,3 +86,25 @@ def test_lines_batch_equals_single(lx640):
     for f in range(4):
         s = slice(f * cap, f * cap + cnt[f])
         _assert_same((kl[s], de[s], fn[s]), ol.line_extract(frames[f]), f"batch{f}")
+
+
+def test_lines_two_frames_per_wave_variant(plvi_lib, monkeypatch):
+    """lsd_grow2_kernel (PLVI_GROW_PACK=2: two frames per region-growing wave)
+    gives the oracle's lines too, including an odd batch (last wave half-empty)."""
+    monkeypatch.setenv("PLVI_GROW_PACK", "2")
+    lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 640, 480, max_batch=3)
+    frames = synth.batch(3, seed0=60)
+    buf = plvi.DeviceBuffer(frames.nbytes)
+    buf.upload(frames)
+    lx.extract_batch(buf.ptr, 3, 640 * 480, 640)
+    plvi.load().plvi_device_synchronize()
+    klp, dep, fnp, cop, cap = lx.outputs()
+    cnt = plvi.download(cop, np.zeros(3, np.int32))
+    kl = plvi.download(klp, np.zeros(3 * cap, plvi.KEYLINE_DTYPE))
+    de = plvi.download(dep, np.zeros((3 * cap, 32), np.uint8))
+    fn = plvi.download(fnp, np.zeros((3 * cap, 3), np.float64))
+    for f in range(3):
+        s = slice(f * cap, f * cap + cnt[f])
+        _assert_same((kl[s], de[s], fn[s]), ol.line_extract(frames[f]), f"pack2 batch{f}")
+    img = real_frames()["rgb1_gray"]
+    _assert_same(lx(img), ol.line_extract(img), "pack2 rgb1_gray")
