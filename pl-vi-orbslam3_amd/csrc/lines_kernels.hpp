@@ -240,6 +240,19 @@ __device__ __forceinline__ bool is_aligned_deg(float deg, double theta, double p
     return deg != kNotdefF && n_theta <= prec;
 }
 
+// The same decision from the float degree difference T - D (theta = (double)T
+// * DEG_TO_RADS, T the float fastAtan2 result the region angle comes from):
+// more than 1e-3 degrees away from prec and 360 - prec the outcome is fixed
+// (the 3pi/2 branch of isAligned cannot flip it there), so the double test
+// runs only inside that margin (float / double rounding is < 1e-4 degrees).
+__device__ __forceinline__ bool is_aligned_fast(float deg, float tdeg, float pdeg, double prec) {
+    const float dd = __builtin_fabsf(tdeg - deg);
+    const bool near = __builtin_fabsf(dd - pdeg) < 1e-3f || __builtin_fabsf(dd - (360.f - pdeg)) < 1e-3f;
+    bool r = deg != kNotdefF && (dd <= pdeg || dd >= 360.f - pdeg);
+    if (__builtin_expect(near, 0)) r = is_aligned_deg(deg, (double)tdeg * kD2R, prec);
+    return r;
+}
+
 __device__ __forceinline__ double angle_diff(double a, double b) {
     double diff = a - b;
     while (diff <= -kPi) diff += (2 * kPi);
@@ -334,6 +347,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
     __syncthreads();
     int nout = 0;
     bool overflow = false;
+    const float pdeg = (float)(prec / kD2R);  // ANG_TH in degrees
     const int min_reg = od.min_reg_size;
     const int bp = lane / 9, bk = lane % 9;  // block point / neighbour index of this lane
     const int kdx = bk % 3 - 1, kdy = bk / 3 - 1;
@@ -371,7 +385,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                 const int sx = xb + b;
                 if (used_get(g, sx, y)) continue;  // absorbed by an earlier region of this chunk
                 // ---- region_grow (lsd.cpp:635-686)
-                double reg_angle = (double)deg_at(g, sx, y) * kD2R;
+                float reg_deg = deg_at(g, sx, y);  // reg_angle = (double)reg_deg * DEG_TO_RADS
                 float sumdx = readlane_f(scl.x, b);
                 float sumdy = readlane_f(scl.y, b);
                 if (lane == 0) {
@@ -415,7 +429,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                         if (do_stats) { n_round++; r0t = __builtin_amdgcn_s_memtime(); }
                         const unsigned long long fromStart = ~0ull << start;
                         const bool candl = lane >= start && deg != kNotdefF && !used_get(g, nx, ny);
-                        const bool al = candl && is_aligned_deg(deg, reg_angle, prec);
+                        const bool al = candl && is_aligned_fast(deg, reg_deg, pdeg, prec);
                         const bool acc = al && (dup & fromStart) == 0ull;
                         const unsigned long long A = __ballot(acc);
                         if (do_stats) { const unsigned long long t = __builtin_amdgcn_s_memtime(); s_ph[0] += t - r0t; r0t = t; }
@@ -430,21 +444,21 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                             if (lane == t) { pfx = sx2; pfy = sy2; }
                         }
                         const int mcount = t;
-                        const double th = lane < mcount ? (double)plvi_fast_atan2(pfy, pfx) * kD2R : 0.0;
+                        const float th = lane < mcount ? plvi_fast_atan2(pfy, pfx) : 0.f;
                         if (do_stats) { const unsigned long long t = __builtin_amdgcn_s_memtime(); s_ph[1] += t - r0t; r0t = t; }
                         // verify every decision against the angle it really sees
                         const int cl = __popcll(A & below);
-                        double theta_l = reg_angle;
+                        float theta_l = reg_deg;
                         if (mcount <= 6) {
                             for (int k = 0; k < mcount; ++k) {
-                                const double v = readlane_d(th, k);
+                                const float v = readlane_f(th, k);
                                 if (cl == k + 1) theta_l = v;
                             }
                         } else {
-                            const double v = shfl_d(th, cl > 0 ? cl - 1 : 0);
+                            const float v = __shfl(th, cl > 0 ? cl - 1 : 0);
                             if (cl > 0) theta_l = v;
                         }
-                        const bool al2 = candl && (dup & A) == 0ull && is_aligned_deg(deg, theta_l, prec);
+                        const bool al2 = candl && (dup & A) == 0ull && is_aligned_fast(deg, theta_l, pdeg, prec);
                         const unsigned long long mism = __ballot(al2 != acc) & fromStart;
                         if (do_stats) { const unsigned long long t = __builtin_amdgcn_s_memtime(); s_ph[2] += t - r0t; r0t = t; }
                         unsigned long long C;
@@ -470,7 +484,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                             reg_size += nc;
                             sumdx = readlane_f(pfx, nc - 1);
                             sumdy = readlane_f(pfy, nc - 1);
-                            reg_angle = readlane_d(th, nc - 1);
+                            reg_deg = readlane_f(th, nc - 1);
                             if (do_stats) n_commit += nc;
                         }
                         __builtin_amdgcn_wave_barrier();
@@ -486,7 +500,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                 // over the region's points in queue order and its angle
                 if (nout < kLsdRawCap) {
                     for (int j = lane; j < reg_size; j += 64) outP[npts + j] = q_get(g, j);
-                    if (lane == 0) outR[nout] = LsdRegion{npts, reg_size, reg_angle};
+                    if (lane == 0) outR[nout] = LsdRegion{npts, reg_size, (double)reg_deg * kD2R};
                     npts += reg_size;
                     ++nout;
                 } else {
@@ -511,19 +525,22 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
 
 // ---------------------------------------------------------------------------
 // LK3b: region2rect (lsd.cpp:688-744) + get_theta (:746-782) of every region
-// lsd_grow_kernel kept (reg_size >= min_reg_size), one lane per region.  The
-// weighted centroid / inertia sums run sequentially in region order as in the
-// reference (double, no contraction); the l extents are order-free max/min.
-// Emits the Vec4f of flsd (:506-518) at the region's index.
+// lsd_grow_kernel kept (reg_size >= min_reg_size), one wave per region: the
+// lanes gather the points and weights (many loads in flight) and form the
+// per-point products, lane 0 adds them from LDS in region order (the
+// reference's double summation order, no contraction); the l extents are
+// order-free max/min reductions.  Emits the Vec4f of flsd (:506-518) at the
+// region's index.
 // ---------------------------------------------------------------------------
-constexpr int kRectBlocks = 8;  // 64-lane blocks per (octave, frame); lanes stride over the regions
+constexpr int kRectBlocks = 32;  // 4-wave workgroups per (octave, frame); waves stride over the regions
 
-__global__ __launch_bounds__(64) void lsd_rect_kernel(const LineOctDev* __restrict__ octs,
-                                                      const double* __restrict__ modgrad,
-                                                      const LsdRegion* __restrict__ regs,
-                                                      const unsigned* __restrict__ regpts, size_t regpts_frame,
-                                                      const int* __restrict__ nlines, double prec, double scale_lsd,
-                                                      LsdLine* __restrict__ lines) {
+__global__ __launch_bounds__(256) void lsd_rect_kernel(const LineOctDev* __restrict__ octs,
+                                                       const double* __restrict__ modgrad,
+                                                       const LsdRegion* __restrict__ regs,
+                                                       const unsigned* __restrict__ regpts, size_t regpts_frame,
+                                                       const int* __restrict__ nlines, double prec, double scale_lsd,
+                                                       LsdLine* __restrict__ lines) {
+    __shared__ double rs[4][3][64];
     const int o = blockIdx.y, f = blockIdx.z, nOct = gridDim.y;
     const int task = f * nOct + o;
     const int n = min(nlines[task], kLsdRawCap);
@@ -531,30 +548,71 @@ __global__ __launch_bounds__(64) void lsd_rect_kernel(const LineOctDev* __restri
     const int sw = od.sw;
     const double* M = modgrad + od.soff + (size_t)f * od.splane;
     const unsigned* P = regpts + (size_t)task * regpts_frame;
-    for (int k = blockIdx.x * 64 + threadIdx.x; k < n; k += gridDim.x * 64) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    double* R0 = rs[wv][0];
+    double* R1 = rs[wv][1];
+    double* R2 = rs[wv][2];
+    for (int k = blockIdx.x * 4 + wv; k < n; k += gridDim.x * 4) {
         const LsdRegion r = regs[(size_t)task * kLsdRawCap + k];
         const unsigned* q = P + r.start;
-        double xs = 0, ys = 0, sum = 0;
-        for (int j = 0; j < r.n; ++j) {
-            const unsigned v = q[j];
-            const int x = (int)(v & 0xffffu), y = (int)(v >> 16);
-            const double w = M[(size_t)y * sw + x];
-            xs += (double)x * w;
-            ys += (double)y * w;
-            sum += w;
+        unsigned v0 = 0u;
+        double w0 = 0.0;
+        if (lane < r.n) {
+            v0 = q[lane];
+            w0 = M[(size_t)(v0 >> 16) * sw + (v0 & 0xffffu)];
         }
-        xs /= sum;
-        ys /= sum;
-        double Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
-        for (int j = 0; j < r.n; ++j) {
-            const unsigned v = q[j];
-            const int x = (int)(v & 0xffffu), y = (int)(v >> 16);
-            const double w = M[(size_t)y * sw + x];
-            const double dx = (double)x - xs, dy = (double)y - ys;
-            Ixx += dy * dy * w;
-            Iyy += dx * dx * w;
-            Ixy -= dx * dy * w;
+        double xs = 0, ys = 0, sum = 0, Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
+        for (int pass = 0; pass < 2; ++pass) {
+            for (int base = 0; base < r.n; base += 64) {
+                const int j = base + lane;
+                if (j < r.n) {
+                    const unsigned v = base == 0 ? v0 : q[j];
+                    const double w = base == 0 ? w0 : M[(size_t)(v >> 16) * sw + (v & 0xffffu)];
+                    const double rx = (double)(int)(v & 0xffffu), ry = (double)(int)(v >> 16);
+                    if (pass == 0) {
+                        R0[lane] = rx * w;
+                        R1[lane] = ry * w;
+                        R2[lane] = w;
+                    } else {
+                        const double dx = rx - xs, dy = ry - ys;
+                        R0[lane] = dy * dy * w;
+                        R1[lane] = dx * dx * w;
+                        R2[lane] = dx * dy * w;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (lane == 0) {
+                    const int nn = min(64, r.n - base);
+                    if (pass == 0) {
+#pragma unroll 4
+                        for (int t = 0; t < nn; ++t) {
+                            xs += R0[t];
+                            ys += R1[t];
+                            sum += R2[t];
+                        }
+                    } else {
+#pragma unroll 4
+                        for (int t = 0; t < nn; ++t) {
+                            Ixx += R0[t];
+                            Iyy += R1[t];
+                            Ixy -= R2[t];
+                        }
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+            if (pass == 0) {
+                xs = readlane_d(xs, 0) / readlane_d(sum, 0);
+                ys = readlane_d(ys, 0) / readlane_d(sum, 0);
+            }
         }
+        Ixx = readlane_d(Ixx, 0);
+        Iyy = readlane_d(Iyy, 0);
+        Ixy = readlane_d(Ixy, 0);
         const double lambda = 0.5 * (Ixx + Iyy - __builtin_sqrt((Ixx - Iyy) * (Ixx - Iyy) + 4.0 * Ixy * Ixy));
         double theta = (__builtin_fabs(Ixx) > __builtin_fabs(Iyy))
                            ? (double)plvi_fast_atan2((float)(lambda - Ixx), (float)Ixy)
@@ -565,11 +623,16 @@ __global__ __launch_bounds__(64) void lsd_rect_kernel(const LineOctDev* __restri
         // l extents: the reference's if/else-if max/min is equivalent to
         // independent max(0, .)/min(0, .) (l_min <= 0 <= l_max throughout).
         double lmax = 0, lmin = 0;
-        for (int j = 0; j < r.n; ++j) {
-            const unsigned v = q[j];
+        for (int j = lane; j < r.n; j += 64) {
+            const unsigned v = j < 64 ? v0 : q[j];
             const double l = ((double)(int)(v & 0xffffu) - xs) * dxv + ((double)(int)(v >> 16) - ys) * dyv;
             lmax = l > lmax ? l : lmax;
             lmin = l < lmin ? l : lmin;
+        }
+        for (int s2 = 32; s2 > 0; s2 >>= 1) {
+            const double a2 = __shfl_xor(lmax, s2), b2 = __shfl_xor(lmin, s2);
+            lmax = a2 > lmax ? a2 : lmax;
+            lmin = b2 < lmin ? b2 : lmin;
         }
         double x1 = xs + lmin * dxv, y1 = ys + lmin * dyv;
         double x2 = xs + lmax * dxv, y2 = ys + lmax * dyv;
@@ -577,7 +640,7 @@ __global__ __launch_bounds__(64) void lsd_rect_kernel(const LineOctDev* __restri
         if (scale_lsd != 1) {
             x1 /= scale_lsd; y1 /= scale_lsd; x2 /= scale_lsd; y2 /= scale_lsd;
         }
-        lines[(size_t)task * kLsdRawCap + k] = LsdLine{(float)x1, (float)y1, (float)x2, (float)y2};
+        if (lane == 0) lines[(size_t)task * kLsdRawCap + k] = LsdLine{(float)x1, (float)y1, (float)x2, (float)y2};
     }
 }
 

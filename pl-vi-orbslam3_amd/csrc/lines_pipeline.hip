@@ -315,7 +315,7 @@ struct LinePipeline {
                                qspill.as<unsigned>(), qspillFrame, prec, regs.as<LsdRegion>(), regpts.as<unsigned>(),
                                qspillFrame, nlines.as<int>(), err.as<int>(), growR, growQL, growStats);
         }
-        hipLaunchKernelGGL(lsd_rect_kernel, dim3(kRectBlocks, nOct, nf), dim3(64), 0, st, d_oct.as<LineOctDev>(),
+        hipLaunchKernelGGL(lsd_rect_kernel, dim3(kRectBlocks, nOct, nf), dim3(256), 0, st, d_oct.as<LineOctDev>(),
                            (const double*)modg.as<double>(), (const LsdRegion*)regs.as<LsdRegion>(),
                            (const unsigned*)regpts.as<unsigned>(), qspillFrame, (const int*)nlines.as<int>(), prec,
                            SCALE, rawLines.as<LsdLine>());

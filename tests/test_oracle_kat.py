@@ -168,3 +168,33 @@ def test_oracle_lapping_area_reverses_order():
     m2, k2, d2 = ol.orb_extract(img, lap=(0, 1000))
     assert m2 == 0
     assert np.array_equal(k2[::-1], k) and np.array_equal(d2[::-1], d)
+
+
+def test_is_aligned_float_prefilter_matches_double():
+    """lsd_grow_kernel's is_aligned_fast: the float |T - D| decision outside a
+    1e-3 degree margin around prec / 360 - prec equals lsd.cpp's double
+    isAligned(a = D*DEG_TO_RADS, theta = T*DEG_TO_RADS, prec) (:1136-1152)."""
+    rng = np.random.default_rng(5)
+    f32, f64 = np.float32, np.float64
+    d2r = np.pi / 180
+    prec = np.pi * 22.5 / 180
+    pdeg = f32(prec / d2r)
+    n = 400000
+    T = rng.uniform(0, 360, n).astype(f32)
+    D = rng.uniform(0, 360, n).astype(f32)
+    # adversarial: differences near 22.5, 337.5, 270 and tiny angles
+    k = n // 4
+    off = rng.choice([22.5, -22.5, 337.5, -337.5, 270.0, -270.0], k) + rng.normal(0, 2e-3, k)
+    D[:k] = rng.uniform(0, 360, k).astype(f32)
+    T[:k] = np.clip(D[:k].astype(f64) + off, 0, 359.9999).astype(f32)
+    T[k:k + 1000] = rng.uniform(0, 1e-6, 1000).astype(f32)
+    a = D.astype(f64) * d2r
+    th = T.astype(f64) * d2r
+    dd = np.abs(th - a)
+    n_theta = np.where(dd > 3 * np.pi / 2, np.abs(dd - 2 * np.pi), dd)
+    exact = n_theta <= prec
+    df = np.abs(T - D).astype(f32)
+    near = (np.abs(df - pdeg) < f32(1e-3)) | (np.abs(df - (f32(360) - pdeg)) < f32(1e-3))
+    fast = (df <= pdeg) | (df >= f32(360) - pdeg)
+    assert near.sum() > 100  # the margin is exercised
+    assert np.array_equal(fast[~near], exact[~near])
