@@ -17,8 +17,11 @@ struct OrbLevelDev {
     int minB;         // EDGE_THRESHOLD-3 = 16
     int rw, rh;       // relative region (maxBorder-minBorder)
     int nCols, nRows, wCell, hCell;
-    long long satOff;    // int offset of this level's frame-0 SAT
-    long long satPlane;  // ints per frame SAT ((rw+1)*(rh+1))
+    long long satOff;    // ushort offset of this level's frame-0 strip-local SAT
+    long long satPlane;  // ushorts per frame ((rh+1) x satStrips*64)
+    long long carryOff;  // int offset of this level's frame-0 strip carry table
+    long long carryPlane;  // ints per frame ((rh+1) x (satStrips+1))
+    int satStrips;       // 64-column strips covering SAT columns 0..rw
     int quota;           // mnFeaturesPerLevel
     int nodeCap;         // octree output capacity (>= quota+3)
     int kpOff;           // offset of this level in the per-frame level-keypoint table

@@ -507,31 +507,37 @@ __global__ __launch_bounds__(64) void orb_cell_nms_kernel(const OrbCellDev* __re
 
 // ---------------------------------------------------------------------------
 // K3: summed-area table of the candidate indicator over each level's octree
-// region [minB, minB+rw) x [minB, minB+rh).  SAT[y][x] = #candidates in
-// [0,x) x [0,y) (relative coords), (rw+1) x (rh+1).
+// region [minB, minB+rw) x [minB, minB+rh): SAT(x, y) = #candidates in
+// [0,x) x [0,y) (relative coords), x in [0, rw], y in [0, rh].  Stored per
+// 64-column strip s: SAT(64s + j, y) = Carry(s, y) + Local(s, j, y), Local
+// the strip's own counts (< 64 * rh < 2^16: ushort), Carry(s, y) the
+// candidates of the strips left of s.  One pass: read the candidate bytes
+// once, write 2 B per pixel (the two-pass int32 table moved 13 B per pixel).
 // ---------------------------------------------------------------------------
 constexpr int kSatRowsPerWave = 8;
 
-// Row prefix counts, kSatRowsPerWave rows per wave (their loads in flight together).
-__global__ __launch_bounds__(64) void orb_sat_rows_kernel(const OrbLevelDev* __restrict__ lvs,
-                                                          const uint8_t* __restrict__ cand, int* __restrict__ sat) {
-    const int l = blockIdx.y, f = blockIdx.z;
+// One wave per (strip, level, frame): lane = column, rows top-down, 8 rows'
+// loads in flight; wave prefix scan per row, running column sums.
+__global__ __launch_bounds__(64) void orb_sat_strip_kernel(const OrbLevelDev* __restrict__ lvs,
+                                                           const uint8_t* __restrict__ cand,
+                                                           unsigned short* __restrict__ lsat, int* __restrict__ carry) {
+    const int s = blockIdx.x, l = blockIdx.y, f = blockIdx.z;
     const OrbLevelDev& L = lvs[l];
-    const int yb = blockIdx.x * kSatRowsPerWave;
-    if (yb > L.rh) return;
-    int* base = sat + L.satOff + (size_t)f * L.satPlane;
+    const int nS = L.satStrips;
+    if (s >= nS) return;
+    const int lane = threadIdx.x, x = 64 * s + lane, pitch = 64 * nS;
+    unsigned short* base = lsat + L.satOff + (size_t)f * L.satPlane;
+    int* T = carry + L.carryOff + (size_t)f * L.carryPlane;
     const uint8_t* C0 = cand + L.off + (size_t)f * L.plane + (size_t)L.minB * L.w + L.minB;
-    const int lane = threadIdx.x;
-    int carry[kSatRowsPerWave];
-#pragma unroll
-    for (int k = 0; k < kSatRowsPerWave; ++k) carry[k] = 0;
-    for (int x0 = 0; x0 < L.rw; x0 += 64) {
-        const int x = x0 + lane;
+    base[x] = 0;
+    if (lane == 0) T[s + 1] = 0;
+    int colacc = 0, tot = 0;
+    for (int y0 = 1; y0 <= L.rh; y0 += kSatRowsPerWave) {
         int v[kSatRowsPerWave];
 #pragma unroll
         for (int k = 0; k < kSatRowsPerWave; ++k) {
-            const int y = yb + k;  // SAT row y counts image row y-1 of the region
-            v[k] = (y >= 1 && y <= L.rh && x < L.rw) ? (C0[(size_t)(y - 1) * L.w + x] != 0) : 0;
+            const int y = y0 + k;  // SAT row y counts image row y-1 of the region
+            v[k] = (y <= L.rh && x < L.rw) ? (C0[(size_t)(y - 1) * L.w + x] != 0) : 0;
         }
 #pragma unroll
         for (int k = 0; k < kSatRowsPerWave; ++k) {
@@ -541,38 +547,32 @@ __global__ __launch_bounds__(64) void orb_sat_rows_kernel(const OrbLevelDev* __r
                 const int nb = __shfl_up(t, o);
                 if (lane >= o) t += nb;
             }
-            const int y = yb + k;
-            if (y <= L.rh && x < L.rw) base[(size_t)y * (L.rw + 1) + x + 1] = carry[k] + t;
-            carry[k] += __shfl(t, 63);
+            colacc += t - v[k];  // candidates of this row left of x within the strip
+            tot += __shfl(t, 63);
+            const int y = y0 + k;
+            if (y <= L.rh) {
+                base[(size_t)y * pitch + x] = (unsigned short)colacc;
+                if (lane == 0) T[(size_t)y * (nS + 1) + s + 1] = tot;
+            }
         }
     }
-    if (lane < kSatRowsPerWave && yb + lane <= L.rh) base[(size_t)(yb + lane) * (L.rw + 1)] = 0;
 }
 
-// Column prefix, one thread per column, 16 rows' loads in flight.
-__global__ __launch_bounds__(256) void orb_sat_cols_kernel(const OrbLevelDev* __restrict__ lvs,
-                                                           int* __restrict__ sat) {
+// Carry(s, y) = sum of the strip totals left of s (in place), one thread per row.
+__global__ __launch_bounds__(256) void orb_sat_carry_kernel(const OrbLevelDev* __restrict__ lvs,
+                                                            int* __restrict__ carry) {
     const int l = blockIdx.y, f = blockIdx.z;
     const OrbLevelDev& L = lvs[l];
-    const int x = blockIdx.x * 256 + threadIdx.x;
-    if (x > L.rw) return;
-    const int st = L.rw + 1;
-    int* col = sat + L.satOff + (size_t)f * L.satPlane + x;
+    const int y = blockIdx.x * 256 + threadIdx.x;
+    if (y > L.rh) return;
+    const int nS = L.satStrips;
+    int* row = carry + L.carryOff + (size_t)f * L.carryPlane + (size_t)y * (nS + 1);
+    // row[k] (k >= 1) holds strip k-1's total; Carry(s) = row[1] + ... + row[s]
     int acc = 0;
-    int y = 1;
-    for (; y + 16 <= L.rh + 1; y += 16) {
-        int v[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = col[(size_t)(y + k) * st];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            acc += v[k];
-            col[(size_t)(y + k) * st] = acc;
-        }
-    }
-    for (; y <= L.rh; ++y) {
-        acc += col[(size_t)y * st];
-        col[(size_t)y * st] = acc;
+    row[0] = 0;
+    for (int k = 1; k <= nS; ++k) {
+        acc += row[k];
+        row[k] = acc;
     }
 }
 
@@ -602,7 +602,8 @@ struct OctNodes {
 // phase will perform are gathered first by all lanes in parallel: the
 // children of a node depend only on the node, not on the list order.
 __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __restrict__ lvs,
-                                                        const int* __restrict__ sat, short4* __restrict__ out_rect,
+                                                        const unsigned short* __restrict__ lsat,
+                                                        const int* __restrict__ carry, short4* __restrict__ out_rect,
                                                         int* __restrict__ out_cnt, int nodeCapMax, int L,
                                                         int* __restrict__ err) {
     extern __shared__ __align__(16) unsigned char smem[];
@@ -622,18 +623,20 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
         n.vsz = sp; sp += C; n.vprev = sp; sp += C; n.todo = sp; sp += C;
         n.nomore = reinterpret_cast<unsigned char*>(sp);
     }
-    const int* S = sat + lv.satOff + (size_t)f * lv.satPlane;
-    const int st = lv.rw + 1, RW = lv.rw, RH = lv.rh;
+    const unsigned short* S = lsat + lv.satOff + (size_t)f * lv.satPlane;
+    const int* T = carry + lv.carryOff + (size_t)f * lv.carryPlane;
+    const int st = 64 * lv.satStrips, ct = lv.satStrips + 1, RW = lv.rw, RH = lv.rh;
+    auto sat_raw = [&](int x, int y) -> int { return T[y * ct + (x >> 6)] + (int)S[y * st + x]; };
     auto sat_at = [&](int x, int y) -> int {
         x = max(0, min(x, RW));
         y = max(0, min(y, RH));
-        return S[y * st + x];
+        return sat_raw(x, y);
     };
     auto count = [&](int x0, int y0, int x1, int y1) -> int {
         x0 = max(0, min(x0, RW)); x1 = max(0, min(x1, RW));
         y0 = max(0, min(y0, RH)); y1 = max(0, min(y1, RH));
         if (x0 >= x1 || y0 >= y1) return 0;
-        return S[y1 * st + x1] - S[y0 * st + x1] - S[y1 * st + x0] + S[y0 * st + x0];
+        return sat_raw(x1, y1) - sat_raw(x1, y0) - sat_raw(x0, y1) + sat_raw(x0, y0);
     };
     // children counts of nodes ids[0..k): lanes in parallel, 16 SAT loads each in flight
     auto prefetch = [&](const short* ids, int k) {

@@ -75,7 +75,7 @@ struct OrbPipeline {
     int kpCapFrame = 0, nodeCapMax = 0;
     size_t pyrBytesFrameTotal = 0, satIntsFrameTotal = 0;
     size_t lvOff0 = 0;  // (unused)
-    DevBuf d_lv, d_cells, d_strips, d_tabs, pyr, blur, score, cand, sat, rects, rectCnt, lvkp, lvdesc, okp, odesc, ocount,
+    DevBuf d_lv, d_cells, d_strips, d_tabs, pyr, blur, score, cand, sat, carry, rects, rectCnt, lvkp, lvdesc, okp, odesc, ocount,
         omono, err, staging;
     std::vector<size_t> tabXofs, tabXa, tabYrow, tabYb;  // byte offsets in d_tabs per level
     int lastFrames = 0;
@@ -191,7 +191,7 @@ struct OrbPipeline {
         // Levels
         lv.resize(L);
         rtab.resize(L);
-        size_t off = 0, satOff = 0;
+        size_t off = 0, satOff = 0, carryOff = 0;
         int kpOff = 0;
         nodeCapMax = 0;
         for (int l = 0; l < L; ++l) {
@@ -213,9 +213,15 @@ struct OrbPipeline {
             d.wCell = (int)std::ceil(width / d.nCols);
             d.hCell = (int)std::ceil(height / d.nRows);
             if (d.wCell + 6 > kOrbCellMax || d.hCell + 6 > kOrbCellMax) return PLVI_E_BADARG;
-            d.satPlane = (long long)(d.rw + 1) * (d.rh + 1);
+            // strip-local SAT (K3): Local counts < 64 * rh must fit a ushort
+            if (64LL * d.rh >= 65536) return PLVI_E_BADARG;
+            d.satStrips = d.rw / 64 + 1;  // covers SAT columns 0..rw
+            d.satPlane = (long long)(d.rh + 1) * 64 * d.satStrips;
             d.satOff = (long long)satOff;
             satOff += (size_t)d.satPlane * Bcap;
+            d.carryPlane = (long long)(d.rh + 1) * (d.satStrips + 1);
+            d.carryOff = (long long)carryOff;
+            carryOff += (size_t)d.carryPlane * Bcap;
             d.quota = quota[l];
             d.scale = scale[l];
             d.size = (float)(int)(31 * scale[l]);
@@ -292,7 +298,7 @@ struct OrbPipeline {
         PLVI_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax.data(), 16 * sizeof(int)));
         // work buffers
         if (pyr.alloc(off) || blur.alloc(off) || score.alloc(off) || cand.alloc(off) ||
-            sat.alloc(satOff * sizeof(int)) || rects.alloc(sizeof(short4) * (size_t)nodeCapMax * L * Bcap) ||
+            sat.alloc(satOff * sizeof(unsigned short)) || carry.alloc(carryOff * sizeof(int)) || rects.alloc(sizeof(short4) * (size_t)nodeCapMax * L * Bcap) ||
             rectCnt.alloc(sizeof(int) * L * Bcap) || lvkp.alloc(sizeof(float4) * (size_t)kpCapFrame * Bcap) ||
             lvdesc.alloc((size_t)32 * kpCapFrame * Bcap) || okp.alloc(sizeof(plvi_keypoint) * (size_t)kpCapFrame * Bcap) ||
             odesc.alloc((size_t)32 * kpCapFrame * Bcap) || ocount.alloc(sizeof(int) * Bcap) ||
@@ -345,18 +351,18 @@ struct OrbPipeline {
                            d_cells.as<OrbCellDev>(), d_lv.as<OrbLevelDev>(), (const uint8_t*)Sc, Cd, t1, t2);
         mark(2, st);
         // K3 SAT
-        int maxRh = 0, maxRw = 0;
-        for (auto& d : lv) { maxRh = std::max(maxRh, d.rh); maxRw = std::max(maxRw, d.rw); }
-        hipLaunchKernelGGL(orb_sat_rows_kernel, dim3((maxRh + kSatRowsPerWave) / kSatRowsPerWave, L, nf), dim3(64), 0,
-                           st, d_lv.as<OrbLevelDev>(),
-                           (const uint8_t*)Cd, sat.as<int>());
-        hipLaunchKernelGGL(orb_sat_cols_kernel, dim3((maxRw + 1 + 255) / 256, L, nf), dim3(256), 0, st,
-                           d_lv.as<OrbLevelDev>(), sat.as<int>());
+        int maxRh = 0, maxStrips = 0;
+        for (auto& d : lv) { maxRh = std::max(maxRh, d.rh); maxStrips = std::max(maxStrips, d.satStrips); }
+        hipLaunchKernelGGL(orb_sat_strip_kernel, dim3(maxStrips, L, nf), dim3(64), 0, st, d_lv.as<OrbLevelDev>(),
+                           (const uint8_t*)Cd, sat.as<unsigned short>(), carry.as<int>());
+        hipLaunchKernelGGL(orb_sat_carry_kernel, dim3((maxRh + 1 + 255) / 256, L, nf), dim3(256), 0, st,
+                           d_lv.as<OrbLevelDev>(), carry.as<int>());
         mark(3, st);
         // K4 octree
         const size_t smem = (size_t)nodeCapMax * (6 * 4 + 14 * 2 + 1) + 16;
         hipLaunchKernelGGL(orb_octree_kernel, dim3(L, nf), dim3(64), smem, st, d_lv.as<OrbLevelDev>(),
-                           (const int*)sat.as<int>(), rects.as<short4>(), rectCnt.as<int>(), nodeCapMax, L,
+                           (const unsigned short*)sat.as<unsigned short>(), (const int*)carry.as<int>(),
+                           rects.as<short4>(), rectCnt.as<int>(), nodeCapMax, L,
                            err.as<int>());
         mark(4, st);
         // K5 best per node
