@@ -74,32 +74,38 @@ __global__ __launch_bounds__(256) void lsd_prep_kernel(const uint8_t* __restrict
     }
     const uint8_t* S = src + (size_t)f * s_frame;
     const int IW = GW + 6, IH = GH + 6;
-    for (int i = threadIdx.x; i < IW * IH; i += 256) {
-        const int r = i / IW, c = i % IW;
-        I[r][c] = S[(size_t)reflect101(gy0 - 3 + r, gh) * s_row + reflect101(gx0 - 3 + c, gw)];
+    // 2-D thread mapping (no runtime divisions): lane = column (IW <= 54, GW <= 48),
+    // the 4 waves take every 4th row
+    const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
+    if (cx < IW) {
+        const int sx = reflect101(gx0 - 3 + cx, gw);
+        for (int r = ry; r < IH; r += 4) I[r][cx] = S[(size_t)reflect101(gy0 - 3 + r, gh) * s_row + sx];
     }
     __syncthreads();
     const double kk[7] = {k0, k1, k2, k3, k2, k1, k0};
-    for (int i = threadIdx.x; i < IH * GW; i += 256) {
-        const int r = i / GW, c = i % GW;
-        double s = kk[0] * (double)I[r][c];
+    if (cx < GW) {
+        for (int r = ry; r < IH; r += 4) {
+            double s = kk[0] * (double)I[r][cx];
 #pragma unroll
-        for (int k = 1; k < 7; ++k) s += kk[k] * (double)I[r][c + k];
-        Hs[r][c] = s;
+            for (int k = 1; k < 7; ++k) s += kk[k] * (double)I[r][cx + k];
+            Hs[r][cx] = s;
+        }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < GH * GW; i += 256) {
-        const int r = i / GW, c = i % GW;
-        double s = k3 * Hs[r + 3][c] + 0.0;
-        s += k2 * (Hs[r + 4][c] + Hs[r + 2][c]);
-        s += k1 * (Hs[r + 5][c] + Hs[r + 1][c]);
-        s += k0 * (Hs[r + 6][c] + Hs[r][c]);
-        Gs[r][c] = s;
+    if (cx < GW) {
+        for (int r = ry; r < GH; r += 4) {
+            double s = k3 * Hs[r + 3][cx] + 0.0;
+            s += k2 * (Hs[r + 4][cx] + Hs[r + 2][cx]);
+            s += k1 * (Hs[r + 5][cx] + Hs[r + 1][cx]);
+            s += k0 * (Hs[r + 6][cx] + Hs[r][cx]);
+            Gs[r][cx] = s;
+        }
     }
     __syncthreads();
     const int TW = Xe - X0 + 1, TH = Ye - Y0 + 1;
-    for (int i = threadIdx.x; i < TW * TH; i += 256) {
-        const int ty = i / TW, tx = i % TW;
+    for (int i = threadIdx.x; i < (kPTX + 1) * (kPTY + 1); i += 256) {
+        const int ty = i / (kPTX + 1), tx = i % (kPTX + 1);  // constant divisor (TW <= 33, TH <= 17)
+        if (tx >= TW || ty >= TH) continue;
         const int dx = X0 + tx, dy = Y0 + ty;
         const int r0 = yrow[2 * dy] - gy0, r1 = yrow[2 * dy + 1] - gy0;
         const double b0 = (double)yb[2 * dy], b1 = (double)yb[2 * dy + 1];
