@@ -111,6 +111,22 @@ static void divide_node(const Node& P, Node& n1, Node& n2, Node& n3, Node& n4) {
 
 typedef std::pair<int, long> SizeKey;  // (size, creation seq) — canonical (size, pointer)
 
+// SURVEY §8c diagnostic: the reference orders equal-size nodes by heap address
+// (B.1).  0 = creation order (a bump allocator: the canonical rule the HIP
+// path follows), 1 = reverse creation order, 2 = a pseudo-random address per
+// node (freed list nodes reused by malloc).
+static int g_tie_mode = 0;
+static long tie_key(long seq) {
+    if (g_tie_mode == 1) return -seq;
+    if (g_tie_mode == 2) {
+        unsigned long long z = (unsigned long long)seq + 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        return (long)((z ^ (z >> 31)) >> 1);
+    }
+    return seq;
+}
+
 // ORBextractor::DistributeOctTree (src/ORBextractor.cc:537-761).
 static std::vector<KP> distribute_octtree(const std::vector<KP>& keys, int minX, int maxX, int minY,
                                           int maxY, int N) {
@@ -143,7 +159,7 @@ static std::vector<KP> distribute_octtree(const std::vector<KP>& keys, int minX,
         lNodes.push_front(c);
         if (c.vKeys.size() > 1) {
             if (nToExpand) ++*nToExpand;
-            rec->push_back({SizeKey((int)c.vKeys.size(), lNodes.front().seq), &lNodes.front()});
+            rec->push_back({SizeKey((int)c.vKeys.size(), tie_key(lNodes.front().seq)), &lNodes.front()});
             lNodes.front().lit = lNodes.begin();
         }
     };
@@ -433,6 +449,8 @@ extern "C" int oracle_orb_stage(const uint8_t* img, int w, int h, int nfeatures,
     }
     return 0;
 }
+
+extern "C" void oracle_orb_set_tie_mode(int mode) { g_tie_mode = mode; }
 
 extern "C" void oracle_orb_params(int nfeatures, float scaleFactor, int nlevels, float* scale, int* perLevel,
                                   int* umax) {

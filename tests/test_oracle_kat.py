@@ -198,3 +198,21 @@ def test_is_aligned_float_prefilter_matches_double():
     fast = (df <= pdeg) | (df >= f32(360) - pdeg)
     assert near.sum() > 100  # the margin is exercised
     assert np.array_equal(fast[~near], exact[~near])
+
+
+def test_octree_tie_order_diagnostic():
+    """SURVEY §8c diagnostic (B.1): the reference breaks DistributeOctTree's
+    equal-size ties by heap address; other tie orders replace a few percent of
+    the keypoints (tools/octree_tie_diag.py), and mode 0 (creation order, the
+    canonical rule of the oracle and the HIP path) is restored afterwards."""
+    import sys
+    sys.path.insert(0, str(ol.ROOT / "tools"))
+    import octree_tie_diag
+    img = synth.frame(3)
+    before = ol.orb_extract(img)[1]
+    nf, out = octree_tie_diag.run(2)
+    assert nf >= 2 and set(out) == {"reverse", "random"}
+    for lv, fr, kp in out.values():
+        assert 0.0 < kp < 0.2  # some, but few, keypoints depend on the tie order
+    after = ol.orb_extract(img)[1]
+    assert before.tobytes() == after.tobytes()
