@@ -48,3 +48,38 @@ def test_frame_extract_equals_separate_extractors():
     mono, okps, odesc = ol.orb_extract(frames[0])
     assert cnt[0] == len(okps)
     np.testing.assert_array_equal(desc[:cnt[0]], odesc)
+
+
+def test_sharded_frames_match_whole_batch_digests():
+    """a rank-sharded run gives the single-GPU per-frame output.
+    Frames are independent, so the frame schedule on a shard (the second half
+    of a batch, as rank 1 of 2 would own it) must reproduce the whole batch's
+    per-frame results: SHA-256 digests of keypoints, descriptors, keylines
+    and LBD descriptors per frame."""
+    import hashlib
+    n = 8
+    frames = synth.batch(n, seed0=300)
+    lib = plvi.load()
+
+    def run(fr):
+        buf = plvi.DeviceBuffer(fr.nbytes)
+        buf.upload(fr)
+        m = len(fr)
+        orb = plvi.ORBextractor(1000, 1.2, 8, 20, 7, 640, 480, max_batch=m)
+        lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 640, 480, max_batch=m)
+        plvi.frame_extract_batch(orb, lx, buf.ptr, m, 640 * 480, 640)
+        lib.plvi_device_synchronize()
+        oc, ok, od, ocap = _orb_out(orb, m)
+        lc, lk, ld, lcap = _line_out(lx, m)
+        out = []
+        for f in range(m):
+            h = hashlib.sha256()
+            for arr, c, cap in ((ok, oc, ocap), (od, oc, ocap), (lk, lc, lcap), (ld, lc, lcap)):
+                h.update(arr[f * cap:f * cap + c[f]].tobytes())
+            out.append(h.hexdigest())
+        return out
+
+    whole = run(frames)
+    shard = run(frames[n // 2:])
+    assert whole[n // 2:] == shard
+    assert len(set(whole)) == n
