@@ -107,6 +107,9 @@ def main():
     ap.add_argument("--width", type=int, default=640,
                     help="frame width (640 = the metric's config; 752 = BASELINE C4's EuRoC-shaped frames)")
     ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--sets", type=int, default=1,
+                    help="frame batches (extractor handle sets) the timed steps alternate between, so consecutive "
+                         "batches overlap on the GPU")
     ap.add_argument("--gather", action="store_true",
                     help="BASELINE C4: all-gather every step's per-frame ORB/line tables over RCCL (timed)")
     args = ap.parse_args()
@@ -125,53 +128,81 @@ def main():
     dev = torch.cuda.current_device()
 
     B, W, H = args.batch, args.width, args.height
-    frames = torch.from_numpy(synth.batch(B, W, H, seed0=pdist.shard_seed(rank))).to(f"cuda:{dev}")
-    orb = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=B, device=dev)
-    orb.kernel_timing(True)  # event pair around every roofline-kernel launch of this process
-    lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=B, device=dev)
-    kp_p, de_p, co_p, mo_p, cap = orb.outputs()
-    kl_p, lde_p, lfn_p, lco_p, lcap = lx.outputs()
-    lib = plvi.load()
     i32 = dict(dtype=torch.int32, device=f"cuda:{dev}")
-    outs = [torch.empty((B - 1) * cap, **i32) for _ in range(4)]
-    lscratch = torch.empty(4 * (B - 1) * 2 * lcap, **i32)
-    lm12 = torch.empty((B - 1) * lcap, **i32)
-    lnm = torch.empty(B - 1, **i32)
-    sA = torch.cuda.Stream()  # non-default: the legacy null stream would serialise
+    lib = plvi.load()
+
+    class FrameSet:
+        """One batch of frames in HBM with its own ORB / line extractor handles,
+        match outputs and stream.  With --sets 2 the timed steps alternate
+        between two sets, so one batch's prep / tail kernels overlap the other
+        batch's region growing (the handles own independent streams)."""
+
+        def __init__(self, k):
+            self.frames = torch.from_numpy(synth.batch(B, W, H, seed0=pdist.shard_seed(rank) + k * B)).to(
+                f"cuda:{dev}")
+            self.orb = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=B, device=dev)
+            self.lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=B, device=dev)
+            self.kp, self.de, self.co, _, self.cap = self.orb.outputs()
+            self.kl, self.lde, _, self.lco, self.lcap = self.lx.outputs()
+            self.outs = [torch.empty((B - 1) * self.cap, **i32) for _ in range(4)]
+            self.lscratch = torch.empty(4 * (B - 1) * 2 * self.lcap, **i32)
+            self.lm12 = torch.empty((B - 1) * self.lcap, **i32)
+            self.lnm = torch.empty(B - 1, **i32)
+            self.s = torch.cuda.Stream()  # non-default: the legacy null stream would serialise
+
+        def match(self):
+            cap, lcap, st = self.cap, self.lcap, self.s.cuda_stream
+            rc = lib.plvi_hamming_knn2_batch(self.de + cap * 32, self.co + 4, cap, self.de, self.co, cap, B - 1,
+                                             *[o.data_ptr() for o in self.outs], st)
+            rc |= lib.plvi_line_match_batch(self.lde + lcap * 32, self.lco + 4, lcap, self.lde, self.lco, lcap,
+                                            B - 1, 0.9, self.lscratch.data_ptr(), self.lm12.data_ptr(),
+                                            self.lnm.data_ptr(), st)
+            if rc:
+                raise RuntimeError(f"match {rc}")
+
+        def extract(self):
+            # Frame::Frame: ORB || lines as one schedule (region growing overlapped
+            # with the ORB pipeline and the LBD Sobel pyramid), then matching
+            plvi.frame_extract_batch(self.orb, self.lx, self.frames.data_ptr(), B, W * H, W, (0, 0),
+                                     stream=self.s.cuda_stream)
+
+    sets = [FrameSet(k) for k in range(max(1, args.sets))]
+    S0 = sets[0]
+    orb, lx, frames, sA = S0.orb, S0.lx, S0.frames, S0.s
+    orb.kernel_timing(True)  # event pair around every roofline-kernel launch of set 0
+    kp_p, de_p, co_p, cap = S0.kp, S0.de, S0.co, S0.cap
+    kl_p, lde_p, lco_p, lcap = S0.kl, S0.lde, S0.lco, S0.lcap
 
     def run_orb():
         orb.extract_batch(frames.data_ptr(), B, W * H, W, (0, 0), stream=sA.cuda_stream)
 
-    def run_match():
-        rc = lib.plvi_hamming_knn2_batch(de_p + cap * 32, co_p + 4, cap, de_p, co_p, cap, B - 1,
-                                         *[o.data_ptr() for o in outs], sA.cuda_stream)
-        rc |= lib.plvi_line_match_batch(lde_p + lcap * 32, lco_p + 4, lcap, lde_p, lco_p, lcap, B - 1, 0.9,
-                                        lscratch.data_ptr(), lm12.data_ptr(), lnm.data_ptr(), sA.cuda_stream)
-        if rc:
-            raise RuntimeError(f"match {rc}")
+    run_match = S0.match
 
-    # C4 (--gather): per-frame tables staged into torch tensors on sA, then one
-    # all_gather per table over RCCL (plvi.dist.gather_tables)
-    tab_src = [(co_p, 4 * B), (kp_p, 28 * cap * B), (de_p, 32 * cap * B), (lco_p, 4 * B), (kl_p, 68 * lcap * B),
-               (lde_p, 32 * lcap * B)]
-    tabs = [torch.empty(n, dtype=torch.uint8, device=f"cuda:{dev}") for _, n in tab_src] if args.gather else []
+    # C4 (--gather): per-frame tables staged into torch tensors on the set's
+    # stream, then one all_gather per table over RCCL (plvi.dist.gather_tables)
+    tabs = ([torch.empty(n, dtype=torch.uint8, device=f"cuda:{dev}")
+             for n in (4 * B, 28 * cap * B, 32 * cap * B, 4 * B, 68 * lcap * B, 32 * lcap * B)]
+            if args.gather else [])
 
-    def run_gather():
-        for (src, n), t in zip(tab_src, tabs):
-            if lib.plvi_memcpy_async(t.data_ptr(), src, n, 3, sA.cuda_stream):
+    def run_gather(fs):
+        srcs = (fs.co, fs.kp, fs.de, fs.lco, fs.kl, fs.lde)
+        for src, t in zip(srcs, tabs):
+            if lib.plvi_memcpy_async(t.data_ptr(), src, t.numel(), 3, fs.s.cuda_stream):
                 raise RuntimeError("gather copy")
-        with torch.cuda.stream(sA):
+        with torch.cuda.stream(fs.s):
             pdist.gather_tables(tabs, world)
 
-    def step():
-        # Frame::Frame: ORB || lines as one schedule (region growing overlapped
-        # with the ORB pipeline and the LBD Sobel pyramid), then matching
-        plvi.frame_extract_batch(orb, lx, frames.data_ptr(), B, W * H, W, (0, 0), stream=sA.cuda_stream)
-        run_match()
-        if args.gather:
-            run_gather()
+    step_no = [0]
 
-    for _ in range(args.warmup):
+    def step():
+        fs = sets[step_no[0] % len(sets)]
+        step_no[0] += 1
+        fs.extract()
+        fs.match()
+        if args.gather:
+            run_gather(fs)
+
+    for _ in range(max(args.warmup, len(sets))):
         step()
     torch.cuda.synchronize()
 
@@ -376,7 +407,7 @@ def main():
                                "(200 lines, scale 0.8, 2 octaves) on two HIP streams, then ORB kNN-2 + "
                                "LineMatcher::match vs previous frame",
                    "batch": B, "width": W, "height": H, "parallelism": f"frames-sharded x{world}",
-                   "gather": bool(args.gather)},
+                   "gather": bool(args.gather), "frame_sets": len(sets)},
         "roofline": roof,
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "dominant_stage": dom,
