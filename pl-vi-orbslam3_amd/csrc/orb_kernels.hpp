@@ -910,7 +910,11 @@ __global__ __launch_bounds__(256) void orb_describe_kernel(const OrbLevelDev* __
         stage_bytes<64>(P, kDescPitch, Bc, (size_t)W, kDescP, kDescP, lane);
         const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
         const float ang = angle * factorPI;
-        const float a = plvi_cosf(ang), b = plvi_sinf(ang);
+        // ang in [0, 2*pi]: the branch-free glibc sincosf (exhaustively equal to
+        // plvi_sinf / plvi_cosf on [0, 120), tests/native/libm_check.cpp); the
+        // general form's large-argument reduction tripled the register count
+        float a, b;
+        plvi_sincosf_pos(ang, &b, &a);
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         uint64_t* out = reinterpret_cast<uint64_t*>(lvdesc + ((size_t)f * kpCapFrame + slot) * 32);
