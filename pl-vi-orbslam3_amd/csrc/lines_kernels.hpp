@@ -320,13 +320,18 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                                                       unsigned* __restrict__ qspill, size_t qspill_frame,
                                                       double prec, LsdRegion* __restrict__ regs, unsigned* __restrict__ regpts,
                                                       size_t regpts_frame, int* __restrict__ nlines,
-                                                      int* __restrict__ err, int R, int QL,
+                                                      int* __restrict__ err, int R, int QL, int nOct,
                                                       unsigned long long* __restrict__ stats) {
     extern __shared__ __align__(16) unsigned lds_u[];
     // latency-bound serial chain: win the SIMD arbiter against co-resident
     // throughput kernels (ORB / LBD on the other stream)
     __builtin_amdgcn_s_setprio(3);
-    const int o = blockIdx.x, f = blockIdx.y, nOct = gridDim.x;
+    // 1-D grid, octave-major: all octave-0 tasks (4x the pixels) first, then
+    // octave 1.  Blocks are dealt round-robin over the 8 XCDs, so every XCD
+    // gets the same mix (a (nOct, nf) grid put every octave-0 task on the
+    // even XCDs) and the heavy tasks are dispatched first.
+    const int nf = gridDim.x / nOct;
+    const int o = blockIdx.x / nf, f = blockIdx.x - o * nf;
     const LineOctDev& od = octs[o];
     const int sw = od.sw, sh = od.sh;
     const int lane = threadIdx.x;

@@ -309,11 +309,11 @@ struct LinePipeline {
                                qspillFrame, nlines.as<int>(), err.as<int>(), growR, growQL, nf, (int)(growSmem / 4));
         } else {
             auto growK = growStats ? lsd_grow_kernel<true> : lsd_grow_kernel<false>;
-            hipLaunchKernelGGL(growK, dim3(nOct, nf), dim3(64), growSmem, st, d_oct.as<LineOctDev>(),
+            hipLaunchKernelGGL(growK, dim3(nOct * nf), dim3(64), growSmem, st, d_oct.as<LineOctDev>(),
                                (const float*)pix.as<float>(), (const double*)modg.as<double>(),
                                (const float4*)seedcs.as<float4>(), gbits.as<unsigned>(), gbitsFrame,
                                qspill.as<unsigned>(), qspillFrame, prec, regs.as<LsdRegion>(), regpts.as<unsigned>(),
-                               qspillFrame, nlines.as<int>(), err.as<int>(), growR, growQL, growStats);
+                               qspillFrame, nlines.as<int>(), err.as<int>(), growR, growQL, nOct, growStats);
         }
         hipLaunchKernelGGL(lsd_rect_kernel, dim3(kRectBlocks, nOct, nf), dim3(256), 0, st, d_oct.as<LineOctDev>(),
                            (const double*)modg.as<double>(), (const LsdRegion*)regs.as<LsdRegion>(),

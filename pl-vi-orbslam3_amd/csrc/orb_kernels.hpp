@@ -607,7 +607,10 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
                                                         int* __restrict__ out_cnt, int nodeCapMax, int L,
                                                         int* __restrict__ err) {
     extern __shared__ __align__(16) unsigned char smem[];
-    const int l = blockIdx.x, f = blockIdx.y, lane = threadIdx.x;
+    // blocks are dealt round-robin over the 8 XCDs: with l = blockIdx.x every
+    // XCD would own one level (level 0, the heaviest, on one XCD); rotating
+    // the level by the frame gives every XCD every level
+    const int f = blockIdx.y, l = (blockIdx.x + f) % L, lane = threadIdx.x;
     const OrbLevelDev& lv = lvs[l];
     const int C = nodeCapMax;
     OctNodes n;
