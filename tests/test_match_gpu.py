@@ -72,3 +72,41 @@ def test_line_match_batch_device(plvi_lib):
             assert cnt[p] == ne and np.array_equal(got[p, :n1[p]], me)
         else:
             assert cnt[p] == 0
+
+
+@pytest.mark.parametrize("nq,nt", [(0, 5), (4, 0), (6, 1)])
+def test_knn2_degenerate_sizes(plvi_lib, nq, nt):
+    # knnMatch with fewer than 2 train rows leaves the missing neighbours at
+    # (-1, INT_MAX) in the oracle's BFMatcher restatement; nq == 0 is a no-op
+    rng = np.random.default_rng(100 + nq * 3 + nt)
+    q = rng.integers(0, 256, size=(nq, 32), dtype=np.uint8)
+    t = rng.integers(0, 256, size=(nt, 32), dtype=np.uint8)
+    got = plvi.hamming_knn2(q, t)
+    exp = ol.knn2(q, t)
+    for g, e, name in zip(got, exp, ["idx0", "d0", "idx1", "d1"]):
+        assert g.shape == (nq,) and np.array_equal(g, e), name
+
+
+def test_knn2_all_equal_targets_and_max_distance(plvi_lib):
+    # every train row identical: all distances tie, first two indices win;
+    # query = bitwise complement of the train rows: distance 256 everywhere
+    rng = np.random.default_rng(77)
+    row = rng.integers(0, 256, size=32, dtype=np.uint8)
+    t = np.tile(row, (300, 1))
+    q = np.stack([row, ~row, row ^ 1])  # row ^ 1 flips one bit per byte
+    got = plvi.hamming_knn2(q, t)
+    exp = ol.knn2(q, t)
+    for g, e in zip(got, exp):
+        assert np.array_equal(g, e)
+    assert list(got[0]) == [0, 0, 0] and list(got[2]) == [1, 1, 1]
+    assert list(got[1]) == [0, 256, 32] and list(got[3]) == [0, 256, 32]
+
+
+def test_line_match_nnr_rejects_single_train_row(plvi_lib):
+    # LineMatcher::matchNNR reads matches_[idx][1] (LineMatcher.cpp:41-61),
+    # undefined with one train row: the C-ABI refuses instead of guessing
+    rng = np.random.default_rng(3)
+    q = rng.integers(0, 256, size=(4, 32), dtype=np.uint8)
+    t = rng.integers(0, 256, size=(1, 32), dtype=np.uint8)
+    with pytest.raises(plvi.PlviError):
+        plvi.LineMatcher.matchNNR(q, t, 0.9)
