@@ -8,7 +8,7 @@ import pytest
 import oracle_lib as ol
 import plvi
 from plvi import synth
-from util import real_frames
+from util import real_frames, structured_frames
 
 pytestmark = pytest.mark.gpu
 
@@ -108,3 +108,9 @@ def test_lines_two_frames_per_wave_variant(plvi_lib, monkeypatch):
         _assert_same((kl[s], de[s], fn[s]), ol.line_extract(frames[f]), f"pack2 batch{f}")
     img = real_frames()["rgb1_gray"]
     _assert_same(lx(img), ol.line_extract(img), "pack2 rgb1_gray")
+
+
+@pytest.mark.parametrize("name", ["step", "checker", "stripes", "binary_noise"])
+def test_lines_structured_extremes(lx640, name):
+    img = structured_frames()[name]
+    _assert_same(lx640(img), ol.line_extract(img), name)

@@ -9,7 +9,7 @@ import pytest
 import oracle_lib as ol
 import plvi
 from plvi import synth
-from util import real_frames
+from util import real_frames, structured_frames
 
 pytestmark = pytest.mark.gpu
 
@@ -103,3 +103,9 @@ def test_orb_batch_equals_single(orb640):
         exp = ol.orb_extract(frames[f])
         got = (int(mono[f]), kps[f * cap:f * cap + cnt[f]], desc[f * cap:f * cap + cnt[f]])
         _assert_same(got, exp, f"batch{f}")
+
+
+@pytest.mark.parametrize("name", ["step", "checker", "stripes", "binary_noise"])
+def test_orb_structured_extremes(orb640, name):
+    img = structured_frames()[name]
+    _assert_same(orb640(img), ol.orb_extract(img), name)

@@ -182,3 +182,18 @@ def proj_params(case, th, forward=0, backward=0):
     for i, s in enumerate(case["scale_factors"]):
         p.scale_factors[i] = s
     return p
+
+
+def structured_frames(w=640, h=480):
+    """Extreme-contrast 640x480 cases: a 0/255 vertical step, a 0/255
+    checkerboard of 40-pixel squares, 3-pixel diagonal stripes and binary
+    (0/255) noise -- gradients at the u8 maximum, lines running into the
+    image border, and FAST / region-growing thresholds met almost everywhere."""
+    yy, xx = np.mgrid[0:h, 0:w]
+    out = {}
+    out["step"] = np.where(xx < w // 2 + 3, 0, 255).astype(np.uint8)
+    out["checker"] = np.where(((xx // 40) + (yy // 40)) % 2 == 0, 0, 255).astype(np.uint8)
+    out["stripes"] = np.where(((xx + yy) // 3) % 2 == 0, 30, 220).astype(np.uint8)
+    rng = np.random.default_rng(11)
+    out["binary_noise"] = (rng.integers(0, 2, size=(h, w)) * 255).astype(np.uint8)
+    return out
