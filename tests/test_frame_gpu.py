@@ -83,3 +83,32 @@ def test_sharded_frames_match_whole_batch_digests():
     shard = run(frames[n // 2:])
     assert whole[n // 2:] == shard
     assert len(set(whole)) == n
+
+
+def test_frame_schedule_mixed_batch_vs_oracle():
+    """One frame-schedule launch over a ragged-content batch (extreme-contrast,
+    flat and textured frames side by side: 0 to 1000 keypoints, 0 to 200
+    lines per frame); every frame's ORB and line output equals the oracle's."""
+    from util import structured_frames
+    st = structured_frames()
+    frames = np.stack([st["checker"], np.full((480, 640), 90, np.uint8), st["binary_noise"],
+                       synth.frame(31), st["step"], st["stripes"]])
+    n = frames.shape[0]
+    buf = plvi.DeviceBuffer(frames.nbytes)
+    buf.upload(frames)
+    orb = plvi.ORBextractor(1000, 1.2, 8, 20, 7, 640, 480, max_batch=n)
+    lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 640, 480, max_batch=n)
+    plvi.frame_extract_batch(orb, lx, buf.ptr, n, 640 * 480, 640)
+    plvi.load().plvi_device_synchronize()
+    ocnt, okp, odesc, ocap = _orb_out(orb, n)
+    lcnt, lkl, ldesc, lcap = _line_out(lx, n)
+    for i in range(n):
+        _, ekp, edesc = ol.orb_extract(frames[i])
+        assert ocnt[i] == len(ekp), f"frame {i}: {ocnt[i]} keypoints vs {len(ekp)}"
+        got = okp[i * ocap:i * ocap + ocnt[i]]
+        assert got.tobytes() == ekp.astype(plvi.KEYPOINT_DTYPE).tobytes(), f"frame {i} keypoints"
+        np.testing.assert_array_equal(odesc[i * ocap:i * ocap + ocnt[i]], edesc)
+        ekl, eld, _ = ol.line_extract(frames[i])
+        assert lcnt[i] == len(ekl), f"frame {i}: {lcnt[i]} lines vs {len(ekl)}"
+        assert lkl[i * lcap:i * lcap + lcnt[i]].tobytes() == ekl.astype(plvi.KEYLINE_DTYPE).tobytes(), f"frame {i} lines"
+        np.testing.assert_array_equal(ldesc[i * lcap:i * lcap + lcnt[i]], eld)
