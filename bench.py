@@ -1,7 +1,7 @@
 """bench.py — throughput of the MI355X feature front end (BASELINE.json metric).
 
-A step = one pass of the hot path over one batch of B synthetic 640x480
-frames already resident in HBM (default B=1536 frames in flight per GPU):
+A step = one pass of the hot path over one batch of B synthetic frames
+already resident in HBM (default B = 3072 frames in flight per GPU):
   ORB extract (ORBextractor 1000/1.2/8/20/7) and LSD + LBD line extract
   (Lineextractor 200/0/0.8/2/2.0) as one schedule (plvi_frame_extract_batch:
   region growing concurrent with the ORB pipeline and the LBD Sobel pyramid),
@@ -10,18 +10,33 @@ frames already resident in HBM (default B=1536 frames in flight per GPU):
   ratio 0.9, mutual check).
 value = frames processed by all ranks / max-over-ranks wall time.
 
-Multi-GPU: one process per GPU (torchrun); each rank owns its own sequence of
-frames (seeded by rank) — no data-path collective (the
-per-frame tables are gathered only for reporting), scaling "weak".
+Launch: `python bench.py --gpus N` with N > 1 starts N ranks itself (a
+torch.distributed.run child, before anything touches the GPU) unless it is
+already running under torchrun, in which case WORLD_SIZE must equal N.  One
+process per GPU; each rank owns its own synthetic sequence (seeds
+rank*10^6 + t) -- no data-path collective, scaling "weak".
+--c4: BASELINE config C4 -- 752x480 EuRoC-shaped frames, each rank walks its
+own sequence in consecutive overlapping windows (one-frame halo, so every
+consecutive pair is matched once), and every step's per-frame tables are
+gathered to rank 0 over RCCL (on by default for world > 1).
 
-Also reported: roofline of the dominant kernel stage (HIP events on the
-launch stream), and the CPU oracle timed on a bounded sample (rank 0, N=1).
+Outside the timed region: the device error flags of every batch are checked
+(any overflow fails the run), frames 0, B/2 and B-1 of the timed batch (and
+their matches) are compared bit-exactly with the CPU oracle, and on rank 0
+at N=1 the oracle is timed as the CPU baseline.  Also reported:
+the rooflines of the two HBM passes (orb_blur_fast_kernel, lsd_prep_kernel;
+HIP events on the launch streams) and the end-to-end HBM fraction, a
+batch-64 line (C1/C2), the single-frame latency of the drop-in entry points
+run as Frame runs them, and an overlapped pinned-H2D variant of the step.
 """
 import argparse
 import ctypes
+import hashlib
 import json
 import os
 import pathlib
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,6 +48,8 @@ sys.path.insert(0, str(ROOT / "tests"))
 
 METRIC = "frames/sec ORB+LSD extract+match, 640×480 mono, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+E2E_BYTES_640 = 15_972_194  # reference-materialisation bytes per 640x480 frame
+E2E_BYTES_752 = 18_775_975
 
 
 def level_dims(w, h, nlevels=8, sf=1.2):
@@ -54,373 +71,767 @@ def blur_fast_bytes(w, h):
     return sum(planes) + 2 * sum(planes) + planes[0]
 
 
-def committed_traffic(batch):
-    """HBM bytes per launch of the roofline kernel from the committed PMC
-    passes (profiles/*/pmc_traffic.json, tools/pmc_traffic.py), when they were
-    taken at this batch size; else None."""
+def lsd_prep_bytes(w, h, scale=0.8, noct=2):
+    """Algorithmic bytes/frame of lsd_prep_kernel (one launch per octave):
+    the octave's u8 image in, the scaled image's f32 angle + f64 modgrad out
+    (the seed-direction float4, written for defined pixels only, is not
+    counted: a lower bound on the kernel's compulsory traffic)."""
+    tot = 0
+    for o in range(noct):
+        ow, oh = w >> o, h >> o
+        sw, sh = int(np.rint(ow * scale)), int(np.rint(oh * scale))
+        tot += ow * oh + 12 * sw * sh
+    return tot
+
+
+def committed_traffic(batch, kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC passes
+    (profiles/*/pmc_traffic*.json, tools/pmc_traffic.py), taken at this batch
+    size; else None."""
     best = None
-    for f in sorted(ROOT.glob("profiles/*/pmc_traffic.json")):
+    for f in sorted(ROOT.glob("profiles/*/pmc_traffic*.json")):
         try:
             d = json.loads(f.read_text())
         except ValueError:
             continue
-        if d.get("batch") == batch and d.get("kernel") == "orb_blur_fast_kernel":
-            best = d
+        for e in d if isinstance(d, list) else [d]:
+            if e.get("batch") == batch and e.get("kernel") == kernel:
+                best = e
     return None if best is None else best["bytes_per_launch"]
 
 
-def cpu_baseline(budget_s=15.0):
-    import oracle_lib
-    from plvi import synth
-    frames = [synth.frame(10_000 + i) for i in range(16)]
-    n = 0
-    prev = None
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` outside torchrun: start the N ranks as a
+    torch.distributed.run child (nothing in this process has touched the
+    GPU) and exit with its status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", str(pathlib.Path(__file__).resolve())]
+    cmd += sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+# ------------------------------------------------------------------ oracle leg
+# The only part of bench.py that loads the CPU oracle (oracle/, test
+# infrastructure): as the checker of the timed batch and as the timed CPU
+# baseline (SURVEY 8(d)).  Never on the measured GPU path.
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def oracle_verify(checks):
+    """Bit-exact comparison of downloaded GPU outputs with the oracle.
+    checks: list of (kind, inputs, gpu_outputs).  Returns a list of failures."""
+    import oracle_lib as ol
+    bad = []
+    for kind, inp, got in checks:
+        if kind == "orb":
+            m, k, d = ol.orb_extract(inp)
+            ok = got[0] == m and got[1].tobytes() == k.tobytes() and np.array_equal(got[2], d)
+        elif kind == "lines":
+            k, d, f = ol.line_extract(inp)
+            ok = got[0].tobytes() == k.tobytes() and np.array_equal(got[1], d) and got[2].tobytes() == f.tobytes()
+        elif kind == "knn2":
+            e = ol.knn2(*inp)
+            ok = all(np.array_equal(g, x) for g, x in zip(got, e))
+        elif kind == "lmatch":
+            n, m = ol.match(inp[0], inp[1], 0.9)
+            ok = got[0] == n and np.array_equal(got[1], m)
+        else:
+            ok = False
+        if not ok:
+            bad.append(kind)
+    return bad
+
+
+def cpu_baseline(frames, runs=5, par_s=5.0):
+    """the oracle (built -O3 -march=x86-64-v3 -ffp-contract=off)
+    single-threaded and pinned to one core, per stage and end to end, median
+    of `runs` passes over the same frames; plus frame-parallel throughput on
+    the host cores this process may use (oracle calls release the GIL)."""
+    import threading
+    import oracle_lib as ol
+    ol.load()
+    cpus = sorted(os.sched_getaffinity(0))
+    stages = ("orb_extract", "line_extract", "orb_knn2", "line_match")
+    per = {k: [] for k in stages}
+    tot = []
+    os.sched_setaffinity(0, {cpus[0]})
+    try:
+        for _ in range(runs):
+            acc = dict.fromkeys(stages, 0.0)
+            prev = None
+            t_run = time.perf_counter()
+            for img in frames:
+                t0 = time.perf_counter()
+                _, _, d = ol.orb_extract(img)
+                t1 = time.perf_counter()
+                _, ld, _ = ol.line_extract(img)
+                t2 = time.perf_counter()
+                if prev is not None:
+                    ol.knn2(d, prev[0])
+                    t3 = time.perf_counter()
+                    if len(ld) >= 2 and len(prev[1]) >= 2:
+                        ol.match(ld, prev[1], 0.9)
+                    t4 = time.perf_counter()
+                    acc["orb_knn2"] += t3 - t2
+                    acc["line_match"] += t4 - t3
+                acc["orb_extract"] += t1 - t0
+                acc["line_extract"] += t2 - t1
+                prev = (d, ld)
+            tot.append(time.perf_counter() - t_run)
+            for k in stages:
+                per[k].append(acc[k] * 1e3 / len(frames))
+    finally:
+        os.sched_setaffinity(0, set(cpus))
+    med = float(np.median(tot))
+    nthr = min(16, len(cpus))  # the GPU box's CPU share per GPU is 16
+    count = [0] * nthr
+    stop = time.perf_counter() + par_s
+
+    def worker(i):
+        prev = None
+        j = i
+        while time.perf_counter() < stop:
+            img = frames[j % len(frames)]
+            _, _, d = ol.orb_extract(img)
+            _, ld, _ = ol.line_extract(img)
+            if prev is not None:
+                ol.knn2(d, prev[0])
+                if len(ld) >= 2 and len(prev[1]) >= 2:
+                    ol.match(ld, prev[1], 0.9)
+            prev = (d, ld)
+            count[i] += 1
+            j += nthr
     t0 = time.perf_counter()
-    while True:
-        img = frames[n % len(frames)]
-        _, k, d = oracle_lib.orb_extract(img)
-        kl, ld, fn = oracle_lib.line_extract(img)
-        if prev is not None:
-            oracle_lib.knn2(d, prev[0])
-            if len(ld) >= 2 and len(prev[1]) >= 2:
-                oracle_lib.match(ld, prev[1], 0.9)
-        prev = (d, ld)
-        n += 1
-        if time.perf_counter() - t0 > budget_s and n >= 3:
-            break
-    el = time.perf_counter() - t0
-    return {"value": n / el, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{n} synthetic 640x480 frames: ORB extract + LSD/LBD extract + ORB kNN-2 + LineMatcher::match "
-                      f"vs previous frame, single-thread CPU restatement (oracle/), {el:.1f}s"}
+    ths = [threading.Thread(target=worker, args=(i,)) for i in range(nthr)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    par_fps = sum(count) / (time.perf_counter() - t0)
+    return {"value": len(frames) / med, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{len(frames)} frames of the timed batch, median of {runs} single-thread runs pinned to core "
+                      f"{cpus[0]} (sched_setaffinity): ORB extract + LSD/LBD extract + ORB kNN-2 + "
+                      f"LineMatcher::match vs previous frame, CPU restatement (oracle/, -O3 -march=x86-64-v3)",
+            "stage_ms_per_frame": {k: round(float(np.median(v)), 3) for k, v in per.items()},
+            "parallel": {"threads": nthr, "value": round(par_fps, 2), "unit": "frames/s",
+                         "sample": f"{sum(count)} frames in {par_s:.0f}s, frame-parallel threads"},
+            "host_cpu": _cpu_model(), "host_nproc": os.cpu_count(), "affinity_cpus": len(cpus)}
 
 
+# ------------------------------------------------------------------ dry run
+def dry_run(args, world, rank):
+    """--dry-run: the launcher and the reductions without the GPU (gloo):
+    each rank builds its own sequence on the CPU, "processes" it with a
+    numpy checksum per frame, and the run reports the max-over-ranks time,
+    the whole-job frame count and every rank's first-batch digest."""
+    import torch
+    from plvi import dist as pdist
+    from plvi import synth
+    if world > 1:
+        pdist.init("gloo")
+    W, H = (752, 480) if args.c4 else (args.width, args.height)
+    B = args.batch
+    nwin = max(1, (2000 - 1) // (B - 1)) if args.c4 else 1
+    seq = synth.device_sequence(B + (nwin - 1) * (B - 1), W, H, seed=pdist.shard_seed(rank))
+    digest = hashlib.sha256(seq[:B].numpy().tobytes()).hexdigest()[:16]
+    pdist.barrier(world)
+    t0 = time.perf_counter()
+    sums = 0
+    for k in range(args.steps):
+        lo = (k % nwin) * (B - 1)
+        sums += int(seq[lo:lo + B].to(torch.int64).sum())
+    el = pdist.max_over_ranks(time.perf_counter() - t0, world)
+    new = (B - 1) if args.c4 else B
+    total = pdist.sum_over_ranks(new * args.steps, world)
+    digests = [digest]
+    if world > 1:
+        import torch.distributed as dist
+        digests = [None] * world
+        dist.all_gather_object(digests, digest)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": world, "steps": args.steps,
+                          "frames_total": total, "max_rank_s": el, "rank_digests": digests,
+                          "config": {"batch": B, "width": W, "height": H, "c4": bool(args.c4)}}), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    return 0
+
+
+# ------------------------------------------------------------------ main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=3072)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-bow", action="store_true", help="skip the DBoW2 transform stage timing")
-    ap.add_argument("--no-proj", action="store_true", help="skip the SearchByProjection stage timing")
-    ap.add_argument("--no-stereo", action="store_true", help="skip the rectified-stereo stage timing")
-    ap.add_argument("--width", type=int, default=640,
-                    help="frame width (640 = the metric's config; 752 = BASELINE C4's EuRoC-shaped frames)")
+    ap.add_argument("--batch", type=int, default=None, help="frames per step (default 3072; C4: 1000)")
+    ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
-    ap.add_argument("--sets", type=int, default=1,
-                    help="frame batches (extractor handle sets) the timed steps alternate between, so consecutive "
-                         "batches overlap on the GPU")
-    ap.add_argument("--gather", action="store_true",
-                    help="BASELINE C4: all-gather every step's per-frame ORB/line tables over RCCL (timed)")
+    ap.add_argument("--c4", action="store_true", help="BASELINE C4: 752x480 sequences, RCCL gather to rank 0")
+    ap.add_argument("--gather", dest="gather", action="store_true", default=None,
+                    help="gather every step's per-frame tables to rank 0 over RCCL (timed; default: on for --c4 "
+                         "with world > 1)")
+    ap.add_argument("--no-gather", dest="gather", action="store_false")
+    ap.add_argument("--dry-run", action="store_true", help="launcher + reductions on CPU (gloo), no GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=32, help="frames of the CPU-baseline sample (SURVEY: 64)")
+    ap.add_argument("--no-check", action="store_true", help="skip the oracle check of the timed batch")
+    ap.add_argument("--no-extra", action="store_true", help="skip the batch-64 / latency / H2D lines")
+    ap.add_argument("--no-side", action="store_true", help="skip the BoW / projection / stereo stage timings")
     args = ap.parse_args()
 
+    world_env = int(os.environ.get("WORLD_SIZE", "0"))
+    if world_env == 0 and args.gpus > 1:
+        return spawn_ranks(args.gpus)
+    world = max(world_env, 1)
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
+    if args.batch is None:
+        args.batch = 1000 if args.c4 else 3072
+    if args.batch < 2:
+        print("bench.py: --batch must be >= 2 (frames are matched against their predecessor)", file=sys.stderr)
+        return 2
+    rank = int(os.environ.get("RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank)
+    if args.c4:
+        args.width, args.height = 752, 480
+    if args.gather is None:
+        args.gather = bool(args.c4 and world > 1)
+    return run(args, world, rank)
+
+
+def run(args, world, rank):
     import torch
     import plvi
     from plvi import dist as pdist
     from plvi import synth
 
-    world, rank, local = pdist.env()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
     if world > 1:
-        torch.cuda.set_device(local)
         pdist.init("nccl", torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
-
+    cuda = f"cuda:{dev}"
     B, W, H = args.batch, args.width, args.height
-    i32 = dict(dtype=torch.int32, device=f"cuda:{dev}")
+    i32 = dict(dtype=torch.int32, device=cuda)
     lib = plvi.load()
+    seed0 = pdist.shard_seed(rank)
 
-    class FrameSet:
-        """One batch of frames in HBM with its own ORB / line extractor handles,
-        match outputs and stream.  With --sets 2 the timed steps alternate
-        between two sets, so one batch's prep / tail kernels overlap the other
-        batch's region growing (the handles own independent streams)."""
+    # frames: C4 = one sequence per rank walked in windows [k(B-1), k(B-1)+B)
+    # (one-frame halo); default = one resident batch re-processed each step
+    # (SURVEY 8d C4: sequences of ~2000 frames; windows wrap to the start)
+    nwin = max(1, (2000 - 1) // (B - 1)) if args.c4 else 1
+    seq = synth.device_sequence(B + (nwin - 1) * (B - 1), W, H, seed=seed0, device=cuda)
+    torch.cuda.synchronize()
+    first_digest = hashlib.sha256(seq[:B].cpu().numpy().tobytes()).hexdigest()[:16]
 
-        def __init__(self, k):
-            self.frames = torch.from_numpy(synth.batch(B, W, H, seed0=pdist.shard_seed(rank) + k * B)).to(
-                f"cuda:{dev}")
-            self.orb = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=B, device=dev)
-            self.lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=B, device=dev)
-            self.kp, self.de, self.co, _, self.cap = self.orb.outputs()
-            self.kl, self.lde, _, self.lco, self.lcap = self.lx.outputs()
-            self.outs = [torch.empty((B - 1) * self.cap, **i32) for _ in range(4)]
-            self.lscratch = torch.empty(4 * (B - 1) * 2 * self.lcap, **i32)
-            self.lm12 = torch.empty((B - 1) * self.lcap, **i32)
-            self.lnm = torch.empty(B - 1, **i32)
-            self.s = torch.cuda.Stream()  # non-default: the legacy null stream would serialise
+    orb = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=B, device=dev)
+    lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=B, device=dev)
+    kp_p, de_p, co_p, _, cap = orb.outputs()
+    kl_p, lde_p, _, lco_p, lcap = lx.outputs()
+    outs = [torch.empty((B - 1) * cap, **i32) for _ in range(4)]
+    lscratch = torch.empty(4 * (B - 1) * 2 * lcap, **i32)
+    lm12 = torch.empty((B - 1) * lcap, **i32)
+    lnm = torch.empty(B - 1, **i32)
+    stream = torch.cuda.Stream()  # non-default: the legacy null stream would serialise
+    st = stream.cuda_stream
+    orb.kernel_timing(True)  # event pair around every blur+FAST launch
+    lx.kernel_timing(True)   # and every lsd_prep launch
 
-        def match(self):
-            cap, lcap, st = self.cap, self.lcap, self.s.cuda_stream
-            rc = lib.plvi_hamming_knn2_batch(self.de + cap * 32, self.co + 4, cap, self.de, self.co, cap, B - 1,
-                                             *[o.data_ptr() for o in self.outs], st)
-            rc |= lib.plvi_line_match_batch(self.lde + lcap * 32, self.lco + 4, lcap, self.lde, self.lco, lcap,
-                                            B - 1, 0.9, self.lscratch.data_ptr(), self.lm12.data_ptr(),
-                                            self.lnm.data_ptr(), st)
-            if rc:
-                raise RuntimeError(f"match {rc}")
+    def extract(fptr, n=B):
+        plvi.frame_extract_batch(orb, lx, fptr, n, W * H, W, (0, 0), stream=st)
 
-        def extract(self):
-            # Frame::Frame: ORB || lines as one schedule (region growing overlapped
-            # with the ORB pipeline and the LBD Sobel pyramid), then matching
-            plvi.frame_extract_batch(self.orb, self.lx, self.frames.data_ptr(), B, W * H, W, (0, 0),
-                                     stream=self.s.cuda_stream)
+    def match(n=B):
+        rc = lib.plvi_hamming_knn2_batch(de_p + cap * 32, co_p + 4, cap, de_p, co_p, cap, n - 1,
+                                         *[o.data_ptr() for o in outs], st)
+        rc |= lib.plvi_line_match_batch(lde_p + lcap * 32, lco_p + 4, lcap, lde_p, lco_p, lcap, n - 1, 0.9,
+                                        lscratch.data_ptr(), lm12.data_ptr(), lnm.data_ptr(), st)
+        if rc:
+            raise RuntimeError(f"match {rc}")
 
-    sets = [FrameSet(k) for k in range(max(1, args.sets))]
-    S0 = sets[0]
-    orb, lx, frames, sA = S0.orb, S0.lx, S0.frames, S0.s
-    orb.kernel_timing(True)  # event pair around every roofline-kernel launch of set 0
-    kp_p, de_p, co_p, cap = S0.kp, S0.de, S0.co, S0.cap
-    kl_p, lde_p, lco_p, lcap = S0.kl, S0.lde, S0.lco, S0.lcap
+    # C4 gather: tables staged on the step's stream, then one RCCL gather per
+    # table to rank 0, asynchronous (waited on before the staging is reused)
+    tab_sizes = (4 * B, 28 * cap * B, 32 * cap * B, 4 * B, 68 * lcap * B, 32 * lcap * B)
+    stage_bufs = [torch.empty(n, dtype=torch.uint8, device=cuda) for n in tab_sizes] if args.gather else []
+    recv = ([[torch.empty(n, dtype=torch.uint8, device=cuda) for _ in range(world)] for n in tab_sizes]
+            if args.gather and rank == 0 else None)
+    pending = []
 
-    def run_orb():
-        orb.extract_batch(frames.data_ptr(), B, W * H, W, (0, 0), stream=sA.cuda_stream)
-
-    run_match = S0.match
-
-    # C4 (--gather): per-frame tables staged into torch tensors on the set's
-    # stream, then one all_gather per table over RCCL (plvi.dist.gather_tables)
-    tabs = ([torch.empty(n, dtype=torch.uint8, device=f"cuda:{dev}")
-             for n in (4 * B, 28 * cap * B, 32 * cap * B, 4 * B, 68 * lcap * B, 32 * lcap * B)]
-            if args.gather else [])
-
-    def run_gather(fs):
-        srcs = (fs.co, fs.kp, fs.de, fs.lco, fs.kl, fs.lde)
-        for src, t in zip(srcs, tabs):
-            if lib.plvi_memcpy_async(t.data_ptr(), src, t.numel(), 3, fs.s.cuda_stream):
+    def gather():
+        import torch.distributed as dist
+        for w_ in pending:
+            w_.wait()
+        pending.clear()
+        for src, t in zip((co_p, kp_p, de_p, lco_p, kl_p, lde_p), stage_bufs):
+            if lib.plvi_memcpy_async(t.data_ptr(), src, t.numel(), 3, st):
                 raise RuntimeError("gather copy")
-        with torch.cuda.stream(fs.s):
-            pdist.gather_tables(tabs, world)
+        with torch.cuda.stream(stream):
+            for i, t in enumerate(stage_bufs):
+                if world == 1:
+                    continue
+                pending.append(dist.gather(t, recv[i] if rank == 0 else None, dst=0, async_op=True))
 
     step_no = [0]
 
     def step():
-        fs = sets[step_no[0] % len(sets)]
+        k = step_no[0]
         step_no[0] += 1
-        fs.extract()
-        fs.match()
+        lo = (k % nwin) * (B - 1)
+        extract(seq[lo].data_ptr())
+        match()
         if args.gather:
-            run_gather(fs)
+            gather()
 
-    for _ in range(max(args.warmup, len(sets))):
+    for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    if args.gather and rank == 0 and world > 1:
+        for w_ in pending:
+            w_.wait()
+        torch.cuda.synchronize()
+    # error flags of the warm-up batches
+    err_warm = (orb.errors(st), lx.errors(st))
 
-    # stage timing run (separate from the timed region: events add markers).
-    # Each extractor runs alone here so its stage times are uncontended.
+    # stage timing (separate from the timed region: events add markers); each
+    # extractor alone so its stage times are uncontended
+    f0 = seq.data_ptr()
     orb.profile(True)
     lx.profile(True)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     match_ms = 0.0
     nprof = max(3, min(args.steps, 10))
     for _ in range(nprof):
-        run_orb()
+        orb.extract_batch(f0, B, W * H, W, (0, 0), stream=st)
         torch.cuda.synchronize()
-        lx.extract_batch(frames.data_ptr(), B, W * H, W, stream=sA.cuda_stream)
+        lx.extract_batch(f0, B, W * H, W, stream=st)
         torch.cuda.synchronize()
-        ev0.record(sA)
-        run_match()
-        ev1.record(sA)
+        ev0.record(stream)
+        match()
+        ev1.record(stream)
         torch.cuda.synchronize()
         match_ms += ev0.elapsed_time(ev1)
     st_orb, runs = orb.profile_read()
     st_lines, lruns = lx.profile_read()
     orb.profile(False)
     lx.profile(False)
-    # SURVEY §8d: ORB-only, LSD+LBD-only and match-only throughput, each part
-    # alone on the chip (no stage events), nprof back-to-back batches
+
     def part_fps(fn):
         fn()
         torch.cuda.synchronize()
-        ev0.record(sA)
+        ev0.record(stream)
         for _ in range(nprof):
             fn()
-        ev1.record(sA)
+        ev1.record(stream)
         torch.cuda.synchronize()
         return B * nprof / (ev0.elapsed_time(ev1) * 1e-3)
-    parts = {"orb_only": part_fps(run_orb),
-             "lines_only": part_fps(lambda: lx.extract_batch(frames.data_ptr(), B, W * H, W, stream=sA.cuda_stream)),
-             "match_only": part_fps(run_match)}
-    # DBoW2 transform (Frame::ComputeBoW, SURVEY §8f rank 1) of the batch's ORB
-    # descriptors on a k=10, L=6 synthetic vocabulary (ORBvoc.txt's shape);
-    # timed separately: the reference runs it for keyframes / relocalisation,
-    # not inside the per-frame extract+match step.
-    bow_ms = None
-    if not args.no_bow:
-        pv = synth.vocabulary(10, 6, seed=1)
-        voc = plvi.ORBVocabulary.from_nodes(10, 6, 0, 0, *pv, device=dev)
-        bo = {k: torch.empty(B * (cap + 1) * sz, dtype=torch.uint8, device=f"cuda:{dev}")
-              for k, sz in (("bw", 4), ("bv", 8), ("bn", 4), ("fn", 4), ("fo", 4), ("fi", 4), ("fc", 4))}
-
-        def run_bow():
-            rc = lib.plvi_vocab_transform_batch(voc._h, de_p, co_p, cap, B, 4, *[bo[k].data_ptr() for k in
-                                                ("bw", "bv", "bn", "fn", "fo", "fi", "fc")], None, None,
-                                                sA.cuda_stream)
-            if rc:
-                raise RuntimeError(f"bow {rc}")
-        run_orb()
-        run_bow()
-        torch.cuda.synchronize()
-        ev0.record(sA)
-        for _ in range(nprof):
-            run_bow()
-        ev1.record(sA)
-        torch.cuda.synchronize()
-        bow_ms = ev0.elapsed_time(ev1) / nprof
-    # SearchByProjection (Tracking::TrackWithMotionModel, SURVEY §8f rank 2):
-    # AssignFeaturesToGrid of the batch, then frame t vs frame t-1's keypoints
-    # as MapPoints (identity motion, depth 5, their own descriptors), th = 15
-    proj_ms = None
-    if not args.no_proj:
-        gp = plvi.GridParams(0.0, 0.0, *[float(x) for x in plvi.grid_geometry(W, H)[4:]])
-        cell_off = torch.empty(B * 3073, dtype=torch.int32, device=f"cuda:{dev}")
-        cell_idx = torch.empty(B * cap, dtype=torch.int32, device=f"cuda:{dev}")
-        kpt = torch.empty(B * cap * 7, dtype=torch.float32, device=f"cuda:{dev}")
-        lib.plvi_memcpy_async(kpt.data_ptr(), kp_p, B * cap * 28, 3, sA.cuda_stream)
-        torch.cuda.synchronize()
-        kv = kpt.view(B, cap, 7)
-        fx, fy, cx, cy, z = 458.654, 457.296, 367.215, 248.375, 5.0
-        x3 = torch.stack([(kv[..., 0] - cx) * z / fx, (kv[..., 1] - cy) * z / fy,
-                          torch.full_like(kv[..., 0], z)], -1).contiguous()
-        loct = kv[..., 5].view(torch.int32).contiguous()
-        lang = kv[..., 3].contiguous()
-        lflags = torch.full((B * cap,), 3, dtype=torch.uint8, device=f"cuda:{dev}")
-        pp = plvi.ProjParams()
-        pp.fx, pp.fy, pp.cx, pp.cy, pp.mbf, pp.th = fx, fy, cx, cy, 40.0, 15.0
-        geo = plvi.grid_geometry(W, H)
-        pp.min_x, pp.max_x, pp.min_y, pp.max_y, pp.inv_w, pp.inv_h = [float(x) for x in geo]
-        pp.check_orientation, pp.nlevels = 1, 8
-        for i, sfac in enumerate(orb.GetScaleFactors()):
-            pp.scale_factors[i] = float(sfac)
-        pm = torch.empty((B - 1) * cap, dtype=torch.int32, device=f"cuda:{dev}")
-        pn = torch.empty(B, dtype=torch.int32, device=f"cuda:{dev}")
-
-        def run_proj():
-            plvi.assign_grid_batch(kp_p, co_p, cap, B, gp, cell_off.data_ptr(), cell_idx.data_ptr(), sA.cuda_stream)
-            rc = lib.plvi_search_by_projection_batch(
-                B - 1, ctypes.byref(pp), kp_p + 28 * cap, de_p + 32 * cap, co_p + 4, cap, None, None,
-                cell_off.data_ptr() + 4 * 3073, cell_idx.data_ptr() + 4 * cap, x3.data_ptr(), loct.data_ptr(),
-                lang.data_ptr(), de_p, lflags.data_ptr(), co_p, cap, pm.data_ptr(), pn.data_ptr(), sA.cuda_stream)
-            if rc:
-                raise RuntimeError(f"projection {rc}")
-        run_proj()
-        torch.cuda.synchronize()
-        ev0.record(sA)
-        for _ in range(nprof):
-            run_proj()
-        ev1.record(sA)
-        torch.cuda.synchronize()
-        proj_ms = ev0.elapsed_time(ev1) / nprof
-    # Stereo (Frame::ComputeStereoMatches / ComputeStereoMatches_Lines, SURVEY
-    # §8f rank 4) on S synthetic rectified pairs extracted by a second set of
-    # handles (left = own, right = the pair's other image); timed per S pairs
-    stereo_ms = None
-    if not args.no_stereo:
-        S = min(B, 256)
-        pairs = [synth.stereo_pair(pdist.shard_seed(rank) + 10 ** 5 + i, W, H) for i in range(S)]
-        sl = torch.from_numpy(np.stack([p[0] for p in pairs])).to(f"cuda:{dev}")
-        sr = torch.from_numpy(np.stack([p[1] for p in pairs])).to(f"cuda:{dev}")
-        o_l = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=S, device=dev)
-        o_r = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=S, device=dev)
-        l_l = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=S, device=dev)
-        l_r = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=S, device=dev)
-        for e, fr in ((o_l, sl), (o_r, sr), (l_l, sl), (l_r, sr)):
-            e.extract_batch(fr.data_ptr(), S, W * H, W, stream=sA.cuda_stream)
-        torch.cuda.synchronize()
-        scap = o_l.kp_cap
-        st_f = torch.empty(2 * S * scap, dtype=torch.float32, device=f"cuda:{dev}")
-        st_i = torch.zeros(S + 1, **i32)
-        a_kl, a_de, _, a_co, a_cap = l_l.outputs()
-        b_kl, b_de, _, b_co, b_cap = l_r.outputs()
-        idx_cap = 32768
-        sbytes = plvi.stereo_lines_scratch_bytes(S, a_cap, b_cap, idx_cap)
-        s_scr = torch.empty(sbytes, dtype=torch.uint8, device=f"cuda:{dev}")
-        s_lo = torch.empty(S * a_cap * 11, dtype=torch.float64, device=f"cuda:{dev}")
-        lo = s_lo.data_ptr()
-        mbf_, mb_ = 47.90639384423901, 0.11
-
-        def run_stereo_orb():
-            plvi.stereo_match_batch(o_l, o_r, S, mb_, mbf_, st_f.data_ptr(), st_f.data_ptr() + 4 * S * scap,
-                                    st_i.data_ptr(), st_i.data_ptr() + 4 * S, stream=sA.cuda_stream)
-
-        def run_stereo_lines():
-            plvi.stereo_lines_batch(S, a_kl, a_de, a_co, a_cap, b_kl, b_de, b_co, b_cap, None, W, H, mbf_, 1,
-                                    idx_cap, s_scr.data_ptr(), sbytes, lo, lo + 4 * S * a_cap,
-                                    lo + 12 * S * a_cap, lo + 20 * S * a_cap, lo + 44 * S * a_cap,
-                                    st_i.data_ptr() + 4 * S, stream=sA.cuda_stream)
-        stereo_ms = {}
-        for name, fn in (("stereo.orb", run_stereo_orb), ("stereo.lines", run_stereo_lines)):
-            fn()
-            torch.cuda.synchronize()
-            ev0.record(sA)
-            for _ in range(nprof):
-                fn()
-            ev1.record(sA)
-            torch.cuda.synchronize()
-            stereo_ms[name] = ev0.elapsed_time(ev1) / nprof
-        if int(st_i[S].item()) != 0:
-            raise RuntimeError(f"stereo err {int(st_i[S].item())}")
-        stereo_ms["stereo.pairs"] = S
-        del o_l, o_r, l_l, l_r
+    parts = {"orb_only": part_fps(lambda: orb.extract_batch(f0, B, W * H, W, (0, 0), stream=st)),
+             "lines_only": part_fps(lambda: lx.extract_batch(f0, B, W * H, W, stream=st)),
+             "match_only": part_fps(match)}
     stage_ms = {f"orb.{k}": v / runs for k, v in st_orb.items()}
     stage_ms.update({f"lines.{k}": v / lruns for k, v in st_lines.items()})
     stage_ms["match"] = match_ms / nprof
-    if bow_ms is not None:
-        stage_ms["bow.transform"] = bow_ms
-    if proj_ms is not None:
-        stage_ms["proj.grid+search"] = proj_ms
-    side = ("bow.transform", "proj.grid+search", "stereo.orb", "stereo.lines", "stereo.pairs")
-    if stereo_ms is not None:
-        stage_ms.update(stereo_ms)
+    side = {}
+    if not args.no_side and world == 1:
+        side = side_stages(args, torch, plvi, synth, lib, orb, st, stream, B, W, H, cap, kp_p, de_p, co_p, nprof,
+                           cuda, seed0)
 
+    # ---------------------------------------------------------- timed region
     pdist.barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    if args.gather and rank == 0 and world > 1:
+        for w_ in pending:
+            w_.wait()
     torch.cuda.synchronize()
     pdist.barrier(world)
-    el = pdist.max_over_ranks(time.perf_counter() - t0, world, f"cuda:{dev}")
+    el = pdist.max_over_ranks(time.perf_counter() - t0, world, cuda)
 
-    frames_total = B * args.steps * world
+    new_frames = (B - 1) if args.c4 else B
+    frames_total = new_frames * args.steps * world
     value = frames_total / el
     ms_step = el / args.steps * 1e3
+    err = (orb.errors(st) | err_warm[0], lx.errors(st) | err_warm[1])
+    # last timed batch's window (for the checks below)
+    lo_last = ((args.steps + args.warmup - 1) % nwin) * (B - 1)
 
-    # roofline: the dominant HBM-streaming kernel, averaged over every launch
-    # of this process (warmup, stage runs, timed steps) = what rocprofv3
-    # --stats averages for the same command
+    # ---------------------------------------------------------- rooflines
     ktot, kn = orb.kernel_timing_read()
-    kavg_ms = ktot / max(kn, 1)
+    ltot, ln = lx.kernel_timing_read()
     bf_bytes = blur_fast_bytes(W, H) * B
-    dom = max((k for k in stage_ms if k not in side), key=stage_ms.get)
-    roof = {
-        "bound": "hbm", "kernel": "orb_blur_fast_kernel (7x7 blur + FAST score, all 8 levels, one launch)",
-        "achieved": bf_bytes / (kavg_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-        "traffic": committed_traffic(B) if (W, H) == (640, 480) else None, "bytes_per_launch": bf_bytes, "avg_launch_ms": kavg_ms, "launches": kn,
-    }
+    lp_bytes = lsd_prep_bytes(W, H) * B
+    roof = {"bound": "hbm", "kernel": "orb_blur_fast_kernel (7x7 blur + FAST score, all 8 levels, one launch)",
+            "achieved": bf_bytes / (ktot / max(kn, 1) * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "traffic": committed_traffic(B, "orb_blur_fast_kernel") if (W, H) == (640, 480) else None,
+            "bytes_per_launch": bf_bytes, "avg_launch_ms": ktot / max(kn, 1), "launches": kn}
     roof["frac"] = roof["achieved"] / roof["peak"]
-    result = {
-        "metric": METRIC if (W, H) == (640, 480) else METRIC.replace("640×480", f"{W}×{H}"), "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-        "config": {"workload": "C1+C2+C3: ORB extract (1000 feats, 1.2, 8 levels, FAST 20/7) || LSD+LBD "
-                               "(200 lines, scale 0.8, 2 octaves) on two HIP streams, then ORB kNN-2 + "
-                               "LineMatcher::match vs previous frame",
-                   "batch": B, "width": W, "height": H, "parallelism": f"frames-sharded x{world}",
-                   "gather": bool(args.gather), "frame_sets": len(sets)},
-        "roofline": roof,
-        "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
-        "dominant_stage": dom,
-        "part_fps": {k: round(v, 1) for k, v in parts.items()},
-    }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline()
-    if rank == 0:
-        print(json.dumps(result), flush=True)
+    roof_lsd = {"bound": "hbm", "kernel": "lsd_prep_kernel (u8 -> f64 blur 7x7, resize x0.8, ll_angle; one launch "
+                                          "per octave)",
+                "achieved": lp_bytes / (ltot * 1e-3) / 1e9 if ltot else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "traffic": committed_traffic(B, "lsd_prep_kernel") if (W, H) == (640, 480) else None,
+                "bytes_per_launch": lp_bytes / 2, "avg_launch_ms": ltot / max(ln, 1), "launches": ln}
+    if roof_lsd["achieved"]:
+        roof_lsd["frac"] = roof_lsd["achieved"] / HBM_PEAK_GBS
+    e2e_b = E2E_BYTES_640 if (W, H) == (640, 480) else E2E_BYTES_752 if (W, H) == (752, 480) else None
+    e2e = None if e2e_b is None else {"bytes_per_frame": e2e_b, "achieved": e2e_b * value / world / 1e9,
+                                      "unit": "GB/s per GPU", "frac": e2e_b * value / world / 1e9 / HBM_PEAK_GBS,
+                                      "model": "SURVEY 8(d) reference-materialisation bytes x FPS per GPU"}
+
+    # ---------------------------------------------------------- checks
+    checks, digests = [], {"first_batch_frames": first_digest}
+    if not args.no_check:
+        checks = collect_checks(torch, plvi, seq, lo_last, B, W, H, orb, lx, outs, lm12, lnm, cap, lcap, extract,
+                                match)
+    # per-rank digest of the first window's tables (what rank 0 receives)
+    if args.gather:
+        extract(seq.data_ptr())
+        match()
+        torch.cuda.synchronize()
+        h = hashlib.sha256()
+        for src, n in zip((co_p, kp_p, de_p, lco_p, kl_p, lde_p), tab_sizes):
+            h.update(plvi.download(src, np.zeros(n, np.uint8)).tobytes())
+        digests["first_batch_tables"] = h.hexdigest()[:16]
+        if world > 1:
+            gather()
+            for w_ in pending:
+                w_.wait()
+            torch.cuda.synchronize()
+            if rank == 0:
+                digests["gathered_tables"] = []
+                for r in range(world):
+                    g = hashlib.sha256()
+                    for i in range(len(tab_sizes)):
+                        g.update(recv[i][r].cpu().numpy().tobytes())
+                    digests["gathered_tables"].append(g.hexdigest()[:16])
+    all_digests = [digests]
     if world > 1:
         import torch.distributed as dist
+        all_digests = [None] * world
+        dist.all_gather_object(all_digests, digests)
+
+    extra = {}
+    if rank == 0 and world == 1 and not args.no_extra:
+        extra = extra_lines(args, torch, plvi, synth, lib, stream, W, H, seed0, orb, lx, extract, match, seq, B)
+
+    result = {
+        "metric": METRIC if (W, H) == (640, 480) else METRIC.replace("640×480", f"{W}×{H}"), "value": value,
+        "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_step,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (plvi.synth.device_sequence: seeded scenes, integer camera shifts, sigma-2 noise)",
+        "config": {"workload": ("C4: 752x480 sequence per rank, windows of B frames with a one-frame halo; "
+                                if args.c4 else "C1+C2+C3: ") +
+                               "ORB extract (1000 feats, 1.2, 8 levels, FAST 20/7) || LSD+LBD (200 lines, scale 0.8, "
+                               "2 octaves) as one HIP-stream schedule, then ORB kNN-2 + LineMatcher::match vs "
+                               "previous frame" + (", RCCL gather of per-frame tables to rank 0" if args.gather
+                                                   else ""),
+                   "batch": B, "frames_per_step": new_frames, "width": W, "height": H,
+                   "parallelism": f"sequence-sharded x{world}", "gather": bool(args.gather)},
+        "roofline": roof,
+        "roofline_lsd_prep": roof_lsd,
+        "end_to_end_hbm": e2e,
+        "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
+        "dominant_stage": max(stage_ms, key=stage_ms.get),
+        "part_fps": {k: round(v, 1) for k, v in parts.items()},
+        "side_ms": side,
+        "device_errors": {"orb": err[0], "lines": err[1]},
+        "digests": all_digests,
+    }
+    result.update(extra)
+    fail = []
+    if err[0] or err[1]:
+        fail.append(f"device error flags orb={err[0]} lines={err[1]}")
+    if checks:
+        bad = oracle_verify(checks)
+        result["oracle_check"] = {"frames": [lo_last, lo_last + B // 2, lo_last + B - 1], "items": len(checks),
+                                  "mismatches": bad}
+        if bad:
+            fail.append(f"oracle mismatch: {bad}")
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        n = min(args.cpu_frames, B)
+        result["cpu_baseline"] = cpu_baseline([seq[i].cpu().numpy() for i in range(n)])
+    if world > 1:
+        import torch.distributed as dist
+        flags = [None] * world
+        dist.all_gather_object(flags, fail)
+        fail = [f"rank {r}: {m}" for r, fl in enumerate(flags) for m in fl]
         dist.destroy_process_group()
+    if fail:
+        result["failed"] = fail
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    return 1 if fail else 0
+
+
+def collect_checks(torch, plvi, seq, lo, B, W, H, orb, lx, outs, lm12, lnm, cap, lcap, extract, match):
+    """Re-run the last timed batch and download frames 0, B/2, B-1 and the
+    match of pair (B/2-1, B/2) for the oracle comparison."""
+    extract(seq[lo].data_ptr())
+    match()
+    torch.cuda.synchronize()
+    kp_p, de_p, co_p, mo_p, _ = orb.outputs()
+    kl_p, lde_p, fn_p, lco_p, _ = lx.outputs()
+    cnt = plvi.download(co_p, np.zeros(B, np.int32))
+    mono = plvi.download(mo_p, np.zeros(B, np.int32))
+    lcnt = plvi.download(lco_p, np.zeros(B, np.int32))
+    checks = []
+    tabs = {}
+    for f in sorted({0, B // 2 - 1, B // 2, B - 1}):
+        n, nl = int(cnt[f]), int(lcnt[f])
+        k = plvi.download(kp_p + 28 * cap * f, np.zeros(n, plvi.KEYPOINT_DTYPE))
+        d = plvi.download(de_p + 32 * cap * f, np.zeros((n, 32), np.uint8))
+        kl = plvi.download(kl_p + 68 * lcap * f, np.zeros(nl, plvi.KEYLINE_DTYPE))
+        ld = plvi.download(lde_p + 32 * lcap * f, np.zeros((nl, 32), np.uint8))
+        fn = plvi.download(fn_p + 24 * lcap * f, np.zeros((nl, 3), np.float64))
+        tabs[f] = (d, ld)
+        if f != B // 2 - 1:
+            img = seq[lo + f].cpu().numpy()
+            checks.append(("orb", img, (int(mono[f]), k, d)))
+            checks.append(("lines", img, (kl, ld, fn)))
+    p = B // 2 - 1  # pair p matches frame p+1 (query) against frame p (train)
+    n1 = int(cnt[p + 1])
+    got = tuple(plvi.download(o.data_ptr() + 4 * cap * p, np.zeros(n1, np.int32)) for o in outs)
+    checks.append(("knn2", (tabs[p + 1][0], tabs[p][0]), got))
+    nl1 = len(tabs[p + 1][1])
+    if nl1 and len(tabs[p][1]) >= 2:
+        m = plvi.download(lm12.data_ptr() + 4 * lcap * p, np.zeros(nl1, np.int32))
+        nm = int(plvi.download(lnm.data_ptr() + 4 * p, np.zeros(1, np.int32))[0])
+        checks.append(("lmatch", (tabs[p + 1][1], tabs[p][1]), (nm, m)))
+    return checks
+
+
+def side_stages(args, torch, plvi, synth, lib, orb, st, stream, B, W, H, cap, kp_p, de_p, co_p, nprof, cuda, seed0):
+    """Stages next to the per-frame step, timed separately on the
+    same batch: DBoW2 transform, AssignFeaturesToGrid + SearchByProjection,
+    rectified stereo (ORB SAD + line matchGrid)."""
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    out = {}
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        ev0.record(stream)
+        for _ in range(nprof):
+            fn()
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        return ev0.elapsed_time(ev1) / nprof
+    # DBoW2 transform of the batch's descriptors on a k=10, L=6 synthetic vocabulary
+    pv = synth.vocabulary(10, 6, seed=1)
+    voc = plvi.ORBVocabulary.from_nodes(10, 6, 0, 0, *pv, device=torch.cuda.current_device())
+    bo = {k: torch.empty(B * (cap + 1) * sz, dtype=torch.uint8, device=cuda)
+          for k, sz in (("bw", 4), ("bv", 8), ("bn", 4), ("fn", 4), ("fo", 4), ("fi", 4), ("fc", 4))}
+
+    def run_bow():
+        rc = lib.plvi_vocab_transform_batch(voc._h, de_p, co_p, cap, B, 4, *[bo[k].data_ptr() for k in
+                                            ("bw", "bv", "bn", "fn", "fo", "fi", "fc")], None, None, st)
+        if rc:
+            raise RuntimeError(f"bow {rc}")
+    out["bow.transform"] = timed(run_bow)
+    # SearchByProjection: frame t vs frame t-1's keypoints as MapPoints
+    gp = plvi.GridParams(0.0, 0.0, *[float(x) for x in plvi.grid_geometry(W, H)[4:]])
+    cell_off = torch.empty(B * 3073, dtype=torch.int32, device=cuda)
+    cell_idx = torch.empty(B * cap, dtype=torch.int32, device=cuda)
+    kpt = torch.empty(B * cap * 7, dtype=torch.float32, device=cuda)
+    lib.plvi_memcpy_async(kpt.data_ptr(), kp_p, B * cap * 28, 3, st)
+    torch.cuda.synchronize()
+    kv = kpt.view(B, cap, 7)
+    fx, fy, cx, cy, z = 458.654, 457.296, 367.215, 248.375, 5.0
+    x3 = torch.stack([(kv[..., 0] - cx) * z / fx, (kv[..., 1] - cy) * z / fy,
+                      torch.full_like(kv[..., 0], z)], -1).contiguous()
+    loct = kv[..., 5].view(torch.int32).contiguous()
+    lang = kv[..., 3].contiguous()
+    lflags = torch.full((B * cap,), 3, dtype=torch.uint8, device=cuda)
+    pp = plvi.ProjParams()
+    pp.fx, pp.fy, pp.cx, pp.cy, pp.mbf, pp.th = fx, fy, cx, cy, 40.0, 15.0
+    pp.min_x, pp.max_x, pp.min_y, pp.max_y, pp.inv_w, pp.inv_h = [float(x) for x in plvi.grid_geometry(W, H)]
+    pp.check_orientation, pp.nlevels = 1, 8
+    for i, sfac in enumerate(orb.GetScaleFactors()):
+        pp.scale_factors[i] = float(sfac)
+    pm = torch.empty((B - 1) * cap, dtype=torch.int32, device=cuda)
+    pn = torch.empty(B, dtype=torch.int32, device=cuda)
+
+    def run_proj():
+        plvi.assign_grid_batch(kp_p, co_p, cap, B, gp, cell_off.data_ptr(), cell_idx.data_ptr(), st)
+        rc = lib.plvi_search_by_projection_batch(
+            B - 1, ctypes.byref(pp), kp_p + 28 * cap, de_p + 32 * cap, co_p + 4, cap, None, None,
+            cell_off.data_ptr() + 4 * 3073, cell_idx.data_ptr() + 4 * cap, x3.data_ptr(), loct.data_ptr(),
+            lang.data_ptr(), de_p, lflags.data_ptr(), co_p, cap, pm.data_ptr(), pn.data_ptr(), st)
+        if rc:
+            raise RuntimeError(f"projection {rc}")
+    out["proj.grid+search"] = timed(run_proj)
+    # stereo on S rectified pairs extracted by their own handles
+    S = min(B, 256)
+    pairs = [synth.stereo_pair(seed0 + 10 ** 5 + i, W, H) for i in range(S)]
+    sl = torch.from_numpy(np.stack([p[0] for p in pairs])).to(cuda)
+    sr = torch.from_numpy(np.stack([p[1] for p in pairs])).to(cuda)
+    dev = torch.cuda.current_device()
+    o_l = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=S, device=dev)
+    o_r = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=S, device=dev)
+    l_l = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=S, device=dev)
+    l_r = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=S, device=dev)
+    for e, fr in ((o_l, sl), (o_r, sr), (l_l, sl), (l_r, sr)):
+        e.extract_batch(fr.data_ptr(), S, W * H, W, stream=st)
+    torch.cuda.synchronize()
+    scap = o_l.kp_cap
+    st_f = torch.empty(2 * S * scap, dtype=torch.float32, device=cuda)
+    st_i = torch.zeros(S + 1, dtype=torch.int32, device=cuda)
+    a_kl, a_de, _, a_co, a_cap = l_l.outputs()
+    b_kl, b_de, _, b_co, b_cap = l_r.outputs()
+    idx_cap = 32768
+    sbytes = plvi.stereo_lines_scratch_bytes(S, a_cap, b_cap, idx_cap)
+    s_scr = torch.empty(sbytes, dtype=torch.uint8, device=cuda)
+    s_lo = torch.empty(S * a_cap * 11, dtype=torch.float64, device=cuda)
+    lo = s_lo.data_ptr()
+    mbf_, mb_ = 47.90639384423901, 0.11
+    out["stereo.orb"] = timed(lambda: plvi.stereo_match_batch(
+        o_l, o_r, S, mb_, mbf_, st_f.data_ptr(), st_f.data_ptr() + 4 * S * scap, st_i.data_ptr(),
+        st_i.data_ptr() + 4 * S, stream=st))
+    out["stereo.lines"] = timed(lambda: plvi.stereo_lines_batch(
+        S, a_kl, a_de, a_co, a_cap, b_kl, b_de, b_co, b_cap, None, W, H, mbf_, 1, idx_cap, s_scr.data_ptr(), sbytes,
+        lo, lo + 4 * S * a_cap, lo + 12 * S * a_cap, lo + 20 * S * a_cap, lo + 44 * S * a_cap,
+        st_i.data_ptr() + 4 * S, stream=st))
+    if int(st_i[S].item()) != 0:
+        raise RuntimeError(f"stereo err {int(st_i[S].item())}")
+    out["stereo.pairs"] = S
+    return {k: round(v, 4) if isinstance(v, float) else v for k, v in out.items()}
+
+
+def extra_lines(args, torch, plvi, synth, lib, stream, W, H, seed0, orb, lx, extract, match, seq, B):
+    """Rank 0, N=1: (1) the same step at batch 64 (BASELINE C1/C2 as stated);
+    (2) single-frame latency of the drop-in entry points run the way Frame
+    runs them (plvi_orb_extract || plvi_lines_extract on two host threads,
+    host image in, host tables out; Frame.cc:558-561); (3) the step with the
+    frames streamed from pinned host memory: H2D of batch k+1 on a copy
+    stream overlapped with batch k (two device frame buffers)."""
+    import threading
+    out = {}
+    st = stream.cuda_stream
+    dev = torch.cuda.current_device()
+    cuda = f"cuda:{dev}"
+    # (1) batch 64
+    b64 = 64
+    o64 = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=b64, device=dev)
+    l64 = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=b64, device=dev)
+    kp, de, co, _, cap = o64.outputs()
+    _, lde, _, lco, lcap = l64.outputs()
+    i32 = dict(dtype=torch.int32, device=cuda)
+    o4 = [torch.empty((b64 - 1) * cap, **i32) for _ in range(4)]
+    lsc = torch.empty(4 * (b64 - 1) * 2 * lcap, **i32)
+    lm = torch.empty((b64 - 1) * lcap, **i32)
+    lnm = torch.empty(b64 - 1, **i32)
+
+    def step64():
+        plvi.frame_extract_batch(o64, l64, seq.data_ptr(), b64, W * H, W, (0, 0), stream=st)
+        rc = lib.plvi_hamming_knn2_batch(de + cap * 32, co + 4, cap, de, co, cap, b64 - 1, *[o.data_ptr() for o in o4],
+                                         st)
+        rc |= lib.plvi_line_match_batch(lde + lcap * 32, lco + 4, lcap, lde, lco, lcap, b64 - 1, 0.9, lsc.data_ptr(),
+                                        lm.data_ptr(), lnm.data_ptr(), st)
+        if rc:
+            raise RuntimeError("b64 match")
+    for _ in range(3):
+        step64()
+    torch.cuda.synchronize()
+    n64 = 50
+    t0 = time.perf_counter()
+    for _ in range(n64):
+        step64()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out["batch64"] = {"value": b64 * n64 / el, "unit": "frames/s", "ms_per_step": el / n64 * 1e3,
+                      "config": "C1/C2/C3 at batch 64 (BASELINE.json configs[1..2]): same extract+match step"}
+    if o64.errors(st) or l64.errors(st):
+        raise RuntimeError("batch-64 device error flags")
+    del o64, l64
+    # (2) single-frame latency: host image -> host tables, ORB || lines on two threads
+    so = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, device=dev)
+    sl = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, device=dev)
+    imgs = [seq[i].cpu().numpy() for i in range(24)]
+    lat, lo_, ll_ = [], [], []
+    for rep in range(len(imgs) + 4):
+        img = imgs[rep % len(imgs)]
+        res = {}
+
+        def ro():
+            t = time.perf_counter()
+            so(img)
+            res["orb"] = time.perf_counter() - t
+
+        def rl():
+            t = time.perf_counter()
+            sl(img)
+            res["lines"] = time.perf_counter() - t
+        t0 = time.perf_counter()
+        th = [threading.Thread(target=ro), threading.Thread(target=rl)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if rep >= 4:
+            lat.append(time.perf_counter() - t0)
+            lo_.append(res["orb"])
+            ll_.append(res["lines"])
+    out["single_frame_latency"] = {
+        "median_ms": float(np.median(lat)) * 1e3, "p90_ms": float(np.percentile(lat, 90)) * 1e3,
+        "orb_median_ms": float(np.median(lo_)) * 1e3, "lines_median_ms": float(np.median(ll_)) * 1e3,
+        "frames": len(lat), "how": "plvi_orb_extract || plvi_lines_extract on two host threads (Frame.cc:558-561), "
+                                   "host frame in, host keypoints/keylines/descriptors out"}
+    del so, sl
+    # (3) pinned-H2D overlapped step (the main handles, two device buffers)
+    host = torch.empty((B, H, W), dtype=torch.uint8, pin_memory=True)
+    host.copy_(seq[:B].cpu())
+    dbuf = [torch.empty((B, H, W), dtype=torch.uint8, device=cuda) for _ in range(2)]
+    cs = torch.cuda.Stream()
+    ev_copied = [torch.cuda.Event() for _ in range(2)]
+    ev_free = [torch.cuda.Event() for _ in range(2)]
+    for e in ev_free:
+        e.record(stream)
+
+    def h2d(k):
+        j = k % 2
+        cs.wait_event(ev_free[j])
+        with torch.cuda.stream(cs):
+            dbuf[j].copy_(host, non_blocking=True)
+        ev_copied[j].record(cs)
+
+    nh = max(args.steps, 5)
+    h2d(0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(nh):
+        h2d(k + 1)
+        j = k % 2
+        stream.wait_event(ev_copied[j])
+        extract(dbuf[j].data_ptr())
+        match()
+        ev_free[j].record(stream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out["h2d_overlapped"] = {"value": B * nh / el, "unit": "frames/s", "ms_per_step": el / nh * 1e3,
+                             "how": "frames from pinned host memory, H2D of batch k+1 on a copy stream overlapped "
+                                    "with batch k's extract+match"}
+    if orb.errors(st) or lx.errors(st):
+        raise RuntimeError("h2d device error flags")
+    return out
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

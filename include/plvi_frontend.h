@@ -35,6 +35,35 @@ enum {
   PLVI_E_SIZE = -6,     /* descriptor row counts differ (LineMatcher.cpp:50-51) */
 };
 
+/* OpenCV-semantics switches for the items no reference test can pin
+ * (confidence "M"); 0 = the default guesses.  Set in
+ * plvi_orb_params.compat / plvi_line_params.compat at create time; the CPU
+ * oracle takes the same flags.
+ *  GAUSS_ROUNDED   A.4: GaussianBlur CV_8U taps by plain rounding
+ *                  ([18,34,49,55,49,34,18] for 7x7 sigma 2, ORBextractor.cc:1115;
+ *                  [14,63,103,63,14] for 5x5 sigma 1, binary_descriptor_custom.cpp:359)
+ *                  instead of the error-diffused [18,34,48,56,..] / [14,62,104,..]
+ *  RESIZE_V_GENERIC A.1: cv::resize INTER_LINEAR 8U vertical pass by the generic
+ *                  (b0*H0 + b1*H1 + (1<<21)) >> 22 instead of the 8U
+ *                  specialisation ((b0*(H0>>4))>>16 + (b1*(H1>>4))>>16 + 2) >> 2
+ *                  (ORBextractor.cc:1165)
+ *  EXP_CV_TABLE    A.6: the f64 7-tap LSD Gaussian (lsd.cpp:455) built with
+ *                  OpenCV's table + polynomial exp (EXPTAB_SCALE 6) instead of
+ *                  glibc exp (which equals the correctly rounded exp there) */
+enum {
+  PLVI_COMPAT_GAUSS_ROUNDED = 1,
+  PLVI_COMPAT_RESIZE_V_GENERIC = 2,
+  PLVI_COMPAT_EXP_CV_TABLE = 4,
+};
+
+/* Per-frame device error flags of a batch (plvi_orb_errors / plvi_lines_errors). */
+enum {
+  PLVI_FERR_OCTREE = 1,   /* ORB: an octree level exceeded its node table (level dropped) */
+  PLVI_FERR_LSD_TILE = 2, /* lines: LSD prep tile footprint exceeded its LDS tile */
+  PLVI_FERR_LSD_RAW = 4,  /* lines: more LSD regions than the raw line table holds */
+  PLVI_FERR_KEYLINES = 8, /* lines: keyline table overflow (frame emitted with 0 lines) */
+};
+
 /* cv::KeyPoint layout (28 bytes): pt.x, pt.y, size, angle, response, octave, class_id. */
 typedef struct plvi_keypoint {
   float x, y, size, angle, response;
@@ -66,6 +95,7 @@ typedef struct plvi_orb_params {
   int nlevels;
   int ini_th_fast;
   int min_th_fast;
+  unsigned compat;    /* PLVI_COMPAT_* (0 = defaults) */
 } plvi_orb_params;
 
 /* Create an extractor for frames of width x height, batches of up to
@@ -80,7 +110,9 @@ int plvi_orb_destroy(plvi_orb_extractor* h);
  * slot order (mono slots ascending from 0, vLappingArea slots from the back);
  * descriptors are n x 32 bytes in the same row order.  *n = number of
  * keypoints, *mono_index = return value of operator() (monoIndex).
- * Returns PLVI_E_EMPTY for an empty image. */
+ * Returns PLVI_E_EMPTY for an empty image.  Like operator() it accepts any
+ * frame size: a size other than the handle's re-plans the handle (pyramid,
+ * cells, buffers) for the new size, which the batch entry points then use. */
 int plvi_orb_extract(plvi_orb_extractor* h, const uint8_t* img, int width, int height, size_t stride,
                      int lap0, int lap1, plvi_keypoint* kps, uint8_t* desc, int cap, int* n, int* mono_index);
 
@@ -91,6 +123,14 @@ int plvi_orb_extract(plvi_orb_extractor* h, const uint8_t* img, int width, int h
  * plvi_orb_outputs. */
 int plvi_orb_extract_batch(plvi_orb_extractor* h, const uint8_t* d_frames, int n_frames, size_t frame_stride,
                            size_t row_stride, int lap0, int lap1, void* stream);
+
+/* Device error flags of the batches run since the last call (PLVI_FERR_*),
+ * read and cleared: frame_flags[f] for frame slot f (max_batch ints, may be
+ * NULL), *any = OR over all slots (may be NULL).  Synchronises `stream`
+ * (NULL = the handle's stream), on which the flags are read and reset.  A
+ * frame with a flag set has truncated tables; the single-frame entry
+ * points report the same condition as PLVI_E_OVERFLOW. */
+int plvi_orb_errors(plvi_orb_extractor* h, int* frame_flags, int* any, void* stream);
 
 /* Device pointers to the last batch's outputs: keypoints [max_batch][cap],
  * descriptors [max_batch][cap][32], counts [max_batch], mono [max_batch].
@@ -147,6 +187,7 @@ typedef struct plvi_line_params {
   int nlevels;     /* pyramid octaves (<= 2) */
   float scale;     /* pyramid scale factor (2.0) */
   int extractor;   /* 0 = LSD (EDLines, extractor==1, is out of scope) */
+  unsigned compat; /* PLVI_COMPAT_* (0 = defaults) */
 } plvi_line_params;
 
 int plvi_lines_create(const plvi_line_params* p, int width, int height, int max_batch, int device,
@@ -157,7 +198,8 @@ int plvi_lines_destroy(plvi_line_extractor* h);
  * (LineExtractor.cc:45-117).  keylines (KeyLine layout) in the reference's
  * order (post top-k sort when truncated), LBD descriptors n x 32, and the
  * normalised line equations n x 3 doubles (keylineFunction).  The reference
- * APPENDS to keylineFunction; callers append line_fns themselves. */
+ * APPENDS to keylineFunction; callers append line_fns themselves. Any frame
+ * size is accepted (re-plans the handle, as for plvi_orb_extract). */
 int plvi_lines_extract(plvi_line_extractor* h, const uint8_t* img, int width, int height, size_t stride,
                        plvi_keyline* keylines, uint8_t* desc, double* line_fns, int cap, int* n);
 
@@ -166,6 +208,8 @@ int plvi_lines_extract_batch(plvi_line_extractor* h, const uint8_t* d_frames, in
                              size_t row_stride, void* stream);
 int plvi_lines_outputs(plvi_line_extractor* h, plvi_keyline** d_kl, uint8_t** d_desc, double** d_fn, int** d_count,
                        int* cap);
+/* Per-frame device error flags (PLVI_FERR_*), read and cleared; as plvi_orb_errors. */
+int plvi_lines_errors(plvi_line_extractor* h, int* frame_flags, int* any, void* stream);
 
 /* mvImagePyramid_l[level] (gaussianPyrs, level >= 1; level 0 is the input). */
 int plvi_lines_pyramid_level(plvi_line_extractor* h, int frame, int level, uint8_t* dst, int* w, int* hgt);
@@ -181,6 +225,10 @@ int plvi_lines_profile(plvi_line_extractor* h, int enable);
  * seeds, pops, commits, rect points, slow-path loads]; NULL disables. */
 int plvi_lines_debug_stats(plvi_line_extractor* h, unsigned long long* d_stats);
 int plvi_lines_profile_read(plvi_line_extractor* h, float* stage_ms, int* runs);
+/* Per-launch timing of lsd_prep_kernel (bench.py's LSD-pass roofline), one
+ * launch per octave: as plvi_orb_kernel_timing / _read. */
+int plvi_lines_kernel_timing(plvi_line_extractor* h, int enable);
+int plvi_lines_kernel_timing_read(plvi_line_extractor* h, float* total_ms, int* launches);
 
 /* ------------------------------------------------------------------ Hamming
  * ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:2350-2366) over a batch. */
@@ -205,6 +253,19 @@ int plvi_line_match_nnr(const uint8_t* desc1, int n1, const uint8_t* desc2, int 
 /* LineMatcher::match(desc1, desc2, nnr, matches_12) (LineMatcher.cpp:92-111):
  * matchNNR both ways + mutual check. */
 int plvi_line_match(const uint8_t* desc1, int n1, const uint8_t* desc2, int n2, float nnr, int* matches_12);
+
+/* In/out variants with the reference's std::vector semantics: matches_12
+ * holds the caller's n_prev existing entries on entry, and
+ * matches_12.resize(n1, -1) (LineMatcher.cpp:44) keeps the first
+ * min(n_prev, n1) of them (only accepted matches overwrite an entry) and
+ * sets the rest to -1.  In plvi_line_match_inout a kept entry i2 >= 0 then
+ * goes through the mutual check like a fresh one (LineMatcher.cpp:101-106);
+ * a kept i2 >= n2 is out of range there (undefined in the reference) and
+ * returns PLVI_E_BADARG. */
+int plvi_line_match_nnr_inout(const uint8_t* desc1, int n1, const uint8_t* desc2, int n2, float nnr, int* matches_12,
+                              int n_prev);
+int plvi_line_match_inout(const uint8_t* desc1, int n1, const uint8_t* desc2, int n2, float nnr, int* matches_12,
+                          int n_prev);
 
 /* Batched LineMatcher::match on device descriptor tables: pair p matches
  * desc1[p] (n1[p] rows, stride cap1) against desc2[p] (n2[p] rows, stride

@@ -113,15 +113,54 @@ void resize_linear_u8(const ImageU8& src, ImageU8& dst, int dw, int dh) {
         hresize(src.row(r0), H0.data());
         hresize(src.row(r1), H1.data());
         uint8_t* D = dst.row(dy);
-        for (int x = 0; x < dw; ++x)
-            D[x] = (uint8_t)((((b0 * (H0[x] >> 4)) >> 16) + ((b1 * (H1[x] >> 4)) >> 16) + 2) >> 2);
+        if (g_compat & 2) {
+            // generic VResizeLinear + FixedPtCast<int, uchar, 22> (A.1 switch)
+            for (int x = 0; x < dw; ++x)
+                D[x] = (uint8_t)std::min(std::max((b0 * H0[x] + b1 * H1[x] + (1 << 21)) >> 22, 0), 255);
+        } else {
+            // VResizeLinear<uchar, int, short, FixedPtCast, VResizeLinearVec_32s8u>
+            for (int x = 0; x < dw; ++x)
+                D[x] = (uint8_t)((((b0 * (H0[x] >> 4)) >> 16) + ((b1 * (H1[x] >> 4)) >> 16) + 2) >> 2);
+        }
     }
+}
+
+unsigned g_compat = 0;
+
+// ---------------------------------------------------------------- A.6 exp
+// OpenCV's exp64f (core/src/mathfuncs_core.simd.hpp; softfloat.cpp's f64_exp
+// follows the same scheme): x * 64/ln2 rounded to an int v, 2^(v>>6) from
+// the exponent bits, 2^((v&63)/64) * A0 from a 64-entry table, and a degree-5
+// polynomial in the remainder.  Constants are the published decimal
+// literals (confidence M: no OpenCV here to confirm them).
+double cv_exp_table(double x) {
+    const double A0s = .9670371139572337719125840413672004409288e-2;  // EXPPOLY_32F_A0
+    struct Tab {
+        double v[64];
+        Tab(double a) { for (int i = 0; i < 64; ++i) v[i] = (double)exp2l((long double)i / 64.0L) * a; }
+    };
+    static const Tab tabs(A0s);  // thread-safe one-time init
+    const double* tab = tabs.v;
+    const double prescale = 1.4426950408889634073599246810019 * 64, postscale = 1. / 64;
+    const double A5 = .99999999999999999998285227504999 / A0s, A4 = .69314718055994546743029643825322 / A0s,
+                 A3 = .24022650695886477918181338054308 / A0s, A2 = .55504108793649567998466049042729e-1 / A0s,
+                 A1 = .96180973140732918010002372686186e-2 / A0s, A0 = .13369713757180123244806654839424e-2 / A0s;
+    double x0 = x * prescale;
+    const int v = cv_round(x0);
+    int t = (v >> 6) + 1023;
+    t = !(t & ~2047) ? t : t < 0 ? 0 : 2047;
+    uint64_t bits = (uint64_t)t << 52;
+    double buf;
+    std::memcpy(&buf, &bits, 8);
+    x0 = (x0 - v) * postscale;
+    return buf * tab[v & 63] * (((((A0 * x0 + A1) * x0 + A2) * x0 + A3) * x0 + A4) * x0 + A5);
 }
 
 // ---------------------------------------------------------------- A.4 / A.6
 // getGaussianKernelBitExact (imgproc/src/smooth.dispatch.cpp) followed by
-// getGaussianKernelFixedPoint_ED(.., 8).  glibc exp stands in for softdouble
-// exp (parity unpinned; the 8-bit taps are insensitive to the last ulp).
+// getGaussianKernelFixedPoint_ED(.., 8).  exp: glibc (default; equals the
+// correctly rounded exp at the configs' arguments) or OpenCV's table exp
+// (g_compat & 4).  Parity vs real OpenCV unpinned.
 static void gaussian_kernel_bitexact(int n, double sigma, std::vector<double>& res) {
     res.assign(n, 0.0);
     if (sigma <= 0) {
@@ -138,7 +177,8 @@ static void gaussian_kernel_bitexact(int n, double sigma, std::vector<double>& r
     std::vector<double> values(n2 + 1);
     double sum = 0;
     for (int i = 0, x = 1 - n; i < n2; ++i, x += 2) {
-        double t = std::exp((double)(x * x) * scale2X);
+        const double a = (double)(x * x) * scale2X;
+        double t = (g_compat & 4) ? cv_exp_table(a) : std::exp(a);
         values[i] = t;
         sum += t;
     }
@@ -165,6 +205,11 @@ void gaussian_taps_u8(int n, double sigma, int* taps) {
     std::vector<double> kd;
     gaussian_kernel_bitexact(n, sigma, kd);
     const int n2 = n / 2;
+    if (g_compat & 1) {
+        // plain rounding of every tap (the pre-error-diffusion conversion)
+        for (int i = 0; i < n; ++i) taps[i] = (int)lrint(kd[i] * 256.0);
+        return;
+    }
     double err = 0;
     long sum = 0;
     for (int i = 0; i < n2; ++i) {

@@ -19,6 +19,14 @@
 
 namespace oracle {
 
+// Switches for the Appendix-A items no reference test pins (same bits as
+// PLVI_COMPAT_* in include/plvi_frontend.h), process-global in the oracle:
+//  1 = A.4 plainly rounded 8-bit Gaussian taps instead of error diffusion
+//  2 = A.1 generic vertical fixed-point cast in resize INTER_LINEAR 8U
+//  4 = A.6 OpenCV table + polynomial exp (exp64f) in getGaussianKernel
+extern unsigned g_compat;
+double cv_exp_table(double x);
+
 // A.10 cvRound: round half to even (SSE cvtss2si / cvtsd2si).
 static inline int cv_round(float v) { return (int)lrintf(v); }
 static inline int cv_round(double v) { return (int)lrint(v); }

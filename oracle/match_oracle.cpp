@@ -8,6 +8,7 @@
 //   LineMatcher::matchNNR / match  src/LineMatcher.cpp:41-111
 //   ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...)  src/ORBmatcher.cc:269-471
 //   LineMatcher::matchGrid  src/LineMatcher.cpp:191-272 (+ gridStructure.cpp:64-75)
+#include <stdexcept>
 #include <climits>
 #include <cmath>
 #include <cstdint>
@@ -53,12 +54,15 @@ extern "C" void oracle_knn2(const uint8_t* q, int nq, const uint8_t* t, int nt, 
     }
 }
 
-extern "C" int oracle_match_nnr(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float nnr, int* m12) {
+// LineMatcher::matchNNR / match (LineMatcher.cpp:41-61, :92-111) on a
+// std::vector<int> exactly as the reference holds it: resize(rows, -1) keeps
+// the caller's existing entries.
+static int match_nnr_vec(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float nnr, std::vector<int>& m12) {
+    m12.resize(n1, -1);
     std::vector<int> i0(n1), a(n1), i1(n1), b(n1);
     oracle_knn2(d1, n1, d2, n2, i0.data(), a.data(), i1.data(), b.data());
     int matches = 0;
     for (int idx = 0; idx < n1; ++idx) {
-        m12[idx] = -1;
         if ((float)a[idx] < (float)b[idx] * nnr) {
             m12[idx] = i0[idx];
             ++matches;
@@ -67,18 +71,48 @@ extern "C" int oracle_match_nnr(const uint8_t* d1, int n1, const uint8_t* d2, in
     return matches;
 }
 
-extern "C" int oracle_match(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float nnr, int* m12) {
-    std::vector<int> m21(n2 > 0 ? n2 : 1);
-    int matches = oracle_match_nnr(d1, n1, d2, n2, nnr, m12);
-    oracle_match_nnr(d2, n2, d1, n1, nnr, m21.data());
-    for (int i1 = 0; i1 < n1; ++i1) {
+static int match_vec(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float nnr, std::vector<int>& m12) {
+    std::vector<int> m21;
+    int matches = match_nnr_vec(d1, n1, d2, n2, nnr, m12);
+    match_nnr_vec(d2, n2, d1, n1, nnr, m21);
+    for (int i1 = 0, nsize = (int)m12.size(); i1 < nsize; ++i1) {
         int& i2 = m12[i1];
-        if (i2 >= 0 && m21[i2] != i1) {
+        if (i2 >= 0 && m21.at(i2) != i1) {  // .at: a stale out-of-range entry is UB in the reference
             i2 = -1;
             --matches;
         }
     }
     return matches;
+}
+
+// m12 holds n_prev existing entries on entry and n1 on return.
+extern "C" int oracle_match_nnr_inout(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float nnr, int* m12,
+                                      int n_prev) {
+    std::vector<int> v(m12, m12 + n_prev);
+    int r = match_nnr_vec(d1, n1, d2, n2, nnr, v);
+    std::copy(v.begin(), v.end(), m12);
+    return r;
+}
+
+extern "C" int oracle_match_inout(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float nnr, int* m12,
+                                  int n_prev) {
+    std::vector<int> v(m12, m12 + n_prev);
+    int r;
+    try {
+        r = match_vec(d1, n1, d2, n2, nnr, v);
+    } catch (const std::out_of_range&) {
+        return -2;
+    }
+    std::copy(v.begin(), v.end(), m12);
+    return r;
+}
+
+extern "C" int oracle_match_nnr(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float nnr, int* m12) {
+    return oracle_match_nnr_inout(d1, n1, d2, n2, nnr, m12, 0);
+}
+
+extern "C" int oracle_match(const uint8_t* d1, int n1, const uint8_t* d2, int n2, float nnr, int* m12) {
+    return oracle_match_inout(d1, n1, d2, n2, nnr, m12, 0);
 }
 
 // ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)

@@ -75,7 +75,7 @@ struct Node {
     long seq = 0;  // creation sequence == bump-allocator address order (B.1)
 };
 
-static long g_seq = 0;
+static thread_local long g_seq = 0;  // per thread: the bench runs the oracle on several host threads
 
 static void divide_node(const Node& P, Node& n1, Node& n2, Node& n3, Node& n4) {
     const int halfX = (int)std::ceil((float)(P.URx - P.ULx) / 2);
@@ -475,6 +475,9 @@ extern "C" void oracle_gaussian_blur_u8(const uint8_t* src, int w, int h, int ks
     std::memcpy(dst, d.px.data(), (size_t)w * h);
 }
 
+extern "C" void oracle_set_compat(unsigned bits) { g_compat = bits; }
+extern "C" unsigned oracle_get_compat(void) { return g_compat; }
+extern "C" double oracle_cv_exp_table(double x) { return cv_exp_table(x); }
 extern "C" void oracle_gaussian_taps_u8(int ksize, double sigma, int* taps) { gaussian_taps_u8(ksize, sigma, taps); }
 extern "C" void oracle_gaussian_kernel_f64(int ksize, double sigma, double* k) { gaussian_kernel_f64(ksize, sigma, k); }
 extern "C" float oracle_fast_atan2(float y, float x) { return fast_atan2(y, x); }

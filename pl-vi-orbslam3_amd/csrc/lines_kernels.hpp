@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void lsd_prep_kernel(const uint8_t* __restrict
     const int gy0 = yrow[2 * Y0], gy1 = yrow[2 * Ye + 1];
     const int GW = gx1 - gx0 + 1, GH = gy1 - gy0 + 1;
     if (GW > kPGW || GH > kPGH) {
-        if (threadIdx.x == 0) atomicOr(err, 2);
+        if (threadIdx.x == 0) atomicOr(err + f, 2);
         return;
     }
     const uint8_t* S = src + (size_t)f * s_frame;
@@ -523,7 +523,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
     }
     if (lane == 0) {
         nlines[f * nOct + o] = nout;
-        if (overflow) atomicOr(err, 4);
+        if (overflow) atomicOr(err + f, 4);
     }
     if (do_stats && lane == 0) {
         unsigned long long* S = stats + (size_t)(f * nOct + o) * 16;
@@ -789,7 +789,7 @@ __global__ __launch_bounds__(256) void line_assemble_kernel(const LineOctDev* __
     }
     const int n = s_base;
     if (n > kKlCap) {
-        if (threadIdx.x == 0) { count_out[f] = 0; atomicOr(err, 8); }
+        if (threadIdx.x == 0) { count_out[f] = 0; atomicOr(err + f, 8); }
         return;
     }
     int nfinal = n;
@@ -802,7 +802,7 @@ __global__ __launch_bounds__(256) void line_assemble_kernel(const LineOctDev* __
         nfinal = nfeatures;
     }
     if (nfinal > fcap) {
-        if (threadIdx.x == 0) { count_out[f] = 0; atomicOr(err, 8); }
+        if (threadIdx.x == 0) { count_out[f] = 0; atomicOr(err + f, 8); }
         return;
     }
     plvi_keyline* outk = kl_out + (size_t)f * fcap;
@@ -823,7 +823,8 @@ __global__ __launch_bounds__(256) void line_assemble_kernel(const LineOctDev* __
 }
 
 // ---------------------------------------------------------------------------
-// LB1: LBD octave 0 = GaussianBlur(5x5, 1) fixed point (taps 14,62,104,62,14)
+// LB1: LBD octave 0 = GaussianBlur(5x5, 1) fixed point (taps t0,t1,t2,t1,t0 =
+// 14,62,104 error-diffused, or 14,63,103 rounded: PLVI_COMPAT_GAUSS_ROUNDED)
 // of the full frame (binary_descriptor_custom.cpp:359), Sobel dx/dy int16
 // (:396-397).  LB2: octave 1 = pyrDown(blurred) (:367) + Sobel.
 // 64x16 tiles; all borders reflect-101.
@@ -832,7 +833,8 @@ constexpr int kBTW = 64, kBTH = 16;
 
 __global__ __launch_bounds__(256) void lbd_blur_sobel_kernel(const uint8_t* __restrict__ src, size_t s_frame,
                                                              size_t s_row, int w, int h, uint8_t* __restrict__ blur,
-                                                             short2* __restrict__ go, size_t d_frame) {
+                                                             short2* __restrict__ go, size_t d_frame, int t0,
+                                                             int t1, int t2) {
     constexpr int EW = kBTW + 6, EH = kBTH + 6;  // input: halo 3 (2 blur + 1 sobel)
     __shared__ uint8_t I[EH][EW];
     __shared__ int Hs[EH][kBTW + 2];
@@ -849,13 +851,13 @@ __global__ __launch_bounds__(256) void lbd_blur_sobel_kernel(const uint8_t* __re
     for (int i = threadIdx.x; i < EH * (kBTW + 2); i += 256) {
         const int r = i / (kBTW + 2), c = i % (kBTW + 2);
         const uint8_t* e = &I[r][c];
-        Hs[r][c] = 14 * (e[0] + e[4]) + 62 * (e[1] + e[3]) + 104 * e[2];
+        Hs[r][c] = t0 * (e[0] + e[4]) + t1 * (e[1] + e[3]) + t2 * e[2];
     }
     __syncthreads();
     for (int i = threadIdx.x; i < (kBTH + 2) * (kBTW + 2); i += 256) {
         const int r = i / (kBTW + 2), c = i % (kBTW + 2);
-        const unsigned s = (unsigned)(14 * (Hs[r][c] + Hs[r + 4][c]) + 62 * (Hs[r + 1][c] + Hs[r + 3][c]) +
-                                      104 * Hs[r + 2][c]);
+        const unsigned s = (unsigned)(t0 * (Hs[r][c] + Hs[r + 4][c]) + t1 * (Hs[r + 1][c] + Hs[r + 3][c]) +
+                                      t2 * Hs[r + 2][c]);
         Bv[r][c] = (uint8_t)min((s + 32768u) >> 16, 255u);
     }
     __syncthreads();
@@ -1062,4 +1064,3 @@ __global__ __launch_bounds__(64) void lbd_describe_kernel(const LineOctDev* __re
 
 }  // namespace plvi
 
-#include "lsd_grow2.hpp"

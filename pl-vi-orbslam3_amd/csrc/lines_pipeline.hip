@@ -22,14 +22,35 @@ static inline int lround_h(float v) { return (int)lrintf(v); }
 static inline int lround_h(double v) { return (int)lrint(v); }
 static inline int lfloor_h(float v) { int i = (int)v; return i - (i > v); }
 
+// exp64f of OpenCV (mathfuncs_core; softfloat's f64_exp uses the same
+// scheme): v = cvRound(x * 64/ln2), 2^(v>>6) in the exponent bits, the table
+// entry 2^((v&63)/64) * EXPPOLY_32F_A0 and a degree-5 polynomial of the
+// remainder.  SURVEY A.6 switch (PLVI_COMPAT_EXP_CV_TABLE).
+static double cv_exp64f(double x) {
+    const double a0s = .9670371139572337719125840413672004409288e-2;
+    const double k5 = .99999999999999999998285227504999 / a0s, k4 = .69314718055994546743029643825322 / a0s,
+                 k3 = .24022650695886477918181338054308 / a0s, k2 = .55504108793649567998466049042729e-1 / a0s,
+                 k1 = .96180973140732918010002372686186e-2 / a0s, k0 = .13369713757180123244806654839424e-2 / a0s;
+    const double pre = 1.4426950408889634073599246810019 * 64;
+    double y = x * pre;
+    const int v = (int)lrint(y);
+    int e = (v >> 6) + 1023;
+    e = e < 0 ? 0 : e > 2047 ? 2047 : e;
+    const double p2 = std::ldexp(1.0, e - 1023);
+    const double tab = (double)exp2l((long double)(v & 63) / 64.0L) * a0s;
+    y = (y - v) * (1. / 64);
+    return p2 * tab * (((((k0 * y + k1) * y + k2) * y + k3) * y + k4) * y + k5);
+}
+
 // getGaussianKernelBitExact (OpenCV 4.2 smooth.dispatch.cpp) in double.
-static void gauss_kernel_f64(int n, double sigma, double* k) {
+static void gauss_kernel_f64(int n, double sigma, double* k, bool cvExp) {
     const double scale2X = -0.125 / (sigma * sigma);
     const int n2 = (n - 1) / 2;
     std::vector<double> values(n2 + 1);
     double sum = 0;
     for (int i = 0, x = 1 - n; i < n2; ++i, x += 2) {
-        double t = std::exp((double)(x * x) * scale2X);
+        const double a = (double)(x * x) * scale2X;
+        double t = cvExp ? cv_exp64f(a) : std::exp(a);
         values[i] = t;
         sum += t;
     }
@@ -52,6 +73,7 @@ struct LinePipeline {
     std::vector<float> scaleF, invScaleF;
     double SCALE = 0.8, prec = 0, rho = 0, min_length = 0;
     double gk[7]{};
+    int lbdTaps[3] = {14, 62, 104};
     DevBuf d_oct, d_tabs, octImg, pix, modg, seedcs, gbits, qspill, regs, regpts, rawLines, nlines, klTmp, klOut, fnOut, cntOut, descOut, lbdBlur,
         lbdG, err, staging;
     size_t qspillFrame = 0, gbitsFrame = 0, lbdPlaneTotal = 0;
@@ -61,7 +83,36 @@ struct LinePipeline {
     int profRuns = 0;
     std::vector<hipEvent_t> evs;
 
+    // Per-launch timing of lsd_prep_kernel (bench.py's LSD-pass roofline): an
+    // event pair on the launch stream around every launch while enabled.
+    static constexpr int kKRing = 4096;
+    bool ktime = false;
+    int kn = 0;
+    std::vector<hipEvent_t> kev;
+    int ktiming(int on) {
+        if (on && kev.empty()) {
+            kev.resize(2 * kKRing);
+            for (auto& e : kev) PLVI_CHECK(hipEventCreate(&e));
+        }
+        ktime = on != 0;
+        if (on) kn = 0;
+        return PLVI_OK;
+    }
+    int ktiming_read(float* total_ms, int* launches) {
+        float tot = 0.f;
+        for (int i = 0; i < kn; ++i) {
+            PLVI_CHECK(hipEventSynchronize(kev[2 * i + 1]));
+            float t = 0.f;
+            PLVI_CHECK(hipEventElapsedTime(&t, kev[2 * i], kev[2 * i + 1]));
+            tot += t;
+        }
+        if (total_ms) *total_ms = tot;
+        if (launches) *launches = kn;
+        return PLVI_OK;
+    }
+
     ~LinePipeline() {
+        for (auto e : kev) (void)hipEventDestroy(e);
         for (auto e : evs) (void)hipEventDestroy(e);
         for (auto e : {evFork, evPrep, evSobel, evOrb, evCrit})
             if (e) (void)hipEventDestroy(e);
@@ -104,7 +155,11 @@ struct LinePipeline {
         const double sigma = (SCALE < 1) ? (SIGMA_SCALE / SCALE) : SIGMA_SCALE;
         const unsigned hk = (unsigned)std::ceil(sigma * std::sqrt(2 * 3.0 * std::log(10.0)));
         if (SCALE != 1 && 1 + 2 * hk != 7) return PLVI_E_BADARG;  // tile kernel is specialised to 7 taps
-        gauss_kernel_f64(7, sigma, gk);
+        gauss_kernel_f64(7, sigma, gk, (p->compat & PLVI_COMPAT_EXP_CV_TABLE) != 0);
+        // LBD 5x5 sigma 1 fixed-point taps (A.4): error-diffused or rounded
+        lbdTaps[0] = 14;
+        lbdTaps[1] = (p->compat & PLVI_COMPAT_GAUSS_ROUNDED) ? 63 : 62;
+        lbdTaps[2] = (p->compat & PLVI_COMPAT_GAUSS_ROUNDED) ? 103 : 104;
         // ComputePyramid(image, scale, nlevels) (LSDDetector_custom.cpp:76-109)
         scaleF.assign(nOct, 1.f); invScaleF.assign(nOct, 1.f);
         for (int l = 0; l < nOct; ++l) {
@@ -214,9 +269,9 @@ struct LinePipeline {
             klOut.alloc(sizeof(plvi_keyline) * (size_t)fcap * Bcap) || fnOut.alloc(sizeof(double) * 3 * fcap * Bcap) ||
             cntOut.alloc(sizeof(int) * Bcap) || descOut.alloc((size_t)32 * fcap * Bcap) ||
             lbdBlur.alloc((size_t)W * H * Bcap) || lbdG.alloc(sizeof(short2) * lbdPlaneTotal) ||
-            err.alloc(sizeof(int)) || staging.alloc((size_t)W * H))
+            err.alloc(sizeof(int) * Bcap) || staging.alloc((size_t)W * H))
             return PLVI_E_HIP;
-        PLVI_CHECK(hipMemset(err.p, 0, sizeof(int)));
+        PLVI_CHECK(hipMemset(err.p, 0, sizeof(int) * Bcap));
         // region-growing LDS: rect staging + R-row USED/angle window + queue,
         // sized so that several waves share a CU and leave LDS to the kernels that
         // run concurrently (PLVI_GROW_LDS, default 6 KB: R = 2 rows, 5.1 KB at
@@ -237,14 +292,10 @@ struct LinePipeline {
         growSmem = fixed + perRow * growR;
         for (const void* k : {(const void*)lsd_grow_kernel<false>, (const void*)lsd_grow_kernel<true>})
             PLVI_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)growSmem));
-        PLVI_CHECK(hipFuncSetAttribute((const void*)lsd_grow2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)(2 * growSmem)));
-        // PLVI_GROW_PACK: tasks per region-growing wave (1 = lsd_grow_kernel, default; 2 = lsd_grow2_kernel)
-        if (const char* e = getenv("PLVI_GROW_PACK")) growPack = atoi(e) == 2 ? 2 : 1;
         return PLVI_OK;
     }
     size_t growSmem = 0;
-    int growR = 0, growQL = 0, growPack = 1;
+    int growR = 0, growQL = 0;
     unsigned long long* growStats = nullptr;  // diagnostic cycle counters (plvi_lines_debug_stats)
 
     int profile(int on) {
@@ -292,31 +343,29 @@ struct LinePipeline {
             const size_t sf = l == 0 ? frame_stride : (size_t)d.plane;
             const size_t sr = l == 0 ? row_stride : (size_t)d.w;
             dim3 grid((d.sw + kPTX - 1) / kPTX, (d.sh + kPTY - 1) / kPTY, nf);
+            const bool kt = ktime && kn < kKRing;
+            if (kt) (void)hipEventRecord(kev[2 * kn], st);
             hipLaunchKernelGGL(lsd_prep_kernel, grid, dim3(256), 0, st, s, sf, sr, d.w, d.h, d.sw, d.sh,
                                (const int*)(T + d.tabXofs), (const float*)(T + d.tabXa), d.xmax,
                                (const int*)(T + d.tabYrow), (const float*)(T + d.tabYb), gk[0], gk[1], gk[2], gk[3],
                                rho, pix.as<float>() + d.soff, modg.as<double>() + d.soff,
                                seedcs.as<float4>() + d.soff, (size_t)d.splane, err.as<int>());
+            if (kt) {
+                (void)hipEventRecord(kev[2 * kn + 1], st);
+                ++kn;
+            }
         }
         mark(2, st);
     }
 
     // Phase B: region growing (LK3) + keyline assembly / top-k (LK4).
     void launch_grow_assemble(int nf, hipStream_t st) {
-        if (growPack == 2 && !growStats) {
-            hipLaunchKernelGGL(lsd_grow2_kernel, dim3(nOct, (nf + 1) / 2), dim3(64), 2 * growSmem, st,
-                               d_oct.as<LineOctDev>(), (const float*)pix.as<float>(),
-                               (const float4*)seedcs.as<float4>(), gbits.as<unsigned>(), gbitsFrame,
-                               qspill.as<unsigned>(), qspillFrame, prec, regs.as<LsdRegion>(), regpts.as<unsigned>(),
-                               qspillFrame, nlines.as<int>(), err.as<int>(), growR, growQL, nf, (int)(growSmem / 4));
-        } else {
-            auto growK = growStats ? lsd_grow_kernel<true> : lsd_grow_kernel<false>;
-            hipLaunchKernelGGL(growK, dim3(nOct * nf), dim3(64), growSmem, st, d_oct.as<LineOctDev>(),
-                               (const float*)pix.as<float>(), (const double*)modg.as<double>(),
-                               (const float4*)seedcs.as<float4>(), gbits.as<unsigned>(), gbitsFrame,
-                               qspill.as<unsigned>(), qspillFrame, prec, regs.as<LsdRegion>(), regpts.as<unsigned>(),
-                               qspillFrame, nlines.as<int>(), err.as<int>(), growR, growQL, nOct, growStats);
-        }
+        auto growK = growStats ? lsd_grow_kernel<true> : lsd_grow_kernel<false>;
+        hipLaunchKernelGGL(growK, dim3(nOct * nf), dim3(64), growSmem, st, d_oct.as<LineOctDev>(),
+                           (const float*)pix.as<float>(), (const double*)modg.as<double>(),
+                           (const float4*)seedcs.as<float4>(), gbits.as<unsigned>(), gbitsFrame,
+                           qspill.as<unsigned>(), qspillFrame, prec, regs.as<LsdRegion>(), regpts.as<unsigned>(),
+                           qspillFrame, nlines.as<int>(), err.as<int>(), growR, growQL, nOct, growStats);
         hipLaunchKernelGGL(lsd_rect_kernel, dim3(kRectBlocks, nOct, nf), dim3(256), 0, st, d_oct.as<LineOctDev>(),
                            (const double*)modg.as<double>(), (const LsdRegion*)regs.as<LsdRegion>(),
                            (const unsigned*)regpts.as<unsigned>(), qspillFrame, (const int*)nlines.as<int>(), prec,
@@ -334,7 +383,8 @@ struct LinePipeline {
         const LineOctDev& d0 = oct[0];
         dim3 g0((d0.lw + kBTW - 1) / kBTW, (d0.lh + kBTH - 1) / kBTH, nf);
         hipLaunchKernelGGL(lbd_blur_sobel_kernel, g0, dim3(256), 0, st, d_frames, frame_stride, row_stride, d0.lw,
-                           d0.lh, lbdBlur.as<uint8_t>(), lbdG.as<short2>() + d0.loff, (size_t)d0.lplane);
+                           d0.lh, lbdBlur.as<uint8_t>(), lbdG.as<short2>() + d0.loff, (size_t)d0.lplane, lbdTaps[0],
+                           lbdTaps[1], lbdTaps[2]);
         for (int l = 1; l < nOct; ++l) {
             const LineOctDev& d = oct[l];
             if (l > 1) return PLVI_E_BADARG;  // pyrDown chain beyond octave 1 not wired (config: 2 levels)
@@ -414,8 +464,21 @@ struct LinePipeline {
 
 using plvi::LinePipeline;
 
+// Pipeline held by pointer so a frame-size change can re-plan the handle
+// (Lineextractor::operator() takes any image, LineExtractor.cc:45).
 struct plvi_line_extractor {
-    LinePipeline p;
+    std::unique_ptr<LinePipeline> up;
+    LinePipeline& p() { return *up; }
+    int replan(int width, int height) {
+        if (width == up->W && height == up->H) return PLVI_OK;
+        PLVI_CHECK(hipStreamSynchronize(up->stream));
+        auto np = std::make_unique<LinePipeline>();
+        int rc = np->init(&up->prm, width, height, up->Bcap, up->device);
+        if (rc) return rc;
+        np->growStats = nullptr;
+        up = std::move(np);
+        return PLVI_OK;
+    }
 };
 
 extern "C" int plvi_lines_create(const plvi_line_params* p, int width, int height, int max_batch, int device,
@@ -423,7 +486,8 @@ extern "C" int plvi_lines_create(const plvi_line_params* p, int width, int heigh
     if (!out) return PLVI_E_BADARG;
     *out = nullptr;
     auto h = std::make_unique<plvi_line_extractor>();
-    int rc = h->p.init(p, width, height, max_batch, device);
+    h->up = std::make_unique<LinePipeline>();
+    int rc = h->p().init(p, width, height, max_batch, device);
     if (rc) return rc;
     *out = h.release();
     return PLVI_OK;
@@ -431,8 +495,8 @@ extern "C" int plvi_lines_create(const plvi_line_params* p, int width, int heigh
 
 extern "C" int plvi_lines_destroy(plvi_line_extractor* h) {
     if (!h) return PLVI_E_BADARG;
-    (void)hipSetDevice(h->p.device);
-    (void)hipStreamSynchronize(h->p.stream);
+    (void)hipSetDevice(h->p().device);
+    (void)hipStreamSynchronize(h->p().stream);
     delete h;
     return PLVI_OK;
 }
@@ -440,27 +504,34 @@ extern "C" int plvi_lines_destroy(plvi_line_extractor* h) {
 extern "C" int plvi_lines_extract_batch(plvi_line_extractor* h, const uint8_t* d_frames, int n_frames,
                                         size_t frame_stride, size_t row_stride, void* stream) {
     if (!h || !d_frames) return PLVI_E_BADARG;
-    PLVI_CHECK(hipSetDevice(h->p.device));
-    return h->p.run(d_frames, n_frames, frame_stride, row_stride, (hipStream_t)stream);
+    PLVI_CHECK(hipSetDevice(h->p().device));
+    return h->p().run(d_frames, n_frames, frame_stride, row_stride, (hipStream_t)stream);
 }
 
 extern "C" int plvi_frame_extract_batch(plvi_orb_extractor* orb, plvi_line_extractor* lines, const uint8_t* d_frames,
                                         int n_frames, size_t frame_stride, size_t row_stride, int lap0, int lap1,
                                         void* stream) {
     if (!orb || !lines || !d_frames) return PLVI_E_BADARG;
-    PLVI_CHECK(hipSetDevice(lines->p.device));
-    return lines->p.run_with_orb(d_frames, n_frames, frame_stride, row_stride, (hipStream_t)stream, orb, lap0, lap1);
+    PLVI_CHECK(hipSetDevice(lines->p().device));
+    return lines->p().run_with_orb(d_frames, n_frames, frame_stride, row_stride, (hipStream_t)stream, orb, lap0, lap1);
 }
 
 extern "C" int plvi_lines_outputs(plvi_line_extractor* h, plvi_keyline** d_kl, uint8_t** d_desc, double** d_fn,
                                   int** d_count, int* cap) {
     if (!h) return PLVI_E_BADARG;
-    if (d_kl) *d_kl = h->p.klOut.as<plvi_keyline>();
-    if (d_desc) *d_desc = h->p.descOut.as<uint8_t>();
-    if (d_fn) *d_fn = h->p.fnOut.as<double>();
-    if (d_count) *d_count = h->p.cntOut.as<int>();
-    if (cap) *cap = h->p.fcap;
+    if (d_kl) *d_kl = h->p().klOut.as<plvi_keyline>();
+    if (d_desc) *d_desc = h->p().descOut.as<uint8_t>();
+    if (d_fn) *d_fn = h->p().fnOut.as<double>();
+    if (d_count) *d_count = h->p().cntOut.as<int>();
+    if (cap) *cap = h->p().fcap;
     return PLVI_OK;
+}
+
+extern "C" int plvi_lines_errors(plvi_line_extractor* h, int* frame_flags, int* any, void* stream) {
+    if (!h) return PLVI_E_BADARG;
+    PLVI_CHECK(hipSetDevice(h->p().device));
+    hipStream_t st = stream ? (hipStream_t)stream : h->p().stream;
+    return plvi::read_frame_errors(h->p().err.as<int>(), h->p().Bcap, frame_flags, any, st);
 }
 
 extern "C" int plvi_lines_extract(plvi_line_extractor* h, const uint8_t* img, int width, int height, size_t stride,
@@ -468,9 +539,9 @@ extern "C" int plvi_lines_extract(plvi_line_extractor* h, const uint8_t* img, in
     if (!h) return PLVI_E_BADARG;
     if (n) *n = 0;
     if (!img || width <= 0 || height <= 0) return PLVI_E_BADARG;
-    LinePipeline& P = h->p;
-    if (width != P.W || height != P.H) return PLVI_E_BADARG;
-    PLVI_CHECK(hipSetDevice(P.device));
+    PLVI_CHECK(hipSetDevice(h->p().device));
+    if (int rc = h->replan(width, height)) return rc;
+    LinePipeline& P = h->p();
     PLVI_CHECK(hipMemcpy2DAsync(P.staging.p, (size_t)P.W, img, stride, (size_t)P.W, (size_t)P.H,
                                 hipMemcpyHostToDevice, P.stream));
     int rc = P.run(P.staging.as<uint8_t>(), 1, (size_t)P.W * P.H, (size_t)P.W, P.stream);
@@ -480,7 +551,7 @@ extern "C" int plvi_lines_extract(plvi_line_extractor* h, const uint8_t* img, in
     PLVI_CHECK(hipMemcpyAsync(&errv, P.err.p, sizeof(int), hipMemcpyDeviceToHost, P.stream));
     PLVI_CHECK(hipStreamSynchronize(P.stream));
     if (errv) {
-        PLVI_CHECK(hipMemset(P.err.p, 0, sizeof(int)));
+        PLVI_CHECK(hipMemset(P.err.p, 0, sizeof(int) * P.Bcap));
         return PLVI_E_OVERFLOW;
     }
     if (n) *n = cnt;
@@ -495,15 +566,15 @@ extern "C" int plvi_lines_extract(plvi_line_extractor* h, const uint8_t* img, in
 
 extern "C" int plvi_lines_pyramid_level(plvi_line_extractor* h, int frame, int level, uint8_t* dst, int* w,
                                         int* hgt) {
-    if (!h || level < 0 || level >= h->p.nOct || frame < 0 || frame >= h->p.Bcap) return PLVI_E_BADARG;
-    const auto& d = h->p.oct[level];
+    if (!h || level < 0 || level >= h->p().nOct || frame < 0 || frame >= h->p().Bcap) return PLVI_E_BADARG;
+    const auto& d = h->p().oct[level];
     if (w) *w = d.w;
     if (hgt) *hgt = d.h;
     if (!dst) return PLVI_OK;
     if (level == 0) return PLVI_E_BADARG;  // level 0 is the caller's own image (gaussianPyrs[0] == image)
-    PLVI_CHECK(hipSetDevice(h->p.device));
-    PLVI_CHECK(hipStreamSynchronize(h->p.stream));
-    PLVI_CHECK(hipMemcpy(dst, h->p.octImg.as<uint8_t>() + d.off + (size_t)frame * d.plane, (size_t)d.plane,
+    PLVI_CHECK(hipSetDevice(h->p().device));
+    PLVI_CHECK(hipStreamSynchronize(h->p().stream));
+    PLVI_CHECK(hipMemcpy(dst, h->p().octImg.as<uint8_t>() + d.off + (size_t)frame * d.plane, (size_t)d.plane,
                          hipMemcpyDeviceToHost));
     return PLVI_OK;
 }
@@ -511,7 +582,7 @@ extern "C" int plvi_lines_pyramid_level(plvi_line_extractor* h, int frame, int l
 extern "C" int plvi_lines_scale_tables(plvi_line_extractor* h, float* scale, float* inv_scale, float* sigma2,
                                        float* inv_sigma2) {
     if (!h) return PLVI_E_BADARG;
-    const auto& P = h->p;
+    const auto& P = h->p();
     for (int i = 0; i < P.nOct; ++i) {
         // Lineextractor (LineExtractor.cc:88-99): sigma2[0] = 1, sigma2[i] = s*s
         const float s = P.scaleF[i];
@@ -526,20 +597,32 @@ extern "C" int plvi_lines_scale_tables(plvi_line_extractor* h, float* scale, flo
 
 extern "C" int plvi_lines_profile(plvi_line_extractor* h, int enable) {
     if (!h) return PLVI_E_BADARG;
-    PLVI_CHECK(hipSetDevice(h->p.device));
-    return h->p.profile(enable);
+    PLVI_CHECK(hipSetDevice(h->p().device));
+    return h->p().profile(enable);
 }
 
 extern "C" int plvi_lines_profile_read(plvi_line_extractor* h, float* stage_ms, int* runs) {
     if (!h || !stage_ms) return PLVI_E_BADARG;
-    PLVI_CHECK(hipSetDevice(h->p.device));
-    return h->p.profile_read(stage_ms, runs);
+    PLVI_CHECK(hipSetDevice(h->p().device));
+    return h->p().profile_read(stage_ms, runs);
 }
 
 // Diagnostic: enable per-task cycle accounting of the region-growing kernel
 // into a caller-provided device buffer of n_frames*nlevels*16 uint64 (NULL disables).
 extern "C" int plvi_lines_debug_stats(plvi_line_extractor* h, unsigned long long* d_stats) {
     if (!h) return PLVI_E_BADARG;
-    h->p.growStats = d_stats;
+    h->p().growStats = d_stats;
     return PLVI_OK;
+}
+
+extern "C" int plvi_lines_kernel_timing(plvi_line_extractor* h, int enable) {
+    if (!h) return PLVI_E_BADARG;
+    PLVI_CHECK(hipSetDevice(h->p().device));
+    return h->p().ktiming(enable);
+}
+
+extern "C" int plvi_lines_kernel_timing_read(plvi_line_extractor* h, float* total_ms, int* launches) {
+    if (!h) return PLVI_E_BADARG;
+    PLVI_CHECK(hipSetDevice(h->p().device));
+    return h->p().ktiming_read(total_ms, launches);
 }

@@ -15,6 +15,7 @@
 #include <climits>
 #include <cstring>
 #include <mutex>
+#include <algorithm>
 #include <vector>
 
 #include "plvi_common.h"
@@ -201,36 +202,49 @@ extern "C" int plvi_hamming_knn2(const uint8_t* q, int nq, const uint8_t* t, int
     return plvi::knn2_host(q, nq, t, nt, idx0, d0, idx1, d1);
 }
 
-// LineMatcher::matchNNR (LineMatcher.cpp:41-61).
-extern "C" int plvi_line_match_nnr(const uint8_t* desc1, int n1, const uint8_t* desc2, int n2, float nnr,
-                                   int* matches_12) {
-    if (n1 < 0 || n2 < 0 || !matches_12) return PLVI_E_BADARG;
+// LineMatcher::matchNNR (LineMatcher.cpp:41-61) with the std::vector
+// semantics of matches_12: resize(n1, -1) keeps the first min(n_prev, n1)
+// caller entries, accepted matches overwrite theirs.
+extern "C" int plvi_line_match_nnr_inout(const uint8_t* desc1, int n1, const uint8_t* desc2, int n2, float nnr,
+                                         int* matches_12, int n_prev) {
+    if (n1 < 0 || n2 < 0 || n_prev < 0 || (n1 > 0 && !matches_12)) return PLVI_E_BADARG;
     if (n1 > 0 && n2 < 2) return PLVI_E_BADARG;  // reference reads matches_[idx][1]
     std::vector<int> i0(n1), d0(n1), i1(n1), d1(n1);
     int rc = plvi::knn2_host(desc1, n1, desc2, n2, i0.data(), d0.data(), i1.data(), d1.data());
     if (rc) return rc;
+    for (int i = n_prev; i < n1; ++i) matches_12[i] = -1;
     int matches = 0;
     for (int i = 0; i < n1; ++i) {
         // DMatch::distance is float: (float)d0 < (float)d1 * nnr
         if ((float)d0[i] < (float)d1[i] * nnr) {
             matches_12[i] = i0[i];
             ++matches;
-        } else {
-            matches_12[i] = -1;
         }
     }
     return matches;
 }
 
-// LineMatcher::match(desc1, desc2, nnr, matches_12) (LineMatcher.cpp:92-111).
-extern "C" int plvi_line_match(const uint8_t* desc1, int n1, const uint8_t* desc2, int n2, float nnr,
-                               int* matches_12) {
-    if (n1 < 0 || n2 < 0 || !matches_12) return PLVI_E_BADARG;
+extern "C" int plvi_line_match_nnr(const uint8_t* desc1, int n1, const uint8_t* desc2, int n2, float nnr,
+                                   int* matches_12) {
+    return plvi_line_match_nnr_inout(desc1, n1, desc2, n2, nnr, matches_12, 0);
+}
+
+// LineMatcher::match(desc1, desc2, nnr, matches_12) (LineMatcher.cpp:92-111):
+// matches_21 is a fresh vector; matches_12 keeps the caller's entries.
+extern "C" int plvi_line_match_inout(const uint8_t* desc1, int n1, const uint8_t* desc2, int n2, float nnr,
+                                     int* matches_12, int n_prev) {
+    if (n1 < 0 || n2 < 0 || n_prev < 0 || (n1 > 0 && !matches_12)) return PLVI_E_BADARG;
     std::vector<int> m21(n2 > 0 ? n2 : 1);
-    int matches = plvi_line_match_nnr(desc1, n1, desc2, n2, nnr, matches_12);
+    std::vector<int> keep(matches_12, matches_12 + std::min(n_prev, n1));
+    int matches = plvi_line_match_nnr_inout(desc1, n1, desc2, n2, nnr, matches_12, n_prev);
     if (matches < 0) return matches;
     int rc = plvi_line_match_nnr(desc2, n2, desc1, n1, nnr, m21.data());
     if (rc < 0) return rc;
+    for (int i1 = 0; i1 < n1; ++i1)
+        if (matches_12[i1] >= n2) {  // stale entry beyond desc2: undefined in the reference
+            std::copy(keep.begin(), keep.end(), matches_12);
+            return PLVI_E_BADARG;
+        }
     for (int i1 = 0; i1 < n1; ++i1) {
         int& i2 = matches_12[i1];
         if (i2 >= 0 && m21[i2] != i1) {
@@ -239,6 +253,11 @@ extern "C" int plvi_line_match(const uint8_t* desc1, int n1, const uint8_t* desc
         }
     }
     return matches;
+}
+
+extern "C" int plvi_line_match(const uint8_t* desc1, int n1, const uint8_t* desc2, int n2, float nnr,
+                               int* matches_12) {
+    return plvi_line_match_inout(desc1, n1, desc2, n2, nnr, matches_12, 0);
 }
 
 // ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:2350-2366, per-word

@@ -15,68 +15,6 @@
 
 namespace plvi {
 
-// ---------------------------------------------------------------------------
-// K1: one pyramid level.  Fused: bilinear resize from level l-1 (or copy of
-// the input at l=0), 7x7 fixed-point Gaussian blur (reflect-101), FAST-9/16
-// score map.  64x32 output tile + 3-px halo staged in LDS.
-//   resize  : cv::resize INTER_LINEAR 8U (ORBextractor.cc:1165),
-//             separable in the tile: the source patch is staged once
-//             (coalesced rows), the horizontal pass runs per (source row,
-//             tile column), the vertical pass per tile pixel
-//   blur    : GaussianBlur(7x7, 2) fixed point, taps k0..k3 (ORBextractor.cc:1115; A.4)
-//   score   : cornerScore<16> closed form S-1 if S >= max(tmin+1, 1) else 0 (A.3).
-//             S >= T needs a 9-arc with every |d| >= T on one side, and any
-//             9-arc of the 16-circle holds two neighbouring compass points
-//             (offsets 0, 4, 8, 12): pixels failing that exact pre-test score 0;
-//             the survivors (~10 %) are compacted per tile and scored by all
-//             lanes.
-// ---------------------------------------------------------------------------
-constexpr int kTW = 64, kTH = 32, kEW = kTW + 6, kEH = kTH + 6;
-constexpr int kPR = 52, kPC = 96;  // staged source patch (scale factor <= ~1.33)
-
-__device__ __forceinline__ int fast_S(const uint8_t (*e)[kEW + 2], int cx, int cy) {
-    // circle offsets (x,y) of cv::FAST makeOffsets(16)
-    const int v = e[cy][cx];
-    int d[16];
-    d[0] = v - e[cy + 3][cx + 0];
-    d[1] = v - e[cy + 3][cx + 1];
-    d[2] = v - e[cy + 2][cx + 2];
-    d[3] = v - e[cy + 1][cx + 3];
-    d[4] = v - e[cy + 0][cx + 3];
-    d[5] = v - e[cy - 1][cx + 3];
-    d[6] = v - e[cy - 2][cx + 2];
-    d[7] = v - e[cy - 3][cx + 1];
-    d[8] = v - e[cy - 3][cx + 0];
-    d[9] = v - e[cy - 3][cx - 1];
-    d[10] = v - e[cy - 2][cx - 2];
-    d[11] = v - e[cy - 1][cx - 3];
-    d[12] = v - e[cy + 0][cx - 3];
-    d[13] = v - e[cy + 1][cx - 3];
-    d[14] = v - e[cy + 2][cx - 2];
-    d[15] = v - e[cy + 3][cx - 1];
-    int mn1[16], mx1[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        mn1[k] = min(d[k], d[(k + 1) & 15]);
-        mx1[k] = max(d[k], d[(k + 1) & 15]);
-    }
-    int mn2[16], mx2[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        mn2[k] = min(mn1[k], mn1[(k + 2) & 15]);
-        mx2[k] = max(mx1[k], mx1[(k + 2) & 15]);
-    }
-    int A = -1000, Bm = 1000;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        int mn8 = min(mn2[k], mn2[(k + 4) & 15]);
-        int mx8 = max(mx2[k], mx2[(k + 4) & 15]);
-        A = max(A, min(mn8, d[(k + 8) & 15]));
-        Bm = min(Bm, max(mx8, d[(k + 8) & 15]));
-    }
-    return max(A, -Bm);
-}
-
 // reflect-101 for an overshoot of at most len-1 (tile halos are 3 px)
 __device__ __forceinline__ int reflect1(int p, int len) {
     p = p < 0 ? -p : p;
@@ -84,173 +22,6 @@ __device__ __forceinline__ int reflect1(int p, int len) {
     return max(p, 0);
 }
 
-// Exact pre-test for S >= T (see K1 header).
-__device__ __forceinline__ bool fast_compass(const uint8_t (*e)[kEW + 2], int cx, int cy, int T) {
-    const int v = e[cy][cx];
-    const int d0 = v - e[cy + 3][cx], d4 = v - e[cy][cx + 3], d8 = v - e[cy - 3][cx], d12 = v - e[cy][cx - 3];
-    const bool p0 = d0 >= T, p4 = d4 >= T, p8 = d8 >= T, p12 = d12 >= T;
-    const bool n0 = d0 <= -T, n4 = d4 <= -T, n8 = d8 <= -T, n12 = d12 <= -T;
-    return (p0 & p4) | (p4 & p8) | (p8 & p12) | (p12 & p0) | (n0 & n4) | (n4 & n8) | (n8 & n12) | (n12 & n0);
-}
-
-template <bool RESIZE>
-__global__ __launch_bounds__(256) void orb_level_kernel(
-    const uint8_t* __restrict__ src, size_t s_frame, size_t s_row, uint8_t* __restrict__ dst,
-    uint8_t* __restrict__ blur, uint8_t* __restrict__ score, int w, int h, size_t d_frame,
-    const int* __restrict__ xofs, const short* __restrict__ xa, int xmax, const int* __restrict__ yrow,
-    const short* __restrict__ yb, int k0, int k1, int k2, int k3, int tmin, int sw, int sh) {
-    __shared__ uint8_t ext[kEH][kEW + 2];
-    __shared__ union {
-        struct {
-            uint8_t patch[kPR][kPC];
-            int hrow[kPR][kEW];
-        } rs;
-        int hs[kEH][kTW];
-    } u;
-    __shared__ int c_xo[kEW], c_a0[kEW], c_a1[kEW], c_r0[kEH], c_r1[kEH], c_b0[kEH], c_b1[kEH];
-    __shared__ uint8_t s_sc[kTH][kTW];
-    __shared__ unsigned short s_list[kTH * kTW];
-    __shared__ int s_n;
-    const int f = blockIdx.z, tid = threadIdx.x;
-    const int tx0 = blockIdx.x * kTW, ty0 = blockIdx.y * kTH;
-    const uint8_t* S = src + (size_t)f * s_frame;
-    if (tid == 0) s_n = 0;
-    if (RESIZE) {
-        // source patch bounds: xofs / yrow are monotone in the destination coordinate
-        const int gxl = max(tx0 - 3, 0), gxh = min(tx0 + kEW - 4, w - 1);
-        const int gyl = max(ty0 - 3, 0), gyh = min(ty0 + kEH - 4, h - 1);
-        const int sx0 = xofs[gxl], sx1 = min(xofs[gxh] + 1, sw - 1);
-        const int sy0 = yrow[2 * gyl], sy1 = yrow[2 * gyh + 1];
-        const int PC = sx1 - sx0 + 1, PR = sy1 - sy0 + 1;
-        if (PC <= kPC && PR <= kPR) {
-            for (int i = tid; i < kEW; i += 256) {
-                const int gx = reflect1(tx0 + i - 3, w);
-                c_xo[i] = xofs[gx] - sx0;
-                c_a0[i] = gx < xmax ? xa[2 * gx] : 2048;
-                c_a1[i] = gx < xmax ? xa[2 * gx + 1] : 0;
-            }
-            for (int i = tid; i < kEH; i += 256) {
-                const int gy = reflect1(ty0 + i - 3, h);
-                c_r0[i] = yrow[2 * gy] - sy0;
-                c_r1[i] = yrow[2 * gy + 1] - sy0;
-                c_b0[i] = yb[2 * gy];
-                c_b1[i] = yb[2 * gy + 1];
-            }
-            // all loads of a thread in flight at once (one wait, not one per element)
-            constexpr int kPL = (kPR * kPC + 255) / 256;
-            uint8_t pv[kPL];
-#pragma unroll
-            for (int k = 0; k < kPL; ++k) {
-                const int i = tid + 256 * k;
-                const int r = i / PC, c = i - r * PC;
-                pv[k] = i < PR * PC ? S[(size_t)(sy0 + r) * s_row + sx0 + c] : 0;
-            }
-#pragma unroll
-            for (int k = 0; k < kPL; ++k) {
-                const int i = tid + 256 * k;
-                const int r = i / PC, c = i - r * PC;
-                if (i < PR * PC) u.rs.patch[r][c] = pv[k];
-            }
-            __syncthreads();
-            // horizontal pass: right-clamped columns (gx >= xmax) use S[sx]*2048
-            // (a1 = 0 and S[sx+1] stays inside the patch row or is unused)
-            for (int i = tid; i < PR * kEW; i += 256) {
-                const int r = i / kEW, c = i - r * kEW;
-                const int sx = c_xo[c];
-                const int a1 = c_a1[c];
-                u.rs.hrow[r][c] = u.rs.patch[r][sx] * c_a0[c] + (a1 ? u.rs.patch[r][sx + 1] * a1 : 0);
-            }
-            __syncthreads();
-            for (int i = tid; i < kEW * kEH; i += 256) {
-                const int ey = i / kEW, ex = i - ey * kEW;
-                const int H0 = u.rs.hrow[c_r0[ey]][ex], H1 = u.rs.hrow[c_r1[ey]][ex];
-                ext[ey][ex] = (uint8_t)((((c_b0[ey] * (H0 >> 4)) >> 16) + ((c_b1[ey] * (H1 >> 4)) >> 16) + 2) >> 2);
-            }
-        } else {
-            for (int i = tid; i < kEW * kEH; i += 256) {
-                const int ex = i % kEW, ey = i / kEW;
-                const int gx = reflect101(tx0 + ex - 3, w), gy = reflect101(ty0 + ey - 3, h);
-                const uint8_t* R0 = S + (size_t)yrow[2 * gy] * s_row;
-                const uint8_t* R1 = S + (size_t)yrow[2 * gy + 1] * s_row;
-                const int b0 = yb[2 * gy], b1 = yb[2 * gy + 1];
-                const int sx = xofs[gx];
-                int H0, H1;
-                if (gx < xmax) {
-                    const int a0 = xa[2 * gx], a1 = xa[2 * gx + 1];
-                    H0 = R0[sx] * a0 + R0[sx + 1] * a1;
-                    H1 = R1[sx] * a0 + R1[sx + 1] * a1;
-                } else {
-                    H0 = R0[sx] * 2048;
-                    H1 = R1[sx] * 2048;
-                }
-                ext[ey][ex] = (uint8_t)((((b0 * (H0 >> 4)) >> 16) + ((b1 * (H1 >> 4)) >> 16) + 2) >> 2);
-            }
-        }
-    } else {
-        constexpr int kXL = (kEW * kEH + 255) / 256;
-        uint8_t xv[kXL];
-#pragma unroll
-        for (int k = 0; k < kXL; ++k) {
-            const int i = tid + 256 * k;
-            const int ey = i / kEW, ex = i - ey * kEW;
-            const int gx = reflect1(tx0 + ex - 3, w), gy = reflect1(ty0 + ey - 3, h);
-            xv[k] = i < kEW * kEH ? S[(size_t)gy * s_row + gx] : 0;
-        }
-#pragma unroll
-        for (int k = 0; k < kXL; ++k) {
-            const int i = tid + 256 * k;
-            const int ey = i / kEW, ex = i - ey * kEW;
-            if (i < kEW * kEH) ext[ey][ex] = xv[k];
-        }
-    }
-    __syncthreads();
-    for (int i = tid; i < kEH * kTW; i += 256) {
-        const int ey = i / kTW, cx = i % kTW;
-        const uint8_t* e = ext[ey];
-        u.hs[ey][cx] = k0 * (e[cx] + e[cx + 6]) + k1 * (e[cx + 1] + e[cx + 5]) + k2 * (e[cx + 2] + e[cx + 4]) +
-                       k3 * e[cx + 3];
-    }
-    __syncthreads();
-    uint8_t* D = dst + (size_t)f * d_frame;
-    uint8_t* Bl = blur + (size_t)f * d_frame;
-    uint8_t* Sc = score + (size_t)f * d_frame;
-    const int T = max(tmin + 1, 1);
-    const int lane = tid & 63;
-    for (int i = tid; i < kTH * kTW; i += 256) {
-        const int cy = i / kTW, cx = i % kTW;  // cx == lane
-        const int x = tx0 + cx, y = ty0 + cy;
-        const bool in = x < w && y < h;
-        if (in) {
-            D[(size_t)y * w + x] = ext[cy + 3][cx + 3];
-            const unsigned s = (unsigned)(k0 * (u.hs[cy][cx] + u.hs[cy + 6][cx]) +
-                                          k1 * (u.hs[cy + 1][cx] + u.hs[cy + 5][cx]) +
-                                          k2 * (u.hs[cy + 2][cx] + u.hs[cy + 4][cx]) + k3 * u.hs[cy + 3][cx]);
-            Bl[(size_t)y * w + x] = (uint8_t)min((s + 32768u) >> 16, 255u);
-        }
-        s_sc[cy][cx] = 0;
-        const bool cand = in && x >= 3 && x < w - 3 && y >= 3 && y < h - 3 && fast_compass(ext, cx + 3, cy + 3, T);
-        const unsigned long long m = __ballot(cand);
-        if (m) {
-            int base = 0;
-            if (lane == 0) base = atomicAdd(&s_n, __popcll(m));
-            base = __shfl(base, 0);
-            if (cand) s_list[base + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned short)((cy << 8) | cx);
-        }
-    }
-    __syncthreads();
-    const int nc = s_n;
-    for (int k = tid; k < nc; k += 256) {
-        const int cy = s_list[k] >> 8, cx = s_list[k] & 0xff;
-        const int Sv = fast_S(ext, cx + 3, cy + 3);
-        s_sc[cy][cx] = (uint8_t)(Sv >= T ? Sv - 1 : 0);
-    }
-    __syncthreads();
-    for (int i = tid; i < kTH * kTW; i += 256) {
-        const int cy = i / kTW, cx = i % kTW;
-        const int x = tx0 + cx, y = ty0 + cy;
-        if (x < w && y < h) Sc[(size_t)y * w + x] = s_sc[cy][cx];
-    }
-}
 
 // ---------------------------------------------------------------------------
 // K1a: level l >= 1 of the pyramid: cv::resize INTER_LINEAR 8U of level l-1
@@ -261,7 +32,8 @@ __global__ __launch_bounds__(256) void orb_resize_kernel(const uint8_t* __restri
                                                          size_t s_row, uint8_t* __restrict__ dst, int w, int h,
                                                          size_t d_frame, const int* __restrict__ xofs,
                                                          const short* __restrict__ xa, int xmax,
-                                                         const int* __restrict__ yrow, const short* __restrict__ yb) {
+                                                         const int* __restrict__ yrow, const short* __restrict__ yb,
+                                                         int generic) {
     const int f = blockIdx.z;
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int y = __builtin_amdgcn_readfirstlane(blockIdx.y * 4 + (threadIdx.x >> 6));
@@ -281,8 +53,10 @@ __global__ __launch_bounds__(256) void orb_resize_kernel(const uint8_t* __restri
         H0 = R0[sx] * 2048;
         H1 = R1[sx] * 2048;
     }
-    dst[(size_t)f * d_frame + (size_t)y * w + x] =
-        (uint8_t)((((b0 * (H0 >> 4)) >> 16) + ((b1 * (H1 >> 4)) >> 16) + 2) >> 2);
+    // 8U specialisation (default) or the generic fixed-point cast (A.1 switch)
+    const int v = generic ? min((b0 * H0 + b1 * H1 + (1 << 21)) >> 22, 255)
+                          : ((((b0 * (H0 >> 4)) >> 16) + ((b1 * (H1 >> 4)) >> 16) + 2) >> 2);
+    dst[(size_t)f * d_frame + (size_t)y * w + x] = (uint8_t)v;
 }
 
 // ---------------------------------------------------------------------------
@@ -797,7 +571,7 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
     }
     if (lane == 0) {
         out_cnt[(size_t)f * L + l] = overflow ? 0 : cntOut;
-        if (overflow) atomicOr(err, 1);
+        if (overflow) atomicOr(err + f, 1);
     }
 }
 

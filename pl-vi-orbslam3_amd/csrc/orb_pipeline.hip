@@ -72,6 +72,7 @@ struct OrbPipeline {
     std::vector<OrbStripDev> strips;
     std::vector<ResizeTab> rtab;
     int taps[7]{};
+    int resizeGeneric = 0;  // A.1 vertical-pass switch (PLVI_COMPAT_RESIZE_V_GENERIC)
     int kpCapFrame = 0, nodeCapMax = 0;
     size_t pyrBytesFrameTotal = 0, satIntsFrameTotal = 0;
     size_t lvOff0 = 0;  // (unused)
@@ -185,9 +186,11 @@ struct OrbPipeline {
                 ++v0;
             }
         }
-        // 7x7 sigma=2 fixed-point taps (error-diffused): [18,34,48,56,48,34,18]
-        const int t7[7] = {18, 34, 48, 56, 48, 34, 18};
-        std::memcpy(taps, t7, sizeof(taps));
+        // 7x7 sigma=2 fixed-point taps: error-diffused
+        // [18,34,48,56,48,34,18] (default) or plainly rounded [18,34,49,55,...]
+        const int t7ed[7] = {18, 34, 48, 56, 48, 34, 18}, t7r[7] = {18, 34, 49, 55, 49, 34, 18};
+        std::memcpy(taps, (p->compat & PLVI_COMPAT_GAUSS_ROUNDED) ? t7r : t7ed, sizeof(taps));
+        resizeGeneric = (p->compat & PLVI_COMPAT_RESIZE_V_GENERIC) ? 1 : 0;
         // Levels
         lv.resize(L);
         rtab.resize(L);
@@ -302,9 +305,9 @@ struct OrbPipeline {
             rectCnt.alloc(sizeof(int) * L * Bcap) || lvkp.alloc(sizeof(float4) * (size_t)kpCapFrame * Bcap) ||
             lvdesc.alloc((size_t)32 * kpCapFrame * Bcap) || okp.alloc(sizeof(plvi_keypoint) * (size_t)kpCapFrame * Bcap) ||
             odesc.alloc((size_t)32 * kpCapFrame * Bcap) || ocount.alloc(sizeof(int) * Bcap) ||
-            omono.alloc(sizeof(int) * Bcap) || err.alloc(sizeof(int)) || staging.alloc((size_t)W * H))
+            omono.alloc(sizeof(int) * Bcap) || err.alloc(sizeof(int) * Bcap) || staging.alloc((size_t)W * H))
             return PLVI_E_HIP;
-        PLVI_CHECK(hipMemset(err.p, 0, sizeof(int)));
+        PLVI_CHECK(hipMemset(err.p, 0, sizeof(int) * Bcap));
         return PLVI_OK;
     }
 
@@ -332,7 +335,7 @@ struct OrbPipeline {
             const size_t sf = l == 1 ? frame_stride : (size_t)s.plane, sr = l == 1 ? row_stride : (size_t)s.w;
             hipLaunchKernelGGL(orb_resize_kernel, grid, dim3(256), 0, st, sp, sf, sr, P + d.off, d.w, d.h,
                                (size_t)d.plane, (const int*)(T + tabXofs[l]), (const short*)(T + tabXa[l]),
-                               rtab[l].xmax, (const int*)(T + tabYrow[l]), (const short*)(T + tabYb[l]));
+                               rtab[l].xmax, (const int*)(T + tabYrow[l]), (const short*)(T + tabYb[l]), resizeGeneric);
         }
         // K1b: blur + FAST score of every level (level 0 also copies the frame into its plane)
         const bool kt = ktime && kn < kKRing;
@@ -392,16 +395,45 @@ struct OrbPipeline {
 
 using plvi::OrbPipeline;
 
+// The handle owns its pipeline by pointer: ORBextractor::operator() takes
+// frames of any size (ORBextractor.cc:1152-1160), so a size change builds a
+// new plan for it (geometry, tables, buffers) and retires the old one.
 struct plvi_orb_extractor {
-    OrbPipeline p;
+    std::unique_ptr<OrbPipeline> up;
+    OrbPipeline& p() { return *up; }
+    int replan(int width, int height) {
+        if (width == up->W && height == up->H) return PLVI_OK;
+        PLVI_CHECK(hipStreamSynchronize(up->stream));
+        auto np = std::make_unique<OrbPipeline>();
+        int rc = np->init(&up->prm, width, height, up->Bcap, up->device);
+        if (rc) return rc;
+        up = std::move(np);
+        return PLVI_OK;
+    }
 };
+
+// Read and clear per-frame device error flags (shared by both extractors).
+int plvi::read_frame_errors(int* d_err, int nslots, int* frame_flags, int* any, hipStream_t st) {
+    std::vector<int> f((size_t)nslots);
+    PLVI_CHECK(hipMemcpyAsync(f.data(), d_err, sizeof(int) * nslots, hipMemcpyDeviceToHost, st));
+    PLVI_CHECK(hipMemsetAsync(d_err, 0, sizeof(int) * nslots, st));
+    PLVI_CHECK(hipStreamSynchronize(st));
+    int a = 0;
+    for (int i = 0; i < nslots; ++i) {
+        a |= f[i];
+        if (frame_flags) frame_flags[i] = f[i];
+    }
+    if (any) *any = a;
+    return PLVI_OK;
+}
 
 extern "C" int plvi_orb_create(const plvi_orb_params* p, int width, int height, int max_batch, int device,
                                plvi_orb_extractor** out) {
     if (!out) return PLVI_E_BADARG;
     *out = nullptr;
     auto h = std::make_unique<plvi_orb_extractor>();
-    int rc = h->p.init(p, width, height, max_batch, device);
+    h->up = std::make_unique<OrbPipeline>();
+    int rc = h->p().init(p, width, height, max_batch, device);
     if (rc) return rc;
     *out = h.release();
     return PLVI_OK;
@@ -409,8 +441,8 @@ extern "C" int plvi_orb_create(const plvi_orb_params* p, int width, int height, 
 
 extern "C" int plvi_orb_destroy(plvi_orb_extractor* h) {
     if (!h) return PLVI_E_BADARG;
-    (void)hipSetDevice(h->p.device);
-    (void)hipStreamSynchronize(h->p.stream);
+    (void)hipSetDevice(h->p().device);
+    (void)hipStreamSynchronize(h->p().stream);
     delete h;
     return PLVI_OK;
 }
@@ -418,18 +450,25 @@ extern "C" int plvi_orb_destroy(plvi_orb_extractor* h) {
 extern "C" int plvi_orb_extract_batch(plvi_orb_extractor* h, const uint8_t* d_frames, int n_frames,
                                       size_t frame_stride, size_t row_stride, int lap0, int lap1, void* stream) {
     if (!h || !d_frames) return PLVI_E_BADARG;
-    PLVI_CHECK(hipSetDevice(h->p.device));
-    return h->p.run(d_frames, n_frames, frame_stride, row_stride, lap0, lap1, (hipStream_t)stream);
+    PLVI_CHECK(hipSetDevice(h->p().device));
+    return h->p().run(d_frames, n_frames, frame_stride, row_stride, lap0, lap1, (hipStream_t)stream);
+}
+
+extern "C" int plvi_orb_errors(plvi_orb_extractor* h, int* frame_flags, int* any, void* stream) {
+    if (!h) return PLVI_E_BADARG;
+    PLVI_CHECK(hipSetDevice(h->p().device));
+    hipStream_t st = stream ? (hipStream_t)stream : h->p().stream;
+    return plvi::read_frame_errors(h->p().err.as<int>(), h->p().Bcap, frame_flags, any, st);
 }
 
 extern "C" int plvi_orb_outputs(plvi_orb_extractor* h, plvi_keypoint** d_kps, uint8_t** d_desc, int** d_count,
                                 int** d_mono, int* cap) {
     if (!h) return PLVI_E_BADARG;
-    if (d_kps) *d_kps = h->p.okp.as<plvi_keypoint>();
-    if (d_desc) *d_desc = h->p.odesc.as<uint8_t>();
-    if (d_count) *d_count = h->p.ocount.as<int>();
-    if (d_mono) *d_mono = h->p.omono.as<int>();
-    if (cap) *cap = h->p.kpCapFrame;
+    if (d_kps) *d_kps = h->p().okp.as<plvi_keypoint>();
+    if (d_desc) *d_desc = h->p().odesc.as<uint8_t>();
+    if (d_count) *d_count = h->p().ocount.as<int>();
+    if (d_mono) *d_mono = h->p().omono.as<int>();
+    if (cap) *cap = h->p().kpCapFrame;
     return PLVI_OK;
 }
 
@@ -439,9 +478,9 @@ extern "C" int plvi_orb_extract(plvi_orb_extractor* h, const uint8_t* img, int w
     if (!h) return PLVI_E_BADARG;
     if (n) *n = 0;
     if (!img || width <= 0 || height <= 0) return PLVI_E_EMPTY;  // _image.empty() -> -1
-    OrbPipeline& P = h->p;
-    if (width != P.W || height != P.H) return PLVI_E_BADARG;
-    PLVI_CHECK(hipSetDevice(P.device));
+    PLVI_CHECK(hipSetDevice(h->p().device));
+    if (int rc = h->replan(width, height)) return rc;
+    OrbPipeline& P = h->p();
     PLVI_CHECK(hipMemcpy2DAsync(P.staging.p, (size_t)P.W, img, stride, (size_t)P.W, (size_t)P.H,
                                 hipMemcpyHostToDevice, P.stream));
     int rc = P.run(P.staging.as<uint8_t>(), 1, (size_t)P.W * P.H, (size_t)P.W, lap0, lap1, P.stream);
@@ -452,7 +491,7 @@ extern "C" int plvi_orb_extract(plvi_orb_extractor* h, const uint8_t* img, int w
     PLVI_CHECK(hipMemcpyAsync(&errv, P.err.p, sizeof(int), hipMemcpyDeviceToHost, P.stream));
     PLVI_CHECK(hipStreamSynchronize(P.stream));
     if (errv) {
-        PLVI_CHECK(hipMemset(P.err.p, 0, sizeof(int)));
+        PLVI_CHECK(hipMemset(P.err.p, 0, sizeof(int) * P.Bcap));
         return PLVI_E_OVERFLOW;
     }
     if (n) *n = cnt;
@@ -466,25 +505,25 @@ extern "C" int plvi_orb_extract(plvi_orb_extractor* h, const uint8_t* img, int w
 }
 
 extern "C" int plvi_orb_pyramid_level(plvi_orb_extractor* h, int frame, int level, uint8_t* dst, int* w, int* hgt) {
-    if (!h || level < 0 || level >= h->p.L || frame < 0 || frame >= h->p.Bcap) return PLVI_E_BADARG;
-    const auto& d = h->p.lv[level];
+    if (!h || level < 0 || level >= h->p().L || frame < 0 || frame >= h->p().Bcap) return PLVI_E_BADARG;
+    const auto& d = h->p().lv[level];
     if (w) *w = d.w;
     if (hgt) *hgt = d.h;
     if (!dst) return PLVI_OK;
-    PLVI_CHECK(hipSetDevice(h->p.device));
-    PLVI_CHECK(hipStreamSynchronize(h->p.stream));
-    PLVI_CHECK(hipMemcpy(dst, h->p.pyr.as<uint8_t>() + d.off + (size_t)frame * d.plane, (size_t)d.plane,
+    PLVI_CHECK(hipSetDevice(h->p().device));
+    PLVI_CHECK(hipStreamSynchronize(h->p().stream));
+    PLVI_CHECK(hipMemcpy(dst, h->p().pyr.as<uint8_t>() + d.off + (size_t)frame * d.plane, (size_t)d.plane,
                          hipMemcpyDeviceToHost));
     return PLVI_OK;
 }
 
 extern "C" int plvi_orb_pyramid_device(plvi_orb_extractor* h, int level, const uint8_t** d_frame0,
                                        size_t* frame_stride, int* w, int* hgt, int* nlevels) {
-    if (!h || level < -1 || level >= h->p.L) return PLVI_E_BADARG;
-    if (nlevels) *nlevels = h->p.L;
+    if (!h || level < -1 || level >= h->p().L) return PLVI_E_BADARG;
+    if (nlevels) *nlevels = h->p().L;
     if (level < 0) return PLVI_OK;
-    const auto& d = h->p.lv[level];
-    if (d_frame0) *d_frame0 = h->p.pyr.as<uint8_t>() + d.off;
+    const auto& d = h->p().lv[level];
+    if (d_frame0) *d_frame0 = h->p().pyr.as<uint8_t>() + d.off;
     if (frame_stride) *frame_stride = (size_t)d.plane;
     if (w) *w = d.w;
     if (hgt) *hgt = d.h;
@@ -494,7 +533,7 @@ extern "C" int plvi_orb_pyramid_device(plvi_orb_extractor* h, int level, const u
 extern "C" int plvi_orb_scale_tables(plvi_orb_extractor* h, float* scale, float* inv_scale, float* sigma2,
                                      float* inv_sigma2) {
     if (!h) return PLVI_E_BADARG;
-    const auto& P = h->p;
+    const auto& P = h->p();
     for (int i = 0; i < P.L; ++i) {
         if (scale) scale[i] = P.scale[i];
         if (inv_scale) inv_scale[i] = P.invScale[i];
@@ -506,30 +545,30 @@ extern "C" int plvi_orb_scale_tables(plvi_orb_extractor* h, float* scale, float*
 
 extern "C" int plvi_orb_level_quota(plvi_orb_extractor* h, int* q) {
     if (!h || !q) return PLVI_E_BADARG;
-    for (int i = 0; i < h->p.L; ++i) q[i] = h->p.quota[i];
+    for (int i = 0; i < h->p().L; ++i) q[i] = h->p().quota[i];
     return PLVI_OK;
 }
 
 extern "C" int plvi_orb_profile(plvi_orb_extractor* h, int enable) {
     if (!h) return PLVI_E_BADARG;
-    PLVI_CHECK(hipSetDevice(h->p.device));
-    return h->p.profile(enable);
+    PLVI_CHECK(hipSetDevice(h->p().device));
+    return h->p().profile(enable);
 }
 
 extern "C" int plvi_orb_profile_read(plvi_orb_extractor* h, float* stage_ms, int* runs) {
     if (!h || !stage_ms) return PLVI_E_BADARG;
-    PLVI_CHECK(hipSetDevice(h->p.device));
-    return h->p.profile_read(stage_ms, runs);
+    PLVI_CHECK(hipSetDevice(h->p().device));
+    return h->p().profile_read(stage_ms, runs);
 }
 
 extern "C" int plvi_orb_kernel_timing(plvi_orb_extractor* h, int enable) {
     if (!h) return PLVI_E_BADARG;
-    PLVI_CHECK(hipSetDevice(h->p.device));
-    return h->p.ktiming(enable);
+    PLVI_CHECK(hipSetDevice(h->p().device));
+    return h->p().ktiming(enable);
 }
 
 extern "C" int plvi_orb_kernel_timing_read(plvi_orb_extractor* h, float* total_ms, int* launches) {
     if (!h) return PLVI_E_BADARG;
-    PLVI_CHECK(hipSetDevice(h->p.device));
-    return h->p.ktiming_read(total_ms, launches);
+    PLVI_CHECK(hipSetDevice(h->p().device));
+    return h->p().ktiming_read(total_ms, launches);
 }

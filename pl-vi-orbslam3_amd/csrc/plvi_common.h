@@ -70,4 +70,7 @@ struct DevBuf {
     T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+// Read and clear a pipeline's per-frame device error flags (orb_pipeline.hip).
+int read_frame_errors(int* d_err, int nslots, int* frame_flags, int* any, hipStream_t st);
+
 }  // namespace plvi

@@ -33,6 +33,11 @@ PLVI_E_HIP = -4
 PLVI_E_OVERFLOW = -5
 PLVI_E_SIZE = -6
 
+# OpenCV-semantics switches (plvi_frontend.h PLVI_COMPAT_*)
+COMPAT_GAUSS_ROUNDED = 1
+COMPAT_RESIZE_V_GENERIC = 2
+COMPAT_EXP_CV_TABLE = 4
+
 KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
                            ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
 KEYLINE_DTYPE = np.dtype([("angle", "<f4"), ("class_id", "<i4"), ("octave", "<i4"), ("pt_x", "<f4"),
@@ -108,12 +113,13 @@ def grid_geometry(width, height):
 
 class OrbParams(ctypes.Structure):
     _fields_ = [("nfeatures", ctypes.c_int), ("scale_factor", ctypes.c_float), ("nlevels", ctypes.c_int),
-                ("ini_th_fast", ctypes.c_int), ("min_th_fast", ctypes.c_int)]
+                ("ini_th_fast", ctypes.c_int), ("min_th_fast", ctypes.c_int), ("compat", ctypes.c_uint)]
 
 
 class LineParams(ctypes.Structure):
     _fields_ = [("nfeatures", ctypes.c_int), ("refine", ctypes.c_int), ("lsd_scale", ctypes.c_float),
-                ("nlevels", ctypes.c_int), ("scale", ctypes.c_float), ("extractor", ctypes.c_int)]
+                ("nlevels", ctypes.c_int), ("scale", ctypes.c_float), ("extractor", ctypes.c_int),
+                ("compat", ctypes.c_uint)]
 
 
 _lib = None
@@ -132,6 +138,12 @@ def _declare(lib):
         "plvi_orb_extract": ([V, V, I, I, S, I, I, V, V, I, P, P], I),
         "plvi_orb_extract_batch": ([V, V, I, S, S, I, I, V], I),
         "plvi_orb_outputs": ([V, c_void_pp, c_void_pp, c_void_pp, c_void_pp, P], I),
+        "plvi_orb_errors": ([V, V, P, V], I),
+        "plvi_lines_errors": ([V, V, P, V], I),
+        "plvi_lines_kernel_timing": ([V, I], I),
+        "plvi_lines_kernel_timing_read": ([V, V, P], I),
+        "plvi_line_match_nnr_inout": ([V, I, V, I, F, V, I], I),
+        "plvi_line_match_inout": ([V, I, V, I, F, V, I], I),
         "plvi_orb_pyramid_level": ([V, I, I, V, P, P], I),
         "plvi_orb_pyramid_device": ([V, I, c_void_pp, ctypes.POINTER(S), P, P, P], I),
         "plvi_orb_scale_tables": ([V, V, V, V, V], I),
@@ -264,9 +276,9 @@ class ORBextractor:
     """
 
     def __init__(self, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, width=640, height=480,
-                 max_batch=1, device=0):
+                 max_batch=1, device=0, compat=0):
         self._lib = load()
-        self.params = OrbParams(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)
+        self.params = OrbParams(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, compat)
         self.width, self.height, self.max_batch = width, height, max_batch
         self.nlevels = nlevels
         h = ctypes.c_void_p()
@@ -289,18 +301,39 @@ class ORBextractor:
             pass
 
     def __call__(self, image, mask=None, vLappingArea=(0, 0)):
-        if image is None or image.size == 0:
-            return -1, np.zeros(0, KEYPOINT_DTYPE), np.zeros((0, 32), np.uint8)
-        image = np.ascontiguousarray(image, dtype=np.uint8)
-        h, w = image.shape
+        """operator(): any frame size (a new size re-plans the handle); an
+        empty image returns (-1, empty, empty) from the C-ABI's PLVI_E_EMPTY."""
+        image = np.ascontiguousarray(image if image is not None else np.zeros((0, 0)), dtype=np.uint8)
+        h, w = image.shape if image.ndim == 2 else (0, 0)
+        if (w, h) != (self.width, self.height) and w > 0 and h > 0:
+            self.width, self.height = w, h
         kps = np.zeros(self.kp_cap, KEYPOINT_DTYPE)
         desc = np.zeros((self.kp_cap, 32), np.uint8)
         n, mono = ctypes.c_int(), ctypes.c_int()
-        rc = self._lib.plvi_orb_extract(self._h, _ptr(image), w, h, w, int(vLappingArea[0]),
-                                        int(vLappingArea[1]), _ptr(kps), _ptr(desc), self.kp_cap,
-                                        ctypes.byref(n), ctypes.byref(mono))
+        rc = self._lib.plvi_orb_extract(self._h, _ptr(image) if image.size else None, w, h, w,
+                                        int(vLappingArea[0]), int(vLappingArea[1]), _ptr(kps), _ptr(desc),
+                                        self.kp_cap, ctypes.byref(n), ctypes.byref(mono))
+        if rc == PLVI_E_EMPTY:
+            return -1, np.zeros(0, KEYPOINT_DTYPE), np.zeros((0, 32), np.uint8)
+        if rc == PLVI_E_CAPACITY:  # a re-planned (larger) frame: grow the host buffers once
+            self._refresh_cap()
+            return self(image, mask, vLappingArea)
         _check(rc, "plvi_orb_extract")
+        self._refresh_cap()
         return mono.value, kps[:n.value].copy(), desc[:n.value].copy()
+
+    def _refresh_cap(self):
+        cap = ctypes.c_int()
+        self._lib.plvi_orb_outputs(self._h, None, None, None, None, ctypes.byref(cap))
+        self.kp_cap = cap.value
+
+    def errors(self, stream=None, per_frame=False):
+        """Read-and-clear device error flags of the batches run so far (PLVI_FERR_*)."""
+        flags = np.zeros(self.max_batch, np.int32)
+        anyf = ctypes.c_int()
+        _check(self._lib.plvi_orb_errors(self._h, _ptr(flags), ctypes.byref(anyf), ctypes.c_void_p(stream or 0)),
+               "plvi_orb_errors")
+        return flags if per_frame else anyf.value
 
     # --- batched device path (bench / multi-frame) ---------------------------
     def extract_batch(self, d_frames_ptr, n_frames, frame_stride, row_stride, lap=(0, 0), stream=None):
@@ -401,9 +434,9 @@ class Lineextractor:
     STAGES = ("pyramid", "lsd_prep", "region_grow", "assemble", "lbd")
 
     def __init__(self, lsd_nfeatures, lsd_refine, lsd_scale, nlevels, scale, extractor=0, width=640, height=480,
-                 max_batch=1, device=0):
+                 max_batch=1, device=0, compat=0):
         self._lib = load()
-        self.params = LineParams(lsd_nfeatures, lsd_refine, lsd_scale, nlevels, scale, extractor)
+        self.params = LineParams(lsd_nfeatures, lsd_refine, lsd_scale, nlevels, scale, extractor, compat)
         self.width, self.height, self.max_batch, self.nlevels = width, height, max_batch, nlevels
         h = ctypes.c_void_p()
         _check(self._lib.plvi_lines_create(ctypes.byref(self.params), width, height, max_batch, device,
@@ -433,8 +466,17 @@ class Lineextractor:
         n = ctypes.c_int()
         _check(self._lib.plvi_lines_extract(self._h, _ptr(image), w, h, w, _ptr(kl), _ptr(desc), _ptr(fn), self.cap,
                                             ctypes.byref(n)), "plvi_lines_extract")
+        self.width, self.height = w, h
         k = n.value
         return kl[:k].copy(), desc[:k].copy(), fn[:k].copy()
+
+    def errors(self, stream=None, per_frame=False):
+        """Read-and-clear device error flags of the batches run so far (PLVI_FERR_*)."""
+        flags = np.zeros(self.max_batch, np.int32)
+        anyf = ctypes.c_int()
+        _check(self._lib.plvi_lines_errors(self._h, _ptr(flags), ctypes.byref(anyf), ctypes.c_void_p(stream or 0)),
+               "plvi_lines_errors")
+        return flags if per_frame else anyf.value
 
     def extract_batch(self, d_frames_ptr, n_frames, frame_stride, row_stride, stream=None):
         _check(self._lib.plvi_lines_extract_batch(self._h, ctypes.c_void_p(d_frames_ptr), n_frames, frame_stride,
@@ -456,6 +498,17 @@ class Lineextractor:
         runs = ctypes.c_int()
         _check(self._lib.plvi_lines_profile_read(self._h, _ptr(ms), ctypes.byref(runs)), "plvi_lines_profile_read")
         return dict(zip(self.STAGES, ms.tolist())), runs.value
+
+    def kernel_timing(self, enable=True):
+        """Event pair around every lsd_prep_kernel launch (LSD-pass roofline)."""
+        _check(self._lib.plvi_lines_kernel_timing(self._h, int(enable)), "plvi_lines_kernel_timing")
+
+    def kernel_timing_read(self):
+        tot = ctypes.c_float()
+        n = ctypes.c_int()
+        _check(self._lib.plvi_lines_kernel_timing_read(self._h, ctypes.byref(tot), ctypes.byref(n)),
+               "plvi_lines_kernel_timing_read")
+        return tot.value, n.value
 
     def pyramid_level(self, level, frame=0):
         w, h = ctypes.c_int(), ctypes.c_int()
@@ -499,24 +552,28 @@ class LineMatcher:
     """ORB_SLAM3::LineMatcher static Hamming matchers (src/LineMatcher.cpp)."""
 
     @staticmethod
-    def matchNNR(desc1, desc2, nnr):
-        lib = load()
-        d1 = np.ascontiguousarray(desc1, np.uint8)
-        d2 = np.ascontiguousarray(desc2, np.uint8)
-        m = np.full(d1.shape[0], -1, np.int32)
-        n = _check(lib.plvi_line_match_nnr(_ptr(d1), d1.shape[0], _ptr(d2), d2.shape[0], nnr, _ptr(m)),
-                   "plvi_line_match_nnr")
-        return n, m
+    def _inout(fn, name, desc1, desc2, nnr, matches_12):
+        d1 = np.ascontiguousarray(desc1, np.uint8).reshape(-1, 32)
+        d2 = np.ascontiguousarray(desc2, np.uint8).reshape(-1, 32)
+        prev = np.zeros(0, np.int32) if matches_12 is None else np.ascontiguousarray(matches_12, np.int32)
+        m = np.full(max(d1.shape[0], prev.size, 1), -1, np.int32)
+        m[:prev.size] = prev
+        n = _check(fn(_ptr(d1), d1.shape[0], _ptr(d2), d2.shape[0], nnr, _ptr(m), prev.size), name)
+        return n, m[:d1.shape[0]].copy()
 
     @staticmethod
-    def match(desc1, desc2, nnr):
+    def matchNNR(desc1, desc2, nnr, matches_12=None):
+        """LineMatcher::matchNNR (LineMatcher.cpp:41-61).  matches_12: the caller's
+        existing vector (kept through resize(rows, -1) like the reference), or None."""
         lib = load()
-        d1 = np.ascontiguousarray(desc1, np.uint8)
-        d2 = np.ascontiguousarray(desc2, np.uint8)
-        m = np.full(d1.shape[0], -1, np.int32)
-        n = _check(lib.plvi_line_match(_ptr(d1), d1.shape[0], _ptr(d2), d2.shape[0], nnr, _ptr(m)),
-                   "plvi_line_match")
-        return n, m
+        return LineMatcher._inout(lib.plvi_line_match_nnr_inout, "plvi_line_match_nnr_inout", desc1, desc2, nnr,
+                                  matches_12)
+
+    @staticmethod
+    def match(desc1, desc2, nnr, matches_12=None):
+        """LineMatcher::match(desc1, desc2, nnr, matches_12) (LineMatcher.cpp:92-111)."""
+        lib = load()
+        return LineMatcher._inout(lib.plvi_line_match_inout, "plvi_line_match_inout", desc1, desc2, nnr, matches_12)
 
     @staticmethod
     def matchGrid(lines1, desc1, grid, desc2, directions2, window=((7, 0), (2, 2)), range_hint=1):

@@ -122,6 +122,36 @@ def batch(n, w=640, h=480, seed0=0):
     return out
 
 
+def device_sequence(n, w=640, h=480, seed=0, device="cpu", run=48):
+    """n consecutive frames of a synthetic camera sequence, generated on
+    `device` (torch) into one contiguous (n, H, W) u8 tensor -- the bench's
+    input, so that thousands of frames per GPU need no host generation.
+
+    Runs of `run` frames share one clean scene (clean_frame(seed + k*run),
+    the numpy generator above); within a run frame t+1 is frame t shifted by
+    an integer (dx, dy) in [-3, 3]^2 (seeded, cumulative, np.roll wrap) plus
+    fresh Gaussian noise sigma 2 (torch generator seeded with `seed`),
+    round-half-even and clip to [0, 255] -- SURVEY 8(d)'s pair rule applied
+    along a sequence.  Deterministic for a given (n, w, h, seed, device type)."""
+    import torch
+    out = torch.empty((n, h, w), dtype=torch.uint8, device=device)
+    if n == 0:
+        return out
+    steps = np.random.default_rng(seed ^ 0x5EED5EED).integers(-3, 4, size=(n, 2))
+    g = torch.Generator(device=device)
+    g.manual_seed(int(seed) & 0x7FFFFFFFFFFFFFFF)
+    for k in range((n + run - 1) // run):
+        lo, hi = k * run, min(n, (k + 1) * run)
+        base = torch.from_numpy(clean_frame(seed + lo, w, h)[0]).to(device=device, dtype=torch.float32)
+        sh = np.cumsum(steps[lo:hi], axis=0)
+        sh -= sh[0]
+        noise = torch.randn((hi - lo, h, w), generator=g, device=device) * 2.0
+        for t in range(lo, hi):
+            img = torch.roll(base, shifts=(int(sh[t - lo, 1]), int(sh[t - lo, 0])), dims=(0, 1))
+            out[t] = torch.clamp(torch.round(img + noise[t - lo]), 0, 255).to(torch.uint8)
+    return out
+
+
 # ---------------------------------------------------------------- vocabulary
 # Seeded synthetic DBoW2 ORB vocabulary in the reference's node-table form
 # (the real Vocabulary/ORBvoc.txt is a missing blob; SURVEY §8f rank 1).

@@ -60,12 +60,41 @@ def load():
     lib.oracle_match_grid.restype = I
     lib.oracle_fast_score.argtypes = [V, I]
     lib.oracle_fast_score.restype = I
+    lib.oracle_set_compat.argtypes = [ctypes.c_uint]
+    lib.oracle_get_compat.restype = ctypes.c_uint
+    lib.oracle_cv_exp_table.argtypes = [D]
+    lib.oracle_cv_exp_table.restype = D
+    lib.oracle_match_nnr_inout.argtypes = [V, I, V, I, F, V, I]
+    lib.oracle_match_nnr_inout.restype = I
+    lib.oracle_match_inout.argtypes = [V, I, V, I, F, V, I]
+    lib.oracle_match_inout.restype = I
     _lib = lib
     return lib
 
 
 def _p(a):
     return ctypes.c_void_p(a.ctypes.data)
+
+
+class compat:
+    """with compat(bits): run the oracle under the PLVI_COMPAT_* switches."""
+
+    def __init__(self, bits):
+        self.bits = bits
+
+    def __enter__(self):
+        lib = load()
+        self.prev = lib.oracle_get_compat()
+        lib.oracle_set_compat(self.bits)
+        return self
+
+    def __exit__(self, *exc):
+        load().oracle_set_compat(self.prev)
+        return False
+
+
+def cv_exp_table(x):
+    return load().oracle_cv_exp_table(float(x))
 
 
 def orb_extract(img, nfeatures=1000, scale=1.2, nlevels=8, ini=20, mn=7, lap=(0, 0), cap=20000):
@@ -149,24 +178,24 @@ def knn2(q, t):
     return tuple(out)
 
 
-def match_nnr(d1, d2, nnr):
-    lib = load()
-    _declare_match(lib)
-    d1 = np.ascontiguousarray(d1, np.uint8)
-    d2 = np.ascontiguousarray(d2, np.uint8)
-    m = np.zeros(d1.shape[0], np.int32)
-    n = lib.oracle_match_nnr(_p(d1), d1.shape[0], _p(d2), d2.shape[0], nnr, _p(m))
-    return n, m
+def _match_inout(fn, d1, d2, nnr, prev):
+    d1 = np.ascontiguousarray(d1, np.uint8).reshape(-1, 32)
+    d2 = np.ascontiguousarray(d2, np.uint8).reshape(-1, 32)
+    prev = np.zeros(0, np.int32) if prev is None else np.ascontiguousarray(prev, np.int32)
+    m = np.full(max(d1.shape[0], prev.size, 1), -1, np.int32)
+    m[:prev.size] = prev
+    n = fn(_p(d1), d1.shape[0], _p(d2), d2.shape[0], nnr, _p(m), prev.size)
+    return n, m[:d1.shape[0]].copy()
 
 
-def match(d1, d2, nnr):
-    lib = load()
-    _declare_match(lib)
-    d1 = np.ascontiguousarray(d1, np.uint8)
-    d2 = np.ascontiguousarray(d2, np.uint8)
-    m = np.zeros(d1.shape[0], np.int32)
-    n = lib.oracle_match(_p(d1), d1.shape[0], _p(d2), d2.shape[0], nnr, _p(m))
-    return n, m
+def match_nnr(d1, d2, nnr, prev=None):
+    """LineMatcher::matchNNR; prev = the caller's existing matches_12 (kept by resize)."""
+    return _match_inout(load().oracle_match_nnr_inout, d1, d2, nnr, prev)
+
+
+def match(d1, d2, nnr, prev=None):
+    """LineMatcher::match (mutual); returns -2 for a stale out-of-range entry (UB in the reference)."""
+    return _match_inout(load().oracle_match_inout, d1, d2, nnr, prev)
 
 
 KEYLINE_DTYPE = np.dtype([("angle", "<f4"), ("class_id", "<i4"), ("octave", "<i4"), ("pt_x", "<f4"),

@@ -53,3 +53,44 @@ def test_gloo_world2_sharding_and_max_time():
     assert [o[2] for o in out] == [4, 4]           # whole-job frame count
     assert out[0][3] != out[1][3]                  # each rank owns different frames
     assert all(o[4] for o in out)                  # per-frame tables gathered rank-major on every rank
+
+
+def _bench(*a, timeout=300):
+    import json
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = {k: v for k, v in __import__("os").environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), *a], capture_output=True, text=True, timeout=timeout,
+                       env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """`bench.py --gpus 2` starts 2 ranks itself (torch.distributed.run child)
+    and reports n_gpus from the actual world size; the max-time and
+    sum-frames reductions cover both ranks, each with its own sequence."""
+    out = _bench("--gpus", "2", "--dry-run", "--batch", "3", "--steps", "2", "--width", "64", "--height", "48")
+    assert out["n_gpus"] == 2 and out["frames_total"] == 2 * 2 * 3
+    d = out["rank_digests"]
+    assert len(d) == 2 and d[0] != d[1]
+
+
+def test_bench_c4_dry_run_world2():
+    """--c4: 752x480 windows with a one-frame halo (B-1 new frames per step)."""
+    out = _bench("--gpus", "2", "--dry-run", "--c4", "--batch", "3", "--steps", "3")
+    assert out["n_gpus"] == 2 and out["config"]["width"] == 752 and out["frames_total"] == 2 * 3 * 2
+
+
+def test_bench_refuses_world_mismatch():
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "4", "--dry-run"], capture_output=True,
+                       text=True, timeout=120, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE" in r.stderr

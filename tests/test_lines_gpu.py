@@ -88,10 +88,13 @@ def test_lines_batch_equals_single(lx640):
         _assert_same((kl[s], de[s], fn[s]), ol.line_extract(frames[f]), f"batch{f}")
 
 
-def test_lines_two_frames_per_wave_variant(plvi_lib, monkeypatch):
-    """lsd_grow2_kernel (PLVI_GROW_PACK=2: two frames per region-growing wave)
-    gives the oracle's lines too, including an odd batch (last wave half-empty)."""
-    monkeypatch.setenv("PLVI_GROW_PACK", "2")
+@pytest.mark.parametrize("lds", [6144, 12288, 40960])
+def test_lines_grow_window_budgets(plvi_lib, monkeypatch, lds):
+    """PLVI_GROW_LDS picks the region-growing LDS window (R = 2 rows by
+    default, 4 / 8+ rows and the 1024-entry queue at the larger budgets):
+    every budget gives the oracle's lines, at 640 px (odd batch) and at the
+    752 px EuRoC width (BASELINE C4)."""
+    monkeypatch.setenv("PLVI_GROW_LDS", str(lds))
     lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 640, 480, max_batch=3)
     frames = synth.batch(3, seed0=60)
     buf = plvi.DeviceBuffer(frames.nbytes)
@@ -105,9 +108,11 @@ def test_lines_two_frames_per_wave_variant(plvi_lib, monkeypatch):
     fn = plvi.download(fnp, np.zeros((3 * cap, 3), np.float64))
     for f in range(3):
         s = slice(f * cap, f * cap + cnt[f])
-        _assert_same((kl[s], de[s], fn[s]), ol.line_extract(frames[f]), f"pack2 batch{f}")
-    img = real_frames()["rgb1_gray"]
-    _assert_same(lx(img), ol.line_extract(img), "pack2 rgb1_gray")
+        _assert_same((kl[s], de[s], fn[s]), ol.line_extract(frames[f]), f"lds{lds} batch{f}")
+    assert lx.errors() == 0
+    lx752 = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 752, 480)
+    img = real_frames()["euroc1"]
+    _assert_same(lx752(img), ol.line_extract(img), f"lds{lds} euroc1")
 
 
 @pytest.mark.parametrize("name", ["step", "checker", "stripes", "binary_noise"])
