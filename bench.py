@@ -247,7 +247,7 @@ def dry_run(args, world, rank):
         pdist.init("gloo")
     W, H = (752, 480) if args.c4 else (args.width, args.height)
     B = args.batch
-    nwin = max(1, (2000 - 1) // (B - 1)) if args.c4 else 1
+    nwin = 2 if args.c4 else 1
     seq = synth.device_sequence(B + (nwin - 1) * (B - 1), W, H, seed=pdist.shard_seed(rank))
     digest = hashlib.sha256(seq[:B].numpy().tobytes()).hexdigest()[:16]
     pdist.barrier(world)
@@ -280,7 +280,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=None, help="frames per step (default 3072; C4: 1000)")
+    ap.add_argument("--batch", type=int, default=None, help="frames per step (default 3072; C4: 2000)")
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--c4", action="store_true", help="BASELINE C4: 752x480 sequences, RCCL gather to rank 0")
@@ -304,7 +304,7 @@ def main():
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
         return 2
     if args.batch is None:
-        args.batch = 1000 if args.c4 else 3072
+        args.batch = 2000 if args.c4 else 3072
     if args.batch < 2:
         print("bench.py: --batch must be >= 2 (frames are matched against their predecessor)", file=sys.stderr)
         return 2
@@ -337,8 +337,8 @@ def run(args, world, rank):
 
     # frames: C4 = one sequence per rank walked in windows [k(B-1), k(B-1)+B)
     # (one-frame halo); default = one resident batch re-processed each step
-    # (sequences of ~2000 frames; windows wrap to the start)
-    nwin = max(1, (2000 - 1) // (B - 1)) if args.c4 else 1
+    # (C4: two windows per sequence, ~2B frames; the walk wraps to the start)
+    nwin = 2 if args.c4 else 1
     seq = synth.device_sequence(B + (nwin - 1) * (B - 1), W, H, seed=seed0, device=cuda)
     torch.cuda.synchronize()
     first_digest = hashlib.sha256(seq[:B].cpu().numpy().tobytes()).hexdigest()[:16]
@@ -486,7 +486,8 @@ def run(args, world, rank):
     roof["frac"] = roof["achieved"] / roof["peak"]
     roof_lsd = {"bound": "hbm", "kernel": "lsd_prep_kernel (u8 -> f64 blur 7x7, resize x0.8, ll_angle; one launch "
                                           "per octave)",
-                "achieved": lp_bytes / (ltot * 1e-3) / 1e9 if ltot else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "achieved": lp_bytes * (ln / 2) / (ltot * 1e-3) / 1e9 if ltot else None, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
                 "traffic": committed_traffic(B, "lsd_prep_kernel") if (W, H) == (640, 480) else None,
                 "bytes_per_launch": lp_bytes / 2, "avg_launch_ms": ltot / max(ln, 1), "launches": ln}
     if roof_lsd["achieved"]:

@@ -226,10 +226,38 @@ extern "C" int oracle_search_by_bow(const uint8_t* kf_desc, const float* kf_angl
 #include <list>
 #include <limits>
 #include <unordered_set>
-extern "C" int oracle_match_grid(const int* lines1, const uint8_t* desc1, int n1, int cols, int rows,
-                                 const int* cell_off, const int* cell_idx, const uint8_t* desc2,
-                                 const double* directions2, int n2, int w0, int w1, int h0, int h1,
-                                 int* matches_12) {
+
+// indices.insert(first, last) as libstdc++ up to GCC 10 performs it (the
+// reference's Ubuntu 20.04 / GCC 9.3 build): _M_insert_range
+// passes the remaining range length __n_elt as the rehash hint of
+// _M_insert_unique_node, reset to 1 after each insertion and decremented
+// for each key already present.  GCC 11 (this host) dropped the hint from
+// insert(first, last) but keeps exactly that loop in _M_merge_unique, so the
+// oracle drives the HOST library's own hashtable through merge(): the
+// source is an unordered_multiset with a constant hash and an equality that
+// never holds, whose iteration order is the reverse of its insertion order
+// (every node is inserted at the front of bucket 0; the multi-key rehash
+// keeps bucket order), so inserting the cell reversed makes the merge visit
+// it in list order.  Independent of the product's emulation
+// (csrc/stl_uset.h): here the host _Hashtable / _Prime_rehash_policy code
+// runs the insertion.
+struct ConstHash {
+    size_t operator()(int) const noexcept { return 0; }
+};
+struct NeverEq {
+    bool operator()(int, int) const noexcept { return false; }
+};
+static void insert_range_gcc10(std::unordered_set<int>& indices, const std::list<int>& cell) {
+    if (cell.empty()) return;
+    std::unordered_multiset<int, ConstHash, NeverEq> src;
+    for (auto it = cell.rbegin(); it != cell.rend(); ++it) src.insert(*it);
+    indices.merge(src);
+}
+
+extern "C" int oracle_match_grid2(const int* lines1, const uint8_t* desc1, int n1, int cols, int rows,
+                                  const int* cell_off, const int* cell_idx, const uint8_t* desc2,
+                                  const double* directions2, int n2, int w0, int w1, int h0, int h1,
+                                  int range_hint, int* matches_12) {
     std::vector<std::vector<std::list<int>>> grid(cols, std::vector<std::list<int>>(rows));
     for (int x = 0; x < cols; ++x)
         for (int y = 0; y < rows; ++y)
@@ -240,7 +268,10 @@ extern "C" int oracle_match_grid(const int* lines1, const uint8_t* desc1, int n1
         int min_y = std::max(0, y - h0);
         int max_y = std::min(rows, y + h1 + 1);
         for (int x_ = min_x; x_ < max_x; ++x_)
-            for (int y_ = min_y; y_ < max_y; ++y_) indices.insert(grid[x_][y_].begin(), grid[x_][y_].end());
+            for (int y_ = min_y; y_ < max_y; ++y_) {
+                if (range_hint) insert_range_gcc10(indices, grid[x_][y_]);
+                else indices.insert(grid[x_][y_].begin(), grid[x_][y_].end());
+            }
     };
     const double lineSimTh = 0.75, minRatio12L = 0.9;
     int matches = 0;
@@ -288,4 +319,26 @@ extern "C" int oracle_match_grid(const int* lines1, const uint8_t* desc1, int n1
         }
     }
     return matches;
+}
+
+extern "C" int oracle_match_grid(const int* lines1, const uint8_t* desc1, int n1, int cols, int rows,
+                                 const int* cell_off, const int* cell_idx, const uint8_t* desc2,
+                                 const double* directions2, int n2, int w0, int w1, int h0, int h1,
+                                 int* matches_12) {
+    return oracle_match_grid2(lines1, desc1, n1, cols, rows, cell_off, cell_idx, desc2, directions2, n2, w0, w1, h0,
+                              h1, 0, matches_12);
+}
+
+// Iteration order of a candidate set filled by range inserts (for the
+// emulation's own checks): out receives the set's elements in iteration order.
+extern "C" int oracle_uset_order(const int* seq_off, const int* seq, int nseq, int range_hint, int* out) {
+    std::unordered_set<int> s;
+    for (int k = 0; k < nseq; ++k) {
+        std::list<int> cell(seq + seq_off[k], seq + seq_off[k + 1]);
+        if (range_hint) insert_range_gcc10(s, cell);
+        else s.insert(cell.begin(), cell.end());
+    }
+    int n = 0;
+    for (int v : s) out[n++] = v;
+    return n;
 }

@@ -26,10 +26,10 @@
 
 #include "oracle_api.h"
 
-extern "C" int oracle_match_grid(const int* lines1, const uint8_t* desc1, int n1, int cols, int rows,
-                                 const int* cell_off, const int* cell_idx, const uint8_t* desc2,
-                                 const double* directions2, int n2, int w0, int w1, int h0, int h1,
-                                 int* matches_12);
+extern "C" int oracle_match_grid2(const int* lines1, const uint8_t* desc1, int n1, int cols, int rows,
+                                  const int* cell_off, const int* cell_idx, const uint8_t* desc2,
+                                  const double* directions2, int n2, int w0, int w1, int h0, int h1,
+                                  int range_hint, int* matches_12);
 
 namespace {
 
@@ -250,7 +250,8 @@ struct KLpts {
 // lines with a depth.
 extern "C" int oracle_stereo_lines(const float* klL, const uint8_t* descL, int nL, const float* klR,
                                    const uint8_t* descR, int nR, const float* klUn, int width, int height,
-                                   float mbf, int* matches_12, float* disparity, float* depth, double* le) {
+                                   float mbf, int range_hint, int* matches_12, float* disparity, float* depth,
+                                   double* le) {
     for (int i = 0; i < nL; ++i) {
         matches_12[i] = -1;
         disparity[2 * i] = disparity[2 * i + 1] = -1;
@@ -292,8 +293,8 @@ extern "C" int oracle_stereo_lines(const float* klL, const uint8_t* descL, int n
             off[x * kGridRows + y + 1] = (int)idxs.size();
         }
     if (idxs.empty()) idxs.push_back(0);
-    oracle_match_grid(coords.data(), descL, nL, kGridCols, kGridRows, off.data(), idxs.data(), descR,
-                      directions.data(), nR, 7, 0, 2, 2, matches_12);
+    oracle_match_grid2(coords.data(), descL, nL, kGridCols, kGridRows, off.data(), idxs.data(), descR,
+                       directions.data(), nR, 7, 0, 2, 2, range_hint, matches_12);
     int nd = 0;
     for (int i1 = 0; i1 < nL; ++i1) {
         const int i2 = matches_12[i1];

@@ -58,6 +58,10 @@ def load():
     lib.oracle_line_descriptor_distance.restype = I
     lib.oracle_match_grid.argtypes = [V, V, I, I, I, V, V, V, V, I, I, I, I, I, V]
     lib.oracle_match_grid.restype = I
+    lib.oracle_match_grid2.argtypes = [V, V, I, I, I, V, V, V, V, I, I, I, I, I, I, V]
+    lib.oracle_match_grid2.restype = I
+    lib.oracle_uset_order.argtypes = [V, V, I, I, V]
+    lib.oracle_uset_order.restype = I
     lib.oracle_fast_score.argtypes = [V, I]
     lib.oracle_fast_score.restype = I
     lib.oracle_set_compat.argtypes = [ctypes.c_uint]
@@ -263,8 +267,22 @@ def search_by_bow(kf_desc, kf_angle, kf_live, kf_fv, f_desc, f_angle, f_fv, nnra
     return n, out[:len(fd)]
 
 
-def match_grid(lines1, desc1, grid, desc2, directions2, window=((7, 0), (2, 2))):
-    """LineMatcher::matchGrid restatement (real std::unordered_set of the host libstdc++)."""
+def uset_order(cells, range_hint):
+    """Iteration order of a std::unordered_set<int> filled by one range insert per cell list."""
+    off = np.zeros(len(cells) + 1, np.int32)
+    flat = []
+    for i, c in enumerate(cells):
+        flat.extend(c)
+        off[i + 1] = len(flat)
+    seq = np.array(flat if flat else [0], np.int32)
+    out = np.zeros(max(len(flat), 1), np.int32)
+    n = load().oracle_uset_order(_p(off), _p(seq), len(cells), range_hint, _p(out))
+    return out[:n].tolist()
+
+
+def match_grid(lines1, desc1, grid, desc2, directions2, window=((7, 0), (2, 2)), range_hint=0):
+    """LineMatcher::matchGrid restatement (real std::unordered_set of the host libstdc++;
+    range_hint=1 drives it with the GCC <= 10 range-insert hint, see match_oracle.cpp)."""
     lib = load()
     cols, rows = len(grid), len(grid[0])
     off = np.zeros(cols * rows + 1, np.int32)
@@ -280,8 +298,8 @@ def match_grid(lines1, desc1, grid, desc2, directions2, window=((7, 0), (2, 2)))
     v2 = np.ascontiguousarray(directions2, np.float64).reshape(-1, 2)
     m = np.full(max(len(l1), 1), -1, np.int32)
     (w0, w1), (h0, h1) = window
-    n = lib.oracle_match_grid(_p(l1), _p(d1), len(l1), cols, rows, _p(off), _p(idx), _p(d2), _p(v2), len(d2),
-                              w0, w1, h0, h1, _p(m))
+    n = lib.oracle_match_grid2(_p(l1), _p(d1), len(l1), cols, rows, _p(off), _p(idx), _p(d2), _p(v2), len(d2),
+                               w0, w1, h0, h1, range_hint, _p(m))
     return n, m[:len(l1)]
 
 
@@ -468,11 +486,11 @@ def stereo_match(kpsL, descL, kpsR, descR, pyrL, pyrR, scale, inv_scale, mb, mbf
     return k, ur[:n], dp[:n]
 
 
-def stereo_lines(klL, descL, klR, descR, klUn, width, height, mbf):
+def stereo_lines(klL, descL, klR, descR, klUn, width, height, mbf, range_hint=0):
     """Frame::ComputeStereoMatches_Lines restatement -> (nstereo, matches, disparity, depth, le)."""
     lib = load()
     V, F, I = ctypes.c_void_p, ctypes.c_float, ctypes.c_int
-    lib.oracle_stereo_lines.argtypes = [V, V, I, V, V, I, V, I, I, F, V, V, V, V]
+    lib.oracle_stereo_lines.argtypes = [V, V, I, V, V, I, V, I, I, F, I, V, V, V, V]
     lib.oracle_stereo_lines.restype = I
 
     def pts(k):
@@ -488,6 +506,7 @@ def stereo_lines(klL, descL, klR, descR, klUn, width, height, mbf):
     disp = np.zeros((max(n, 1), 2), np.float32)
     dep = np.zeros((max(n, 1), 2), np.float32)
     le = np.zeros((max(n, 1), 3), np.float64)
-    k = lib.oracle_stereo_lines(_p(a), _p(dl), n, _p(b), _p(dr), len(b), _p(u), width, height, mbf, _p(m), _p(disp),
+    k = lib.oracle_stereo_lines(_p(a), _p(dl), n, _p(b), _p(dr), len(b), _p(u), width, height, mbf, range_hint,
+                                _p(m), _p(disp),
                                 _p(dep), _p(le))
     return k, m[:n], disp[:n], dep[:n], le[:n]
