@@ -347,9 +347,11 @@ int plvi_line_match_grid_batch(int n_pairs, const int* d_lines1, const uint8_t* 
 typedef struct plvi_vocabulary plvi_vocabulary;
 
 /* loadFromTextFile (TemplatedVocabulary.h:1338-1424; System.cc:84).
- * emulate_tail != 0 reproduces the loader's extra node read from the empty
- * tail after the file's final newline (a weight-0 leaf child of the root,
- * descriptor zero here, uninitialised in the reference). */
+ * The reference's loop also builds a node from the empty line after the
+ * file's final newline; its parent, leaf flag and descriptor are never
+ * assigned (the istream sentry fails), i.e. undefined behaviour.
+ * emulate_tail = 0 (recommended) skips it; != 0 models one outcome: a
+ * weight-0, zero-descriptor, non-word child of the root. */
 int plvi_vocab_load_text(const char* path, int emulate_tail, int device, plvi_vocabulary** out);
 
 /* Build from a node table (row i = node i+1 in file order; parent[i] < i+1):

@@ -13,12 +13,14 @@
 // (Vocabulary/ORBvoc.txt) is absent; this follows the cited lines with
 // std::map containers and iostream parsing exactly like the reference.
 //
-// The loader's `while(!f.eof()) getline` loop turns the empty tail after the
-// file's final newline into one more node: parent 0 (failed extraction -> 0),
-// no children (so a leaf), weight 0, not registered as a word (nIsLeaf 0),
-// descriptor bytes left uninitialised by FORB::fromString.  With
-// emulate_tail != 0 the oracle reproduces that node with a zero descriptor
-// (the reference's bytes are indeterminate: unpinned).
+// The loader's `while(!f.eof()) getline` loop reads one more (empty) line
+// after the file's final newline and creates one more node from it.  On that
+// empty stream `ssnode >> pid` fails in the istream sentry, so pid and
+// nIsLeaf keep whatever the uninitialised locals held and the descriptor
+// bytes stay uninitialised (FORB::fromString): the node is undefined
+// behaviour in the reference.  Default (emulate_tail = 0): no such node.
+// emulate_tail != 0 models one outcome -- pid and nIsLeaf reading 0, i.e. a
+// weight-0, zero-descriptor, non-word child of the root -- unpinned.
 #include <cmath>
 #include <cstdint>
 #include <cstring>

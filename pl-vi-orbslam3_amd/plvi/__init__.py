@@ -700,7 +700,11 @@ class ORBVocabulary:
         self.k, self.L, self.scoring, self.weighting, self.n_nodes, self.n_words = (int(x) for x in info)
 
     @classmethod
-    def loadFromTextFile(cls, path, emulate_tail=True, device=0):
+    def loadFromTextFile(cls, path, emulate_tail=False, device=0):
+        """TemplatedVocabulary::loadFromTextFile (TemplatedVocabulary.h:1338-1424).  emulate_tail=True adds
+        the node the reference's `while(!f.eof()) getline` loop reads from the empty tail after a final
+        newline -- undefined in the reference (pid / nIsLeaf / the descriptor stay unassigned), modelled here
+        as a zero-descriptor non-word child of the root; off by default."""
         h = ctypes.c_void_p()
         _check(load().plvi_vocab_load_text(str(path).encode(), int(emulate_tail), device, ctypes.byref(h)),
                "plvi_vocab_load_text")

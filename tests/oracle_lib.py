@@ -329,7 +329,7 @@ class Vocab:
         self.k, self.L, self.scoring, self.weighting, self.n_nodes, self.n_words = (int(x) for x in info)
 
     @classmethod
-    def load_text(cls, path, emulate_tail=True):
+    def load_text(cls, path, emulate_tail=False):
         lib = load()
         _declare_vocab(lib)
         return cls(lib.oracle_vocab_load(str(path).encode(), int(emulate_tail)))

@@ -46,3 +46,41 @@ def test_branch_free_sincosf_every_float(libm_check):
 
 def test_fast_atan2_select_form(libm_check):
     _run(libm_check, "fastatan2", "30000000")  # branch-free device cv::fastAtan2 vs the oracle restatement
+
+
+# ---------------------------------------------------------------- on device
+DSRC = ROOT / "tests" / "native" / "libm_device_check.hip"
+DBIN = ROOT / "tests" / "native" / "_build" / "libm_device_check"
+
+
+def build_device_check():
+    """hipcc with the library's flags (gfx950, -O3, -ffp-contract=off), linked
+    to the oracle for cv::fastAtan2."""
+    hdr = ROOT / "pl-vi-orbslam3_amd" / "csrc" / "plvi_math.h"
+    olib = ROOT / "oracle" / "_build"
+    if not (olib / "liboracle.so").exists():
+        subprocess.run(["make", "-s", "-C", str(ROOT / "oracle")], check=True)
+    if not DBIN.exists() or DBIN.stat().st_mtime < max(DSRC.stat().st_mtime, hdr.stat().st_mtime):
+        DBIN.parent.mkdir(exist_ok=True)
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                        "-fno-fast-math", "-pthread", "-o", str(DBIN), str(DSRC), f"-L{olib}", "-loracle",
+                        f"-Wl,-rpath,{olib}"], check=True)
+    return str(DBIN)
+
+
+def test_device_libm_check_builds():
+    assert pathlib.Path(build_device_check()).exists()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,args,count", [
+    ("sincosf", (), 4294967296),          # every float bit pattern, sinf and cosf
+    ("sincospos", (), None),              # branch-free sincosf, every float in [0, 120)
+    ("lsdangles", (), None),              # float(cos/sin(+-deg*pi/180)), every float deg in [0, 360]
+    ("atan2f", ("30000000",), 30000000),
+    ("fastatan2", ("30000000",), 30000000),
+])
+def test_device_libm_matches_host_glibc(mode, args, count):
+    out = _run(build_device_check(), mode, *args)
+    if count:
+        assert f"checked={count}" in out

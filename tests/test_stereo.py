@@ -329,6 +329,22 @@ def test_stereo_match_batch_on_extractor_outputs():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", [11, 12])
+def test_stereo_lines_gcc10_order_matches_oracle(seed):
+    """ComputeStereoMatches_Lines with the shipped candidate order
+    (range_hint=1, GCC <= 10 unordered_set range insert)."""
+    import plvi
+    L, R, _ = synth.stereo_pair(seed)
+    kl, dl, _ = oracle_lib.line_extract(L)
+    kr, dr, _ = oracle_lib.line_extract(R)
+    exp = oracle_lib.stereo_lines(kl, dl, kr, dr, None, 640, 480, MBF, range_hint=1)
+    got = plvi.ComputeStereoMatches_Lines(kl, dl, kr, dr, None, 640, 480, MBF, range_hint=1)
+    assert got[0] == exp[0] > 10
+    for g, e in zip(got[1:], exp[1:]):
+        assert np.array_equal(g, e)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [11, 12])
 def test_stereo_lines_host_matches_oracle(seed):
     import plvi
     L, R, _ = synth.stereo_pair(seed)
