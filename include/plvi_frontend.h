@@ -470,6 +470,40 @@ int plvi_search_by_projection(const plvi_proj_params* p, const plvi_keypoint* cu
                               const int* last_octave, const float* last_angle, const uint8_t* mp_desc,
                               const uint8_t* last_flags, int n_last, int* match);
 
+/* ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>&
+ * vpMapPoints, th, bFarPoints, thFarPoints) (src/ORBmatcher.cc:44-145,
+ * F.Nleft == -1, RadiusByViewingCos :216-222): the local-map search of
+ * Tracking::SearchLocalPoints (src/Tracking.cc:5119/5211). */
+typedef struct plvi_local_params {
+  float min_x, min_y, inv_w, inv_h; /* F.mnMinX, mnMinY, mfGridElementWidthInv / HeightInv */
+  float th;                         /* th (the radius is scaled by th when th != 1) */
+  float nnratio;                    /* ORBmatcher(nnratio): 0.8 in SearchLocalPoints */
+  int nlevels;
+  float scale_factors[16];          /* F.mvScaleFactors */
+} plvi_local_params;
+
+/* Batched over n_frames frames: frame f's keypoints (mvKeysUn) /
+ * descriptors [f][cap] (counts d_n), grid CSR from plvi_assign_grid_batch,
+ * blocked[idx] = mvpMapPoints[idx] && Observations() > 0 on entry (NULL =
+ * none), mvuRight (NULL = none); its MapPoints [f][mp_cap] (counts d_mp_n,
+ * vector order): flags bit0 = searched (mbTrackInView && not far &&
+ * !isBad()), bit1 = Observations() > 0; proj [4] = mTrackProjX,
+ * mTrackProjY, mTrackProjXR, mTrackViewCos; level = mnTrackScaleLevel;
+ * GetDescriptor() (32 B).  Output match [f][cap] = the MapPoint index
+ * stored in F.mvpMapPoints[idx] by the call, or -1; nmatches [f] = the
+ * return value.  cap <= 65535 and ~17 B per keypoint + 8 B per MapPoint +
+ * 12 KB of LDS <= 160 KB. */
+int plvi_search_local_batch(int n_frames, const plvi_local_params* p, const plvi_keypoint* d_kps, const uint8_t* d_desc,
+                            const int* d_n, int cap, const uint8_t* d_blocked, const float* d_uright,
+                            const int* d_cell_off, const int* d_cell_idx, const uint8_t* d_mp_flags,
+                            const float* d_mp_proj, const int* d_mp_level, const uint8_t* d_mp_desc, const int* d_mp_n,
+                            int mp_cap, int* d_match, int* d_nmatches, void* stream);
+
+/* One frame from host memory, synchronous.  Returns nmatches or an error. */
+int plvi_search_local(const plvi_local_params* p, const plvi_keypoint* kps, const uint8_t* desc, int n,
+                      const uint8_t* blocked, const float* uright, const uint8_t* mp_flags, const float* mp_proj,
+                      const int* mp_level, const uint8_t* mp_desc, int n_mp, int* match);
+
 /* ---------------------------------------------------------------- Stereo
  * Rectified stereo of the stereo Frame constructors (src/Frame.cc:95-140,
  * :225-300). */

@@ -8,6 +8,8 @@
 //   ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono)
 //                                    src/ORBmatcher.cc:1962-2178 (Nleft == -1 branch)
 //   ORBmatcher::ComputeThreeMaxima   src/ORBmatcher.cc:2304-2345
+//   ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th, bFarPoints, thFarPoints)
+//                                    src/ORBmatcher.cc:44-145 (F.Nleft == -1) + RadiusByViewingCos :216-222
 //   Pinhole::project                 src/CameraModels/Pinhole.cpp:30-39
 // The pose product x3Dc = Rcw*x3Dw + tcw (cv::Mat) is an input: it is taken
 // from the caller, as the drop-in shim keeps it on the host.
@@ -227,5 +229,69 @@ extern "C" int oracle_search_by_projection(
                 }
     }
     for (int i2 = 0; i2 < n_cur; ++i2) match[i2] = nulled[i2] ? -2 : mp[i2];
+    return nmatches;
+}
+
+// ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoints,
+// th, bFarPoints, thFarPoints) (src/ORBmatcher.cc:44-145), F.Nleft == -1, the
+// local-map search of Tracking::SearchLocalPoints (Tracking.cc:5119/5211).
+// Per MapPoint iMP (vector order) the caller evaluates the MapPoint state:
+// mp_flags bit0 = it is searched (mbTrackInView && !(bFarPoints && mTrackDepth
+// > thFarPoints) && !isBad()), bit1 = Observations() > 0; mTrackProjX/Y,
+// mTrackProjXR, mTrackViewCos, mnTrackScaleLevel, GetDescriptor().  Frame:
+// mvKeysUn (x, y, octave), descriptors, blocked = mvpMapPoints[idx] &&
+// Observations() > 0 on entry, mvuRight (nullable).  Output match[idx] = iMP
+// stored in F.mvpMapPoints[idx] by this call, or -1.  Returns nmatches.
+extern "C" int oracle_search_local(int n_cur, const float* cx_, const float* cy_, const int* coct,
+                                   const uint8_t* cdesc, const uint8_t* cblocked, const float* curight, float minX,
+                                   float minY, float invW, float invH, const float* scale_factors, float nnratio,
+                                   float th, int n_mp, const uint8_t* mp_flags, const float* px, const float* py,
+                                   const float* pxr, const float* view_cos, const int* level, const uint8_t* mpdesc,
+                                   int* match) {
+    std::vector<float> ang(n_cur, 0.f);
+    const std::vector<Kp> kps = make_kps(n_cur, cx_, cy_, coct, ang.data());
+    Grid g;
+    assign_grid(kps, minX, minY, invW, invH, g);
+    std::vector<char> blocked(cblocked, cblocked + n_cur);
+    for (int i = 0; i < n_cur; ++i) match[i] = -1;
+    const bool bFactor = th != 1.0;
+    int nmatches = 0;
+    for (int iMP = 0; iMP < n_mp; iMP++) {
+        if (!(mp_flags[iMP] & 1)) continue;
+        const int nPredictedLevel = level[iMP];
+        float r = view_cos[iMP] > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos
+        if (bFactor) r *= th;
+        const std::vector<size_t> vIndices =
+            features_in_area(g, kps, minX, minY, invW, invH, px[iMP], py[iMP], r * scale_factors[nPredictedLevel],
+                             nPredictedLevel - 1, nPredictedLevel);
+        if (vIndices.empty()) continue;
+        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+        for (size_t idx : vIndices) {
+            if (blocked[idx]) continue;
+            if (curight && curight[idx] > 0) {
+                const float er = std::fabs(pxr[iMP] - curight[idx]);
+                if (er > r * scale_factors[nPredictedLevel]) continue;
+            }
+            const int dist = dist256(mpdesc + 32 * (size_t)iMP, cdesc + 32 * idx);
+            if (dist < bestDist) {
+                bestDist2 = bestDist;
+                bestDist = dist;
+                bestLevel2 = bestLevel;
+                bestLevel = kps[idx].octave;
+                bestIdx = (int)idx;
+            } else if (dist < bestDist2) {
+                bestLevel2 = kps[idx].octave;
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= kThHigh) {
+            if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
+            if (bestLevel != bestLevel2 || bestDist <= nnratio * bestDist2) {
+                match[bestIdx] = iMP;
+                blocked[bestIdx] = (mp_flags[iMP] & 2) ? 1 : 0;
+                nmatches++;
+            }
+        }
+    }
     return nmatches;
 }

@@ -177,10 +177,6 @@ __global__ __launch_bounds__(256) void lsd_prep_kernel(const uint8_t* __restrict
 // lane is re-decided with the exact angle in the next round.  The result is
 // identical to the sequential algorithm.
 // ---------------------------------------------------------------------------
-// LDS pointers carry address space 3 so every access is a ds_* instruction
-// (a generic pointer turns them into flat accesses that wait on vmcnt too).
-typedef unsigned __attribute__((address_space(3))) lds_u32;
-typedef float __attribute__((address_space(3))) lds_f32;
 
 struct GrowCtx {
     const float* P;   // angle plane (degrees, NOTDEF = -1024)

@@ -30,6 +30,8 @@ struct OrbLevelDev {
     int nIni;
     int rootGx[kOrbMaxRoots + 1];  // geometric root x: (int)(hX*i)
     int rootB[kOrbMaxRoots + 1];   // membership: root i holds x in [rootB[i], rootB[i+1])
+    double rsx, rsy;               // cv::resize scale_x / scale_y from level l-1 (1 / ((double)dw / sw))
+    int xtab;                      // offset of this level's packed column table (orb_pyramid_kernel)
 };
 
 // One column strip of a level for the blur + FAST kernel: output columns

@@ -24,39 +24,199 @@ __device__ __forceinline__ int reflect1(int p, int len) {
 
 
 // ---------------------------------------------------------------------------
-// K1a: level l >= 1 of the pyramid: cv::resize INTER_LINEAR 8U of level l-1
-// (ORBextractor.cc:1165).  Thread per destination pixel; the row
-// coefficients are wave-uniform (scalar loads).
+// K1a: ComputePyramid (ORBextractor.cc:1152-1177): levels 1..L-1 of one
+// frame per workgroup, chained cv::resize INTER_LINEAR 8U (level l from
+// l-1), streamed top to bottom in a single launch.
+//   wave 0 (loader): streams the level-0 rows from HBM (dword loads,
+//     kPyrAhead rows in flight) into an LDS ring of kPyrRing rows;
+//   wave 1 (resizer): every new source row yields the (at most one:
+//     scale > 1) next row of the level above it, cascading through the
+//     levels; each level keeps its last two rows in LDS, and every level row
+//     is written to HBM once -- no intermediate HBM round trip.
+// The waves hand rows over through two LDS counters (rows loaded / rows
+// consumed) and s_sleep polling, never a workgroup barrier: the resizer
+// issues only stores and LDS traffic, so nothing in its loop waits for
+// memory, and the loader's waits cover only its own loads.
+// The per-column coefficients (sx, a0, a1 of cv::resize, computed on the
+// host exactly as OpenCV does: pyr_xtab_entry) are one packed table in LDS
+// shared by all rows; the row coefficients are computed per output row.
+// Limits: level-0 width <= 4 * 64 * kPyrDw, source widths <= 1024.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void orb_resize_kernel(const uint8_t* __restrict__ src, size_t s_frame,
-                                                         size_t s_row, uint8_t* __restrict__ dst, int w, int h,
-                                                         size_t d_frame, const int* __restrict__ xofs,
-                                                         const short* __restrict__ xa, int xmax,
-                                                         const int* __restrict__ yrow, const short* __restrict__ yb,
-                                                         int generic) {
-    const int f = blockIdx.z;
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int y = __builtin_amdgcn_readfirstlane(blockIdx.y * 4 + (threadIdx.x >> 6));
-    if (y >= h) return;
-    const uint8_t* S = src + (size_t)f * s_frame;
-    const uint8_t* R0 = S + (size_t)yrow[2 * y] * s_row;
-    const uint8_t* R1 = S + (size_t)yrow[2 * y + 1] * s_row;
-    const int b0 = yb[2 * y], b1 = yb[2 * y + 1];
-    if (x >= w) return;
-    const int sx = xofs[x];
-    int H0, H1;
-    if (x < xmax) {
-        const int a0 = xa[2 * x], a1 = xa[2 * x + 1];
-        H0 = R0[sx] * a0 + R0[sx + 1] * a1;
-        H1 = R1[sx] * a0 + R1[sx + 1] * a1;
-    } else {
-        H0 = R0[sx] * 2048;
-        H1 = R1[sx] * 2048;
+constexpr int kPyrAhead = 4, kPyrDw = 4, kPyrRing = 4, kPyrUnroll = 4;
+
+// packed column entry: sx (10 bits) | a0 (12 bits) << 10 | (a0 + a1 - 2047) (2 bits) << 22 | clampR << 24
+__host__ __device__ inline uint32_t pyr_xtab_pack(int sx, int a0, int a1, bool clampR) {
+    return (uint32_t)sx | ((uint32_t)a0 << 10) | ((uint32_t)(a0 + a1 - 2047) << 22) | ((uint32_t)clampR << 24);
+}
+
+__device__ __forceinline__ int lds_load_volatile(lds_i32* p) { return *(volatile lds_i32*)p; }
+__device__ __forceinline__ void lds_publish(lds_i32* p, int v) {
+    // earlier LDS writes of this wave complete before the counter moves
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    *(volatile lds_i32*)p = v;
+}
+
+__global__ __launch_bounds__(128) void orb_pyramid_kernel(const OrbLevelDev* __restrict__ lvs, int L,
+                                                          const uint8_t* __restrict__ frames, size_t f_frame,
+                                                          size_t f_row, uint8_t* __restrict__ pyr,
+                                                          const uint32_t* __restrict__ xtab, int xtab_n,
+                                                          int generic) {
+    extern __shared__ __align__(16) uint8_t lds_pyr_g[];
+    __shared__ int s_w[kOrbMaxLevels], s_h[kOrbMaxLevels], s_roff[kOrbMaxLevels], s_xoff[kOrbMaxLevels];
+    __shared__ double s_sy[kOrbMaxLevels];
+    __shared__ int s_cnt[2];  // rows loaded, rows consumed
+    lds_u32* ltab = (lds_u32*)lds_pyr_g;  // column table first (xtab_n words)
+    lds_u8* lds_pyr = (lds_u8*)(lds_pyr_g + 4 * xtab_n);
+    lds_i32* s_loaded = (lds_i32*)&s_cnt[0];
+    lds_i32* s_consumed = (lds_i32*)&s_cnt[1];
+    const int f = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x < L) {
+        s_w[threadIdx.x] = lvs[threadIdx.x].w;
+        s_h[threadIdx.x] = lvs[threadIdx.x].h;
+        s_sy[threadIdx.x] = lvs[threadIdx.x].rsy;
+        s_xoff[threadIdx.x] = lvs[threadIdx.x].xtab;
     }
-    // 8U specialisation (default) or the generic fixed-point cast (A.1 switch)
-    const int v = generic ? min((b0 * H0 + b1 * H1 + (1 << 21)) >> 22, 255)
-                          : ((((b0 * (H0 >> 4)) >> 16) + ((b1 * (H1 >> 4)) >> 16) + 2) >> 2);
-    dst[(size_t)f * d_frame + (size_t)y * w + x] = (uint8_t)v;
+    if (threadIdx.x == 0) {
+        int o = kPyrRing * ((lvs[0].w + 3) & ~3);  // level-0 ring first
+        s_roff[0] = 0;
+        for (int l = 1; l < L - 1; ++l) {
+            s_roff[l] = o;
+            o += 2 * ((lvs[l].w + 3) & ~3);
+        }
+        s_cnt[0] = 0;
+        s_cnt[1] = 0;
+    }
+    for (int i = threadIdx.x; i < xtab_n; i += 128) ltab[i] = xtab[i];
+    __syncthreads();  // the only workgroup barrier
+    const int W0 = s_w[0], H0 = s_h[0];
+    const int pitch0 = (W0 + 3) & ~3;
+    if (wave == 0) {
+        // ------------------------------------------------ loader
+        const int nd = (W0 + 3) >> 2;
+        const uint8_t* src = frames + (size_t)f * f_frame;
+        const bool al4 = (((reinterpret_cast<uintptr_t>(src) | (uintptr_t)f_row) & 3) == 0) && (W0 & 3) == 0;
+        auto load_row = [&](int r, uint32_t* v) {
+            const uint8_t* row = src + (size_t)r * f_row;
+            if (al4) {
+                const uint32_t* rw = reinterpret_cast<const uint32_t*>(row);
+#pragma unroll
+                for (int k = 0; k < kPyrDw; ++k)
+                    v[k] = lane + 64 * k < nd ? __builtin_nontemporal_load(rw + lane + 64 * k) : 0u;
+            } else {
+#pragma unroll
+                for (int k = 0; k < kPyrDw; ++k) {
+                    const int d = lane + 64 * k;
+                    uint32_t x = 0;
+                    for (int b = 0; b < 4; ++b)
+                        if (4 * d + b < W0) x |= (uint32_t)row[4 * d + b] << (8 * b);
+                    v[k] = x;
+                }
+            }
+        };
+        uint32_t pf[kPyrAhead][kPyrDw];
+#pragma unroll
+        for (int j = 0; j < kPyrAhead; ++j)
+            if (j < H0) load_row(j, pf[j]);
+        for (int rb = 0; rb < H0; rb += kPyrAhead) {
+#pragma unroll
+            for (int j = 0; j < kPyrAhead; ++j) {
+                const int r = rb + j;
+                if (r >= H0) break;
+                // the resizer needs rows consumed-1 and consumed: slot r % ring is free once r - ring <= consumed - 2
+#ifndef PYR_NO_WAIT
+                while (r - kPyrRing > lds_load_volatile(s_consumed) - 2) __builtin_amdgcn_s_sleep(1);
+#endif
+                lds_u32* slot = (lds_u32*)(lds_pyr + (r % kPyrRing) * pitch0);
+#pragma unroll
+                for (int k = 0; k < kPyrDw; ++k)
+                    if (lane + 64 * k < nd) slot[lane + 64 * k] = pf[j][k];
+                if (lane == 0) lds_publish(s_loaded, r + 1);
+#ifndef PYR_NO_LOAD
+                if (r + kPyrAhead < H0) load_row(r + kPyrAhead, pf[j]);
+#endif
+            }
+        }
+        return;
+    }
+    // ---------------------------------------------------- resizer
+    int prod[kOrbMaxLevels];
+#pragma unroll
+    for (int l = 0; l < kOrbMaxLevels; ++l) prod[l] = 0;
+    for (int r = 0; r < H0; ++r) {
+#ifndef PYR_NO_WAIT
+        while (lds_load_volatile(s_loaded) <= r) __builtin_amdgcn_s_sleep(1);
+#endif
+        int avail = r + 1;  // rows of the source level available
+        for (int l = 1; l < L; ++l) {
+            const int sh = s_h[l - 1], w = s_w[l], h = s_h[l];
+            const int spitch = (s_w[l - 1] + 3) & ~3, pitch = (w + 3) & ~3;
+            const int sring = l == 1 ? kPyrRing : 2;
+            const double scy = s_sy[l];
+            const lds_u32* T = ltab + s_xoff[l];
+            int y = prod[l];
+            const int y_start = y;
+            while (y < h) {
+                float fy = (float)((y + 0.5) * scy - 0.5);
+                int sy = (int)fy;
+                sy -= (sy > fy);
+                fy -= (float)sy;
+                const int r1 = min(max(sy + 1, 0), sh - 1);
+                if (r1 >= avail) break;
+                const int r0 = min(max(sy, 0), sh - 1);
+                const int b0 = (int)__builtin_rintf((1.f - fy) * 2048), b1 = (int)__builtin_rintf(fy * 2048);
+                const lds_u8* S0 = lds_pyr + s_roff[l - 1] + (r0 % sring) * spitch;
+                const lds_u8* S1 = lds_pyr + s_roff[l - 1] + (r1 % sring) * spitch;
+                uint8_t* D = pyr + lvs[l].off + (size_t)f * lvs[l].plane + (size_t)y * w;
+                lds_u8* R = l < L - 1 ? lds_pyr + s_roff[l] + (y & 1) * pitch : nullptr;
+                for (int x0 = 0; x0 < w; x0 += 64 * kPyrUnroll) {
+                    // kPyrUnroll columns per lane: all LDS reads issued before the first use
+                    uint32_t e[kPyrUnroll];
+                    int p00[kPyrUnroll], p01[kPyrUnroll], p10[kPyrUnroll], p11[kPyrUnroll];
+#pragma unroll
+                    for (int u = 0; u < kPyrUnroll; ++u) {
+                        const int x = x0 + 64 * u + lane;
+                        e[u] = x < w ? T[x] : 0u;
+                    }
+#pragma unroll
+                    for (int u = 0; u < kPyrUnroll; ++u) {
+                        const int sx = e[u] & 1023;
+                        const int sx1 = (e[u] >> 24) & 1 ? sx : sx + 1;
+                        p00[u] = S0[sx];
+                        p01[u] = S0[sx1];
+                        p10[u] = S1[sx];
+                        p11[u] = S1[sx1];
+                    }
+#pragma unroll
+                    for (int u = 0; u < kPyrUnroll; ++u) {
+                        const int x = x0 + 64 * u + lane;
+                        if (x >= w) break;
+                        int a0 = (e[u] >> 10) & 4095, a1 = 2047 - a0 + ((e[u] >> 22) & 3);
+                        int h0, h1;
+                        if (!((e[u] >> 24) & 1)) {
+                            h0 = p00[u] * a0 + p01[u] * a1;
+                            h1 = p10[u] * a0 + p11[u] * a1;
+                        } else {
+                            h0 = p00[u] * 2048;
+                            h1 = p10[u] * 2048;
+                        }
+                        // 8U specialisation (default) or the generic fixed-point cast (A.1 switch)
+                        const int v = generic ? min((b0 * h0 + b1 * h1 + (1 << 21)) >> 22, 255)
+                                              : ((((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2);
+                        D[x] = (uint8_t)v;
+                        if (R) R[x] = (uint8_t)v;
+                    }
+                }
+                ++y;
+                // one wave: its LDS row writes precede the next level's reads in
+                // program order (compiler ordering point only)
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            }
+            prod[l] = y;
+            if (y == y_start) break;  // nothing new at level l: deeper levels have no new source rows
+            avail = y;
+        }
+        if (lane == 0) lds_publish(s_consumed, r + 1);
+    }
 }
 
 // ---------------------------------------------------------------------------

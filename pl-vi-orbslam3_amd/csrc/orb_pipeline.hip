@@ -21,44 +21,24 @@ static inline int cv_round_h(double v) { return (int)lrint(v); }
 static inline int cv_floor_h(float v) { int i = (int)v; return i - (i > v); }
 static inline int cv_ceil_h(float v) { int i = (int)v; return i + (i < v); }
 
-struct ResizeTab {
-    std::vector<int> xofs, yrow;
-    std::vector<short> xa, yb;
-    int xmax = 0;
-};
-
-// cv::resize INTER_LINEAR coefficient tables (imgproc/src/resize.cpp, 4.2).
-static ResizeTab make_resize_tab(int sw, int sh, int dw, int dh) {
-    ResizeTab t;
-    const double scale_x = 1. / ((double)dw / sw), scale_y = 1. / ((double)dh / sh);
-    t.xofs.resize(dw);
-    t.xa.resize(2 * dw);
-    t.xmax = dw;
+// cv::resize INTER_LINEAR 8U column coefficients (imgproc/src/resize.cpp,
+// OpenCV 4.2: scale_x = 1/inv_scale_x, fx = (float)((dx+0.5)*scale_x-0.5),
+// sx = cvFloor(fx), border clamps, cvRound(... * INTER_RESIZE_COEF_SCALE)),
+// packed for orb_pyramid_kernel; dx >= xmax columns use S[sx] * 2048 only.
+static int append_xtab(std::vector<uint32_t>& tab, int sw, int dw) {
+    const double scale_x = 1. / ((double)dw / sw);
     for (int dx = 0; dx < dw; ++dx) {
         float fx = (float)((dx + 0.5) * scale_x - 0.5);
         int sx = cv_floor_h(fx);
         fx -= sx;
         if (sx < 0) { fx = 0; sx = 0; }
-        if (sx + 1 >= sw) {
-            t.xmax = std::min(t.xmax, dx);
-            if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
-        }
-        t.xofs[dx] = sx;
-        t.xa[2 * dx] = (short)cv_round_h((1.f - fx) * 2048);
-        t.xa[2 * dx + 1] = (short)cv_round_h(fx * 2048);
+        const bool clampR = sx + 1 >= sw;
+        if (clampR && sx >= sw - 1) { fx = 0; sx = sw - 1; }
+        const int a0 = cv_round_h((1.f - fx) * 2048), a1 = cv_round_h(fx * 2048);
+        if (sx > 1023 || a0 + a1 < 2047 || a0 + a1 > 2049) return PLVI_E_BADARG;
+        tab.push_back(pyr_xtab_pack(sx, a0, a1, clampR));
     }
-    t.yrow.resize(2 * dh);
-    t.yb.resize(2 * dh);
-    for (int dy = 0; dy < dh; ++dy) {
-        float fy = (float)((dy + 0.5) * scale_y - 0.5);
-        int sy = cv_floor_h(fy);
-        fy -= sy;
-        t.yrow[2 * dy] = std::min(std::max(sy, 0), sh - 1);
-        t.yrow[2 * dy + 1] = std::min(std::max(sy + 1, 0), sh - 1);
-        t.yb[2 * dy] = (short)cv_round_h((1.f - fy) * 2048);
-        t.yb[2 * dy + 1] = (short)cv_round_h(fy * 2048);
-    }
-    return t;
+    return PLVI_OK;
 }
 
 struct OrbPipeline {
@@ -70,15 +50,15 @@ struct OrbPipeline {
     std::vector<OrbLevelDev> lv;
     std::vector<OrbCellDev> cells;
     std::vector<OrbStripDev> strips;
-    std::vector<ResizeTab> rtab;
     int taps[7]{};
     int resizeGeneric = 0;  // A.1 vertical-pass switch (PLVI_COMPAT_RESIZE_V_GENERIC)
     int kpCapFrame = 0, nodeCapMax = 0;
     size_t pyrBytesFrameTotal = 0, satIntsFrameTotal = 0;
     size_t lvOff0 = 0;  // (unused)
-    DevBuf d_lv, d_cells, d_strips, d_tabs, pyr, blur, score, cand, sat, carry, rects, rectCnt, lvkp, lvdesc, okp, odesc, ocount,
+    DevBuf d_lv, d_cells, d_strips, d_xtab, pyr, blur, score, cand, sat, carry, rects, rectCnt, lvkp, lvdesc, okp, odesc, ocount,
         omono, err, staging;
-    std::vector<size_t> tabXofs, tabXa, tabYrow, tabYb;  // byte offsets in d_tabs per level
+    size_t pyrSmem = 0;  // orb_pyramid_kernel LDS: column table + source-level row rings
+    int xtabN = 0;
     int lastFrames = 0;
     // Stage timing with HIP events on the launch stream (bench.py roofline).
     static constexpr int kStages = 7, kRing = 512;
@@ -193,8 +173,8 @@ struct OrbPipeline {
         resizeGeneric = (p->compat & PLVI_COMPAT_RESIZE_V_GENERIC) ? 1 : 0;
         // Levels
         lv.resize(L);
-        rtab.resize(L);
         size_t off = 0, satOff = 0, carryOff = 0;
+        std::vector<uint32_t> xtab;
         int kpOff = 0;
         nodeCapMax = 0;
         for (int l = 0; l < L; ++l) {
@@ -264,7 +244,15 @@ struct OrbPipeline {
                     if (c.x1 > c.x0 && c.y1 > c.y0) cells.push_back(c);
                 }
             }
-            if (l > 0) rtab[l] = make_resize_tab(lv[l - 1].w, lv[l - 1].h, d.w, d.h);
+            // cv::resize scale from level l-1 (resize.cpp: scale_x = 1 / inv_scale_x)
+            if (l > 0) {
+                d.rsx = 1. / ((double)d.w / lv[l - 1].w);
+                d.rsy = 1. / ((double)d.h / lv[l - 1].h);
+                d.xtab = (int)xtab.size();
+                if (append_xtab(xtab, lv[l - 1].w, d.w)) return PLVI_E_BADARG;
+                // LDS: a kPyrRing-row ring of level 0, two rows of every other source level
+                pyrSmem += (l == 1 ? kPyrRing : 2) * (size_t)((lv[l - 1].w + 3) & ~3);
+            }
             // column strips of the blur + FAST kernel (candidate queue packs rows in 10 bits)
             if (d.h >= 1024) return PLVI_E_BADARG;
             for (int y0 = 0; y0 < d.h; y0 += kStripRows)
@@ -281,23 +269,12 @@ struct OrbPipeline {
         PLVI_CHECK(hipMemcpy(d_strips.p, strips.data(), sizeof(OrbStripDev) * strips.size(), hipMemcpyHostToDevice));
         PLVI_CHECK(hipMemcpy(d_lv.p, lv.data(), sizeof(OrbLevelDev) * L, hipMemcpyHostToDevice));
         PLVI_CHECK(hipMemcpy(d_cells.p, cells.data(), sizeof(OrbCellDev) * cells.size(), hipMemcpyHostToDevice));
-        std::vector<uint8_t> tabs;
-        tabXofs.assign(L, 0); tabXa.assign(L, 0); tabYrow.assign(L, 0); tabYb.assign(L, 0);
-        auto put = [&](const void* src, size_t n) {
-            size_t o = (tabs.size() + 15) & ~size_t(15);
-            tabs.resize(o + n);
-            std::memcpy(tabs.data() + o, src, n);
-            return o;
-        };
-        for (int l = 1; l < L; ++l) {
-            tabXofs[l] = put(rtab[l].xofs.data(), rtab[l].xofs.size() * 4);
-            tabXa[l] = put(rtab[l].xa.data(), rtab[l].xa.size() * 2);
-            tabYrow[l] = put(rtab[l].yrow.data(), rtab[l].yrow.size() * 4);
-            tabYb[l] = put(rtab[l].yb.data(), rtab[l].yb.size() * 2);
-        }
-        if (tabs.empty()) tabs.resize(16);
-        if (d_tabs.alloc(tabs.size())) return PLVI_E_HIP;
-        PLVI_CHECK(hipMemcpy(d_tabs.p, tabs.data(), tabs.size(), hipMemcpyHostToDevice));
+        xtabN = (int)xtab.size();
+        pyrSmem += 4 * (size_t)xtabN;
+        if (W > 4 * 64 * kPyrDw || pyrSmem > 64 * 1024) return PLVI_E_BADARG;  // orb_pyramid_kernel limits
+        if (xtab.empty()) xtab.push_back(0);
+        if (d_xtab.alloc(4 * xtab.size())) return PLVI_E_HIP;
+        PLVI_CHECK(hipMemcpy(d_xtab.p, xtab.data(), 4 * xtab.size(), hipMemcpyHostToDevice));
         PLVI_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax.data(), 16 * sizeof(int)));
         // work buffers
         if (pyr.alloc(off) || blur.alloc(off) || score.alloc(off) || cand.alloc(off) ||
@@ -323,20 +300,13 @@ struct OrbPipeline {
         uint8_t* Bl = blur.as<uint8_t>();
         uint8_t* Sc = score.as<uint8_t>();
         uint8_t* Cd = cand.as<uint8_t>();
-        const uint8_t* T = d_tabs.as<uint8_t>();
         mark(0, st);
-        // K1a: the pyramid (ComputePyramid, chained resize: level l from l-1;
-        // level 1 reads the caller's frames directly)
-        for (int l = 1; l < L; ++l) {
-            const OrbLevelDev& d = lv[l];
-            const OrbLevelDev& s = lv[l - 1];
-            dim3 grid((d.w + 63) / 64, (d.h + 3) / 4, nf);
-            const uint8_t* sp = l == 1 ? d_frames : (const uint8_t*)(P + s.off);
-            const size_t sf = l == 1 ? frame_stride : (size_t)s.plane, sr = l == 1 ? row_stride : (size_t)s.w;
-            hipLaunchKernelGGL(orb_resize_kernel, grid, dim3(256), 0, st, sp, sf, sr, P + d.off, d.w, d.h,
-                               (size_t)d.plane, (const int*)(T + tabXofs[l]), (const short*)(T + tabXa[l]),
-                               rtab[l].xmax, (const int*)(T + tabYrow[l]), (const short*)(T + tabYb[l]), resizeGeneric);
-        }
+        // K1a: the pyramid (ComputePyramid, chained resize: level l from l-1)
+        // of every frame in one streaming launch, one wave per frame
+        if (L > 1)
+            hipLaunchKernelGGL(orb_pyramid_kernel, dim3(nf), dim3(128), pyrSmem, st, d_lv.as<OrbLevelDev>(), L,
+                               d_frames, frame_stride, row_stride, P, (const uint32_t*)d_xtab.as<uint32_t>(), xtabN,
+                               resizeGeneric);
         // K1b: blur + FAST score of every level (level 0 also copies the frame into its plane)
         const bool kt = ktime && kn < kKRing;
         if (kt) PLVI_CHECK(hipEventRecord(kev[2 * kn], st));

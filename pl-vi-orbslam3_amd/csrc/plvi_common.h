@@ -21,6 +21,13 @@ namespace plvi {
 
 constexpr int kWave = 64;
 
+// LDS pointers carry address space 3 so every access is a ds_* instruction
+// (a generic pointer turns them into flat accesses that wait on vmcnt too).
+typedef unsigned __attribute__((address_space(3))) lds_u32;
+typedef float __attribute__((address_space(3))) lds_f32;
+typedef uint8_t __attribute__((address_space(3))) lds_u8;
+typedef int __attribute__((address_space(3))) lds_i32;
+
 __host__ __device__ inline int reflect101(int p, int len) {
     if (len == 1) return 0;
     while (p < 0 || p >= len) p = p < 0 ? -p : 2 * len - 2 - p;

@@ -284,6 +284,160 @@ __global__ __launch_bounds__(256) void search_by_projection_kernel(
     if (tid == 0) nmatches[pr] = s_nm;
 }
 
+// ---------------------------------------------------------------------------
+// ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>&, th,
+// bFarPoints, thFarPoints) (src/ORBmatcher.cc:44-145, F.Nleft == -1): the
+// local-map search of Tracking::SearchLocalPoints (Tracking.cc:5119/5211).
+// Same schedule as above: phase 1 scans every MapPoint's window in parallel
+// against the flags on entry and keeps its best and second candidate
+// (first argmin, then first argmin of the rest -- the scan order of
+// GetFeaturesInArea); phase 2 walks the MapPoints in vector order and
+// re-scans only one whose best or second candidate was blocked meanwhile
+// (removing any other candidate leaves both unchanged), then applies the
+// level-aware ratio test and the assignment.
+__device__ void local_scan(const plvi_local_params& p, const ProjLds& s, const unsigned char* blk, int m,
+                           const unsigned char* __restrict__ fl, const float* __restrict__ proj,
+                           const int* __restrict__ lvl, const uint8_t* __restrict__ mpdesc,
+                           const uint8_t* __restrict__ cdesc, const float* __restrict__ uright, unsigned* b1,
+                           unsigned* b2) {
+    *b1 = *b2 = 0xFFFFFFFFu;
+    if (!(fl[m] & 1)) return;
+    const float x = proj[4 * m], y = proj[4 * m + 1], xr = proj[4 * m + 2], vcos = proj[4 * m + 3];
+    const int L = lvl[m];
+    float r = vcos > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos (:216-222)
+    if (p.th != 1.0) r *= p.th;
+    const float radius = r * p.scale_factors[L];
+    const int minLevel = L - 1, maxLevel = L;
+    const int nMinCellX = max(0, (int)floorf((x - p.min_x - radius) * p.inv_w));
+    if (nMinCellX >= kGridCols) return;
+    const int nMaxCellX = min(kGridCols - 1, (int)ceilf((x - p.min_x + radius) * p.inv_w));
+    if (nMaxCellX < 0) return;
+    const int nMinCellY = max(0, (int)floorf((y - p.min_y - radius) * p.inv_h));
+    if (nMinCellY >= kGridRows) return;
+    const int nMaxCellY = min(kGridRows - 1, (int)ceilf((y - p.min_y + radius) * p.inv_h));
+    if (nMaxCellY < 0) return;
+    const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+    const uint4* dm = reinterpret_cast<const uint4*>(mpdesc + (size_t)32 * m);
+    const uint4 m0 = dm[0], m1 = dm[1];
+    int bestDist = 256, bestDist2 = 256, bestIdx = -1, secondIdx = -1;
+    for (int ix = nMinCellX; ix <= nMaxCellX; ++ix) {
+        const int k0 = s.cell_off[ix * kGridRows + nMinCellY], k1 = s.cell_off[ix * kGridRows + nMaxCellY + 1];
+        for (int k = k0; k < k1; ++k) {
+            const int idx = s.cell_idx[k];
+            if (bCheckLevels) {
+                const int o = s.koct[idx];
+                if (o < minLevel) continue;
+                if (maxLevel >= 0 && o > maxLevel) continue;
+            }
+            const float distx = s.kx[idx] - x, disty = s.ky[idx] - y;
+            if (!(fabsf(distx) < radius && fabsf(disty) < radius)) continue;
+            if (blk[idx]) continue;
+            if (uright && uright[idx] > 0) {
+                const float er = fabsf(xr - uright[idx]);
+                if (er > radius) continue;
+            }
+            const uint4* dc = reinterpret_cast<const uint4*>(cdesc + (size_t)32 * idx);
+            const uint4 c0 = dc[0], c1 = dc[1];
+            const int dist = __popc(m0.x ^ c0.x) + __popc(m0.y ^ c0.y) + __popc(m0.z ^ c0.z) + __popc(m0.w ^ c0.w) +
+                             __popc(m1.x ^ c1.x) + __popc(m1.y ^ c1.y) + __popc(m1.z ^ c1.z) + __popc(m1.w ^ c1.w);
+            if (dist < bestDist) {
+                bestDist2 = bestDist;
+                secondIdx = bestIdx;
+                bestDist = dist;
+                bestIdx = idx;
+            } else if (dist < bestDist2) {
+                bestDist2 = dist;
+                secondIdx = idx;
+            }
+        }
+    }
+    if (bestIdx < 0) return;
+    *b1 = ((unsigned)bestDist << 16) | (unsigned)bestIdx;
+    if (secondIdx >= 0) *b2 = ((unsigned)bestDist2 << 16) | (unsigned)secondIdx;
+}
+
+__global__ __launch_bounds__(256) void search_local_kernel(
+    plvi_local_params p, const plvi_keypoint* __restrict__ ckps, const uint8_t* __restrict__ cdesc_all,
+    const int* __restrict__ cur_n, int cur_cap, const uint8_t* __restrict__ cblocked, const float* __restrict__ curight,
+    const int* __restrict__ cell_off_all, const int* __restrict__ cell_idx_all, const uint8_t* __restrict__ flags_all,
+    const float* __restrict__ proj_all, const int* __restrict__ level_all, const uint8_t* __restrict__ mpdesc_all,
+    const int* __restrict__ mp_n, int mp_cap, int* __restrict__ match, int* __restrict__ nmatches) {
+    extern __shared__ __align__(16) unsigned char lds[];
+    const int fr = blockIdx.x, tid = threadIdx.x;
+    const int nc = min(cur_n[fr], cur_cap), nm = min(mp_n[fr], mp_cap);
+    ProjLds s;
+    unsigned *best1, *best2;
+    {
+        unsigned char* q = lds;
+        s.kx = reinterpret_cast<float*>(q); q += 4 * cur_cap;
+        s.ky = reinterpret_cast<float*>(q); q += 4 * cur_cap;
+        s.assign = reinterpret_cast<int*>(q); q += 4 * cur_cap;
+        best1 = reinterpret_cast<unsigned*>(q); q += 4 * mp_cap;
+        best2 = reinterpret_cast<unsigned*>(q); q += 4 * mp_cap;
+        s.cell_off = reinterpret_cast<int*>(q); q += 4 * (kGridCells + 1);
+        s.cell_idx = reinterpret_cast<unsigned short*>(q); q += 2 * cur_cap;
+        s.koct = q; q += cur_cap;
+        s.blocked = q; q += cur_cap;
+        s.pre = q;
+    }
+    const plvi_keypoint* K = ckps + (size_t)fr * cur_cap;
+    const uint8_t* cdesc = cdesc_all + (size_t)fr * cur_cap * 32;
+    const float* ur = curight ? curight + (size_t)fr * cur_cap : nullptr;
+    for (int i = tid; i < nc; i += 256) {
+        s.kx[i] = K[i].x;
+        s.ky[i] = K[i].y;
+        s.koct[i] = (unsigned char)K[i].octave;
+        const unsigned char b = cblocked ? cblocked[(size_t)fr * cur_cap + i] : 0;
+        s.blocked[i] = b;
+        s.pre[i] = b;
+        s.assign[i] = -1;
+    }
+    const int* CO = cell_off_all + (size_t)fr * (kGridCells + 1);
+    for (int c = tid; c <= kGridCells; c += 256) s.cell_off[c] = CO[c];
+    const int ncell = CO[kGridCells];
+    for (int k = tid; k < ncell; k += 256) s.cell_idx[k] = (unsigned short)cell_idx_all[(size_t)fr * cur_cap + k];
+    __syncthreads();
+    const unsigned char* fl = flags_all + (size_t)fr * mp_cap;
+    const float* proj = proj_all + (size_t)fr * mp_cap * 4;
+    const int* lvl = level_all + (size_t)fr * mp_cap;
+    const uint8_t* mpdesc = mpdesc_all + (size_t)fr * mp_cap * 32;
+    // phase 1: every MapPoint against the flags on entry
+    for (int m = tid; m < nm; m += 256) local_scan(p, s, s.pre, m, fl, proj, lvl, mpdesc, cdesc, ur, &best1[m], &best2[m]);
+    __syncthreads();
+    // phase 2: the assignment in vpMapPoints order (:98-117)
+    if (tid == 0) {
+        int nmt = 0;
+        for (int m = 0; m < nm; ++m) {
+            unsigned b1 = best1[m], b2 = best2[m];
+            if (b1 == 0xFFFFFFFFu) continue;
+            const int i1 = (int)(b1 & 0xFFFFu), i2 = b2 == 0xFFFFFFFFu ? -1 : (int)(b2 & 0xFFFFu);
+            if (s.blocked[i1] != s.pre[i1] || (i2 >= 0 && s.blocked[i2] != s.pre[i2])) {
+                local_scan(p, s, s.blocked, m, fl, proj, lvl, mpdesc, cdesc, ur, &b1, &b2);  // blocked meanwhile
+                if (b1 == 0xFFFFFFFFu) continue;
+            }
+            const int bestDist = (int)(b1 >> 16), bestIdx = (int)(b1 & 0xFFFFu);
+            const int bestDist2 = b2 == 0xFFFFFFFFu ? 256 : (int)(b2 >> 16);
+            const int bestLevel = s.koct[bestIdx], bestLevel2 = b2 == 0xFFFFFFFFu ? -1 : s.koct[b2 & 0xFFFFu];
+            if (bestDist <= kProjThHigh) {
+                if (bestLevel == bestLevel2 && bestDist > p.nnratio * bestDist2) continue;
+                if (bestLevel != bestLevel2 || bestDist <= p.nnratio * bestDist2) {
+                    s.assign[bestIdx] = m;
+                    s.blocked[bestIdx] = (fl[m] & 2) ? 1 : 0;  // the stored MapPoint's Observations() > 0
+                    ++nmt;
+                }
+            }
+        }
+        nmatches[fr] = nmt;
+    }
+    __syncthreads();
+    int* M = match + (size_t)fr * cur_cap;
+    for (int i = tid; i < nc; i += 256) M[i] = s.assign[i];
+}
+
+static size_t local_smem(int cur_cap, int mp_cap) {
+    return (size_t)cur_cap * (4 + 4 + 4 + 2 + 1 + 1 + 1) + (size_t)mp_cap * 8 + 4 * (kGridCells + 1) + 64;
+}
+
 static size_t proj_smem(int cur_cap, int last_cap) {
     return (size_t)cur_cap * (4 + 4 + 4 + 2 + 1 + 1 + 1 + 1) + (size_t)last_cap * (4 + 4) + 4 * (kGridCells + 1) + 64;
 }
@@ -392,4 +546,79 @@ extern "C" int plvi_search_by_projection(const plvi_proj_params* p, const plvi_k
     PLVI_CHECK(hipMemcpy(match, B + off[oM], 4 * (size_t)n_cur, hipMemcpyDeviceToHost));
     PLVI_CHECK(hipMemcpy(&nm, dN + 2, 4, hipMemcpyDeviceToHost));
     return nm;
+}
+
+extern "C" int plvi_search_local_batch(int n_frames, const plvi_local_params* p, const plvi_keypoint* d_kps,
+                                       const uint8_t* d_desc, const int* d_n, int cap, const uint8_t* d_blocked,
+                                       const float* d_uright, const int* d_cell_off, const int* d_cell_idx,
+                                       const uint8_t* d_mp_flags, const float* d_mp_proj, const int* d_mp_level,
+                                       const uint8_t* d_mp_desc, const int* d_mp_n, int mp_cap, int* d_match,
+                                       int* d_nmatches, void* stream) {
+    if (!p || n_frames < 0 || cap < 1 || mp_cap < 1 || cap > 65535) return PLVI_E_BADARG;
+    if (p->nlevels < 1 || p->nlevels > 16) return PLVI_E_BADARG;
+    if (n_frames == 0) return PLVI_OK;
+    const size_t smem = local_smem(cap, mp_cap);
+    if (smem > 160 * 1024) return PLVI_E_CAPACITY;
+    PLVI_CHECK(hipFuncSetAttribute((const void*)search_local_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)smem));
+    hipLaunchKernelGGL(search_local_kernel, dim3(n_frames), dim3(256), smem, (hipStream_t)stream, *p, d_kps, d_desc,
+                       d_n, cap, d_blocked, d_uright, d_cell_off, d_cell_idx, d_mp_flags, d_mp_proj, d_mp_level,
+                       d_mp_desc, d_mp_n, mp_cap, d_match, d_nmatches);
+    PLVI_CHECK(hipGetLastError());
+    return PLVI_OK;
+}
+
+// One frame from host memory, synchronous (grid built on the device).
+extern "C" int plvi_search_local(const plvi_local_params* p, const plvi_keypoint* kps, const uint8_t* desc, int n,
+                                 const uint8_t* blocked, const float* uright, const uint8_t* mp_flags,
+                                 const float* mp_proj, const int* mp_level, const uint8_t* mp_desc, int n_mp,
+                                 int* match) {
+    if (!p || n < 0 || n_mp < 0 || (n > 0 && (!kps || !desc || !match))) return PLVI_E_BADARG;
+    if (n == 0) return 0;
+    const int cc = n, mc = std::max(n_mp, 1);
+    std::vector<size_t> off;
+    size_t tot = 0;
+    auto put = [&](size_t bytes) {
+        off.push_back(tot);
+        tot += (bytes + 255) & ~size_t(255);
+        return off.size() - 1;
+    };
+    const size_t oK = put(sizeof(plvi_keypoint) * cc), oD = put(32 * (size_t)cc), oB = put(cc), oU = put(4 * (size_t)cc);
+    const size_t oCO = put(4 * (size_t)(kGridCells + 1)), oCI = put(4 * (size_t)cc), oF = put(mc);
+    const size_t oP = put(16 * (size_t)mc), oL = put(4 * (size_t)mc), oMD = put(32 * (size_t)mc);
+    const size_t oM = put(4 * (size_t)cc), oN = put(16);
+    DevBuf d;
+    if (d.alloc(tot)) return PLVI_E_HIP;
+    uint8_t* B = d.as<uint8_t>();
+    auto up = [&](size_t slot, const void* src, size_t bytes) -> int {
+        if (src && bytes) PLVI_CHECK(hipMemcpy(B + off[slot], src, bytes, hipMemcpyHostToDevice));
+        return PLVI_OK;
+    };
+    int rc = up(oK, kps, sizeof(plvi_keypoint) * cc) | up(oD, desc, 32 * (size_t)cc);
+    if (blocked) rc |= up(oB, blocked, cc);
+    else PLVI_CHECK(hipMemset(B + off[oB], 0, cc));
+    if (uright) rc |= up(oU, uright, 4 * (size_t)cc);
+    if (n_mp > 0)
+        rc |= up(oF, mp_flags, n_mp) | up(oP, mp_proj, 16 * (size_t)n_mp) | up(oL, mp_level, 4 * (size_t)n_mp) |
+              up(oMD, mp_desc, 32 * (size_t)n_mp);
+    if (rc) return PLVI_E_HIP;
+    int counts[2] = {n, n_mp};
+    PLVI_CHECK(hipMemcpy(B + off[oN], counts, 8, hipMemcpyHostToDevice));
+    int* dN = reinterpret_cast<int*>(B + off[oN]);
+    plvi_grid_params gp{p->min_x, p->min_y, p->inv_w, p->inv_h};
+    rc = plvi_assign_grid_batch(reinterpret_cast<const plvi_keypoint*>(B + off[oK]), dN, cc, 1, &gp,
+                                reinterpret_cast<int*>(B + off[oCO]), reinterpret_cast<int*>(B + off[oCI]), nullptr);
+    if (rc) return rc;
+    rc = plvi_search_local_batch(1, p, reinterpret_cast<const plvi_keypoint*>(B + off[oK]), B + off[oD], dN, cc,
+                                 B + off[oB], uright ? reinterpret_cast<const float*>(B + off[oU]) : nullptr,
+                                 reinterpret_cast<const int*>(B + off[oCO]), reinterpret_cast<const int*>(B + off[oCI]),
+                                 B + off[oF], reinterpret_cast<const float*>(B + off[oP]),
+                                 reinterpret_cast<const int*>(B + off[oL]), B + off[oMD], dN + 1, mc,
+                                 reinterpret_cast<int*>(B + off[oM]), dN + 2, nullptr);
+    if (rc) return rc;
+    PLVI_CHECK(hipDeviceSynchronize());
+    int nmt = 0;
+    PLVI_CHECK(hipMemcpy(match, B + off[oM], 4 * (size_t)n, hipMemcpyDeviceToHost));
+    PLVI_CHECK(hipMemcpy(&nmt, dN + 2, 4, hipMemcpyDeviceToHost));
+    return nmt;
 }

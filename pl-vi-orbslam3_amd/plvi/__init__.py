@@ -104,6 +104,13 @@ class ProjParams(ctypes.Structure):
                 ("scale_factors", ctypes.c_float * 16)]
 
 
+class LocalParams(ctypes.Structure):
+    """plvi_local_params (include/plvi_frontend.h): ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>...)."""
+    _fields_ = [("min_x", ctypes.c_float), ("min_y", ctypes.c_float), ("inv_w", ctypes.c_float),
+                ("inv_h", ctypes.c_float), ("th", ctypes.c_float), ("nnratio", ctypes.c_float),
+                ("nlevels", ctypes.c_int), ("scale_factors", ctypes.c_float * 16)]
+
+
 def grid_geometry(width, height):
     """Frame ctor grid geometry without distortion (mnMinX = 0, mnMaxX = cols, ...;
     Frame.cc:156-157): (min_x, max_x, min_y, max_y, inv_w, inv_h) as float32."""
@@ -180,6 +187,8 @@ def _declare(lib):
         "plvi_image_bounds": ([V, I, I, V], I),
         "plvi_search_by_projection_batch": ([I, V, V, V, V, I, V, V, V, V, V, V, V, V, V, V, I, V, V, V], I),
         "plvi_search_by_projection": ([V, V, V, I, V, V, V, V, V, V, V, I, V], I),
+        "plvi_search_local_batch": ([I, V, V, V, V, I, V, V, V, V, V, V, V, V, V, I, V, V, V], I),
+        "plvi_search_local": ([V, V, V, I, V, V, V, V, V, V, I, V], I),
         "plvi_vocab_load_text": ([ctypes.c_char_p, I, I, c_void_pp], I),
         "plvi_vocab_create": ([I, I, I, I, I, V, V, V, V, I, c_void_pp], I),
         "plvi_vocab_destroy": ([V], I),
@@ -655,6 +664,30 @@ class ORBmatcher:
                                                         _ptr(la), _ptr(md), _ptr(lf), len(lf), _ptr(out)),
                     "plvi_search_by_projection")
         return nm, out[:n]
+
+    def SearchByProjectionLocal(self, params, kps, desc, mp_flags, mp_proj, mp_level, mp_desc, blocked=None,
+                                uright=None):
+        """SearchByProjection(Frame&, const vector<MapPoint*>&, th, bFarPoints, thFarPoints)
+        (src/ORBmatcher.cc:44-145, monocular / rectified branch) with this matcher's nnratio.  params:
+        LocalParams (grid, th, scale factors); kps: F.mvKeysUn; mp_*: per MapPoint (vector order) flags (bit0
+        searched, bit1 Observations() > 0), proj (n x 4: mTrackProjX, mTrackProjY, mTrackProjXR,
+        mTrackViewCos), mnTrackScaleLevel, descriptor.  Returns (nmatches, match) with match[idx] = MapPoint
+        index stored in F.mvpMapPoints[idx] or -1."""
+        params.nnratio = self.nnratio
+        k = np.ascontiguousarray(kps).view(KEYPOINT_DTYPE)
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        fl = np.ascontiguousarray(mp_flags, np.uint8)
+        pr = np.ascontiguousarray(mp_proj, np.float32).reshape(-1, 4)
+        lv = np.ascontiguousarray(mp_level, np.int32)
+        md = np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32)
+        cb = None if blocked is None else np.ascontiguousarray(blocked, np.uint8)
+        cu = None if uright is None else np.ascontiguousarray(uright, np.float32)
+        out = np.full(max(len(k), 1), -1, np.int32)
+        nm = _check(self._lib.plvi_search_local(ctypes.byref(params), _ptr(k), _ptr(d), len(k),
+                                                None if cb is None else _ptr(cb), None if cu is None else _ptr(cu),
+                                                _ptr(fl), _ptr(pr), _ptr(lv), _ptr(md), len(fl), _ptr(out)),
+                    "plvi_search_local")
+        return nm, out[:len(k)]
 
     @staticmethod
     def DescriptorDistance(a, b, line_matcher_quirk=False):

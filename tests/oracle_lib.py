@@ -430,6 +430,33 @@ def search_by_projection(case, th, forward=0, backward=0, check_ori=1):
     return n, out[:len(kx)]
 
 
+def search_local(case, th, nnratio=0.8):
+    """ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th, ...) restatement -> (nmatches, match)."""
+    lib = load()
+    V, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    lib.oracle_search_local.argtypes = [I, V, V, V, V, V, V, F, F, F, F, V, F, F, I, V, V, V, V, V, V, V, V]
+    lib.oracle_search_local.restype = I
+    c = case
+    k = c["cur_kps"]
+    kx = np.ascontiguousarray(k["x"], np.float32); ky = np.ascontiguousarray(k["y"], np.float32)
+    ko = np.ascontiguousarray(k["octave"], np.int32)
+    cd = np.ascontiguousarray(c["cur_desc"], np.uint8)
+    cb = np.ascontiguousarray(c["cur_blocked"], np.uint8)
+    cu = None if c.get("cur_uright") is None else np.ascontiguousarray(c["cur_uright"], np.float32)
+    min_x, _, min_y, _, inv_w, inv_h = c["grid"]
+    sf = np.ascontiguousarray(c["scale_factors"], np.float32)
+    fl = np.ascontiguousarray(c["mp_flags"], np.uint8)
+    pr = np.ascontiguousarray(c["mp_proj"], np.float32)
+    px, py, pxr, vc = (np.ascontiguousarray(pr[:, j]) for j in range(4))
+    lv = np.ascontiguousarray(c["mp_level"], np.int32)
+    md = np.ascontiguousarray(c["mp_desc"], np.uint8)
+    out = np.full(max(len(kx), 1), -1, np.int32)
+    n = lib.oracle_search_local(len(kx), _p(kx), _p(ky), _p(ko), _p(cd), _p(cb), None if cu is None else _p(cu),
+                                min_x, min_y, inv_w, inv_h, _p(sf), nnratio, th, len(fl), _p(fl), _p(px), _p(py),
+                                _p(pxr), _p(vc), _p(lv), _p(md), _p(out))
+    return n, out[:len(kx)]
+
+
 def undistort_points(K4, dist, xy):
     lib = load()
     V, I = ctypes.c_void_p, ctypes.c_int

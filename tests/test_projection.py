@@ -151,3 +151,42 @@ def test_assign_grid_and_projection_batch_device():
         n_ref, m_ref = oracle_lib.search_by_projection(c, 15.0)
         assert N[p] == n_ref
         np.testing.assert_array_equal(M[p, :len(m_ref)], m_ref)
+
+
+# ------------------------------------------------- local-map search (ORBmatcher.cc:44-145)
+def test_oracle_local_search_sanity():
+    case = util.local_case(0)
+    n, m = oracle_lib.search_local(case, 1.0)
+    assert n > 200 and (m >= 0).sum() <= n
+    # blocked keypoints never receive a MapPoint
+    assert (m[case["cur_blocked"] == 1] == -1).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,th,uright", [(0, 1.0, False), (1, 3.0, False), (2, 1.0, True), (3, 10.0, False),
+                                            (4, 1.0, False), (5, 5.0, True)])
+def test_local_search_matches_oracle(seed, th, uright):
+    import plvi
+    case = util.local_case(seed, uright=uright)
+    ne, me = oracle_lib.search_local(case, th, 0.8)
+    mt = plvi.ORBmatcher(0.8, True)
+    ng, mg = mt.SearchByProjectionLocal(util.local_params(case, th), case["cur_kps"], case["cur_desc"],
+                                        case["mp_flags"], case["mp_proj"], case["mp_level"], case["mp_desc"],
+                                        case["cur_blocked"], case["cur_uright"])
+    assert ng == ne
+    np.testing.assert_array_equal(mg, me)
+
+
+@pytest.mark.gpu
+def test_local_search_degenerate():
+    import plvi
+    case = util.local_case(9, n_cur=50, n_mp=1)
+    mt = plvi.ORBmatcher(0.8, True)
+    for nmp in (0, 1):
+        c = dict(case)
+        for k in ("mp_flags", "mp_proj", "mp_level", "mp_desc"):
+            c[k] = case[k][:nmp]
+        ne, me = oracle_lib.search_local(c, 1.0)
+        ng, mg = mt.SearchByProjectionLocal(util.local_params(c, 1.0), c["cur_kps"], c["cur_desc"], c["mp_flags"],
+                                            c["mp_proj"], c["mp_level"], c["mp_desc"], c["cur_blocked"])
+        assert ng == ne and np.array_equal(mg, me)

@@ -172,6 +172,57 @@ def projection_case(seed, n_cur=1000, n_last=900, W=752, H=480, uright=False, du
     return case
 
 
+def local_case(seed, n_cur=1000, n_mp=1500, W=752, H=480, uright=False, dup=0.15):
+    """Synthetic local-map search input (ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>...),
+    SURVEY 8f / VERDICT r1 item 8): current-frame keypoints with octaves and descriptors; MapPoints whose
+    predicted projections fall near a keypoint (75 %) or anywhere, predicted level = the keypoint's octave
+    +-1, descriptors = the keypoint's with ~6 % bit flips (ties and near-ties via duplicated MapPoints:
+    `dup` of them aim at an earlier MapPoint's keypoint, so the sequential blocking matters), some not in
+    view / bad, most with Observations() > 0, a few keypoints pre-blocked; view cosines on both sides of
+    RadiusByViewingCos's 0.998."""
+    from plvi import KEYPOINT_DTYPE, grid_geometry
+    rng = np.random.default_rng(seed)
+    kps = np.zeros(n_cur, KEYPOINT_DTYPE)
+    kps["x"] = rng.uniform(-3, W + 3, n_cur).astype(np.float32)
+    kps["y"] = rng.uniform(-3, H + 3, n_cur).astype(np.float32)
+    kps["octave"] = np.minimum(rng.geometric(0.35, n_cur) - 1, 7)
+    kps["size"] = 31
+    kps["class_id"] = -1
+    desc = rng.integers(0, 256, (n_cur, 32), dtype=np.uint8)
+    near = rng.random(n_mp) < 0.75
+    src = rng.integers(0, n_cur, n_mp)
+    nd = int(dup * n_mp)
+    src[-nd:] = src[rng.integers(0, n_mp - nd, nd)]
+    px = np.where(near, kps["x"][src] + rng.normal(0, 1.5, n_mp), rng.uniform(0, W, n_mp)).astype(np.float32)
+    py = np.where(near, kps["y"][src] + rng.normal(0, 1.5, n_mp), rng.uniform(0, H, n_mp)).astype(np.float32)
+    pxr = (px - rng.uniform(0, 30, n_mp)).astype(np.float32)
+    vc = np.where(rng.random(n_mp) < 0.5, rng.uniform(0.999, 1.0, n_mp), rng.uniform(0.5, 0.998, n_mp)).astype(
+        np.float32)
+    lvl = np.clip(np.where(near, kps["octave"][src] + rng.integers(-1, 2, n_mp), rng.integers(0, 8, n_mp)), 0, 7)
+    bits = np.unpackbits(desc[src], axis=1)
+    bits ^= (rng.random(bits.shape) < 0.06).astype(np.uint8)
+    md = np.where(near[:, None], np.packbits(bits, axis=1), rng.integers(0, 256, (n_mp, 32), dtype=np.uint8))
+    flags = ((rng.random(n_mp) < 0.9).astype(np.uint8) | ((rng.random(n_mp) < 0.85).astype(np.uint8) << 1))
+    case = {"cur_kps": kps, "cur_desc": desc, "cur_blocked": (rng.random(n_cur) < 0.05).astype(np.uint8),
+            "cur_uright": None, "grid": grid_geometry(W, H), "scale_factors": orb_scale_factors(),
+            "mp_flags": flags, "mp_proj": np.stack([px, py, pxr, vc], 1).astype(np.float32),
+            "mp_level": lvl.astype(np.int32), "mp_desc": md.astype(np.uint8)}
+    if uright:
+        case["cur_uright"] = np.where(rng.random(n_cur) < 0.6, kps["x"] - rng.uniform(0, 30, n_cur), -1).astype(
+            np.float32)
+    return case
+
+
+def local_params(case, th):
+    import plvi
+    p = plvi.LocalParams()
+    min_x, _, min_y, _, inv_w, inv_h = case["grid"]
+    p.min_x, p.min_y, p.inv_w, p.inv_h, p.th, p.nlevels = min_x, min_y, inv_w, inv_h, th, 8
+    for i, s in enumerate(case["scale_factors"]):
+        p.scale_factors[i] = s
+    return p
+
+
 def proj_params(case, th, forward=0, backward=0):
     import plvi
     p = plvi.ProjParams()
