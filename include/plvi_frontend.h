@@ -338,6 +338,42 @@ int plvi_line_match_grid_batch(int n_pairs, const int* d_lines1, const uint8_t* 
                                int cap2, int win_w0, int win_w1, int win_h0, int win_h1, int libstdcxx_range_hint,
                                int* d_matches_12, int* d_nmatches, int* d_err, void* stream);
 
+/* LineMatcher::SearchByProjection(Frame& CurrentFrame, Frame& LastFrame,
+ * const GridStructure& grid, th, angth) (src/LineMatcher.cpp:274-372; its
+ * Tracking.cc:3976/3984 call sites are commented out in the reference, kept
+ * for drop-in completeness).  Per last-frame line (in order): flags bit0 =
+ * mvpMapLines[i] && !mvbOutlier_Line[i], bit1 = that MapLine's
+ * Observations() > 0; x3dc[6] = Rcw*x3Dw+tcw of its start and end point
+ * (cv::Mat float, the caller's); octave = mvKeys_Line[i].octave; the
+ * MapLine descriptor.  Current frame: mvKeysUn_Line angles, descriptors,
+ * blocked = mvpMapLines[i2] && Observations() > 0 on entry (NULL = none),
+ * grid_Line as in plvi_line_match_grid (cell (x, y) = x * rows + y, list
+ * order).  Output match [cur] = last-frame line whose MapLine the call
+ * stores in mvpMapLines[i2], -1 untouched; the count of assignments. */
+typedef struct plvi_line_proj_params {
+  float fx, fy, cx, cy;             /* Pinhole mvParameters */
+  float min_x, max_x, min_y, max_y; /* mnMinX, mnMaxX, mnMinY, mnMaxY */
+  double inv_w, inv_h;              /* Frame::inv_width / inv_height (grid cells per pixel) */
+  float th, angth;
+  int grid_cols, grid_rows;
+  int range_hint;                   /* unordered_set range-insert rule: 1 = GCC <= 10, 0 = GCC >= 11 */
+  int nlevels;                      /* <= 8 */
+  float scale_l[8];                 /* CurrentFrame.mvScaleFactors_l */
+} plvi_line_proj_params;
+
+int plvi_line_search_projection_batch(int n_pairs, const plvi_line_proj_params* p, const float* d_cur_angle,
+                                      const uint8_t* d_cur_desc, const uint8_t* d_cur_blocked, const int* d_cur_n,
+                                      int cur_cap, const int* d_cell_off, const int* d_cell_idx, int idx_cap,
+                                      const uint8_t* d_last_flags, const float* d_x3dc, const int* d_last_octave,
+                                      const uint8_t* d_ml_desc, const int* d_last_n, int last_cap, int* d_match,
+                                      int* d_nmatches, int* d_err, void* stream);
+/* One pair from host memory, synchronous (n_cur <= 2048).  Returns the
+ * count or an error (PLVI_E_CAPACITY when a candidate set exceeds 1024). */
+int plvi_line_search_projection(const plvi_line_proj_params* p, const float* cur_angle, const uint8_t* cur_desc,
+                                const uint8_t* cur_blocked, int n_cur, const int* cell_off, const int* cell_idx,
+                                const uint8_t* last_flags, const float* x3dc, const int* last_octave,
+                                const uint8_t* ml_desc, int n_last, int* match);
+
 /* ------------------------------------------------------------- Vocabulary
  * DBoW2::TemplatedVocabulary<FORB::TDescriptor, FORB>
  * (Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h), the ORB vocabulary of

@@ -342,3 +342,82 @@ extern "C" int oracle_uset_order(const int* seq_off, const int* seq, int nseq, i
     for (int v : s) out[n++] = v;
     return n;
 }
+
+// LineMatcher::SearchByProjection(Frame& CurrentFrame, Frame& LastFrame,
+// const GridStructure& grid, th, angth) (src/LineMatcher.cpp:274-372).
+// The per-line MapLine state is evaluated by the caller: last_flags bit0 =
+// mvpMapLines[i] && !mvbOutlier_Line[i], bit1 = that MapLine's Observations() > 0;
+// x3dc = Rcw*x3Dw+tcw of its two endpoints (cv::Mat float, 6 floats);
+// last_oct = mvKeys_Line[i].octave.  Current frame: mvKeysUn_Line angles,
+// descriptors, blocked = mvpMapLines[i2] && Observations() > 0 on entry,
+// grid_Line as CSR cells (x * rows + y) in std::list order.  inv_w / inv_h
+// are Frame::inv_width / inv_height (double).  Literal: the second endpoint's
+// grid y is uv_ep.x * inv_height (:329), atan2 of floats is the float
+// overload (std::atan2(float, float) via the `using namespace std` of
+// GeometricCamera.h).  match[i2] = last-frame line whose MapLine is stored in
+// mvpMapLines[i2] (-1 untouched); returns matches (every assignment counts).
+extern "C" int oracle_line_search_projection(
+    int n_cur, const float* cur_angle, const uint8_t* cur_desc, const uint8_t* cur_blocked, int cols, int rows,
+    const int* cell_off, const int* cell_idx, int n_last, const uint8_t* last_flags, const float* x3dc,
+    const int* last_oct, const uint8_t* ml_desc, float fx, float fy, float cx, float cy, float minX, float maxX,
+    float minY, float maxY, double inv_w, double inv_h, const float* scale_l, float th, float angth, int range_hint,
+    int* match) {
+    std::vector<std::vector<std::list<int>>> grid(cols, std::vector<std::list<int>>(rows));
+    for (int x = 0; x < cols; ++x)
+        for (int y = 0; y < rows; ++y)
+            for (int k = cell_off[x * rows + y]; k < cell_off[x * rows + y + 1]; ++k) grid[x][y].push_back(cell_idx[k]);
+    auto get = [&](int x, int y, int win, std::unordered_set<int>& indices) {
+        int min_x = std::max(0, x - win), max_x = std::min(cols, x + win + 1);
+        int min_y = std::max(0, y - win), max_y = std::min(rows, y + win + 1);
+        for (int x_ = min_x; x_ < max_x; ++x_)
+            for (int y_ = min_y; y_ < max_y; ++y_) {
+                if (range_hint) insert_range_gcc10(indices, grid[x_][y_]);
+                else indices.insert(grid[x_][y_].begin(), grid[x_][y_].end());
+            }
+    };
+    std::vector<char> blocked(cur_blocked, cur_blocked + n_cur);
+    for (int i = 0; i < n_cur; ++i) match[i] = -1;
+    const int TH_HIGH = 120;
+    int matches = 0;
+    for (int i = 0; i < n_last; i++) {
+        if (!(last_flags[i] & 1)) continue;
+        const float* sp = x3dc + 6 * (size_t)i;
+        const float* ep = sp + 3;
+        const float invzc_sp = 1.0 / sp[2];
+        const float invzc_ep = 1.0 / ep[2];
+        if (invzc_sp < 0 || invzc_ep < 0) continue;
+        const float usx = fx * sp[0] / sp[2] + cx, usy = fy * sp[1] / sp[2] + cy;  // Pinhole::project
+        const float uex = fx * ep[0] / ep[2] + cx, uey = fy * ep[1] / ep[2] + cy;
+        if (usx < minX || usx > maxX || uex < minX || uex > maxX) continue;
+        if (usy < minY || usy > maxY || uey < minY || uey > maxY) continue;
+        const int nLastOctave = last_oct[i];
+        int window = std::floor(th);
+        if (scale_l[nLastOctave] > 1) window = std::floor(th + scale_l[nLastOctave]);
+        const std::pair<int, int> spoint = std::make_pair(usx * inv_w, usy * inv_h);
+        const std::pair<int, int> epoint = std::make_pair(uex * inv_w, uex * inv_h);  // sic (:329)
+        std::unordered_set<int> candidates;
+        get(spoint.first, spoint.second, window, candidates);
+        get(epoint.first, epoint.second, window, candidates);
+        if (candidates.empty()) continue;
+        int bestDist = 256, bestidx = -1;
+        for (const int& i2 : candidates) {
+            if (blocked[i2]) continue;
+            const int dist = descriptor_distance(ml_desc + 32 * (size_t)i, cur_desc + 32 * (size_t)i2, 24);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestidx = i2;
+            }
+        }
+        if (bestDist <= TH_HIGH) {
+            float theta = cur_angle[bestidx] - std::atan2(uey - usy, uex - usx);  // float overload
+            if (theta < -M_PI) theta += 2 * M_PI;
+            else if (theta > M_PI) theta -= 2 * M_PI;
+            if (std::fabs(theta) < angth) {
+                match[bestidx] = i;
+                blocked[bestidx] = (last_flags[i] & 2) ? 1 : 0;
+                matches++;
+            }
+        }
+    }
+    return matches;
+}

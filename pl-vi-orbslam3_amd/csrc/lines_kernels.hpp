@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void lsd_half_kernel(const uint8_t* __restrict
 //   resize x SCALE f64 INTER_LINEAR with float coefficients (lsd.cpp:457),
 //   ll_angle gradient / norm / fastAtan2 angle (lsd.cpp:561-584).
 // Outputs per scaled pixel: angle in degrees (float, NOTDEF = -1024), modgrad
-// (f64) and, for defined pixels, the seed direction (float cos, float sin).
+// (f64) and, for defined pixels, cos/sin(float(angle)) (float2).
 // ---------------------------------------------------------------------------
 constexpr int kPTX = 32, kPTY = 16;         // scaled tile
 constexpr int kPGW = 48, kPGH = 28;         // max blurred (G) region
@@ -56,7 +56,7 @@ __global__ __launch_bounds__(256) void lsd_prep_kernel(const uint8_t* __restrict
                                                        const int* __restrict__ yrow, const float* __restrict__ yb,
                                                        double k0, double k1, double k2, double k3, double rho,
                                                        float* __restrict__ pix, double* __restrict__ modgrad,
-                                                       float4* __restrict__ seedcs, size_t p_frame,
+                                                       float2* __restrict__ pixcs, size_t p_frame,
                                                        int* __restrict__ err) {
     __shared__ uint8_t I[kPIH][kPIW];
     __shared__ double Hs[kPIH][kPGW];
@@ -140,14 +140,12 @@ __global__ __launch_bounds__(256) void lsd_prep_kernel(const uint8_t* __restrict
         P[(size_t)y * sw + x] = deg;
         M[(size_t)y * sw + x] = norm;
         if (deg != kNotdefF) {
-            // region_grow's seed direction float(cos/sin(reg_angle)) (lsd.cpp:648-649)
-            // and the per-pixel cos/sin(float(angle)) of its sums (:678-679)
-            const double a = (double)deg * kD2R;
+            // the per-pixel cos/sin(float(angle)) of region_grow's sums (lsd.cpp:678-679);
+            // the seed direction (double cos/sin, :648-649) is computed by the
+            // region-growing kernel for the few pixels that become seeds
             float ps, pc;
-            plvi_sincosf_pos((float)a, &ps, &pc);
-            double ds, dc;
-            plvi_sincos(a, &ds, &dc);
-            seedcs[(size_t)f * p_frame + (size_t)y * sw + x] = make_float4((float)dc, (float)ds, pc, ps);
+            plvi_sincosf_pos((float)((double)deg * kD2R), &ps, &pc);
+            pixcs[(size_t)f * p_frame + (size_t)y * sw + x] = make_float2(pc, ps);
         }
     }
 }
@@ -311,7 +309,7 @@ template <bool STATS>
 __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restrict__ octs,
                                                       const float* __restrict__ pix,
                                                       const double* __restrict__ modgrad,
-                                                      const float4* __restrict__ seedcs,
+                                                      const float2* __restrict__ pixcs,
                                                       unsigned* __restrict__ gbits_all, size_t gbits_frame,
                                                       unsigned* __restrict__ qspill, size_t qspill_frame,
                                                       double prec, LsdRegion* __restrict__ regs, unsigned* __restrict__ regpts,
@@ -335,7 +333,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
     g.sw = sw; g.sh = sh; g.R = R; g.QL = QL;
     g.wpr = (sw + 31) >> 5;
     g.P = pix + od.soff + (size_t)f * od.splane;
-    const float4* SC = seedcs + od.soff + (size_t)f * od.splane;
+    const float2* SC = pixcs + od.soff + (size_t)f * od.splane;
     LsdRegion* outR = regs + (size_t)(f * nOct + o) * kLsdRawCap;
     unsigned* outP = regpts + (size_t)(f * nOct + o) * regpts_frame;
     int npts = 0;
@@ -384,8 +382,6 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
             if (x < sw - 1) cand = !used_get(g, x, y) && deg_at(g, x, y) != kNotdefF;
             unsigned long long m = __ballot(cand);
             if (!m) continue;
-            const float2 scl = cand ? make_float2(SC[(size_t)y * sw + x].x, SC[(size_t)y * sw + x].y)
-                                    : make_float2(0.f, 0.f);
             while (m) {
                 const int b = __ffsll((long long)m) - 1;
                 m &= m - 1;
@@ -393,8 +389,15 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                 if (used_get(g, sx, y)) continue;  // absorbed by an earlier region of this chunk
                 // ---- region_grow (lsd.cpp:635-686)
                 float reg_deg = deg_at(g, sx, y);  // reg_angle = (double)reg_deg * DEG_TO_RADS
-                float sumdx = readlane_f(scl.x, b);
-                float sumdy = readlane_f(scl.y, b);
+                // seed direction: sumdx = (float)cos(reg_angle), sumdy = (float)sin(reg_angle)
+                // (lsd.cpp:648-649), double libm restated (plvi_math.h), wave-uniform
+                float sumdx, sumdy;
+                {
+                    double ds, dc;
+                    plvi_sincos((double)reg_deg * kD2R, &ds, &dc);
+                    sumdx = (float)dc;
+                    sumdy = (float)ds;
+                }
                 if (lane == 0) {
                     used_set(g, sx, y);
                     g.qlds[0] = (unsigned)sx | ((unsigned)y << 16);
@@ -424,9 +427,9 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                     if (deg != kNotdefF) {
                         // precomputed by lsd_prep_kernel (computing them here costs
                         // more VALU issue than the load's latency)
-                        const float4 cs4 = SC[(size_t)ny * sw + nx];
-                        cc = cs4.z;
-                        ss = cs4.w;
+                        const float2 cs2 = SC[(size_t)ny * sw + nx];
+                        cc = cs2.x;
+                        ss = cs2.y;
                     }
                     unsigned long long t1 = 0;
                     if (do_stats) { t1 = __builtin_amdgcn_s_memtime(); s_setup += t1 - t0; n_block++; }

@@ -260,7 +260,7 @@ struct LinePipeline {
             PLVI_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_comb), comb, sizeof(comb)));
         }
         if (octImg.alloc(std::max<size_t>(imgOff, 16)) || pix.alloc(sizeof(float) * sOff) ||
-            modg.alloc(sizeof(double) * sOff) || seedcs.alloc(sizeof(float4) * sOff) ||
+            modg.alloc(sizeof(double) * sOff) || seedcs.alloc(sizeof(float2) * sOff) ||
             gbits.alloc(sizeof(unsigned) * gbitsFrame * nOct * Bcap) || qspill.alloc(sizeof(unsigned) * qspillFrame * nOct * Bcap) ||
             rawLines.alloc(sizeof(LsdLine) * (size_t)kLsdRawCap * nOct * Bcap) ||
             regs.alloc(sizeof(LsdRegion) * (size_t)kLsdRawCap * nOct * Bcap) ||
@@ -349,7 +349,7 @@ struct LinePipeline {
                                (const int*)(T + d.tabXofs), (const float*)(T + d.tabXa), d.xmax,
                                (const int*)(T + d.tabYrow), (const float*)(T + d.tabYb), gk[0], gk[1], gk[2], gk[3],
                                rho, pix.as<float>() + d.soff, modg.as<double>() + d.soff,
-                               seedcs.as<float4>() + d.soff, (size_t)d.splane, err.as<int>());
+                               seedcs.as<float2>() + d.soff, (size_t)d.splane, err.as<int>());
             if (kt) {
                 (void)hipEventRecord(kev[2 * kn + 1], st);
                 ++kn;
@@ -363,7 +363,7 @@ struct LinePipeline {
         auto growK = growStats ? lsd_grow_kernel<true> : lsd_grow_kernel<false>;
         hipLaunchKernelGGL(growK, dim3(nOct * nf), dim3(64), growSmem, st, d_oct.as<LineOctDev>(),
                            (const float*)pix.as<float>(), (const double*)modg.as<double>(),
-                           (const float4*)seedcs.as<float4>(), gbits.as<unsigned>(), gbitsFrame,
+                           (const float2*)seedcs.as<float2>(), gbits.as<unsigned>(), gbitsFrame,
                            qspill.as<unsigned>(), qspillFrame, prec, regs.as<LsdRegion>(), regpts.as<unsigned>(),
                            qspillFrame, nlines.as<int>(), err.as<int>(), growR, growQL, nOct, growStats);
         hipLaunchKernelGGL(lsd_rect_kernel, dim3(kRectBlocks, nOct, nf), dim3(256), 0, st, d_oct.as<LineOctDev>(),

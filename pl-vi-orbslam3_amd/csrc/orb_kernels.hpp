@@ -24,25 +24,28 @@ __device__ __forceinline__ int reflect1(int p, int len) {
 
 
 // ---------------------------------------------------------------------------
-// K1a: ComputePyramid (ORBextractor.cc:1152-1177): levels 1..L-1 of one
-// frame per workgroup, chained cv::resize INTER_LINEAR 8U (level l from
-// l-1), streamed top to bottom in a single launch.
-//   wave 0 (loader): streams the level-0 rows from HBM (dword loads,
-//     kPyrAhead rows in flight) into an LDS ring of kPyrRing rows;
-//   wave 1 (resizer): every new source row yields the (at most one:
-//     scale > 1) next row of the level above it, cascading through the
-//     levels; each level keeps its last two rows in LDS, and every level row
-//     is written to HBM once -- no intermediate HBM round trip.
-// The waves hand rows over through two LDS counters (rows loaded / rows
-// consumed) and s_sleep polling, never a workgroup barrier: the resizer
-// issues only stores and LDS traffic, so nothing in its loop waits for
-// memory, and the loader's waits cover only its own loads.
+// K1a: ComputePyramid (ORBextractor.cc:1152-1177): levels 1..L-1, chained
+// cv::resize INTER_LINEAR 8U (level l from l-1), streamed top to
+// bottom in a single launch.  A workgroup holds kPyrFrames frames:
+//   wave 0 (loader): streams the level-0 rows of its frames from HBM (dword
+//     loads, kPyrAhead rows per frame in flight) into per-frame LDS rings of
+//     kPyrRing rows;
+//   waves 1..kPyrFrames (resizers, one per frame): every new source row
+//     yields the (at most one: scale > 1) next row of the level above it,
+//     cascading through the levels; each level keeps its last two rows in
+//     LDS, and every level row is written to HBM once -- no intermediate
+//     HBM round trip.
+// Waves hand rows over through per-frame LDS counters (rows loaded / rows
+// consumed) and s_sleep polling, never a workgroup barrier: a resizer issues
+// only stores and LDS traffic, so nothing in its loop waits for memory.
 // The per-column coefficients (sx, a0, a1 of cv::resize, computed on the
-// host exactly as OpenCV does: pyr_xtab_entry) are one packed table in LDS
-// shared by all rows; the row coefficients are computed per output row.
+// host exactly as OpenCV does: append_xtab) are one packed table in LDS
+// shared by the workgroup's frames; the row coefficients are computed per
+// output row.  The fixed-point products use 24-bit multiplies (operands
+// < 2^24: pixel x 2048 and (H >> 4) x 2048).
 // Limits: level-0 width <= 4 * 64 * kPyrDw, source widths <= 1024.
 // ---------------------------------------------------------------------------
-constexpr int kPyrAhead = 4, kPyrDw = 4, kPyrRing = 4, kPyrUnroll = 4;
+constexpr int kPyrAhead = 2, kPyrDw = 4, kPyrRing = 4, kPyrUnroll = 4, kPyrFrames = 4;
 
 // packed column entry: sx (10 bits) | a0 (12 bits) << 10 | (a0 + a1 - 2047) (2 bits) << 22 | clampR << 24
 __host__ __device__ inline uint32_t pyr_xtab_pack(int sx, int a0, int a1, bool clampR) {
@@ -56,20 +59,17 @@ __device__ __forceinline__ void lds_publish(lds_i32* p, int v) {
     *(volatile lds_i32*)p = v;
 }
 
-__global__ __launch_bounds__(128) void orb_pyramid_kernel(const OrbLevelDev* __restrict__ lvs, int L,
-                                                          const uint8_t* __restrict__ frames, size_t f_frame,
-                                                          size_t f_row, uint8_t* __restrict__ pyr,
-                                                          const uint32_t* __restrict__ xtab, int xtab_n,
-                                                          int generic) {
+__global__ __launch_bounds__(64 * (kPyrFrames + 1)) void orb_pyramid_kernel(
+    const OrbLevelDev* __restrict__ lvs, int L, const uint8_t* __restrict__ frames, size_t f_frame, size_t f_row,
+    int nf, uint8_t* __restrict__ pyr, const uint32_t* __restrict__ xtab, int xtab_n, int frame_lds, int generic) {
     extern __shared__ __align__(16) uint8_t lds_pyr_g[];
     __shared__ int s_w[kOrbMaxLevels], s_h[kOrbMaxLevels], s_roff[kOrbMaxLevels], s_xoff[kOrbMaxLevels];
     __shared__ double s_sy[kOrbMaxLevels];
-    __shared__ int s_cnt[2];  // rows loaded, rows consumed
-    lds_u32* ltab = (lds_u32*)lds_pyr_g;  // column table first (xtab_n words)
-    lds_u8* lds_pyr = (lds_u8*)(lds_pyr_g + 4 * xtab_n);
-    lds_i32* s_loaded = (lds_i32*)&s_cnt[0];
-    lds_i32* s_consumed = (lds_i32*)&s_cnt[1];
-    const int f = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __shared__ int s_cnt[2 * kPyrFrames];  // per frame: rows loaded, rows consumed
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int f0 = blockIdx.x * kPyrFrames;
+    const int nfw = min(kPyrFrames, nf - f0);  // frames of this workgroup
+    lds_u32* ltab = (lds_u32*)lds_pyr_g;     // column table first (xtab_n words)
     if (threadIdx.x < L) {
         s_w[threadIdx.x] = lvs[threadIdx.x].w;
         s_h[threadIdx.x] = lvs[threadIdx.x].h;
@@ -83,69 +83,82 @@ __global__ __launch_bounds__(128) void orb_pyramid_kernel(const OrbLevelDev* __r
             s_roff[l] = o;
             o += 2 * ((lvs[l].w + 3) & ~3);
         }
-        s_cnt[0] = 0;
-        s_cnt[1] = 0;
     }
-    for (int i = threadIdx.x; i < xtab_n; i += 128) ltab[i] = xtab[i];
+    if (threadIdx.x < 2 * kPyrFrames) s_cnt[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < xtab_n; i += 64 * (kPyrFrames + 1)) ltab[i] = xtab[i];
     __syncthreads();  // the only workgroup barrier
     const int W0 = s_w[0], H0 = s_h[0];
     const int pitch0 = (W0 + 3) & ~3;
+    lds_u8* fbase = (lds_u8*)(lds_pyr_g + 4 * xtab_n);  // per-frame regions of frame_lds bytes
     if (wave == 0) {
         // ------------------------------------------------ loader
         const int nd = (W0 + 3) >> 2;
-        const uint8_t* src = frames + (size_t)f * f_frame;
-        const bool al4 = (((reinterpret_cast<uintptr_t>(src) | (uintptr_t)f_row) & 3) == 0) && (W0 & 3) == 0;
-        auto load_row = [&](int r, uint32_t* v) {
-            const uint8_t* row = src + (size_t)r * f_row;
+        bool al4 = (W0 & 3) == 0 && (f_row & 3) == 0 && (f_frame & 3) == 0 &&
+                   (reinterpret_cast<uintptr_t>(frames) & 3) == 0;
+        auto load_row = [&](int k, int r, uint32_t* v) {
+            const uint8_t* row = frames + (size_t)(f0 + k) * f_frame + (size_t)r * f_row;
             if (al4) {
                 const uint32_t* rw = reinterpret_cast<const uint32_t*>(row);
 #pragma unroll
-                for (int k = 0; k < kPyrDw; ++k)
-                    v[k] = lane + 64 * k < nd ? __builtin_nontemporal_load(rw + lane + 64 * k) : 0u;
+                for (int q = 0; q < kPyrDw; ++q)
+                    v[q] = lane + 64 * q < nd ? __builtin_nontemporal_load(rw + lane + 64 * q) : 0u;
             } else {
 #pragma unroll
-                for (int k = 0; k < kPyrDw; ++k) {
-                    const int d = lane + 64 * k;
+                for (int q = 0; q < kPyrDw; ++q) {
+                    const int d = lane + 64 * q;
                     uint32_t x = 0;
                     for (int b = 0; b < 4; ++b)
                         if (4 * d + b < W0) x |= (uint32_t)row[4 * d + b] << (8 * b);
-                    v[k] = x;
+                    v[q] = x;
                 }
             }
         };
-        uint32_t pf[kPyrAhead][kPyrDw];
+        uint32_t pf[kPyrAhead][kPyrFrames][kPyrDw];
 #pragma unroll
         for (int j = 0; j < kPyrAhead; ++j)
-            if (j < H0) load_row(j, pf[j]);
+#pragma unroll
+            for (int k = 0; k < kPyrFrames; ++k)
+                if (j < H0 && k < nfw) load_row(k, j, pf[j][k]);
         for (int rb = 0; rb < H0; rb += kPyrAhead) {
 #pragma unroll
             for (int j = 0; j < kPyrAhead; ++j) {
                 const int r = rb + j;
                 if (r >= H0) break;
-                // the resizer needs rows consumed-1 and consumed: slot r % ring is free once r - ring <= consumed - 2
-#ifndef PYR_NO_WAIT
-                while (r - kPyrRing > lds_load_volatile(s_consumed) - 2) __builtin_amdgcn_s_sleep(1);
-#endif
-                lds_u32* slot = (lds_u32*)(lds_pyr + (r % kPyrRing) * pitch0);
 #pragma unroll
-                for (int k = 0; k < kPyrDw; ++k)
-                    if (lane + 64 * k < nd) slot[lane + 64 * k] = pf[j][k];
-                if (lane == 0) lds_publish(s_loaded, r + 1);
-#ifndef PYR_NO_LOAD
-                if (r + kPyrAhead < H0) load_row(r + kPyrAhead, pf[j]);
-#endif
+                for (int k = 0; k < kPyrFrames; ++k) {
+                    if (k >= nfw) break;
+                    lds_i32* loaded = (lds_i32*)&s_cnt[2 * k];
+                    lds_i32* consumed = (lds_i32*)&s_cnt[2 * k + 1];
+                    // the resizer needs rows consumed-1 and consumed: slot r % ring is free once r - ring <= consumed - 2
+                    while (r - kPyrRing > lds_load_volatile(consumed) - 2) __builtin_amdgcn_s_sleep(1);
+                    lds_u32* slot = (lds_u32*)(fbase + (size_t)k * frame_lds + (r % kPyrRing) * pitch0);
+#pragma unroll
+                    for (int q = 0; q < kPyrDw; ++q)
+                        if (lane + 64 * q < nd) slot[lane + 64 * q] = pf[j][k][q];
+                    if (lane == 0) lds_publish(loaded, r + 1);
+                    if (r + kPyrAhead < H0) load_row(k, r + kPyrAhead, pf[j][k]);
+                }
             }
         }
         return;
     }
-    // ---------------------------------------------------- resizer
+    // ---------------------------------------------------- resizer of frame f
+    const int k = wave - 1;
+    if (k >= nfw) return;
+    const int f = f0 + k;
+    lds_u8* lds_pyr = fbase + (size_t)k * frame_lds;
+    lds_i32* s_loaded = (lds_i32*)&s_cnt[2 * k];
+    lds_i32* s_consumed = (lds_i32*)&s_cnt[2 * k + 1];
+    // this frame's level planes (no global parameter loads inside the row loop)
+    uint8_t* dbase[kOrbMaxLevels];
+#pragma unroll
+    for (int l = 0; l < kOrbMaxLevels; ++l)
+        dbase[l] = l < L ? pyr + lvs[l].off + (size_t)f * lvs[l].plane : nullptr;
     int prod[kOrbMaxLevels];
 #pragma unroll
     for (int l = 0; l < kOrbMaxLevels; ++l) prod[l] = 0;
     for (int r = 0; r < H0; ++r) {
-#ifndef PYR_NO_WAIT
         while (lds_load_volatile(s_loaded) <= r) __builtin_amdgcn_s_sleep(1);
-#endif
         int avail = r + 1;  // rows of the source level available
         for (int l = 1; l < L; ++l) {
             const int sh = s_h[l - 1], w = s_w[l], h = s_h[l];
@@ -163,15 +176,16 @@ __global__ __launch_bounds__(128) void orb_pyramid_kernel(const OrbLevelDev* __r
                 const int r1 = min(max(sy + 1, 0), sh - 1);
                 if (r1 >= avail) break;
                 const int r0 = min(max(sy, 0), sh - 1);
-                const int b0 = (int)__builtin_rintf((1.f - fy) * 2048), b1 = (int)__builtin_rintf(fy * 2048);
+                const unsigned b0 = (unsigned)__builtin_rintf((1.f - fy) * 2048),
+                               b1 = (unsigned)__builtin_rintf(fy * 2048);
                 const lds_u8* S0 = lds_pyr + s_roff[l - 1] + (r0 % sring) * spitch;
                 const lds_u8* S1 = lds_pyr + s_roff[l - 1] + (r1 % sring) * spitch;
-                uint8_t* D = pyr + lvs[l].off + (size_t)f * lvs[l].plane + (size_t)y * w;
+                uint8_t* D = dbase[l] + (size_t)y * w;
                 lds_u8* R = l < L - 1 ? lds_pyr + s_roff[l] + (y & 1) * pitch : nullptr;
                 for (int x0 = 0; x0 < w; x0 += 64 * kPyrUnroll) {
                     // kPyrUnroll columns per lane: all LDS reads issued before the first use
                     uint32_t e[kPyrUnroll];
-                    int p00[kPyrUnroll], p01[kPyrUnroll], p10[kPyrUnroll], p11[kPyrUnroll];
+                    unsigned p00[kPyrUnroll], p01[kPyrUnroll], p10[kPyrUnroll], p11[kPyrUnroll];
 #pragma unroll
                     for (int u = 0; u < kPyrUnroll; ++u) {
                         const int x = x0 + 64 * u + lane;
@@ -190,18 +204,18 @@ __global__ __launch_bounds__(128) void orb_pyramid_kernel(const OrbLevelDev* __r
                     for (int u = 0; u < kPyrUnroll; ++u) {
                         const int x = x0 + 64 * u + lane;
                         if (x >= w) break;
-                        int a0 = (e[u] >> 10) & 4095, a1 = 2047 - a0 + ((e[u] >> 22) & 3);
-                        int h0, h1;
-                        if (!((e[u] >> 24) & 1)) {
-                            h0 = p00[u] * a0 + p01[u] * a1;
-                            h1 = p10[u] * a0 + p11[u] * a1;
-                        } else {
-                            h0 = p00[u] * 2048;
-                            h1 = p10[u] * 2048;
-                        }
+                        const bool cr = (e[u] >> 24) & 1;
+                        // right-border column: H = S[sx] * 2048 (a0 = 2048, a1 = 0)
+                        const unsigned a0 = cr ? 2048u : (e[u] >> 10) & 4095;
+                        const unsigned a1 = cr ? 0u : 2047u - ((e[u] >> 10) & 4095) + ((e[u] >> 22) & 3);
+                        const unsigned h0 = __umul24(p00[u], a0) + __umul24(p01[u], a1);
+                        const unsigned h1 = __umul24(p10[u], a0) + __umul24(p11[u], a1);
                         // 8U specialisation (default) or the generic fixed-point cast (A.1 switch)
-                        const int v = generic ? min((b0 * h0 + b1 * h1 + (1 << 21)) >> 22, 255)
-                                              : ((((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2);
+                        int v;
+                        if (!generic)
+                            v = (int)(((__umul24(b0, h0 >> 4) >> 16) + (__umul24(b1, h1 >> 4) >> 16) + 2) >> 2);
+                        else
+                            v = min((int)((b0 * h0 + b1 * h1 + (1u << 21)) >> 22), 255);
                         D[x] = (uint8_t)v;
                         if (R) R[x] = (uint8_t)v;
                     }

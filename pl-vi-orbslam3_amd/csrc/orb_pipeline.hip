@@ -58,7 +58,7 @@ struct OrbPipeline {
     DevBuf d_lv, d_cells, d_strips, d_xtab, pyr, blur, score, cand, sat, carry, rects, rectCnt, lvkp, lvdesc, okp, odesc, ocount,
         omono, err, staging;
     size_t pyrSmem = 0;  // orb_pyramid_kernel LDS: column table + source-level row rings
-    int xtabN = 0;
+    int xtabN = 0, pyrFrameLds = 0;
     int lastFrames = 0;
     // Stage timing with HIP events on the launch stream (bench.py roofline).
     static constexpr int kStages = 7, kRing = 512;
@@ -270,7 +270,8 @@ struct OrbPipeline {
         PLVI_CHECK(hipMemcpy(d_lv.p, lv.data(), sizeof(OrbLevelDev) * L, hipMemcpyHostToDevice));
         PLVI_CHECK(hipMemcpy(d_cells.p, cells.data(), sizeof(OrbCellDev) * cells.size(), hipMemcpyHostToDevice));
         xtabN = (int)xtab.size();
-        pyrSmem += 4 * (size_t)xtabN;
+        pyrFrameLds = (int)((pyrSmem + 15) & ~size_t(15));
+        pyrSmem = 4 * (size_t)xtabN + (size_t)kPyrFrames * pyrFrameLds;
         if (W > 4 * 64 * kPyrDw || pyrSmem > 64 * 1024) return PLVI_E_BADARG;  // orb_pyramid_kernel limits
         if (xtab.empty()) xtab.push_back(0);
         if (d_xtab.alloc(4 * xtab.size())) return PLVI_E_HIP;
@@ -304,9 +305,9 @@ struct OrbPipeline {
         // K1a: the pyramid (ComputePyramid, chained resize: level l from l-1)
         // of every frame in one streaming launch, one wave per frame
         if (L > 1)
-            hipLaunchKernelGGL(orb_pyramid_kernel, dim3(nf), dim3(128), pyrSmem, st, d_lv.as<OrbLevelDev>(), L,
-                               d_frames, frame_stride, row_stride, P, (const uint32_t*)d_xtab.as<uint32_t>(), xtabN,
-                               resizeGeneric);
+            hipLaunchKernelGGL(orb_pyramid_kernel, dim3((nf + kPyrFrames - 1) / kPyrFrames), dim3(64 * (kPyrFrames + 1)),
+                               pyrSmem, st, d_lv.as<OrbLevelDev>(), L, d_frames, frame_stride, row_stride, nf, P,
+                               (const uint32_t*)d_xtab.as<uint32_t>(), xtabN, pyrFrameLds, resizeGeneric);
         // K1b: blur + FAST score of every level (level 0 also copies the frame into its plane)
         const bool kt = ktime && kn < kKRing;
         if (kt) PLVI_CHECK(hipEventRecord(kev[2 * kn], st));

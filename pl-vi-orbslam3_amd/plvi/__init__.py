@@ -111,6 +111,16 @@ class LocalParams(ctypes.Structure):
                 ("nlevels", ctypes.c_int), ("scale_factors", ctypes.c_float * 16)]
 
 
+class LineProjParams(ctypes.Structure):
+    """plvi_line_proj_params (include/plvi_frontend.h): LineMatcher::SearchByProjection."""
+    _fields_ = [("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
+                ("min_x", ctypes.c_float), ("max_x", ctypes.c_float), ("min_y", ctypes.c_float),
+                ("max_y", ctypes.c_float), ("inv_w", ctypes.c_double), ("inv_h", ctypes.c_double),
+                ("th", ctypes.c_float), ("angth", ctypes.c_float), ("grid_cols", ctypes.c_int),
+                ("grid_rows", ctypes.c_int), ("range_hint", ctypes.c_int), ("nlevels", ctypes.c_int),
+                ("scale_l", ctypes.c_float * 8)]
+
+
 def grid_geometry(width, height):
     """Frame ctor grid geometry without distortion (mnMinX = 0, mnMaxX = cols, ...;
     Frame.cc:156-157): (min_x, max_x, min_y, max_y, inv_w, inv_h) as float32."""
@@ -189,6 +199,8 @@ def _declare(lib):
         "plvi_search_by_projection": ([V, V, V, I, V, V, V, V, V, V, V, I, V], I),
         "plvi_search_local_batch": ([I, V, V, V, V, I, V, V, V, V, V, V, V, V, V, I, V, V, V], I),
         "plvi_search_local": ([V, V, V, I, V, V, V, V, V, V, I, V], I),
+        "plvi_line_search_projection_batch": ([I, V, V, V, V, V, I, V, V, I, V, V, V, V, V, I, V, V, V, V], I),
+        "plvi_line_search_projection": ([V, V, V, V, I, V, V, V, V, V, V, I, V], I),
         "plvi_vocab_load_text": ([ctypes.c_char_p, I, I, c_void_pp], I),
         "plvi_vocab_create": ([I, I, I, I, I, V, V, V, V, I, c_void_pp], I),
         "plvi_vocab_destroy": ([V], I),
@@ -583,6 +595,29 @@ class LineMatcher:
         """LineMatcher::match(desc1, desc2, nnr, matches_12) (LineMatcher.cpp:92-111)."""
         lib = load()
         return LineMatcher._inout(lib.plvi_line_match_inout, "plvi_line_match_inout", desc1, desc2, nnr, matches_12)
+
+    @staticmethod
+    def SearchByProjection(params, cur_angle, cur_desc, grid, last_flags, last_x3dc, last_octave, ml_desc,
+                           cur_blocked=None):
+        """LineMatcher::SearchByProjection(CurrentFrame, LastFrame, grid, th, angth) (src/LineMatcher.cpp:274-372).
+        params: LineProjParams; grid: grid[x][y] lists of current-line indices (grid_Line); last_x3dc: n x 6
+        camera-frame endpoints.  Returns (count, match) with match[i2] = last-frame line index or -1."""
+        lib = load()
+        ca = np.ascontiguousarray(cur_angle, np.float32)
+        cd = np.ascontiguousarray(cur_desc, np.uint8).reshape(-1, 32)
+        cols, rows, off, idx = grid_csr(grid)
+        params.grid_cols, params.grid_rows = cols, rows
+        fl = np.ascontiguousarray(last_flags, np.uint8)
+        x3 = np.ascontiguousarray(last_x3dc, np.float32).reshape(-1, 6)
+        oc = np.ascontiguousarray(last_octave, np.int32)
+        md = np.ascontiguousarray(ml_desc, np.uint8).reshape(-1, 32)
+        cb = None if cur_blocked is None else np.ascontiguousarray(cur_blocked, np.uint8)
+        out = np.full(max(len(ca), 1), -1, np.int32)
+        n = _check(lib.plvi_line_search_projection(ctypes.byref(params), _ptr(ca), _ptr(cd),
+                                                   None if cb is None else _ptr(cb), len(ca), _ptr(off), _ptr(idx),
+                                                   _ptr(fl), _ptr(x3), _ptr(oc), _ptr(md), len(fl), _ptr(out)),
+                   "plvi_line_search_projection")
+        return n, out[:len(ca)]
 
     @staticmethod
     def matchGrid(lines1, desc1, grid, desc2, directions2, window=((7, 0), (2, 2)), range_hint=1):

@@ -457,6 +457,40 @@ def search_local(case, th, nnratio=0.8):
     return n, out[:len(kx)]
 
 
+def line_search_projection(case, th, angth, range_hint=1):
+    """LineMatcher::SearchByProjection restatement -> (count, match)."""
+    lib = load()
+    V, I, F, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_double
+    lib.oracle_line_search_projection.argtypes = [I, V, V, V, I, I, V, V, I, V, V, V, V, F, F, F, F, F, F, F, F, D, D,
+                                                  V, F, F, I, V]
+    lib.oracle_line_search_projection.restype = I
+    c = case
+    grid = c["grid"]
+    cols, rows = len(grid), len(grid[0])
+    off = np.zeros(cols * rows + 1, np.int32)
+    flat = []
+    for x in range(cols):
+        for y in range(rows):
+            flat.extend(grid[x][y])
+            off[x * rows + y + 1] = len(flat)
+    idx = np.array(flat if flat else [0], np.int32)
+    ca = np.ascontiguousarray(c["cur_angle"], np.float32)
+    cd = np.ascontiguousarray(c["cur_desc"], np.uint8)
+    cb = np.ascontiguousarray(c["cur_blocked"], np.uint8)
+    fl = np.ascontiguousarray(c["last_flags"], np.uint8)
+    x3 = np.ascontiguousarray(c["x3dc"], np.float32)
+    oc = np.ascontiguousarray(c["last_octave"], np.int32)
+    md = np.ascontiguousarray(c["ml_desc"], np.uint8)
+    sl = np.ascontiguousarray(c["scale_l"], np.float32)
+    fx, fy, cx, cy = c["camera"]
+    mnx, mxx, mny, mxy = c["bounds"]
+    out = np.full(max(len(ca), 1), -1, np.int32)
+    n = lib.oracle_line_search_projection(len(ca), _p(ca), _p(cd), _p(cb), cols, rows, _p(off), _p(idx), len(fl),
+                                          _p(fl), _p(x3), _p(oc), _p(md), fx, fy, cx, cy, mnx, mxx, mny, mxy,
+                                          c["inv_w"], c["inv_h"], _p(sl), th, angth, range_hint, _p(out))
+    return n, out[:len(ca)]
+
+
 def undistort_points(K4, dist, xy):
     lib = load()
     V, I = ctypes.c_void_p, ctypes.c_int

@@ -93,3 +93,26 @@ def test_match_grid_degenerate_lines_and_empty():
     empty = [[[] for _ in range(48)] for _ in range(64)]
     n, m = plvi.LineMatcher.matchGrid(lines1, desc1, empty, desc2, dirs, range_hint=1)
     assert n == 0 and (m == -1).all()
+
+
+# ------------------------------------ LineMatcher::SearchByProjection (LineMatcher.cpp:274-372)
+def test_oracle_line_search_projection_sanity():
+    case = util.line_proj_case(0)
+    for hint in (0, 1):
+        n, m = oracle_lib.line_search_projection(case, 3.0, float(np.float32(np.pi / 8)), hint)
+        assert n >= (m >= 0).sum() > 20
+        assert (m[case["cur_blocked"] == 1] == -1).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,th,hint", [(0, 3.0, 1), (1, 5.0, 1), (2, 3.0, 0), (3, 5.0, 0), (4, 8.0, 1)])
+def test_line_search_projection_matches_oracle(seed, th, hint):
+    import plvi
+    case = util.line_proj_case(seed)
+    angth = float(np.float32(np.pi / 8))
+    ne, me = oracle_lib.line_search_projection(case, th, angth, hint)
+    ng, mg = plvi.LineMatcher.SearchByProjection(util.line_proj_params(case, th, angth, hint), case["cur_angle"],
+                                                 case["cur_desc"], case["grid"], case["last_flags"], case["x3dc"],
+                                                 case["last_octave"], case["ml_desc"], case["cur_blocked"])
+    assert ng == ne
+    np.testing.assert_array_equal(mg, me)

@@ -192,7 +192,8 @@ def local_case(seed, n_cur=1000, n_mp=1500, W=752, H=480, uright=False, dup=0.15
     near = rng.random(n_mp) < 0.75
     src = rng.integers(0, n_cur, n_mp)
     nd = int(dup * n_mp)
-    src[-nd:] = src[rng.integers(0, n_mp - nd, nd)]
+    if nd:
+        src[-nd:] = src[rng.integers(0, n_mp - nd, nd)]
     px = np.where(near, kps["x"][src] + rng.normal(0, 1.5, n_mp), rng.uniform(0, W, n_mp)).astype(np.float32)
     py = np.where(near, kps["y"][src] + rng.normal(0, 1.5, n_mp), rng.uniform(0, H, n_mp)).astype(np.float32)
     pxr = (px - rng.uniform(0, 30, n_mp)).astype(np.float32)
@@ -220,6 +221,60 @@ def local_params(case, th):
     p.min_x, p.min_y, p.inv_w, p.inv_h, p.th, p.nlevels = min_x, min_y, inv_w, inv_h, th, 8
     for i, s in enumerate(case["scale_factors"]):
         p.scale_factors[i] = s
+    return p
+
+
+def line_proj_case(seed, n_cur=200, n_last=180, W=640, H=480, cols=64, rows=48):
+    """Synthetic LineMatcher::SearchByProjection input: current-frame lines rasterised into the 64 x 48
+    grid_Line with LineIterator (angles = atan2f of their endpoints, as KeyLine.angle), last-frame MapLines
+    whose camera-frame endpoints project near a current line's (80 %) or anywhere, descriptors = the
+    line's with ~8 % bit flips, duplicates aiming at the same current line (blocking order), some outliers
+    / behind the camera / Observations() == 0, a few current lines pre-blocked."""
+    rng = np.random.default_rng(seed)
+    inv_w, inv_h = cols / W, rows / H
+    sp = np.stack([rng.uniform(0, W - 1, n_cur), rng.uniform(0, H - 1, n_cur)], 1)
+    ang = rng.uniform(0, 2 * np.pi, n_cur)
+    ln = rng.uniform(10, 150, n_cur)
+    ep = np.clip(sp + np.stack([np.cos(ang), np.sin(ang)], 1) * ln[:, None], 0, [W - 1, H - 1])
+    sp32, ep32 = sp.astype(np.float32), ep.astype(np.float32)
+    cur_angle = np.arctan2(ep32[:, 1] - sp32[:, 1], ep32[:, 0] - sp32[:, 0]).astype(np.float32)
+    grid = [[[] for _ in range(rows)] for _ in range(cols)]
+    for i in range(n_cur):
+        for (x, y) in line_iterator(sp[i, 0] * inv_w, sp[i, 1] * inv_h, ep[i, 0] * inv_w, ep[i, 1] * inv_h):
+            if 0 <= x < cols and 0 <= y < rows:
+                grid[x][y].append(i)
+    cur_desc = rng.integers(0, 256, (n_cur, 32), dtype=np.uint8)
+    fx, fy, cx, cy = np.float32(458.654), np.float32(457.296), np.float32(320.0), np.float32(240.0)
+    near = rng.random(n_last) < 0.8
+    src = rng.integers(0, n_cur, n_last)
+    k = n_last // 8
+    src[-k:] = src[:k]
+    x3 = np.zeros((n_last, 6), np.float32)
+    for i in range(n_last):
+        for e, P in enumerate((sp, ep)):
+            u, v = (P[src[i]] + rng.normal(0, 1.0, 2)) if near[i] else rng.uniform([0, 0], [W, H])
+            z = rng.uniform(1.0, 15.0)
+            x3[i, 3 * e:3 * e + 3] = ((u - cx) * z / fx, (v - cy) * z / fy, z)
+    x3[rng.random(n_last) < 0.03, 2] *= -1
+    bits = np.unpackbits(cur_desc[src], axis=1)
+    bits ^= (rng.random(bits.shape) < 0.08).astype(np.uint8)
+    ml = np.where(near[:, None], np.packbits(bits, axis=1), rng.integers(0, 256, (n_last, 32), dtype=np.uint8))
+    flags = ((rng.random(n_last) < 0.92).astype(np.uint8) | ((rng.random(n_last) < 0.85).astype(np.uint8) << 1))
+    return {"cur_angle": cur_angle, "cur_desc": cur_desc, "cur_blocked": (rng.random(n_cur) < 0.05).astype(np.uint8),
+            "grid": grid, "last_flags": flags, "x3dc": x3,
+            "last_octave": (rng.random(n_last) < 0.3).astype(np.int32), "ml_desc": ml.astype(np.uint8),
+            "scale_l": np.array([1, 2, 0, 0, 0, 0, 0, 0], np.float32), "camera": (fx, fy, cx, cy),
+            "bounds": (np.float32(0), np.float32(W), np.float32(0), np.float32(H)), "inv_w": inv_w, "inv_h": inv_h}
+
+
+def line_proj_params(case, th, angth, range_hint=1):
+    import plvi
+    p = plvi.LineProjParams()
+    p.fx, p.fy, p.cx, p.cy = case["camera"]
+    p.min_x, p.max_x, p.min_y, p.max_y = case["bounds"]
+    p.inv_w, p.inv_h, p.th, p.angth, p.range_hint, p.nlevels = case["inv_w"], case["inv_h"], th, angth, range_hint, 2
+    for i, s in enumerate(case["scale_l"]):
+        p.scale_l[i] = s
     return p
 
 
