@@ -679,6 +679,27 @@ def side_stages(args, torch, plvi, synth, lib, orb, st, stream, B, W, H, cap, kp
         if rc:
             raise RuntimeError(f"projection {rc}")
     out["proj.grid+search"] = timed(run_proj)
+    # local-map search (ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>), Tracking.cc:5119):
+    # frame t against frame t-1's keypoints as the local map (predicted position = keypoint,
+    # level = octave, view cosine 1, their descriptors), th = 1, nnratio 0.8
+    lpp = plvi.LocalParams()
+    lpp.min_x, lpp.min_y, lpp.inv_w, lpp.inv_h = 0.0, 0.0, *[float(x) for x in plvi.grid_geometry(W, H)[4:]]
+    lpp.th, lpp.nnratio, lpp.nlevels = 1.0, 0.8, 8
+    for i, sfac in enumerate(orb.GetScaleFactors()):
+        lpp.scale_factors[i] = float(sfac)
+    mproj = torch.stack([kv[..., 0], kv[..., 1], kv[..., 0], torch.ones_like(kv[..., 0])], -1).contiguous()
+    mflags = torch.full((B * cap,), 3, dtype=torch.uint8, device=cuda)
+    lm = torch.empty((B - 1) * cap, dtype=torch.int32, device=cuda)
+    ln = torch.empty(B, dtype=torch.int32, device=cuda)
+
+    def run_local():
+        rc = lib.plvi_search_local_batch(
+            B - 1, ctypes.byref(lpp), kp_p + 28 * cap, de_p + 32 * cap, co_p + 4, cap, None, None,
+            cell_off.data_ptr() + 4 * 3073, cell_idx.data_ptr() + 4 * cap, mflags.data_ptr(), mproj.data_ptr(),
+            loct.data_ptr(), de_p, co_p, cap, lm.data_ptr(), ln.data_ptr(), st)
+        if rc:
+            raise RuntimeError(f"local search {rc}")
+    out["local.search"] = timed(run_local)
     # stereo on S rectified pairs extracted by their own handles
     S = min(B, 256)
     pairs = [synth.stereo_pair(seed0 + 10 ** 5 + i, W, H) for i in range(S)]
