@@ -406,50 +406,73 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
 // K2: per-cell FAST non-max suppression with the reference's threshold
 // fallback (ORBextractor.cc:808-829): survivors at iniThFAST; if none in the
 // cell, survivors at minThFAST.  NMS is cell-local: neighbours outside the
-// cell's detection window count as 0 (cv::FAST on the cell ROI).
-// One wave per (cell, frame).
+// cell's detection window count as 0 (cv::FAST on the cell ROI), a
+// neighbour below the threshold counts as 0, and a survivor is strictly
+// greater than all 8 (A.3).
+// One wave per (cell, frame), lane = window column (windows are < 64 wide):
+// the window's score column is held in registers (4 rows per dword),
+// horizontal neighbours come over DPP lane shifts, so there is no LDS and
+// no per-pixel index arithmetic.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool nms_keep(const uint8_t* sc, int ww, int wh, int xx, int yy, int t) {
-    const int s = sc[yy * kOrbCellMax + xx];
-    if (s == 0 || s < t) return false;
-#pragma unroll
-    for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-        for (int dx = -1; dx <= 1; ++dx) {
-            if (!dx && !dy) continue;
-            const int nx = xx + dx, ny = yy + dy;
-            int nv = 0;
-            if (nx >= 0 && nx < ww && ny >= 0 && ny < wh) {
-                nv = sc[ny * kOrbCellMax + nx];
-                if (nv < t) nv = 0;
-            }
-            if (!(s > nv)) return false;
-        }
-    return true;
-}
+constexpr int kNmsRows = 64;  // >= window height (hCell <= 58, orb_pipeline.hip plan checks)
 
 __global__ __launch_bounds__(64) void orb_cell_nms_kernel(const OrbCellDev* __restrict__ cells,
                                                           const OrbLevelDev* __restrict__ lvs,
                                                           const uint8_t* __restrict__ score,
                                                           uint8_t* __restrict__ cand, int t1, int t2) {
-    __shared__ uint8_t sc[kOrbCellMax * kOrbCellMax];
+    __shared__ uint8_t sv[kNmsRows * 64];
     const OrbCellDev c = cells[blockIdx.x];
     const int f = blockIdx.y;
     const OrbLevelDev& L = lvs[c.level];
-    const uint8_t* S = score + L.off + (size_t)f * L.plane;
-    uint8_t* C = cand + L.off + (size_t)f * L.plane;
-    const int ww = c.x1 - c.x0, wh = c.y1 - c.y0;
+    const int ww = c.x1 - c.x0, wh = c.y1 - c.y0, w = L.w;
     const int lane = threadIdx.x;
-    stage_bytes<64>(sc, kOrbCellMax, S + (size_t)c.y0 * L.w + c.x0, (size_t)L.w, ww, wh, lane);
-    __syncthreads();
-    int cnt = 0;
-    for (int i = lane; i < ww * wh; i += 64) cnt += nms_keep(sc, ww, wh, i % ww, i / ww, t1) ? 1 : 0;
-    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-    const int t = cnt ? t1 : t2;
-    for (int i = lane; i < ww * wh; i += 64) {
-        const int yy = i / ww, xx = i % ww;
-        const bool k = nms_keep(sc, ww, wh, xx, yy, t);
-        C[(size_t)(c.y0 + yy) * L.w + c.x0 + xx] = k ? sc[yy * kOrbCellMax + xx] : 0;
+    const bool incol = lane < ww;
+    const size_t base = L.off + (size_t)f * L.plane + (size_t)c.y0 * w + c.x0 + lane;
+    const uint8_t* S = score + base;
+    // stage the window column-per-lane (rows beyond wh and lanes beyond ww hold 0)
+    for (int r0 = 0; r0 < wh; r0 += 8) {
+        uint8_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = (incol && r0 + k < wh) ? S[(size_t)(r0 + k) * w] : (uint8_t)0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sv[(r0 + k) * 64 + lane] = v[k];
+    }
+    sv[wh * 64 + lane] = 0;  // row wh (wh < kNmsRows) is the bottom neighbour of the last row
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // both thresholds in one sweep: a = iniThFAST, b = minThFAST
+    unsigned long long ka = 0, kb = 0;
+    int s = sv[lane];
+    int ac = s >= t1 ? s : 0, bc = s >= t2 ? s : 0;
+    int ahp = 0, bhp = 0;  // max over columns c-1..c+1 of row r-1
+    for (int r = 0; r < wh; ++r) {
+        const int sn = sv[(r + 1) * 64 + lane];
+        const int an = sn >= t1 ? sn : 0, bn = sn >= t2 ? sn : 0;
+        const int alc = lane_from_left(ac), arc = lane_from_right(ac);
+        const int aln = lane_from_left(an), arn = lane_from_right(an);
+        const int blc = lane_from_left(bc), brc = lane_from_right(bc);
+        const int bln = lane_from_left(bn), brn = lane_from_right(bn);
+        const int ah = max(alc, arc), bh = max(blc, brc);
+        const int am = max(max(ahp, ah), max(max(aln, arn), an));
+        const int bm = max(max(bhp, bh), max(max(bln, brn), bn));
+        // s > m >= 0 also excludes s == 0
+        if (s >= t1 && s > am) ka |= 1ull << r;
+        if (s >= t2 && s > bm) kb |= 1ull << r;
+        ahp = max(ah, ac);
+        bhp = max(bh, bc);
+        ac = an;
+        bc = bn;
+        s = sn;
+    }
+    const unsigned long long keep = __ballot(ka != 0ull) != 0ull ? ka : kb;
+    if (!incol) return;
+    uint8_t* C = cand + base;
+    for (int r0 = 0; r0 < wh; r0 += 8) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int r = r0 + k;
+            if (r < wh) C[(size_t)r * w] = ((keep >> r) & 1ull) ? sv[r * 64 + lane] : (uint8_t)0;
+        }
     }
 }
 
