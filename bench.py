@@ -39,6 +39,7 @@ import socket
 import subprocess
 import sys
 import time
+import types
 
 import numpy as np
 
@@ -294,6 +295,9 @@ def main():
     ap.add_argument("--no-check", action="store_true", help="skip the oracle check of the timed batch")
     ap.add_argument("--no-extra", action="store_true", help="skip the batch-64 / latency / H2D lines")
     ap.add_argument("--no-side", action="store_true", help="skip the BoW / projection / stereo stage timings")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="batches in flight: consecutive steps alternate over this many extractor/stream slots, "
+                         "so one batch's ORB tail overlaps the next batch's LSD front")
     args = ap.parse_args()
 
     world_env = int(os.environ.get("WORLD_SIZE", "0"))
@@ -343,72 +347,98 @@ def run(args, world, rank):
     torch.cuda.synchronize()
     first_digest = hashlib.sha256(seq[:B].cpu().numpy().tobytes()).hexdigest()[:16]
 
-    orb = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=B, device=dev)
-    lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=B, device=dev)
-    kp_p, de_p, co_p, _, cap = orb.outputs()
-    kl_p, lde_p, _, lco_p, lcap = lx.outputs()
-    outs = [torch.empty((B - 1) * cap, **i32) for _ in range(4)]
-    lscratch = torch.empty(4 * (B - 1) * 2 * lcap, **i32)
-    lm12 = torch.empty((B - 1) * lcap, **i32)
-    lnm = torch.empty(B - 1, **i32)
-    stream = torch.cuda.Stream()  # non-default: the legacy null stream would serialise
-    st = stream.cuda_stream
-    orb.kernel_timing(True)  # event pair around every blur+FAST launch
-    lx.kernel_timing(True)   # and every lsd_prep launch
+    # Slots: an ORB + line extractor pair with its own output tables, match
+    # buffers and stream.  Step k runs on slot k % inflight, so batch k+1's
+    # LSD front (prep, region growing) overlaps batch k's ORB tail.  Every step
+    # still extracts and matches its full batch inside the timed region.
+    tab_sizes = None
+    recv = None
 
-    def extract(fptr, n=B):
-        plvi.frame_extract_batch(orb, lx, fptr, n, W * H, W, (0, 0), stream=st)
+    def make_slot():
+        nonlocal tab_sizes, recv
+        sl = types.SimpleNamespace()
+        sl.orb = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=B, device=dev)
+        sl.lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=B, device=dev)
+        sl.kp_p, sl.de_p, sl.co_p, _, cap_ = sl.orb.outputs()
+        sl.kl_p, sl.lde_p, _, sl.lco_p, lcap_ = sl.lx.outputs()
+        sl.outs = [torch.empty((B - 1) * cap_, **i32) for _ in range(4)]
+        sl.lscratch = torch.empty(4 * (B - 1) * 2 * lcap_, **i32)
+        sl.lm12 = torch.empty((B - 1) * lcap_, **i32)
+        sl.lnm = torch.empty(B - 1, **i32)
+        sl.stream = torch.cuda.Stream()  # non-default: the legacy null stream would serialise
+        sl.st = sl.stream.cuda_stream
+        # C4 gather: tables staged on the slot's stream, then one RCCL gather
+        # per table to rank 0, asynchronous (waited on before the staging is reused)
+        tab_sizes = (4 * B, 28 * cap_ * B, 32 * cap_ * B, 4 * B, 68 * lcap_ * B, 32 * lcap_ * B)
+        sl.stage_bufs = [torch.empty(n, dtype=torch.uint8, device=cuda) for n in tab_sizes] if args.gather else []
+        if args.gather and rank == 0 and recv is None:
+            recv = [[torch.empty(n, dtype=torch.uint8, device=cuda) for _ in range(world)] for n in tab_sizes]
+        sl.pending = []
+        return sl, cap_, lcap_
 
-    def match(n=B):
-        rc = lib.plvi_hamming_knn2_batch(de_p + cap * 32, co_p + 4, cap, de_p, co_p, cap, n - 1,
-                                         *[o.data_ptr() for o in outs], st)
-        rc |= lib.plvi_line_match_batch(lde_p + lcap * 32, lco_p + 4, lcap, lde_p, lco_p, lcap, n - 1, 0.9,
-                                        lscratch.data_ptr(), lm12.data_ptr(), lnm.data_ptr(), st)
+    s0, cap, lcap = make_slot()
+    slots = [s0] + [make_slot()[0] for _ in range(max(1, args.inflight) - 1)]
+    orb, lx, stream, st = s0.orb, s0.lx, s0.stream, s0.st
+    kp_p, de_p, co_p, kl_p, lde_p, lco_p = s0.kp_p, s0.de_p, s0.co_p, s0.kl_p, s0.lde_p, s0.lco_p
+    outs, lscratch, lm12, lnm = s0.outs, s0.lscratch, s0.lm12, s0.lnm
+    for sl in slots:
+        sl.orb.kernel_timing(True)  # event pair around every blur+FAST launch
+        sl.lx.kernel_timing(True)   # and every lsd_prep launch
+
+    def extract(fptr, n=B, sl=s0):
+        plvi.frame_extract_batch(sl.orb, sl.lx, fptr, n, W * H, W, (0, 0), stream=sl.st)
+
+    def match(n=B, sl=s0):
+        rc = lib.plvi_hamming_knn2_batch(sl.de_p + cap * 32, sl.co_p + 4, cap, sl.de_p, sl.co_p, cap, n - 1,
+                                         *[o.data_ptr() for o in sl.outs], sl.st)
+        rc |= lib.plvi_line_match_batch(sl.lde_p + lcap * 32, sl.lco_p + 4, lcap, sl.lde_p, sl.lco_p, lcap, n - 1,
+                                        0.9, sl.lscratch.data_ptr(), sl.lm12.data_ptr(), sl.lnm.data_ptr(), sl.st)
         if rc:
             raise RuntimeError(f"match {rc}")
 
-    # C4 gather: tables staged on the step's stream, then one RCCL gather per
-    # table to rank 0, asynchronous (waited on before the staging is reused)
-    tab_sizes = (4 * B, 28 * cap * B, 32 * cap * B, 4 * B, 68 * lcap * B, 32 * lcap * B)
-    stage_bufs = [torch.empty(n, dtype=torch.uint8, device=cuda) for n in tab_sizes] if args.gather else []
-    recv = ([[torch.empty(n, dtype=torch.uint8, device=cuda) for _ in range(world)] for n in tab_sizes]
-            if args.gather and rank == 0 else None)
-    pending = []
-
-    def gather():
+    def gather(sl=s0):
         import torch.distributed as dist
-        for w_ in pending:
+        for w_ in sl.pending:
             w_.wait()
-        pending.clear()
-        for src, t in zip((co_p, kp_p, de_p, lco_p, kl_p, lde_p), stage_bufs):
-            if lib.plvi_memcpy_async(t.data_ptr(), src, t.numel(), 3, st):
+        sl.pending.clear()
+        for src, t in zip((sl.co_p, sl.kp_p, sl.de_p, sl.lco_p, sl.kl_p, sl.lde_p), sl.stage_bufs):
+            if lib.plvi_memcpy_async(t.data_ptr(), src, t.numel(), 3, sl.st):
                 raise RuntimeError("gather copy")
-        with torch.cuda.stream(stream):
-            for i, t in enumerate(stage_bufs):
+        with torch.cuda.stream(sl.stream):
+            for i, t in enumerate(sl.stage_bufs):
                 if world == 1:
                     continue
-                pending.append(dist.gather(t, recv[i] if rank == 0 else None, dst=0, async_op=True))
+                sl.pending.append(dist.gather(t, recv[i] if rank == 0 else None, dst=0, async_op=True))
+
+    def wait_gathers():
+        for sl in slots:
+            for w_ in sl.pending:
+                w_.wait()
+            sl.pending.clear()
 
     step_no = [0]
 
     def step():
         k = step_no[0]
         step_no[0] += 1
+        sl = slots[k % len(slots)]
         lo = (k % nwin) * (B - 1)
-        extract(seq[lo].data_ptr())
-        match()
+        extract(seq[lo].data_ptr(), sl=sl)
+        match(sl=sl)
         if args.gather:
-            gather()
+            gather(sl)
 
-    for _ in range(args.warmup):
+    for _ in range(max(args.warmup, len(slots))):
         step()
     torch.cuda.synchronize()
-    if args.gather and rank == 0 and world > 1:
-        for w_ in pending:
-            w_.wait()
+    if args.gather and world > 1:
+        wait_gathers()
         torch.cuda.synchronize()
     # error flags of the warm-up batches
-    err_warm = (orb.errors(st), lx.errors(st))
+    err_warm = [0, 0]
+    for sl in slots:
+        err_warm[0] |= sl.orb.errors(sl.st)
+        err_warm[1] |= sl.lx.errors(sl.st)
 
     # stage timing (separate from the timed region: events add markers); each
     # extractor alone so its stage times are uncontended
@@ -459,9 +489,8 @@ def run(args, world, rank):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    if args.gather and rank == 0 and world > 1:
-        for w_ in pending:
-            w_.wait()
+    if args.gather and world > 1:
+        wait_gathers()
     torch.cuda.synchronize()
     pdist.barrier(world)
     el = pdist.max_over_ranks(time.perf_counter() - t0, world, cuda)
@@ -470,13 +499,18 @@ def run(args, world, rank):
     frames_total = new_frames * args.steps * world
     value = frames_total / el
     ms_step = el / args.steps * 1e3
-    err = (orb.errors(st) | err_warm[0], lx.errors(st) | err_warm[1])
+    err = list(err_warm)
+    ktot = kn = ltot = ln = 0
+    for sl in slots:
+        err[0] |= sl.orb.errors(sl.st)
+        err[1] |= sl.lx.errors(sl.st)
+        a, b = sl.orb.kernel_timing_read()
+        c, d = sl.lx.kernel_timing_read()
+        ktot, kn, ltot, ln = ktot + a, kn + b, ltot + c, ln + d
     # last timed batch's window (for the checks below)
-    lo_last = ((args.steps + args.warmup - 1) % nwin) * (B - 1)
+    lo_last = ((step_no[0] - 1) % nwin) * (B - 1)
 
     # ---------------------------------------------------------- rooflines
-    ktot, kn = orb.kernel_timing_read()
-    ltot, ln = lx.kernel_timing_read()
     bf_bytes = blur_fast_bytes(W, H) * B
     lp_bytes = lsd_prep_bytes(W, H) * B
     roof = {"bound": "hbm", "kernel": "orb_blur_fast_kernel (7x7 blur + FAST score, all 8 levels, one launch)",
@@ -513,8 +547,7 @@ def run(args, world, rank):
         digests["first_batch_tables"] = h.hexdigest()[:16]
         if world > 1:
             gather()
-            for w_ in pending:
-                w_.wait()
+            wait_gathers()
             torch.cuda.synchronize()
             if rank == 0:
                 digests["gathered_tables"] = []
@@ -545,7 +578,8 @@ def run(args, world, rank):
                                "previous frame" + (", RCCL gather of per-frame tables to rank 0" if args.gather
                                                    else ""),
                    "batch": B, "frames_per_step": new_frames, "width": W, "height": H,
-                   "parallelism": f"sequence-sharded x{world}", "gather": bool(args.gather)},
+                   "parallelism": f"sequence-sharded x{world}", "gather": bool(args.gather),
+                   "inflight": len(slots)},
         "roofline": roof,
         "roofline_lsd_prep": roof_lsd,
         "end_to_end_hbm": e2e,

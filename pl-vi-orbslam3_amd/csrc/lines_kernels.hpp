@@ -178,12 +178,12 @@ __global__ __launch_bounds__(256) void lsd_prep_kernel(const uint8_t* __restrict
 
 struct GrowCtx {
     const float* P;   // angle plane (degrees, NOTDEF = -1024)
-    unsigned* gbits;  // global USED bitmap (rows at or beyond the window)
-    lds_u32* bits;    // LDS USED ring: R rows x wpr words
+    unsigned* gbits;  // global USED bitmap (rows at or beyond the bits window)
+    lds_u32* bits;    // LDS USED ring: RB rows x wpr words
     lds_u32* qlds;    // LDS region queue (x | y << 16), QL entries
     unsigned* qglob;  // global queue spill
-    lds_f32* win;     // LDS angle ring: R rows x sw
-    int sw, sh, R, wpr, wb, QL, ys;  // ys = row of the current seed
+    lds_f32* win;     // LDS angle ring: R rows x sw (R = 0: angles from the plane)
+    int sw, sh, R, RB, wpr, wb, wbb, QL, ys;  // window bases wb (angles) / wbb (bits); ys = seed row
 };
 
 __device__ __forceinline__ unsigned gload_l2(unsigned* p) {
@@ -199,17 +199,25 @@ __device__ __forceinline__ void vm_drain() { __builtin_amdgcn_s_waitcnt(0); }
 // is unconditional (row clamped into the window); rows beyond the window
 // (rare) take the global bitmap.
 __device__ __forceinline__ bool used_get(const GrowCtx& g, int x, int y) {
-    const bool inwin = y < g.wb + g.R;
-    const int yy = inwin ? y : g.wb;
-    unsigned v = g.bits[(yy & (g.R - 1)) * g.wpr + (x >> 5)];
+    const bool inwin = y < g.wbb + g.RB;
+    const int yy = inwin ? y : g.wbb;
+    unsigned v = g.bits[(yy & (g.RB - 1)) * g.wpr + (x >> 5)];
     if (__builtin_expect(!inwin, 0)) v = gload_l2(g.gbits + (size_t)y * g.wpr + (x >> 5));
     return y < g.ys || ((v >> (x & 31)) & 1u);
 }
 __device__ __forceinline__ void used_set(const GrowCtx& g, int x, int y) {
     const unsigned b = 1u << (x & 31);
-    if (__builtin_expect(y < g.wb + g.R, 1))
-        __atomic_fetch_or(&g.bits[(y & (g.R - 1)) * g.wpr + (x >> 5)], b, __ATOMIC_RELAXED);  // ds_or_b32
+    if (__builtin_expect(y < g.wbb + g.RB, 1))
+        __atomic_fetch_or(&g.bits[(y & (g.RB - 1)) * g.wpr + (x >> 5)], b, __ATOMIC_RELAXED);  // ds_or_b32
     else __hip_atomic_fetch_or(g.gbits + (size_t)y * g.wpr + (x >> 5), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// OR a 64-pixel chunk mask (pixels xb..xb+63 of row y, row y inside the
+// window, xb a multiple of 64) into the USED bits: lanes 0 and 1 take a word each
+__device__ __forceinline__ void used_set_chunk(const GrowCtx& g, int xb, int y, unsigned long long mask, int lane) {
+    const unsigned w = lane == 0 ? (unsigned)mask : (unsigned)(mask >> 32);
+    if (lane < 2 && w) __atomic_fetch_or(&g.bits[(y & (g.RB - 1)) * g.wpr + (xb >> 5) + lane], w, __ATOMIC_RELAXED);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 }
 __device__ __forceinline__ unsigned q_get(const GrowCtx& g, int i) {
     if (__builtin_expect(i < g.QL, 1)) return g.qlds[i];
@@ -220,6 +228,7 @@ __device__ __forceinline__ void q_put(const GrowCtx& g, int i, unsigned v) {
     else gstore_l2(g.qglob + (i - g.QL), v);
 }
 __device__ __forceinline__ float deg_at(const GrowCtx& g, int x, int y) {
+    if (g.R == 0) return g.P[(size_t)y * g.sw + x];
     const bool inwin = y < g.wb + g.R;
     const int yy = inwin ? y : g.wb;
     float v = g.win[(yy & (g.R - 1)) * g.sw + x];
@@ -277,9 +286,7 @@ __device__ __forceinline__ double shfl_d(double v, int src) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-// Load image rows [r0, r1) into their window slots: angles from the angle
-// plane, USED bits from the global bitmap (set while the rows were beyond
-// the window).
+// Load image rows [r0, r1) into their angle-window slots.
 __device__ __forceinline__ void win_load_rows(const GrowCtx& g, int r0, int r1, int lane) {
     const int n = (r1 - r0) * g.sw;
     const float* src = g.P + (size_t)r0 * g.sw;
@@ -298,10 +305,14 @@ __device__ __forceinline__ void win_load_rows(const GrowCtx& g, int r0, int r1, 
         const int row = r0 + i / g.sw, x = i % g.sw;
         g.win[(row & (g.R - 1)) * g.sw + x] = src[i];
     }
+}
+// Load the USED bits of rows [r0, r1) into their bits-window slots from the
+// global bitmap (set while the rows were beyond the window).
+__device__ __forceinline__ void bits_load_rows(const GrowCtx& g, int r0, int r1, int lane) {
     const int nw = (r1 - r0) * g.wpr;
     for (int k = lane; k < nw; k += 64) {
         const int row = r0 + k / g.wpr, w = k % g.wpr;
-        g.bits[(row & (g.R - 1)) * g.wpr + w] = gload_l2(g.gbits + (size_t)row * g.wpr + w);
+        g.bits[(row & (g.RB - 1)) * g.wpr + w] = gload_l2(g.gbits + (size_t)row * g.wpr + w);
     }
 }
 
@@ -314,7 +325,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                                                       unsigned* __restrict__ qspill, size_t qspill_frame,
                                                       double prec, LsdRegion* __restrict__ regs, unsigned* __restrict__ regpts,
                                                       size_t regpts_frame, int* __restrict__ nlines,
-                                                      int* __restrict__ err, int R, int QL, int nOct,
+                                                      int* __restrict__ err, int R, int RB, int QL, int nOct,
                                                       unsigned long long* __restrict__ stats) {
     extern __shared__ __align__(16) unsigned lds_u[];
     // latency-bound serial chain: win the SIMD arbiter against co-resident
@@ -330,7 +341,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
     const int sw = od.sw, sh = od.sh;
     const int lane = threadIdx.x;
     GrowCtx g;
-    g.sw = sw; g.sh = sh; g.R = R; g.QL = QL;
+    g.sw = sw; g.sh = sh; g.R = R; g.RB = RB; g.QL = QL;
     g.wpr = (sw + 31) >> 5;
     g.P = pix + od.soff + (size_t)f * od.splane;
     const float2* SC = pixcs + od.soff + (size_t)f * od.splane;
@@ -341,13 +352,14 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
     g.qglob = qspill + (size_t)(f * nOct + o) * qspill_frame;
     // LDS: USED ring | queue | angle ring
     g.bits = (lds_u32*)lds_u;
-    g.qlds = g.bits + R * g.wpr;
+    g.qlds = g.bits + RB * g.wpr;
     g.win = (lds_f32*)(g.qlds + QL);
     g.wb = 0;
+    g.wbb = 0;
     g.ys = 0;
     for (int i = lane; i < sh * g.wpr; i += 64) g.gbits[i] = 0u;
-    vm_drain();
-    win_load_rows(g, 0, min(R, sh), lane);
+    for (int i = lane; i < RB * g.wpr; i += 64) g.bits[i] = 0u;
+    if (R) win_load_rows(g, 0, min(R, sh), lane);
     vm_drain();
     __syncthreads();
     int nout = 0;
@@ -364,28 +376,64 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
     unsigned long long s_ph[4] = {0, 0, 0, 0};
     constexpr bool do_stats = STATS;  // diagnostic variant only (keeps SGPRs free in the product kernel)
     const unsigned long long t_begin = do_stats ? __builtin_amdgcn_s_memtime() : 0;
-    const int half = R / 2;
+    const int half = R / 2, halfb = RB / 2;
     for (int y = 0; y < sh - 1; ++y) {
-        // slide the window by half its height once row y is past its middle;
+        // slide each window by half its height once row y is past its middle;
         // the rows leaving it are above y and never read again
-        while (y >= g.wb + half && g.wb + R < sh) {
+        bool slid = false;
+        while (R && y >= g.wb + half && g.wb + R < sh) {
             const int r0 = g.wb + R, r1 = min(sh, r0 + half);
             win_load_rows(g, r0, r1, lane);
             g.wb += r1 - r0;
+            slid = true;
+        }
+        while (y >= g.wbb + halfb && g.wbb + RB < sh) {
+            const int r0 = g.wbb + RB, r1 = min(sh, r0 + halfb);
+            bits_load_rows(g, r0, r1, lane);
+            g.wbb += r1 - r0;
+            slid = true;
+        }
+        if (slid) {
             vm_drain();
             __syncthreads();
         }
         g.ys = y;
         for (int xb = 0; xb < sw - 1; xb += 64) {
             const int x = xb + lane;
-            bool cand = false;
-            if (x < sw - 1) cand = !used_get(g, x, y) && deg_at(g, x, y) != kNotdefF;
+            bool cand = false, grow = false;
+            if (x < sw - 1) {
+                const float d0 = deg_at(g, x, y);
+                cand = !used_get(g, x, y) && d0 != kNotdefF;
+                // A seed's first round tests its forward neighbours (rows above y
+                // are all USED) against its own angle: when none of them is aligned
+                // (a static property, whatever is USED), the region stays at size 1
+                // < min_reg_size and the seed only marks itself USED.
+                if (cand) {
+                    // neighbours (x-1,y) (x+1,y) (x-1,y+1) (x,y+1) (x+1,y+1)
+#pragma unroll 1
+                    for (int k = 0; k < 5 && !grow; ++k) {
+                        const int nx = x + (k == 0 || k == 2 ? -1 : k == 3 ? 0 : 1), ny = y + (k >= 2);
+                        const float dn = nx >= 0 ? deg_at(g, nx, ny) : kNotdefF;
+                        grow = is_aligned_fast(dn, d0, pdeg, prec);
+                    }
+                }
+            }
             unsigned long long m = __ballot(cand);
             if (!m) continue;
+            const unsigned long long gm = __ballot(grow);
+            // USED bits of seeds that cannot grow, set before the next seed grows
+            // (it must see them USED, as the reference's scan order implies)
+            unsigned long long pend = m & ~gm;
+            m &= gm;
             while (m) {
                 const int b = __ffsll((long long)m) - 1;
                 m &= m - 1;
                 const int sx = xb + b;
+                const unsigned long long before = pend & ((1ull << b) - 1ull);
+                if (before) {
+                    used_set_chunk(g, xb, y, before, lane);
+                    pend &= ~before;
+                }
                 if (used_get(g, sx, y)) continue;  // absorbed by an earlier region of this chunk
                 // ---- region_grow (lsd.cpp:635-686)
                 float reg_deg = deg_at(g, sx, y);  // reg_angle = (double)reg_deg * DEG_TO_RADS
@@ -490,7 +538,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                                 q_put(g, reg_size + __popcll(C & below), (unsigned)nx | ((unsigned)ny << 16));
                             }
                             // global USED bits / queue spill must land before they are read back
-                            if (__ballot(mine && ny >= g.wb + R) || reg_size + nc > QL) vm_drain();
+                            if (__ballot(mine && ny >= g.wbb + RB) || reg_size + nc > QL) vm_drain();
                             reg_size += nc;
                             sumdx = readlane_f(pfx, nc - 1);
                             sumdy = readlane_f(pfy, nc - 1);
@@ -518,6 +566,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                 }
                 if (do_stats) s_rect += __builtin_amdgcn_s_memtime() - tr0;
             }
+            if (pend) used_set_chunk(g, xb, y, pend, lane);
         }
     }
     if (lane == 0) {

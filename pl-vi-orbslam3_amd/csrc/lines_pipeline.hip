@@ -272,30 +272,40 @@ struct LinePipeline {
             err.alloc(sizeof(int) * Bcap) || staging.alloc((size_t)W * H))
             return PLVI_E_HIP;
         PLVI_CHECK(hipMemset(err.p, 0, sizeof(int) * Bcap));
-        // region-growing LDS: rect staging + R-row USED/angle window + queue,
-        // sized so that several waves share a CU and leave LDS to the kernels that
-        // run concurrently (PLVI_GROW_LDS, default 6 KB: R = 2 rows, 5.1 KB at
-        // 640 px; measured vs R = 4: region growing 48.0 -> 43.2 ms per 3072
-        // frames, whole step +0.8 %)
+        // region-growing LDS: USED-bits ring (RB rows) + queue + angle ring (R
+        // rows, 0 = angles straight from the plane), sized so that every wave of
+        // a 3072-frame batch is resident with the kernels that run concurrently.
+        // PLVI_GROW_RB: bits rows (power of two >= 2, default 64: regions rarely
+        // reach 32 rows below their seed, so USED updates stay in LDS);
+        // PLVI_GROW_LDS: total budget (default 6 KB) from which R takes the
+        // largest power of two that fits; PLVI_GROW_RD overrides R.
         size_t maxSw = 0;
         for (auto& d : oct) maxSw = std::max(maxSw, (size_t)d.sw);
+        const size_t wprMax = (maxSw + 31) / 32;
         size_t budget = 6 * 1024;
         if (const char* e = getenv("PLVI_GROW_LDS")) budget = (size_t)atol(e);
         budget = std::min<size_t>(budget, 160 * 1024);
+        growRB = 64;
+        if (const char* e = getenv("PLVI_GROW_RB")) growRB = atoi(e);
+        if (growRB < 2 || (growRB & (growRB - 1)) || growRB > 1024) return PLVI_E_BADARG;
         growQL = budget >= 32 * 1024 ? 1024 : 256;
-        const size_t fixed = (size_t)growQL * sizeof(unsigned);
-        const size_t perRow = maxSw * sizeof(float) + (maxSw + 31) / 32 * sizeof(unsigned);
-        growR = 2;
-        budget = std::max(budget, fixed + perRow * 2);  // at least a 2-row window
-        if (budget > 160 * 1024) return PLVI_E_BADARG;
-        while (growR * 2 <= 1024 && fixed + perRow * growR * 2 <= budget) growR *= 2;
+        const size_t fixed = (size_t)growQL * sizeof(unsigned) + (size_t)growRB * wprMax * sizeof(unsigned);
+        const size_t perRow = maxSw * sizeof(float);
+        growR = 0;
+        if (fixed + perRow * 2 <= budget) {
+            growR = 2;
+            while (growR * 2 <= 1024 && fixed + perRow * growR * 2 <= budget) growR *= 2;
+        }
+        if (const char* e = getenv("PLVI_GROW_RD")) growR = atoi(e);
+        if (growR < 0 || (growR & (growR - 1)) || growR == 1 || growR > 1024) return PLVI_E_BADARG;
         growSmem = fixed + perRow * growR;
+        if (growSmem > 160 * 1024) return PLVI_E_BADARG;
         for (const void* k : {(const void*)lsd_grow_kernel<false>, (const void*)lsd_grow_kernel<true>})
             PLVI_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)growSmem));
         return PLVI_OK;
     }
     size_t growSmem = 0;
-    int growR = 0, growQL = 0;
+    int growR = 0, growRB = 0, growQL = 0;
     unsigned long long* growStats = nullptr;  // diagnostic cycle counters (plvi_lines_debug_stats)
 
     int profile(int on) {
@@ -365,7 +375,7 @@ struct LinePipeline {
                            (const float*)pix.as<float>(), (const double*)modg.as<double>(),
                            (const float2*)seedcs.as<float2>(), gbits.as<unsigned>(), gbitsFrame,
                            qspill.as<unsigned>(), qspillFrame, prec, regs.as<LsdRegion>(), regpts.as<unsigned>(),
-                           qspillFrame, nlines.as<int>(), err.as<int>(), growR, growQL, nOct, growStats);
+                           qspillFrame, nlines.as<int>(), err.as<int>(), growR, growRB, growQL, nOct, growStats);
         hipLaunchKernelGGL(lsd_rect_kernel, dim3(kRectBlocks, nOct, nf), dim3(256), 0, st, d_oct.as<LineOctDev>(),
                            (const double*)modg.as<double>(), (const LsdRegion*)regs.as<LsdRegion>(),
                            (const unsigned*)regpts.as<unsigned>(), qspillFrame, (const int*)nlines.as<int>(), prec,

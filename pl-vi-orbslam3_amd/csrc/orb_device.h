@@ -9,11 +9,19 @@ namespace plvi {
 constexpr int kOrbMaxLevels = 16;
 constexpr int kOrbMaxRoots = 8;
 constexpr int kOrbCellMax = 64;  // max detection-window side (wCell+2 < 64)
+#ifndef PLVI_BF_ALIGN
+#define PLVI_BF_ALIGN 32
+#endif
+constexpr int kBfAlign = PLVI_BF_ALIGN;  // byte alignment of the blur / score / candidate rows and strips
 
 struct OrbLevelDev {
     int w, h;
     long long off;    // byte offset of this level's frame-0 plane in pyr/blur/score/cand
-    long long plane;  // bytes per frame plane (w*h)
+    long long plane;  // bytes per frame plane (w*h) of the pyramid
+    // blur / FAST score / candidate planes: rows padded to bpitch (a multiple
+    // of kBfAlign) so that every blur+FAST strip writes whole aligned segments
+    int bpitch;
+    long long boff, bplane;
     int minB;         // EDGE_THRESHOLD-3 = 16
     int rw, rh;       // relative region (maxBorder-minBorder)
     int nCols, nRows, wCell, hCell;
@@ -34,10 +42,11 @@ struct OrbLevelDev {
     int xtab;                      // offset of this level's packed column table (orb_pyramid_kernel)
 };
 
-// One column strip of a level for the blur + FAST kernel: output columns
-// [x0, x0 + 58) (64 lanes minus a 3-px halo each side), rows [y0, y1).
+// One strip of a level for the blur + FAST kernel: output columns [x0, x1)
+// (x0 a multiple of kBfAlign, x1 - x0 <= kBfCols, four per lane after a halo
+// lane), rows [y0, y1).
 struct OrbStripDev {
-    int level, x0, y0, y1;
+    int level, x0, x1, y0, y1;
 };
 
 struct OrbCellDev {

@@ -235,17 +235,21 @@ __global__ __launch_bounds__(64 * (kPyrFrames + 1)) void orb_pyramid_kernel(
 
 // ---------------------------------------------------------------------------
 // K1b: 7x7 fixed-point Gaussian blur (ORBextractor.cc:1115; A.4) and FAST
-// score map (A.3) of every level in one launch.  One wave per column strip:
-// lane = image column (58 output columns + 3 halo lanes each side), rows
-// streamed top to bottom.  The horizontal taps come from neighbouring lanes
-// (DPP wave shifts), the vertical taps and the FAST column neighbours from a
-// 7-row register window, so the image is read once and never staged
-// through LDS.  The exact compass pre-test of K1 (two neighbouring compass
-// points beyond T) rejects ~90 % of pixels; survivors are queued (row, lane)
-// and scored 64 at a time from an LDS ring of the last 32 raw rows.
-// Level 0 also writes its pyramid plane (the input copy).
+// score map (A.3) of every level in one launch.  One wave per strip of up to
+// kBfCols output columns x kBfRows rows: lane L holds the four columns
+// x0 - 4 + 4L .. +3 as one dword (lane 0 and the lane after the last output
+// lane are the 3-px halo), rows streamed top to bottom.  Vertical pass first,
+// SWAR: the 7-row window holds each row as its even / odd bytes in 16-bit
+// fields (tap sums <= 255 * 256 never carry across a field), 7 v_mad_u32_u24
+// per field pair; horizontal pass on those sums with v_dot2_u32_u16 and the
+// neighbouring lanes' pairs (DPP wave shifts).  Exact integer sums rounded
+// once, so the pass order does not change the result.  The image is read once with dword
+// loads and the blur / score / level-0 planes are written with dword stores.
+// The exact compass pre-test of K1 (two neighbouring compass points beyond
+// T) rejects ~90 % of pixels; survivors are queued (row, column) and scored
+// 64 at a time from an LDS ring of the last 32 raw rows.
 // ---------------------------------------------------------------------------
-constexpr int kStripOut = 58, kStripRows = 64, kRingRows = 32;
+constexpr int kBfCols = (244 / kBfAlign) * kBfAlign, kBfRows = 128, kRingRows = 32, kRingW = 256, kBfQCap = 320;
 
 __device__ __forceinline__ int lane_from_left(int v) {  // lane i <- lane i-1 (wave_shr:1)
     return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
@@ -253,8 +257,27 @@ __device__ __forceinline__ int lane_from_left(int v) {  // lane i <- lane i-1 (w
 __device__ __forceinline__ int lane_from_right(int v) {  // lane i <- lane i+1 (wave_shl:1)
     return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false);
 }
+__device__ __forceinline__ uint32_t ld_u32(const uint8_t* p) {  // any alignment (gfx950 unaligned access)
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);
+    return v;
+}
+__device__ __forceinline__ void st_u32(uint8_t* p, uint32_t v) {
+    __builtin_memcpy(p, &v, 4);
+}
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+}
+__device__ __forceinline__ int byte_of(uint32_t v, int j) { return (int)((v >> (8 * j)) & 255u); }
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+__device__ __forceinline__ uint32_t udot2(uint32_t a, uint32_t b, uint32_t c) {  // a.lo*b.lo + a.hi*b.hi + c
+    return __builtin_amdgcn_udot2(as_u16x2(a), as_u16x2(b), c, false);
+}
 
-__device__ __forceinline__ int fast_S_ring(const uint8_t (*rg)[64], int y, int c) {
+__device__ __forceinline__ int fast_S_ring(const uint8_t (*rg)[kRingW], int y, int c) {
 #define RG(dy, dx) ((int)rg[(y + (dy)) & (kRingRows - 1)][c + (dx)])
     const int v = RG(0, 0);
     int d[16];
@@ -275,25 +298,19 @@ __device__ __forceinline__ int fast_S_ring(const uint8_t (*rg)[64], int y, int c
     d[14] = v - RG(2, -2);
     d[15] = v - RG(3, -1);
 #undef RG
-    int mn1[16], mx1[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        mn1[k] = min(d[k], d[(k + 1) & 15]);
-        mx1[k] = max(d[k], d[(k + 1) & 15]);
-    }
-    int mn2[16], mx2[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        mn2[k] = min(mn1[k], mn1[(k + 2) & 15]);
-        mx2[k] = max(mx1[k], mx1[(k + 2) & 15]);
-    }
+    // max over the 16 arcs of 9 contiguous points of min(arc) (brighter) and
+    // of -max(arc) (darker); arcs starting at k and k+1 share d[k+1..k+8]
     int A = -1000, Bm = 1000;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int mn8 = min(mn2[k], mn2[(k + 4) & 15]);
-        const int mx8 = max(mx2[k], mx2[(k + 4) & 15]);
-        A = max(A, min(mn8, d[(k + 8) & 15]));
-        Bm = min(Bm, max(mx8, d[(k + 8) & 15]));
+    for (int k = 0; k < 16; k += 2) {
+        int a = d[(k + 1) & 15], b = a;
+#pragma unroll
+        for (int t = 2; t <= 8; ++t) {
+            a = min(a, d[(k + t) & 15]);
+            b = max(b, d[(k + t) & 15]);
+        }
+        A = max(A, max(min(a, d[k]), min(a, d[(k + 9) & 15])));
+        Bm = min(Bm, min(max(b, d[k]), max(b, d[(k + 9) & 15])));
     }
     return max(A, -Bm);
 }
@@ -303,103 +320,192 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
                                                            const uint8_t* __restrict__ frames, size_t f_frame,
                                                            size_t f_row, uint8_t* __restrict__ pyr,
                                                            uint8_t* __restrict__ blur, uint8_t* __restrict__ score,
-                                                           int k0, int k1, int k2, int k3, int tmin) {
-    __shared__ uint8_t ring[kRingRows][64];
-    __shared__ unsigned short q[128];
-    const OrbStripDev sd = strips[blockIdx.x];
-    const int f = blockIdx.y, lane = threadIdx.x;
+                                                           int k0, int k1, int k2, int k3, int tmin, int nstrips,
+                                                           int nf) {
+    __shared__ __align__(16) uint8_t ring[kRingRows][kRingW];
+    __shared__ unsigned q[kBfQCap];
+    // XCD-affine mapping: blocks b and b + 8 share an XCD (and its L2), so
+    // every strip of a frame goes to one XCD and the rows / columns two
+    // strips share are fetched from HBM once
+    const int bx = blockIdx.x, xk = bx >> 3;
+    const int f = (bx & 7) + 8 * (xk / nstrips);
+    if (f >= nf) return;
+    const OrbStripDev sd = strips[xk % nstrips];
+    const int lane = threadIdx.x;
     const OrbLevelDev& L = lvs[sd.level];
     const int w = L.w, h = L.h;
-    const int c = sd.x0 - 3 + lane;
-    const int gc = reflect1(c, w);
-    const bool outl = lane >= 3 && lane < 3 + kStripOut && c < w;
-    const bool fastl = outl && c >= 3 && c < w - 3;
+    const int c0 = sd.x0 - 4 + 4 * lane;          // first of this lane's four columns
+    const bool need = lane <= (sd.x1 - sd.x0 + 3) / 4 + 1;  // output lanes and the two halo lanes
+    const bool inner = need && c0 >= 0 && c0 + 4 <= w;     // all four inside the row: one dword
+    const int xe = min(sd.x1, w);
+    const bool outl = lane >= 1 && c0 < xe;        // output lane
+    const int nout = min(4, xe - c0);              // its output columns
     const uint8_t* src = sd.level == 0 ? frames + (size_t)f * f_frame : pyr + L.off + (size_t)f * L.plane;
     const size_t srow = sd.level == 0 ? f_row : (size_t)w;
     uint8_t* Dp = pyr + L.off + (size_t)f * L.plane;
-    uint8_t* Bp = blur + L.off + (size_t)f * L.plane;
-    uint8_t* Sp = score + L.off + (size_t)f * L.plane;
+    uint8_t* Bp = blur + L.boff + (size_t)f * L.bplane;
+    uint8_t* Sp = score + L.boff + (size_t)f * L.bplane;
+    const int bw = L.bpitch;
     const int T = max(tmin + 1, 1);
+    unsigned fastok = 0;  // pixel j may be a FAST candidate (column in [3, w-3), output column)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (outl && j < nout && c0 + j >= 3 && c0 + j < w - 3) fastok |= 1u << j;
     const int y0 = sd.y0, y1 = sd.y1;
-    int pw[7] = {0, 0, 0, 0, 0, 0, 0}, hw[7] = {0, 0, 0, 0, 0, 0, 0};
+    // rows r-6..r as even bytes (columns c0, c0+2) and odd bytes (c0+1, c0+3) in 16-bit fields
+    uint32_t pe[7] = {0, 0, 0, 0, 0, 0, 0}, po[7] = {0, 0, 0, 0, 0, 0, 0};
+    const uint32_t kt[7] = {(uint32_t)k0, (uint32_t)k1, (uint32_t)k2, (uint32_t)k3,
+                            (uint32_t)k2, (uint32_t)k1, (uint32_t)k0};
+    auto pk = [](int lo, int hi) { return (uint32_t)lo | (uint32_t)hi << 16; };
     int nq = 0;      // queued candidates (wave-uniform)
     int oldest = 0;  // row of the oldest queued candidate
-    auto flush = [&](int n) {  // score the first n queued candidates
-        __syncthreads();
+    auto flush = [&](int n) {  // score the first n (<= 64) queued candidates
+        // one wave per block: wave-scope ordering only (no store drain).  The
+        // candidate bytes below land after this wave's earlier zero stores of
+        // the same pixels: a wavefront observes its own memory operations in
+        // program order (wavefront-scope acquire/release needs no waits).
+        wave_sync();
         if (lane < n) {
-            const int e = q[lane];
-            const int yy = e >> 6, ln = e & 63;
-            const int Sv = fast_S_ring(ring, yy, ln);
-            Sp[(size_t)yy * w + (sd.x0 - 3 + ln)] = (uint8_t)(Sv >= T ? Sv - 1 : 0);
+            const unsigned e = q[lane];
+            const int yy = (int)(e >> 8), rc = (int)(e & 255u);
+            const int Sv = fast_S_ring(ring, yy, rc);
+            Sp[(size_t)yy * bw + (sd.x0 - 4 + rc)] = (uint8_t)(Sv >= T ? Sv - 1 : 0);
         }
-        __syncthreads();
+        wave_sync();
         const int rest = nq - n;
-        unsigned short t0 = 0, t1 = 0;
-        if (lane < rest) t0 = q[n + lane];
-        if (lane + 64 < rest) t1 = q[n + 64 + lane];
-        __syncthreads();
-        if (lane < rest) q[lane] = t0;
-        if (lane + 64 < rest) q[64 + lane] = t1;
+        unsigned t[(kBfQCap - 64) / 64];
+#pragma unroll
+        for (int k = 0; k < (kBfQCap - 64) / 64; ++k) t[k] = lane + 64 * k < rest ? q[n + lane + 64 * k] : 0u;
+        wave_sync();
+#pragma unroll
+        for (int k = 0; k < (kBfQCap - 64) / 64; ++k)
+            if (lane + 64 * k < rest) q[lane + 64 * k] = t[k];
         nq = rest;
-        __syncthreads();
-        oldest = rest > 0 ? (int)(q[0] >> 6) : 0;
+        wave_sync();
+        oldest = rest > 0 ? (int)(q[0] >> 8) : 0;
     };
+    // rows rb..rb+7 of the source (reflected), four columns per lane
+    auto load_rows = [&](int rb, uint32_t* pv) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int r = rb + k;
+            pv[k] = (inner && r < y1 + 3) ? ld_u32(src + (size_t)reflect1(r, h) * srow + c0) : 0u;
+        }
+        if (need && !inner) {  // image-edge lanes: reflected columns byte by byte
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int r = rb + k;
+                if (r < y1 + 3) {
+                    const uint8_t* rp = src + (size_t)reflect1(r, h) * srow;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) pv[k] |= (uint32_t)rp[reflect1(c0 + j, w)] << (8 * j);
+                }
+            }
+        }
+    };
+    uint32_t pv[8];
+    load_rows(y0 - 3, pv);
     for (int rb = y0 - 3; rb < y1 + 3; rb += 8) {
         // writing rows rb..rb+7 replaces rows rb-32..rb-25 of the ring; a
         // queued row yy needs rows yy-3..yy+3
         if (nq > 0 && oldest - 3 < rb - (kRingRows - 8)) flush(nq);
-        int pv[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int r = rb + k;
-            pv[k] = r < y1 + 3 ? src[(size_t)reflect1(r, h) * srow + gc] : 0;
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) ring[(rb + k) & (kRingRows - 1)][lane] = (uint8_t)pv[k];
+        for (int k = 0; k < 8; ++k)
+            *reinterpret_cast<uint32_t*>(&ring[(rb + k) & (kRingRows - 1)][4 * lane]) = pv[k];
+        // next batch in flight while this one is filtered
+        if (rb + 8 < y1 + 3) load_rows(rb + 8, pv);
 #pragma unroll 1
         for (int k = 0; k < 8; ++k) {
             const int r = rb + k;
             if (r >= y1 + 3) break;
-            const int v = ring[r & (kRingRows - 1)][lane];
-            const int m1 = lane_from_left(v), m2 = lane_from_left(m1), m3 = lane_from_left(m2);
-            const int p1 = lane_from_right(v), p2 = lane_from_right(p1), p3 = lane_from_right(p2);
-            const int hs = k0 * (m3 + p3) + k1 * (m2 + p2) + k2 * (m1 + p1) + k3 * v;
+            const uint32_t V = *reinterpret_cast<const uint32_t*>(&ring[r & (kRingRows - 1)][4 * lane]);
 #pragma unroll
-            for (int j = 0; j < 6; ++j) {
-                pw[j] = pw[j + 1];
-                hw[j] = hw[j + 1];
+            for (int rr = 0; rr < 6; ++rr) {
+                pe[rr] = pe[rr + 1];
+                po[rr] = po[rr + 1];
             }
-            pw[6] = v;
-            hw[6] = hs;
+            pe[6] = V & 0x00ff00ffu;
+            po[6] = (V >> 8) & 0x00ff00ffu;
             const int y = r - 3;
             if (y < y0) continue;
-            // ---- output row y: rows y-3..y+3 are pw[0..6]
-            const unsigned s = (unsigned)(k0 * (hw[0] + hw[6]) + k1 * (hw[1] + hw[5]) + k2 * (hw[2] + hw[4]) +
-                                          k3 * hw[3]);
-            const int cv = pw[3];
-            const int cl = lane_from_left(lane_from_left(lane_from_left(cv)));     // column c-3
-            const int cr = lane_from_right(lane_from_right(lane_from_right(cv)));  // column c+3
-            const int d0 = cv - pw[6], d4 = cv - cr, d8 = cv - pw[0], d12 = cv - cl;
-            const bool cand = fastl && y >= 3 && y < h - 3 &&
-                              (((d0 >= T) & (d4 >= T)) | ((d4 >= T) & (d8 >= T)) | ((d8 >= T) & (d12 >= T)) |
-                               ((d12 >= T) & (d0 >= T)) | ((d0 <= -T) & (d4 <= -T)) | ((d4 <= -T) & (d8 <= -T)) |
-                               ((d8 <= -T) & (d12 <= -T)) | ((d12 <= -T) & (d0 <= -T)));
+            // ---- output row y: rows y-3..y+3 are pe/po[0..6]
+            uint32_t E = 0, O = 0;  // vertical sums: E = (c0, c0+2), O = (c0+1, c0+3)
+#pragma unroll
+            for (int t = 0; t < 7; ++t) {  // fields < 2^24: v_mad_u32_u24
+                E += __umul24(kt[t], pe[t]);
+                O += __umul24(kt[t], po[t]);
+            }
+            const uint32_t El = (uint32_t)lane_from_left((int)E), Ol = (uint32_t)lane_from_left((int)O);
+            const uint32_t Er = (uint32_t)lane_from_right((int)E), Or = (uint32_t)lane_from_right((int)O);
+            // El = (c0-4, c0-2), Ol = (c0-3, c0-1), Er = (c0+4, c0+6), Or = (c0+5, c0+7)
+            const unsigned h0 = udot2(Ol, pk(k0, k2), udot2(E, pk(k3, k1), udot2(O, pk(k2, k0), udot2(El, pk(0, k1), 0u))));
+            const unsigned h1 = udot2(El, pk(0, k0), udot2(Ol, pk(0, k1), udot2(E, pk(k2, k2),
+                                udot2(O, pk(k3, k1), udot2(Er, pk(k0, 0), 0u)))));
+            const unsigned h2 = udot2(Ol, pk(0, k0), udot2(E, pk(k1, k3), udot2(O, pk(k2, k2),
+                                udot2(Er, pk(k1, 0), udot2(Or, pk(k0, 0), 0u)))));
+            const unsigned h3 = udot2(E, pk(k0, k2), udot2(O, pk(k1, k3), udot2(Er, pk(k2, k0), udot2(Or, pk(k1, 0), 0u))));
+            const uint32_t Bv = min((h0 + 32768u) >> 16, 255u) | min((h1 + 32768u) >> 16, 255u) << 8 |
+                                min((h2 + 32768u) >> 16, 255u) << 16 | min((h3 + 32768u) >> 16, 255u) << 24;
+            const uint32_t cvw = pe[3] | po[3] << 8;
+            const uint32_t L3 = __builtin_amdgcn_alignbyte(cvw, (uint32_t)lane_from_left((int)cvw), 1);   // column c-3
+            const uint32_t R3 = __builtin_amdgcn_alignbyte((uint32_t)lane_from_right((int)cvw), cvw, 3);  // column c+3
+            // compass pre-test on 16-bit fields (even pixels 0/2, odd pixels 1/3):
+            // brighter-by-T / darker-by-T at two cyclically adjacent compass points
+            // (0 = row+3, 4 = col+3, 8 = row-3, 12 = col-3)
+            const uint32_t ce[2] = {pe[3], po[3]};
+            const uint32_t p0[2] = {pe[6], po[6]}, p8[2] = {pe[0], po[0]};
+            const uint32_t p4[2] = {R3 & 0x00ff00ffu, (R3 >> 8) & 0x00ff00ffu};
+            const uint32_t p12[2] = {L3 & 0x00ff00ffu, (L3 >> 8) & 0x00ff00ffu};
+            unsigned candm = 0;  // bit j: pixel j passes the pre-test
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const u16x2 c = as_u16x2(ce[e]);
+                const u16x2 q0 = as_u16x2(p0[e]), q4 = as_u16x2(p4[e]), q8 = as_u16x2(p8[e]), q12 = as_u16x2(p12[e]);
+                const u16x2 b0 = __builtin_elementwise_sub_sat(c, q0), b4 = __builtin_elementwise_sub_sat(c, q4);
+                const u16x2 b8 = __builtin_elementwise_sub_sat(c, q8), b12 = __builtin_elementwise_sub_sat(c, q12);
+                const u16x2 d0 = __builtin_elementwise_sub_sat(q0, c), d4 = __builtin_elementwise_sub_sat(q4, c);
+                const u16x2 d8 = __builtin_elementwise_sub_sat(q8, c), d12 = __builtin_elementwise_sub_sat(q12, c);
+                const u16x2 mb = __builtin_elementwise_max(
+                    __builtin_elementwise_max(__builtin_elementwise_min(b0, b4), __builtin_elementwise_min(b4, b8)),
+                    __builtin_elementwise_max(__builtin_elementwise_min(b8, b12), __builtin_elementwise_min(b12, b0)));
+                const u16x2 md = __builtin_elementwise_max(
+                    __builtin_elementwise_max(__builtin_elementwise_min(d0, d4), __builtin_elementwise_min(d4, d8)),
+                    __builtin_elementwise_max(__builtin_elementwise_min(d8, d12), __builtin_elementwise_min(d12, d0)));
+                const uint32_t m = as_u32(__builtin_elementwise_max(mb, md));
+                candm |= ((m & 0xffffu) >= (unsigned)T ? 1u : 0u) << e;
+                candm |= ((m >> 16) >= (unsigned)T ? 4u : 0u) << e;
+            }
+            if (!(y >= 3 && y < h - 3)) candm = 0;
+            candm &= fastok;
+            bool cand[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) cand[j] = (candm >> j) & 1u;
             if (outl) {
-                const size_t o = (size_t)y * w + c;
-                if (sd.level == 0) Dp[o] = (uint8_t)cv;
-                Bp[o] = (uint8_t)min((s + 32768u) >> 16, 255u);
-                if (!cand) Sp[o] = 0;
+                const uint32_t o = (uint32_t)(y * w + c0), ob = (uint32_t)(y * bw + c0);
+                if (nout == 4) {
+                    if (sd.level == 0) st_u32(Dp + o, cvw);
+                    st_u32(Bp + ob, Bv);
+                    st_u32(Sp + ob, 0u);  // candidates are overwritten by flush (wave-ordered)
+                } else {
+                    for (int j = 0; j < nout; ++j) {
+                        if (sd.level == 0) Dp[o + j] = (uint8_t)byte_of(cvw, j);
+                        Bp[ob + j] = (uint8_t)byte_of(Bv, j);
+                        Sp[ob + j] = 0;
+                    }
+                }
             }
-            const unsigned long long m = __ballot(cand);
-            if (m) {
-                if (nq == 0) oldest = y;
-                if (cand) q[nq + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned short)((y << 6) | lane);
+            const int nq0 = nq;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const unsigned long long m = __ballot(cand[j]);
+                if (cand[j]) q[nq + __popcll(m & ((1ull << lane) - 1ull))] = ((unsigned)y << 8) | (unsigned)(4 * lane + j);
                 nq += __popcll(m);
-                if (nq >= 64) flush(64);
             }
+            if (nq0 == 0 && nq > 0) oldest = y;
+            while (nq >= 64) flush(64);
         }
     }
-    if (nq > 0) flush(nq);
+    while (nq > 0) flush(min(nq, 64));
 }
 
 // ---------------------------------------------------------------------------
@@ -410,9 +516,9 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
 // neighbour below the threshold counts as 0, and a survivor is strictly
 // greater than all 8 (A.3).
 // One wave per (cell, frame), lane = window column (windows are < 64 wide):
-// the window's score column is held in registers (4 rows per dword),
-// horizontal neighbours come over DPP lane shifts, so there is no LDS and
-// no per-pixel index arithmetic.
+// the window is staged column-per-lane in LDS, each row's 8 neighbours come
+// from the rows above / below and DPP lane shifts, and both thresholds are
+// decided in the same sweep, so there is no per-pixel index arithmetic.
 // ---------------------------------------------------------------------------
 constexpr int kNmsRows = 64;  // >= window height (hCell <= 58, orb_pipeline.hip plan checks)
 
@@ -424,10 +530,10 @@ __global__ __launch_bounds__(64) void orb_cell_nms_kernel(const OrbCellDev* __re
     const OrbCellDev c = cells[blockIdx.x];
     const int f = blockIdx.y;
     const OrbLevelDev& L = lvs[c.level];
-    const int ww = c.x1 - c.x0, wh = c.y1 - c.y0, w = L.w;
+    const int ww = c.x1 - c.x0, wh = c.y1 - c.y0, w = L.bpitch;
     const int lane = threadIdx.x;
     const bool incol = lane < ww;
-    const size_t base = L.off + (size_t)f * L.plane + (size_t)c.y0 * w + c.x0 + lane;
+    const size_t base = L.boff + (size_t)f * L.bplane + (size_t)c.y0 * w + c.x0 + lane;
     const uint8_t* S = score + base;
     // stage the window column-per-lane (rows beyond wh and lanes beyond ww hold 0)
     for (int r0 = 0; r0 < wh; r0 += 8) {
@@ -499,7 +605,7 @@ __global__ __launch_bounds__(64) void orb_sat_strip_kernel(const OrbLevelDev* __
     const int lane = threadIdx.x, x = 64 * s + lane, pitch = 64 * nS;
     unsigned short* base = lsat + L.satOff + (size_t)f * L.satPlane;
     int* T = carry + L.carryOff + (size_t)f * L.carryPlane;
-    const uint8_t* C0 = cand + L.off + (size_t)f * L.plane + (size_t)L.minB * L.w + L.minB;
+    const uint8_t* C0 = cand + L.boff + (size_t)f * L.bplane + (size_t)L.minB * L.bpitch + L.minB;
     base[x] = 0;
     if (lane == 0) T[s + 1] = 0;
     int colacc = 0, tot = 0;
@@ -508,7 +614,7 @@ __global__ __launch_bounds__(64) void orb_sat_strip_kernel(const OrbLevelDev* __
 #pragma unroll
         for (int k = 0; k < kSatRowsPerWave; ++k) {
             const int y = y0 + k;  // SAT row y counts image row y-1 of the region
-            v[k] = (y <= L.rh && x < L.rw) ? (C0[(size_t)(y - 1) * L.w + x] != 0) : 0;
+            v[k] = (y <= L.rh && x < L.rw) ? (C0[(size_t)(y - 1) * L.bpitch + x] != 0) : 0;
         }
 #pragma unroll
         for (int k = 0; k < kSatRowsPerWave; ++k) {
@@ -614,7 +720,7 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
     };
     // children counts of nodes ids[0..k): lanes in parallel, 16 SAT loads each in flight
     auto prefetch = [&](const short* ids, int k) {
-        __syncthreads();
+        wave_sync();  // one wave per block
         for (int i = lane; i < k; i += 64) {
             const int p = ids[i];
             const int x0 = n.gx0[p], y0 = n.gy0[p], x1 = n.gx1[p], y1 = n.gy1[p];
@@ -638,7 +744,7 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
                                         : v[ya + 1][xa + 1] - v[ya][xa + 1] - v[ya + 1][xa] + v[ya][xa];
             }
         }
-        __syncthreads();
+        wave_sync();
     };
     const int N = lv.quota;
     int nfree = 0;
@@ -788,7 +894,7 @@ __global__ __launch_bounds__(64) void orb_node_best_kernel(const OrbLevelDev* __
     if (node >= ncnt) return;
     const OrbLevelDev& lv = lvs[l];
     const short4 r = rects[((size_t)f * L + l) * nodeCapMax + node];
-    const uint8_t* Cm = cand + lv.off + (size_t)f * lv.plane;
+    const uint8_t* Cm = cand + lv.boff + (size_t)f * lv.bplane;
     const int lane = threadIdx.x;
     const int rx0 = r.x, ry0 = r.y, rx1 = r.z, ry1 = r.w;
     const int wdt = rx1 - rx0;
@@ -796,7 +902,7 @@ __global__ __launch_bounds__(64) void orb_node_best_kernel(const OrbLevelDev* __
     const int total = wdt * (ry1 - ry0);
     for (int i = lane; i < total; i += 64) {
         const int yy = ry0 + i / wdt, xx = rx0 + i % wdt;
-        const int resp = Cm[(size_t)(lv.minB + yy) * lv.w + lv.minB + xx];
+        const int resp = Cm[(size_t)(lv.minB + yy) * lv.bpitch + lv.minB + xx];
         if (!resp) continue;
         const unsigned ci = (unsigned)(yy - 3) / (unsigned)lv.hCell, cj = (unsigned)(xx - 3) / (unsigned)lv.wCell;
         const unsigned key = ((ci * (unsigned)lv.nCols + cj) * (unsigned)lv.rh + (unsigned)yy) * (unsigned)lv.rw + (unsigned)xx;
@@ -880,8 +986,8 @@ __global__ __launch_bounds__(256) void orb_describe_kernel(const OrbLevelDev* __
             lvkp[(size_t)f * kpCapFrame + slot] = kp;
         }
         // ---- rBRIEF (computeOrbDescriptor, ORBextractor.cc:106-145)
-        const uint8_t* Bc = blur + lv.off + (size_t)f * lv.plane + (size_t)(cy - kDescR) * W + (cx - kDescR);
-        stage_bytes<64>(P, kDescPitch, Bc, (size_t)W, kDescP, kDescP, lane);
+        const uint8_t* Bc = blur + lv.boff + (size_t)f * lv.bplane + (size_t)(cy - kDescR) * lv.bpitch + (cx - kDescR);
+        stage_bytes<64>(P, kDescPitch, Bc, (size_t)lv.bpitch, kDescP, kDescP, lane);
         const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
         const float ang = angle * factorPI;
         // ang in [0, 2*pi]: the branch-free glibc sincosf (exhaustively equal to

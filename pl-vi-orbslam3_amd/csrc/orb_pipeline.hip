@@ -53,7 +53,7 @@ struct OrbPipeline {
     int taps[7]{};
     int resizeGeneric = 0;  // A.1 vertical-pass switch (PLVI_COMPAT_RESIZE_V_GENERIC)
     int kpCapFrame = 0, nodeCapMax = 0;
-    size_t pyrBytesFrameTotal = 0, satIntsFrameTotal = 0;
+    size_t pyrBytesFrameTotal = 0, candBytesTotal = 0, satIntsFrameTotal = 0;
     size_t lvOff0 = 0;  // (unused)
     DevBuf d_lv, d_cells, d_strips, d_xtab, pyr, blur, score, cand, sat, carry, rects, rectCnt, lvkp, lvdesc, okp, odesc, ocount,
         omono, err, staging;
@@ -173,7 +173,7 @@ struct OrbPipeline {
         resizeGeneric = (p->compat & PLVI_COMPAT_RESIZE_V_GENERIC) ? 1 : 0;
         // Levels
         lv.resize(L);
-        size_t off = 0, satOff = 0, carryOff = 0;
+        size_t off = 0, boffAll = 0, satOff = 0, carryOff = 0;
         std::vector<uint32_t> xtab;
         int kpOff = 0;
         nodeCapMax = 0;
@@ -185,6 +185,10 @@ struct OrbPipeline {
             d.plane = (long long)d.w * d.h;
             d.off = (long long)off;
             off += (size_t)d.plane * Bcap;
+            d.bpitch = (d.w + kBfAlign - 1) / kBfAlign * kBfAlign;
+            d.bplane = (long long)d.bpitch * d.h;
+            d.boff = (long long)boffAll;
+            boffAll += (size_t)d.bplane * Bcap;
             d.minB = 16;
             const int maxBX = d.w - 16, maxBY = d.h - 16;
             d.rw = maxBX - d.minB;
@@ -253,14 +257,21 @@ struct OrbPipeline {
                 // LDS: a kPyrRing-row ring of level 0, two rows of every other source level
                 pyrSmem += (l == 1 ? kPyrRing : 2) * (size_t)((lv[l - 1].w + 3) & ~3);
             }
-            // column strips of the blur + FAST kernel (candidate queue packs rows in 10 bits)
-            if (d.h >= 1024) return PLVI_E_BADARG;
-            for (int y0 = 0; y0 < d.h; y0 += kStripRows)
-                for (int x0 = 0; x0 < d.w; x0 += kStripOut)
-                    strips.push_back(OrbStripDev{l, x0, y0, std::min(y0 + kStripRows, d.h)});
+            // strips of the blur + FAST kernel: columns split into kBfAlign-aligned
+            // strips of <= kBfCols, rows split evenly (<= kBfRows rows)
+            {
+                const int ncs = (d.w + kBfCols - 1) / kBfCols, nrs = (d.h + kBfRows - 1) / kBfRows;
+                const int cols = ((d.w + ncs - 1) / ncs + kBfAlign - 1) / kBfAlign * kBfAlign;
+                const int rows = (d.h + nrs - 1) / nrs;
+                if (cols > kBfCols) return PLVI_E_BADARG;
+                for (int y0 = 0; y0 < d.h; y0 += rows)
+                    for (int x0 = 0; x0 < d.w; x0 += cols)
+                        strips.push_back(OrbStripDev{l, x0, std::min(x0 + cols, d.w), y0, std::min(y0 + rows, d.h)});
+            }
         }
         kpCapFrame = kpOff;
         pyrBytesFrameTotal = off;
+        candBytesTotal = boffAll;
         satIntsFrameTotal = satOff;
         // device tables
         if (d_lv.alloc(sizeof(OrbLevelDev) * L) || d_cells.alloc(sizeof(OrbCellDev) * cells.size()) ||
@@ -278,7 +289,7 @@ struct OrbPipeline {
         PLVI_CHECK(hipMemcpy(d_xtab.p, xtab.data(), 4 * xtab.size(), hipMemcpyHostToDevice));
         PLVI_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax.data(), 16 * sizeof(int)));
         // work buffers
-        if (pyr.alloc(off) || blur.alloc(off) || score.alloc(off) || cand.alloc(off) ||
+        if (pyr.alloc(off) || blur.alloc(boffAll) || score.alloc(boffAll) || cand.alloc(boffAll) ||
             sat.alloc(satOff * sizeof(unsigned short)) || carry.alloc(carryOff * sizeof(int)) || rects.alloc(sizeof(short4) * (size_t)nodeCapMax * L * Bcap) ||
             rectCnt.alloc(sizeof(int) * L * Bcap) || lvkp.alloc(sizeof(float4) * (size_t)kpCapFrame * Bcap) ||
             lvdesc.alloc((size_t)32 * kpCapFrame * Bcap) || okp.alloc(sizeof(plvi_keypoint) * (size_t)kpCapFrame * Bcap) ||
@@ -311,16 +322,16 @@ struct OrbPipeline {
         // K1b: blur + FAST score of every level (level 0 also copies the frame into its plane)
         const bool kt = ktime && kn < kKRing;
         if (kt) PLVI_CHECK(hipEventRecord(kev[2 * kn], st));
-        hipLaunchKernelGGL(orb_blur_fast_kernel, dim3((unsigned)strips.size(), nf), dim3(64), 0, st,
+        hipLaunchKernelGGL(orb_blur_fast_kernel, dim3((unsigned)(strips.size() * 8 * ((nf + 7) / 8))), dim3(64), 0, st,
                            d_lv.as<OrbLevelDev>(), d_strips.as<OrbStripDev>(), d_frames, frame_stride, row_stride, P,
-                           Bl, Sc, taps[0], taps[1], taps[2], taps[3], tmin);
+                           Bl, Sc, taps[0], taps[1], taps[2], taps[3], tmin, (int)strips.size(), nf);
         if (kt) {
             PLVI_CHECK(hipEventRecord(kev[2 * kn + 1], st));
             ++kn;
         }
         mark(1, st);
         // K2 cell NMS -> candidate map (zeroed first: only detection windows are written)
-        PLVI_CHECK(hipMemsetAsync(Cd, 0, pyrBytesFrameTotal, st));
+        PLVI_CHECK(hipMemsetAsync(Cd, 0, candBytesTotal, st));
         hipLaunchKernelGGL(orb_cell_nms_kernel, dim3((unsigned)cells.size(), nf), dim3(64), 0, st,
                            d_cells.as<OrbCellDev>(), d_lv.as<OrbLevelDev>(), (const uint8_t*)Sc, Cd, t1, t2);
         mark(2, st);

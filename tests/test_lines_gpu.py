@@ -88,13 +88,19 @@ def test_lines_batch_equals_single(lx640):
         _assert_same((kl[s], de[s], fn[s]), ol.line_extract(frames[f]), f"batch{f}")
 
 
-@pytest.mark.parametrize("lds", [6144, 12288, 40960])
-def test_lines_grow_window_budgets(plvi_lib, monkeypatch, lds):
-    """PLVI_GROW_LDS picks the region-growing LDS window (R = 2 rows by
-    default, 4 / 8+ rows and the 1024-entry queue at the larger budgets):
-    every budget gives the oracle's lines, at 640 px (odd batch) and at the
-    752 px EuRoC width (BASELINE C4)."""
+@pytest.mark.parametrize("lds,rb,rd", [(6144, "64", None), (6144, "2", None), (6144, "8", "0"),
+                                       (12288, "64", "2"), (40960, "16", None), (40960, "1024", None)])
+def test_lines_grow_window_budgets(plvi_lib, monkeypatch, lds, rb, rd):
+    """PLVI_GROW_LDS / _RB / _RD pick the region-growing LDS windows (USED
+    bits ring of RB rows, angle ring of R rows or none, the 1024-entry queue
+    at the larger budgets): every choice gives the oracle's lines, at 640 px
+    (odd batch) and at the 752 px EuRoC width (BASELINE C4)."""
     monkeypatch.setenv("PLVI_GROW_LDS", str(lds))
+    monkeypatch.setenv("PLVI_GROW_RB", rb)
+    if rd is not None:
+        monkeypatch.setenv("PLVI_GROW_RD", rd)
+    else:
+        monkeypatch.delenv("PLVI_GROW_RD", raising=False)
     lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 640, 480, max_batch=3)
     frames = synth.batch(3, seed0=60)
     buf = plvi.DeviceBuffer(frames.nbytes)

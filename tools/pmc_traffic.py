@@ -1,41 +1,59 @@
-"""Per-launch HBM traffic of the roofline kernel from separate rocprofv3 --pmc
-passes of the bench command (tools/gpu_session.sh: pmc_FETCH_SIZE/,
-pmc_WRITE_SIZE/).  Writes profiles/<round>/pmc_traffic.json for bench.py.
-
-FETCH_SIZE / WRITE_SIZE are KiB per dispatch (TCC_EA0_RDREQ/WRREQ based).
-MI355X_MICROARCH.md: FETCH_SIZE counts 1/2 of the bytes of 16-B/lane
-streaming reads; this kernel reads 1 B per lane (byte loads), a width the
-guide leaves uncalibrated, so the raw value is reported, uncorrected, next
-to the x2 reading for comparison.
-
-usage: python tools/pmc_traffic.py gpurun_out profiles/r01 BATCH"""
+"""Per-launch HBM traffic of the roofline kernels from two separate
+rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over tools/pmc_frame.py,
+calibrated per MI355X_MICROARCH.md (HBM/rocprofv3): FETCH_SIZE reads 1/2 of
+the bytes of 16-B/lane streams and other widths are uncalibrated, so the
+calibration kernels (tools/calib/pmc_calib.hip) stream a known byte count
+with the widths the kernels use and give the bytes-per-counted-byte factor:
+  reads  of orb_blur_fast_kernel: dword loads  -> calib_dword_read
+  writes of orb_blur_fast_kernel: dword stores -> calib_dword_copy (writes)
+  reads  of lsd_prep_kernel:      dword loads  -> calib_dword_read
+  writes of lsd_prep_kernel:      4/8-B stores -> calib_dword_copy / calib_dwordx2_store (mean)
+Writes profiles/<round>/pmc_traffic.json (a list, one entry per kernel) for bench.py.
+usage: python tools/pmc_traffic.py <pmc_dir> profiles/r02 BATCH CAL_BYTES"""
 import csv
 import json
 import pathlib
 import sys
+from collections import defaultdict
 
-KERNEL = "orb_blur_fast_kernel"
 
-
-def per_dispatch(path, counter):
-    vals = []
+def per_kernel(path, counter):
+    """KiB values per dispatch (FETCH_SIZE / WRITE_SIZE are KiB) -> bytes, by kernel."""
+    out = defaultdict(list)
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] == counter and KERNEL in r["Kernel_Name"]:
-            vals.append(float(r["Counter_Value"]) * 1024.0)
-    return vals
+        if r["Counter_Name"] == counter:
+            name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("plvi::", "")
+            out[name].append(float(r["Counter_Value"]) * 1024.0)
+    return out
 
 
 def main():
-    out, dst, batch = pathlib.Path(sys.argv[1]), pathlib.Path(sys.argv[2]), int(sys.argv[3])
-    fe = per_dispatch(out / "pmc_FETCH_SIZE" / "run_counter_collection.csv", "FETCH_SIZE")
-    wr = per_dispatch(out / "pmc_WRITE_SIZE" / "run_counter_collection.csv", "WRITE_SIZE")
-    f, w = sum(fe) / len(fe), sum(wr) / len(wr)
-    d = {"kernel": KERNEL, "batch": batch, "dispatches": [len(fe), len(wr)], "fetch_bytes_raw": f,
-         "fetch_bytes_x2": 2 * f, "write_bytes": w, "bytes_per_launch": f + w,
-         "note": "FETCH_SIZE raw (byte-wide loads: the guide's x2 rule is for 16 B/lane reads) + WRITE_SIZE"}
+    d, dst, batch, cal_bytes = pathlib.Path(sys.argv[1]), pathlib.Path(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
+    fe = per_kernel(next(d.glob("pmc_FETCH_SIZE/**/*counter_collection.csv")), "FETCH_SIZE")
+    wr = per_kernel(next(d.glob("pmc_WRITE_SIZE/**/*counter_collection.csv")), "WRITE_SIZE")
+    mean = lambda v: sum(v) / len(v)  # noqa: E731
+    f_rd = cal_bytes / mean(fe["calib_dword_read"])
+    f_wr4 = cal_bytes / mean(wr["calib_dword_copy"])
+    f_wr8 = cal_bytes / mean(wr["calib_dwordx2_store"])
+    f_rd1 = cal_bytes / mean(fe["calib_byte_copy"])
+    f_wr1 = cal_bytes / mean(wr["calib_byte_copy"])
+    calib = {"read_dword": f_rd, "read_byte": f_rd1, "write_dword": f_wr4, "write_dwordx2": f_wr8, "write_byte": f_wr1,
+             "note": "true bytes per counted byte, from calibration kernels streaming %d B" % cal_bytes}
+    entries = []
+    for k, fr, fw in (("orb_blur_fast_kernel", f_rd, f_wr4), ("lsd_prep_kernel", f_rd, (f_wr4 + f_wr8) / 2)):
+        if k not in fe or k not in wr:
+            continue
+        if k == "lsd_prep_kernel":  # two launches per batch (octaves): per-batch sum of the first pair
+            rf, rw = fe[k][0] + fe[k][1], wr[k][0] + wr[k][1]
+        else:
+            rf, rw = mean(fe[k]), mean(wr[k])
+        entries.append({"kernel": k, "batch": batch, "dispatches": [len(fe[k]), len(wr[k])],
+                        "fetch_bytes_raw": rf, "write_bytes_raw": rw,
+                        "fetch_bytes": rf * fr, "write_bytes": rw * fw, "bytes_per_launch": rf * fr + rw * fw,
+                        "calibration": calib})
     dst.mkdir(parents=True, exist_ok=True)
-    (dst / "pmc_traffic.json").write_text(json.dumps(d, indent=1) + "\n")
-    print(json.dumps(d))
+    (dst / "pmc_traffic.json").write_text(json.dumps(entries, indent=1) + "\n")
+    print(json.dumps(entries, indent=1))
 
 
 if __name__ == "__main__":
