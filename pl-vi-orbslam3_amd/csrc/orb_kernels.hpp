@@ -933,14 +933,17 @@ __constant__ signed char c_pattern[1024] = {
 __constant__ int c_umax[16];
 
 // One wave per keypoint (4 waves per workgroup, grid-stride over the slots):
+//  * both neighbourhoods are staged in LDS with unaligned dword loads issued
+//    together (one memory round trip): the level image's 31x32 disc box for
+//    IC_Angle and the blurred level's 37x37 box for rBRIEF (rotated pattern
+//    offsets are within +-18);
 //  * IC_Angle moments: lanes 0..30 / 32..62 take the disc columns u=-15..15
-//    of rows v = 0..7 / 8..15, read straight from the level image (each row
-//    one coalesced 31-byte segment); integer sums, so any order is exact.
-//  * rBRIEF: the 37x37 neighbourhood of the blurred level (rotated pattern
-//    offsets are within +-18) is staged in LDS with row-coalesced loads;
-//    lane l evaluates tests l, l+64, l+128, l+192 and one ballot per 64
-//    tests yields 8 descriptor bytes directly (test j = byte j/8, bit j%8).
+//    of rows v = 0..7 / 8..15; integer sums, so any order is exact;
+//  * rBRIEF: the pattern is held in registers (loaded once per wave); lane l
+//    evaluates tests l, l+64, l+128, l+192 and one ballot per 64 tests yields
+//    8 descriptor bytes directly (test j = byte j/8, bit j%8).
 constexpr int kDescR = 18, kDescP = 2 * kDescR + 1, kDescPitch = 40;
+constexpr int kAngR = 15, kAngRows = 2 * kAngR + 1, kAngPitch = 32;
 
 __global__ __launch_bounds__(256) void orb_describe_kernel(const OrbLevelDev* __restrict__ lvs, int L,
                                                            const uint8_t* __restrict__ pyr,
@@ -948,11 +951,23 @@ __global__ __launch_bounds__(256) void orb_describe_kernel(const OrbLevelDev* __
                                                            const int* __restrict__ rect_cnt,
                                                            float4* __restrict__ lvkp, uint8_t* __restrict__ lvdesc,
                                                            int kpCapFrame) {
-    __shared__ uint8_t patch[4][kDescP * kDescPitch];
+    __shared__ __align__(16) uint8_t patch[4][kDescP * kDescPitch];
+    __shared__ __align__(16) uint8_t ipatch[4][kAngRows * kAngPitch];
     const int f = blockIdx.y;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint8_t* P = patch[wv];
+    uint8_t* IP = ipatch[wv];
     const int half = lane >> 5, u = (lane & 31) - 15;
+    // this lane's four tests: (x0, y0, x1, y1) of tests lane + 64k
+    float px0[4], py0[4], px1[4], py1[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int j = lane + 64 * k;
+        px0[k] = c_pattern[4 * j];
+        py0[k] = c_pattern[4 * j + 1];
+        px1[k] = c_pattern[4 * j + 2];
+        py1[k] = c_pattern[4 * j + 3];
+    }
     for (int slot = blockIdx.x * 4 + wv; slot < kpCapFrame; slot += gridDim.x * 4) {
         int l = 0;
         while (l + 1 < L && slot >= lvs[l + 1].kpOff) ++l;
@@ -960,17 +975,45 @@ __global__ __launch_bounds__(256) void orb_describe_kernel(const OrbLevelDev* __
         const int idx = slot - lv.kpOff;
         if (idx >= rect_cnt[(size_t)f * L + l]) continue;  // wave-uniform
         float4 kp = lvkp[(size_t)f * kpCapFrame + slot];
-        const int cx = (int)kp.x, cy = (int)kp.y;  // integer-valued level coords
-        const int W = lv.w;
+        const int cx = (int)kp.x, cy = (int)kp.y;  // integer-valued level coords (>= 19 from every border)
+        const int W = lv.w, BW = lv.bpitch;
+        // ---- stage both boxes: dword loads first, then LDS writes
+        const uint8_t* I0 = pyr + lv.off + (size_t)f * lv.plane + (size_t)(cy - kAngR) * W + (cx - kAngR);
+        const uint8_t* B0 = blur + lv.boff + (size_t)f * lv.bplane + (size_t)(cy - kDescR) * BW + (cx - kDescR);
+        uint32_t iv[4], bv[6];
+        uint8_t blast = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // 31 rows x 8 dwords (columns cx-15 .. cx+16)
+            const int i = lane + 64 * k;
+            iv[k] = i < kAngRows * 8 ? ld_u32(I0 + (size_t)(i >> 3) * W + 4 * (i & 7)) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {  // 37 rows x 9 dwords (columns cx-18 .. cx+17)
+            const int i = lane + 64 * k, r = i / 9;
+            bv[k] = i < kDescP * 9 ? ld_u32(B0 + (size_t)r * BW + 4 * (i - 9 * r)) : 0u;
+        }
+        if (lane < kDescP) blast = B0[(size_t)lane * BW + 36];  // column cx+18
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = lane + 64 * k;
+            if (i < kAngRows * 8) *reinterpret_cast<uint32_t*>(IP + (i >> 3) * kAngPitch + 4 * (i & 7)) = iv[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const int i = lane + 64 * k, r = i / 9;
+            if (i < kDescP * 9) *reinterpret_cast<uint32_t*>(P + r * kDescPitch + 4 * (i - 9 * r)) = bv[k];
+        }
+        if (lane < kDescP) P[lane * kDescPitch + 36] = blast;
+        wave_sync();
         // ---- IC_Angle (ORBextractor.cc:75-102)
-        const uint8_t* center = pyr + lv.off + (size_t)f * lv.plane + (size_t)cy * W + cx;
+        const uint8_t* center = IP + kAngR * kAngPitch + kAngR;
         int m_01 = 0, m_10 = 0;
         if (u <= 15) {
             if (half == 0) m_10 += u * center[u];
             for (int v = half ? 8 : 1; v <= (half ? 15 : 7); ++v) {
                 const int d = c_umax[v];
                 if (u >= -d && u <= d) {
-                    const int vp = center[u + v * W], vm = center[u - v * W];
+                    const int vp = center[u + v * kAngPitch], vm = center[u - v * kAngPitch];
                     m_01 += v * (vp - vm);
                     m_10 += u * (vp + vm);
                 }
@@ -986,8 +1029,6 @@ __global__ __launch_bounds__(256) void orb_describe_kernel(const OrbLevelDev* __
             lvkp[(size_t)f * kpCapFrame + slot] = kp;
         }
         // ---- rBRIEF (computeOrbDescriptor, ORBextractor.cc:106-145)
-        const uint8_t* Bc = blur + lv.boff + (size_t)f * lv.bplane + (size_t)(cy - kDescR) * lv.bpitch + (cx - kDescR);
-        stage_bytes<64>(P, kDescPitch, Bc, (size_t)lv.bpitch, kDescP, kDescP, lane);
         const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
         const float ang = angle * factorPI;
         // ang in [0, 2*pi]: the branch-free glibc sincosf (exhaustively equal to
@@ -995,20 +1036,17 @@ __global__ __launch_bounds__(256) void orb_describe_kernel(const OrbLevelDev* __
         // general form's large-argument reduction tripled the register count
         float a, b;
         plvi_sincosf_pos(ang, &b, &a);
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         uint64_t* out = reinterpret_cast<uint64_t*>(lvdesc + ((size_t)f * kpCapFrame + slot) * 32);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int j = lane + 64 * k;
-            const float x0 = c_pattern[4 * j], y0 = c_pattern[4 * j + 1];
-            const float x1 = c_pattern[4 * j + 2], y1 = c_pattern[4 * j + 3];
-            const int t0 = P[(cv_round_f(x0 * b + y0 * a) + kDescR) * kDescPitch + cv_round_f(x0 * a - y0 * b) + kDescR];
-            const int t1 = P[(cv_round_f(x1 * b + y1 * a) + kDescR) * kDescPitch + cv_round_f(x1 * a - y1 * b) + kDescR];
+            const int t0 = P[(cv_round_f(px0[k] * b + py0[k] * a) + kDescR) * kDescPitch +
+                             cv_round_f(px0[k] * a - py0[k] * b) + kDescR];
+            const int t1 = P[(cv_round_f(px1[k] * b + py1[k] * a) + kDescR) * kDescPitch +
+                             cv_round_f(px1[k] * a - py1[k] * b) + kDescR];
             const unsigned long long m = __ballot(t0 < t1);
             if (lane == 0) out[k] = m;
         }
-        __builtin_amdgcn_wave_barrier();
+        wave_sync();  // the next slot's staging overwrites the boxes
     }
 }
 
