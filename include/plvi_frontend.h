@@ -59,7 +59,7 @@ enum {
 /* Per-frame device error flags of a batch (plvi_orb_errors / plvi_lines_errors). */
 enum {
   PLVI_FERR_OCTREE = 1,   /* ORB: an octree level exceeded its node table (level dropped) */
-  PLVI_FERR_LSD_TILE = 2, /* lines: LSD prep tile footprint exceeded its LDS tile */
+  PLVI_FERR_LSD_TILE = 2, /* lines: reserved (the streaming LSD prep has no tile to overflow) */
   PLVI_FERR_LSD_RAW = 4,  /* lines: more LSD regions than the raw line table holds */
   PLVI_FERR_KEYLINES = 8, /* lines: keyline table overflow (frame emitted with 0 lines) */
 };
@@ -224,6 +224,11 @@ int plvi_lines_profile(plvi_line_extractor* h, int enable);
  * per (frame, octave) 16 uint64 = [total, pop-prep, commit rounds, rect,
  * seeds, pops, commits, rect points, slow-path loads]; NULL disables. */
 int plvi_lines_debug_stats(plvi_line_extractor* h, unsigned long long* d_stats);
+/* Diagnostic: LSD planes of the last batch for one (frame, octave), copied to
+ * host: angle in degrees (float, NOTDEF = -1024), modgrad (f64), cos/sin
+ * pairs (float2, defined pixels only); any pointer may be NULL. */
+int plvi_lines_debug_planes(plvi_line_extractor* h, int frame, int octave, float* deg, double* modgrad, float* cs,
+                            int* sw, int* sh);
 int plvi_lines_profile_read(plvi_line_extractor* h, float* stage_ms, int* runs);
 /* Per-launch timing of lsd_prep_kernel (bench.py's LSD-pass roofline), one
  * launch per octave: as plvi_orb_kernel_timing / _read. */

@@ -23,6 +23,9 @@ struct LineOctDev {
     // resize x0.8 tables (offsets in the table buffer)
     long long tabXofs, tabXa, tabYrow, tabYb;
     int xmax;
+    // lsd_prep2_kernel column strips (int4 {X0, X1, gx0, nc}, offset in the table buffer)
+    long long tabStrips;
+    int nstrips;
     // Sobel/LBD pyramid (computeGaussianPyramid): dims and offsets
     int lw, lh;
     long long loff, lplane;

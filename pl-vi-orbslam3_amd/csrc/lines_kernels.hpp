@@ -38,116 +38,164 @@ __global__ __launch_bounds__(256) void lsd_half_kernel(const uint8_t* __restrict
 }
 
 // ---------------------------------------------------------------------------
-// LK2: LSD preparation, fused per 32x16 tile of the scaled image:
-//   u8 -> f64, GaussianBlur(7x7, sigma=0.6/SCALE) f64 reflect-101
-//   (RowFilter sequential sum, SymmColumnFilter; lsd.cpp:455),
-//   resize x SCALE f64 INTER_LINEAR with float coefficients (lsd.cpp:457),
-//   ll_angle gradient / norm / fastAtan2 angle (lsd.cpp:561-584).
-// Outputs per scaled pixel: angle in degrees (float, NOTDEF = -1024), modgrad
-// (f64) and, for defined pixels, cos/sin(float(angle)) (float2).
+// LK2: LSD preparation (lsd.cpp:412-584): u8 -> f64, GaussianBlur(7x7,
+// sigma = 0.6/SCALE) f64 reflect-101 (RowFilter sequential sum,
+// SymmColumnFilter; lsd.cpp:455), resize x SCALE f64 INTER_LINEAR with
+// float coefficients (lsd.cpp:457), ll_angle gradient / norm / fastAtan2
+// (lsd.cpp:561-584); outputs per scaled pixel the angle in degrees (float,
+// NOTDEF = -1024), modgrad (f64) and, for defined pixels,
+// cos/sin(float(angle)) (float2).  One wave per column strip of the
+// scaled image, rows streamed top to bottom: lane l holds blurred-image
+// column gx0 - 3 + l.  Per source row the 7 horizontal taps come from the
+// neighbouring lanes (DPP wave shifts of the byte), the 7 vertical taps from
+// a register window of 7 row sums; each G row that completes a scaled row
+// (yrow[2dy+1] == g) is interpolated at the lane holding xofs[dx], gathered
+// to compact lane dx - X0 (bpermute) and, with the previous scaled row,
+// turned into the gradient / angle / cos-sin of scaled row dy - 1.  Rows are
+// prefetched 7 ahead; nothing but the wave's own registers is re-read.
+// Strip table (host, LinePipeline::init): output columns [X0, X1), compact
+// columns computed nc = X1 - X0 (+1: the gradient's right neighbour), all
+// G columns needed within lanes 3..60.
 // ---------------------------------------------------------------------------
-constexpr int kPTX = 32, kPTY = 16;         // scaled tile
-constexpr int kPGW = 48, kPGH = 28;         // max blurred (G) region
-constexpr int kPIW = kPGW + 6, kPIH = kPGH + 6;
+__device__ __forceinline__ int readlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float readlane_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), l);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double shfl_d(double v, int src) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __shfl((int)(b & 0xffffffff), src);
+    const int hi = __shfl((int)(b >> 32), src);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
 
-__global__ __launch_bounds__(256) void lsd_prep_kernel(const uint8_t* __restrict__ src, size_t s_frame, size_t s_row,
-                                                       int gw, int gh, int sw, int sh, const int* __restrict__ xofs,
-                                                       const float* __restrict__ xa, int xmax,
-                                                       const int* __restrict__ yrow, const float* __restrict__ yb,
-                                                       double k0, double k1, double k2, double k3, double rho,
-                                                       float* __restrict__ pix, double* __restrict__ modgrad,
-                                                       float2* __restrict__ pixcs, size_t p_frame,
-                                                       int* __restrict__ err) {
-    __shared__ uint8_t I[kPIH][kPIW];
-    __shared__ double Hs[kPIH][kPGW];
-    __shared__ double Gs[kPGH][kPGW];
-    __shared__ double Ss[kPTY + 1][kPTX + 1];
-    const int f = blockIdx.z;
-    const int X0 = blockIdx.x * kPTX, Y0 = blockIdx.y * kPTY;
-    const int Xe = min(X0 + kPTX, sw - 1), Ye = min(Y0 + kPTY, sh - 1);  // inclusive (+1 for the gradient)
-    const int gx0 = xofs[X0], gx1 = min(xofs[Xe] + 1, gw - 1);
-    const int gy0 = yrow[2 * Y0], gy1 = yrow[2 * Ye + 1];
-    const int GW = gx1 - gx0 + 1, GH = gy1 - gy0 + 1;
-    if (GW > kPGW || GH > kPGH) {
-        if (threadIdx.x == 0) atomicOr(err + f, 2);
-        return;
-    }
-    const uint8_t* S = src + (size_t)f * s_frame;
-    const int IW = GW + 6, IH = GH + 6;
-    // 2-D thread mapping (no runtime divisions): lane = column (IW <= 54, GW <= 48),
-    // the 4 waves take every 4th row
-    const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
-    if (cx < IW) {
-        const int sx = reflect101(gx0 - 3 + cx, gw);
-        for (int r = ry; r < IH; r += 4) I[r][cx] = S[(size_t)reflect101(gy0 - 3 + r, gh) * s_row + sx];
-    }
-    __syncthreads();
-    const double kk[7] = {k0, k1, k2, k3, k2, k1, k0};
-    if (cx < GW) {
-        for (int r = ry; r < IH; r += 4) {
-            double s = kk[0] * (double)I[r][cx];
+__device__ __forceinline__ int dpp_from_right(int v) {  // lane i <- lane i+1 (wave_shl:1), edge lane 0
+    return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int dpp_from_left(int v) {  // lane i <- lane i-1 (wave_shr:1), edge lane 0
+    return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ double dpp_from_right_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = dpp_from_right((int)(b & 0xffffffff)), hi = dpp_from_right((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__global__ __launch_bounds__(64) void lsd_prep_kernel(const uint8_t* __restrict__ src, size_t s_frame, size_t s_row,
+                                                       int gw, int gh, int sw, int sh, const int4* __restrict__ strips,
+                                                       const int* __restrict__ xofs, const float* __restrict__ xa,
+                                                       int xmax, const int* __restrict__ yrow,
+                                                       const float* __restrict__ yb, double k0, double k1, double k2,
+                                                       double k3, double rho, float* __restrict__ pix,
+                                                       double* __restrict__ modgrad, float2* __restrict__ pixcs,
+                                                       size_t p_frame) {
+    __shared__ int hostdx[64];
+    const int4 sd = strips[blockIdx.x];
+    const int f = blockIdx.y;
+    const int X0 = sd.x, X1 = sd.y, gx0 = sd.z, nc = sd.w;
+    const int lane = threadIdx.x;
+    // compact lane t = lane takes scaled column X0 + t from lane Lt (the one
+    // holding G column xofs[X0 + t]); which scaled column a lane hosts
+    const int Lt = xofs[X0 + min(lane, nc - 1)] - gx0 + 3;
+    hostdx[lane] = -1;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if (lane < nc) hostdx[Lt] = X0 + lane;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const int hdx = hostdx[lane];
+    const bool interp = hdx >= 0 && hdx < xmax;
+    const double a0 = interp ? (double)xa[2 * hdx] : 1.0, a1 = interp ? (double)xa[2 * hdx + 1] : 0.0;
+    const uint8_t* S = src + (size_t)f * s_frame + reflect101(gx0 - 3 + lane, gw);
+    const int nout = X1 - X0;
+    float* P = pix + (size_t)f * p_frame + X0;
+    double* M = modgrad + (size_t)f * p_frame + X0;
+    float2* CS = pixcs + (size_t)f * p_frame + X0;
+    const int yend = gh + 3;  // source rows -3 .. gh+2 (reflect-101)
+    uint32_t pb[7];
 #pragma unroll
-            for (int k = 1; k < 7; ++k) s += kk[k] * (double)I[r][cx + k];
-            Hs[r][cx] = s;
-        }
-    }
-    __syncthreads();
-    if (cx < GW) {
-        for (int r = ry; r < GH; r += 4) {
-            double s = k3 * Hs[r + 3][cx] + 0.0;
-            s += k2 * (Hs[r + 4][cx] + Hs[r + 2][cx]);
-            s += k1 * (Hs[r + 5][cx] + Hs[r + 1][cx]);
-            s += k0 * (Hs[r + 6][cx] + Hs[r][cx]);
-            Gs[r][cx] = s;
-        }
-    }
-    __syncthreads();
-    const int TW = Xe - X0 + 1, TH = Ye - Y0 + 1;
-    for (int i = threadIdx.x; i < (kPTX + 1) * (kPTY + 1); i += 256) {
-        const int ty = i / (kPTX + 1), tx = i % (kPTX + 1);  // constant divisor (TW <= 33, TH <= 17)
-        if (tx >= TW || ty >= TH) continue;
-        const int dx = X0 + tx, dy = Y0 + ty;
-        const int r0 = yrow[2 * dy] - gy0, r1 = yrow[2 * dy + 1] - gy0;
-        const double b0 = (double)yb[2 * dy], b1 = (double)yb[2 * dy + 1];
-        const int sx = xofs[dx] - gx0;
-        double H0, H1;
-        if (dx < xmax) {
-            const double a0 = (double)xa[2 * dx], a1 = (double)xa[2 * dx + 1];
-            H0 = Gs[r0][sx] * a0 + Gs[r0][sx + 1] * a1;
-            H1 = Gs[r1][sx] * a0 + Gs[r1][sx + 1] * a1;
-        } else {
-            H0 = Gs[r0][sx] * 1.0;
-            H1 = Gs[r1][sx] * 1.0;
-        }
-        Ss[ty][tx] = H0 * b0 + H1 * b1;
-    }
-    __syncthreads();
-    float* P = pix + (size_t)f * p_frame;
-    double* M = modgrad + (size_t)f * p_frame;
-    for (int i = threadIdx.x; i < kPTX * kPTY; i += 256) {
-        const int ty = i / kPTX, tx = i % kPTX;
-        const int x = X0 + tx, y = Y0 + ty;
-        if (x >= sw || y >= sh) continue;
+    for (int k = 0; k < 7; ++k) pb[k] = S[(size_t)reflect101(k - 3, gh) * s_row];
+    double Hw[7];
+    double Gprev = 0.0, Gprevn = 0.0, Sp = 0.0, Spn = 0.0;
+    int dy = 0;
+    // gradient / angle / cos-sin of scaled row y from rows y (Sp, Spn) and y + 1 (Sc, Scn)
+    auto emit = [&](int y, double Sc, double Scn) {
+        if (lane >= nout) return;
+        const int x = X0 + lane;
         float deg = kNotdefF;
         double norm = 0.0;
         if (x < sw - 1 && y < sh - 1) {
-            const double DA = Ss[ty + 1][tx + 1] - Ss[ty][tx];
-            const double BC = Ss[ty][tx + 1] - Ss[ty + 1][tx];
+            const double DA = Scn - Sp;
+            const double BC = Spn - Sc;
             const double gx = DA + BC, gy = DA - BC;
             norm = __builtin_sqrt((gx * gx + gy * gy) / 4);
             if (!(norm <= rho)) deg = plvi_fast_atan2((float)gx, (float)-gy);
         }
-        P[(size_t)y * sw + x] = deg;
-        M[(size_t)y * sw + x] = norm;
+        const size_t o = (size_t)y * sw + lane;
+        P[o] = deg;
+        M[o] = norm;
         if (deg != kNotdefF) {
-            // the per-pixel cos/sin(float(angle)) of region_grow's sums (lsd.cpp:678-679);
-            // the seed direction (double cos/sin, :648-649) is computed by the
-            // region-growing kernel for the few pixels that become seeds
             float ps, pc;
             plvi_sincosf_pos((float)((double)deg * kD2R), &ps, &pc);
-            pixcs[(size_t)f * p_frame + (size_t)y * sw + x] = make_float2(pc, ps);
+            CS[o] = make_float2(pc, ps);
+        }
+    };
+    for (int ybase = -3; ybase < yend; ybase += 7) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+            const int y = ybase + k;
+            if (y >= yend) break;
+            const int v0 = (int)pb[k];
+            if (y + 7 < yend) pb[k] = S[(size_t)reflect101(y + 7, gh) * s_row];
+            // RowFilter: sequential sum over columns c-3 .. c+3
+            const int r1 = dpp_from_right(v0), r2 = dpp_from_right(r1), r3 = dpp_from_right(r2);
+            const int l1 = dpp_from_left(v0), l2 = dpp_from_left(l1), l3 = dpp_from_left(l2);
+            double s = k0 * (double)l3;
+            s += k1 * (double)l2;
+            s += k2 * (double)l1;
+            s += k3 * (double)v0;
+            s += k2 * (double)r1;
+            s += k1 * (double)r2;
+            s += k0 * (double)r3;
+            Hw[k] = s;  // slot k = source row ybase + k (ybase = -3 mod 7)
+            const int g = y - 3;
+            if (g < 0) continue;
+            // SymmColumnFilter over rows g-3 .. g+3 (slots k+1 .. k+7 mod 7)
+            double G = k3 * Hw[(k + 4) % 7] + 0.0;
+            G += k2 * (Hw[(k + 5) % 7] + Hw[(k + 3) % 7]);
+            G += k1 * (Hw[(k + 6) % 7] + Hw[(k + 2) % 7]);
+            G += k0 * (Hw[k] + Hw[(k + 1) % 7]);
+            const double Gn = dpp_from_right_d(G);
+            while (dy < sh && yrow[2 * dy + 1] == g) {
+                const bool same = yrow[2 * dy] == g;  // else g - 1
+                const double G0 = same ? G : Gprev, G0n = same ? Gn : Gprevn;
+                const double b0 = (double)yb[2 * dy], b1 = (double)yb[2 * dy + 1];
+                double H0, H1;
+                if (interp) {
+                    H0 = G0 * a0 + G0n * a1;
+                    H1 = G * a0 + Gn * a1;
+                } else {
+                    H0 = G0 * 1.0;
+                    H1 = G * 1.0;
+                }
+                const double Sv = H0 * b0 + H1 * b1;
+                const double Sc = shfl_d(Sv, Lt);
+                const double Scn = dpp_from_right_d(Sc);
+                if (dy > 0) emit(dy - 1, Sc, Scn);
+                Sp = Sc;
+                Spn = Scn;
+                ++dy;
+            }
+            Gprev = G;
+            Gprevn = Gn;
         }
     }
+    emit(sh - 1, 0.0, 0.0);  // last row: NOTDEF (ll_angle leaves row h-1 undefined)
 }
 
 // ---------------------------------------------------------------------------
@@ -267,23 +315,6 @@ __device__ __forceinline__ double angle_diff(double a, double b) {
     while (diff <= -kPi) diff += (2 * kPi);
     while (diff > kPi) diff -= (2 * kPi);
     return diff < 0 ? -diff : diff;
-}
-
-__device__ __forceinline__ int readlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
-__device__ __forceinline__ float readlane_f(float v, int l) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-__device__ __forceinline__ double readlane_d(double v, int l) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), l);
-    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ double shfl_d(double v, int src) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __shfl((int)(b & 0xffffffff), src);
-    const int hi = __shfl((int)(b >> 32), src);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
 // Load image rows [r0, r1) into their angle-window slots.

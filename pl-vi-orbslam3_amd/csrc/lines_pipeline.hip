@@ -156,6 +156,9 @@ struct LinePipeline {
         const unsigned hk = (unsigned)std::ceil(sigma * std::sqrt(2 * 3.0 * std::log(10.0)));
         if (SCALE != 1 && 1 + 2 * hk != 7) return PLVI_E_BADARG;  // tile kernel is specialised to 7 taps
         gauss_kernel_f64(7, sigma, gk, (p->compat & PLVI_COMPAT_EXP_CV_TABLE) != 0);
+        // SCALE == 1: flsd uses the image as is (lsd.cpp:460-463); identity
+        // taps keep every f64 sum exact (0 * I adds +0)
+        if (SCALE == 1) gk[0] = gk[1] = gk[2] = 0.0, gk[3] = 1.0;
         // LBD 5x5 sigma 1 fixed-point taps (A.4): error-diffused or rounded
         lbdTaps[0] = 14;
         lbdTaps[1] = (p->compat & PLVI_COMPAT_GAUSS_ROUNDED) ? 63 : 62;
@@ -227,6 +230,26 @@ struct LinePipeline {
                     yb[2 * dy + 1] = fy;
                 }
                 d.xmax = xmax;
+                // streaming prep strips: scaled columns [X0, X1) plus the
+                // gradient's right neighbour, every G column they read
+                // (xofs, xofs + 1 where interpolated) on lanes 3..60
+                std::vector<int> strips;
+                for (int X0 = 0; X0 < d.sw;) {
+                    const int gx0 = xofs[X0];
+                    int E = X0;
+                    while (E < d.sw && xofs[E] + (E < xmax ? 1 : 0) - gx0 + 3 <= 60) ++E;
+                    const int X1 = E == d.sw ? E : E - 1;
+                    if (X1 <= X0) return PLVI_E_BADARG;
+                    strips.insert(strips.end(), {X0, X1, gx0, E - X0});
+                    X0 = X1;
+                }
+                // each G row completes scaled rows whose two source rows are g - 1 or g
+                for (int dy = 0; dy < d.sh; ++dy) {
+                    const int r1 = yrow[2 * dy + 1], r0 = yrow[2 * dy];
+                    if (r0 > r1 || r1 - r0 > 1 || (dy > 0 && r1 < yrow[2 * dy - 1])) return PLVI_E_BADARG;
+                }
+                d.nstrips = (int)strips.size() / 4;
+                d.tabStrips = put(strips.data(), strips.size() * 4);
                 d.tabXofs = put(xofs.data(), xofs.size() * 4);
                 d.tabXa = put(xa.data(), xa.size() * 4);
                 d.tabYrow = put(yrow.data(), yrow.size() * 4);
@@ -352,14 +375,14 @@ struct LinePipeline {
             const uint8_t* s = l == 0 ? d_frames : octImg.as<uint8_t>() + d.off;
             const size_t sf = l == 0 ? frame_stride : (size_t)d.plane;
             const size_t sr = l == 0 ? row_stride : (size_t)d.w;
-            dim3 grid((d.sw + kPTX - 1) / kPTX, (d.sh + kPTY - 1) / kPTY, nf);
             const bool kt = ktime && kn < kKRing;
             if (kt) (void)hipEventRecord(kev[2 * kn], st);
-            hipLaunchKernelGGL(lsd_prep_kernel, grid, dim3(256), 0, st, s, sf, sr, d.w, d.h, d.sw, d.sh,
-                               (const int*)(T + d.tabXofs), (const float*)(T + d.tabXa), d.xmax,
-                               (const int*)(T + d.tabYrow), (const float*)(T + d.tabYb), gk[0], gk[1], gk[2], gk[3],
-                               rho, pix.as<float>() + d.soff, modg.as<double>() + d.soff,
-                               seedcs.as<float2>() + d.soff, (size_t)d.splane, err.as<int>());
+            hipLaunchKernelGGL(lsd_prep_kernel, dim3(d.nstrips, nf), dim3(64), 0, st, s, sf, sr, d.w, d.h, d.sw,
+                               d.sh, (const int4*)(T + d.tabStrips), (const int*)(T + d.tabXofs),
+                               (const float*)(T + d.tabXa), d.xmax, (const int*)(T + d.tabYrow),
+                               (const float*)(T + d.tabYb), gk[0], gk[1], gk[2], gk[3], rho,
+                               pix.as<float>() + d.soff, modg.as<double>() + d.soff, seedcs.as<float2>() + d.soff,
+                               (size_t)d.splane);
             if (kt) {
                 (void)hipEventRecord(kev[2 * kn + 1], st);
                 ++kn;
@@ -622,6 +645,25 @@ extern "C" int plvi_lines_profile_read(plvi_line_extractor* h, float* stage_ms, 
 extern "C" int plvi_lines_debug_stats(plvi_line_extractor* h, unsigned long long* d_stats) {
     if (!h) return PLVI_E_BADARG;
     h->p().growStats = d_stats;
+    return PLVI_OK;
+}
+
+// Diagnostic: the LSD planes of the last batch for one (frame, octave):
+// angle in degrees (float, NOTDEF = -1024), modgrad (f64) and the per-pixel
+// cos/sin pairs (valid where the angle is defined), copied to host memory.
+extern "C" int plvi_lines_debug_planes(plvi_line_extractor* h, int frame, int octave, float* deg, double* modgrad,
+                                       float* cs, int* sw, int* sh) {
+    if (!h || octave < 0 || octave >= h->p().nOct || frame < 0 || frame >= h->p().Bcap) return PLVI_E_BADARG;
+    LinePipeline& P = h->p();
+    PLVI_CHECK(hipSetDevice(P.device));
+    const plvi::LineOctDev& d = P.oct[octave];
+    const size_t n = (size_t)d.splane, o = (size_t)d.soff + (size_t)frame * n;
+    if (sw) *sw = d.sw;
+    if (sh) *sh = d.sh;
+    PLVI_CHECK(hipDeviceSynchronize());
+    if (deg) PLVI_CHECK(hipMemcpy(deg, P.pix.as<float>() + o, n * sizeof(float), hipMemcpyDeviceToHost));
+    if (modgrad) PLVI_CHECK(hipMemcpy(modgrad, P.modg.as<double>() + o, n * sizeof(double), hipMemcpyDeviceToHost));
+    if (cs) PLVI_CHECK(hipMemcpy(cs, P.seedcs.as<float2>() + o, n * sizeof(float2), hipMemcpyDeviceToHost));
     return PLVI_OK;
 }
 

@@ -184,6 +184,7 @@ def _declare(lib):
         "plvi_lines_profile": ([V, I], I),
         "plvi_lines_profile_read": ([V, V, P], I),
         "plvi_lines_debug_stats": ([V, V], I),
+        "plvi_lines_debug_planes": ([V, I, I, V, V, V, P, P], I),
         "plvi_descriptor_distance_batch": ([V, V, I, I, V, V], I),
         "plvi_search_by_bow": ([F, I, V, V, V, I, V, V, I, V, V, V, I, V, V, I, V, V], I),
         "plvi_search_by_bow_batch": ([I, F, I, I, I, I, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V], I),
@@ -539,6 +540,18 @@ class Lineextractor:
         _check(self._lib.plvi_lines_pyramid_level(self._h, frame, level, _ptr(out), None, None),
                "plvi_lines_pyramid_level")
         return out
+
+    def debug_planes(self, level, frame=0):
+        """(deg f32, modgrad f64, cos/sin f32 [h, w, 2]) LSD planes of the last batch (diagnostic)."""
+        w, h = ctypes.c_int(), ctypes.c_int()
+        _check(self._lib.plvi_lines_debug_planes(self._h, frame, level, None, None, None, ctypes.byref(w),
+                                                  ctypes.byref(h)), "plvi_lines_debug_planes")
+        deg = np.zeros((h.value, w.value), np.float32)
+        mg = np.zeros((h.value, w.value), np.float64)
+        cs = np.zeros((h.value, w.value, 2), np.float32)
+        _check(self._lib.plvi_lines_debug_planes(self._h, frame, level, _ptr(deg), _ptr(mg), _ptr(cs), None, None),
+               "plvi_lines_debug_planes")
+        return deg, mg, cs
 
     def scale_tables(self):
         out = [np.zeros(self.nlevels, np.float32) for _ in range(4)]

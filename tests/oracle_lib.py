@@ -238,6 +238,22 @@ def lsd_raw(img, lsd_scale=0.8, cap=20000):
     return out[:n.value].copy()
 
 
+def lsd_planes(img, lsd_scale=0.8):
+    """flsd's scaled image, angle (rad, NOTDEF -1024) and modgrad planes (f64)."""
+    lib = load()
+    V, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    lib.oracle_lsd_planes.argtypes = [V, I, I, F, V, V, V, ctypes.POINTER(I), ctypes.POINTER(I)]
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    n = (w + 2) * (h + 2)
+    bufs = [np.zeros(n, np.float64) for _ in range(3)]
+    sw, sh = ctypes.c_int(), ctypes.c_int()
+    rc = lib.oracle_lsd_planes(_p(img), w, h, lsd_scale, *[_p(b) for b in bufs], ctypes.byref(sw), ctypes.byref(sh))
+    assert rc == 0, rc
+    m = sw.value * sh.value
+    return tuple(b[:m].reshape(sh.value, sw.value).copy() for b in bufs)
+
+
 def line_iterator_count(W, H, x1, y1, x2, y2):
     lib = load()
     F, I = ctypes.c_float, ctypes.c_int
