@@ -229,6 +229,9 @@ int plvi_lines_debug_stats(plvi_line_extractor* h, unsigned long long* d_stats);
  * pairs (float2, defined pixels only); any pointer may be NULL. */
 int plvi_lines_debug_planes(plvi_line_extractor* h, int frame, int octave, float* deg, double* modgrad, float* cs,
                             int* sw, int* sh);
+/* Diagnostic: LBD Sobel plane of the last batch for one (frame, octave),
+ * interleaved int16 (dx, dy) per pixel, copied to host; dxdy may be NULL. */
+int plvi_lines_debug_sobel(plvi_line_extractor* h, int frame, int octave, short* dxdy, int* w, int* hgt);
 int plvi_lines_profile_read(plvi_line_extractor* h, float* stage_ms, int* runs);
 /* Per-launch timing of lsd_prep_kernel (bench.py's LSD-pass roofline), one
  * launch per octave: as plvi_orb_kernel_timing / _read. */

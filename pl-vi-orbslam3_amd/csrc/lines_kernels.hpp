@@ -408,6 +408,17 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
     constexpr bool do_stats = STATS;  // diagnostic variant only (keeps SGPRs free in the product kernel)
     const unsigned long long t_begin = do_stats ? __builtin_amdgcn_s_memtime() : 0;
     const int half = R / 2, halfb = RB / 2;
+    // Seed-chunk angles, prefetched one chunk ahead from the (static) angle
+    // plane: (x, y), (x-1, y), (x+1, y), (x-1, y+1), (x, y+1), (x+1, y+1)
+    auto chunk_load = [&](int cy, int cxb, float* v) {
+        const int x = cxb + lane, xm = max(x - 1, 0), xx = min(x, sw - 1), xp = min(x + 1, sw - 1);
+        const float* r0 = g.P + (size_t)cy * sw;
+        const float* r1 = r0 + sw;
+        v[0] = r0[xx]; v[1] = r0[xm]; v[2] = r0[xp];
+        v[3] = r1[xm]; v[4] = r1[xx]; v[5] = r1[xp];
+    };
+    float nv[6];
+    chunk_load(0, 0, nv);
     for (int y = 0; y < sh - 1; ++y) {
         // slide each window by half its height once row y is past its middle;
         // the rows leaving it are above y and never read again
@@ -430,24 +441,27 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
         }
         g.ys = y;
         for (int xb = 0; xb < sw - 1; xb += 64) {
+            float cv[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k) cv[k] = nv[k];
+            {
+                const int nxb = xb + 64 < sw - 1 ? xb + 64 : 0, ny = xb + 64 < sw - 1 ? y : y + 1;
+                if (ny < sh - 1) chunk_load(ny, nxb, nv);
+            }
             const int x = xb + lane;
             bool cand = false, grow = false;
             if (x < sw - 1) {
-                const float d0 = deg_at(g, x, y);
-                cand = !used_get(g, x, y) && d0 != kNotdefF;
+                const float d0 = cv[0];
+                cand = d0 != kNotdefF && !used_get(g, x, y);
                 // A seed's first round tests its forward neighbours (rows above y
                 // are all USED) against its own angle: when none of them is aligned
                 // (a static property, whatever is USED), the region stays at size 1
                 // < min_reg_size and the seed only marks itself USED.
-                if (cand) {
-                    // neighbours (x-1,y) (x+1,y) (x-1,y+1) (x,y+1) (x+1,y+1)
-#pragma unroll 1
-                    for (int k = 0; k < 5 && !grow; ++k) {
-                        const int nx = x + (k == 0 || k == 2 ? -1 : k == 3 ? 0 : 1), ny = y + (k >= 2);
-                        const float dn = nx >= 0 ? deg_at(g, nx, ny) : kNotdefF;
-                        grow = is_aligned_fast(dn, d0, pdeg, prec);
-                    }
-                }
+                // neighbours (x-1,y) (x+1,y) (x-1,y+1) (x,y+1) (x+1,y+1)
+                if (cand)
+                    grow = (x > 0 && is_aligned_fast(cv[1], d0, pdeg, prec)) || is_aligned_fast(cv[2], d0, pdeg, prec) ||
+                           (x > 0 && is_aligned_fast(cv[3], d0, pdeg, prec)) || is_aligned_fast(cv[4], d0, pdeg, prec) ||
+                           is_aligned_fast(cv[5], d0, pdeg, prec);
             }
             unsigned long long m = __ballot(cand);
             if (!m) continue;
@@ -492,7 +506,15 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                     const int px = (int)(pv & 0xffffu), py = (int)(pv >> 16);
                     const int nx = px + kdx, ny = py + kdy;
                     const bool valid = active && nx >= 0 && nx < sw && ny >= y && ny < sh;
-                    const float deg = valid ? deg_at(g, nx, ny) : kNotdefF;
+                    // angle and cos/sin(float(angle)) of lsd.cpp:678-679 (precomputed by
+                    // lsd_prep_kernel for defined pixels) in one round trip
+                    float deg = kNotdefF, cc = 0.f, ss = 0.f;
+                    if (valid) {
+                        const float2 cs2 = SC[(size_t)ny * sw + nx];
+                        deg = deg_at(g, nx, ny);
+                        cc = cs2.x;
+                        ss = cs2.y;
+                    }
                     // lanes of earlier block points that test the same pixel
                     unsigned long long dup = 0;
                     for (int p2 = 0; p2 < nb - 1; ++p2) {
@@ -500,15 +522,6 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                         const int ddx = nx - (int)(q2 & 0xffffu) + 1, ddy = ny - (int)(q2 >> 16) + 1;
                         if (p2 < bp && ddx >= 0 && ddx <= 2 && ddy >= 0 && ddy <= 2)
                             dup |= 1ull << (9 * p2 + ddy * 3 + ddx);
-                    }
-                    // cos/sin(float(angle)) of lsd.cpp:678-679
-                    float cc = 0.f, ss = 0.f;
-                    if (deg != kNotdefF) {
-                        // precomputed by lsd_prep_kernel (computing them here costs
-                        // more VALU issue than the load's latency)
-                        const float2 cs2 = SC[(size_t)ny * sw + nx];
-                        cc = cs2.x;
-                        ss = cs2.y;
                     }
                     unsigned long long t1 = 0;
                     if (do_stats) { t1 = __builtin_amdgcn_s_memtime(); s_setup += t1 - t0; n_block++; }
@@ -905,93 +918,228 @@ __global__ __launch_bounds__(256) void line_assemble_kernel(const LineOctDev* __
 // LB1: LBD octave 0 = GaussianBlur(5x5, 1) fixed point (taps t0,t1,t2,t1,t0 =
 // 14,62,104 error-diffused, or 14,63,103 rounded: PLVI_COMPAT_GAUSS_ROUNDED)
 // of the full frame (binary_descriptor_custom.cpp:359), Sobel dx/dy int16
-// (:396-397).  LB2: octave 1 = pyrDown(blurred) (:367) + Sobel.
-// 64x16 tiles; all borders reflect-101.
+// (:396-397).  LB2: octave 1 = pyrDown(blurred) (:367) + Sobel.  All
+// borders reflect-101.
 // ---------------------------------------------------------------------------
-constexpr int kBTW = 64, kBTH = 16;
+// LB1: one wave per column strip, lane
+// L holds columns x0 - 4 + 4L .. +3 as one dword (lane 0 and the lane after
+// the last output lane are halo), rows streamed top to bottom with 8 rows of
+// loads in flight.  Vertical 5-tap first on the even / odd bytes in 16-bit
+// fields (v_pk_mad_u16: fields never carry), horizontal 5-tap with
+// v_dot2_u32_u16 on the lane's and its neighbours' field pairs (DPP), one
+// rounding (exact integer sums, so the pass order is free).  Sobel from the
+// last three blurred rows (reflect-101 of the blurred image at the borders:
+// blurred row -1 = row 1, row h = row h - 2), again SWAR with the two
+// neighbour columns from the adjacent lanes.
+__device__ __forceinline__ uint32_t pk_madu16(uint32_t a, uint32_t b, uint32_t c) {  // per 16-bit field a*b+c
+    typedef unsigned short u16v2 __attribute__((ext_vector_type(2)));
+    const u16v2 r = __builtin_bit_cast(u16v2, a) * __builtin_bit_cast(u16v2, b) + __builtin_bit_cast(u16v2, c);
+    return __builtin_bit_cast(uint32_t, r);
+}
+__device__ __forceinline__ uint32_t lb_dot2(uint32_t a, uint32_t b, uint32_t c) {  // a.lo*b.lo + a.hi*b.hi + c
+    typedef unsigned short u16v2 __attribute__((ext_vector_type(2)));
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16v2, a), __builtin_bit_cast(u16v2, b), c, false);
+}
+__device__ __forceinline__ uint32_t lb_ld4(const uint8_t* p) {
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);
+    return v;
+}
+constexpr int kLbOutLanes = 62;  // output lanes per strip (4 columns each)
 
-__global__ __launch_bounds__(256) void lbd_blur_sobel_kernel(const uint8_t* __restrict__ src, size_t s_frame,
-                                                             size_t s_row, int w, int h, uint8_t* __restrict__ blur,
-                                                             short2* __restrict__ go, size_t d_frame, int t0,
-                                                             int t1, int t2) {
-    constexpr int EW = kBTW + 6, EH = kBTH + 6;  // input: halo 3 (2 blur + 1 sobel)
-    __shared__ uint8_t I[EH][EW];
-    __shared__ int Hs[EH][kBTW + 2];
-    __shared__ uint8_t Bv[kBTH + 2][kBTW + 2];
-    const int f = blockIdx.z;
-    const int X0 = blockIdx.x * kBTW, Y0 = blockIdx.y * kBTH;
+__global__ __launch_bounds__(64) void lbd_sobel0_kernel(const uint8_t* __restrict__ src, size_t s_frame, size_t s_row,
+                                                        int w, int h, int strip_w, uint8_t* __restrict__ blur,
+                                                        short2* __restrict__ go, size_t d_frame, int t0, int t1,
+                                                        int t2) {
+    const int f = blockIdx.y;
+    const int lane = threadIdx.x;
+    const int X0 = blockIdx.x * strip_w, X1 = min(X0 + strip_w, w);
+    const int c0 = X0 - 4 + 4 * lane;
+    const bool need = c0 < X1 + 4;                      // output lanes and the two halo lanes
+    const bool inner = need && c0 >= 0 && c0 + 4 <= w;  // a plain dword load
+    const bool outl = lane >= 1 && c0 < X1;
+    const int nout = min(4, X1 - c0);
     const uint8_t* S = src + (size_t)f * s_frame;
-    for (int i = threadIdx.x; i < EW * EH; i += 256) {
-        const int r = i / EW, c = i % EW;
-        I[r][c] = S[(size_t)reflect101(Y0 - 3 + r, h) * s_row + reflect101(X0 - 3 + c, w)];
+    uint8_t* Bp = blur + (size_t)f * d_frame;
+    short2* Gp = go + (size_t)f * d_frame;
+    auto load_row = [&](int r) -> uint32_t {
+        const uint8_t* rp = S + (size_t)reflect101(r, h) * s_row;
+        if (inner) return lb_ld4(rp + c0);
+        uint32_t v = 0;
+        if (need)
+            for (int j = 0; j < 4; ++j) v |= (uint32_t)rp[reflect101(c0 + j, w)] << (8 * j);
+        return v;
+    };
+    const uint32_t T0 = (uint32_t)t0 * 0x10001u, T1 = (uint32_t)t1 * 0x10001u, T2 = (uint32_t)t2 * 0x10001u;
+    auto pk = [](int lo, int hi) { return (uint32_t)lo | (uint32_t)hi << 16; };
+    // 5-row windows of even (c0, c0+2) / odd (c0+1, c0+3) bytes in 16-bit fields
+    uint32_t pe[5] = {0, 0, 0, 0, 0}, po[5] = {0, 0, 0, 0, 0};
+    uint32_t bm1 = 0, b0 = 0;  // blurred rows y-2, y-1 (4 bytes per lane)
+    auto sobel_row = [&](int y, uint32_t bu, uint32_t bc, uint32_t bd) {
+        // S(c) = up + 2 mid + down, D(c) = down - up, per 16-bit field (even / odd columns)
+        const uint32_t ue = bu & 0x00ff00ffu, uo = (bu >> 8) & 0x00ff00ffu;
+        const uint32_t me = bc & 0x00ff00ffu, mo = (bc >> 8) & 0x00ff00ffu;
+        const uint32_t de = bd & 0x00ff00ffu, dd = (bd >> 8) & 0x00ff00ffu;
+        const uint32_t Se = ue + 2 * me + de, So = uo + 2 * mo + dd;            // fields <= 1020
+        const uint32_t De = de + 0x00ff00ffu - ue, Do = dd + 0x00ff00ffu - uo;  // D + 255, fields <= 510
+        const uint32_t Sol = (uint32_t)dpp_from_left((int)So), Ser = (uint32_t)dpp_from_right((int)Se);
+        const uint32_t Dol = (uint32_t)dpp_from_left((int)Do), Der = (uint32_t)dpp_from_right((int)De);
+        const int gx0 = (int)(So & 0xffffu) - (int)(Sol >> 16), gx1 = (int)(Se >> 16) - (int)(Se & 0xffffu);
+        const int gx2 = (int)(So >> 16) - (int)(So & 0xffffu), gx3 = (int)(Ser & 0xffffu) - (int)(Se >> 16);
+        // gy(c) = D(c-1) + 2 D(c) + D(c+1) (offsets: 4 * 255)
+        const int gy0 = (int)(Dol >> 16) + 2 * (int)(De & 0xffffu) + (int)(Do & 0xffffu) - 1020;
+        const int gy1 = (int)(De & 0xffffu) + 2 * (int)(Do & 0xffffu) + (int)(De >> 16) - 1020;
+        const int gy2 = (int)(Do & 0xffffu) + 2 * (int)(De >> 16) + (int)(Do >> 16) - 1020;
+        const int gy3 = (int)(De >> 16) + 2 * (int)(Do >> 16) + (int)(Der & 0xffffu) - 1020;
+        if (!outl) return;
+        short2* o = Gp + (size_t)y * w + c0;
+        const short2 g4[4] = {make_short2((short)gx0, (short)gy0), make_short2((short)gx1, (short)gy1),
+                              make_short2((short)gx2, (short)gy2), make_short2((short)gx3, (short)gy3)};
+        if (nout == 4 && (w & 3) == 0) {
+            *reinterpret_cast<int4*>(o) = *reinterpret_cast<const int4*>(g4);
+        } else {
+            for (int j = 0; j < nout; ++j) o[j] = g4[j];
+        }
+    };
+    uint32_t pv[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) pv[k] = load_row(k - 2);
+    for (int rb = -2; rb < h + 2; rb += 8) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int r = rb + k;
+            if (r >= h + 2) break;
+            const uint32_t V = pv[k];
+            if (r + 8 < h + 2) pv[k] = load_row(r + 8);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                pe[q] = pe[q + 1];
+                po[q] = po[q + 1];
+            }
+            pe[4] = V & 0x00ff00ffu;
+            po[4] = (V >> 8) & 0x00ff00ffu;
+            const int y = r - 2;  // blurred row from rows y-2 .. y+2
+            if (y < 0) continue;
+            // vertical: E = (c0, c0+2), O = (c0+1, c0+3); fields <= 255 * 256
+            const uint32_t E = pk_madu16(T0, pe[0] + pe[4], pk_madu16(T1, pe[1] + pe[3], pk_madu16(T2, pe[2], 0u)));
+            const uint32_t O = pk_madu16(T0, po[0] + po[4], pk_madu16(T1, po[1] + po[3], pk_madu16(T2, po[2], 0u)));
+            const uint32_t El = (uint32_t)dpp_from_left((int)E), Ol = (uint32_t)dpp_from_left((int)O);
+            const uint32_t Er = (uint32_t)dpp_from_right((int)E), Or = (uint32_t)dpp_from_right((int)O);
+            // El = (c0-4, c0-2), Ol = (c0-3, c0-1), Er = (c0+4, c0+6), Or = (c0+5, c0+7)
+            const uint32_t h0 = lb_dot2(El, pk(0, t0), lb_dot2(Ol, pk(0, t1), lb_dot2(E, pk(t2, t0), lb_dot2(O, pk(t1, 0), 0u))));
+            const uint32_t h1 = lb_dot2(Ol, pk(0, t0), lb_dot2(E, pk(t1, t1), lb_dot2(O, pk(t2, t0), 0u)));
+            const uint32_t h2 = lb_dot2(E, pk(t0, t2), lb_dot2(O, pk(t1, t1), lb_dot2(Er, pk(t0, 0), 0u)));
+            const uint32_t h3 = lb_dot2(O, pk(t0, t2), lb_dot2(E, pk(0, t1), lb_dot2(Er, pk(t1, 0), lb_dot2(Or, pk(t0, 0), 0u))));
+            const uint32_t Bv = min((h0 + 32768u) >> 16, 255u) | min((h1 + 32768u) >> 16, 255u) << 8 |
+                                min((h2 + 32768u) >> 16, 255u) << 16 | min((h3 + 32768u) >> 16, 255u) << 24;
+            if (outl) {
+                uint8_t* o = Bp + (size_t)y * w + c0;
+                if (nout == 4 && (w & 3) == 0) {
+                    *reinterpret_cast<uint32_t*>(o) = Bv;
+                } else {
+                    for (int j = 0; j < nout; ++j) o[j] = (uint8_t)(Bv >> (8 * j));
+                }
+            }
+            // Sobel row y - 1 (needs blurred rows y-2 .. y; row -1 = row 1)
+            if (y == 1) sobel_row(0, Bv, b0, Bv);
+            else if (y >= 2) sobel_row(y - 1, bm1, b0, Bv);
+            bm1 = b0;
+            b0 = Bv;
+        }
     }
-    __syncthreads();
-    // horizontal 5-tap at virtual cols X0-1 .. X0+kBTW (kBTW+2), all EH rows
-    for (int i = threadIdx.x; i < EH * (kBTW + 2); i += 256) {
-        const int r = i / (kBTW + 2), c = i % (kBTW + 2);
-        const uint8_t* e = &I[r][c];
-        Hs[r][c] = t0 * (e[0] + e[4]) + t1 * (e[1] + e[3]) + t2 * e[2];
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < (kBTH + 2) * (kBTW + 2); i += 256) {
-        const int r = i / (kBTW + 2), c = i % (kBTW + 2);
-        const unsigned s = (unsigned)(t0 * (Hs[r][c] + Hs[r + 4][c]) + t1 * (Hs[r + 1][c] + Hs[r + 3][c]) +
-                                      t2 * Hs[r + 2][c]);
-        Bv[r][c] = (uint8_t)min((s + 32768u) >> 16, 255u);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kBTH * kBTW; i += 256) {
-        const int ty = i / kBTW, tx = i % kBTW;
-        const int x = X0 + tx, y = Y0 + ty;
-        if (x >= w || y >= h) continue;
-        const int r = ty + 1, c = tx + 1;
-        const int gx = (Bv[r - 1][c + 1] - Bv[r - 1][c - 1]) + 2 * (Bv[r][c + 1] - Bv[r][c - 1]) +
-                       (Bv[r + 1][c + 1] - Bv[r + 1][c - 1]);
-        const int gy = (Bv[r + 1][c - 1] - Bv[r - 1][c - 1]) + 2 * (Bv[r + 1][c] - Bv[r - 1][c]) +
-                       (Bv[r + 1][c + 1] - Bv[r - 1][c + 1]);
-        const size_t o = (size_t)f * d_frame + (size_t)y * w + x;
-        blur[o] = Bv[r][c];
-        go[o] = make_short2((short)gx, (short)gy);
-    }
+    if (h >= 2) sobel_row(h - 1, bm1, b0, bm1);  // row h = row h - 2
+    else sobel_row(0, b0, b0, b0);
 }
 
-__global__ __launch_bounds__(256) void lbd_pyrdown_sobel_kernel(const uint8_t* __restrict__ blur0, int w0, int h0,
-                                                                size_t s_frame, int w, int h,
-                                                                short2* __restrict__ go, size_t d_frame) {
-    __shared__ uint8_t P[kBTH + 2][kBTW + 2];
-    const int f = blockIdx.z;
-    const int X0 = blockIdx.x * kBTW, Y0 = blockIdx.y * kBTH;
+// LB2: pyrDown(blurred octave 0) + Sobel.
+// One wave per column strip of the output, lane L holds output columns
+// xa = X0 - 2 + 2L, xa + 1 and the four source columns 2xa .. 2xa + 3 (one
+// dword); source rows streamed, each pair of rows completes an output row.
+// 1-4-6-4-1 vertical sums in 16-bit fields (<= 4080), horizontal with the
+// left lane's two and the right lane's one column (DPP), (s + 128) >> 8.
+// Sobel on the output with reflect-101 of the OUTPUT grid (P(-1) = P(1),
+// P(w) = P(w - 2): the 2:1 grid is not symmetric about the far edge).
+constexpr int kLb2OutLanes = 62;  // output lanes per strip (2 columns each)
+
+__global__ __launch_bounds__(64) void lbd_sobel1_kernel(const uint8_t* __restrict__ blur0, int w0, int h0,
+                                                        size_t s_frame, int w, int h, int strip_w,
+                                                        short2* __restrict__ go, size_t d_frame) {
+    const int f = blockIdx.y;
+    const int lane = threadIdx.x;
+    const int X0 = blockIdx.x * strip_w, X1 = min(X0 + strip_w, w);
+    const int xa = X0 - 2 + 2 * lane;
+    const int c0 = 2 * xa;  // first source column of this lane
+    const bool need = xa < X1 + 2;
+    const bool inner = need && c0 >= 0 && c0 + 4 <= w0;
+    const bool out0 = lane >= 1 && xa < X1, out1 = lane >= 1 && xa + 1 < X1;
     const uint8_t* S = blur0 + (size_t)f * s_frame;
-    for (int i = threadIdx.x; i < (kBTH + 2) * (kBTW + 2); i += 256) {
-        const int r = i / (kBTW + 2), c = i % (kBTW + 2);
-        // pyrDown output at the reflected physical position (the 2:1 grid is not
-        // symmetric about the far edge, so reflect before evaluating).
-        const int py = reflect101(Y0 - 1 + r, h), px = reflect101(X0 - 1 + c, w);
-        int s = 0;
-        const int kk[5] = {1, 4, 6, 4, 1};
+    short2* Gp = go + (size_t)f * d_frame;
+    auto load_row = [&](int r) -> uint32_t {
+        const uint8_t* rp = S + (size_t)reflect101(r, h0) * w0;
+        if (inner) return lb_ld4(rp + c0);
+        uint32_t v = 0;
+        if (need)
+            for (int j = 0; j < 4; ++j) v |= (uint32_t)rp[reflect101(c0 + j, w0)] << (8 * j);
+        return v;
+    };
+    uint32_t pe[5] = {0, 0, 0, 0, 0}, po[5] = {0, 0, 0, 0, 0};
+    int pm1 = 0, p0 = 0;  // output rows y-2, y-1: columns xa (bits 0-7) and xa+1 (bits 8-15)
+    const bool xl = xa == 0, xr = xa + 1 == w - 1;  // output-grid reflection at the borders
+    auto sobel_row = [&](int y, int up, int mid, int dn) {
+        const int su = up & 255, su1 = up >> 8, sm = mid & 255, sm1 = mid >> 8, sd = dn & 255, sd1 = dn >> 8;
+        const int S0 = su + 2 * sm + sd, S1 = su1 + 2 * sm1 + sd1;  // columns xa, xa + 1
+        const int D0 = sd - su, D1 = sd1 - su1;
+        const int pk = S1 | (D1 + 1024) << 12, pkl = S0 | (D0 + 1024) << 12;
+        const int L = dpp_from_left(pk);    // column xa - 1 (left lane's xa + 1)
+        const int R = dpp_from_right(pkl);  // column xa + 2 (right lane's xa)
+        const int Sl = xl ? S1 : (L & 4095), Dl = xl ? D1 : (L >> 12) - 1024;
+        const int Sr = xr ? S0 : (R & 4095), Dr = xr ? D0 : (R >> 12) - 1024;
+        // column xa the last one (odd w): its right neighbour P(w) = P(w - 2)
+        const bool last0 = xa + 1 >= w;
+        const int Sr0 = last0 ? Sl : S1, Dr0 = last0 ? Dl : D1;
+        const int gx0 = Sr0 - Sl, gy0 = Dl + 2 * D0 + Dr0;
+        const int gx1 = Sr - S0, gy1 = D0 + 2 * D1 + Dr;
+        short2* o = Gp + (size_t)y * w + xa;
+        if (out0) o[0] = make_short2((short)gx0, (short)gy0);
+        if (out1) o[1] = make_short2((short)gx1, (short)gy1);
+    };
+    uint32_t pv[8];
 #pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            const uint8_t* R = S + (size_t)reflect101(2 * py + j - 2, h0) * w0;
-            int row = 0;
+    for (int k = 0; k < 8; ++k) pv[k] = load_row(k - 2);
+    const int rend = 2 * h + 3;  // source rows -2 .. 2h
+    for (int rb = -2; rb < rend - 2; rb += 8) {
 #pragma unroll
-            for (int i2 = 0; i2 < 5; ++i2) row += kk[i2] * R[reflect101(2 * px + i2 - 2, w0)];
-            s += kk[j] * row;
+        for (int k = 0; k < 8; ++k) {
+            const int r = rb + k;
+            if (r > 2 * h) break;
+            const uint32_t V = pv[k];
+            if (r + 8 <= 2 * h) pv[k] = load_row(r + 8);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                pe[q] = pe[q + 1];
+                po[q] = po[q + 1];
+            }
+            pe[4] = V & 0x00ff00ffu;
+            po[4] = (V >> 8) & 0x00ff00ffu;
+            if ((k & 1) || r < 2) continue;  // output row y = (r - 2) / 2 from source rows 2y-2 .. 2y+2
+            const int y = (r - 2) >> 1;
+            // vertical 1-4-6-4-1: Ve = (c0, c0+2), Vo = (c0+1, c0+3), fields <= 4080
+            const uint32_t Ve = pe[0] + pe[4] + 4 * (pe[1] + pe[3]) + 6 * pe[2];
+            const uint32_t Vo = po[0] + po[4] + 4 * (po[1] + po[3]) + 6 * po[2];
+            const uint32_t Vel = (uint32_t)dpp_from_left((int)Ve), Vol = (uint32_t)dpp_from_left((int)Vo);
+            const uint32_t Ver = (uint32_t)dpp_from_right((int)Ve);
+            // xa: columns c0-2 .. c0+2; xa+1: c0 .. c0+4
+            const uint32_t s0 = (Vel >> 16) + 4 * (Vol >> 16) + 6 * (Ve & 0xffffu) + 4 * (Vo & 0xffffu) + (Ve >> 16);
+            const uint32_t s1 = (Ve & 0xffffu) + 4 * (Vo & 0xffffu) + 6 * (Ve >> 16) + 4 * (Vo >> 16) + (Ver & 0xffffu);
+            const int P = (int)((s0 + 128u) >> 8) | (int)((s1 + 128u) >> 8) << 8;
+            if (y == 1) sobel_row(0, P, p0, P);
+            else if (y >= 2) sobel_row(y - 1, pm1, p0, P);
+            pm1 = p0;
+            p0 = P;
         }
-        P[r][c] = (uint8_t)((s + 128) >> 8);
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kBTH * kBTW; i += 256) {
-        const int ty = i / kBTW, tx = i % kBTW;
-        const int x = X0 + tx, y = Y0 + ty;
-        if (x >= w || y >= h) continue;
-        const int r = ty + 1, c = tx + 1;
-        const int gx = (P[r - 1][c + 1] - P[r - 1][c - 1]) + 2 * (P[r][c + 1] - P[r][c - 1]) +
-                       (P[r + 1][c + 1] - P[r + 1][c - 1]);
-        const int gy = (P[r + 1][c - 1] - P[r - 1][c - 1]) + 2 * (P[r + 1][c] - P[r - 1][c]) +
-                       (P[r + 1][c + 1] - P[r - 1][c + 1]);
-        const size_t o = (size_t)f * d_frame + (size_t)y * w + x;
-        go[o] = make_short2((short)gx, (short)gy);
-    }
+    if (h >= 2) sobel_row(h - 1, pm1, p0, pm1);
+    else sobel_row(0, p0, p0, p0);
 }
 
 // ---------------------------------------------------------------------------

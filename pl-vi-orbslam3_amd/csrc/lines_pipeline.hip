@@ -68,7 +68,7 @@ struct LinePipeline {
     hipStream_t aux[2] = {nullptr, nullptr};  // frame mode: ORB and LBD-Sobel streams
     hipEvent_t evFork = nullptr, evPrep = nullptr, evSobel = nullptr, evOrb = nullptr, evCrit = nullptr;
     hipStream_t critStream = nullptr;  // frame schedule: prep -> grow -> describe
-    bool orbAfterPrep = true;
+    bool orbAfterPrep = false;
     std::vector<LineOctDev> oct;
     std::vector<float> scaleF, invScaleF;
     double SCALE = 0.8, prec = 0, rho = 0, min_length = 0;
@@ -137,8 +137,10 @@ struct LinePipeline {
             PLVI_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
             const char* e1 = getenv("PLVI_STREAM_PRIO");
             const bool prio = !e1 || atoi(e1) != 0;
+            // PLVI_ORB_AFTER_PREP=1: ORB waits for the LSD prep (default: ORB and
+            // the prep start together, +2 % at B = 3072 with the streaming prep)
             const char* e2 = getenv("PLVI_ORB_AFTER_PREP");
-            orbAfterPrep = !e2 || atoi(e2) != 0;
+            orbAfterPrep = e2 && atoi(e2) != 0;
             for (auto& a : aux) PLVI_CHECK(hipStreamCreateWithPriority(&a, hipStreamNonBlocking, prio ? least : 0));
             if (prio) PLVI_CHECK(hipStreamCreateWithPriority(&critStream, hipStreamNonBlocking, greatest));
         }
@@ -414,17 +416,22 @@ struct LinePipeline {
     // LB1/LB2: LBD Gaussian pyramid + Sobel (depends on the frames only).
     int launch_sobel(const uint8_t* d_frames, int nf, size_t frame_stride, size_t row_stride, hipStream_t st) {
         const LineOctDev& d0 = oct[0];
-        dim3 g0((d0.lw + kBTW - 1) / kBTW, (d0.lh + kBTH - 1) / kBTH, nf);
-        hipLaunchKernelGGL(lbd_blur_sobel_kernel, g0, dim3(256), 0, st, d_frames, frame_stride, row_stride, d0.lw,
-                           d0.lh, lbdBlur.as<uint8_t>(), lbdG.as<short2>() + d0.loff, (size_t)d0.lplane, lbdTaps[0],
-                           lbdTaps[1], lbdTaps[2]);
+        {
+            // column strips of at most kLbOutLanes * 4 columns, balanced, multiples of 4
+            const int ns = (d0.lw + 4 * kLbOutLanes - 1) / (4 * kLbOutLanes);
+            const int sw4 = ((d0.lw + ns - 1) / ns + 3) & ~3;
+            hipLaunchKernelGGL(lbd_sobel0_kernel, dim3((d0.lw + sw4 - 1) / sw4, nf), dim3(64), 0, st, d_frames,
+                               frame_stride, row_stride, d0.lw, d0.lh, sw4, lbdBlur.as<uint8_t>(),
+                               lbdG.as<short2>() + d0.loff, (size_t)d0.lplane, lbdTaps[0], lbdTaps[1], lbdTaps[2]);
+        }
         for (int l = 1; l < nOct; ++l) {
             const LineOctDev& d = oct[l];
             if (l > 1) return PLVI_E_BADARG;  // pyrDown chain beyond octave 1 not wired (config: 2 levels)
-            dim3 g1((d.lw + kBTW - 1) / kBTW, (d.lh + kBTH - 1) / kBTH, nf);
-            hipLaunchKernelGGL(lbd_pyrdown_sobel_kernel, g1, dim3(256), 0, st, (const uint8_t*)lbdBlur.as<uint8_t>(),
-                               d0.lw, d0.lh, (size_t)d0.lplane, d.lw, d.lh, lbdG.as<short2>() + d.loff,
-                               (size_t)d.lplane);
+            const int ns = (d.lw + 2 * kLb2OutLanes - 1) / (2 * kLb2OutLanes);
+            const int sw2 = ((d.lw + ns - 1) / ns + 1) & ~1;
+            hipLaunchKernelGGL(lbd_sobel1_kernel, dim3((d.lw + sw2 - 1) / sw2, nf), dim3(64), 0, st,
+                               (const uint8_t*)lbdBlur.as<uint8_t>(), d0.lw, d0.lh, (size_t)d0.lplane, d.lw, d.lh,
+                               sw2, lbdG.as<short2>() + d.loff, (size_t)d.lplane);
         }
         return PLVI_OK;
     }
@@ -664,6 +671,22 @@ extern "C" int plvi_lines_debug_planes(plvi_line_extractor* h, int frame, int oc
     if (deg) PLVI_CHECK(hipMemcpy(deg, P.pix.as<float>() + o, n * sizeof(float), hipMemcpyDeviceToHost));
     if (modgrad) PLVI_CHECK(hipMemcpy(modgrad, P.modg.as<double>() + o, n * sizeof(double), hipMemcpyDeviceToHost));
     if (cs) PLVI_CHECK(hipMemcpy(cs, P.seedcs.as<float2>() + o, n * sizeof(float2), hipMemcpyDeviceToHost));
+    return PLVI_OK;
+}
+
+// Diagnostic: the LBD Sobel plane (interleaved int16 dx, dy) of the last
+// batch for one (frame, octave), copied to host memory.
+extern "C" int plvi_lines_debug_sobel(plvi_line_extractor* h, int frame, int octave, short* dxdy, int* w, int* hgt) {
+    if (!h || octave < 0 || octave >= h->p().nOct || frame < 0 || frame >= h->p().Bcap) return PLVI_E_BADARG;
+    LinePipeline& P = h->p();
+    PLVI_CHECK(hipSetDevice(P.device));
+    const plvi::LineOctDev& d = P.oct[octave];
+    if (w) *w = d.lw;
+    if (hgt) *hgt = d.lh;
+    PLVI_CHECK(hipDeviceSynchronize());
+    if (dxdy)
+        PLVI_CHECK(hipMemcpy(dxdy, P.lbdG.as<short2>() + d.loff + (size_t)frame * d.lplane,
+                             (size_t)d.lplane * sizeof(short2), hipMemcpyDeviceToHost));
     return PLVI_OK;
 }
 

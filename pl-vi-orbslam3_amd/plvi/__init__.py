@@ -185,6 +185,7 @@ def _declare(lib):
         "plvi_lines_profile_read": ([V, V, P], I),
         "plvi_lines_debug_stats": ([V, V], I),
         "plvi_lines_debug_planes": ([V, I, I, V, V, V, P, P], I),
+        "plvi_lines_debug_sobel": ([V, I, I, V, P, P], I),
         "plvi_descriptor_distance_batch": ([V, V, I, I, V, V], I),
         "plvi_search_by_bow": ([F, I, V, V, V, I, V, V, I, V, V, V, I, V, V, I, V, V], I),
         "plvi_search_by_bow_batch": ([I, F, I, I, I, I, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V], I),
@@ -552,6 +553,15 @@ class Lineextractor:
         _check(self._lib.plvi_lines_debug_planes(self._h, frame, level, _ptr(deg), _ptr(mg), _ptr(cs), None, None),
                "plvi_lines_debug_planes")
         return deg, mg, cs
+
+    def debug_sobel(self, level, frame=0):
+        """(dx, dy) int16 LBD Sobel planes of the last batch (diagnostic)."""
+        w, h = ctypes.c_int(), ctypes.c_int()
+        _check(self._lib.plvi_lines_debug_sobel(self._h, frame, level, None, ctypes.byref(w), ctypes.byref(h)),
+               "plvi_lines_debug_sobel")
+        g = np.zeros((h.value, w.value, 2), np.int16)
+        _check(self._lib.plvi_lines_debug_sobel(self._h, frame, level, _ptr(g), None, None), "plvi_lines_debug_sobel")
+        return g[..., 0].copy(), g[..., 1].copy()
 
     def scale_tables(self):
         out = [np.zeros(self.nlevels, np.float32) for _ in range(4)]

@@ -254,6 +254,21 @@ def lsd_planes(img, lsd_scale=0.8):
     return tuple(b[:m].reshape(sh.value, sw.value).copy() for b in bufs)
 
 
+def lbd_sobel(img, octave):
+    """LBD octave `octave` Sobel planes (dx, dy) int16 of computeGaussianPyramid + Sobel."""
+    lib = load()
+    V, I = ctypes.c_void_p, ctypes.c_int
+    lib.oracle_lbd_sobel.argtypes = [V, I, I, I, V, V, ctypes.POINTER(I), ctypes.POINTER(I)]
+    img = np.ascontiguousarray(img, np.uint8)
+    h, w = img.shape
+    dx = np.zeros(w * h, np.int16)
+    dy = np.zeros(w * h, np.int16)
+    ow, oh = ctypes.c_int(), ctypes.c_int()
+    assert lib.oracle_lbd_sobel(_p(img), w, h, octave, _p(dx), _p(dy), ctypes.byref(ow), ctypes.byref(oh)) == 0
+    n = ow.value * oh.value
+    return dx[:n].reshape(oh.value, ow.value), dy[:n].reshape(oh.value, ow.value)
+
+
 def line_iterator_count(W, H, x1, y1, x2, y2):
     lib = load()
     F, I = ctypes.c_float, ctypes.c_int

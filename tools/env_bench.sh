@@ -16,6 +16,6 @@ import json, sys
 d = json.load(open(sys.argv[2]))
 s = d["stage_ms"]
 print(f"{sys.argv[1]:12s} fps {d['value']:9.1f} ms/step {d['ms_per_step']:7.2f} grow {s['lines.region_grow']:7.2f} "
-      f"prep {s['lines.lsd_prep']:6.2f} lbd {s['lines.lbd']:6.2f} parts {d.get('part_fps')} chk {len(d['oracle_check']['mismatches'])}", flush=True)
+      f"prep {s['lines.lsd_prep']:6.2f} lbd {s['lines.lbd']:6.2f} parts {d.get('part_fps')} chk {len(d.get('oracle_check', {}).get('mismatches', []))}", flush=True)
 PY
 done
