@@ -405,6 +405,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
     unsigned long long s_setup = 0, s_round = 0, s_rect = 0, n_seed = 0, n_block = 0, n_round = 0, n_rpt = 0,
                        n_commit = 0;
     unsigned long long s_ph[4] = {0, 0, 0, 0};
+    unsigned long long n_dy[3] = {0, 0, 0};
     constexpr bool do_stats = STATS;  // diagnostic variant only (keeps SGPRs free in the product kernel)
     const unsigned long long t_begin = do_stats ? __builtin_amdgcn_s_memtime() : 0;
     const int half = R / 2, halfb = RB / 2;
@@ -524,58 +525,58 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                             dup |= 1ull << (9 * p2 + ddy * 3 + ddx);
                     }
                     unsigned long long t1 = 0;
-                    if (do_stats) { t1 = __builtin_amdgcn_s_memtime(); s_setup += t1 - t0; n_block++; }
+                    if (do_stats) {
+                        t1 = __builtin_amdgcn_s_memtime(); s_setup += t1 - t0; n_block++;
+                        // rows below the seed row of the tested neighbours: 0-1 / 2-7 / 8+
+                        n_dy[0] += __popcll(__ballot(valid && ny - y <= 1));
+                        n_dy[1] += __popcll(__ballot(valid && ny - y >= 2 && ny - y < 8));
+                        n_dy[2] += __popcll(__ballot(valid && ny - y >= 8));
+                    }
+                    // USED is read once per block: within the block a lane's pixel
+                    // only becomes USED through a commit of an earlier lane testing
+                    // the same pixel (dup), tracked in Ccum
+                    const bool live0 = valid && deg != kNotdefF && !used_get(g, nx, ny);
+                    unsigned long long Ccum = 0;
                     int start = 0;
                     while (start < 9 * nb) {
                         unsigned long long r0t = 0;
                         if (do_stats) { n_round++; r0t = __builtin_amdgcn_s_memtime(); }
                         const unsigned long long fromStart = ~0ull << start;
-                        const bool candl = lane >= start && deg != kNotdefF && !used_get(g, nx, ny);
+                        const bool candl = lane >= start && live0 && (dup & Ccum) == 0ull;
                         const bool al = candl && is_aligned_fast(deg, reg_deg, pdeg, prec);
                         const bool acc = al && (dup & fromStart) == 0ull;
                         const unsigned long long A = __ballot(acc);
                         if (do_stats) { const unsigned long long t = __builtin_amdgcn_s_memtime(); s_ph[0] += t - r0t; r0t = t; }
                         if (!A) break;  // no commit: every remaining decision is final
-                        // exact angle sequence of the speculated commits (sequential float sums)
-                        float sx2 = sumdx, sy2 = sumdy, pfx = 0.f, pfy = 0.f;
+                        // exact angle sequence of the speculated commits (sequential float
+                        // sums); every lane keeps the sums after its cl accepted
+                        // predecessors, i.e. the region angle its own test really sees
+                        const int cl = __popcll(A & below);
+                        float sx2 = sumdx, sy2 = sumdy, pfx = sumdx, pfy = sumdy;
                         int t = 0;
-                        for (unsigned long long mm = A; mm; mm &= mm - 1, ++t) {
+                        for (unsigned long long mm = A; mm; mm &= mm - 1) {
                             const int bl = __ffsll((long long)mm) - 1;
                             sx2 += readlane_f(cc, bl);
                             sy2 += readlane_f(ss, bl);
-                            if (lane == t) { pfx = sx2; pfy = sy2; }
+                            ++t;
+                            if (cl == t) { pfx = sx2; pfy = sy2; }
                         }
-                        const int mcount = t;
-                        const float th = lane < mcount ? plvi_fast_atan2(pfy, pfx) : 0.f;
+                        const float tha = plvi_fast_atan2(pfy, pfx);
+                        const float th = cl > 0 ? tha : reg_deg;
                         if (do_stats) { const unsigned long long t = __builtin_amdgcn_s_memtime(); s_ph[1] += t - r0t; r0t = t; }
                         // verify every decision against the angle it really sees
-                        const int cl = __popcll(A & below);
-                        float theta_l = reg_deg;
-                        if (mcount <= 6) {
-                            for (int k = 0; k < mcount; ++k) {
-                                const float v = readlane_f(th, k);
-                                if (cl == k + 1) theta_l = v;
-                            }
-                        } else {
-                            const float v = __shfl(th, cl > 0 ? cl - 1 : 0);
-                            if (cl > 0) theta_l = v;
-                        }
-                        const bool al2 = candl && (dup & A) == 0ull && is_aligned_fast(deg, theta_l, pdeg, prec);
+                        const bool al2 = candl && (dup & A) == 0ull && is_aligned_fast(deg, th, pdeg, prec);
                         const unsigned long long mism = __ballot(al2 != acc) & fromStart;
                         if (do_stats) { const unsigned long long t = __builtin_amdgcn_s_memtime(); s_ph[2] += t - r0t; r0t = t; }
-                        unsigned long long C;
-                        int nc;
-                        if (!mism) {
-                            C = A;
-                            nc = mcount;
-                            start = 9 * nb;
-                        } else {
-                            const int ls = __ffsll((long long)mism) - 1;
-                            C = A & ((1ull << ls) - 1ull);
-                            nc = __popcll(C);
-                            start = ls;  // re-decided exactly next round
-                        }
+                        // commit the consistent prefix: lanes below the first mismatch (lane
+                        // 63, never a test lane, when all agree); that lane holds the sums
+                        // and angle after exactly those commits
+                        const int ls = mism ? __ffsll((long long)mism) - 1 : 63;
+                        const unsigned long long C = A & ((1ull << ls) - 1ull);
+                        const int nc = __popcll(C);
+                        start = mism ? ls : 9 * nb;  // a mismatch is re-decided exactly next round
                         if (nc > 0) {
+                            Ccum |= C;
                             const bool mine = (C >> lane) & 1ull;
                             if (mine) {
                                 used_set(g, nx, ny);
@@ -584,9 +585,9 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
                             // global USED bits / queue spill must land before they are read back
                             if (__ballot(mine && ny >= g.wbb + RB) || reg_size + nc > QL) vm_drain();
                             reg_size += nc;
-                            sumdx = readlane_f(pfx, nc - 1);
-                            sumdy = readlane_f(pfy, nc - 1);
-                            reg_deg = readlane_f(th, nc - 1);
+                            sumdx = readlane_f(pfx, ls);
+                            sumdy = readlane_f(pfy, ls);
+                            reg_deg = readlane_f(th, ls);
                             if (do_stats) n_commit += nc;
                         }
                         __builtin_amdgcn_wave_barrier();
@@ -623,6 +624,7 @@ __global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restri
         S[1] = s_setup; S[2] = s_round; S[3] = s_rect; S[4] = n_seed;
         S[5] = n_block; S[6] = n_round; S[7] = n_rpt; S[8] = n_commit;
         S[9] = s_ph[0]; S[10] = s_ph[1]; S[11] = s_ph[2]; S[12] = s_ph[3];
+        S[13] = n_dy[0]; S[14] = n_dy[1]; S[15] = n_dy[2];
     }
 }
 

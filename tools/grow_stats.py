@@ -1,26 +1,46 @@
-"""Diagnostic: cycle accounting of the LSD region-growing kernel on one batch."""
-import sys, pathlib, numpy as np
+"""Diagnostic: cycle accounting of the LSD region-growing kernel on one batch
+(the bench's device sequence, so B = 3072 shows the contended per-wave times).
+usage: python tools/grow_stats.py [B]"""
+import ctypes
+import pathlib
+import sys
+
+import numpy as np
+import torch
+
 ROOT = pathlib.Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "pl-vi-orbslam3_amd"))
-import plvi
-from plvi import synth
+import plvi  # noqa: E402
+from plvi import synth  # noqa: E402
+
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 16
-frames = synth.batch(B)
+seq = synth.device_sequence(B, 640, 480, seed=0, device="cuda:0")
+torch.cuda.synchronize()
 lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 640, 480, max_batch=B)
-buf = plvi.DeviceBuffer(frames.nbytes); buf.upload(frames)
-st = plvi.DeviceBuffer(B * 2 * 16 * 8)
+st = torch.zeros(B * 2 * 16, dtype=torch.int64, device="cuda:0")
 lib = plvi.load()
-lx.extract_batch(buf.ptr, B, 640 * 480, 640); lib.plvi_device_synchronize()
-lib.plvi_lines_debug_stats(lx._h, __import__("ctypes").c_void_p(st.ptr))
-lx.extract_batch(buf.ptr, B, 640 * 480, 640); lib.plvi_device_synchronize()
-s = st.download(np.zeros((B, 2, 16), np.uint64)).astype(np.float64)
-names = ["total", "block_setup", "rounds", "rect", "seeds", "blocks", "rounds_n", "rect_pts", "commits", "ph_decide", "ph_angles", "ph_verify", "ph_commit"]
+lx.extract_batch(seq.data_ptr(), B, 640 * 480, 640)
+lib.plvi_device_synchronize()
+lib.plvi_lines_debug_stats(lx._h, ctypes.c_void_p(st.data_ptr()))
+lx.extract_batch(seq.data_ptr(), B, 640 * 480, 640)
+lib.plvi_device_synchronize()
+lib.plvi_lines_debug_stats(lx._h, ctypes.c_void_p(0))
+s = st.cpu().numpy().reshape(B, 2, 16).astype(np.float64)
+names = ["total", "block_setup", "rounds", "rect", "seeds", "blocks", "rounds_n", "rect_pts", "commits", "ph_decide",
+         "ph_angles", "ph_verify", "ph_commit", "dy_0_1", "dy_2_7", "dy_8p"]
+print(f"B = {B}")
 for o in range(2):
     print(f"octave {o}:")
     for i, n in enumerate(names):
         print(f"  {n:10s} mean {s[:, o, i].mean():14.0f}  max {s[:, o, i].max():14.0f}")
     t = s[:, o]
-    print("  setup cycles/block %.0f  round cycles/round %.0f  rounds/block %.2f  commits/round %.2f  rect cycles/pt %.0f  total cycles/commit %.0f" % (
-        (t[:, 1] / t[:, 5]).mean(), (t[:, 2] / t[:, 6]).mean(), (t[:, 6] / t[:, 5]).mean(), (t[:, 8] / t[:, 6]).mean(),
-        (t[:, 3] / np.maximum(t[:, 7], 1)).mean(), (t[:, 0] / np.maximum(t[:, 8], 1)).mean()))
-    print("  per round: decide %.0f  angles %.0f  verify %.0f  commit %.0f" % tuple((t[:, 9 + k] / t[:, 6]).mean() for k in range(4)))
+    print("  setup cycles/block %.0f  round cycles/round %.0f  rounds/block %.2f  commits/round %.2f  "
+          "rect cycles/pt %.0f  total cycles/commit %.0f" % (
+              (t[:, 1] / t[:, 5]).mean(), (t[:, 2] / t[:, 6]).mean(), (t[:, 6] / t[:, 5]).mean(),
+              (t[:, 8] / t[:, 6]).mean(), (t[:, 3] / np.maximum(t[:, 7], 1)).mean(),
+              (t[:, 0] / np.maximum(t[:, 8], 1)).mean()))
+    print("  per round: decide %.0f  angles %.0f  verify %.0f  commit %.0f" % tuple(
+        (t[:, 9 + k] / t[:, 6]).mean() for k in range(4)))
+    dy = t[:, 13:16].sum(axis=0)
+    print("  tested neighbours by rows below the seed: 0-1 %.1f%%  2-7 %.1f%%  8+ %.1f%%" % tuple(100 * dy / dy.sum()))
+    print("  wave time: mean %.0f  max %.0f cycles" % (t[:, 0].mean(), t[:, 0].max()))
