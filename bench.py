@@ -484,6 +484,13 @@ def run(args, world, rank):
                            cuda, seed0)
 
     # ---------------------------------------------------------- timed region
+    # the roofline events cover exactly the timed launches; a spin_kernel on
+    # each side marks the same window in a rocprofv3 kernel trace
+    # (tools/timed_stats.py)
+    for sl in slots:
+        sl.orb.kernel_timing(True)
+        sl.lx.kernel_timing(True)
+    torch.cuda._sleep(1000)
     pdist.barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -494,6 +501,7 @@ def run(args, world, rank):
     torch.cuda.synchronize()
     pdist.barrier(world)
     el = pdist.max_over_ranks(time.perf_counter() - t0, world, cuda)
+    torch.cuda._sleep(1000)
 
     new_frames = (B - 1) if args.c4 else B
     frames_total = new_frames * args.steps * world

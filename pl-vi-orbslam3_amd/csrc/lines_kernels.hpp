@@ -347,8 +347,14 @@ __device__ __forceinline__ void bits_load_rows(const GrowCtx& g, int r0, int r1,
     }
 }
 
+// waves per SIMD the region-growing kernel is compiled for: 8 caps it at 64
+// VGPRs, so its 6 resident waves per SIMD (a 3072-frame batch) leave room for
+// the ORB / LBD waves of the frame schedule
+#ifndef PLVI_GROW_WPE
+#define PLVI_GROW_WPE 8
+#endif
 template <bool STATS>
-__global__ __launch_bounds__(64) void lsd_grow_kernel(const LineOctDev* __restrict__ octs,
+__global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineOctDev* __restrict__ octs,
                                                       const float* __restrict__ pix,
                                                       const double* __restrict__ modgrad,
                                                       const float2* __restrict__ pixcs,

@@ -26,12 +26,12 @@ if [ "${SKIP_PROF:-0}" != 1 ]; then
   # the bench command itself (default arguments unless STATS_ARGS is set)
   timeout -k 10 ${PROF_T:-400} rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py ${STATS_ARGS:-} > $OUT/prof.log 2>&1
   rc=$?; tail -3 $OUT/prof.log; fatal $rc rocprof hard
+  python3 $R/tools/timed_stats.py $OUT/prof/run_kernel_trace.csv $OUT/kernel_stats_timed.csv
 fi
 if [ "${SKIP_PMC:-0}" != 1 ]; then
-  for c in FETCH_SIZE WRITE_SIZE; do
-    echo "== pmc $c"
-    timeout -s KILL ${PMC_T:-240} rocprofv3 --pmc $c -d $OUT/pmc_$c -o run --output-format csv -- python3 $R/bench.py $PARGS > $OUT/pmc_$c.log 2>&1
-    rc=$?; tail -2 $OUT/pmc_$c.log; fatal $rc pmc_$c hard
-  done
+  # calibrated HBM traffic of the roofline kernels (separate FETCH_SIZE / WRITE_SIZE passes)
+  echo "== pmc traffic"
+  cd $R && B=${PMC_B:-3072} bash tools/gpu_traffic.sh > $OUT/pmc.log 2>&1
+  rc=$?; tail -4 $OUT/pmc.log; fatal $rc pmc hard
 fi
 exit 0
