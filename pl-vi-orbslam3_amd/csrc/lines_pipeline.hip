@@ -16,6 +16,9 @@
 #include "lines_kernels.hpp"
 #include "plvi_common.h"
 
+// internal hook of the ORB pipeline (orb_pipeline.hip): event after the blur + FAST launch
+extern "C" int plvi_orb_internal_blur_event(plvi_orb_extractor* h, hipEvent_t ev);
+
 namespace plvi {
 
 static inline int lround_h(float v) { return (int)lrintf(v); }
@@ -66,7 +69,9 @@ struct LinePipeline {
     int W = 0, H = 0, Bcap = 0, device = 0, nOct = 0, fcap = 0;
     hipStream_t stream = nullptr;
     hipStream_t aux[2] = {nullptr, nullptr};  // frame mode: ORB and LBD-Sobel streams
-    hipEvent_t evFork = nullptr, evPrep = nullptr, evSobel = nullptr, evOrb = nullptr, evCrit = nullptr;
+    hipEvent_t evFork = nullptr, evPrep = nullptr, evSobel = nullptr, evOrb = nullptr, evCrit = nullptr,
+               evBlur = nullptr;
+    bool growAfterBlur = true;
     hipStream_t critStream = nullptr;  // frame schedule: prep -> grow -> describe
     bool orbAfterPrep = false;
     std::vector<LineOctDev> oct;
@@ -114,7 +119,7 @@ struct LinePipeline {
     ~LinePipeline() {
         for (auto e : kev) (void)hipEventDestroy(e);
         for (auto e : evs) (void)hipEventDestroy(e);
-        for (auto e : {evFork, evPrep, evSobel, evOrb, evCrit})
+        for (auto e : {evFork, evPrep, evSobel, evOrb, evCrit, evBlur})
             if (e) (void)hipEventDestroy(e);
         if (critStream) (void)hipStreamDestroy(critStream);
         for (auto a : aux)
@@ -141,10 +146,16 @@ struct LinePipeline {
             // the prep start together, +2 % at B = 3072 with the streaming prep)
             const char* e2 = getenv("PLVI_ORB_AFTER_PREP");
             orbAfterPrep = e2 && atoi(e2) != 0;
+            // PLVI_GROW_AFTER_BLUR=0: region growing starts right after the prep
+            // (default 1: it waits for the ORB blur + FAST launch, whose 81-VGPR /
+            // 9 KB-LDS waves cannot share a CU with the region-growing waves; the
+            // rest of the ORB chain then runs alongside region growing)
+            const char* e3 = getenv("PLVI_GROW_AFTER_BLUR");
+            growAfterBlur = !e3 || atoi(e3) != 0;
             for (auto& a : aux) PLVI_CHECK(hipStreamCreateWithPriority(&a, hipStreamNonBlocking, prio ? least : 0));
             if (prio) PLVI_CHECK(hipStreamCreateWithPriority(&critStream, hipStreamNonBlocking, greatest));
         }
-        for (auto* e : {&evFork, &evPrep, &evSobel, &evOrb, &evCrit})
+        for (auto* e : {&evFork, &evPrep, &evSobel, &evOrb, &evCrit, &evBlur})
             PLVI_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         fcap = p->nfeatures > 0 ? p->nfeatures : kKlCap;
         SCALE = (double)p->lsd_scale;  // LSDOptions::scale is float
@@ -481,11 +492,14 @@ struct LinePipeline {
         PLVI_CHECK(hipEventRecord(evPrep, crit));
         hipEvent_t auxStart = orbAfterPrep ? evPrep : evFork;
         PLVI_CHECK(hipStreamWaitEvent(aux[0], auxStart, 0));
+        if (growAfterBlur) plvi_orb_internal_blur_event(orb, evBlur);
         int rc = plvi_orb_extract_batch(orb, d_frames, nf, frame_stride, row_stride, lap0, lap1, aux[0]);
+        if (growAfterBlur) plvi_orb_internal_blur_event(orb, nullptr);
         PLVI_CHECK(hipEventRecord(evOrb, aux[0]));
         PLVI_CHECK(hipStreamWaitEvent(aux[1], auxStart, 0));
         if (!rc) rc = launch_sobel(d_frames, nf, frame_stride, row_stride, aux[1]);
         PLVI_CHECK(hipEventRecord(evSobel, aux[1]));
+        if (growAfterBlur && !rc) PLVI_CHECK(hipStreamWaitEvent(crit, evBlur, 0));
         launch_grow_assemble(nf, crit);
         PLVI_CHECK(hipStreamWaitEvent(crit, evSobel, 0));
         launch_describe(nf, crit);

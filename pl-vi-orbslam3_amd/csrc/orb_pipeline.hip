@@ -77,6 +77,7 @@ struct OrbPipeline {
     static constexpr int kKRing = 4096;
     bool ktime = false;
     int kn = 0;
+    hipEvent_t evAfterBlur = nullptr;  // frame schedule hook (plvi_orb_internal_blur_event)
     std::vector<hipEvent_t> kev;
     int ktiming(int on) {
         if (on && kev.empty()) {
@@ -329,6 +330,7 @@ struct OrbPipeline {
             PLVI_CHECK(hipEventRecord(kev[2 * kn + 1], st));
             ++kn;
         }
+        if (evAfterBlur) PLVI_CHECK(hipEventRecord(evAfterBlur, st));
         mark(1, st);
         // K2 cell NMS -> candidate map (zeroed first: only detection windows are written)
         PLVI_CHECK(hipMemsetAsync(Cd, 0, candBytesTotal, st));
@@ -541,6 +543,14 @@ extern "C" int plvi_orb_profile_read(plvi_orb_extractor* h, float* stage_ms, int
     if (!h || !stage_ms) return PLVI_E_BADARG;
     PLVI_CHECK(hipSetDevice(h->p().device));
     return h->p().profile_read(stage_ms, runs);
+}
+
+// Internal (frame schedule): record `ev` on the batch stream right after the
+// blur + FAST launch of every later batch (nullptr: off).
+extern "C" int plvi_orb_internal_blur_event(plvi_orb_extractor* h, hipEvent_t ev) {
+    if (!h) return PLVI_E_BADARG;
+    h->p().evAfterBlur = ev;
+    return PLVI_OK;
 }
 
 extern "C" int plvi_orb_kernel_timing(plvi_orb_extractor* h, int enable) {
