@@ -249,7 +249,14 @@ __global__ __launch_bounds__(64 * (kPyrFrames + 1)) void orb_pyramid_kernel(
 // T) rejects ~90 % of pixels; survivors are queued (row, column) and scored
 // 64 at a time from an LDS ring of the last 32 raw rows.
 // ---------------------------------------------------------------------------
-constexpr int kBfCols = (244 / kBfAlign) * kBfAlign, kBfRows = 128, kRingRows = 32, kRingW = 256, kBfQCap = 320;
+// PLVI_BF_LEAN (default): a 16-row ring and 16-bit queue entries (row modulo
+// 256: queued rows are never 256 rows old), 4.6 KB of LDS and <= 64 VGPRs, so 8
+// waves fit a SIMD and the launch can share CUs with region growing
+#ifndef PLVI_BF_LEAN
+#define PLVI_BF_LEAN 1
+#endif
+constexpr int kBfCols = (244 / kBfAlign) * kBfAlign, kBfRows = 128, kRingRows = PLVI_BF_LEAN ? 16 : 32, kRingW = 256,
+              kBfQCap = 320;
 
 __device__ __forceinline__ int lane_from_left(int v) {  // lane i <- lane i-1 (wave_shr:1)
     return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
@@ -322,8 +329,9 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
                                                            uint8_t* __restrict__ blur, uint8_t* __restrict__ score,
                                                            int k0, int k1, int k2, int k3, int tmin, int nstrips,
                                                            int nf) {
+    typedef typename std::conditional<PLVI_BF_LEAN != 0, unsigned short, unsigned>::type QT;
     __shared__ __align__(16) uint8_t ring[kRingRows][kRingW];
-    __shared__ unsigned q[kBfQCap];
+    __shared__ QT q[kBfQCap];
     // XCD-affine mapping: blocks b and b + 8 share an XCD (and its L2), so
     // every strip of a frame goes to one XCD and the rows / columns two
     // strips share are fetched from HBM once
@@ -359,7 +367,8 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
     auto pk = [](int lo, int hi) { return (uint32_t)lo | (uint32_t)hi << 16; };
     int nq = 0;      // queued candidates (wave-uniform)
     int oldest = 0;  // row of the oldest queued candidate
-    auto flush = [&](int n) {  // score the first n (<= 64) queued candidates
+    int ynew = 0;    // row of the newest queued candidate (queue rows are stored modulo 256)
+    auto flush = [&](int n, int ycur) {  // score the first n (<= 64) queued candidates (ycur: newest queued row)
         // one wave per block: wave-scope ordering only (no store drain).  The
         // candidate bytes below land after this wave's earlier zero stores of
         // the same pixels: a wavefront observes its own memory operations in
@@ -367,22 +376,22 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
         wave_sync();
         if (lane < n) {
             const unsigned e = q[lane];
-            const int yy = (int)(e >> 8), rc = (int)(e & 255u);
+            const int yy = ycur - (int)((((unsigned)ycur & 255u) - (e >> 8)) & 255u), rc = (int)(e & 255u);
             const int Sv = fast_S_ring(ring, yy, rc);
             Sp[(size_t)yy * bw + (sd.x0 - 4 + rc)] = (uint8_t)(Sv >= T ? Sv - 1 : 0);
         }
         wave_sync();
         const int rest = nq - n;
-        unsigned t[(kBfQCap - 64) / 64];
+        QT t[(kBfQCap - 64) / 64];
 #pragma unroll
-        for (int k = 0; k < (kBfQCap - 64) / 64; ++k) t[k] = lane + 64 * k < rest ? q[n + lane + 64 * k] : 0u;
+        for (int k = 0; k < (kBfQCap - 64) / 64; ++k) t[k] = lane + 64 * k < rest ? q[n + lane + 64 * k] : (QT)0;
         wave_sync();
 #pragma unroll
         for (int k = 0; k < (kBfQCap - 64) / 64; ++k)
             if (lane + 64 * k < rest) q[lane + 64 * k] = t[k];
         nq = rest;
         wave_sync();
-        oldest = rest > 0 ? (int)(q[0] >> 8) : 0;
+        oldest = rest > 0 ? ycur - (int)((((unsigned)ycur & 255u) - ((unsigned)q[0] >> 8)) & 255u) : 0;
     };
     // rows rb..rb+7 of the source (reflected), four columns per lane
     auto load_rows = [&](int rb, uint32_t* pv) {
@@ -408,7 +417,7 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
     for (int rb = y0 - 3; rb < y1 + 3; rb += 8) {
         // writing rows rb..rb+7 replaces rows rb-32..rb-25 of the ring; a
         // queued row yy needs rows yy-3..yy+3
-        if (nq > 0 && oldest - 3 < rb - (kRingRows - 8)) flush(nq);
+        if (nq > 0 && oldest - 3 < rb - (kRingRows - 8)) flush(nq, ynew);
 #pragma unroll
         for (int k = 0; k < 8; ++k)
             *reinterpret_cast<uint32_t*>(&ring[(rb + k) & (kRingRows - 1)][4 * lane]) = pv[k];
@@ -498,14 +507,15 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const unsigned long long m = __ballot(cand[j]);
-                if (cand[j]) q[nq + __popcll(m & ((1ull << lane) - 1ull))] = ((unsigned)y << 8) | (unsigned)(4 * lane + j);
+                if (cand[j]) q[nq + __popcll(m & ((1ull << lane) - 1ull))] = (QT)(((unsigned)y & 255u) << 8 | (unsigned)(4 * lane + j));
                 nq += __popcll(m);
             }
             if (nq0 == 0 && nq > 0) oldest = y;
-            while (nq >= 64) flush(64);
+            if (nq > nq0) ynew = y;
+            while (nq >= 64) flush(64, ynew);
         }
     }
-    while (nq > 0) flush(min(nq, 64));
+    while (nq > 0) flush(min(nq, 64), ynew);
 }
 
 // ---------------------------------------------------------------------------
