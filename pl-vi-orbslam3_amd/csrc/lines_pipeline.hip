@@ -492,14 +492,18 @@ struct LinePipeline {
         PLVI_CHECK(hipEventRecord(evPrep, crit));
         hipEvent_t auxStart = orbAfterPrep ? evPrep : evFork;
         PLVI_CHECK(hipStreamWaitEvent(aux[0], auxStart, 0));
-        if (growAfterBlur) plvi_orb_internal_blur_event(orb, evBlur);
+        // only a batch whose region-growing waves fill the SIMDs (>= 2 per SIMD
+        // from 1024 frames on) starves blur + FAST; a small batch is latency-bound
+        // and starts region growing right after the prep
+        const bool waitBlur = growAfterBlur && nf >= 1024;
+        if (waitBlur) plvi_orb_internal_blur_event(orb, evBlur);
         int rc = plvi_orb_extract_batch(orb, d_frames, nf, frame_stride, row_stride, lap0, lap1, aux[0]);
-        if (growAfterBlur) plvi_orb_internal_blur_event(orb, nullptr);
+        if (waitBlur) plvi_orb_internal_blur_event(orb, nullptr);
         PLVI_CHECK(hipEventRecord(evOrb, aux[0]));
         PLVI_CHECK(hipStreamWaitEvent(aux[1], auxStart, 0));
         if (!rc) rc = launch_sobel(d_frames, nf, frame_stride, row_stride, aux[1]);
         PLVI_CHECK(hipEventRecord(evSobel, aux[1]));
-        if (growAfterBlur && !rc) PLVI_CHECK(hipStreamWaitEvent(crit, evBlur, 0));
+        if (waitBlur && !rc) PLVI_CHECK(hipStreamWaitEvent(crit, evBlur, 0));
         launch_grow_assemble(nf, crit);
         PLVI_CHECK(hipStreamWaitEvent(crit, evSobel, 0));
         launch_describe(nf, crit);
