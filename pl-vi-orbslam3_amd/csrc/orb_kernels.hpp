@@ -255,6 +255,9 @@ __global__ __launch_bounds__(64 * (kPyrFrames + 1)) void orb_pyramid_kernel(
 #ifndef PLVI_BF_LEAN
 #define PLVI_BF_LEAN 1
 #endif
+#ifndef PLVI_BF_SRING
+#define PLVI_BF_SRING 0
+#endif
 constexpr int kBfCols = (244 / kBfAlign) * kBfAlign, kBfRows = 128, kRingRows = PLVI_BF_LEAN ? 16 : 32, kRingW = 256,
               kBfQCap = 320;
 
@@ -332,6 +335,12 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
     typedef typename std::conditional<PLVI_BF_LEAN != 0, unsigned short, unsigned>::type QT;
     __shared__ __align__(16) uint8_t ring[kRingRows][kRingW];
     __shared__ QT q[kBfQCap];
+#if PLVI_BF_SRING
+    // score rows of the last kRingRows output rows: candidates are scored into
+    // LDS and a row is stored once, complete, when it leaves the window (no
+    // zero-then-candidate double writes of the score plane)
+    __shared__ __align__(16) uint8_t sring[kRingRows][kRingW];
+#endif
     // XCD-affine mapping: blocks b and b + 8 share an XCD (and its L2), so
     // every strip of a frame goes to one XCD and the rows / columns two
     // strips share are fetched from HBM once
@@ -378,7 +387,11 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
             const unsigned e = q[lane];
             const int yy = ycur - (int)((((unsigned)ycur & 255u) - (e >> 8)) & 255u), rc = (int)(e & 255u);
             const int Sv = fast_S_ring(ring, yy, rc);
+#if PLVI_BF_SRING
+            sring[yy & (kRingRows - 1)][rc] = (uint8_t)(Sv >= T ? Sv - 1 : 0);
+#else
             Sp[(size_t)yy * bw + (sd.x0 - 4 + rc)] = (uint8_t)(Sv >= T ? Sv - 1 : 0);
+#endif
         }
         wave_sync();
         const int rest = nq - n;
@@ -393,6 +406,17 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
         wave_sync();
         oldest = rest > 0 ? ycur - (int)((((unsigned)ycur & 255u) - ((unsigned)q[0] >> 8)) & 255u) : 0;
     };
+#if PLVI_BF_SRING
+    auto store_score_row = [&](int yy) {  // LDS score row yy -> score plane (complete dwords)
+        if (outl) {
+            const uint32_t v = *reinterpret_cast<const uint32_t*>(&sring[yy & (kRingRows - 1)][4 * lane]);
+            const uint32_t ob = (uint32_t)(yy * bw + c0);
+            if (nout == 4) st_u32(Sp + ob, v);
+            else
+                for (int j = 0; j < nout; ++j) Sp[ob + j] = (uint8_t)byte_of(v, j);
+        }
+    };
+#endif
     // rows rb..rb+7 of the source (reflected), four columns per lane
     auto load_rows = [&](int rb, uint32_t* pv) {
 #pragma unroll
@@ -489,17 +513,21 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
             bool cand[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) cand[j] = (candm >> j) & 1u;
+#if PLVI_BF_SRING
+            if (y - kRingRows >= y0) store_score_row(y - kRingRows);
+            *reinterpret_cast<uint32_t*>(&sring[y & (kRingRows - 1)][4 * lane]) = 0u;  // candidates land by flush
+#endif
             if (outl) {
                 const uint32_t o = (uint32_t)(y * w + c0), ob = (uint32_t)(y * bw + c0);
                 if (nout == 4) {
                     if (sd.level == 0) st_u32(Dp + o, cvw);
                     st_u32(Bp + ob, Bv);
-                    st_u32(Sp + ob, 0u);  // candidates are overwritten by flush (wave-ordered)
+                    if (!PLVI_BF_SRING) st_u32(Sp + ob, 0u);  // candidates are overwritten by flush (wave-ordered)
                 } else {
                     for (int j = 0; j < nout; ++j) {
                         if (sd.level == 0) Dp[o + j] = (uint8_t)byte_of(cvw, j);
                         Bp[ob + j] = (uint8_t)byte_of(Bv, j);
-                        Sp[ob + j] = 0;
+                        if (!PLVI_BF_SRING) Sp[ob + j] = 0;
                     }
                 }
             }
@@ -516,6 +544,10 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
         }
     }
     while (nq > 0) flush(min(nq, 64), ynew);
+#if PLVI_BF_SRING
+    wave_sync();
+    for (int yy = max(y0, y1 - kRingRows); yy < y1; ++yy) store_score_row(yy);
+#endif
 }
 
 // ---------------------------------------------------------------------------
