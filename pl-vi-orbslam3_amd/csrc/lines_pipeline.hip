@@ -70,8 +70,8 @@ struct LinePipeline {
     hipStream_t stream = nullptr;
     hipStream_t aux[2] = {nullptr, nullptr};  // frame mode: ORB and LBD-Sobel streams
     hipEvent_t evFork = nullptr, evPrep = nullptr, evSobel = nullptr, evOrb = nullptr, evCrit = nullptr,
-               evBlur = nullptr;
-    bool growAfterBlur = true;
+               evBlur = nullptr, evGate = nullptr;
+    bool growAfterBlur = true, sobelWithGrow = false;
     hipStream_t critStream = nullptr;  // frame schedule: prep -> grow -> describe
     bool orbAfterPrep = false;
     std::vector<LineOctDev> oct;
@@ -119,7 +119,7 @@ struct LinePipeline {
     ~LinePipeline() {
         for (auto e : kev) (void)hipEventDestroy(e);
         for (auto e : evs) (void)hipEventDestroy(e);
-        for (auto e : {evFork, evPrep, evSobel, evOrb, evCrit, evBlur})
+        for (auto e : {evFork, evPrep, evSobel, evOrb, evCrit, evBlur, evGate})
             if (e) (void)hipEventDestroy(e);
         if (critStream) (void)hipStreamDestroy(critStream);
         for (auto a : aux)
@@ -152,10 +152,21 @@ struct LinePipeline {
             // rest of the ORB chain then runs alongside region growing)
             const char* e3 = getenv("PLVI_GROW_AFTER_BLUR");
             growAfterBlur = !e3 || atoi(e3) != 0;
-            for (auto& a : aux) PLVI_CHECK(hipStreamCreateWithPriority(&a, hipStreamNonBlocking, prio ? least : 0));
+            // PLVI_ORB_PRIO (default 1): the ORB stream at the greatest priority as
+            // well (its pyramid + blur gate region growing from 1024 frames on)
+            const char* e4 = getenv("PLVI_ORB_PRIO");
+            const bool orbHigh = !e4 || atoi(e4) != 0;
+            for (int a = 0; a < 2; ++a)
+                PLVI_CHECK(hipStreamCreateWithPriority(&aux[a], hipStreamNonBlocking,
+                                                       prio ? (a == 0 && orbHigh ? greatest : least) : 0));
+            // PLVI_SOBEL_WITH_GROW (default 1): the LBD Sobel pyramid (needed only
+            // by the LBD describe at the end) starts with region growing instead
+            // of competing with the prep and the ORB pyramid
+            const char* e5 = getenv("PLVI_SOBEL_WITH_GROW");
+            sobelWithGrow = !e5 || atoi(e5) != 0;
             if (prio) PLVI_CHECK(hipStreamCreateWithPriority(&critStream, hipStreamNonBlocking, greatest));
         }
-        for (auto* e : {&evFork, &evPrep, &evSobel, &evOrb, &evCrit, &evBlur})
+        for (auto* e : {&evFork, &evPrep, &evSobel, &evOrb, &evCrit, &evBlur, &evGate})
             PLVI_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         fcap = p->nfeatures > 0 ? p->nfeatures : kKlCap;
         SCALE = (double)p->lsd_scale;  // LSDOptions::scale is float
@@ -500,10 +511,12 @@ struct LinePipeline {
         int rc = plvi_orb_extract_batch(orb, d_frames, nf, frame_stride, row_stride, lap0, lap1, aux[0]);
         if (waitBlur) plvi_orb_internal_blur_event(orb, nullptr);
         PLVI_CHECK(hipEventRecord(evOrb, aux[0]));
-        PLVI_CHECK(hipStreamWaitEvent(aux[1], auxStart, 0));
+        if (waitBlur && !rc) PLVI_CHECK(hipStreamWaitEvent(crit, evBlur, 0));
+        // evGate: everything region growing waits for (the prep, blur + FAST)
+        PLVI_CHECK(hipEventRecord(evGate, crit));
+        PLVI_CHECK(hipStreamWaitEvent(aux[1], sobelWithGrow ? evGate : auxStart, 0));
         if (!rc) rc = launch_sobel(d_frames, nf, frame_stride, row_stride, aux[1]);
         PLVI_CHECK(hipEventRecord(evSobel, aux[1]));
-        if (waitBlur && !rc) PLVI_CHECK(hipStreamWaitEvent(crit, evBlur, 0));
         launch_grow_assemble(nf, crit);
         PLVI_CHECK(hipStreamWaitEvent(crit, evSobel, 0));
         launch_describe(nf, crit);
