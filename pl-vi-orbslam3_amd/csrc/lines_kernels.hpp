@@ -363,7 +363,7 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
                                                       double prec, LsdRegion* __restrict__ regs, unsigned* __restrict__ regpts,
                                                       size_t regpts_frame, int* __restrict__ nlines,
                                                       int* __restrict__ err, int R, int RB, int QL, int nOct,
-                                                      unsigned long long* __restrict__ stats) {
+                                                      int oBase, int oCount, unsigned long long* __restrict__ stats) {
     extern __shared__ __align__(16) unsigned lds_u[];
     // latency-bound serial chain: win the SIMD arbiter against co-resident
     // throughput kernels (ORB / LBD on the other stream)
@@ -372,8 +372,9 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
     // octave 1.  Blocks are dealt round-robin over the 8 XCDs, so every XCD
     // gets the same mix (a (nOct, nf) grid put every octave-0 task on the
     // even XCDs) and the heavy tasks are dispatched first.
-    const int nf = gridDim.x / nOct;
-    const int o = blockIdx.x / nf, f = blockIdx.x - o * nf;
+    // this launch covers octaves oBase .. oBase + oCount - 1
+    const int nf = gridDim.x / oCount;
+    const int o = oBase + blockIdx.x / nf, f = blockIdx.x - (o - oBase) * nf;
     const LineOctDev& od = octs[o];
     const int sw = od.sw, sh = od.sh;
     const int lane = threadIdx.x;

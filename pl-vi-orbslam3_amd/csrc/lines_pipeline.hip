@@ -70,9 +70,10 @@ struct LinePipeline {
     hipStream_t stream = nullptr;
     hipStream_t aux[2] = {nullptr, nullptr};  // frame mode: ORB and LBD-Sobel streams
     hipEvent_t evFork = nullptr, evPrep = nullptr, evSobel = nullptr, evOrb = nullptr, evCrit = nullptr,
-               evBlur = nullptr, evGate = nullptr;
-    bool growAfterBlur = true, sobelWithGrow = false;
+               evBlur = nullptr, evGate = nullptr, evGrow2 = nullptr;
+    bool growAfterBlur = true, sobelWithGrow = false, growSplit = false;
     hipStream_t critStream = nullptr;  // frame schedule: prep -> grow -> describe
+    hipStream_t crit2 = nullptr;       // frame schedule: octave-1 region growing (split mode)
     bool orbAfterPrep = false;
     std::vector<LineOctDev> oct;
     std::vector<float> scaleF, invScaleF;
@@ -119,9 +120,10 @@ struct LinePipeline {
     ~LinePipeline() {
         for (auto e : kev) (void)hipEventDestroy(e);
         for (auto e : evs) (void)hipEventDestroy(e);
-        for (auto e : {evFork, evPrep, evSobel, evOrb, evCrit, evBlur, evGate})
+        for (auto e : {evFork, evPrep, evSobel, evOrb, evCrit, evBlur, evGate, evGrow2})
             if (e) (void)hipEventDestroy(e);
         if (critStream) (void)hipStreamDestroy(critStream);
+        if (crit2) (void)hipStreamDestroy(crit2);
         for (auto a : aux)
             if (a) (void)hipStreamDestroy(a);
         if (stream) (void)hipStreamDestroy(stream);
@@ -165,8 +167,14 @@ struct LinePipeline {
             const char* e5 = getenv("PLVI_SOBEL_WITH_GROW");
             sobelWithGrow = !e5 || atoi(e5) != 0;
             if (prio) PLVI_CHECK(hipStreamCreateWithPriority(&critStream, hipStreamNonBlocking, greatest));
+            if (prio) PLVI_CHECK(hipStreamCreateWithPriority(&crit2, hipStreamNonBlocking, greatest));
+            // PLVI_GROW_SPLIT=1: octave 0 grows right after the prep, octave 1
+            // after blur + FAST (batches from 1024 frames; +1 % in a 3-way
+            // sweep, within run-to-run noise, so off by default)
+            const char* e6 = getenv("PLVI_GROW_SPLIT");
+            growSplit = e6 && atoi(e6) != 0;
         }
-        for (auto* e : {&evFork, &evPrep, &evSobel, &evOrb, &evCrit, &evBlur, &evGate})
+        for (auto* e : {&evFork, &evPrep, &evSobel, &evOrb, &evCrit, &evBlur, &evGate, &evGrow2})
             PLVI_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         fcap = p->nfeatures > 0 ? p->nfeatures : kKlCap;
         SCALE = (double)p->lsd_scale;  // LSDOptions::scale is float
@@ -416,13 +424,18 @@ struct LinePipeline {
     }
 
     // Phase B: region growing (LK3) + keyline assembly / top-k (LK4).
-    void launch_grow_assemble(int nf, hipStream_t st) {
+    // region growing of octaves [oBase, oBase + oCount) (LK3)
+    void launch_grow(int nf, int oBase, int oCount, hipStream_t st) {
         auto growK = growStats ? lsd_grow_kernel<true> : lsd_grow_kernel<false>;
-        hipLaunchKernelGGL(growK, dim3(nOct * nf), dim3(64), growSmem, st, d_oct.as<LineOctDev>(),
+        hipLaunchKernelGGL(growK, dim3(oCount * nf), dim3(64), growSmem, st, d_oct.as<LineOctDev>(),
                            (const float*)pix.as<float>(), (const double*)modg.as<double>(),
                            (const float2*)seedcs.as<float2>(), gbits.as<unsigned>(), gbitsFrame,
                            qspill.as<unsigned>(), qspillFrame, prec, regs.as<LsdRegion>(), regpts.as<unsigned>(),
-                           qspillFrame, nlines.as<int>(), err.as<int>(), growR, growRB, growQL, nOct, growStats);
+                           qspillFrame, nlines.as<int>(), err.as<int>(), growR, growRB, growQL, nOct, oBase, oCount,
+                           growStats);
+    }
+    void launch_grow_assemble(int nf, hipStream_t st, bool grown = false) {
+        if (!grown) launch_grow(nf, 0, nOct, st);
         hipLaunchKernelGGL(lsd_rect_kernel, dim3(kRectBlocks, nOct, nf), dim3(256), 0, st, d_oct.as<LineOctDev>(),
                            (const double*)modg.as<double>(), (const LsdRegion*)regs.as<LsdRegion>(),
                            (const unsigned*)regpts.as<unsigned>(), qspillFrame, (const int*)nlines.as<int>(), prec,
@@ -511,13 +524,27 @@ struct LinePipeline {
         int rc = plvi_orb_extract_batch(orb, d_frames, nf, frame_stride, row_stride, lap0, lap1, aux[0]);
         if (waitBlur) plvi_orb_internal_blur_event(orb, nullptr);
         PLVI_CHECK(hipEventRecord(evOrb, aux[0]));
-        if (waitBlur && !rc) PLVI_CHECK(hipStreamWaitEvent(crit, evBlur, 0));
-        // evGate: everything region growing waits for (the prep, blur + FAST)
-        PLVI_CHECK(hipEventRecord(evGate, crit));
+        // split: octave 0 (the long waves, 3 per SIMD at 3072 frames) grows
+        // right after the prep and leaves room for the ORB pyramid and blur +
+        // FAST; the shorter octave-1 waves start after blur + FAST on crit2
+        const bool split = waitBlur && growSplit && nOct == 2 && crit2 && !rc;
+        hipStream_t gate = split ? crit2 : crit;
+        if (split) {
+            launch_grow(nf, 0, 1, crit);
+            PLVI_CHECK(hipStreamWaitEvent(crit2, evPrep, 0));
+        }
+        if (waitBlur && !rc) PLVI_CHECK(hipStreamWaitEvent(gate, evBlur, 0));
+        // evGate: everything the (last) region-growing launch waits for
+        PLVI_CHECK(hipEventRecord(evGate, gate));
         PLVI_CHECK(hipStreamWaitEvent(aux[1], sobelWithGrow ? evGate : auxStart, 0));
         if (!rc) rc = launch_sobel(d_frames, nf, frame_stride, row_stride, aux[1]);
         PLVI_CHECK(hipEventRecord(evSobel, aux[1]));
-        launch_grow_assemble(nf, crit);
+        if (split) {
+            launch_grow(nf, 1, 1, crit2);
+            PLVI_CHECK(hipEventRecord(evGrow2, crit2));
+            PLVI_CHECK(hipStreamWaitEvent(crit, evGrow2, 0));
+        }
+        launch_grow_assemble(nf, crit, split);
         PLVI_CHECK(hipStreamWaitEvent(crit, evSobel, 0));
         launch_describe(nf, crit);
         if (crit != st) {

@@ -45,7 +45,10 @@ __device__ __forceinline__ int reflect1(int p, int len) {
 // < 2^24: pixel x 2048 and (H >> 4) x 2048).
 // Limits: level-0 width <= 4 * 64 * kPyrDw, source widths <= 1024.
 // ---------------------------------------------------------------------------
-constexpr int kPyrAhead = 2, kPyrDw = 4, kPyrRing = 4, kPyrUnroll = 4, kPyrFrames = 4;
+#ifndef PLVI_PYR_FRAMES
+#define PLVI_PYR_FRAMES 4
+#endif
+constexpr int kPyrAhead = 2, kPyrDw = 4, kPyrRing = 4, kPyrUnroll = 4, kPyrFrames = PLVI_PYR_FRAMES;
 
 // packed column entry: sx (10 bits) | a0 (12 bits) << 10 | (a0 + a1 - 2047) (2 bits) << 22 | clampR << 24
 __host__ __device__ inline uint32_t pyr_xtab_pack(int sx, int a0, int a1, bool clampR) {

@@ -112,3 +112,33 @@ def test_frame_schedule_mixed_batch_vs_oracle():
         assert lcnt[i] == len(ekl), f"frame {i}: {lcnt[i]} lines vs {len(ekl)}"
         assert lkl[i * lcap:i * lcap + lcnt[i]].tobytes() == ekl.astype(plvi.KEYLINE_DTYPE).tobytes(), f"frame {i} lines"
         np.testing.assert_array_equal(ldesc[i * lcap:i * lcap + lcnt[i]], eld)
+
+
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_frame_schedule_large_batch_vs_oracle(monkeypatch, split):
+    """From 1024 frames on the schedule changes shape: region growing waits
+    for blur + FAST and (PLVI_GROW_SPLIT, default) octave 0 and octave 1 grow
+    as two launches on two streams.  Frames 0, 511 and 1023 of a 1024-frame
+    batch equal the oracle (ORB keypoints/descriptors, keylines/LBD)."""
+    import torch
+    monkeypatch.setenv("PLVI_GROW_SPLIT", split)
+    n = 1024
+    seq = synth.device_sequence(n, 640, 480, seed=12, device="cuda:0")
+    torch.cuda.synchronize()
+    orb = plvi.ORBextractor(1000, 1.2, 8, 20, 7, 640, 480, max_batch=n)
+    lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 640, 480, max_batch=n)
+    plvi.frame_extract_batch(orb, lx, seq.data_ptr(), n, 640 * 480, 640)
+    plvi.load().plvi_device_synchronize()
+    assert orb.errors() == 0 and lx.errors() == 0
+    ocnt, okp, odesc, ocap = _orb_out(orb, n)
+    lcnt, lkl, ldesc, lcap = _line_out(lx, n)
+    for i in (0, 511, 1023):
+        img = seq[i].cpu().numpy()
+        _, ekp, edesc = ol.orb_extract(img)
+        assert ocnt[i] == len(ekp), f"frame {i}"
+        assert okp[i * ocap:i * ocap + ocnt[i]].tobytes() == ekp.astype(plvi.KEYPOINT_DTYPE).tobytes()
+        np.testing.assert_array_equal(odesc[i * ocap:i * ocap + ocnt[i]], edesc)
+        ekl, eld, _ = ol.line_extract(img)
+        assert lcnt[i] == len(ekl), f"frame {i}"
+        assert lkl[i * lcap:i * lcap + lcnt[i]].tobytes() == ekl.astype(plvi.KEYLINE_DTYPE).tobytes()
+        np.testing.assert_array_equal(ldesc[i * lcap:i * lcap + lcnt[i]], eld)
