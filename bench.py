@@ -825,6 +825,78 @@ def extra_lines(args, torch, plvi, synth, lib, stream, W, H, seed0, orb, lx, ext
     if o64.errors(st) or l64.errors(st):
         raise RuntimeError("batch-64 device error flags")
     del o64, l64
+    # (1b) batch 64 with K batches in flight: K independent extractor slots
+    # (own tables and streams), step i on slot i % K over its own 64 frames;
+    # every step is the full 64-frame extract + match
+    K = 16
+    slots = []
+    for k in range(K):
+        sl_ = types.SimpleNamespace()
+        sl_.o = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=b64, device=dev)
+        sl_.l = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=b64, device=dev)
+        sl_.kp, sl_.de, sl_.co, _, _ = sl_.o.outputs()
+        _, sl_.lde, _, sl_.lco, _ = sl_.l.outputs()
+        sl_.o4 = [torch.empty((b64 - 1) * cap, **i32) for _ in range(4)]
+        sl_.lsc = torch.empty(4 * (b64 - 1) * 2 * lcap, **i32)
+        sl_.lm = torch.empty((b64 - 1) * lcap, **i32)
+        sl_.lnm = torch.empty(b64 - 1, **i32)
+        sl_.s = torch.cuda.Stream()
+        sl_.f = seq[(k * b64) % max(1, seq.shape[0] - b64)].data_ptr()
+        slots.append(sl_)
+
+    def step64k(i):
+        q = slots[i % K]
+        sq = q.s.cuda_stream
+        plvi.frame_extract_batch(q.o, q.l, q.f, b64, W * H, W, (0, 0), stream=sq)
+        rc = lib.plvi_hamming_knn2_batch(q.de + cap * 32, q.co + 4, cap, q.de, q.co, cap, b64 - 1,
+                                         *[o.data_ptr() for o in q.o4], sq)
+        rc |= lib.plvi_line_match_batch(q.lde + lcap * 32, q.lco + 4, lcap, q.lde, q.lco, lcap, b64 - 1, 0.9,
+                                        q.lsc.data_ptr(), q.lm.data_ptr(), q.lnm.data_ptr(), sq)
+        if rc:
+            raise RuntimeError("b64 pipelined match")
+    for i in range(K):
+        step64k(i)
+    torch.cuda.synchronize()
+    nk = 8 * K
+
+    def timed_steps(fn):
+        t0 = time.perf_counter()
+        for i in range(nk):
+            fn(i)
+        torch.cuda.synchronize()
+        return b64 * nk / (time.perf_counter() - t0)
+    v_api = timed_steps(step64k)
+    # the same step replayed from HIP graphs, one capture per slot; the graph
+    # holds the step on the slot's one stream (ORB extract, line extract,
+    # matches: the multi-stream frame schedule does not survive
+    # hipStreamEndCapture on this ROCm, a segfault inside the runtime), the
+    # 16 slots provide the concurrency
+    def step64g(q, sq):
+        q.o.extract_batch(q.f, b64, W * H, W, (0, 0), stream=sq)
+        q.l.extract_batch(q.f, b64, W * H, W, stream=sq)
+        rc = lib.plvi_hamming_knn2_batch(q.de + cap * 32, q.co + 4, cap, q.de, q.co, cap, b64 - 1,
+                                         *[o.data_ptr() for o in q.o4], sq)
+        rc |= lib.plvi_line_match_batch(q.lde + lcap * 32, q.lco + 4, lcap, q.lde, q.lco, lcap, b64 - 1, 0.9,
+                                        q.lsc.data_ptr(), q.lm.data_ptr(), q.lnm.data_ptr(), sq)
+        if rc:
+            raise RuntimeError("b64 graph match")
+    for q in slots:
+        q.g = plvi.StepGraph(lambda sq, q=q: step64g(q, sq), q.s.cuda_stream)
+    for q in slots:
+        q.g.launch()
+    torch.cuda.synchronize()
+    v_graph = timed_steps(lambda i: slots[i % K].g.launch())
+    out["batch64_in_flight"] = {
+        "value": max(v_api, v_graph), "unit": "frames/s", "batches_in_flight": K, "api_calls": v_api,
+        "hip_graphs": v_graph, "ms_per_batch_latency_floor": out["batch64"]["ms_per_step"],
+        "config": f"batch 64 per step, {K} independent batches in flight (own extractors and streams, "
+                  f"{K * b64} frames resident): the C1/C2 step as a stream of 64-frame batches; steps issued "
+                  f"call by call (frame schedule) and as one HIP-graph launch each (plvi_graph_*, the step "
+                  f"on one stream)"}
+    for q in slots:
+        if q.o.errors(q.s.cuda_stream) or q.l.errors(q.s.cuda_stream):
+            raise RuntimeError("pipelined batch-64 device error flags")
+    del slots
     # (2) single-frame latency: host image -> host tables, ORB || lines on two threads
     so = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, device=dev)
     sl = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, device=dev)

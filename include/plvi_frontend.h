@@ -620,6 +620,18 @@ int plvi_memcpy(void* dst, const void* src, size_t bytes, int kind);
 int plvi_memcpy_async(void* dst, const void* src, size_t bytes, int kind, void* stream);
 int plvi_device_synchronize(void);
 
+/* HIP graphs (no reference counterpart: a runtime facility of this
+ * library).  plvi_graph_capture_begin starts capturing `stream` (a created
+ * stream, not the null stream); every plvi_* call issued on it until
+ * plvi_graph_capture_end is recorded, not run, including the work the
+ * extractors fork to their own streams.  The captured step is instantiated
+ * into *graph_exec and replayed by plvi_graph_launch with the same device
+ * pointers and parameters; plvi_graph_destroy frees it. */
+int plvi_graph_capture_begin(void* stream);
+int plvi_graph_capture_end(void* stream, void** graph_exec);
+int plvi_graph_launch(void* graph_exec, void* stream);
+int plvi_graph_destroy(void* graph_exec);
+
 /* Device/library information for diagnostics. */
 const char* plvi_version(void);
 int plvi_device_count(void);

@@ -42,3 +42,36 @@ extern "C" int plvi_device_synchronize(void) {
     PLVI_CHECK(hipDeviceSynchronize());
     return PLVI_OK;
 }
+
+// HIP graphs: a batch step (any sequence of plvi_* calls on `stream`, their
+// internal streams joined by events) captured once and replayed with one
+// launch, which takes the per-call host work (~100 API calls per frame
+// schedule) off the path of small batches.
+extern "C" int plvi_graph_capture_begin(void* stream) {
+    if (!stream) return PLVI_E_BADARG;  // the legacy null stream cannot be captured
+    PLVI_CHECK(hipStreamBeginCapture((hipStream_t)stream, hipStreamCaptureModeRelaxed));
+    return PLVI_OK;
+}
+
+extern "C" int plvi_graph_capture_end(void* stream, void** graph_exec) {
+    if (!stream || !graph_exec) return PLVI_E_BADARG;
+    hipGraph_t g = nullptr;
+    PLVI_CHECK(hipStreamEndCapture((hipStream_t)stream, &g));
+    hipGraphExec_t e = nullptr;
+    const hipError_t rc = hipGraphInstantiate(&e, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (rc != hipSuccess) return PLVI_E_HIP;
+    *graph_exec = (void*)e;
+    return PLVI_OK;
+}
+
+extern "C" int plvi_graph_launch(void* graph_exec, void* stream) {
+    if (!graph_exec) return PLVI_E_BADARG;
+    PLVI_CHECK(hipGraphLaunch((hipGraphExec_t)graph_exec, (hipStream_t)stream));
+    return PLVI_OK;
+}
+
+extern "C" int plvi_graph_destroy(void* graph_exec) {
+    if (graph_exec) PLVI_CHECK(hipGraphExecDestroy((hipGraphExec_t)graph_exec));
+    return PLVI_OK;
+}

@@ -220,6 +220,10 @@ def _declare(lib):
         "plvi_memcpy": ([V, V, S, I], I),
         "plvi_memcpy_async": ([V, V, S, I, V], I),
         "plvi_device_synchronize": ([], I),
+        "plvi_graph_capture_begin": ([V], I),
+        "plvi_graph_capture_end": ([V, c_void_pp], I),
+        "plvi_graph_launch": ([V, V], I),
+        "plvi_graph_destroy": ([V], I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -770,6 +774,32 @@ def frame_extract_batch(orb, lines, d_frames_ptr, n_frames, frame_stride, row_st
     _check(load().plvi_frame_extract_batch(orb._h, lines._h, ctypes.c_void_p(d_frames_ptr), n_frames, frame_stride,
                                            row_stride, lap[0], lap[1], ctypes.c_void_p(stream or 0)),
            "plvi_frame_extract_batch")
+
+
+class StepGraph:
+    """A batch step captured into a HIP graph (plvi_graph_*): ``fn(stream)``
+    issues plvi_* calls on ``stream`` (a created stream); the graph replays
+    them with one launch.  The captured pointers and parameters are fixed."""
+
+    def __init__(self, fn, stream):
+        self._lib = load()
+        self._stream = stream
+        _check(self._lib.plvi_graph_capture_begin(ctypes.c_void_p(stream)), "plvi_graph_capture_begin")
+        try:
+            fn(stream)
+        finally:
+            ex = ctypes.c_void_p()
+            rc = self._lib.plvi_graph_capture_end(ctypes.c_void_p(stream), ctypes.byref(ex))
+        _check(rc, "plvi_graph_capture_end")
+        self._exec = ex
+
+    def launch(self, stream=None):
+        _check(self._lib.plvi_graph_launch(self._exec, ctypes.c_void_p(stream or self._stream)), "plvi_graph_launch")
+
+    def __del__(self):
+        if getattr(self, "_exec", None):
+            self._lib.plvi_graph_destroy(self._exec)
+            self._exec = None
 
 
 class ORBVocabulary:

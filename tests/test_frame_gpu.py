@@ -142,3 +142,43 @@ def test_frame_schedule_large_batch_vs_oracle(monkeypatch, split):
         assert lcnt[i] == len(ekl), f"frame {i}"
         assert lkl[i * lcap:i * lcap + lcnt[i]].tobytes() == ekl.astype(plvi.KEYLINE_DTYPE).tobytes()
         np.testing.assert_array_equal(ldesc[i * lcap:i * lcap + lcnt[i]], eld)
+
+
+def test_frame_step_hip_graph_replay():
+    """plvi_graph_*: a batch step on one stream (ORB extract, line extract,
+    kNN-2) captured into a HIP graph and replayed gives the same tables as
+    the step issued call by call.  (The multi-stream frame schedule is not
+    captured: hipStreamEndCapture segfaults on it in this ROCm,
+    tools/graph_probe.py.)"""
+    import torch
+    n = 16
+    seq = synth.device_sequence(n, 640, 480, seed=5, device="cuda:0")
+    torch.cuda.synchronize()
+    lib = plvi.load()
+    orb = plvi.ORBextractor(1000, 1.2, 8, 20, 7, 640, 480, max_batch=n)
+    lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 640, 480, max_batch=n)
+    kp, de, co, _, cap = orb.outputs()
+    s = torch.cuda.Stream()
+    outs = [torch.full(((n - 1) * cap,), -7, dtype=torch.int32, device="cuda:0") for _ in range(4)]
+
+    def step(st):
+        orb.extract_batch(seq.data_ptr(), n, 640 * 480, 640, stream=st)
+        lx.extract_batch(seq.data_ptr(), n, 640 * 480, 640, stream=st)
+        assert lib.plvi_hamming_knn2_batch(de + cap * 32, co + 4, cap, de, co, cap, n - 1,
+                                           *[o.data_ptr() for o in outs], st) == 0
+
+    step(s.cuda_stream)
+    torch.cuda.synchronize()
+    ref_o, ref_l = _orb_out(orb, n), _line_out(lx, n)
+    ref_m = [o.cpu().numpy().copy() for o in outs]
+    for o in outs:
+        o.fill_(-7)
+    g = plvi.StepGraph(step, s.cuda_stream)
+    g.launch()
+    g.launch()
+    torch.cuda.synchronize()
+    got_o, got_l = _orb_out(orb, n), _line_out(lx, n)
+    for a, b in zip(ref_o[:3] + ref_l[:3], got_o[:3] + got_l[:3]):
+        np.testing.assert_array_equal(a.view(np.uint8), b.view(np.uint8))
+    for a, o in zip(ref_m, outs):
+        np.testing.assert_array_equal(a, o.cpu().numpy())
