@@ -347,6 +347,10 @@ __device__ __forceinline__ void bits_load_rows(const GrowCtx& g, int r0, int r1,
     }
 }
 
+#ifndef PLVI_GROW_SETPRIO
+#define PLVI_GROW_SETPRIO 3  // wave priority of the region-growing waves (s_setprio)
+#endif
+
 // waves per SIMD the region-growing kernel is compiled for: 8 caps it at 64
 // VGPRs, so its 6 resident waves per SIMD (a 3072-frame batch) leave room for
 // the ORB / LBD waves of the frame schedule
@@ -367,7 +371,7 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
     extern __shared__ __align__(16) unsigned lds_u[];
     // latency-bound serial chain: win the SIMD arbiter against co-resident
     // throughput kernels (ORB / LBD on the other stream)
-    __builtin_amdgcn_s_setprio(3);
+    __builtin_amdgcn_s_setprio(PLVI_GROW_SETPRIO);
     // 1-D grid, octave-major: all octave-0 tasks (4x the pixels) first, then
     // octave 1.  Blocks are dealt round-robin over the 8 XCDs, so every XCD
     // gets the same mix (a (nOct, nf) grid put every octave-0 task on the
