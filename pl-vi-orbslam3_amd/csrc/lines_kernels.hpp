@@ -648,7 +648,10 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
 // order-free max/min reductions.  Emits the Vec4f of flsd (:506-518) at the
 // region's index.
 // ---------------------------------------------------------------------------
-constexpr int kRectBlocks = 32;  // 4-wave workgroups per (octave, frame); waves stride over the regions
+#ifndef PLVI_RECT_BLOCKS
+#define PLVI_RECT_BLOCKS 32
+#endif
+constexpr int kRectBlocks = PLVI_RECT_BLOCKS;  // 4-wave workgroups per (octave, frame); waves stride over the regions
 
 __global__ __launch_bounds__(256) void lsd_rect_kernel(const LineOctDev* __restrict__ octs,
                                                        const double* __restrict__ modgrad,
