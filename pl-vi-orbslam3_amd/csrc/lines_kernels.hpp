@@ -234,6 +234,10 @@ struct GrowCtx {
     int sw, sh, R, RB, wpr, wb, wbb, QL, ys;  // window bases wb (angles) / wbb (bits); ys = seed row
 };
 
+// set bits of m below this lane (v_mbcnt_lo/hi: popcount(m & ((1 << lane) - 1)))
+__device__ __forceinline__ int mbcnt64(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
 __device__ __forceinline__ unsigned gload_l2(unsigned* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -562,7 +566,7 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
                         // exact angle sequence of the speculated commits (sequential float
                         // sums); every lane keeps the sums after its cl accepted
                         // predecessors, i.e. the region angle its own test really sees
-                        const int cl = __popcll(A & below);
+                        const int cl = mbcnt64(A);
                         float sx2 = sumdx, sy2 = sumdy, pfx = sumdx, pfy = sumdy;
                         int t = 0;
                         for (unsigned long long mm = A; mm; mm &= mm - 1) {
@@ -591,7 +595,7 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
                             const bool mine = (C >> lane) & 1ull;
                             if (mine) {
                                 used_set(g, nx, ny);
-                                q_put(g, reg_size + __popcll(C & below), (unsigned)nx | ((unsigned)ny << 16));
+                                q_put(g, reg_size + mbcnt64(C), (unsigned)nx | ((unsigned)ny << 16));
                             }
                             // global USED bits / queue spill must land before they are read back
                             if (__ballot(mine && ny >= g.wbb + RB) || reg_size + nc > QL) vm_drain();
