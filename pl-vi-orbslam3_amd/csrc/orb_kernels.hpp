@@ -639,7 +639,8 @@ __global__ __launch_bounds__(64) void orb_cell_nms_kernel(const OrbCellDev* __re
 constexpr int kSatRowsPerWave = 8;
 
 // One wave per (strip, level, frame): lane = column, rows top-down, 8 rows'
-// loads in flight; wave prefix scan per row, running column sums.
+// loads in flight; per row a ballot gives the prefix counts (v_mbcnt) and the
+// row total (popcount) without any cross-lane scan; running column sums.
 __global__ __launch_bounds__(64) void orb_sat_strip_kernel(const OrbLevelDev* __restrict__ lvs,
                                                            const uint8_t* __restrict__ cand,
                                                            unsigned short* __restrict__ lsat, int* __restrict__ carry) {
@@ -663,14 +664,11 @@ __global__ __launch_bounds__(64) void orb_sat_strip_kernel(const OrbLevelDev* __
         }
 #pragma unroll
         for (int k = 0; k < kSatRowsPerWave; ++k) {
-            int t = v[k];
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int nb = __shfl_up(t, o);
-                if (lane >= o) t += nb;
-            }
-            colacc += t - v[k];  // candidates of this row left of x within the strip
-            tot += __shfl(t, 63);
+            // the row's indicator as a wave mask: candidates left of x within the
+            // strip = set bits below this lane (v_mbcnt), the row total = popcount
+            const unsigned long long m = __ballot(v[k] != 0);
+            colacc += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+            tot += __popcll(m);
             const int y = y0 + k;
             if (y <= L.rh) {
                 base[(size_t)y * pitch + x] = (unsigned short)colacc;
