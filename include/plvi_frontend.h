@@ -224,6 +224,14 @@ int plvi_lines_profile(plvi_line_extractor* h, int enable);
  * per (frame, octave) 16 uint64 = [total, pop-prep, commit rounds, rect,
  * seeds, pops, commits, rect points, slow-path loads]; NULL disables. */
 int plvi_lines_debug_stats(plvi_line_extractor* h, unsigned long long* d_stats);
+/* Diagnostic counters of the multi-wave (small-batch) region-growing kernel:
+ * per (frame, octave) 16 int32 = [regions dispatched speculatively, dropped,
+ * regrown after a failed validation, grown exactly by the walk (never
+ * dispatched), trivial seeds, speculative regions committed, walk cycles,
+ * walker growth cycles, walk entries, walks blocked on a growing head seed,
+ * kernel cycles, speculative growth cycles, idle polls, 0, 0, 0]; NULL
+ * disables.  Batches up to PLVI_GROW_MW frames (default 256) take that kernel. */
+int plvi_lines_debug_mw_stats(plvi_line_extractor* h, int* d_stats);
 /* Diagnostic: LSD planes of the last batch for one (frame, octave), copied to
  * host: angle in degrees (float, NOTDEF = -1024), modgrad (f64), cos/sin
  * pairs (float2, defined pixels only); any pointer may be NULL. */

@@ -14,6 +14,7 @@
 
 #include "lines_device.h"
 #include "lines_kernels.hpp"
+#include "lsd_grow_mw.hpp"
 #include "plvi_common.h"
 
 // internal hook of the ORB pipeline (orb_pipeline.hip): event after the blur + FAST launch
@@ -81,7 +82,7 @@ struct LinePipeline {
     double gk[7]{};
     int lbdTaps[3] = {14, 62, 104};
     DevBuf d_oct, d_tabs, octImg, pix, modg, seedcs, gbits, qspill, regs, regpts, rawLines, nlines, klTmp, klOut, fnOut, cntOut, descOut, lbdBlur,
-        lbdG, err, staging;
+        lbdG, err, staging, mwOwn, mwSlot;
     size_t qspillFrame = 0, gbitsFrame = 0, lbdPlaneTotal = 0;
     int lastFrames = 0;
     static constexpr int kStages = 5, kRing = 512;
@@ -357,8 +358,40 @@ struct LinePipeline {
         if (growSmem > 160 * 1024) return PLVI_E_BADARG;
         for (const void* k : {(const void*)lsd_grow_kernel<false>, (const void*)lsd_grow_kernel<true>})
             PLVI_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)growSmem));
+        // Small batches (latency): lsd_grow_mw_kernel, kMwWaves waves per
+        // (frame, octave) growing regions of one frame concurrently.
+        // PLVI_GROW_MW = largest batch that takes it (default 256; 0 = off).
+        mwMaxFrames = 256;
+        if (const char* e = getenv("PLVI_GROW_MW")) mwMaxFrames = atoi(e);
+        mwMaxFrames = std::min(mwMaxFrames, Bcap);
+        if (mwMaxFrames > 0) {
+            const size_t nwords = gbitsFrame;  // max over octaves of sh * wpr
+            constexpr int NS = kMwWaves * kMwSlotsPerWave;
+            const size_t fixedMw = sizeof(MwCtl) + NS * sizeof(MwSlot) +
+                                   4 * (3 * nwords + (size_t)kMwWaves * kMwRB * wprMax + kMwXQ);
+            mwSQ = 256;
+            while (mwSQ > 32 && fixedMw + 4 * (size_t)NS * mwSQ > 160 * 1024) mwSQ /= 2;
+            mwSmem = fixedMw + 4 * (size_t)NS * mwSQ;
+            if (mwSmem > 160 * 1024) {
+                mwMaxFrames = 0;  // frame too large for the LDS bitmaps: sequential kernel only
+            } else {
+                const size_t tasks = (size_t)mwMaxFrames * nOct;
+                mwOwnTask = (size_t)kMwWaves * gbitsFrame;
+                if (mwOwn.alloc(sizeof(unsigned) * mwOwnTask * tasks) ||
+                    mwSlot.alloc(sizeof(unsigned) * (size_t)NS * kMwSlotSpill * tasks))
+                    return PLVI_E_HIP;
+                PLVI_CHECK(hipMemset(mwOwn.p, 0, mwOwn.bytes));  // kept zero by every launch
+                for (const void* k : {(const void*)lsd_grow_mw_kernel<kMwWaves, false>,
+                                      (const void*)lsd_grow_mw_kernel<kMwWaves, true>})
+                    PLVI_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mwSmem));
+            }
+        }
         return PLVI_OK;
     }
+    static constexpr int kMwWaves = 16;
+    int mwMaxFrames = 0, mwSQ = 0;
+    size_t mwSmem = 0, mwOwnTask = 0;
+    int* mwStats = nullptr;  // diagnostic counters (plvi_lines_debug_mw_stats)
     size_t growSmem = 0;
     int growR = 0, growRB = 0, growQL = 0;
     unsigned long long* growStats = nullptr;  // diagnostic cycle counters (plvi_lines_debug_stats)
@@ -426,6 +459,15 @@ struct LinePipeline {
     // Phase B: region growing (LK3) + keyline assembly / top-k (LK4).
     // region growing of octaves [oBase, oBase + oCount) (LK3)
     void launch_grow(int nf, int oBase, int oCount, hipStream_t st) {
+        if (nf <= mwMaxFrames) {
+            auto mwK = mwStats ? lsd_grow_mw_kernel<kMwWaves, true> : lsd_grow_mw_kernel<kMwWaves, false>;
+            hipLaunchKernelGGL(mwK, dim3(oCount * nf), dim3(kMwWaves * 64), mwSmem, st, d_oct.as<LineOctDev>(),
+                               (const float*)pix.as<float>(), (const float2*)seedcs.as<float2>(),
+                               mwOwn.as<unsigned>(), mwOwnTask, mwSlot.as<unsigned>(), qspill.as<unsigned>(),
+                               qspillFrame, prec, regs.as<LsdRegion>(), regpts.as<unsigned>(), qspillFrame,
+                               nlines.as<int>(), err.as<int>(), mwSQ, nOct, oBase, oCount, mwStats);
+            return;
+        }
         auto growK = growStats ? lsd_grow_kernel<true> : lsd_grow_kernel<false>;
         hipLaunchKernelGGL(growK, dim3(oCount * nf), dim3(64), growSmem, st, d_oct.as<LineOctDev>(),
                            (const float*)pix.as<float>(), (const double*)modg.as<double>(),
@@ -710,6 +752,15 @@ extern "C" int plvi_lines_profile_read(plvi_line_extractor* h, float* stage_ms, 
 extern "C" int plvi_lines_debug_stats(plvi_line_extractor* h, unsigned long long* d_stats) {
     if (!h) return PLVI_E_BADARG;
     h->p().growStats = d_stats;
+    return PLVI_OK;
+}
+
+// Diagnostic: counters of the multi-wave region-growing kernel per (frame,
+// octave): 16 ints (plvi_frontend.h) into a caller-provided device buffer
+// (NULL disables).
+extern "C" int plvi_lines_debug_mw_stats(plvi_line_extractor* h, int* d_stats) {
+    if (!h) return PLVI_E_BADARG;
+    h->p().mwStats = d_stats;
     return PLVI_OK;
 }
 

@@ -1,0 +1,613 @@
+// lsd_grow_mw.hpp — LK3 for small batches (latency): flsd's region loop
+// (lsd.cpp:476-533, region_grow :635-686) with SEVERAL regions of ONE frame
+// growing at once, bit-exact with the sequential raster-order loop.
+//
+// One workgroup of NW waves per (frame, octave).  Seeds are resolved in
+// raster order by a single "walk" (the lock holder); the other waves grow
+// regions speculatively ahead of it:
+//
+//  * A region grown from seed s only depends on the USED state of the pixels
+//    it tests.  Every defined pixel before s (raster order) is USED when flsd
+//    reaches s, so a speculative region treats them as USED; for pixels after
+//    s it sees the committed bitmap C (regions already walked) and its own
+//    marks.  Earlier regions can only ADD USED pixels, so the region is exactly
+//    the reference's iff none of the pixels it accepted is in C when the walk
+//    reaches s (validation); otherwise the walker regrows it exactly (all
+//    earlier regions are then committed).
+//  * The walk goes over the pixels after the last committed seed: committed /
+//    NOTDEF pixels (C) are skipped, "trivial" seeds (no forward neighbour
+//    aligned with the seed angle: a static property, the region is the seed
+//    alone, T) are committed in place, any other seed takes its speculative
+//    region (validated) or is grown exactly by the walker when no wave has it.
+//  * Waves pick the next seed after a shared cursor that is neither in C, T
+//    nor claimed by any region so far (H, a hint: skipped seeds are found by
+//    the walk).  A speculative region whose seed the walk passed is dropped.
+//
+// LDS: C, T, H (whole frame, one bit per pixel), per wave an own-mark window
+// of RB rows from the seed row (rows below it spill to a global bitmap), per
+// region slot a queue of SQ entries (spill to global), the walker's exact
+// queue (spill to the qspill plane).  Commit order = raster seed order, so the
+// region list handed to lsd_rect_kernel is the sequential kernel's.
+// ---------------------------------------------------------------------------
+#pragma once
+
+namespace plvi {
+
+constexpr int kMwSlotsPerWave = 2;
+constexpr int kMwRB = 32;          // own-mark window rows
+constexpr int kMwSlotSpill = 4096; // global queue entries per slot beyond the LDS part
+constexpr int kMwXQ = 256;         // LDS entries of the walker's exact queue
+
+enum : int { kMwFree = 0, kMwGrowing = 1, kMwDone = 2, kMwBusy = 3 };
+
+struct MwSlot {
+    int seed;   // bit index y * (wpr * 32) + x
+    int state;  // kMw*
+    int n;      // region size
+    float deg;  // final region angle (float degrees)
+    int ovf;    // queue overflow: the walker regrows it
+    int pad[3];
+};
+// control block (LDS)
+struct MwCtl {
+    int lock, dlock, head, cursor, finished, npts, nout, overflow;
+    int stat[16];  // [0] dispatched [1] dropped [2] regrown [3] exact (undispatched) [4] trivial [5] committed
+                   // speculative [6] walk cycles [7] walker growth cycles [8] walk entries [9] blocked on a
+                   // growing head [10] kernel cycles (wave 0) [11] speculative growth cycles (sum over waves)
+                   // [12] idle polls
+};
+
+typedef MwSlot __attribute__((address_space(3))) lds_slot;
+typedef MwCtl __attribute__((address_space(3))) lds_ctl;
+
+struct MwQueue {
+    lds_u32* lq;
+    int lcap;
+    unsigned* gq;
+    int gcap;
+};
+
+struct MwEnv {
+    const float* P;    // angle plane (degrees, NOTDEF = -1024)
+    const float2* SC;  // cosf / sinf of float(angle)
+    lds_u32* C;        // committed or NOTDEF
+    lds_u32* T;        // trivial seeds
+    lds_u32* H;        // claimed by some region (dispatch hint)
+    lds_u32* own;      // this wave's own-mark window (RB rows x wpr)
+    unsigned* ownG;    // this wave's own-mark spill (sh x wpr)
+    lds_ctl* ctl;
+    int sw, sh, wpr, rowbits;  // rowbits = wpr * 32
+    float pdeg;
+    double prec;
+};
+
+__device__ __forceinline__ unsigned mw_word(const lds_u32* B, int wpr, int x, int y) { return B[y * wpr + (x >> 5)]; }
+__device__ __forceinline__ bool mw_bit(const lds_u32* B, int wpr, int x, int y) {
+    return (mw_word(B, wpr, x, y) >> (x & 31)) & 1u;
+}
+__device__ __forceinline__ void mw_or(lds_u32* B, int wpr, int x, int y) {
+    __atomic_fetch_or(&B[y * wpr + (x >> 5)], 1u << (x & 31), __ATOMIC_RELAXED);
+}
+__device__ __forceinline__ bool mw_own_get(const MwEnv& E, int x, int y, int sy) {
+    const bool inwin = y < sy + kMwRB;
+    const int yy = inwin ? y - sy : 0;
+    unsigned v = E.own[yy * E.wpr + (x >> 5)];
+    if (__builtin_expect(!inwin, 0)) v = gload_l2(E.ownG + (size_t)y * E.wpr + (x >> 5));
+    return (v >> (x & 31)) & 1u;
+}
+__device__ __forceinline__ void mw_own_set(const MwEnv& E, int x, int y, int sy) {
+    const unsigned b = 1u << (x & 31);
+    if (__builtin_expect(y < sy + kMwRB, 1)) __atomic_fetch_or(&E.own[(y - sy) * E.wpr + (x >> 5)], b, __ATOMIC_RELAXED);
+    else __hip_atomic_fetch_or(E.ownG + (size_t)y * E.wpr + (x >> 5), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned mw_qget(const MwQueue& Q, int i) {
+    if (__builtin_expect(i < Q.lcap, 1)) return Q.lq[i];
+    return gload_l2(Q.gq + (i - Q.lcap));
+}
+__device__ __forceinline__ void mw_qput(const MwQueue& Q, int i, unsigned v) {
+    if (__builtin_expect(i < Q.lcap, 1)) Q.lq[i] = v;
+    else gstore_l2(Q.gq + (i - Q.lcap), v);
+}
+__device__ __forceinline__ void mw_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+__device__ __forceinline__ int mw_lds_load(lds_i32* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void mw_lds_store(lds_i32* p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// wave-uniform try-lock (lane 0 does the CAS)
+__device__ __forceinline__ void mw_stat(lds_ctl* c, int i, int v) {
+    __hip_atomic_fetch_add(&c->stat[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ bool mw_try_lock(lds_i32* l, int lane) {
+    int got = 0;
+    if (lane == 0) {
+        int e = 0;
+        got = __hip_atomic_compare_exchange_strong(l, &e, 1, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_WORKGROUP) ? 1 : 0;
+    }
+    got = __builtin_amdgcn_readfirstlane(got);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    return got != 0;
+}
+__device__ __forceinline__ void mw_unlock(lds_i32* l, int lane) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (lane == 0) __hip_atomic_store(l, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Grow the region of seed (sx, sy) into Q (region_grow, lsd.cpp:635-686).
+// SPEC: abandon when the walk passes the seed.  Returns 0 = grown, 1 =
+// abandoned, 2 = queue overflow; n = points in Q (own marks set for them).
+template <bool SPEC>
+__device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_out, float& deg_out, bool& spilled,
+                       int lane) {
+    const int sw = E.sw, sh = E.sh;
+    const int seedb = sy * E.rowbits + sx;
+    const float pdeg = E.pdeg;
+    const double prec = E.prec;
+    const int bp = lane / 9, bk = lane % 9;
+    const int kdx = bk % 3 - 1, kdy = bk / 3 - 1;
+    float reg_deg = E.P[(size_t)sy * sw + sx];
+    float sumdx, sumdy;
+    {
+        double ds, dc;
+        plvi_sincos((double)reg_deg * kD2R, &ds, &dc);
+        sumdx = (float)dc;
+        sumdy = (float)ds;
+    }
+    if (lane == 0) {
+        mw_own_set(E, sx, sy, sy);
+        mw_or(E.H, E.wpr, sx, sy);
+        Q.lq[0] = (unsigned)sx | ((unsigned)sy << 16);
+    }
+    mw_wave_sync();
+    spilled = false;
+    int reg_size = 1;
+    const int cap = Q.lcap + Q.gcap;
+    for (int i = 0; i < reg_size;) {
+        if (SPEC && mw_lds_load(&E.ctl->head) > seedb) {
+            n_out = reg_size;
+            deg_out = reg_deg;
+            return 1;
+        }
+        const int nb = min(7, reg_size - i);
+        const bool active = lane < 9 * nb;
+        const unsigned pv = active ? mw_qget(Q, i + bp) : 0u;
+        const int px = (int)(pv & 0xffffu), py = (int)(pv >> 16);
+        const int nx = px + kdx, ny = py + kdy;
+        // pixels before the seed in raster order are USED when flsd reaches it
+        const bool valid = active && nx >= 0 && nx < sw && ny < sh && (ny > sy || (ny == sy && nx >= sx));
+        float deg = kNotdefF, cc = 0.f, ss = 0.f;
+        if (valid) {
+            const float2 cs2 = E.SC[(size_t)ny * sw + nx];
+            deg = E.P[(size_t)ny * sw + nx];
+            cc = cs2.x;
+            ss = cs2.y;
+        }
+        unsigned long long dup = 0;
+        for (int p2 = 0; p2 < nb - 1; ++p2) {
+            const unsigned q2 = (unsigned)readlane_i((int)pv, 9 * p2);
+            const int ddx = nx - (int)(q2 & 0xffffu) + 1, ddy = ny - (int)(q2 >> 16) + 1;
+            if (p2 < bp && ddx >= 0 && ddx <= 2 && ddy >= 0 && ddy <= 2) dup |= 1ull << (9 * p2 + ddy * 3 + ddx);
+        }
+        // own marks and the committed bitmap, read once per block (within the
+        // block a lane's pixel only changes through an earlier lane's commit
+        // of the same pixel: dup / Ccum)
+        const bool live0 = valid && deg != kNotdefF && !mw_bit(E.C, E.wpr, nx, ny) && !mw_own_get(E, nx, ny, sy);
+        unsigned long long Ccum = 0;
+        int start = 0;
+        while (start < 9 * nb) {
+            const unsigned long long fromStart = ~0ull << start;
+            const bool candl = lane >= start && live0 && (dup & Ccum) == 0ull;
+            const bool al = candl && is_aligned_fast(deg, reg_deg, pdeg, prec);
+            const bool acc = al && (dup & fromStart) == 0ull;
+            const unsigned long long A = __ballot(acc);
+            if (!A) break;
+            const int cl = mbcnt64(A);
+            float sx2 = sumdx, sy2 = sumdy, pfx = sumdx, pfy = sumdy;
+            int t = 0;
+            for (unsigned long long mm = A; mm; mm &= mm - 1) {
+                const int bl = __ffsll((long long)mm) - 1;
+                sx2 += readlane_f(cc, bl);
+                sy2 += readlane_f(ss, bl);
+                ++t;
+                if (cl == t) {
+                    pfx = sx2;
+                    pfy = sy2;
+                }
+            }
+            const float tha = plvi_fast_atan2(pfy, pfx);
+            const float th = cl > 0 ? tha : reg_deg;
+            const bool al2 = candl && (dup & A) == 0ull && is_aligned_fast(deg, th, pdeg, prec);
+            const unsigned long long mism = __ballot(al2 != acc) & fromStart;
+            const int ls = mism ? __ffsll((long long)mism) - 1 : 63;
+            const unsigned long long Cm = A & ((1ull << ls) - 1ull);
+            const int nc = __popcll(Cm);
+            start = mism ? ls : 9 * nb;
+            if (nc > 0) {
+                if (reg_size + nc > cap) {  // the slot queue is full: the walker regrows it exactly
+                    n_out = reg_size;
+                    deg_out = reg_deg;
+                    return 2;
+                }
+                Ccum |= Cm;
+                const bool mine = (Cm >> lane) & 1ull;
+                if (mine) {
+                    mw_own_set(E, nx, ny, sy);
+                    mw_or(E.H, E.wpr, nx, ny);
+                    mw_qput(Q, reg_size + mbcnt64(Cm), (unsigned)nx | ((unsigned)ny << 16));
+                }
+                const bool sp = __ballot(mine && ny >= sy + kMwRB) != 0ull;
+                spilled |= sp;
+                if (sp || reg_size + nc > Q.lcap) vm_drain();
+                reg_size += nc;
+                sumdx = readlane_f(pfx, ls);
+                sumdy = readlane_f(pfy, ls);
+                reg_deg = readlane_f(th, ls);
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+        i += nb;
+    }
+    n_out = reg_size;
+    deg_out = reg_deg;
+    return 0;
+}
+
+// Clear the own marks of a region grown from row sy (n points in Q).
+__device__ __forceinline__ void mw_own_clear(const MwEnv& E, int sy, const MwQueue& Q, int n, bool spilled, int lane) {
+    mw_wave_sync();
+    for (int k = lane; k < kMwRB * E.wpr; k += 64) E.own[k] = 0u;
+    if (spilled) {
+        for (int j = lane; j < n; j += 64) {
+            const unsigned v = mw_qget(Q, j);
+            const int x = (int)(v & 0xffffu), y = (int)(v >> 16);
+            if (y >= sy + kMwRB) gstore_l2(E.ownG + (size_t)y * E.wpr + (x >> 5), 0u);
+        }
+        vm_drain();
+    }
+    mw_wave_sync();
+}
+
+// The walk (lock holder): resolve seeds from ctl->head in raster order.
+// Returns when the next seed's region is still growing (or all are done).
+template <int NW, bool STATS>
+__device__ void mw_walk(const MwEnv& E, lds_slot* slots, lds_u32* slotq, unsigned* slotspill, int SQ, lds_u32* xq,
+                        unsigned* xspill, int xgcap, int min_reg, LsdRegion* outR, unsigned* outP, int lane) {
+    lds_ctl* ctl = E.ctl;
+    const int nwords = E.sh * E.wpr;
+    const int rowbits = E.rowbits;
+    int head = ctl->head;
+    while (true) {
+        // next unresolved pixel >= head: first zero bit of C
+        int w = head >> 5;
+        if (w >= nwords) break;
+        unsigned m = ~E.C[w] & (~0u << (head & 31));
+        if (!m) {
+            // wave-parallel scan of the following words
+            int found = -1;
+            for (int w0 = w + 1; w0 < nwords && found < 0; w0 += 64) {
+                const int ww = w0 + lane;
+                const bool nz = ww < nwords && ~E.C[ww] != 0u;
+                const unsigned long long b = __ballot(nz);
+                if (b) found = w0 + __ffsll((long long)b) - 1;
+            }
+            if (found < 0) {
+                head = nwords * 32;
+                break;
+            }
+            w = found;
+            m = ~E.C[w];
+        }
+        // trivial seeds before the first non-trivial one are committed in place
+        const unsigned tw = E.T[w];
+        const unsigned nt = m & ~tw;
+        const unsigned run = nt ? (m & tw & ((nt & (0u - nt)) - 1u)) : (m & tw);
+        if (run) {
+            if (lane == 0) {
+                __atomic_fetch_or(&E.C[w], run, __ATOMIC_RELAXED);
+                mw_stat(ctl, 4, __popc(run));
+            }
+            mw_wave_sync();
+        }
+        if (!nt) {
+            head = (w + 1) * 32;
+            continue;
+        }
+        const int q = w * 32 + (__ffs((int)nt) - 1);
+        head = q;
+        const int qx = q % rowbits, qy = q / rowbits;
+        // the slot holding seed q, if any
+        int si = -1, sst = kMwFree;
+        {
+            const bool hit = lane < NW * kMwSlotsPerWave && mw_lds_load(&slots[lane].state) != kMwFree &&
+                             slots[lane].seed == q;
+            const unsigned long long b = __ballot(hit);
+            if (b) {
+                si = __ffsll((long long)b) - 1;
+                sst = mw_lds_load(&slots[si].state);
+            }
+        }
+        if (si >= 0 && sst == kMwGrowing) {  // wait for it
+            if (STATS && lane == 0) mw_stat(ctl, 9, 1);
+            break;
+        }
+        bool use_slot = false;
+        int n = 0;
+        float deg = 0.f;
+        MwQueue Q;
+        if (si >= 0 && sst == kMwDone) {
+            // take it (its wave may drop it only once the walk has passed q)
+            int ok = 0;
+            if (lane == 0) {
+                int e = kMwDone;
+                ok = __hip_atomic_compare_exchange_strong(&slots[si].state, &e, kMwBusy, __ATOMIC_ACQUIRE,
+                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ? 1 : 0;
+            }
+            ok = __builtin_amdgcn_readfirstlane(ok);
+            if (ok) {
+                Q = MwQueue{slotq + si * SQ, SQ, slotspill + (size_t)si * kMwSlotSpill, kMwSlotSpill};
+                n = slots[si].n;
+                deg = slots[si].deg;
+                bool valid = slots[si].ovf == 0;
+                if (valid) {
+                    bool bad = false;
+                    for (int j = lane; j < n; j += 64) {
+                        const unsigned v = mw_qget(Q, j);
+                        bad |= mw_bit(E.C, E.wpr, (int)(v & 0xffffu), (int)(v >> 16));
+                    }
+                    valid = __ballot(bad) == 0ull;
+                }
+                if (valid) {
+                    use_slot = true;
+                    if (lane == 0) mw_stat(ctl, 5, 1);
+                } else {
+                    if (lane == 0) mw_stat(ctl, 2, 1);
+                    mw_lds_store(&slots[si].state, kMwFree);
+                }
+            }
+        }
+        if (!use_slot) {
+            // exact growth: every earlier seed is committed
+            Q = MwQueue{xq, kMwXQ, xspill, xgcap};
+            bool spilled = false;
+            const unsigned long long tg0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
+            mw_grow<false>(E, qx, qy, Q, n, deg, spilled, lane);
+            mw_own_clear(E, qy, Q, n, spilled, lane);
+            if (STATS && lane == 0) mw_stat(ctl, 7, (int)(__builtin_amdgcn_s_memtime() - tg0));
+            if (lane == 0 && si < 0) mw_stat(ctl, 3, 1);
+        }
+        // commit: the region's pixels become USED for every later seed
+        for (int j = lane; j < n; j += 64) {
+            const unsigned v = mw_qget(Q, j);
+            mw_or(E.C, E.wpr, (int)(v & 0xffffu), (int)(v >> 16));
+        }
+        // region2rect input for lsd_rect_kernel (flsd :500-518 order)
+        if (n >= min_reg) {
+            const int nout = ctl->nout, npts = ctl->npts;
+            if (nout < kLsdRawCap) {
+                for (int j = lane; j < n; j += 64) outP[npts + j] = mw_qget(Q, j);
+                if (lane == 0) {
+                    outR[nout] = LsdRegion{npts, n, (double)deg * kD2R};
+                    ctl->npts = npts + n;
+                    ctl->nout = nout + 1;
+                }
+            } else if (lane == 0) {
+                ctl->overflow = 1;
+            }
+        }
+        mw_wave_sync();
+        if (use_slot) mw_lds_store(&slots[si].state, kMwFree);
+        head = q + 1;
+        if (lane == 0) mw_lds_store(&ctl->head, head);
+    }
+    if (lane == 0) {
+        mw_lds_store(&ctl->head, head);
+        if ((head >> 5) >= nwords) mw_lds_store(&ctl->finished, 1);
+    }
+    mw_wave_sync();
+}
+
+// Next seed for a speculative region: the first pixel after the cursor (and
+// the walk) that is neither committed / NOTDEF, trivial nor claimed.
+__device__ __forceinline__ int mw_dispatch(const MwEnv& E, int lane) {
+    lds_ctl* ctl = E.ctl;
+    const int nwords = E.sh * E.wpr;
+    const int head = mw_lds_load(&ctl->head);
+    int cur = max(ctl->cursor, head);
+    int w = cur >> 5;
+    if (w >= nwords) return -1;
+    unsigned m = ~(E.C[w] | E.T[w] | E.H[w]) & (~0u << (cur & 31));
+    if (!m) {
+        int found = -1;
+        for (int w0 = w + 1; w0 < nwords && found < 0; w0 += 64) {
+            const int ww = w0 + lane;
+            const bool nz = ww < nwords && (E.C[ww] | E.T[ww] | E.H[ww]) != ~0u;
+            const unsigned long long b = __ballot(nz);
+            if (b) found = w0 + __ffsll((long long)b) - 1;
+        }
+        if (found < 0) {
+            if (lane == 0) ctl->cursor = nwords * 32;
+            return -1;
+        }
+        w = found;
+        m = ~(E.C[w] | E.T[w] | E.H[w]);
+    }
+    const int q = w * 32 + (__ffs((int)m) - 1);
+    if (lane == 0) ctl->cursor = q + 1;
+    return q;
+}
+
+template <int NW, bool STATS>
+__global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
+    const LineOctDev* __restrict__ octs, const float* __restrict__ pix, const float2* __restrict__ pixcs,
+    unsigned* __restrict__ ownspill, size_t ownspill_task, unsigned* __restrict__ slotspill, unsigned* __restrict__ xspill,
+    size_t xspill_task, double prec, LsdRegion* __restrict__ regs, unsigned* __restrict__ regpts, size_t regpts_frame,
+    int* __restrict__ nlines, int* __restrict__ err, int SQ, int nOct, int oBase, int oCount,
+    int* __restrict__ stats) {
+    extern __shared__ __align__(16) unsigned lds_u[];
+    __builtin_amdgcn_s_setprio(PLVI_GROW_SETPRIO);
+    const int nf = gridDim.x / oCount;
+    const int o = oBase + blockIdx.x / nf, f = blockIdx.x - (o - oBase) * nf;
+    const int task = f * nOct + o;
+    const LineOctDev& od = octs[o];
+    const int sw = od.sw, sh = od.sh, wpr = (sw + 31) >> 5;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    constexpr int NS = NW * kMwSlotsPerWave;
+    // LDS carve-up
+    lds_ctl* ctl = (lds_ctl*)lds_u;
+    lds_slot* slots = (lds_slot*)(lds_u + sizeof(MwCtl) / 4);
+    lds_u32* base = (lds_u32*)(lds_u + sizeof(MwCtl) / 4 + NS * sizeof(MwSlot) / 4);
+    const int nwords = sh * wpr;
+    lds_u32* C = base;
+    lds_u32* T = C + nwords;
+    lds_u32* H = T + nwords;
+    lds_u32* ownAll = H + nwords;
+    lds_u32* slotq = ownAll + NW * kMwRB * wpr;
+    lds_u32* xq = slotq + NS * SQ;
+
+    MwEnv E;
+    E.P = pix + od.soff + (size_t)f * od.splane;
+    E.SC = pixcs + od.soff + (size_t)f * od.splane;
+    E.C = C; E.T = T; E.H = H;
+    E.own = ownAll + wv * kMwRB * wpr;
+    E.ownG = ownspill + (size_t)task * ownspill_task + (size_t)wv * sh * wpr;
+    E.ctl = ctl;
+    E.sw = sw; E.sh = sh; E.wpr = wpr; E.rowbits = wpr * 32;
+    E.pdeg = (float)(prec / kD2R);
+    E.prec = prec;
+    unsigned* sspill = slotspill + (size_t)task * NS * kMwSlotSpill;
+    unsigned* xsp = xspill + (size_t)task * xspill_task;
+    const int xgcap = (int)min<size_t>(xspill_task, (size_t)sw * sh);
+    LsdRegion* outR = regs + (size_t)task * kLsdRawCap;
+    unsigned* outP = regpts + (size_t)task * regpts_frame;
+
+    const unsigned long long t_kernel = STATS ? __builtin_amdgcn_s_memtime() : 0;
+    // ---- init: C = NOTDEF (and row padding), T = trivial seeds, H = 0
+    // (each wave builds whole 32-pixel words: lanes = 64 consecutive pixels)
+    const float pdeg = E.pdeg;
+    const int min_reg = od.min_reg_size;
+    for (int k = wv; k < sh * ((wpr + 1) >> 1); k += NW) {
+        const int y = k / ((wpr + 1) >> 1), xb = (k - y * ((wpr + 1) >> 1)) * 64;
+        const int x = xb + lane;
+        const float* r0 = E.P + (size_t)y * sw;
+        float d0 = kNotdefF, dr = kNotdefF, dbl = kNotdefF, db = kNotdefF, dbr = kNotdefF;
+        if (x < sw) {
+            d0 = r0[x];
+            if (x + 1 < sw) dr = r0[x + 1];
+            if (y + 1 < sh) {
+                const float* r1 = r0 + sw;
+                if (x > 0) dbl = r1[x - 1];
+                db = r1[x];
+                if (x + 1 < sw) dbr = r1[x + 1];
+            }
+        }
+        const bool def = x < sw && d0 != kNotdefF;
+        // forward neighbours of a seed: (x+1,y) (x-1,y+1) (x,y+1) (x+1,y+1);
+        // none aligned with its angle -> region = {seed} (< min_reg_size)
+        const bool grows = is_aligned_fast(dr, d0, pdeg, prec) || is_aligned_fast(dbl, d0, pdeg, prec) ||
+                           is_aligned_fast(db, d0, pdeg, prec) || is_aligned_fast(dbr, d0, pdeg, prec);
+        const unsigned long long cm = __ballot(!def);
+        const unsigned long long tm = __ballot(def && !grows && min_reg > 1);
+        if (lane < 2 && (xb >> 5) + lane < wpr) {
+            const int wi = y * wpr + (xb >> 5) + lane;
+            C[wi] = lane == 0 ? (unsigned)cm : (unsigned)(cm >> 32);
+            T[wi] = lane == 0 ? (unsigned)tm : (unsigned)(tm >> 32);
+            H[wi] = 0u;
+        }
+    }
+    for (int k = threadIdx.x; k < NW * kMwRB * wpr; k += NW * 64) ownAll[k] = 0u;
+    if (threadIdx.x < NS) {
+        slots[threadIdx.x].state = kMwFree;
+        slots[threadIdx.x].seed = -1;
+    }
+    if (threadIdx.x == 0) {
+        ctl->lock = ctl->dlock = ctl->head = ctl->cursor = ctl->finished = 0;
+        ctl->npts = ctl->nout = ctl->overflow = 0;
+        for (int i = 0; i < 16; ++i) ctl->stat[i] = 0;
+    }
+    __syncthreads();
+
+    // ---- main loop
+    lds_slot* my = slots + wv * kMwSlotsPerWave;
+    while (true) {
+        // 1. the walk, by whoever holds the lock
+        if (mw_try_lock(&ctl->lock, lane)) {
+            const unsigned long long tw0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
+            mw_walk<NW, STATS>(E, slots, slotq, sspill, SQ, xq, xsp, xgcap, min_reg, outR, outP, lane);
+            if (STATS && lane == 0) {
+                mw_stat(ctl, 6, (int)(__builtin_amdgcn_s_memtime() - tw0));
+                mw_stat(ctl, 8, 1);
+            }
+            mw_unlock(&ctl->lock, lane);
+        }
+        if (mw_lds_load(&ctl->finished)) break;
+        const int head = mw_lds_load(&ctl->head);
+        // 2. drop own regions the walk has passed (their seeds were absorbed or
+        // grown by the walker)
+        int fs = -1;
+        for (int j = 0; j < kMwSlotsPerWave; ++j) {
+            int stj = mw_lds_load(&my[j].state);
+            if (stj == kMwDone && my[j].seed < head) {
+                int ok = 0;
+                if (lane == 0) {
+                    int e = kMwDone;
+                    ok = __hip_atomic_compare_exchange_strong(&my[j].state, &e, kMwFree, __ATOMIC_ACQ_REL,
+                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ? 1 : 0;
+                    if (ok) mw_stat(ctl, 1, 1);
+                }
+                if (__builtin_amdgcn_readfirstlane(ok)) stj = kMwFree;
+            }
+            if (stj == kMwFree) fs = j;
+        }
+        // 3. a new speculative region in a free slot
+        int q = -1;
+        if (fs >= 0 && mw_try_lock(&ctl->dlock, lane)) {
+            q = mw_dispatch(E, lane);
+            if (q >= 0 && lane == 0) {
+                my[fs].seed = q;
+                my[fs].ovf = 0;
+                mw_stat(ctl, 0, 1);
+                mw_lds_store(&my[fs].state, kMwGrowing);
+            }
+            mw_unlock(&ctl->dlock, lane);
+        }
+        if (q < 0) {
+            if (STATS && lane == 0) mw_stat(ctl, 12, 1);
+            __builtin_amdgcn_s_sleep(2);
+            continue;
+        }
+        const int si = wv * kMwSlotsPerWave + fs;
+        const MwQueue Q{slotq + si * SQ, SQ, sspill + (size_t)si * kMwSlotSpill, kMwSlotSpill};
+        int n = 0;
+        float deg = 0.f;
+        bool spilled = false;
+        const unsigned long long ts0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
+        const int rc = mw_grow<true>(E, q % E.rowbits, q / E.rowbits, Q, n, deg, spilled, lane);
+        mw_own_clear(E, q / E.rowbits, Q, n, spilled, lane);
+        if (STATS && lane == 0) mw_stat(ctl, 11, (int)(__builtin_amdgcn_s_memtime() - ts0));
+        if (lane == 0) {
+            my[fs].n = n;
+            my[fs].deg = deg;
+            my[fs].ovf = rc == 2 ? 1 : 0;
+            if (rc == 1) mw_stat(ctl, 1, 1);
+        }
+        mw_wave_sync();  // (queue spill stores were drained as they were made)
+        if (lane == 0) mw_lds_store(&my[fs].state, rc == 1 ? kMwFree : kMwDone);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        nlines[task] = ctl->nout;
+        if (ctl->overflow) atomicOr(err + f, 4);
+        if (STATS) {
+            ctl->stat[10] = (int)(__builtin_amdgcn_s_memtime() - t_kernel);
+            for (int i = 0; i < 16; ++i) stats[(size_t)task * 16 + i] = ctl->stat[i];
+        }
+    }
+}
+
+}  // namespace plvi

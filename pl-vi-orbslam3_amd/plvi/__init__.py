@@ -184,6 +184,7 @@ def _declare(lib):
         "plvi_lines_profile": ([V, I], I),
         "plvi_lines_profile_read": ([V, V, P], I),
         "plvi_lines_debug_stats": ([V, V], I),
+        "plvi_lines_debug_mw_stats": ([V, V], I),
         "plvi_lines_debug_planes": ([V, I, I, V, V, V, P, P], I),
         "plvi_lines_debug_sobel": ([V, I, I, V, P, P], I),
         "plvi_descriptor_distance_batch": ([V, V, I, I, V, V], I),

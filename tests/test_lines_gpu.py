@@ -95,6 +95,7 @@ def test_lines_grow_window_budgets(plvi_lib, monkeypatch, lds, rb, rd):
     bits ring of RB rows, angle ring of R rows or none, the 1024-entry queue
     at the larger budgets): every choice gives the oracle's lines, at 640 px
     (odd batch) and at the 752 px EuRoC width (BASELINE C4)."""
+    monkeypatch.setenv("PLVI_GROW_MW", "0")  # the sequential (large-batch) kernel
     monkeypatch.setenv("PLVI_GROW_LDS", str(lds))
     monkeypatch.setenv("PLVI_GROW_RB", rb)
     if rd is not None:

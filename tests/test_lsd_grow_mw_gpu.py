@@ -1,0 +1,90 @@
+"""Multi-wave region growing (lsd_grow_mw_kernel, small batches): several
+regions of one frame grow concurrently and commit in raster seed order after
+validation (lsd.cpp:476-533, 635-686).  Parity: the lines equal the oracle's
+and the sequential kernel's bit for bit; the counters show the speculative
+path, the regrow path and the walker's exact path all ran."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle_lib as ol
+import plvi
+from plvi import synth
+from util import real_frames, structured_frames
+
+pytestmark = pytest.mark.gpu
+
+
+def _tables(lx, n):
+    klp, dep, fnp, cop, cap = lx.outputs()
+    cnt = plvi.download(cop, np.zeros(n, np.int32))
+    kl = plvi.download(klp, np.zeros(n * cap, plvi.KEYLINE_DTYPE))
+    de = plvi.download(dep, np.zeros((n * cap, 32), np.uint8))
+    fn = plvi.download(fnp, np.zeros((n * cap, 3), np.float64))
+    return [(kl[f * cap:f * cap + cnt[f]], de[f * cap:f * cap + cnt[f]], fn[f * cap:f * cap + cnt[f]])
+            for f in range(n)]
+
+
+def _same(a, b):
+    return a[0].tobytes() == b[0].tobytes() and np.array_equal(a[1], b[1]) and a[2].tobytes() == b[2].tobytes()
+
+
+def _run(monkeypatch, frames, mw, stats=False):
+    monkeypatch.setenv("PLVI_GROW_MW", str(mw))
+    n, h, w = frames.shape
+    lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, w, h, max_batch=n)
+    buf = plvi.DeviceBuffer(frames.nbytes)
+    buf.upload(frames)
+    st = None
+    lib = plvi.load()
+    if stats:
+        st = plvi.DeviceBuffer(n * 2 * 16 * 4)
+        st.upload(np.zeros(n * 2 * 16, np.int32))
+        lib.plvi_lines_debug_mw_stats(lx._h, ctypes.c_void_p(st.ptr))
+    lx.extract_batch(buf.ptr, n, w * h, w)
+    lib.plvi_device_synchronize()
+    assert lx.errors() == 0
+    out = _tables(lx, n)
+    if stats:
+        lib.plvi_lines_debug_mw_stats(lx._h, ctypes.c_void_p(0))
+        return out, plvi.download(st.ptr, np.zeros(n * 2 * 16, np.int32)).reshape(n, 2, 16)
+    return out
+
+
+def test_mw_matches_oracle_and_sequential(plvi_lib, monkeypatch):
+    frames = synth.batch(6, seed0=300)
+    mw, st = _run(monkeypatch, frames, 256, stats=True)
+    seq = _run(monkeypatch, frames, 0)
+    for f in range(len(frames)):
+        assert _same(mw[f], seq[f]), f"frame {f}: multi-wave != sequential kernel"
+        exp = ol.line_extract(frames[f])
+        assert _same(mw[f], exp), f"frame {f}: multi-wave != oracle"
+    tot = st.sum(axis=(0, 1))
+    # dispatched, dropped, regrown, exact, trivial, committed speculative
+    assert tot[0] > 0 and tot[5] > 0 and tot[4] > 0, tot
+    assert tot[5] + tot[2] <= tot[0]
+
+
+def test_mw_real_and_extreme_frames(plvi_lib, monkeypatch):
+    fr = real_frames()
+    imgs = [fr["rgb1_gray"]] + [structured_frames()[k] for k in ("step", "checker", "stripes", "binary_noise")]
+    frames = np.stack(imgs)
+    mw = _run(monkeypatch, frames, 256)
+    for f, img in enumerate(imgs):
+        assert _same(mw[f], ol.line_extract(img)), f"image {f}"
+
+
+def test_mw_euroc_752(plvi_lib, monkeypatch):
+    fr = real_frames()
+    frames = np.stack([fr["euroc1"], fr["euroc2"]])
+    mw = _run(monkeypatch, frames, 256)
+    for f in range(2):
+        assert _same(mw[f], ol.line_extract(frames[f])), f"euroc{f + 1}"
+
+
+def test_mw_flat_and_single_frame(plvi_lib, monkeypatch):
+    flat = np.full((1, 480, 640), 77, np.uint8)
+    assert len(_run(monkeypatch, flat, 256)[0][0]) == 0
+    one = synth.batch(1, seed0=7)
+    assert _same(_run(monkeypatch, one, 256)[0], ol.line_extract(one[0]))

@@ -1,0 +1,47 @@
+"""Region-growing stage time, sequential kernel vs the multi-wave kernel, at
+small batches, plus the multi-wave counters (diagnostic).
+usage: python tools/mw_probe.py [B,...]"""
+import ctypes
+import os
+import pathlib
+import sys
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "pl-vi-orbslam3_amd"))
+import torch  # noqa: E402
+
+import plvi  # noqa: E402
+from plvi import synth  # noqa: E402
+
+batches = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "1,16,64,128").split(",")]
+W, H = 640, 480
+allf = synth.device_sequence(max(batches), W, H, 0, "cuda")
+lib = plvi.load()
+names = ["disp", "drop", "regrow", "exact", "trivial", "spec_ok", "walk_cyc", "wgrow_cyc", "walks", "blocked",
+         "kern_cyc", "spec_cyc", "idle"]
+for B in batches:
+    for mw in (0, 256):
+        os.environ["PLVI_GROW_MW"] = str(mw)
+        lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=B)
+        lx.extract_batch(allf.data_ptr(), B, W * H, W)
+        torch.cuda.synchronize()
+        lx.profile(True)
+        for _ in range(5):
+            lx.extract_batch(allf.data_ptr(), B, W * H, W)
+        st, runs = lx.profile_read()
+        lx.profile(False)
+        line = f"B={B} mw={mw} " + " ".join(f"{k}={v / runs:.2f}" for k, v in st.items())
+        if mw:
+            s = torch.zeros(B * 2 * 16, dtype=torch.int32, device="cuda")
+            lib.plvi_lines_debug_mw_stats(lx._h, ctypes.c_void_p(s.data_ptr()))
+            lx.extract_batch(allf.data_ptr(), B, W * H, W)
+            torch.cuda.synchronize()
+            lib.plvi_lines_debug_mw_stats(lx._h, ctypes.c_void_p(0))
+            a = s.cpu().numpy().reshape(B, 2, 16).mean(axis=0)
+            for o in range(2):
+                line += f" | oct{o} " + " ".join(f"{n}={a[o, i]:.0f}" for i, n in enumerate(names))
+        assert lx.errors() == 0
+        print(line, flush=True)
+        lx.close()
