@@ -65,30 +65,38 @@ def level_dims(w, h, nlevels=8, sf=1.2):
 
 
 def blur_fast_bytes(w, h):
-    """Algorithmic bytes/frame of orb_blur_fast_kernel (one launch covers all
-    8 levels): read every level image once (level 0 = the input frame), write
-    its 7x7 blur and FAST score planes once, and level 0's pyramid copy (u8)."""
+    """SURVEY 8(d) algorithmic bytes/frame of the ORB blur + FAST pass (the
+    roofline numerator): 7x7 blur of every level (read + write, 1 901 064 B at
+    640x480) + FAST scoring read of every level (950 532 B) = 2 851 596 B."""
+    planes = [a * b for a, b in level_dims(w, h)]
+    return 3 * sum(planes)
+
+
+def blur_fast_kernel_bytes(w, h):
+    """What orb_blur_fast_kernel itself materialises per frame (reported next
+    to the SURVEY model, not used for frac): every level read once, its blur
+    and FAST score planes written once, and level 0's pyramid copy (u8)."""
     planes = [a * b for a, b in level_dims(w, h)]
     return sum(planes) + 2 * sum(planes) + planes[0]
 
 
 def lsd_prep_bytes(w, h, scale=0.8, noct=2):
-    """Algorithmic bytes/frame of lsd_prep_kernel (one launch per octave):
-    the octave's u8 image in, the scaled image's f32 angle + f64 modgrad out
-    (the seed-direction float4, written for defined pixels only, is not
-    counted: a lower bound on the kernel's compulsory traffic)."""
+    """Algorithmic bytes/frame of lsd_prep_kernel (one launch per octave): the
+    octave's u8 image in; out per scaled pixel the f32 angle, the f64 modgrad
+    and the float2 cos/sin pair region growing reads (20 B)."""
     tot = 0
     for o in range(noct):
         ow, oh = w >> o, h >> o
         sw, sh = int(np.rint(ow * scale)), int(np.rint(oh * scale))
-        tot += ow * oh + 12 * sw * sh
+        tot += ow * oh + 20 * sw * sh
     return tot
 
 
 def committed_traffic(batch, kernel):
     """HBM bytes per launch of `kernel` from the committed PMC passes
     (profiles/*/pmc_traffic*.json, tools/pmc_traffic.py), taken at this batch
-    size; else None."""
+    size; else None.  Entries before r03 held lsd_prep_kernel's per-batch sum
+    of its two octave launches: halved to a per-launch mean."""
     best = None
     for f in sorted(ROOT.glob("profiles/*/pmc_traffic*.json")):
         try:
@@ -98,7 +106,12 @@ def committed_traffic(batch, kernel):
         for e in d if isinstance(d, list) else [d]:
             if e.get("batch") == batch and e.get("kernel") == kernel:
                 best = e
-    return None if best is None else best["bytes_per_launch"]
+    if best is None:
+        return None
+    v = best["bytes_per_launch"]
+    if best.get("unit") != "bytes per launch" and kernel == "lsd_prep_kernel":
+        v /= 2
+    return v
 
 
 def free_port():
@@ -521,17 +534,23 @@ def run(args, world, rank):
     # ---------------------------------------------------------- rooflines
     bf_bytes = blur_fast_bytes(W, H) * B
     lp_bytes = lsd_prep_bytes(W, H) * B
+    bf_ms = ktot / max(kn, 1)
     roof = {"bound": "hbm", "kernel": "orb_blur_fast_kernel (7x7 blur + FAST score, all 8 levels, one launch)",
-            "achieved": bf_bytes / (ktot / max(kn, 1) * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "achieved": bf_bytes / (bf_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "traffic": committed_traffic(B, "orb_blur_fast_kernel") if (W, H) == (640, 480) else None,
-            "bytes_per_launch": bf_bytes, "avg_launch_ms": ktot / max(kn, 1), "launches": kn}
+            "bytes_per_launch": bf_bytes, "bytes_model": "SURVEY 8(d): blur read+write + FAST read of all levels",
+            "kernel_bytes_per_launch": blur_fast_kernel_bytes(W, H) * B,
+            "kernel_bytes_frac": blur_fast_kernel_bytes(W, H) * B / (bf_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "avg_launch_ms": bf_ms, "launches": kn}
     roof["frac"] = roof["achieved"] / roof["peak"]
+    lp_ms = ltot / max(ln, 1)
     roof_lsd = {"bound": "hbm", "kernel": "lsd_prep_kernel (u8 -> f64 blur 7x7, resize x0.8, ll_angle; one launch "
                                           "per octave)",
-                "achieved": lp_bytes * (ln / 2) / (ltot * 1e-3) / 1e9 if ltot else None, "peak": HBM_PEAK_GBS,
+                "achieved": (lp_bytes / 2) / (lp_ms * 1e-3) / 1e9 if ltot else None, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "traffic": committed_traffic(B, "lsd_prep_kernel") if (W, H) == (640, 480) else None,
-                "bytes_per_launch": lp_bytes / 2, "avg_launch_ms": ltot / max(ln, 1), "launches": ln}
+                "bytes_per_launch": lp_bytes / 2, "per_launch": "mean of the two octave launches (bytes and traffic)",
+                "avg_launch_ms": lp_ms, "launches": ln}
     if roof_lsd["achieved"]:
         roof_lsd["frac"] = roof_lsd["achieved"] / HBM_PEAK_GBS
     e2e_b = E2E_BYTES_640 if (W, H) == (640, 480) else E2E_BYTES_752 if (W, H) == (752, 480) else None

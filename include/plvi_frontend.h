@@ -347,7 +347,7 @@ int plvi_line_match_grid(const int* lines1, const uint8_t* desc1, int n1, int gr
  * cell_off + p*(ncell+1), cell_idx + p*idx_cap, desc2 + p*cap2*32,
  * directions2 + p*cap2*2, counts n1[p], n2[p].  Outputs matches_12
  * [n_pairs][cap1], nmatches [n_pairs]; *d_err |= 1 when a candidate set
- * exceeds 1024 lines. */
+ * exceeds 1024 lines (d_err may be NULL: no report). */
 int plvi_line_match_grid_batch(int n_pairs, const int* d_lines1, const uint8_t* d_desc1, const int* d_n1, int cap1,
                                int grid_cols, int grid_rows, const int* d_cell_off, const int* d_cell_idx,
                                int idx_cap, const uint8_t* d_desc2, const double* d_directions2, const int* d_n2,
@@ -383,6 +383,8 @@ int plvi_line_search_projection_batch(int n_pairs, const plvi_line_proj_params* 
                                       const uint8_t* d_last_flags, const float* d_x3dc, const int* d_last_octave,
                                       const uint8_t* d_ml_desc, const int* d_last_n, int last_cap, int* d_match,
                                       int* d_nmatches, int* d_err, void* stream);
+/* d_err (may be NULL): |= 1 when a candidate set overflows, |= 2 when a last-frame
+ * octave is outside [0, nlevels) (that line is skipped). */
 /* One pair from host memory, synchronous (n_cur <= 2048).  Returns the
  * count or an error (PLVI_E_CAPACITY when a candidate set exceeds 1024). */
 int plvi_line_search_projection(const plvi_line_proj_params* p, const float* cur_angle, const uint8_t* cur_desc,
@@ -543,7 +545,8 @@ typedef struct plvi_local_params {
  * mTrackProjY, mTrackProjXR, mTrackViewCos; level = mnTrackScaleLevel;
  * GetDescriptor() (32 B).  Output match [f][cap] = the MapPoint index
  * stored in F.mvpMapPoints[idx] by the call, or -1; nmatches [f] = the
- * return value.  cap <= 65535 and ~17 B per keypoint + 8 B per MapPoint +
+ * return value.  A MapPoint whose level is outside [0, nlevels) gets no
+ * candidate.  cap <= 65535 and ~17 B per keypoint + 8 B per MapPoint +
  * 12 KB of LDS <= 160 KB. */
 int plvi_search_local_batch(int n_frames, const plvi_local_params* p, const plvi_keypoint* d_kps, const uint8_t* d_desc,
                             const int* d_n, int cap, const uint8_t* d_blocked, const float* d_uright,

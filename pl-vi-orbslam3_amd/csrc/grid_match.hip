@@ -145,7 +145,7 @@ __global__ __launch_bounds__(64) void line_match_grid_kernel(
     for (int s = 32; s > 0; s >>= 1) drop += __shfl_xor(drop, s);
     if (lane == 0) {
         nmatch[p] = matches - drop;
-        if (s_overflow) atomicOr(err, 1);
+        if (s_overflow && err) atomicOr(err, 1);
     }
 }
 
@@ -202,8 +202,14 @@ __global__ __launch_bounds__(64) void line_search_proj_kernel(
             bool ok = !(invzc_sp < 0 || invzc_ep < 0);
             ok = ok && !(usx < p.min_x || usx > p.max_x || uex < p.min_x || uex > p.max_x);
             ok = ok && !(usy < p.min_y || usy > p.max_y || uey < p.min_y || uey > p.max_y);
+            // a last-frame octave outside [0, nlevels) has no scale: skip the
+            // line and flag it (bit 2) instead of reading past scale_l
+            const int oct = ok ? OC[i] : 0;
+            if (ok && (oct < 0 || oct >= p.nlevels)) {
+                ok = false;
+                if (err) atomicOr(err, 2);
+            }
             if (ok) {
-                const int oct = OC[i];
                 int window = (int)floorf(p.th);
                 if (p.scale_l[oct] > 1) window = (int)floorf(p.th + p.scale_l[oct]);
                 const int pts[4] = {(int)((double)usx * p.inv_w), (int)((double)usy * p.inv_h),
@@ -271,7 +277,7 @@ __global__ __launch_bounds__(64) void line_search_proj_kernel(
     }
     if (lane == 0) {
         nmatch[pr] = matches;
-        if (s_overflow) atomicOr(err, 1);
+        if (s_overflow && err) atomicOr(err, 1);
     }
 }
 

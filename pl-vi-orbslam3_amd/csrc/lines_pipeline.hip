@@ -82,7 +82,7 @@ struct LinePipeline {
     double gk[7]{};
     int lbdTaps[3] = {14, 62, 104};
     DevBuf d_oct, d_tabs, octImg, pix, modg, seedcs, gbits, qspill, regs, regpts, rawLines, nlines, klTmp, klOut, fnOut, cntOut, descOut, lbdBlur,
-        lbdG, err, staging, mwOwn, mwSlot;
+        lbdG, err, staging, mwOwn, mwSlot, mwGrow;
     size_t qspillFrame = 0, gbitsFrame = 0, lbdPlaneTotal = 0;
     int lastFrames = 0;
     static constexpr int kStages = 5, kRing = 512;
@@ -365,20 +365,22 @@ struct LinePipeline {
         if (const char* e = getenv("PLVI_GROW_MW")) mwMaxFrames = atoi(e);
         mwMaxFrames = std::min(mwMaxFrames, Bcap);
         if (mwMaxFrames > 0) {
+            // LDS: ctl + dispatch log + C/T/H bitmaps + own windows + growth
+            // queues, the rest for the slot pool (up to kMwMaxSlots)
             const size_t nwords = gbitsFrame;  // max over octaves of sh * wpr
-            constexpr int NS = kMwWaves * kMwSlotsPerWave;
-            const size_t fixedMw = sizeof(MwCtl) + NS * sizeof(MwSlot) +
-                                   4 * (3 * nwords + (size_t)kMwWaves * kMwRB * wprMax + kMwXQ);
-            mwSQ = 256;
-            while (mwSQ > 32 && fixedMw + 4 * (size_t)NS * mwSQ > 160 * 1024) mwSQ /= 2;
-            mwSmem = fixedMw + 4 * (size_t)NS * mwSQ;
-            if (mwSmem > 160 * 1024) {
+            const size_t fixedMw = sizeof(MwCtl) + 8 * kMwLog +
+                                   4 * (3 * nwords + (size_t)kMwWaves * kMwRB * wprMax + (size_t)kMwWaves * kMwGQ);
+            const size_t ldsMax = 160 * 1024;
+            mwSlots = fixedMw < ldsMax ? (int)std::min<size_t>(kMwMaxSlots, (ldsMax - fixedMw) / kMwSlotBytes) : 0;
+            mwSmem = fixedMw + (size_t)mwSlots * kMwSlotBytes;
+            if (mwSlots < 2 * kMwWaves) {
                 mwMaxFrames = 0;  // frame too large for the LDS bitmaps: sequential kernel only
             } else {
                 const size_t tasks = (size_t)mwMaxFrames * nOct;
                 mwOwnTask = (size_t)kMwWaves * gbitsFrame;
                 if (mwOwn.alloc(sizeof(unsigned) * mwOwnTask * tasks) ||
-                    mwSlot.alloc(sizeof(unsigned) * (size_t)NS * kMwSlotSpill * tasks))
+                    mwSlot.alloc(sizeof(unsigned) * (size_t)kMwMaxSlots * kMwSlotSpill * tasks) ||
+                    mwGrow.alloc(sizeof(unsigned) * (size_t)kMwWaves * kMwGSpill * tasks))
                     return PLVI_E_HIP;
                 PLVI_CHECK(hipMemset(mwOwn.p, 0, mwOwn.bytes));  // kept zero by every launch
                 for (const void* k : {(const void*)lsd_grow_mw_kernel<kMwWaves, false>,
@@ -389,7 +391,7 @@ struct LinePipeline {
         return PLVI_OK;
     }
     static constexpr int kMwWaves = 16;
-    int mwMaxFrames = 0, mwSQ = 0;
+    int mwMaxFrames = 0, mwSlots = 0;
     size_t mwSmem = 0, mwOwnTask = 0;
     int* mwStats = nullptr;  // diagnostic counters (plvi_lines_debug_mw_stats)
     size_t growSmem = 0;
@@ -463,9 +465,9 @@ struct LinePipeline {
             auto mwK = mwStats ? lsd_grow_mw_kernel<kMwWaves, true> : lsd_grow_mw_kernel<kMwWaves, false>;
             hipLaunchKernelGGL(mwK, dim3(oCount * nf), dim3(kMwWaves * 64), mwSmem, st, d_oct.as<LineOctDev>(),
                                (const float*)pix.as<float>(), (const float2*)seedcs.as<float2>(),
-                               mwOwn.as<unsigned>(), mwOwnTask, mwSlot.as<unsigned>(), qspill.as<unsigned>(),
-                               qspillFrame, prec, regs.as<LsdRegion>(), regpts.as<unsigned>(), qspillFrame,
-                               nlines.as<int>(), err.as<int>(), mwSQ, nOct, oBase, oCount, mwStats);
+                               mwOwn.as<unsigned>(), mwOwnTask, mwGrow.as<unsigned>(), mwSlot.as<unsigned>(),
+                               qspill.as<unsigned>(), qspillFrame, prec, regs.as<LsdRegion>(), regpts.as<unsigned>(),
+                               qspillFrame, nlines.as<int>(), err.as<int>(), mwSlots, nOct, oBase, oCount, mwStats);
             return;
         }
         auto growK = growStats ? lsd_grow_kernel<true> : lsd_grow_kernel<false>;

@@ -19,26 +19,35 @@
 //    aligned with the seed angle: a static property, the region is the seed
 //    alone, T) are committed in place, any other seed takes its speculative
 //    region (validated) or is grown exactly by the walker when no wave has it.
-//  * Waves pick the next seed after a shared cursor that is neither in C, T
-//    nor claimed by any region so far (H, a hint: skipped seeds are found by
-//    the walk).  A speculative region whose seed the walk passed is dropped.
+//  * Waves 1..NW-1 pick the next seed after a shared cursor that is neither
+//    in C, T nor claimed by any region so far (H, a hint: skipped seeds are
+//    found by the walk) and grow it into their own LDS queue; a finished
+//    region is copied into a free slot of a shared pool (first kMwSP points in
+//    LDS, the rest in global memory).  Wave 0 is the walker.  A speculative
+//    region whose seed the walk passed is dropped.
 //
 // LDS: C, T, H (whole frame, one bit per pixel), per wave an own-mark window
-// of RB rows from the seed row (rows below it spill to a global bitmap), per
-// region slot a queue of SQ entries (spill to global), the walker's exact
-// queue (spill to the qspill plane).  Commit order = raster seed order, so the
-// region list handed to lsd_rect_kernel is the sequential kernel's.
+// of kMwRB rows from the seed row (rows below it spill to a global bitmap)
+// and a growth queue (spill to global), the slot pool, the dispatch log (the
+// speculative seeds in increasing order with their slots).  Commit order =
+// raster seed order, so the region list handed to lsd_rect_kernel is the
+// sequential kernel's.
 // ---------------------------------------------------------------------------
 #pragma once
 
 namespace plvi {
 
-constexpr int kMwSlotsPerWave = 2;
-constexpr int kMwRB = 32;          // own-mark window rows
-constexpr int kMwSlotSpill = 4096; // global queue entries per slot beyond the LDS part
-constexpr int kMwXQ = 256;         // LDS entries of the walker's exact queue
+constexpr int kMwRB = 32;           // own-mark window rows
+constexpr int kMwGQ = 256;          // LDS growth-queue entries per wave
+constexpr int kMwGSpill = 4096;     // global growth-queue entries per speculative wave
+constexpr int kMwSP = 64;           // points of a slot kept in LDS
+constexpr int kMwSlotSpill = 2048;  // points of a slot beyond kMwSP (global)
+constexpr int kMwMaxSlots = 128;
+constexpr int kMwLog = 256;         // dispatch log entries (seed order)
 
-enum : int { kMwFree = 0, kMwGrowing = 1, kMwDone = 2, kMwBusy = 3 };
+// slot states; COMMITTED: validated and committed, a grower still copies
+// its points out (regions of more than kMwSP points)
+enum : int { kMwFree = 0, kMwGrowing = 1, kMwDone = 2, kMwCommitted = 3, kMwCopying = 4 };
 
 struct MwSlot {
     int seed;   // bit index y * (wpr * 32) + x
@@ -46,15 +55,19 @@ struct MwSlot {
     int n;      // region size
     float deg;  // final region angle (float degrees)
     int ovf;    // queue overflow: the walker regrows it
-    int pad[3];
+    int out;    // COMMITTED: offset of its points in the task's point list
+    int pad[2];
 };
+constexpr int kMwSlotBytes = sizeof(MwSlot) + 4 * kMwSP;
 // control block (LDS)
 struct MwCtl {
     int lock, dlock, head, cursor, finished, npts, nout, overflow;
+    int dlog_n, wptr, pad0, pad1;  // dispatch log: entries appended / next entry the walk examines
     int stat[16];  // [0] dispatched [1] dropped [2] regrown [3] exact (undispatched) [4] trivial [5] committed
                    // speculative [6] walk cycles [7] walker growth cycles [8] walk entries [9] blocked on a
                    // growing head [10] kernel cycles (wave 0) [11] speculative growth cycles (sum over waves)
-                   // [12] idle polls
+                   // [12] idle polls [13] blocks (completed regions) [14] block setup cycles / 16
+                   // [15] block round cycles / 16
 };
 
 typedef MwSlot __attribute__((address_space(3))) lds_slot;
@@ -113,38 +126,51 @@ __device__ __forceinline__ void mw_wave_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// LDS synchronisation: the LDS unit executes one wave's DS instructions in
+// issue order, so a flag written after data is seen by another wave only
+// after that data; compiler fences keep the program order.  (Workgroup-scope
+// acquire / release would also wait for this wave's outstanding global
+// stores, which nothing here needs: global spills are drained when written.)
+__device__ __forceinline__ void mw_cfence() { __atomic_signal_fence(__ATOMIC_SEQ_CST); }
 __device__ __forceinline__ int mw_lds_load(lds_i32* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    mw_cfence();
+    const int v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    mw_cfence();
+    return v;
 }
 __device__ __forceinline__ void mw_lds_store(lds_i32* p, int v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    mw_cfence();
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    mw_cfence();
 }
-// wave-uniform try-lock (lane 0 does the CAS)
 __device__ __forceinline__ void mw_stat(lds_ctl* c, int i, int v) {
     __hip_atomic_fetch_add(&c->stat[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+// wave-uniform try-lock (lane 0 does the CAS)
 __device__ __forceinline__ bool mw_try_lock(lds_i32* l, int lane) {
     int got = 0;
+    mw_cfence();
     if (lane == 0) {
         int e = 0;
-        got = __hip_atomic_compare_exchange_strong(l, &e, 1, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+        got = __hip_atomic_compare_exchange_strong(l, &e, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_WORKGROUP) ? 1 : 0;
     }
     got = __builtin_amdgcn_readfirstlane(got);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    mw_cfence();
     return got != 0;
 }
 __device__ __forceinline__ void mw_unlock(lds_i32* l, int lane) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (lane == 0) __hip_atomic_store(l, 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    mw_wave_sync();
+    if (lane == 0) mw_lds_store(l, 0);
 }
 
 // Grow the region of seed (sx, sy) into Q (region_grow, lsd.cpp:635-686).
 // SPEC: abandon when the walk passes the seed.  Returns 0 = grown, 1 =
 // abandoned, 2 = queue overflow; n = points in Q (own marks set for them).
-template <bool SPEC>
+template <bool SPEC, bool STATS = false>
 __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_out, float& deg_out, bool& spilled,
                        int lane) {
+    unsigned long long c_setup = 0, c_round = 0, n_blk = 0;
     const int sw = E.sw, sh = E.sh;
     const int seedb = sy * E.rowbits + sx;
     const float pdeg = E.pdeg;
@@ -174,6 +200,7 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
             deg_out = reg_deg;
             return 1;
         }
+        const unsigned long long tb0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
         const int nb = min(7, reg_size - i);
         const bool active = lane < 9 * nb;
         const unsigned pv = active ? mw_qget(Q, i + bp) : 0u;
@@ -198,6 +225,12 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
         // block a lane's pixel only changes through an earlier lane's commit
         // of the same pixel: dup / Ccum)
         const bool live0 = valid && deg != kNotdefF && !mw_bit(E.C, E.wpr, nx, ny) && !mw_own_get(E, nx, ny, sy);
+        unsigned long long tb1 = 0;
+        if (STATS) {
+            tb1 = __builtin_amdgcn_s_memtime();
+            c_setup += tb1 - tb0;
+            ++n_blk;
+        }
         unsigned long long Ccum = 0;
         int start = 0;
         while (start < 9 * nb) {
@@ -251,7 +284,13 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
             }
             __builtin_amdgcn_wave_barrier();
         }
+        if (STATS) c_round += __builtin_amdgcn_s_memtime() - tb1;
         i += nb;
+    }
+    if (STATS && lane == 0) {
+        mw_stat(E.ctl, 13, (int)n_blk);
+        mw_stat(E.ctl, 14, (int)(c_setup >> 4));
+        mw_stat(E.ctl, 15, (int)(c_round >> 4));
     }
     n_out = reg_size;
     deg_out = reg_deg;
@@ -273,20 +312,33 @@ __device__ __forceinline__ void mw_own_clear(const MwEnv& E, int sy, const MwQue
     mw_wave_sync();
 }
 
-// The walk (lock holder): resolve seeds from ctl->head in raster order.
-// Returns when the next seed's region is still growing (or all are done).
-template <int NW, bool STATS>
-__device__ void mw_walk(const MwEnv& E, lds_slot* slots, lds_u32* slotq, unsigned* slotspill, int SQ, lds_u32* xq,
-                        unsigned* xspill, int xgcap, int min_reg, LsdRegion* outR, unsigned* outP, int lane) {
+// A slot's points: the first kMwSP in LDS after its header, the rest in
+// global memory.
+__device__ __forceinline__ MwQueue mw_slot_queue(lds_u8* pool, unsigned* slotspill, int si) {
+    return MwQueue{(lds_u32*)(pool + (size_t)si * kMwSlotBytes + sizeof(MwSlot)), kMwSP,
+                   slotspill + (size_t)si * kMwSlotSpill, kMwSlotSpill};
+}
+__device__ __forceinline__ lds_slot* mw_slot(lds_u8* pool, int si) { return (lds_slot*)(pool + (size_t)si * kMwSlotBytes); }
+
+// The walk (wave 0): resolve seeds from ctl->head in raster order.  Returns
+// the slot whose region the next seed waits for, or -1 once every seed is
+// resolved.  The dispatch log lists the speculative seeds in increasing
+// order, so the region of seed q (if any) is found by advancing one pointer.
+template <bool STATS>
+__device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* slotspill, const MwQueue& XQ,
+                       int min_reg, LsdRegion* outR, unsigned* outP, int lane) {
     lds_ctl* ctl = E.ctl;
     const int nwords = E.sh * E.wpr;
     const int rowbits = E.rowbits;
     int head = ctl->head;
+    int wp = ctl->wptr;
+    int blocked = -1;
     while (true) {
         // next unresolved pixel >= head: first zero bit of C
         int w = head >> 5;
         if (w >= nwords) break;
-        unsigned m = ~E.C[w] & (~0u << (head & 31));
+        unsigned cw = E.C[w], tw = E.T[w];
+        unsigned m = ~cw & (~0u << (head & 31));
         if (!m) {
             // wave-parallel scan of the following words
             int found = -1;
@@ -301,18 +353,16 @@ __device__ void mw_walk(const MwEnv& E, lds_slot* slots, lds_u32* slotq, unsigne
                 break;
             }
             w = found;
-            m = ~E.C[w];
+            cw = E.C[w];
+            tw = E.T[w];
+            m = ~cw;
         }
         // trivial seeds before the first non-trivial one are committed in place
-        const unsigned tw = E.T[w];
         const unsigned nt = m & ~tw;
         const unsigned run = nt ? (m & tw & ((nt & (0u - nt)) - 1u)) : (m & tw);
-        if (run) {
-            if (lane == 0) {
-                __atomic_fetch_or(&E.C[w], run, __ATOMIC_RELAXED);
-                mw_stat(ctl, 4, __popc(run));
-            }
-            mw_wave_sync();
+        if (run && lane == 0) {
+            __atomic_fetch_or(&E.C[w], run, __ATOMIC_RELAXED);
+            if (STATS) mw_stat(ctl, 4, __popc(run));
         }
         if (!nt) {
             head = (w + 1) * 32;
@@ -320,104 +370,150 @@ __device__ void mw_walk(const MwEnv& E, lds_slot* slots, lds_u32* slotq, unsigne
         }
         const int q = w * 32 + (__ffs((int)nt) - 1);
         head = q;
-        const int qx = q % rowbits, qy = q / rowbits;
-        // the slot holding seed q, if any
-        int si = -1, sst = kMwFree;
-        {
-            const bool hit = lane < NW * kMwSlotsPerWave && mw_lds_load(&slots[lane].state) != kMwFree &&
-                             slots[lane].seed == q;
-            const unsigned long long b = __ballot(hit);
-            if (b) {
-                si = __ffsll((long long)b) - 1;
-                sst = mw_lds_load(&slots[si].state);
-            }
-        }
-        if (si >= 0 && sst == kMwGrowing) {  // wait for it
+        // the speculative region of seed q, if one was dispatched
+        const int dn = mw_lds_load(&ctl->dlog_n);
+        while (wp < dn && dlog[2 * (wp & (kMwLog - 1))] < q) ++wp;
+        int si = -1;
+        if (wp < dn && dlog[2 * (wp & (kMwLog - 1))] == q) si = dlog[2 * (wp & (kMwLog - 1)) + 1];
+        lds_slot* S = si >= 0 ? mw_slot(pool, si) : nullptr;
+        const int sst = si >= 0 ? mw_lds_load(&S->state) : kMwFree;
+        if (sst == kMwGrowing) {  // wait for it
             if (STATS && lane == 0) mw_stat(ctl, 9, 1);
+            blocked = si;
             break;
         }
-        bool use_slot = false;
+        if (si >= 0) ++wp;
         int n = 0;
-        float deg = 0.f;
-        MwQueue Q;
-        if (si >= 0 && sst == kMwDone) {
-            // take it (its wave may drop it only once the walk has passed q)
-            int ok = 0;
-            if (lane == 0) {
-                int e = kMwDone;
-                ok = __hip_atomic_compare_exchange_strong(&slots[si].state, &e, kMwBusy, __ATOMIC_ACQUIRE,
-                                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ? 1 : 0;
+        bool done = false;
+        if (sst == kMwDone) {
+            // validate (none of its pixels committed by an earlier region) and
+            // commit; the first kMwSP points stay in registers
+            n = S->n;
+            const float deg = S->deg;
+            const MwQueue Q = mw_slot_queue(pool, slotspill, si);
+            bool valid = S->ovf == 0;
+            unsigned v0 = 0u;
+            if (valid) {
+                bool bad = false;
+                if (lane < n) {
+                    v0 = Q.lq[lane];
+                    bad = mw_bit(E.C, E.wpr, (int)(v0 & 0xffffu), (int)(v0 >> 16));
+                }
+                for (int j = lane + 64; j < n; j += 64) {
+                    const unsigned v = mw_qget(Q, j);
+                    bad |= mw_bit(E.C, E.wpr, (int)(v & 0xffffu), (int)(v >> 16));
+                }
+                valid = __ballot(bad) == 0ull;
             }
-            ok = __builtin_amdgcn_readfirstlane(ok);
-            if (ok) {
-                Q = MwQueue{slotq + si * SQ, SQ, slotspill + (size_t)si * kMwSlotSpill, kMwSlotSpill};
-                n = slots[si].n;
-                deg = slots[si].deg;
-                bool valid = slots[si].ovf == 0;
-                if (valid) {
-                    bool bad = false;
-                    for (int j = lane; j < n; j += 64) {
-                        const unsigned v = mw_qget(Q, j);
-                        bad |= mw_bit(E.C, E.wpr, (int)(v & 0xffffu), (int)(v >> 16));
+            if (valid) {
+                if (lane < n) mw_or(E.C, E.wpr, (int)(v0 & 0xffffu), (int)(v0 >> 16));
+                for (int j = lane + 64; j < n; j += 64) {
+                    const unsigned v = mw_qget(Q, j);
+                    mw_or(E.C, E.wpr, (int)(v & 0xffffu), (int)(v >> 16));
+                }
+                int st_next = kMwFree;
+                if (n >= min_reg) {
+                    const int nout = ctl->nout, npts = ctl->npts;
+                    if (nout < kLsdRawCap) {
+                        if (lane == 0) {
+                            outR[nout] = LsdRegion{npts, n, (double)deg * kD2R};
+                            ctl->npts = npts + n;
+                            ctl->nout = nout + 1;
+                            S->out = npts;
+                        }
+                        // up to 64 points now; longer regions are copied by a grower
+                        if (n <= 64) {
+                            if (lane < n) outP[npts + lane] = v0;
+                        } else {
+                            st_next = kMwCommitted;
+                        }
+                    } else if (lane == 0) {
+                        ctl->overflow = 1;
                     }
-                    valid = __ballot(bad) == 0ull;
                 }
-                if (valid) {
-                    use_slot = true;
-                    if (lane == 0) mw_stat(ctl, 5, 1);
-                } else {
-                    if (lane == 0) mw_stat(ctl, 2, 1);
-                    mw_lds_store(&slots[si].state, kMwFree);
-                }
+                if (STATS && lane == 0) mw_stat(ctl, 5, 1);
+                mw_wave_sync();
+                if (lane == 0) mw_lds_store(&S->state, st_next);
+                done = true;
+            } else {
+                if (STATS && lane == 0) mw_stat(ctl, 2, 1);
+                mw_wave_sync();
+                if (lane == 0) mw_lds_store(&S->state, kMwFree);
             }
         }
-        if (!use_slot) {
+        if (!done) {
             // exact growth: every earlier seed is committed
-            Q = MwQueue{xq, kMwXQ, xspill, xgcap};
             bool spilled = false;
+            float deg = 0.f;
+            const int qx = q % rowbits, qy = q / rowbits;
             const unsigned long long tg0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
-            mw_grow<false>(E, qx, qy, Q, n, deg, spilled, lane);
-            mw_own_clear(E, qy, Q, n, spilled, lane);
-            if (STATS && lane == 0) mw_stat(ctl, 7, (int)(__builtin_amdgcn_s_memtime() - tg0));
-            if (lane == 0 && si < 0) mw_stat(ctl, 3, 1);
-        }
-        // commit: the region's pixels become USED for every later seed
-        for (int j = lane; j < n; j += 64) {
-            const unsigned v = mw_qget(Q, j);
-            mw_or(E.C, E.wpr, (int)(v & 0xffffu), (int)(v >> 16));
-        }
-        // region2rect input for lsd_rect_kernel (flsd :500-518 order)
-        if (n >= min_reg) {
-            const int nout = ctl->nout, npts = ctl->npts;
-            if (nout < kLsdRawCap) {
-                for (int j = lane; j < n; j += 64) outP[npts + j] = mw_qget(Q, j);
-                if (lane == 0) {
-                    outR[nout] = LsdRegion{npts, n, (double)deg * kD2R};
-                    ctl->npts = npts + n;
-                    ctl->nout = nout + 1;
-                }
-            } else if (lane == 0) {
-                ctl->overflow = 1;
+            mw_grow<false, STATS>(E, qx, qy, XQ, n, deg, spilled, lane);
+            mw_own_clear(E, qy, XQ, n, spilled, lane);
+            if (STATS && lane == 0) {
+                mw_stat(ctl, 7, (int)(__builtin_amdgcn_s_memtime() - tg0));
+                if (si < 0) mw_stat(ctl, 3, 1);
             }
+            for (int j = lane; j < n; j += 64) {
+                const unsigned v = mw_qget(XQ, j);
+                mw_or(E.C, E.wpr, (int)(v & 0xffffu), (int)(v >> 16));
+            }
+            // region2rect input for lsd_rect_kernel (flsd :500-518 order)
+            if (n >= min_reg) {
+                const int nout = ctl->nout, npts = ctl->npts;
+                if (nout < kLsdRawCap) {
+                    for (int j = lane; j < n; j += 64) outP[npts + j] = mw_qget(XQ, j);
+                    if (lane == 0) {
+                        outR[nout] = LsdRegion{npts, n, (double)deg * kD2R};
+                        ctl->npts = npts + n;
+                        ctl->nout = nout + 1;
+                    }
+                } else if (lane == 0) {
+                    ctl->overflow = 1;
+                }
+            }
+            mw_wave_sync();
         }
-        mw_wave_sync();
-        if (use_slot) mw_lds_store(&slots[si].state, kMwFree);
         head = q + 1;
-        if (lane == 0) mw_lds_store(&ctl->head, head);
+        if (lane == 0) {
+            ctl->wptr = wp;  // frees log entries for the dispatchers as the walk goes
+            mw_lds_store(&ctl->head, head);
+        }
     }
     if (lane == 0) {
+        ctl->wptr = wp;
         mw_lds_store(&ctl->head, head);
         if ((head >> 5) >= nwords) mw_lds_store(&ctl->finished, 1);
     }
     mw_wave_sync();
+    return blocked;
 }
 
-// Next seed for a speculative region: the first pixel after the cursor (and
-// the walk) that is neither committed / NOTDEF, trivial nor claimed.
-__device__ __forceinline__ int mw_dispatch(const MwEnv& E, int lane) {
+// A free slot (FREE, or DONE with a seed the walk passed) and the next seed
+// for a speculative region: the first pixel after the cursor (and the walk)
+// that is neither committed / NOTDEF, trivial nor claimed; appended to the
+// dispatch log with its slot.  Returns the seed (-1: none) and the slot.
+template <bool STATS>
+__device__ __forceinline__ int mw_dispatch(const MwEnv& E, lds_u8* pool, int nslots, lds_i32* dlog, int& slot,
+                                           int lane) {
     lds_ctl* ctl = E.ctl;
     const int nwords = E.sh * E.wpr;
+    const int dn = ctl->dlog_n;
+    if (dn - mw_lds_load(&ctl->wptr) >= kMwLog - 1) return -1;  // log full: the walk is far behind
     const int head = mw_lds_load(&ctl->head);
+    // a free slot (lanes scan the pool)
+    slot = -1;
+    for (int b0 = 0; b0 < nslots && slot < 0; b0 += 64) {
+        const int si = b0 + lane;
+        bool ok = false;
+        if (si < nslots) {
+            lds_slot* S = mw_slot(pool, si);
+            const int st = S->state;
+            ok = st == kMwFree || (st == kMwDone && S->seed < head);
+        }
+        const unsigned long long b = __ballot(ok);
+        if (b) slot = b0 + __ffsll((long long)b) - 1;
+    }
+    if (slot < 0) return -1;
     int cur = max(ctl->cursor, head);
     int w = cur >> 5;
     if (w >= nwords) return -1;
@@ -438,17 +534,38 @@ __device__ __forceinline__ int mw_dispatch(const MwEnv& E, int lane) {
         m = ~(E.C[w] | E.T[w] | E.H[w]);
     }
     const int q = w * 32 + (__ffs((int)m) - 1);
-    if (lane == 0) ctl->cursor = q + 1;
+    if (lane == 0) {
+        lds_slot* S = mw_slot(pool, slot);
+        if (STATS && S->state == kMwDone) mw_stat(ctl, 1, 1);  // a passed region, dropped
+        S->seed = q;
+        S->ovf = 0;
+        S->state = kMwGrowing;  // before the log entry that names it
+        ctl->cursor = q + 1;
+        dlog[2 * (dn & (kMwLog - 1))] = q;
+        dlog[2 * (dn & (kMwLog - 1)) + 1] = slot;
+        mw_lds_store(&ctl->dlog_n, dn + 1);
+        if (STATS) mw_stat(ctl, 0, 1);
+    }
     return q;
+}
+
+// Copy region points [0, n) from queue A to queue B (one wave).
+__device__ __forceinline__ void mw_copy_points(const MwQueue& A, const MwQueue& B, int n, int lane) {
+    bool g = false;
+    for (int j = lane; j < n; j += 64) {
+        mw_qput(B, j, mw_qget(A, j));
+        g |= j >= B.lcap;
+    }
+    if (__ballot(g)) vm_drain();
 }
 
 template <int NW, bool STATS>
 __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
     const LineOctDev* __restrict__ octs, const float* __restrict__ pix, const float2* __restrict__ pixcs,
-    unsigned* __restrict__ ownspill, size_t ownspill_task, unsigned* __restrict__ slotspill, unsigned* __restrict__ xspill,
-    size_t xspill_task, double prec, LsdRegion* __restrict__ regs, unsigned* __restrict__ regpts, size_t regpts_frame,
-    int* __restrict__ nlines, int* __restrict__ err, int SQ, int nOct, int oBase, int oCount,
-    int* __restrict__ stats) {
+    unsigned* __restrict__ ownspill, size_t ownspill_task, unsigned* __restrict__ gspill, unsigned* __restrict__ slotspill,
+    unsigned* __restrict__ xspill, size_t xspill_task, double prec, LsdRegion* __restrict__ regs,
+    unsigned* __restrict__ regpts, size_t regpts_frame, int* __restrict__ nlines, int* __restrict__ err, int nslots,
+    int nOct, int oBase, int oCount, int* __restrict__ stats) {
     extern __shared__ __align__(16) unsigned lds_u[];
     __builtin_amdgcn_s_setprio(PLVI_GROW_SETPRIO);
     const int nf = gridDim.x / oCount;
@@ -457,18 +574,16 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
     const LineOctDev& od = octs[o];
     const int sw = od.sw, sh = od.sh, wpr = (sw + 31) >> 5;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    constexpr int NS = NW * kMwSlotsPerWave;
-    // LDS carve-up
+    // LDS carve-up: ctl | dispatch log | C | T | H | own windows | growth queues | slot pool
     lds_ctl* ctl = (lds_ctl*)lds_u;
-    lds_slot* slots = (lds_slot*)(lds_u + sizeof(MwCtl) / 4);
-    lds_u32* base = (lds_u32*)(lds_u + sizeof(MwCtl) / 4 + NS * sizeof(MwSlot) / 4);
+    lds_i32* dlog = (lds_i32*)(lds_u + sizeof(MwCtl) / 4);
     const int nwords = sh * wpr;
-    lds_u32* C = base;
+    lds_u32* C = (lds_u32*)(dlog + 2 * kMwLog);
     lds_u32* T = C + nwords;
     lds_u32* H = T + nwords;
     lds_u32* ownAll = H + nwords;
-    lds_u32* slotq = ownAll + NW * kMwRB * wpr;
-    lds_u32* xq = slotq + NS * SQ;
+    lds_u32* gqAll = ownAll + NW * kMwRB * wpr;
+    lds_u8* pool = (lds_u8*)(gqAll + NW * kMwGQ);
 
     MwEnv E;
     E.P = pix + od.soff + (size_t)f * od.splane;
@@ -480,9 +595,12 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
     E.sw = sw; E.sh = sh; E.wpr = wpr; E.rowbits = wpr * 32;
     E.pdeg = (float)(prec / kD2R);
     E.prec = prec;
-    unsigned* sspill = slotspill + (size_t)task * NS * kMwSlotSpill;
-    unsigned* xsp = xspill + (size_t)task * xspill_task;
-    const int xgcap = (int)min<size_t>(xspill_task, (size_t)sw * sh);
+    unsigned* sspill = slotspill + (size_t)task * kMwMaxSlots * kMwSlotSpill;
+    // growth queue: LDS part + global part (the walker's spans a whole plane)
+    const MwQueue GQ = wv == 0 ? MwQueue{gqAll, kMwGQ, xspill + (size_t)task * xspill_task,
+                                         (int)min<size_t>(xspill_task, (size_t)sw * sh)}
+                               : MwQueue{gqAll + wv * kMwGQ, kMwGQ,
+                                         gspill + ((size_t)task * NW + wv) * kMwGSpill, kMwGSpill};
     LsdRegion* outR = regs + (size_t)task * kLsdRawCap;
     unsigned* outP = regpts + (size_t)task * regpts_frame;
 
@@ -521,83 +639,88 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
         }
     }
     for (int k = threadIdx.x; k < NW * kMwRB * wpr; k += NW * 64) ownAll[k] = 0u;
-    if (threadIdx.x < NS) {
-        slots[threadIdx.x].state = kMwFree;
-        slots[threadIdx.x].seed = -1;
+    for (int k = threadIdx.x; k < nslots; k += NW * 64) {
+        mw_slot(pool, k)->state = kMwFree;
+        mw_slot(pool, k)->seed = -1;
     }
     if (threadIdx.x == 0) {
         ctl->lock = ctl->dlock = ctl->head = ctl->cursor = ctl->finished = 0;
         ctl->npts = ctl->nout = ctl->overflow = 0;
+        ctl->dlog_n = ctl->wptr = 0;
         for (int i = 0; i < 16; ++i) ctl->stat[i] = 0;
     }
     __syncthreads();
 
-    // ---- main loop
-    lds_slot* my = slots + wv * kMwSlotsPerWave;
-    while (true) {
-        // 1. the walk, by whoever holds the lock
-        if (mw_try_lock(&ctl->lock, lane)) {
+    if (wv == 0) {
+        // ---- the walker: resolves seeds in raster order, waits on the head
+        // seed's region while it grows
+        while (true) {
             const unsigned long long tw0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
-            mw_walk<NW, STATS>(E, slots, slotq, sspill, SQ, xq, xsp, xgcap, min_reg, outR, outP, lane);
+            const int b = mw_walk<STATS>(E, pool, dlog, sspill, GQ, min_reg, outR, outP, lane);
             if (STATS && lane == 0) {
                 mw_stat(ctl, 6, (int)(__builtin_amdgcn_s_memtime() - tw0));
                 mw_stat(ctl, 8, 1);
             }
-            mw_unlock(&ctl->lock, lane);
+            if (b < 0) break;  // every seed resolved
+            while (mw_lds_load(&mw_slot(pool, b)->state) == kMwGrowing) __builtin_amdgcn_s_sleep(1);
         }
-        if (mw_lds_load(&ctl->finished)) break;
-        const int head = mw_lds_load(&ctl->head);
-        // 2. drop own regions the walk has passed (their seeds were absorbed or
-        // grown by the walker)
-        int fs = -1;
-        for (int j = 0; j < kMwSlotsPerWave; ++j) {
-            int stj = mw_lds_load(&my[j].state);
-            if (stj == kMwDone && my[j].seed < head) {
-                int ok = 0;
-                if (lane == 0) {
-                    int e = kMwDone;
-                    ok = __hip_atomic_compare_exchange_strong(&my[j].state, &e, kMwFree, __ATOMIC_ACQ_REL,
-                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ? 1 : 0;
-                    if (ok) mw_stat(ctl, 1, 1);
+    } else {
+        // ---- growers
+        while (true) {
+            // copy out a committed long region (the walker wrote its record)
+            int cs = -1;
+            if (mw_try_lock(&ctl->dlock, lane)) {
+                for (int b0 = 0; b0 < nslots && cs < 0; b0 += 64) {
+                    const int si = b0 + lane;
+                    const bool ok = si < nslots && mw_slot(pool, si)->state == kMwCommitted;
+                    const unsigned long long b = __ballot(ok);
+                    if (b) cs = b0 + __ffsll((long long)b) - 1;
                 }
-                if (__builtin_amdgcn_readfirstlane(ok)) stj = kMwFree;
+                if (cs >= 0 && lane == 0) mw_slot(pool, cs)->state = kMwCopying;
+                mw_unlock(&ctl->dlock, lane);
             }
-            if (stj == kMwFree) fs = j;
-        }
-        // 3. a new speculative region in a free slot
-        int q = -1;
-        if (fs >= 0 && mw_try_lock(&ctl->dlock, lane)) {
-            q = mw_dispatch(E, lane);
-            if (q >= 0 && lane == 0) {
-                my[fs].seed = q;
-                my[fs].ovf = 0;
-                mw_stat(ctl, 0, 1);
-                mw_lds_store(&my[fs].state, kMwGrowing);
+            if (cs >= 0) {
+                lds_slot* S = mw_slot(pool, cs);
+                const MwQueue Q = mw_slot_queue(pool, sspill, cs);
+                const int n = S->n, out = S->out;
+                for (int k = lane; k < n; k += 64) outP[out + k] = mw_qget(Q, k);
+                mw_wave_sync();
+                if (lane == 0) mw_lds_store(&S->state, kMwFree);
+                continue;
             }
-            mw_unlock(&ctl->dlock, lane);
+            if (mw_lds_load(&ctl->finished)) break;
+            // a new speculative region
+            int q = -1, si = -1;
+            if (mw_try_lock(&ctl->dlock, lane)) {
+                q = mw_dispatch<STATS>(E, pool, nslots, dlog, si, lane);
+                mw_unlock(&ctl->dlock, lane);
+            }
+            if (q < 0) {
+                if (STATS && lane == 0) mw_stat(ctl, 12, 1);
+                __builtin_amdgcn_s_sleep(2);
+                continue;
+            }
+            int n = 0;
+            float deg = 0.f;
+            bool spilled = false;
+            const unsigned long long ts0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
+            int rc = mw_grow<true, STATS>(E, q % E.rowbits, q / E.rowbits, GQ, n, deg, spilled, lane);
+            mw_own_clear(E, q / E.rowbits, GQ, n, spilled, lane);
+            lds_slot* S = mw_slot(pool, si);
+            if (rc == 0) {
+                if (n > kMwSP + kMwSlotSpill) rc = 2;  // too long for a slot: the walker regrows it
+                else mw_copy_points(GQ, mw_slot_queue(pool, sspill, si), n, lane);
+            }
+            if (STATS && lane == 0) mw_stat(ctl, 11, (int)(__builtin_amdgcn_s_memtime() - ts0));
+            if (lane == 0) {
+                S->n = n;
+                S->deg = deg;
+                S->ovf = rc == 2 ? 1 : 0;
+                if (STATS && rc == 1) mw_stat(ctl, 1, 1);
+            }
+            mw_wave_sync();
+            if (lane == 0) mw_lds_store(&S->state, rc == 1 ? kMwFree : kMwDone);
         }
-        if (q < 0) {
-            if (STATS && lane == 0) mw_stat(ctl, 12, 1);
-            __builtin_amdgcn_s_sleep(2);
-            continue;
-        }
-        const int si = wv * kMwSlotsPerWave + fs;
-        const MwQueue Q{slotq + si * SQ, SQ, sspill + (size_t)si * kMwSlotSpill, kMwSlotSpill};
-        int n = 0;
-        float deg = 0.f;
-        bool spilled = false;
-        const unsigned long long ts0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
-        const int rc = mw_grow<true>(E, q % E.rowbits, q / E.rowbits, Q, n, deg, spilled, lane);
-        mw_own_clear(E, q / E.rowbits, Q, n, spilled, lane);
-        if (STATS && lane == 0) mw_stat(ctl, 11, (int)(__builtin_amdgcn_s_memtime() - ts0));
-        if (lane == 0) {
-            my[fs].n = n;
-            my[fs].deg = deg;
-            my[fs].ovf = rc == 2 ? 1 : 0;
-            if (rc == 1) mw_stat(ctl, 1, 1);
-        }
-        mw_wave_sync();  // (queue spill stores were drained as they were made)
-        if (lane == 0) mw_lds_store(&my[fs].state, rc == 1 ? kMwFree : kMwDone);
     }
     __syncthreads();
     if (threadIdx.x == 0) {

@@ -442,8 +442,8 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
     uint32_t pv[8];
     load_rows(y0 - 3, pv);
     for (int rb = y0 - 3; rb < y1 + 3; rb += 8) {
-        // writing rows rb..rb+7 replaces rows rb-32..rb-25 of the ring; a
-        // queued row yy needs rows yy-3..yy+3
+        // writing rows rb..rb+7 replaces rows rb-kRingRows..rb-kRingRows+7
+        // of the ring; a queued row yy needs rows yy-3..yy+3
         if (nq > 0 && oldest - 3 < rb - (kRingRows - 8)) flush(nq, ynew);
 #pragma unroll
         for (int k = 0; k < 8; ++k)

@@ -304,6 +304,7 @@ __device__ void local_scan(const plvi_local_params& p, const ProjLds& s, const u
     if (!(fl[m] & 1)) return;
     const float x = proj[4 * m], y = proj[4 * m + 1], xr = proj[4 * m + 2], vcos = proj[4 * m + 3];
     const int L = lvl[m];
+    if (L < 0 || L >= p.nlevels) return;  // no scale factor for that level: no candidate
     float r = vcos > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos (:216-222)
     if (p.th != 1.0) r *= p.th;
     const float radius = r * p.scale_factors[L];

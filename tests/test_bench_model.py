@@ -13,15 +13,24 @@ def _bench():
     return m
 
 
-def test_blur_fast_bytes_is_baseline_blur_plus_fast_read_plus_copy():
+def test_blur_fast_bytes_is_survey_blur_plus_fast_read():
     b = _bench()
-    # BASELINE.md §3 (640x480): 7x7 blur of 8 levels 1 901 064 (read + write),
-    # FAST scoring read 950 532; the kernel also writes the score planes and
-    # level 0's pyramid copy
+    # SURVEY 8(d) (640x480): 7x7 blur of 8 levels 1 901 064 (read + write),
+    # FAST scoring read 950 532 -> the roofline numerator
     dims = b.level_dims(640, 480)
     planes = sum(w * h for w, h in dims)
     assert planes == 950_532
-    assert b.blur_fast_bytes(640, 480) == 3_158_796 == planes + 2 * planes + 640 * 480
+    assert b.blur_fast_bytes(640, 480) == 2_851_596 == 1_901_064 + 950_532
+    # the kernel's own materialisation (score planes, level-0 copy) is reported beside it
+    assert b.blur_fast_kernel_bytes(640, 480) == 3_158_796 == planes + 2 * planes + 640 * 480
+
+
+def test_roofline_frac_is_bytes_over_avg_launch_over_peak():
+    b = _bench()
+    # frac = SURVEY bytes x frames / average launch time / 8 TB/s, checkable by hand
+    B, ms = 3072, 7.39
+    frac = b.blur_fast_bytes(640, 480) * B / (ms * 1e-3) / 1e9 / b.HBM_PEAK_GBS
+    assert abs(frac - 0.148) < 0.001
 
 
 def test_end_to_end_bytes_match_baseline_totals():
@@ -30,16 +39,26 @@ def test_end_to_end_bytes_match_baseline_totals():
     assert b.E2E_BYTES_752 == 18_775_975
 
 
-def test_lsd_prep_bytes_counts_u8_in_and_f32_f64_out():
+def test_lsd_prep_bytes_counts_u8_in_and_angle_modgrad_cossin_out():
     b = _bench()
-    # octave 0: 640x480 u8 -> 512x384 scaled; octave 1: 320x240 -> 256x192
-    assert b.lsd_prep_bytes(640, 480) == 640 * 480 + 12 * 512 * 384 + 320 * 240 + 12 * 256 * 192
+    # octave 0: 640x480 u8 -> 512x384 scaled; octave 1: 320x240 -> 256x192;
+    # out per scaled pixel: f32 angle + f64 modgrad + float2 cos/sin = 20 B
+    assert b.lsd_prep_bytes(640, 480) == 640 * 480 + 20 * 512 * 384 + 320 * 240 + 20 * 256 * 192
+
+
+def test_lsd_prep_traffic_is_per_launch():
+    b = _bench()
+    t = b.committed_traffic(3072, "lsd_prep_kernel")
+    assert t is not None
+    alg = b.lsd_prep_bytes(640, 480) * 3072 / 2  # mean per octave launch, as bytes_per_launch
+    assert 0.9 <= t / alg < 1.6
 
 
 def test_committed_traffic_is_calibrated_and_near_algorithmic():
     b = _bench()
     t = b.committed_traffic(3072, "orb_blur_fast_kernel")
     assert t is not None
-    alg = b.blur_fast_bytes(640, 480) * 3072
+    alg = b.blur_fast_kernel_bytes(640, 480) * 3072
     assert 1.0 <= t / alg < 1.3  # measured 1.20
+    assert 1.0 <= t / (b.blur_fast_bytes(640, 480) * 3072) < 1.45  # vs the SURVEY model: 1.36
     assert b.committed_traffic(3071, "orb_blur_fast_kernel") is None

@@ -20,7 +20,7 @@ W, H = 640, 480
 allf = synth.device_sequence(max(batches), W, H, 0, "cuda")
 lib = plvi.load()
 names = ["disp", "drop", "regrow", "exact", "trivial", "spec_ok", "walk_cyc", "wgrow_cyc", "walks", "blocked",
-         "kern_cyc", "spec_cyc", "idle"]
+         "kern_cyc", "spec_cyc", "idle", "blocks", "setup16", "round16"]
 for B in batches:
     for mw in (0, 256):
         os.environ["PLVI_GROW_MW"] = str(mw)
@@ -42,6 +42,7 @@ for B in batches:
             a = s.cpu().numpy().reshape(B, 2, 16).mean(axis=0)
             for o in range(2):
                 line += f" | oct{o} " + " ".join(f"{n}={a[o, i]:.0f}" for i, n in enumerate(names))
+                line += f" setup/blk={16 * a[o, 14] / max(a[o, 13], 1):.0f} round/blk={16 * a[o, 15] / max(a[o, 13], 1):.0f}"
         assert lx.errors() == 0
         print(line, flush=True)
         lx.close()

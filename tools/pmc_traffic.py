@@ -9,7 +9,7 @@ with the widths the kernels use and give the bytes-per-counted-byte factor:
   reads  of lsd_prep_kernel:      dword loads  -> calib_dword_read
   writes of lsd_prep_kernel:      4/8-B stores -> calib_dword_copy / calib_dwordx2_store (mean)
 Writes profiles/<round>/pmc_traffic.json (a list, one entry per kernel) for bench.py.
-usage: python tools/pmc_traffic.py <pmc_dir> profiles/r02 BATCH CAL_BYTES"""
+usage: python tools/pmc_traffic.py <pmc_dir> profiles/r03 BATCH CAL_BYTES"""
 import csv
 import json
 import pathlib
@@ -43,13 +43,14 @@ def main():
     for k, fr, fw in (("orb_blur_fast_kernel", f_rd, f_wr4), ("lsd_prep_kernel", f_rd, (f_wr4 + f_wr8) / 2)):
         if k not in fe or k not in wr:
             continue
-        if k == "lsd_prep_kernel":  # two launches per batch (octaves): per-batch sum of the first pair
-            rf, rw = fe[k][0] + fe[k][1], wr[k][0] + wr[k][1]
+        if k == "lsd_prep_kernel":  # two launches per batch (octaves): mean of the first pair
+            rf, rw = (fe[k][0] + fe[k][1]) / 2, (wr[k][0] + wr[k][1]) / 2
         else:
             rf, rw = mean(fe[k]), mean(wr[k])
         entries.append({"kernel": k, "batch": batch, "dispatches": [len(fe[k]), len(wr[k])],
                         "fetch_bytes_raw": rf, "write_bytes_raw": rw,
                         "fetch_bytes": rf * fr, "write_bytes": rw * fw, "bytes_per_launch": rf * fr + rw * fw,
+                        "unit": "bytes per launch",
                         "calibration": calib})
     dst.mkdir(parents=True, exist_ok=True)
     (dst / "pmc_traffic.json").write_text(json.dumps(entries, indent=1) + "\n")
