@@ -264,12 +264,30 @@ def dry_run(args, world, rank):
     nwin = 2 if args.c4 else 1
     seq = synth.device_sequence(B + (nwin - 1) * (B - 1), W, H, seed=pdist.shard_seed(rank))
     digest = hashlib.sha256(seq[:B].numpy().tobytes()).hexdigest()[:16]
+    gather = args.c4 and world > 1 if args.gather is None else args.gather
+
+    def tables(lo):
+        # stand-ins for the per-frame tables (counts, keypoints, descriptors,
+        # line counts, keylines, LBD descriptors): fixed-capacity byte tables
+        # derived from the window's frames, the shapes TableGather sees on a GPU
+        win = seq[lo:lo + B]
+        flat = win.reshape(B, -1)
+        cnt = flat[:, :64].to(torch.int32).sum(1).to(torch.int32)
+        return (cnt, flat[:, :28 * 4].contiguous(), flat[:, -32 * 4:].contiguous(), cnt + 1,
+                flat[:, 1000:1000 + 68 * 2].contiguous(), flat[:, 2000:2000 + 32 * 2].contiguous())
+    tg = None
+    if gather:
+        tg = pdist.TableGather([t.numel() * t.element_size() for t in tables(0)], world, rank)
     pdist.barrier(world)
     t0 = time.perf_counter()
     sums = 0
     for k in range(args.steps):
         lo = (k % nwin) * (B - 1)
         sums += int(seq[lo:lo + B].to(torch.int64).sum())
+        if tg is not None:
+            tg.post(tables(lo))
+    if tg is not None:
+        tg.wait()
     el = pdist.max_over_ranks(time.perf_counter() - t0, world)
     new = (B - 1) if args.c4 else B
     total = pdist.sum_over_ranks(new * args.steps, world)
@@ -278,9 +296,21 @@ def dry_run(args, world, rank):
         import torch.distributed as dist
         digests = [None] * world
         dist.all_gather_object(digests, digest)
+    gathered = None
+    if tg is not None:
+        # the last step's tables of every rank, as rank 0 received them, next
+        # to each rank's own digest of the same tables
+        own = pdist.tables_digest(tables(((args.steps - 1) % nwin) * (B - 1)))
+        owns = [own]
+        if world > 1:
+            owns = [None] * world
+            dist.all_gather_object(owns, own)
+        gathered = {"posts": tg.posted, "rank_tables": owns,
+                    "received": tg.digests() if rank == 0 else None}
     if rank == 0:
         print(json.dumps({"metric": METRIC, "dry_run": True, "n_gpus": world, "steps": args.steps,
                           "frames_total": total, "max_rank_s": el, "rank_digests": digests,
+                          "gather": gathered,
                           "config": {"batch": B, "width": W, "height": H, "c4": bool(args.c4)}}), flush=True)
     if world > 1:
         import torch.distributed as dist
@@ -365,10 +395,9 @@ def run(args, world, rank):
     # LSD front (prep, region growing) overlaps batch k's ORB tail.  Every step
     # still extracts and matches its full batch inside the timed region.
     tab_sizes = None
-    recv = None
 
     def make_slot():
-        nonlocal tab_sizes, recv
+        nonlocal tab_sizes
         sl = types.SimpleNamespace()
         sl.orb = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=B, device=dev)
         sl.lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=B, device=dev)
@@ -380,13 +409,17 @@ def run(args, world, rank):
         sl.lnm = torch.empty(B - 1, **i32)
         sl.stream = torch.cuda.Stream()  # non-default: the legacy null stream would serialise
         sl.st = sl.stream.cuda_stream
-        # C4 gather: tables staged on the slot's stream, then one RCCL gather
-        # per table to rank 0, asynchronous (waited on before the staging is reused)
+        # C4 gather (plvi.dist.TableGather): tables staged on the slot's stream,
+        # then one asynchronous RCCL gather per table to rank 0 (waited on
+        # before the slot's staging is reused)
         tab_sizes = (4 * B, 28 * cap_ * B, 32 * cap_ * B, 4 * B, 68 * lcap_ * B, 32 * lcap_ * B)
-        sl.stage_bufs = [torch.empty(n, dtype=torch.uint8, device=cuda) for n in tab_sizes] if args.gather else []
-        if args.gather and rank == 0 and recv is None:
-            recv = [[torch.empty(n, dtype=torch.uint8, device=cuda) for _ in range(world)] for n in tab_sizes]
-        sl.pending = []
+        sl.tables = (sl.co_p, sl.kp_p, sl.de_p, sl.lco_p, sl.kl_p, sl.lde_p)
+        sl.tg = None
+        if args.gather:
+            def dev_copy(t, src, st_=sl.st):
+                if lib.plvi_memcpy_async(t.data_ptr(), src, t.numel(), 3, st_):
+                    raise RuntimeError("gather copy")
+            sl.tg = pdist.TableGather(tab_sizes, world, rank, device=cuda, copy=dev_copy)
         return sl, cap_, lcap_
 
     s0, cap, lcap = make_slot()
@@ -410,24 +443,11 @@ def run(args, world, rank):
             raise RuntimeError(f"match {rc}")
 
     def gather(sl=s0):
-        import torch.distributed as dist
-        for w_ in sl.pending:
-            w_.wait()
-        sl.pending.clear()
-        for src, t in zip((sl.co_p, sl.kp_p, sl.de_p, sl.lco_p, sl.kl_p, sl.lde_p), sl.stage_bufs):
-            if lib.plvi_memcpy_async(t.data_ptr(), src, t.numel(), 3, sl.st):
-                raise RuntimeError("gather copy")
-        with torch.cuda.stream(sl.stream):
-            for i, t in enumerate(sl.stage_bufs):
-                if world == 1:
-                    continue
-                sl.pending.append(dist.gather(t, recv[i] if rank == 0 else None, dst=0, async_op=True))
+        sl.tg.post(sl.tables, stream=sl.stream)
 
     def wait_gathers():
         for sl in slots:
-            for w_ in sl.pending:
-                w_.wait()
-            sl.pending.clear()
+            sl.tg.wait()
 
     step_no = [0]
 
@@ -577,12 +597,7 @@ def run(args, world, rank):
             wait_gathers()
             torch.cuda.synchronize()
             if rank == 0:
-                digests["gathered_tables"] = []
-                for r in range(world):
-                    g = hashlib.sha256()
-                    for i in range(len(tab_sizes)):
-                        g.update(recv[i][r].cpu().numpy().tobytes())
-                    digests["gathered_tables"].append(g.hexdigest()[:16])
+                digests["gathered_tables"] = s0.tg.digests()
     all_digests = [digests]
     if world > 1:
         import torch.distributed as dist

@@ -52,6 +52,91 @@ def sum_over_ranks(value, world, device="cpu"):
     return int(t.item())
 
 
+class TableGather:
+    """BASELINE C4's per-step collection of every rank's per-frame tables on
+    rank 0 ("RCCL gather of per-frame descriptor tables"), the
+    code bench.py runs inside its timed region.
+
+    `sizes` are the byte sizes of the tables (counts, keypoints, descriptors,
+    line counts, keylines, LBD descriptors).  `post(srcs, stream)` waits for
+    this gatherer's previous gathers, stages each source into its own byte
+    buffer (`copy(dst_tensor, src)`: a device-pointer copy on the step's
+    stream in the bench, a tensor copy on CPU) and issues one asynchronous
+    `dist.gather` per table to rank 0 on `stream` (RCCL over xGMI on GPUs,
+    gloo in the CPU tests).  Staging decouples the gather from the extractor
+    outputs, which the next step overwrites.  Rank 0 owns a receive buffer
+    per (table, rank): `received(r)` is rank r's tables, rank-major, once
+    `wait()` has returned.  At world 1 `post` only stages."""
+
+    def __init__(self, sizes, world, rank, device="cpu", copy=None):
+        import torch
+        self.world, self.rank = world, rank
+        self.sizes = tuple(int(n) for n in sizes)
+        self.stage = [torch.empty(n, dtype=torch.uint8, device=device) for n in self.sizes]
+        self.recv = None
+        if world > 1 and rank == 0:
+            self.recv = [[torch.empty(n, dtype=torch.uint8, device=device) for _ in range(world)]
+                         for n in self.sizes]
+        self.copy = copy if copy is not None else _copy_tensor
+        self.pending = []
+        self.posted = 0
+
+    def wait(self):
+        for w in self.pending:
+            w.wait()
+        self.pending.clear()
+
+    def post(self, srcs, stream=None):
+        import contextlib
+        import torch
+        if len(srcs) != len(self.stage):
+            raise ValueError(f"TableGather.post: {len(srcs)} sources for {len(self.stage)} tables")
+        self.wait()
+        for src, t in zip(srcs, self.stage):
+            self.copy(t, src)
+        self.posted += 1
+        if self.world == 1:
+            return
+        import torch.distributed as dist
+        ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
+        with ctx:
+            for i, t in enumerate(self.stage):
+                self.pending.append(dist.gather(t, self.recv[i] if self.rank == 0 else None, dst=0,
+                                                async_op=True))
+
+    def received(self, r):
+        """Rank r's staged tables as rank 0 received them (rank 0 only)."""
+        if self.world == 1:
+            return list(self.stage)
+        if self.recv is None:
+            raise RuntimeError("TableGather.received: only rank 0 receives")
+        return [self.recv[i][r] for i in range(len(self.sizes))]
+
+    def digests(self):
+        """SHA-256 (16 hex) of every rank's received tables, rank order (rank 0)."""
+        import hashlib
+        out = []
+        for r in range(self.world):
+            h = hashlib.sha256()
+            for t in self.received(r):
+                h.update(t.cpu().numpy().tobytes())
+            out.append(h.hexdigest()[:16])
+        return out
+
+
+def _copy_tensor(dst, src):
+    dst.copy_(src.contiguous().reshape(-1).view(dst.dtype))
+
+
+def tables_digest(tables):
+    """SHA-256 (16 hex) of a rank's own tables in TableGather order."""
+    import hashlib
+    h = hashlib.sha256()
+    for t in tables:
+        h.update(t.cpu().contiguous().numpy().tobytes())
+    return h.hexdigest()[:16]
+
+
 def gather_tables(tables, world):
     """SURVEY §8e / BASELINE C4: collect every rank's fixed-capacity per-frame
     tables (e.g. counts [B], keypoints [B, cap, 28 B], descriptors

@@ -33,6 +33,23 @@ def _worker(rank, world, port, q):
     gc, gd = pdist.gather_tables([counts, desc], w)
     ok = (gc.tolist() == [[1, 2], [11, 12]] and gd.shape == (2, 2, 5, 32) and int(gd[0].max()) == 7
           and int(gd[1].min()) == 8)
+    # bench.py's timed C4 gather (plvi.dist.TableGather): staged per-frame
+    # tables of several steps gathered to rank 0, rank-major, the last step's
+    # tables intact after the earlier gathers completed
+    tabs = lambda s: (torch.tensor([s, 100 * r + s], dtype=torch.int32),  # noqa: E731
+                      torch.full((3, 28), 16 * r + s, dtype=torch.uint8),
+                      torch.arange(64, dtype=torch.uint8) + r)
+    tg = pdist.TableGather([8, 84, 64], w, r)
+    for s in range(3):
+        tg.post(tabs(s))
+    tg.wait()
+    if r == 0:
+        got = [[t.clone() for t in tg.received(k)] for k in range(w)]
+        ok = ok and tg.posted == 3
+        for k in range(w):
+            ok = ok and got[k][0].view(torch.int32).tolist() == [2, 100 * k + 2]
+            ok = ok and bool((got[k][1] == 16 * k + 2).all()) and got[k][2].tolist() == list(range(k, 64 + k))
+        ok = ok and len(set(tg.digests())) == 2
     q.put((r, el, total, int(frames.astype(np.int64).sum()), ok))
     import torch.distributed as dist
     dist.destroy_process_group()
@@ -83,6 +100,10 @@ def test_bench_c4_dry_run_world2():
     """--c4: 752x480 windows with a one-frame halo (B-1 new frames per step)."""
     out = _bench("--gpus", "2", "--dry-run", "--c4", "--batch", "3", "--steps", "3")
     assert out["n_gpus"] == 2 and out["config"]["width"] == 752 and out["frames_total"] == 2 * 3 * 2
+    # the dry run drives bench.py's TableGather every step (on by default for
+    # --c4 at world > 1): rank 0 received each rank's own last-step tables
+    g = out["gather"]
+    assert g["posts"] == 3 and g["received"] == g["rank_tables"] and g["rank_tables"][0] != g["rank_tables"][1]
 
 
 def test_bench_refuses_world_mismatch():
