@@ -768,6 +768,129 @@ __global__ __launch_bounds__(256) void lsd_rect_kernel(const LineOctDev* __restr
 }
 
 // ---------------------------------------------------------------------------
+// LK3c: the same region2rect + get_theta with lane = region.  Each lane walks
+// its own region's points in region order through the reference's three
+// loops (centroid sums, inertia sums, l extents; lsd.cpp:697-744, :755-771):
+// the identical sequence of double products and adds per region, with no
+// LDS round trip and no idle lanes behind a serial lane 0.  Points and
+// weights are fetched kRectU at a time so each lane keeps several loads in
+// flight; regions of one wave are consecutive indices of one (frame, octave).
+// ---------------------------------------------------------------------------
+#ifndef PLVI_RECT_LANE_BLOCKS
+#define PLVI_RECT_LANE_BLOCKS 2
+#endif
+constexpr int kRectLaneBlocks = PLVI_RECT_LANE_BLOCKS;  // 4-wave workgroups per (octave, frame), 256 regions each
+constexpr int kRectU = 4;
+
+__global__ __launch_bounds__(256) void lsd_rect_lanes_kernel(const LineOctDev* __restrict__ octs,
+                                                             const double* __restrict__ modgrad,
+                                                             const LsdRegion* __restrict__ regs,
+                                                             const unsigned* __restrict__ regpts,
+                                                             size_t regpts_frame, const int* __restrict__ nlines,
+                                                             double prec, double scale_lsd,
+                                                             LsdLine* __restrict__ lines) {
+    const int o = blockIdx.y, f = blockIdx.z, nOct = gridDim.y;
+    const int task = f * nOct + o;
+    const int n = min(nlines[task], kLsdRawCap);
+    const LineOctDev& od = octs[o];
+    const int sw = od.sw;
+    const double* M = modgrad + od.soff + (size_t)f * od.splane;
+    const unsigned* P = regpts + (size_t)task * regpts_frame;
+    for (int k = blockIdx.x * 256 + threadIdx.x; k - (int)(threadIdx.x & 63) < n; k += gridDim.x * 256) {
+        if (k >= n) continue;
+        const LsdRegion r = regs[(size_t)task * kLsdRawCap + k];
+        const unsigned* q = P + r.start;
+        const int rn = r.n;
+        // centroid (lsd.cpp:697-705)
+        double xs = 0.0, ys = 0.0, sum = 0.0;
+        int i = 0;
+        for (; i + kRectU <= rn; i += kRectU) {
+            unsigned v[kRectU];
+            double w[kRectU];
+#pragma unroll
+            for (int u = 0; u < kRectU; ++u) v[u] = q[i + u];
+#pragma unroll
+            for (int u = 0; u < kRectU; ++u) w[u] = M[(size_t)(v[u] >> 16) * sw + (v[u] & 0xffffu)];
+#pragma unroll
+            for (int u = 0; u < kRectU; ++u) {
+                xs += (double)(int)(v[u] & 0xffffu) * w[u];
+                ys += (double)(int)(v[u] >> 16) * w[u];
+                sum += w[u];
+            }
+        }
+        for (; i < rn; ++i) {
+            const unsigned v = q[i];
+            const double w = M[(size_t)(v >> 16) * sw + (v & 0xffffu)];
+            xs += (double)(int)(v & 0xffffu) * w;
+            ys += (double)(int)(v >> 16) * w;
+            sum += w;
+        }
+        xs /= sum;
+        ys /= sum;
+        // inertia (get_theta, lsd.cpp:755-763)
+        double Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
+        i = 0;
+        for (; i + kRectU <= rn; i += kRectU) {
+            unsigned v[kRectU];
+            double w[kRectU];
+#pragma unroll
+            for (int u = 0; u < kRectU; ++u) v[u] = q[i + u];
+#pragma unroll
+            for (int u = 0; u < kRectU; ++u) w[u] = M[(size_t)(v[u] >> 16) * sw + (v[u] & 0xffffu)];
+#pragma unroll
+            for (int u = 0; u < kRectU; ++u) {
+                const double dx = (double)(int)(v[u] & 0xffffu) - xs, dy = (double)(int)(v[u] >> 16) - ys;
+                Ixx += dy * dy * w[u];
+                Iyy += dx * dx * w[u];
+                Ixy -= dx * dy * w[u];
+            }
+        }
+        for (; i < rn; ++i) {
+            const unsigned v = q[i];
+            const double w = M[(size_t)(v >> 16) * sw + (v & 0xffffu)];
+            const double dx = (double)(int)(v & 0xffffu) - xs, dy = (double)(int)(v >> 16) - ys;
+            Ixx += dy * dy * w;
+            Iyy += dx * dx * w;
+            Ixy -= dx * dy * w;
+        }
+        const double lambda = 0.5 * (Ixx + Iyy - __builtin_sqrt((Ixx - Iyy) * (Ixx - Iyy) + 4.0 * Ixy * Ixy));
+        double theta = (__builtin_fabs(Ixx) > __builtin_fabs(Iyy))
+                           ? (double)plvi_fast_atan2((float)(lambda - Ixx), (float)Ixy)
+                           : (double)plvi_fast_atan2((float)Ixy, (float)(lambda - Iyy));
+        theta *= kD2R;
+        if (angle_diff(theta, r.angle) > prec) theta += kPi;
+        const double dxv = plvi_cos(theta), dyv = plvi_sin(theta);
+        // l extents (lsd.cpp:722-735): order-free max(0, .) / min(0, .)
+        double lmax = 0, lmin = 0;
+        i = 0;
+        for (; i + kRectU <= rn; i += kRectU) {
+            unsigned v[kRectU];
+#pragma unroll
+            for (int u = 0; u < kRectU; ++u) v[u] = q[i + u];
+#pragma unroll
+            for (int u = 0; u < kRectU; ++u) {
+                const double l = ((double)(int)(v[u] & 0xffffu) - xs) * dxv + ((double)(int)(v[u] >> 16) - ys) * dyv;
+                lmax = l > lmax ? l : lmax;
+                lmin = l < lmin ? l : lmin;
+            }
+        }
+        for (; i < rn; ++i) {
+            const unsigned v = q[i];
+            const double l = ((double)(int)(v & 0xffffu) - xs) * dxv + ((double)(int)(v >> 16) - ys) * dyv;
+            lmax = l > lmax ? l : lmax;
+            lmin = l < lmin ? l : lmin;
+        }
+        double x1 = xs + lmin * dxv, y1 = ys + lmin * dyv;
+        double x2 = xs + lmax * dxv, y2 = ys + lmax * dyv;
+        x1 += 0.5; y1 += 0.5; x2 += 0.5; y2 += 0.5;
+        if (scale_lsd != 1) {
+            x1 /= scale_lsd; y1 /= scale_lsd; x2 /= scale_lsd; y2 /= scale_lsd;
+        }
+        lines[(size_t)task * kLsdRawCap + k] = LsdLine{(float)x1, (float)y1, (float)x2, (float)y2};
+    }
+}
+
+// ---------------------------------------------------------------------------
 // LK4: KeyLine assembly (LSDDetector_custom.cpp:306-346) + top-k filter
 // (LineExtractor.cc:75-84: libstdc++ std::sort by response desc, truncate,
 // class_id = i) + line equations (:106-115).  One workgroup per frame.

@@ -358,6 +358,10 @@ struct LinePipeline {
         if (growSmem > 160 * 1024) return PLVI_E_BADARG;
         for (const void* k : {(const void*)lsd_grow_kernel<false>, (const void*)lsd_grow_kernel<true>})
             PLVI_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)growSmem));
+        // region2rect: PLVI_RECT_LANES=1 (default) lane = region
+        // (lsd_rect_lanes_kernel), 0 = wave = region (lsd_rect_kernel)
+        rectLanes = true;
+        if (const char* e = getenv("PLVI_RECT_LANES")) rectLanes = atoi(e) != 0;
         // Small batches (latency): lsd_grow_mw_kernel, kMwWaves waves per
         // (frame, octave) growing regions of one frame concurrently.
         // PLVI_GROW_MW = largest batch that takes it (default 256; 0 = off).
@@ -391,6 +395,7 @@ struct LinePipeline {
         return PLVI_OK;
     }
     static constexpr int kMwWaves = 16;
+    bool rectLanes = true;
     int mwMaxFrames = 0, mwSlots = 0;
     size_t mwSmem = 0, mwOwnTask = 0;
     int* mwStats = nullptr;  // diagnostic counters (plvi_lines_debug_mw_stats)
@@ -480,10 +485,19 @@ struct LinePipeline {
     }
     void launch_grow_assemble(int nf, hipStream_t st, bool grown = false) {
         if (!grown) launch_grow(nf, 0, nOct, st);
-        hipLaunchKernelGGL(lsd_rect_kernel, dim3(kRectBlocks, nOct, nf), dim3(256), 0, st, d_oct.as<LineOctDev>(),
-                           (const double*)modg.as<double>(), (const LsdRegion*)regs.as<LsdRegion>(),
-                           (const unsigned*)regpts.as<unsigned>(), qspillFrame, (const int*)nlines.as<int>(), prec,
-                           SCALE, rawLines.as<LsdLine>());
+        if (rectLanes) {
+            // small batches spread a frame's regions over more workgroups (latency)
+            const int bx = nf <= 16 ? 8 : kRectLaneBlocks;
+            hipLaunchKernelGGL(lsd_rect_lanes_kernel, dim3(bx, nOct, nf), dim3(256), 0, st, d_oct.as<LineOctDev>(),
+                               (const double*)modg.as<double>(), (const LsdRegion*)regs.as<LsdRegion>(),
+                               (const unsigned*)regpts.as<unsigned>(), qspillFrame, (const int*)nlines.as<int>(),
+                               prec, SCALE, rawLines.as<LsdLine>());
+        } else {
+            hipLaunchKernelGGL(lsd_rect_kernel, dim3(kRectBlocks, nOct, nf), dim3(256), 0, st,
+                               d_oct.as<LineOctDev>(), (const double*)modg.as<double>(),
+                               (const LsdRegion*)regs.as<LsdRegion>(), (const unsigned*)regpts.as<unsigned>(),
+                               qspillFrame, (const int*)nlines.as<int>(), prec, SCALE, rawLines.as<LsdLine>());
+        }
         mark(3, st);
         hipLaunchKernelGGL(line_assemble_kernel, dim3(nf), dim3(256), 0, st, d_oct.as<LineOctDev>(), nOct,
                            (const LsdLine*)rawLines.as<LsdLine>(), (const int*)nlines.as<int>(), min_length,

@@ -88,3 +88,23 @@ def test_mw_flat_and_single_frame(plvi_lib, monkeypatch):
     assert len(_run(monkeypatch, flat, 256)[0][0]) == 0
     one = synth.batch(1, seed0=7)
     assert _same(_run(monkeypatch, one, 256)[0], ol.line_extract(one[0]))
+
+
+@pytest.mark.parametrize("mw", [256, 0])
+def test_rect_lane_per_region_equals_wave_per_region(plvi_lib, monkeypatch, mw):
+    """region2rect + get_theta (lsd.cpp:688-782): lsd_rect_lanes_kernel (lane =
+    region, the default) and lsd_rect_kernel (wave = region,
+    PLVI_RECT_LANES=0) give the same lines bit for bit, behind either
+    region-growing kernel; frame 0 equals the oracle.  Includes the small-batch
+    grid (8 workgroups per (frame, octave)) and the batch grid."""
+    st_ = structured_frames()
+    frames = np.concatenate([synth.batch(17, seed0=900), np.stack([st_["checker"], st_["stripes"]])])
+    for n in (2, len(frames)):
+        monkeypatch.setenv("PLVI_RECT_LANES", "1")
+        lanes = _run(monkeypatch, frames[:n], mw)
+        monkeypatch.setenv("PLVI_RECT_LANES", "0")
+        waves = _run(monkeypatch, frames[:n], mw)
+        for f in range(n):
+            assert _same(lanes[f], waves[f]), f"n={n} frame {f}: lane-per-region != wave-per-region"
+    kl, de, fn = ol.line_extract(frames[0])
+    assert _same(lanes[0], (kl.astype(plvi.KEYLINE_DTYPE), de, fn))
