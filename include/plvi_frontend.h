@@ -621,6 +621,48 @@ int plvi_stereo_lines(const plvi_keyline* klL, const uint8_t* descL, int nL, con
 int plvi_frame_extract_batch(plvi_orb_extractor* orb, plvi_line_extractor* lines, const uint8_t* d_frames,
                              int n_frames, size_t frame_stride, size_t row_stride, int lap0, int lap1, void* stream);
 
+/* ------------------------------------------------------------ initialization
+ * The monocular initializer's matchers, called on every frame until
+ * Tracking::MonocularInitialization succeeds (src/Tracking.cc:3111-3113). */
+
+/* ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12,
+ * windowSize) (src/ORBmatcher.cc:705-814). */
+typedef struct plvi_init_params {
+  float min_x, min_y, inv_w, inv_h; /* F2.mnMinX, mnMinY, mfGridElementWidthInv / HeightInv */
+  int window;                       /* windowSize (100 in MonocularInitialization) */
+  float nnratio;                    /* ORBmatcher(0.9, true): mfNNratio */
+  int check_orientation;            /* mbCheckOrientation */
+} plvi_init_params;
+
+/* Batched over n_pairs (F1 = mInitialFrame, F2 = mCurrentFrame) pairs.
+ * F1 p: keypoints (mvKeysUn) / descriptors [p][cap1] (counts d_n1) and
+ * vbPrevMatched as float2 [p][cap1] (in/out: matched entries become
+ * F2.mvKeysUn[vnMatches12[i1]].pt, as the reference updates them); F2 p:
+ * keypoints / descriptors [p][cap2] (counts d_n2) and the grid CSR from
+ * plvi_assign_grid_batch over the same keypoints.  Output vnMatches12
+ * [p][cap1] (first n1 entries) and nmatches [p].  cap1, cap2 <= 65535 and
+ * ~24 B per F1 + ~19 B per F2 keypoint + 12 KB of LDS <= 160 KB.
+ * Replaces ORBmatcher.h:71 (SearchForInitialization). */
+int plvi_search_for_initialization_batch(int n_pairs, const plvi_init_params* p, const plvi_keypoint* d_kps1,
+                                         const uint8_t* d_desc1, const int* d_n1, int cap1, float* d_prev_matched,
+                                         const plvi_keypoint* d_kps2, const uint8_t* d_desc2, const int* d_n2,
+                                         int cap2, const int* d_cell_off, const int* d_cell_idx, int* d_matches12,
+                                         int* d_nmatches, void* stream);
+
+/* LineMatcher::SerachForInitialize(InitialFrame, CurrentFrame, LineMatches)
+ * (src/LineMatcher.cpp:113-139) with Frame::lineDescriptorMAD
+ * (src/Frame.cc:1089-1112): knnMatch(k=2) of the initial frame's LBD
+ * descriptors [p][cap1] (counts d_n1) against the current frame's [p][cap2],
+ * then the pairs whose d1 - d0 exceeds 0.5 * nn12_mad.  Output LineMatches
+ * as int2 (query, train) [p][cap1] in query order, their count [p], and
+ * (nullable) {nn_mad, nn12_mad} as double [p][2].  d_scratch holds
+ * 4 * n_pairs * cap1 ints.  The reference reads lmatches[0] and [i][1]:
+ * with no query lines or fewer than 2 train lines it is undefined; here the
+ * pair gets 0 matches.  Replaces LineMatcher.h:95 (SerachForInitialize). */
+int plvi_line_search_init_batch(const uint8_t* d_desc1, const int* d_n1, int cap1, const uint8_t* d_desc2,
+                                const int* d_n2, int cap2, int n_pairs, int* d_scratch, int* d_pairs, int* d_npairs,
+                                double* d_mad, void* stream);
+
 /* Device memory helpers for bindings that have no HIP runtime of their own
  * (ctypes, JNI): thin wrappers over hipMalloc/hipFree/hipMemcpy on the
  * current device.  kind: 1 = host->device, 2 = device->host, 3 = d->d. */

@@ -8,6 +8,7 @@
 //   LineMatcher::matchNNR / match  src/LineMatcher.cpp:41-111
 //   ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...)  src/ORBmatcher.cc:269-471
 //   LineMatcher::matchGrid  src/LineMatcher.cpp:191-272 (+ gridStructure.cpp:64-75)
+#include <algorithm>
 #include <stdexcept>
 #include <climits>
 #include <cmath>
@@ -420,4 +421,81 @@ extern "C" int oracle_line_search_projection(
         }
     }
     return matches;
+}
+
+// LineMatcher::SerachForInitialize (src/LineMatcher.cpp:113-139) with
+// Frame::lineDescriptorMAD (src/Frame.cc:1089-1112) and the comparators of
+// include/LineMatcher.h:56-76, on std::vector<std::vector<DMatch>> as the
+// reference holds them (knnMatch k = 2 of the initial frame's lines against
+// the current frame's).  Outputs the LineMatches pairs (query, train) in
+// order; mad = {nn_mad, nn12_mad}.  The reference indexes [0] and [1] of
+// every knnMatch list: with n1 == 0 or n2 < 2 it is undefined, here 0 pairs.
+namespace {
+struct DMatchO {
+    int queryIdx, trainIdx, imgIdx;
+    float distance;
+};
+typedef std::vector<std::vector<DMatchO>> MatchLists;
+struct ByNN {
+    bool operator()(const std::vector<DMatchO>& a, const std::vector<DMatchO>& b) const {
+        return a[0].distance < b[0].distance;
+    }
+};
+struct ByNN12Desc {
+    bool operator()(const std::vector<DMatchO>& a, const std::vector<DMatchO>& b) const {
+        return (a[1].distance - a[0].distance) > (b[1].distance - b[0].distance);
+    }
+};
+struct ByQuery {
+    bool operator()(const std::vector<DMatchO>& a, const std::vector<DMatchO>& b) const {
+        return a[0].queryIdx < b[0].queryIdx;
+    }
+};
+void line_descriptor_mad(MatchLists matches, double& nn_mad, double& nn12_mad) {
+    MatchLists matches_nn = matches, matches_12 = matches;
+    std::sort(matches_nn.begin(), matches_nn.end(), ByNN());
+    const double nn_dist_median = matches_nn[int(matches_nn.size() / 2)][0].distance;
+    for (unsigned int i = 0; i < matches_nn.size(); i++)
+        matches_nn[i][0].distance = fabsf(matches_nn[i][0].distance - nn_dist_median);
+    std::sort(matches_nn.begin(), matches_nn.end(), ByNN());
+    nn_mad = 1.4826 * matches_nn[int(matches_nn.size() / 2)][0].distance;
+    std::sort(matches_12.begin(), matches_12.end(), ByNN12Desc());
+    const double nn12_dist_median = matches_12[int(matches_12.size() / 2)][1].distance -
+                                    matches_12[int(matches_12.size() / 2)][0].distance;
+    for (unsigned int j = 0; j < matches_12.size(); j++)
+        matches_12[j][0].distance = fabsf(matches_12[j][1].distance - matches_12[j][0].distance - nn12_dist_median);
+    std::sort(matches_12.begin(), matches_12.end(), ByNN());
+    nn12_mad = 1.4826 * matches_12[int(matches_12.size() / 2)][0].distance;
+}
+}  // namespace
+
+extern "C" int oracle_line_search_init(const uint8_t* d1, int n1, const uint8_t* d2, int n2, int* q_out, int* t_out,
+                                       double* mad) {
+    if (n1 <= 0 || n2 < 2) return 0;
+    std::vector<int> i0(n1), a(n1), i1(n1), b(n1);
+    oracle_knn2(d1, n1, d2, n2, i0.data(), a.data(), i1.data(), b.data());
+    MatchLists lmatches(n1);
+    for (int i = 0; i < n1; ++i) {
+        lmatches[i].push_back(DMatchO{i, i0[i], 0, (float)a[i]});
+        lmatches[i].push_back(DMatchO{i, i1[i], 0, (float)b[i]});
+    }
+    double nn_dist_th, nn12_dist_th;
+    line_descriptor_mad(lmatches, nn_dist_th, nn12_dist_th);
+    if (mad) {
+        mad[0] = nn_dist_th;
+        mad[1] = nn12_dist_th;
+    }
+    nn12_dist_th = nn12_dist_th * 0.5;
+    std::sort(lmatches.begin(), lmatches.end(), ByQuery());
+    int nmatches = 0;
+    for (int i = 0; i < (int)lmatches.size(); i++) {
+        const int qdx = lmatches[i][0].queryIdx, tdx = lmatches[i][0].trainIdx;
+        const double dist_12 = lmatches[i][1].distance - lmatches[i][0].distance;
+        if (dist_12 > nn12_dist_th) {
+            q_out[nmatches] = qdx;
+            t_out[nmatches] = tdx;
+            nmatches++;
+        }
+    }
+    return nmatches;
 }

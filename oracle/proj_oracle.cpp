@@ -13,6 +13,7 @@
 //   Pinhole::project                 src/CameraModels/Pinhole.cpp:30-39
 // The pose product x3Dc = Rcw*x3Dw + tcw (cv::Mat) is an input: it is taken
 // from the caller, as the drop-in shim keeps it on the host.
+#include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -293,5 +294,92 @@ extern "C" int oracle_search_local(int n_cur, const float* cx_, const float* cy_
             }
         }
     }
+    return nmatches;
+}
+
+// ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12,
+// windowSize) (src/ORBmatcher.cc:705-814), the monocular initializer's matcher
+// (Tracking::MonocularInitialization, Tracking.cc:3023/3111: ORBmatcher(0.9,
+// true), windowSize 100).  F1 = mInitialFrame.mvKeysUn (x, y, octave, angle)
+// + mDescriptors; prev_xy = vbPrevMatched (in/out, [n1][2]); F2 =
+// mCurrentFrame.mvKeysUn + mDescriptors, its mGrid built by
+// AssignFeaturesToGrid from the same keypoints.  Output m12 = vnMatches12
+// [n1]; returns nmatches.
+extern "C" int oracle_search_for_initialization(int n1, const float* x1, const float* y1, const int* oct1,
+                                                const float* ang1, const uint8_t* desc1, float* prev_xy, int n2,
+                                                const float* x2, const float* y2, const int* oct2, const float* ang2,
+                                                const uint8_t* desc2, float minX, float minY, float invW, float invH,
+                                                int windowSize, float nnratio, int check_ori, int* m12) {
+    const int TH_LOW = 50;
+    const std::vector<Kp> K1 = make_kps(n1, x1, y1, oct1, ang1), K2 = make_kps(n2, x2, y2, oct2, ang2);
+    Grid g;
+    assign_grid(K2, minX, minY, invW, invH, g);
+    int nmatches = 0;
+    std::vector<int> vnMatches12(n1, -1);
+    std::vector<int> rotHist[kHisto];
+    for (int i = 0; i < kHisto; i++) rotHist[i].reserve(500);
+    const float factor = 1.0f / kHisto;
+    std::vector<int> vMatchedDistance(n2, INT_MAX);
+    std::vector<int> vnMatches21(n2, -1);
+    for (int i1 = 0; i1 < n1; i1++) {
+        const Kp kp1 = K1[i1];
+        const int level1 = kp1.octave;
+        if (level1 > 0) continue;
+        const float px = prev_xy[2 * i1], py = prev_xy[2 * i1 + 1];
+        const float r = (float)windowSize;
+        std::vector<size_t> vIndices2 = features_in_area(g, K2, minX, minY, invW, invH, px, py, r, level1, level1);
+        if (vIndices2.empty()) continue;
+        int bestDist = INT_MAX, bestDist2 = INT_MAX, bestIdx2 = -1;
+        for (size_t i2 : vIndices2) {
+            const int dist = dist256(desc1 + (size_t)32 * i1, desc2 + (size_t)32 * i2);
+            if (vMatchedDistance[i2] <= dist) continue;
+            if (dist < bestDist) {
+                bestDist2 = bestDist;
+                bestDist = dist;
+                bestIdx2 = (int)i2;
+            } else if (dist < bestDist2) {
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= TH_LOW) {
+            if (bestDist < (float)bestDist2 * nnratio) {
+                if (vnMatches21[bestIdx2] >= 0) {
+                    vnMatches12[vnMatches21[bestIdx2]] = -1;
+                    nmatches--;
+                }
+                vnMatches12[i1] = bestIdx2;
+                vnMatches21[bestIdx2] = i1;
+                vMatchedDistance[bestIdx2] = bestDist;
+                nmatches++;
+                if (check_ori) {
+                    float rot = K1[i1].angle - K2[bestIdx2].angle;
+                    if (rot < 0.0) rot += 360.0f;
+                    int bin = (int)std::round(rot * factor);
+                    if (bin == kHisto) bin = 0;
+                    rotHist[bin].push_back(i1);
+                }
+            }
+        }
+    }
+    if (check_ori) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        three_maxima(rotHist, kHisto, ind1, ind2, ind3);
+        for (int i = 0; i < kHisto; i++) {
+            if (i == ind1 || i == ind2 || i == ind3) continue;
+            for (size_t j = 0; j < rotHist[i].size(); j++) {
+                const int idx1 = rotHist[i][j];
+                if (vnMatches12[idx1] >= 0) {
+                    vnMatches12[idx1] = -1;
+                    nmatches--;
+                }
+            }
+        }
+    }
+    for (int i1 = 0; i1 < n1; i1++)
+        if (vnMatches12[i1] >= 0) {
+            prev_xy[2 * i1] = K2[vnMatches12[i1]].x;
+            prev_xy[2 * i1 + 1] = K2[vnMatches12[i1]].y;
+        }
+    for (int i1 = 0; i1 < n1; i1++) m12[i1] = vnMatches12[i1];
     return nmatches;
 }

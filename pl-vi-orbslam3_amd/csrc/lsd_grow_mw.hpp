@@ -44,10 +44,24 @@ constexpr int kMwSP = 64;           // points of a slot kept in LDS
 constexpr int kMwSlotSpill = 2048;  // points of a slot beyond kMwSP (global)
 constexpr int kMwMaxSlots = 128;
 constexpr int kMwLog = 256;         // dispatch log entries (seed order)
+#ifndef PLVI_MW_LOOK
+#define PLVI_MW_LOOK 16
+#endif
+// wave priorities (s_setprio) of the walker and the speculative growers: the
+// walk is the critical path, the growers fill the issue slots it leaves
+#ifndef PLVI_MW_WALKER_PRIO
+#define PLVI_MW_WALKER_PRIO 3
+#endif
+#ifndef PLVI_MW_GROWER_PRIO
+#define PLVI_MW_GROWER_PRIO 3
+#endif
+constexpr int kMwLook = PLVI_MW_LOOK;  // dispatch-log entries ahead of the walk that growers revalidate (0 = off)
 
 // slot states; COMMITTED: validated and committed, a grower still copies
-// its points out (regions of more than kMwSP points)
-enum : int { kMwFree = 0, kMwGrowing = 1, kMwDone = 2, kMwCommitted = 3, kMwCopying = 4 };
+// its points out (regions of more than kMwSP points); WALKING: the walker
+// validates it (claimed from DONE by compare-and-swap, like a grower's
+// revalidation, which holds it as GROWING)
+enum : int { kMwFree = 0, kMwGrowing = 1, kMwDone = 2, kMwCommitted = 3, kMwCopying = 4, kMwWalking = 5 };
 
 struct MwSlot {
     int seed;   // bit index y * (wpr * 32) + x
@@ -56,13 +70,15 @@ struct MwSlot {
     float deg;  // final region angle (float degrees)
     int ovf;    // queue overflow: the walker regrows it
     int out;    // COMMITTED: offset of its points in the task's point list
-    int pad[2];
+    int chk;    // ctl->ncommit when the region was last grown / found valid
+    int pad;
 };
 constexpr int kMwSlotBytes = sizeof(MwSlot) + 4 * kMwSP;
 // control block (LDS)
 struct MwCtl {
     int lock, dlock, head, cursor, finished, npts, nout, overflow;
-    int dlog_n, wptr, pad0, pad1;  // dispatch log: entries appended / next entry the walk examines
+    int dlog_n, wptr, ncommit, pad1;  // dispatch log: entries appended / next entry the walk examines;
+                                      // regions committed so far (revalidation epoch)
     int stat[16];  // [0] dispatched [1] dropped [2] regrown [3] exact (undispatched) [4] trivial [5] committed
                    // speculative [6] walk cycles [7] walker growth cycles [8] walk entries [9] blocked on a
                    // growing head [10] kernel cycles (wave 0) [11] speculative growth cycles (sum over waves)
@@ -376,7 +392,20 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
         int si = -1;
         if (wp < dn && dlog[2 * (wp & (kMwLog - 1))] == q) si = dlog[2 * (wp & (kMwLog - 1)) + 1];
         lds_slot* S = si >= 0 ? mw_slot(pool, si) : nullptr;
-        const int sst = si >= 0 ? mw_lds_load(&S->state) : kMwFree;
+        int sst = si >= 0 ? mw_lds_load(&S->state) : kMwFree;
+        if (sst == kMwDone) {
+            // claim it against a grower's revalidation
+            int got = 0;
+            mw_cfence();
+            if (lane == 0) {
+                int e = kMwDone;
+                got = __hip_atomic_compare_exchange_strong(&S->state, &e, kMwWalking, __ATOMIC_RELAXED,
+                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ? 1 : 0;
+            }
+            got = __builtin_amdgcn_readfirstlane(got);
+            mw_cfence();
+            if (!got) sst = kMwGrowing;
+        }
         if (sst == kMwGrowing) {  // wait for it
             if (STATS && lane == 0) mw_stat(ctl, 9, 1);
             blocked = si;
@@ -386,7 +415,7 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
         int n = 0;
         bool done = false;
         if (sst == kMwDone) {
-            // validate (none of its pixels committed by an earlier region) and
+            // (now WALKING) validate (none of its pixels committed by an earlier region) and
             // commit; the first kMwSP points stay in registers
             n = S->n;
             const float deg = S->deg;
@@ -433,7 +462,10 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
                 }
                 if (STATS && lane == 0) mw_stat(ctl, 5, 1);
                 mw_wave_sync();
-                if (lane == 0) mw_lds_store(&S->state, st_next);
+                if (lane == 0) {
+                    mw_lds_store(&ctl->ncommit, ctl->ncommit + 1);
+                    mw_lds_store(&S->state, st_next);
+                }
                 done = true;
             } else {
                 if (STATS && lane == 0) mw_stat(ctl, 2, 1);
@@ -457,6 +489,8 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
                 const unsigned v = mw_qget(XQ, j);
                 mw_or(E.C, E.wpr, (int)(v & 0xffffu), (int)(v >> 16));
             }
+            mw_wave_sync();
+            if (lane == 0) mw_lds_store(&ctl->ncommit, ctl->ncommit + 1);
             // region2rect input for lsd_rect_kernel (flsd :500-518 order)
             if (n >= min_reg) {
                 const int nout = ctl->nout, npts = ctl->npts;
@@ -539,6 +573,7 @@ __device__ __forceinline__ int mw_dispatch(const MwEnv& E, lds_u8* pool, int nsl
         if (STATS && S->state == kMwDone) mw_stat(ctl, 1, 1);  // a passed region, dropped
         S->seed = q;
         S->ovf = 0;
+        S->chk = ctl->ncommit;
         S->state = kMwGrowing;  // before the log entry that names it
         ctl->cursor = q + 1;
         dlog[2 * (dn & (kMwLog - 1))] = q;
@@ -646,7 +681,7 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
     if (threadIdx.x == 0) {
         ctl->lock = ctl->dlock = ctl->head = ctl->cursor = ctl->finished = 0;
         ctl->npts = ctl->nout = ctl->overflow = 0;
-        ctl->dlog_n = ctl->wptr = 0;
+        ctl->dlog_n = ctl->wptr = ctl->ncommit = 0;
         for (int i = 0; i < 16; ++i) ctl->stat[i] = 0;
     }
     __syncthreads();
@@ -654,6 +689,7 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
     if (wv == 0) {
         // ---- the walker: resolves seeds in raster order, waits on the head
         // seed's region while it grows
+        __builtin_amdgcn_s_setprio(PLVI_MW_WALKER_PRIO);
         while (true) {
             const unsigned long long tw0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
             const int b = mw_walk<STATS>(E, pool, dlog, sspill, GQ, min_reg, outR, outP, lane);
@@ -666,6 +702,7 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
         }
     } else {
         // ---- growers
+        __builtin_amdgcn_s_setprio(PLVI_MW_GROWER_PRIO);
         while (true) {
             // copy out a committed long region (the walker wrote its record)
             int cs = -1;
@@ -689,6 +726,80 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
                 continue;
             }
             if (mw_lds_load(&ctl->finished)) break;
+            // revalidate one of the regions the walk reaches next (the first
+            // kMwLook dispatch-log entries after it) that was grown or checked
+            // before the latest commit: one whose pixels an earlier region has
+            // since taken is regrown here, off the walker's path (the walker
+            // still validates every region it commits)
+            if (kMwLook > 0) {
+                int rs = -1;
+                if (mw_try_lock(&ctl->dlock, lane)) {
+                    const int wp = mw_lds_load(&ctl->wptr), dn = ctl->dlog_n;
+                    const int nc = mw_lds_load(&ctl->ncommit), head = mw_lds_load(&ctl->head);
+                    const int j = wp + lane;
+                    int sj = -1;
+                    bool ok = false;
+                    if (lane < kMwLook && j < dn) {
+                        const int e = j & (kMwLog - 1);
+                        sj = dlog[2 * e + 1];
+                        lds_slot* S = mw_slot(pool, sj);
+                        ok = S->state == kMwDone && S->seed == dlog[2 * e] && S->seed >= head && S->chk < nc;
+                    }
+                    const unsigned long long b = __ballot(ok);
+                    if (b) {
+                        const int cand = readlane_i(sj, __ffsll((long long)b) - 1);
+                        int got = 0;
+                        if (lane == 0) {
+                            int e = kMwDone;
+                            got = __hip_atomic_compare_exchange_strong(&mw_slot(pool, cand)->state, &e, kMwGrowing,
+                                                                        __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_WORKGROUP) ? 1 : 0;
+                        }
+                        if (__builtin_amdgcn_readfirstlane(got)) rs = cand;
+                    }
+                    mw_unlock(&ctl->dlock, lane);
+                }
+                if (rs >= 0) {
+                    lds_slot* S = mw_slot(pool, rs);
+                    const int nc0 = mw_lds_load(&ctl->ncommit);
+                    const int seed = S->seed, n0 = S->n;
+                    const int sx = seed % E.rowbits, sy = seed / E.rowbits;
+                    const MwQueue Q = mw_slot_queue(pool, sspill, rs);
+                    bool bad = false;
+                    for (int k = lane; k < n0; k += 64) {
+                        const unsigned v = mw_qget(Q, k);
+                        bad |= mw_bit(E.C, E.wpr, (int)(v & 0xffffu), (int)(v >> 16));
+                    }
+                    int nst = kMwDone;
+                    if (mw_bit(E.C, E.wpr, sx, sy)) {
+                        nst = kMwFree;  // the seed itself was taken: the walk never visits it
+                    } else if (__ballot(bad) == 0ull) {
+                        if (lane == 0) S->chk = nc0;
+                    } else {
+                        int n = 0;
+                        float deg = 0.f;
+                        bool spilled = false;
+                        const unsigned long long ts0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
+                        int rc = mw_grow<true, STATS>(E, sx, sy, GQ, n, deg, spilled, lane);
+                        mw_own_clear(E, sy, GQ, n, spilled, lane);
+                        if (rc == 0) {
+                            if (n > kMwSP + kMwSlotSpill) rc = 2;
+                            else mw_copy_points(GQ, Q, n, lane);
+                        }
+                        if (STATS && lane == 0) mw_stat(ctl, 11, (int)(__builtin_amdgcn_s_memtime() - ts0));
+                        if (lane == 0) {
+                            S->n = n;
+                            S->deg = deg;
+                            S->ovf = rc == 2 ? 1 : 0;
+                            S->chk = nc0;
+                        }
+                        nst = rc == 1 ? kMwFree : kMwDone;
+                    }
+                    mw_wave_sync();
+                    if (lane == 0) mw_lds_store(&S->state, nst);
+                    continue;
+                }
+            }
             // a new speculative region
             int q = -1, si = -1;
             if (mw_try_lock(&ctl->dlock, lane)) {
@@ -723,6 +834,17 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
         }
     }
     __syncthreads();
+    // copy out the long regions committed after the last growers' copy-out
+    // scans (a grower skips its scan while another holds dlock, so every
+    // grower can miss a region committed just before the walk finishes)
+    for (int si = wv; si < nslots; si += NW) {
+        lds_slot* S = mw_slot(pool, si);
+        if (S->state == kMwCommitted) {
+            const MwQueue Q = mw_slot_queue(pool, sspill, si);
+            const int n = S->n, out = S->out;
+            for (int k = lane; k < n; k += 64) outP[out + k] = mw_qget(Q, k);
+        }
+    }
     if (threadIdx.x == 0) {
         nlines[task] = ctl->nout;
         if (ctl->overflow) atomicOr(err + f, 4);

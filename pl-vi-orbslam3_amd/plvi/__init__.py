@@ -104,6 +104,13 @@ class ProjParams(ctypes.Structure):
                 ("scale_factors", ctypes.c_float * 16)]
 
 
+class InitParams(ctypes.Structure):
+    """plvi_init_params (include/plvi_frontend.h): ORBmatcher::SearchForInitialization."""
+    _fields_ = [("min_x", ctypes.c_float), ("min_y", ctypes.c_float), ("inv_w", ctypes.c_float),
+                ("inv_h", ctypes.c_float), ("window", ctypes.c_int), ("nnratio", ctypes.c_float),
+                ("check_orientation", ctypes.c_int)]
+
+
 class LocalParams(ctypes.Structure):
     """plvi_local_params (include/plvi_frontend.h): ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>...)."""
     _fields_ = [("min_x", ctypes.c_float), ("min_y", ctypes.c_float), ("inv_w", ctypes.c_float),
@@ -200,6 +207,8 @@ def _declare(lib):
         "plvi_image_bounds": ([V, I, I, V], I),
         "plvi_search_by_projection_batch": ([I, V, V, V, V, I, V, V, V, V, V, V, V, V, V, V, I, V, V, V], I),
         "plvi_search_by_projection": ([V, V, V, I, V, V, V, V, V, V, V, I, V], I),
+        "plvi_search_for_initialization_batch": ([I, V, V, V, V, I, V, V, V, V, I, V, V, V, V, V], I),
+        "plvi_line_search_init_batch": ([V, V, I, V, V, I, I, V, V, V, V, V], I),
         "plvi_search_local_batch": ([I, V, V, V, V, I, V, V, V, V, V, V, V, V, V, I, V, V, V], I),
         "plvi_search_local": ([V, V, V, I, V, V, V, V, V, V, I, V], I),
         "plvi_line_search_projection_batch": ([I, V, V, V, V, V, I, V, V, I, V, V, V, V, V, I, V, V, V, V], I),
@@ -892,6 +901,89 @@ def assign_grid_batch(d_kps, d_count, cap, n_frames, grid, d_cell_off, d_cell_id
                                          ctypes.byref(grid), ctypes.c_void_p(d_cell_off),
                                          ctypes.c_void_p(d_cell_idx), ctypes.c_void_p(stream or 0)),
            "plvi_assign_grid_batch")
+
+
+# ------------------------------------------------------- initialization
+def search_for_initialization_batch(n_pairs, params, d_kps1, d_desc1, d_n1, cap1, d_prev, d_kps2, d_desc2, d_n2, cap2,
+                                    d_cell_off, d_cell_idx, d_m12, d_nm, stream=None):
+    """ORBmatcher::SearchForInitialization (src/ORBmatcher.cc:705-814) over device pair tables."""
+    V = ctypes.c_void_p
+    _check(load().plvi_search_for_initialization_batch(n_pairs, ctypes.byref(params), V(d_kps1), V(d_desc1), V(d_n1),
+                                                       cap1, V(d_prev), V(d_kps2), V(d_desc2), V(d_n2), cap2,
+                                                       V(d_cell_off), V(d_cell_idx), V(d_m12), V(d_nm),
+                                                       V(stream or 0)),
+           "plvi_search_for_initialization_batch")
+
+
+def search_for_initialization(kps1, desc1, prev_xy, kps2, desc2, width=640, height=480, window=100, nnratio=0.9,
+                              check_orientation=True, grid=None):
+    """One (F1, F2) pair from host arrays (keypoints in KEYPOINT_DTYPE = mvKeysUn,
+    descriptors n x 32, prev_xy = vbPrevMatched n1 x 2): returns (nmatches,
+    vnMatches12, updated vbPrevMatched).  grid = (min_x, min_y, inv_w, inv_h)
+    (default: the Frame grid of an undistorted width x height image)."""
+    n1, n2 = len(kps1), len(kps2)
+    if grid is None:
+        g = grid_geometry(width, height)
+        grid = (g[0], g[2], g[4], g[5])
+    p = InitParams(float(grid[0]), float(grid[1]), float(grid[2]), float(grid[3]), int(window), float(nnratio),
+                   int(bool(check_orientation)))
+    c1, c2 = max(n1, 1), max(n2, 1)
+    k1 = np.zeros(c1, KEYPOINT_DTYPE)
+    k1[:n1] = kps1
+    k2 = np.zeros(c2, KEYPOINT_DTYPE)
+    k2[:n2] = kps2
+    d1 = np.zeros((c1, 32), np.uint8)
+    d1[:n1] = desc1
+    d2 = np.zeros((c2, 32), np.uint8)
+    d2[:n2] = desc2
+    pv = np.zeros((c1, 2), np.float32)
+    pv[:n1] = prev_xy
+    bufs = [DeviceBuffer(a.nbytes) for a in (k1, d1, pv, k2, d2)]
+    for b, a in zip(bufs, (k1, d1, pv, k2, d2)):
+        b.upload(a)
+    cnt = DeviceBuffer(16)
+    cnt.upload(np.array([n1, n2, 0, 0], np.int32))
+    co = DeviceBuffer(4 * 3073)
+    ci = DeviceBuffer(4 * c2)
+    m = DeviceBuffer(4 * c1)
+    assign_grid_batch(bufs[3].ptr, cnt.ptr + 4, c2, 1, GridParams(*[float(v) for v in grid]), co.ptr, ci.ptr)
+    search_for_initialization_batch(1, p, bufs[0].ptr, bufs[1].ptr, cnt.ptr, c1, bufs[2].ptr, bufs[3].ptr, bufs[4].ptr,
+                                    cnt.ptr + 4, c2, co.ptr, ci.ptr, m.ptr, cnt.ptr + 8)
+    load().plvi_device_synchronize()
+    out = cnt.download(np.zeros(4, np.int32))
+    return int(out[2]), m.download(np.zeros(c1, np.int32))[:n1], bufs[2].download(np.zeros((c1, 2), np.float32))[:n1]
+
+
+def line_search_init_batch(d_desc1, d_n1, cap1, d_desc2, d_n2, cap2, n_pairs, d_scratch, d_pairs, d_npairs, d_mad=0,
+                           stream=None):
+    """LineMatcher::SerachForInitialize + Frame::lineDescriptorMAD over device pair tables."""
+    V = ctypes.c_void_p
+    _check(load().plvi_line_search_init_batch(V(d_desc1), V(d_n1), cap1, V(d_desc2), V(d_n2), cap2, n_pairs,
+                                              V(d_scratch), V(d_pairs), V(d_npairs), V(d_mad), V(stream or 0)),
+           "plvi_line_search_init_batch")
+
+
+def line_search_init(desc1, desc2):
+    """One pair from host arrays: returns (LineMatches as an n x 2 int array
+    (query, train), (nn_mad, nn12_mad))."""
+    n1, n2 = len(desc1), len(desc2)
+    c1, c2 = max(n1, 1), max(n2, 1)
+    d1 = np.zeros((c1, 32), np.uint8)
+    d1[:n1] = desc1
+    d2 = np.zeros((c2, 32), np.uint8)
+    d2[:n2] = desc2
+    b1, b2 = DeviceBuffer(d1.nbytes), DeviceBuffer(d2.nbytes)
+    b1.upload(d1)
+    b2.upload(d2)
+    cnt = DeviceBuffer(16)
+    cnt.upload(np.array([n1, n2, 0, 0], np.int32))
+    scr = DeviceBuffer(16 * c1)
+    pr = DeviceBuffer(8 * c1)
+    mad = DeviceBuffer(16)
+    line_search_init_batch(b1.ptr, cnt.ptr, c1, b2.ptr, cnt.ptr + 4, c2, 1, scr.ptr, pr.ptr, cnt.ptr + 8, mad.ptr)
+    load().plvi_device_synchronize()
+    n = int(cnt.download(np.zeros(4, np.int32))[2])
+    return pr.download(np.zeros((c1, 2), np.int32))[:n], tuple(mad.download(np.zeros(2, np.float64)))
 
 
 # ----------------------------------------------------------------- stereo

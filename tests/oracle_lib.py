@@ -602,3 +602,42 @@ def stereo_lines(klL, descL, klR, descR, klUn, width, height, mbf, range_hint=0)
                                 _p(m), _p(disp),
                                 _p(dep), _p(le))
     return k, m[:n], disp[:n], dep[:n], le[:n]
+
+
+def search_for_initialization(kps1, desc1, prev_xy, kps2, desc2, grid, window=100, nnratio=0.9, check_ori=True):
+    """ORBmatcher::SearchForInitialization (oracle/proj_oracle.cpp).  kps in
+    plvi.KEYPOINT_DTYPE (or any record with x, y, octave, angle); grid =
+    (min_x, min_y, inv_w, inv_h).  Returns (nmatches, vnMatches12, vbPrevMatched)."""
+    lib = load()
+    V, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    lib.oracle_search_for_initialization.argtypes = [I, V, V, V, V, V, V, I, V, V, V, V, V, F, F, F, F, I, F, I, V]
+    lib.oracle_search_for_initialization.restype = I
+    f32 = lambda a: np.ascontiguousarray(a, np.float32)  # noqa: E731
+    i32 = lambda a: np.ascontiguousarray(a, np.int32)  # noqa: E731
+    n1, n2 = len(kps1), len(kps2)
+    x1, y1, o1, a1 = f32(kps1["x"]), f32(kps1["y"]), i32(kps1["octave"]), f32(kps1["angle"])
+    x2, y2, o2, a2 = f32(kps2["x"]), f32(kps2["y"]), i32(kps2["octave"]), f32(kps2["angle"])
+    d1 = np.ascontiguousarray(desc1, np.uint8).reshape(-1, 32)
+    d2 = np.ascontiguousarray(desc2, np.uint8).reshape(-1, 32)
+    pv = np.array(prev_xy, np.float32).reshape(-1, 2).copy()
+    m = np.full(max(n1, 1), -1, np.int32)
+    n = lib.oracle_search_for_initialization(n1, _p(x1), _p(y1), _p(o1), _p(a1), _p(d1), _p(pv), n2, _p(x2), _p(y2),
+                                             _p(o2), _p(a2), _p(d2), *[float(g) for g in grid], int(window),
+                                             float(nnratio), int(bool(check_ori)), _p(m))
+    return n, m[:n1].copy(), pv
+
+
+def line_search_init(d1, d2):
+    """LineMatcher::SerachForInitialize + Frame::lineDescriptorMAD (oracle/match_oracle.cpp):
+    returns (pairs n x 2 (query, train), (nn_mad, nn12_mad))."""
+    lib = load()
+    V, I = ctypes.c_void_p, ctypes.c_int
+    lib.oracle_line_search_init.argtypes = [V, I, V, I, V, V, V]
+    lib.oracle_line_search_init.restype = I
+    d1 = np.ascontiguousarray(d1, np.uint8).reshape(-1, 32)
+    d2 = np.ascontiguousarray(d2, np.uint8).reshape(-1, 32)
+    q = np.zeros(max(len(d1), 1), np.int32)
+    t = np.zeros(max(len(d1), 1), np.int32)
+    mad = np.zeros(2, np.float64)
+    n = lib.oracle_line_search_init(_p(d1), len(d1), _p(d2), len(d2), _p(q), _p(t), _p(mad))
+    return np.stack([q[:n], t[:n]], 1), (float(mad[0]), float(mad[1]))

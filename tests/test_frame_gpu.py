@@ -144,12 +144,27 @@ def test_frame_schedule_large_batch_vs_oracle(monkeypatch, split):
         np.testing.assert_array_equal(ldesc[i * lcap:i * lcap + lcnt[i]], eld)
 
 
+@pytest.mark.parametrize("n", [16, 1024])
+def test_frame_schedule_hip_graph_replay(n):
+    """plvi_graph_* over the multi-stream frame schedule (plvi_frame_extract_batch
+    forks to the extractors' priority streams and joins back) + kNN-2: the
+    graph replayed (once, then twice more) reproduces every table of the step
+    issued call by call.  n = 1024 takes the large-batch shape (region growing
+    gated on blur + FAST through the ORB-internal event).  Run as a child
+    process (tools/graph_probe.py) so that a runtime crash fails this test only."""
+    import subprocess
+    import sys
+    from conftest import ROOT
+    r = subprocess.run([sys.executable, str(ROOT / "tools" / "graph_probe.py"), "frame", str(n)],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "frame replay equal" in r.stdout, (r.returncode, r.stdout[-2000:],
+                                                                    r.stderr[-2000:])
+
+
 def test_frame_step_hip_graph_replay():
     """plvi_graph_*: a batch step on one stream (ORB extract, line extract,
     kNN-2) captured into a HIP graph and replayed gives the same tables as
-    the step issued call by call.  (The multi-stream frame schedule is not
-    captured: hipStreamEndCapture segfaults on it in this ROCm,
-    tools/graph_probe.py.)"""
+    the step issued call by call."""
     import torch
     n = 16
     seq = synth.device_sequence(n, 640, 480, seed=5, device="cuda:0")

@@ -1,0 +1,55 @@
+"""The bench's batch-64 step (C1/C2 with one batch in flight) for a rocprofv3
+kernel trace: warm-up, then a spin_kernel marker, N steps, a marker
+(tools/step_timeline.py reads one step's kernel timeline from the trace).
+usage: python tools/b64_probe.py [B] [N]"""
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "pl-vi-orbslam3_amd"))
+import torch  # noqa: E402
+
+import plvi  # noqa: E402
+from plvi import synth  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+N = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+W, H = 640, 480
+seq = synth.device_sequence(B, W, H, seed=0, device="cuda:0")
+lib = plvi.load()
+o = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=B)
+lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=B)
+kp, de, co, _, cap = o.outputs()
+_, lde, _, lco, lcap = lx.outputs()
+i32 = dict(dtype=torch.int32, device="cuda:0")
+o4 = [torch.empty((B - 1) * cap, **i32) for _ in range(4)]
+lsc = torch.empty(4 * (B - 1) * 2 * lcap, **i32)
+lm = torch.empty((B - 1) * lcap, **i32)
+lnm = torch.empty(B - 1, **i32)
+s = torch.cuda.Stream()
+st = s.cuda_stream
+
+
+def step():
+    plvi.frame_extract_batch(o, lx, seq.data_ptr(), B, W * H, W, (0, 0), stream=st)
+    rc = lib.plvi_hamming_knn2_batch(de + cap * 32, co + 4, cap, de, co, cap, B - 1, *[x.data_ptr() for x in o4], st)
+    rc |= lib.plvi_line_match_batch(lde + lcap * 32, lco + 4, lcap, lde, lco, lcap, B - 1, 0.9, lsc.data_ptr(),
+                                    lm.data_ptr(), lnm.data_ptr(), st)
+    assert rc == 0
+
+
+for _ in range(3):
+    step()
+torch.cuda.synchronize()
+torch.cuda._sleep(1000)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(N):
+    step()
+torch.cuda.synchronize()
+el = time.perf_counter() - t0
+torch.cuda._sleep(1000)
+torch.cuda.synchronize()
+print(f"B={B}: {el / N * 1e3:.2f} ms per step, {B * N / el:.0f} FPS", flush=True)
+assert o.errors() == 0 and lx.errors() == 0
