@@ -33,6 +33,7 @@ enum {
   PLVI_E_HIP = -4,      /* HIP runtime failure */
   PLVI_E_OVERFLOW = -5, /* internal fixed-capacity table overflowed on device */
   PLVI_E_SIZE = -6,     /* descriptor row counts differ (LineMatcher.cpp:50-51) */
+  PLVI_E_CAPTURE = -7,  /* stream capture of the multi-stream frame schedule on a HIP runtime < 7.2 */
 };
 
 /* OpenCV-semantics switches for the items no reference test can pin
@@ -672,6 +673,11 @@ int plvi_memcpy(void* dst, const void* src, size_t bytes, int kind);
 /* Same, asynchronous on `stream` (hipStream_t). */
 int plvi_memcpy_async(void* dst, const void* src, size_t bytes, int kind, void* stream);
 int plvi_device_synchronize(void);
+/* A non-blocking HIP stream (hipStreamCreateWithFlags(hipStreamNonBlocking))
+ * for bindings without a HIP runtime of their own; destroy / synchronize. */
+int plvi_stream_create(void** stream);
+int plvi_stream_destroy(void* stream);
+int plvi_stream_synchronize(void* stream);
 
 /* HIP graphs (no reference counterpart: a runtime facility of this
  * library).  plvi_graph_capture_begin starts capturing `stream` (a created
@@ -679,7 +685,10 @@ int plvi_device_synchronize(void);
  * plvi_graph_capture_end is recorded, not run, including the work the
  * extractors fork to their own streams.  The captured step is instantiated
  * into *graph_exec and replayed by plvi_graph_launch with the same device
- * pointers and parameters; plvi_graph_destroy frees it. */
+ * pointers and parameters; plvi_graph_destroy frees it.  The multi-stream
+ * frame schedule (plvi_frame_extract_batch) needs HIP runtime >= 7.2 to be
+ * captured (the 7.0 runtime crashes in hipStreamEndCapture on its
+ * fork/join): on an older runtime it returns PLVI_E_CAPTURE while capturing. */
 int plvi_graph_capture_begin(void* stream);
 int plvi_graph_capture_end(void* stream, void** graph_exec);
 int plvi_graph_launch(void* graph_exec, void* stream);

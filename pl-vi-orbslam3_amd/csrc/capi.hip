@@ -43,6 +43,25 @@ extern "C" int plvi_device_synchronize(void) {
     return PLVI_OK;
 }
 
+extern "C" int plvi_stream_create(void** stream) {
+    if (!stream) return PLVI_E_BADARG;
+    hipStream_t s = nullptr;
+    PLVI_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = (void*)s;
+    return PLVI_OK;
+}
+
+extern "C" int plvi_stream_destroy(void* stream) {
+    if (!stream) return PLVI_E_BADARG;
+    PLVI_CHECK(hipStreamDestroy((hipStream_t)stream));
+    return PLVI_OK;
+}
+
+extern "C" int plvi_stream_synchronize(void* stream) {
+    PLVI_CHECK(hipStreamSynchronize((hipStream_t)stream));
+    return PLVI_OK;
+}
+
 // HIP graphs: a batch step (any sequence of plvi_* calls on `stream`, their
 // internal streams joined by events) captured once and replayed with one
 // launch, which takes the per-call host work (~100 API calls per frame

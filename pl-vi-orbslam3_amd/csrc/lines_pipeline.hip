@@ -168,12 +168,16 @@ struct LinePipeline {
             const char* e5 = getenv("PLVI_SOBEL_WITH_GROW");
             sobelWithGrow = !e5 || atoi(e5) != 0;
             if (prio) PLVI_CHECK(hipStreamCreateWithPriority(&critStream, hipStreamNonBlocking, greatest));
-            if (prio) PLVI_CHECK(hipStreamCreateWithPriority(&crit2, hipStreamNonBlocking, greatest));
             // PLVI_GROW_SPLIT=1: octave 0 grows right after the prep, octave 1
             // after blur + FAST (batches from 1024 frames; +1 % in a 3-way
             // sweep, within run-to-run noise, so off by default)
             const char* e6 = getenv("PLVI_GROW_SPLIT");
             growSplit = e6 && atoi(e6) != 0;
+            // crit2 only when split: every greatest-priority stream takes a slot
+            // in the runtime's pool of hardware queues, and a pool shared by many
+            // handles can put two streams of one schedule on one queue
+            if (prio && growSplit)
+                PLVI_CHECK(hipStreamCreateWithPriority(&crit2, hipStreamNonBlocking, greatest));
         }
         for (auto* e : {&evFork, &evPrep, &evSobel, &evOrb, &evCrit, &evBlur, &evGate, &evGrow2})
             PLVI_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
@@ -669,6 +673,19 @@ extern "C" int plvi_frame_extract_batch(plvi_orb_extractor* orb, plvi_line_extra
                                         void* stream) {
     if (!orb || !lines || !d_frames) return PLVI_E_BADARG;
     PLVI_CHECK(hipSetDevice(lines->p().device));
+    if (stream) {
+        // Capturing the fork/join of this schedule crashes inside
+        // hipStreamEndCapture on the HIP 7.0 runtime that PyTorch bundles
+        // (torch/lib/libamdhip64.so, mapped by any process that imports torch
+        // first); ROCm 7.2's runtime captures and replays it bit-exactly
+        // (tests/test_frame_gpu.py, tools/graph_probe.py).  Refuse the capture
+        // on older runtimes instead of letting it crash later.
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        PLVI_CHECK(hipStreamIsCapturing((hipStream_t)stream, &cs));
+        int ver = 0;
+        PLVI_CHECK(hipRuntimeGetVersion(&ver));
+        if (cs != hipStreamCaptureStatusNone && ver < 70200000) return PLVI_E_CAPTURE;
+    }
     return lines->p().run_with_orb(d_frames, n_frames, frame_stride, row_stride, (hipStream_t)stream, orb, lap0, lap1);
 }
 

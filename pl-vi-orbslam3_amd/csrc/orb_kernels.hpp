@@ -566,6 +566,9 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
 // decided in the same sweep, so there is no per-pixel index arithmetic.
 // ---------------------------------------------------------------------------
 constexpr int kNmsRows = 64;  // >= window height (hCell <= 58, orb_pipeline.hip plan checks)
+#ifndef PLVI_NMS_MAXONLY
+#define PLVI_NMS_MAXONLY 1  // one strict-local-max sweep, survivors-only writes (0: both thresholds per row)
+#endif
 
 __global__ __launch_bounds__(64) void orb_cell_nms_kernel(const OrbCellDev* __restrict__ cells,
                                                           const OrbLevelDev* __restrict__ lvs,
@@ -591,6 +594,42 @@ __global__ __launch_bounds__(64) void orb_cell_nms_kernel(const OrbCellDev* __re
     sv[wh * 64 + lane] = 0;  // row wh (wh < kNmsRows) is the bottom neighbour of the last row
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#if PLVI_NMS_MAXONLY
+    // A pixel at or above threshold t survives iff its score is strictly
+    // greater than all 8 RAW neighbour scores: a neighbour below t counts as 0
+    // in the reference's buffer but is then below the pixel's score anyway,
+    // and one at or above t is compared as it is.  So one sweep finds the
+    // strict local maxima (s > 0) and the thresholds only filter the pixel
+    // itself; the cand plane is zeroed beforehand, only survivors are written.
+    unsigned long long ka = 0, kb = 0;
+    {
+        int s = sv[lane];
+        int hp = 0;  // max over columns c-1..c+1 of row r-1
+        int hc = max(s, max(lane_from_left(s), lane_from_right(s)));
+        int lr = max(lane_from_left(s), lane_from_right(s));
+        for (int r = 0; r < wh; ++r) {
+            const int sn = sv[(r + 1) * 64 + lane];
+            const int lrn = max(lane_from_left(sn), lane_from_right(sn));
+            const int hn = max(sn, lrn);
+            const int m = max(max(hp, hn), lr);
+            if (s > m) {
+                if (s >= t1) ka |= 1ull << r;
+                if (s >= t2) kb |= 1ull << r;
+            }
+            hp = hc;
+            hc = hn;
+            lr = lrn;
+            s = sn;
+        }
+    }
+    const unsigned long long keep = __ballot(ka != 0ull) != 0ull ? ka : kb;
+    if (!incol) return;
+    uint8_t* C = cand + base;
+    for (unsigned long long kk = keep; kk; kk &= kk - 1) {
+        const int r = __ffsll((long long)kk) - 1;
+        C[(size_t)r * w] = sv[r * 64 + lane];
+    }
+#else
     // both thresholds in one sweep: a = iniThFAST, b = minThFAST
     unsigned long long ka = 0, kb = 0;
     int s = sv[lane];
@@ -625,6 +664,7 @@ __global__ __launch_bounds__(64) void orb_cell_nms_kernel(const OrbCellDev* __re
             if (r < wh) C[(size_t)r * w] = ((keep >> r) & 1ull) ? sv[r * 64 + lane] : (uint8_t)0;
         }
     }
+#endif
 }
 
 // ---------------------------------------------------------------------------

@@ -32,6 +32,7 @@ PLVI_E_CAPACITY = -3
 PLVI_E_HIP = -4
 PLVI_E_OVERFLOW = -5
 PLVI_E_SIZE = -6
+PLVI_E_CAPTURE = -7
 
 # OpenCV-semantics switches (plvi_frontend.h PLVI_COMPAT_*)
 COMPAT_GAUSS_ROUNDED = 1
@@ -207,6 +208,9 @@ def _declare(lib):
         "plvi_image_bounds": ([V, I, I, V], I),
         "plvi_search_by_projection_batch": ([I, V, V, V, V, I, V, V, V, V, V, V, V, V, V, V, I, V, V, V], I),
         "plvi_search_by_projection": ([V, V, V, I, V, V, V, V, V, V, V, I, V], I),
+        "plvi_stream_create": ([c_void_pp], I),
+        "plvi_stream_destroy": ([V], I),
+        "plvi_stream_synchronize": ([V], I),
         "plvi_search_for_initialization_batch": ([I, V, V, V, V, I, V, V, V, V, I, V, V, V, V, V], I),
         "plvi_line_search_init_batch": ([V, V, I, V, V, I, I, V, V, V, V, V], I),
         "plvi_search_local_batch": ([I, V, V, V, V, I, V, V, V, V, V, V, V, V, V, I, V, V, V], I),

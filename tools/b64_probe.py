@@ -13,10 +13,19 @@ import torch  # noqa: E402
 import plvi  # noqa: E402
 from plvi import synth  # noqa: E402
 
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-N = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+argv = [a for a in sys.argv[1:] if not a.startswith("--")]
+B = int(argv[0]) if len(argv) > 0 else 64
+N = int(argv[1]) if len(argv) > 1 else 10
 W, H = 640, 480
-seq = synth.device_sequence(B, W, H, seed=0, device="cuda:0")
+big = "--big" in sys.argv  # the bench's situation: 3072-frame handles exist and have run
+seq = synth.device_sequence(3072 if big else B, W, H, seed=0, device="cuda:0")
+if big:
+    ob = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=3072)
+    lb = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=3072)
+    sb = torch.cuda.Stream()
+    for _ in range(3):
+        plvi.frame_extract_batch(ob, lb, seq.data_ptr(), 3072, W * H, W, (0, 0), stream=sb.cuda_stream)
+    torch.cuda.synchronize()
 lib = plvi.load()
 o = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=B)
 lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=B)
