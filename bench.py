@@ -173,13 +173,46 @@ def oracle_verify(checks):
 
 
 def cpu_baseline(frames, runs=5, par_s=5.0):
-    """the oracle (built -O3 -march=x86-64-v3 -ffp-contract=off)
-    single-threaded and pinned to one core, per stage and end to end, median
-    of `runs` passes over the same frames; plus frame-parallel throughput on
-    the host cores this process may use (oracle calls release the GIL)."""
+    """the oracle restatement timed on this box's host cores, in
+    a child process (`bench.py --cpu-baseline-child`, no GPU) so that no host
+    thread of the GPU process competes with it.  The oracle is rebuilt here
+    with -O3 -march=native (MARCH=-march=native, into a temp dir; the
+    checker's own build stays -march=x86-64-v3); on a build failure the
+    checker's build is timed and the line says so."""
+    import tempfile
+    tmp = pathlib.Path(tempfile.mkdtemp(prefix="plvi_cpu_"))
+    lib = tmp / "liboracle.so"
+    march = "native"
+    r = subprocess.run(["make", "-s", "-C", str(ROOT / "oracle"), "MARCH=-march=native", f"OUT={lib}"],
+                       capture_output=True, text=True)
+    env = dict(os.environ)
+    if r.returncode == 0 and lib.exists():
+        env["ORACLE_LIB"] = str(lib)
+    else:
+        march = "x86-64-v3 (native build failed)"
+    np.save(tmp / "frames.npy", np.stack(frames))
+    out = tmp / "cpu.json"
+    r = subprocess.run([sys.executable, str(pathlib.Path(__file__).resolve()), "--cpu-baseline-child",
+                        str(tmp / "frames.npy"), str(out), str(runs), str(par_s)], env=env, capture_output=True,
+                       text=True, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError(f"cpu baseline child failed: {r.stderr[-2000:]}")
+    res = json.loads(out.read_text())
+    res["build"] = f"oracle/ -O3 -march={march} -ffp-contract=off"
+    return res
+
+
+def cpu_baseline_child(frames_npy, out_json, runs, par_s):
+    """The CPU-baseline measurement proper (child process, no GPU): per stage
+    and end to end on the timed batch's frames, single thread pinned to one
+    core (median of `runs`); frame-parallel throughput on every core this
+    process may use; and BASELINE C0 (752x480 EuRoC-shaped frames, ORB 1000 +
+    LineExtractor 100 lines, extraction only, single thread)."""
     import threading
     import oracle_lib as ol
+    from plvi import synth
     ol.load()
+    frames = list(np.load(frames_npy))
     cpus = sorted(os.sched_getaffinity(0))
     stages = ("orb_extract", "line_extract", "orb_knn2", "line_match")
     per = {k: [] for k in stages}
@@ -210,10 +243,19 @@ def cpu_baseline(frames, runs=5, par_s=5.0):
             tot.append(time.perf_counter() - t_run)
             for k in stages:
                 per[k].append(acc[k] * 1e3 / len(frames))
+        # BASELINE C0: 752x480, 1000 ORB features, 100 lines, extraction only
+        c0 = synth.device_sequence(16, 752, 480, seed=7).numpy()
+        c0t = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            for img in c0:
+                ol.orb_extract(img)
+                ol.line_extract(img, nfeatures=100)
+            c0t.append(time.perf_counter() - t0)
     finally:
         os.sched_setaffinity(0, set(cpus))
     med = float(np.median(tot))
-    nthr = min(16, len(cpus))  # the GPU box's CPU share per GPU is 16
+    nthr = len(cpus)
     count = [0] * nthr
     stop = time.perf_counter() + par_s
 
@@ -238,14 +280,21 @@ def cpu_baseline(frames, runs=5, par_s=5.0):
     for t in ths:
         t.join()
     par_fps = sum(count) / (time.perf_counter() - t0)
-    return {"value": len(frames) / med, "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{len(frames)} frames of the timed batch, median of {runs} single-thread runs pinned to core "
-                      f"{cpus[0]} (sched_setaffinity): ORB extract + LSD/LBD extract + ORB kNN-2 + "
-                      f"LineMatcher::match vs previous frame, CPU restatement (oracle/, -O3 -march=x86-64-v3)",
-            "stage_ms_per_frame": {k: round(float(np.median(v)), 3) for k, v in per.items()},
-            "parallel": {"threads": nthr, "value": round(par_fps, 2), "unit": "frames/s",
-                         "sample": f"{sum(count)} frames in {par_s:.0f}s, frame-parallel threads"},
-            "host_cpu": _cpu_model(), "host_nproc": os.cpu_count(), "affinity_cpus": len(cpus)}
+    res = {"value": len(frames) / med, "unit": "frames/s", "cores": 1, "kind": "port",
+           "sample": f"{len(frames)} frames of the timed batch (640x480), median of {runs} single-thread runs "
+                     f"pinned to core {cpus[0]} (sched_setaffinity): ORB extract + LSD/LBD extract + ORB kNN-2 + "
+                     f"LineMatcher::match vs previous frame, CPU restatement (oracle/)",
+           "stage_ms_per_frame": {k: round(float(np.median(v)), 3) for k, v in per.items()},
+           "parallel": {"threads": nthr, "value": round(par_fps, 2), "unit": "frames/s",
+                        "sample": f"{sum(count)} frames in {par_s:.0f}s, one frame-parallel thread per CPU in "
+                                  f"this process's affinity set ({nthr})"},
+           "c0_752x480": {"value": round(len(c0) / float(np.median(c0t)), 3), "unit": "frames/s", "cores": 1,
+                          "sample": f"BASELINE C0 shape: {len(c0)} synthetic 752x480 EuRoC-shaped frames, "
+                                    "ORBextractor 1000 + Lineextractor 100 lines, extraction only, median of 3 "
+                                    "single-thread runs"},
+           "host_cpu": _cpu_model(), "host_nproc": os.cpu_count(), "affinity_cpus": len(cpus)}
+    pathlib.Path(out_json).write_text(json.dumps(res))
+    return 0
 
 
 # ------------------------------------------------------------------ dry run
@@ -334,7 +383,9 @@ def main():
     ap.add_argument("--no-gather", dest="gather", action="store_false")
     ap.add_argument("--dry-run", action="store_true", help="launcher + reductions on CPU (gloo), no GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-frames", type=int, default=32, help="frames of the CPU-baseline sample (SURVEY: 64)")
+    ap.add_argument("--cpu-frames", type=int, default=64, help="frames of the CPU-baseline sample (SURVEY 8(d): 64)")
+    ap.add_argument("--cpu-baseline-child", nargs=4, metavar=("FRAMES_NPY", "OUT_JSON", "RUNS", "PAR_S"),
+                    help=argparse.SUPPRESS)
     ap.add_argument("--no-check", action="store_true", help="skip the oracle check of the timed batch")
     ap.add_argument("--no-extra", action="store_true", help="skip the batch-64 / latency / H2D lines")
     ap.add_argument("--no-side", action="store_true", help="skip the BoW / projection / stereo stage timings")
@@ -343,6 +394,9 @@ def main():
                          "so one batch's ORB tail overlaps the next batch's LSD front")
     args = ap.parse_args()
 
+    if args.cpu_baseline_child:
+        f, o, runs, par_s = args.cpu_baseline_child
+        return cpu_baseline_child(f, o, int(runs), float(par_s))
     world_env = int(os.environ.get("WORLD_SIZE", "0"))
     if world_env == 0 and args.gpus > 1:
         return spawn_ranks(args.gpus)

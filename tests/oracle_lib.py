@@ -4,6 +4,7 @@ Builds oracle/_build/liboracle.so with `make -C oracle` when missing.
 Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline use this.
 """
 import ctypes
+import os
 import pathlib
 import subprocess
 
@@ -12,6 +13,8 @@ import numpy as np
 ROOT = pathlib.Path(__file__).resolve().parent.parent
 ORACLE_DIR = ROOT / "oracle"
 LIB = ORACLE_DIR / "_build" / "liboracle.so"
+# ORACLE_LIB: another build of the same sources (bench.py's -march=native CPU baseline)
+LIB_OVERRIDE = os.environ.get("ORACLE_LIB")
 
 
 class KP(ctypes.Structure):
@@ -34,9 +37,12 @@ def load():
     if _lib is not None:
         return _lib
     srcs = list(ORACLE_DIR.glob("*.cpp")) + list(ORACLE_DIR.glob("*.h")) + list(ORACLE_DIR.glob("*.inc"))
-    if not LIB.exists() or any(s.stat().st_mtime > LIB.stat().st_mtime for s in srcs):
-        build()
-    lib = ctypes.CDLL(str(LIB))
+    if LIB_OVERRIDE:
+        lib = ctypes.CDLL(LIB_OVERRIDE)
+    else:
+        if not LIB.exists() or any(s.stat().st_mtime > LIB.stat().st_mtime for s in srcs):
+            build()
+        lib = ctypes.CDLL(str(LIB))
     V, I, F, D = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_double
     P = ctypes.POINTER(ctypes.c_int)
     lib.oracle_orb_extract.argtypes = [V, I, I, I, I, F, I, I, I, I, I, V, V, I, P]
