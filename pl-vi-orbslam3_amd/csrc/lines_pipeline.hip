@@ -145,10 +145,13 @@ struct LinePipeline {
             PLVI_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
             const char* e1 = getenv("PLVI_STREAM_PRIO");
             const bool prio = !e1 || atoi(e1) != 0;
-            // PLVI_ORB_AFTER_PREP=1: ORB waits for the LSD prep (default: ORB and
-            // the prep start together, +2 % at B = 3072 with the streaming prep)
+            // PLVI_ORB_AFTER_PREP (default 1): ORB waits for the LSD prep.  With
+            // the faster ORB chain of r03 the pyramid otherwise ends while the
+            // prep still runs and blur + FAST shares the CUs with it (9-12 ms
+            // instead of 7.4 per 3072 frames); the step time is the same either
+            // way (region growing waits for blur + FAST from 1024 frames on)
             const char* e2 = getenv("PLVI_ORB_AFTER_PREP");
-            orbAfterPrep = e2 && atoi(e2) != 0;
+            orbAfterPrep = !e2 || atoi(e2) != 0;
             // PLVI_GROW_AFTER_BLUR=0: region growing starts right after the prep
             // (default 1: it waits for the ORB blur + FAST launch, whose 81-VGPR /
             // 9 KB-LDS waves cannot share a CU with the region-growing waves; the

@@ -570,13 +570,9 @@ constexpr int kNmsRows = 64;  // >= window height (hCell <= 58, orb_pipeline.hip
 #define PLVI_NMS_MAXONLY 1  // one strict-local-max sweep, survivors-only writes (0: both thresholds per row)
 #endif
 
-__global__ __launch_bounds__(64) void orb_cell_nms_kernel(const OrbCellDev* __restrict__ cells,
-                                                          const OrbLevelDev* __restrict__ lvs,
-                                                          const uint8_t* __restrict__ score,
-                                                          uint8_t* __restrict__ cand, int t1, int t2) {
-    __shared__ uint8_t sv[kNmsRows * 64];
-    const OrbCellDev c = cells[blockIdx.x];
-    const int f = blockIdx.y;
+__device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, const OrbLevelDev* __restrict__ lvs,
+                                             const uint8_t* __restrict__ score, uint8_t* __restrict__ cand, int t1,
+                                             int t2, uint8_t* sv) {
     const OrbLevelDev& L = lvs[c.level];
     const int ww = c.x1 - c.x0, wh = c.y1 - c.y0, w = L.bpitch;
     const int lane = threadIdx.x;
@@ -665,6 +661,24 @@ __global__ __launch_bounds__(64) void orb_cell_nms_kernel(const OrbCellDev* __re
         }
     }
 #endif
+}
+
+#ifndef PLVI_NMS_CELLS
+#define PLVI_NMS_CELLS 1
+#endif
+constexpr int kNmsCells = PLVI_NMS_CELLS;  // cells per wave (the launch grid's x extent is ncells / kNmsCells)
+
+__global__ __launch_bounds__(64) void orb_cell_nms_kernel(const OrbCellDev* __restrict__ cells, int ncells,
+                                                          const OrbLevelDev* __restrict__ lvs,
+                                                          const uint8_t* __restrict__ score,
+                                                          uint8_t* __restrict__ cand, int t1, int t2) {
+    __shared__ uint8_t sv[kNmsRows * 64];
+    const int f = blockIdx.y;
+    for (int ci = blockIdx.x; ci < ncells; ci += gridDim.x) {
+        orb_nms_cell(cells[ci], f, lvs, score, cand, t1, t2, sv);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next cell's staging overwrites sv
+    }
 }
 
 // ---------------------------------------------------------------------------

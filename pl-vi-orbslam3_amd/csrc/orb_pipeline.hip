@@ -334,8 +334,9 @@ struct OrbPipeline {
         mark(1, st);
         // K2 cell NMS -> candidate map (zeroed first: only detection windows are written)
         PLVI_CHECK(hipMemsetAsync(Cd, 0, candBytesTotal, st));
-        hipLaunchKernelGGL(orb_cell_nms_kernel, dim3((unsigned)cells.size(), nf), dim3(64), 0, st,
-                           d_cells.as<OrbCellDev>(), d_lv.as<OrbLevelDev>(), (const uint8_t*)Sc, Cd, t1, t2);
+        hipLaunchKernelGGL(orb_cell_nms_kernel, dim3((unsigned)((cells.size() + kNmsCells - 1) / kNmsCells), nf),
+                           dim3(64), 0, st, d_cells.as<OrbCellDev>(), (int)cells.size(), d_lv.as<OrbLevelDev>(),
+                           (const uint8_t*)Sc, Cd, t1, t2);
         mark(2, st);
         // K3 SAT
         int maxRh = 0, maxStrips = 0;
