@@ -664,6 +664,19 @@ int plvi_line_search_init_batch(const uint8_t* d_desc1, const int* d_n1, int cap
                                 const int* d_n2, int cap2, int n_pairs, int* d_scratch, int* d_pairs, int* d_npairs,
                                 double* d_mad, void* stream);
 
+/* The stereo-line Frame ctor (src/Frame.cc:200-249: ExtractORB left || right,
+ * ExtractLine left || right): both sides' ORB + line extraction of a batch of
+ * rectified pairs as two concurrent frame schedules (the right one forked
+ * from `stream` onto lines_right's own stream and joined back).  Asynchronous
+ * on `stream`; each handle keeps its side's results (plvi_orb_outputs /
+ * plvi_lines_outputs), which plvi_stereo_match_batch and
+ * plvi_stereo_lines_batch then read on the same stream.  Left and right
+ * handles must be distinct. */
+int plvi_stereo_frame_extract_batch(plvi_orb_extractor* orb_left, plvi_orb_extractor* orb_right,
+                                    plvi_line_extractor* lines_left, plvi_line_extractor* lines_right,
+                                    const uint8_t* d_left, const uint8_t* d_right, int n_frames, size_t frame_stride,
+                                    size_t row_stride, int lap0, int lap1, void* stream);
+
 /* Device memory helpers for bindings that have no HIP runtime of their own
  * (ctypes, JNI): thin wrappers over hipMalloc/hipFree/hipMemcpy on the
  * current device.  kind: 1 = host->device, 2 = device->host, 3 = d->d. */

@@ -71,7 +71,7 @@ struct LinePipeline {
     hipStream_t stream = nullptr;
     hipStream_t aux[2] = {nullptr, nullptr};  // frame mode: ORB and LBD-Sobel streams
     hipEvent_t evFork = nullptr, evPrep = nullptr, evSobel = nullptr, evOrb = nullptr, evCrit = nullptr,
-               evBlur = nullptr, evGate = nullptr, evGrow2 = nullptr;
+               evBlur = nullptr, evGate = nullptr, evGrow2 = nullptr, evPair = nullptr;
     bool growAfterBlur = true, sobelWithGrow = false, growSplit = false;
     hipStream_t critStream = nullptr;  // frame schedule: prep -> grow -> describe
     hipStream_t crit2 = nullptr;       // frame schedule: octave-1 region growing (split mode)
@@ -121,7 +121,7 @@ struct LinePipeline {
     ~LinePipeline() {
         for (auto e : kev) (void)hipEventDestroy(e);
         for (auto e : evs) (void)hipEventDestroy(e);
-        for (auto e : {evFork, evPrep, evSobel, evOrb, evCrit, evBlur, evGate, evGrow2})
+        for (auto e : {evFork, evPrep, evSobel, evOrb, evCrit, evBlur, evGate, evGrow2, evPair})
             if (e) (void)hipEventDestroy(e);
         if (critStream) (void)hipStreamDestroy(critStream);
         if (crit2) (void)hipStreamDestroy(crit2);
@@ -182,7 +182,7 @@ struct LinePipeline {
             if (prio && growSplit)
                 PLVI_CHECK(hipStreamCreateWithPriority(&crit2, hipStreamNonBlocking, greatest));
         }
-        for (auto* e : {&evFork, &evPrep, &evSobel, &evOrb, &evCrit, &evBlur, &evGate, &evGrow2})
+        for (auto* e : {&evFork, &evPrep, &evSobel, &evOrb, &evCrit, &evBlur, &evGate, &evGrow2, &evPair})
             PLVI_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         fcap = p->nfeatures > 0 ? p->nfeatures : kKlCap;
         SCALE = (double)p->lsd_scale;  // LSDOptions::scale is float
@@ -690,6 +690,39 @@ extern "C" int plvi_frame_extract_batch(plvi_orb_extractor* orb, plvi_line_extra
         if (cs != hipStreamCaptureStatusNone && ver < 70200000) return PLVI_E_CAPTURE;
     }
     return lines->p().run_with_orb(d_frames, n_frames, frame_stride, row_stride, (hipStream_t)stream, orb, lap0, lap1);
+}
+
+// The stereo-line Frame (src/Frame.cc:200-249): ORB left || right and lines
+// left || right as two frame schedules that run concurrently, the right one
+// forked from the caller's stream onto the right line handle's own stream and
+// joined back, so the caller's stream holds all four extractions (stereo
+// matching follows on it: plvi_stereo_match_batch / plvi_stereo_lines_batch).
+extern "C" int plvi_stereo_frame_extract_batch(plvi_orb_extractor* orb_left, plvi_orb_extractor* orb_right,
+                                               plvi_line_extractor* lines_left, plvi_line_extractor* lines_right,
+                                               const uint8_t* d_left, const uint8_t* d_right, int n_frames,
+                                               size_t frame_stride, size_t row_stride, int lap0, int lap1,
+                                               void* stream) {
+    if (!orb_left || !orb_right || !lines_left || !lines_right || !d_left || !d_right) return PLVI_E_BADARG;
+    if (orb_left == orb_right || lines_left == lines_right) return PLVI_E_BADARG;  // each side owns its tables
+    LinePipeline& L = lines_left->p();
+    LinePipeline& R = lines_right->p();
+    if (L.device != R.device) return PLVI_E_BADARG;
+    PLVI_CHECK(hipSetDevice(L.device));
+    hipStream_t st = stream ? (hipStream_t)stream : L.stream;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    PLVI_CHECK(hipStreamIsCapturing(st, &cs));
+    int ver = 0;
+    PLVI_CHECK(hipRuntimeGetVersion(&ver));
+    if (cs != hipStreamCaptureStatusNone && ver < 70200000) return PLVI_E_CAPTURE;  // see plvi_frame_extract_batch
+    // fork the right side off the caller's stream
+    PLVI_CHECK(hipEventRecord(R.evPair, st));
+    PLVI_CHECK(hipStreamWaitEvent(R.stream, R.evPair, 0));
+    int rc = L.run_with_orb(d_left, n_frames, frame_stride, row_stride, st, orb_left, lap0, lap1);
+    int rc2 = R.run_with_orb(d_right, n_frames, frame_stride, row_stride, R.stream, orb_right, lap0, lap1);
+    // join it back
+    PLVI_CHECK(hipEventRecord(L.evPair, R.stream));
+    PLVI_CHECK(hipStreamWaitEvent(st, L.evPair, 0));
+    return rc ? rc : rc2;
 }
 
 extern "C" int plvi_lines_outputs(plvi_line_extractor* h, plvi_keyline** d_kl, uint8_t** d_desc, double** d_fn,

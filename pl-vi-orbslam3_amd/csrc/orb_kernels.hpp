@@ -569,6 +569,9 @@ constexpr int kNmsRows = 64;  // >= window height (hCell <= 58, orb_pipeline.hip
 #ifndef PLVI_NMS_MAXONLY
 #define PLVI_NMS_MAXONLY 1  // one strict-local-max sweep, survivors-only writes (0: both thresholds per row)
 #endif
+#ifndef PLVI_NMS_STREAM
+#define PLVI_NMS_STREAM 1  // rows streamed through registers, no LDS (0: the window staged in LDS)
+#endif
 
 __device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, const OrbLevelDev* __restrict__ lvs,
                                              const uint8_t* __restrict__ score, uint8_t* __restrict__ cand, int t1,
@@ -579,6 +582,58 @@ __device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, co
     const bool incol = lane < ww;
     const size_t base = L.boff + (size_t)f * L.bplane + (size_t)c.y0 * w + c.x0 + lane;
     const uint8_t* S = score + base;
+#if PLVI_NMS_MAXONLY && PLVI_NMS_STREAM
+    // Register streaming, no LDS: rows come straight from the score plane,
+    // eight in flight (the next chunk is loaded while this one is swept), so
+    // the kernel occupies no LDS next to the region-growing waves it runs
+    // with; survivors are re-read from the (L2-resident) plane when written.
+    (void)sv;
+    unsigned long long ka = 0, kb = 0;
+    {
+        auto ld = [&](int r) -> int { return (incol && r < wh) ? (int)S[(size_t)r * w] : 0; };
+        int nx[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) nx[k] = ld(1 + k);
+        int s = ld(0);
+        int hp = 0;
+        int lr = max(lane_from_left(s), lane_from_right(s));
+        int hc = max(s, lr);
+        for (int r0 = 0; r0 < wh; r0 += 8) {
+            int cur[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) cur[k] = nx[k];
+            if (r0 + 8 < wh) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) nx[k] = ld(r0 + 9 + k);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int r = r0 + k;
+                if (r < wh) {
+                    const int sn = cur[k];
+                    const int lrn = max(lane_from_left(sn), lane_from_right(sn));
+                    const int hn = max(sn, lrn);
+                    const int m = max(max(hp, hn), lr);
+                    if (s > m) {
+                        if (s >= t1) ka |= 1ull << r;
+                        if (s >= t2) kb |= 1ull << r;
+                    }
+                    hp = hc;
+                    hc = hn;
+                    lr = lrn;
+                    s = sn;
+                }
+            }
+        }
+    }
+    const unsigned long long keep = __ballot(ka != 0ull) != 0ull ? ka : kb;
+    if (!incol) return;
+    uint8_t* C = cand + base;
+    for (unsigned long long kk = keep; kk; kk &= kk - 1) {
+        const int r = __ffsll((long long)kk) - 1;
+        C[(size_t)r * w] = S[(size_t)r * w];
+    }
+#else
     // stage the window column-per-lane (rows beyond wh and lanes beyond ww hold 0)
     for (int r0 = 0; r0 < wh; r0 += 8) {
         uint8_t v[8];
@@ -660,6 +715,7 @@ __device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, co
             if (r < wh) C[(size_t)r * w] = ((keep >> r) & 1ull) ? sv[r * 64 + lane] : (uint8_t)0;
         }
     }
+#endif
 #endif
 }
 

@@ -208,6 +208,7 @@ def _declare(lib):
         "plvi_image_bounds": ([V, I, I, V], I),
         "plvi_search_by_projection_batch": ([I, V, V, V, V, I, V, V, V, V, V, V, V, V, V, V, I, V, V, V], I),
         "plvi_search_by_projection": ([V, V, V, I, V, V, V, V, V, V, V, I, V], I),
+        "plvi_stereo_frame_extract_batch": ([V, V, V, V, V, V, I, S, S, I, I, V], I),
         "plvi_stream_create": ([c_void_pp], I),
         "plvi_stream_destroy": ([V], I),
         "plvi_stream_synchronize": ([V], I),
@@ -250,6 +251,17 @@ def load():
     """Load the HIP library (raises if it was not built: there is no fallback)."""
     global _lib
     if _lib is None:
+        # One HIP runtime per process: PyTorch's bundled libamdhip64 and
+        # /opt/rocm's share the SONAME libamdhip64.so.7, so whichever loads first
+        # serves both -- unless ours comes first, in which case torch later
+        # loads its own copy by file name and that second runtime finds no
+        # device.  Import torch (if installed) before the library; set
+        # PLVI_NO_TORCH=1 to run on the system runtime alone.
+        if not os.environ.get("PLVI_NO_TORCH"):
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
         if not LIB_PATH.exists():
             raise RuntimeError(f"{LIB_PATH} missing: build it with `make -C pl-vi-orbslam3_amd`")
         _lib = _declare(ctypes.CDLL(str(LIB_PATH)))
@@ -788,6 +800,15 @@ def frame_extract_batch(orb, lines, d_frames_ptr, n_frames, frame_stride, row_st
     _check(load().plvi_frame_extract_batch(orb._h, lines._h, ctypes.c_void_p(d_frames_ptr), n_frames, frame_stride,
                                            row_stride, lap[0], lap[1], ctypes.c_void_p(stream or 0)),
            "plvi_frame_extract_batch")
+
+
+def stereo_frame_extract_batch(orb_left, orb_right, lines_left, lines_right, d_left_ptr, d_right_ptr, n_frames,
+                               frame_stride, row_stride, lap=(0, 0), stream=None):
+    """The stereo-line Frame's four extractions (plvi_stereo_frame_extract_batch)."""
+    V = ctypes.c_void_p
+    _check(load().plvi_stereo_frame_extract_batch(orb_left._h, orb_right._h, lines_left._h, lines_right._h,
+                                                  V(d_left_ptr), V(d_right_ptr), n_frames, frame_stride, row_stride,
+                                                  lap[0], lap[1], V(stream or 0)), "plvi_stereo_frame_extract_batch")
 
 
 class StepGraph:

@@ -412,3 +412,91 @@ def test_stereo_lines_batch_on_extractor_outputs():
         assert np.array_equal(m12h[f, :nl[f]], m)
         assert np.array_equal(disph[f, :nl[f]], d) and np.array_equal(deph[f, :nl[f]], z)
         assert np.array_equal(leh[f, :nl[f]], l_)
+
+
+@pytest.mark.gpu
+def test_stereo_frame_schedule_then_stereo_matching():
+    """The stereo-line Frame (src/Frame.cc:200-249) as one call: ORB and lines
+    of the left and right images as two concurrent frame schedules
+    (plvi_stereo_frame_extract_batch), then ComputeStereoMatches and
+    ComputeStereoMatches_Lines on the same stream.  Each side equals its own
+    single-schedule extraction bit for bit, a left and a right frame equal
+    the oracle, and the stereo tables equal the oracle's on every pair."""
+    import torch
+    import plvi
+    B = 4
+    pairs = [synth.stereo_pair(300 + i) for i in range(B)]
+    lib = plvi.load()
+    L = np.stack([p[0] for p in pairs])
+    R = np.stack([p[1] for p in pairs])
+    bl, br = plvi.DeviceBuffer(L.nbytes), plvi.DeviceBuffer(R.nbytes)
+    bl.upload(L)
+    br.upload(R)
+    mk = lambda: (plvi.ORBextractor(1000, 1.2, 8, 20, 7, 640, 480, max_batch=B),  # noqa: E731
+                  plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 640, 480, max_batch=B))
+    (ol_, ll_), (or_, lr_) = mk(), mk()
+    s = torch.cuda.Stream()
+    st = s.cuda_stream
+    plvi.stereo_frame_extract_batch(ol_, or_, ll_, lr_, bl.ptr, br.ptr, B, 640 * 480, 640, stream=st)
+    cap = ol_.kp_cap
+    out = plvi.DeviceBuffer(B * cap * 8 + B * 4 + 4)
+    ur, dp, ns, err = out.ptr, out.ptr + B * cap * 4, out.ptr + B * cap * 8, out.ptr + B * cap * 8 + B * 4
+    out.upload(np.zeros(B * cap * 2 + B + 1, np.int32))
+    plvi.stereo_match_batch(ol_, or_, B, MB, MBF, ur, dp, ns, err, stream=st)
+    kl, dl, _, cl, lcap = ll_.outputs()
+    kr, dr, _, cr, lcapr = lr_.outputs()
+    idx_cap = 32768
+    sb = plvi.stereo_lines_scratch_bytes(B, lcap, lcapr, idx_cap)
+    scratch = plvi.DeviceBuffer(sb)
+    o = plvi.DeviceBuffer(B * lcap * (4 + 8 + 8 + 24) + B * 4 + 4)
+    m12 = o.ptr
+    disp, dep = m12 + B * lcap * 4, m12 + B * lcap * 12
+    le, lns = m12 + B * lcap * 20, m12 + B * lcap * 44
+    lerr = lns + B * 4
+    o.upload(np.zeros(o.nbytes, np.uint8))
+    plvi.stereo_lines_batch(B, kl, dl, cl, lcap, kr, dr, cr, lcapr, None, 640, 480, MBF, 0, idx_cap, scratch.ptr, sb,
+                            m12, disp, dep, le, lns, lerr, stream=st)
+    torch.cuda.synchronize()
+    assert plvi.download(err, np.zeros(1, np.int32))[0] == 0 and plvi.download(lerr, np.zeros(1, np.int32))[0] == 0
+    assert ol_.errors() == 0 and or_.errors() == 0 and ll_.errors() == 0 and lr_.errors() == 0
+
+    def tabs(orb, lx):
+        kp, de, co, _, c = orb.outputs()
+        k2, d2, _, c2, cc = lx.outputs()
+        n = plvi.download(co, np.zeros(B, np.int32))
+        m = plvi.download(c2, np.zeros(B, np.int32))
+        K = plvi.download(kp, np.zeros(B * c, plvi.KEYPOINT_DTYPE)).reshape(B, c)
+        D = plvi.download(de, np.zeros((B * c, 32), np.uint8)).reshape(B, c, 32)
+        KL = plvi.download(k2, np.zeros(B * cc, plvi.KEYLINE_DTYPE)).reshape(B, cc)
+        DL = plvi.download(d2, np.zeros((B * cc, 32), np.uint8)).reshape(B, cc, 32)
+        return [(K[f, :n[f]], D[f, :n[f]], KL[f, :m[f]], DL[f, :m[f]]) for f in range(B)]
+    sides = tabs(ol_, ll_), tabs(or_, lr_)
+    # each side equals its own single-side frame schedule
+    for img_buf, side in ((bl, sides[0]), (br, sides[1])):
+        o2, l2 = mk()
+        plvi.frame_extract_batch(o2, l2, img_buf.ptr, B, 640 * 480, 640)
+        lib.plvi_device_synchronize()
+        for a, b in zip(side, tabs(o2, l2)):
+            assert all(x.tobytes() == y.tobytes() for x, y in zip(a, b))
+    # left frame 0 and right frame B-1 against the oracle
+    for img, t in ((L[0], sides[0][0]), (R[B - 1], sides[1][B - 1])):
+        _, ek, ed = oracle_lib.orb_extract(img)
+        assert t[0].tobytes() == ek.astype(plvi.KEYPOINT_DTYPE).tobytes() and np.array_equal(t[1], ed)
+        ekl, eld, _ = oracle_lib.line_extract(img)
+        assert t[2].tobytes() == ekl.astype(plvi.KEYLINE_DTYPE).tobytes() and np.array_equal(t[3], eld)
+    # stereo tables
+    scale, inv = ol_.GetScaleFactors(), ol_.GetInverseScaleFactors()
+    urh = plvi.download(ur, np.zeros((B, cap), np.float32))
+    dph = plvi.download(dp, np.zeros((B, cap), np.float32))
+    nsh = plvi.download(ns, np.zeros(B, np.int32))
+    m12h = plvi.download(m12, np.zeros((B, lcap), np.int32))
+    lnsh = plvi.download(lns, np.zeros(B, np.int32))
+    for f in range(B):
+        (k, d, a, da), (kr_, dr_, b, db) = sides[0][f], sides[1][f]
+        pL = [ol_.pyramid_level(lv, f) for lv in range(8)]
+        pR = [or_.pyramid_level(lv, f) for lv in range(8)]
+        n, eu, ed = oracle_lib.stereo_match(k, d, kr_, dr_, pL, pR, scale, inv, MB, MBF)
+        assert nsh[f] == n > 100
+        assert np.array_equal(urh[f, :len(k)], eu) and np.array_equal(dph[f, :len(k)], ed)
+        n2, m, _, _, _ = oracle_lib.stereo_lines(a, da, b, db, None, 640, 480, MBF)
+        assert lnsh[f] == n2 > 5 and np.array_equal(m12h[f, :len(a)], m)

@@ -18,6 +18,9 @@ use_torch = "--torch" in sys.argv
 args = [a for a in sys.argv[1:] if a != "--torch"]
 if use_torch:
     import torch  # noqa: F401,E402
+else:
+    import os
+    os.environ["PLVI_NO_TORCH"] = "1"  # plvi.load() would import torch (and its HIP runtime) first
 import numpy as np  # noqa: E402
 
 import plvi  # noqa: E402
