@@ -401,7 +401,10 @@ struct LinePipeline {
         }
         return PLVI_OK;
     }
-    static constexpr int kMwWaves = 16;
+#ifndef PLVI_MW_WAVES
+#define PLVI_MW_WAVES 16
+#endif
+    static constexpr int kMwWaves = PLVI_MW_WAVES;  // waves per (frame, octave) of the multi-wave kernel
     bool rectLanes = true;
     int mwMaxFrames = 0, mwSlots = 0;
     size_t mwSmem = 0, mwOwnTask = 0;
@@ -549,10 +552,27 @@ struct LinePipeline {
         if (nf <= 0 || nf > Bcap) return PLVI_E_BADARG;
         if (!st) st = stream;
         lastFrames = nf;
+        // the LBD Sobel pyramid depends on the frames only: it runs on aux[1]
+        // beside prep + region growing and joins before the LBD describe
+        // (stage profiling and stream capture keep the sequential order)
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        PLVI_CHECK(hipStreamIsCapturing(st, &cs));
+        const bool fork = !prof && aux[1] && cs == hipStreamCaptureStatusNone;
+        int rc = PLVI_OK;
+        if (fork) {
+            PLVI_CHECK(hipEventRecord(evFork, st));
+            PLVI_CHECK(hipStreamWaitEvent(aux[1], evFork, 0));
+            rc = launch_sobel(d_frames, nf, frame_stride, row_stride, aux[1]);
+            PLVI_CHECK(hipEventRecord(evSobel, aux[1]));
+        }
         mark(0, st);
         launch_prep(d_frames, nf, frame_stride, row_stride, st);
         launch_grow_assemble(nf, st);
-        int rc = launch_sobel(d_frames, nf, frame_stride, row_stride, st);
+        if (fork) {
+            PLVI_CHECK(hipStreamWaitEvent(st, evSobel, 0));
+        } else {
+            rc = launch_sobel(d_frames, nf, frame_stride, row_stride, st);
+        }
         if (rc) return rc;
         launch_describe(nf, st);
         if (prof && profRuns < kRing) ++profRuns;

@@ -10,4 +10,5 @@ for v in default ${VARIANTS:-}; do
   echo "== $v" >> $OUT/mw_ab.log
   PLVI_LIB=$L timeout -k 10 150 python tools/mw_probe.py 1,64 2>&1 | grep "mw=256" | cut -c1-400 >> $OUT/mw_ab.log || exit $?
   PLVI_LIB=$L timeout -k 10 120 python tools/b64_probe.py 64 20 2>&1 | grep FPS >> $OUT/mw_ab.log || exit $?
+  PLVI_LIB=$L timeout -k 10 120 python tools/latency_probe.py 2>&1 | grep median >> $OUT/mw_ab.log || exit $?
 done
