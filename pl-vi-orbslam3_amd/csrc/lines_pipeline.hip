@@ -441,9 +441,11 @@ struct LinePipeline {
     }
 
     // Phase A: octave pyramid + LSD prep (LK1, LK2).
-    void launch_prep(const uint8_t* d_frames, int nf, size_t frame_stride, size_t row_stride, hipStream_t st) {
+    void launch_prep(const uint8_t* d_frames, int nf, size_t frame_stride, size_t row_stride, hipStream_t st,
+                     int lFirst = 0, int lEnd = -1) {
         const uint8_t* T = d_tabs.as<uint8_t>();
-        for (int l = 1; l < nOct; ++l) {
+        if (lEnd < 0) lEnd = nOct;
+        for (int l = 1; l < nOct && lFirst == 0; ++l) {
             const LineOctDev& d = oct[l];
             const uint8_t* s = l == 1 ? d_frames : octImg.as<uint8_t>() + oct[l - 1].off;
             const size_t sf = l == 1 ? frame_stride : (size_t)oct[l - 1].plane;
@@ -451,8 +453,8 @@ struct LinePipeline {
             hipLaunchKernelGGL(lsd_half_kernel, dim3((d.w * d.h + 255) / 256, nf), dim3(256), 0, st, s, sf, sr,
                                octImg.as<uint8_t>() + d.off, d.w, d.h, (size_t)d.plane);
         }
-        mark(1, st);
-        for (int l = 0; l < nOct; ++l) {
+        if (lFirst == 0) mark(1, st);
+        for (int l = lFirst; l < lEnd; ++l) {
             const LineOctDev& d = oct[l];
             const uint8_t* s = l == 0 ? d_frames : octImg.as<uint8_t>() + d.off;
             const size_t sf = l == 0 ? frame_stride : (size_t)d.plane;
@@ -470,7 +472,7 @@ struct LinePipeline {
                 ++kn;
             }
         }
-        mark(2, st);
+        if (lEnd == nOct) mark(2, st);
     }
 
     // Phase B: region growing (LK3) + keyline assembly / top-k (LK4).
@@ -566,8 +568,23 @@ struct LinePipeline {
             PLVI_CHECK(hipEventRecord(evSobel, aux[1]));
         }
         mark(0, st);
-        launch_prep(d_frames, nf, frame_stride, row_stride, st);
-        launch_grow_assemble(nf, st);
+        if (fork && nOct > 1 && nf <= mwMaxFrames) {
+            // small batches (latency): octave 0's region growing, the long
+            // pole, starts right after its own prep; the other octaves are
+            // prepared and grown on aux[0] beside it
+            launch_prep(d_frames, nf, frame_stride, row_stride, st, 0, 1);
+            PLVI_CHECK(hipEventRecord(evPrep, st));
+            PLVI_CHECK(hipStreamWaitEvent(aux[0], evPrep, 0));
+            launch_prep(d_frames, nf, frame_stride, row_stride, aux[0], 1, nOct);
+            launch_grow(nf, 1, nOct - 1, aux[0]);
+            PLVI_CHECK(hipEventRecord(evGrow2, aux[0]));
+            launch_grow(nf, 0, 1, st);
+            PLVI_CHECK(hipStreamWaitEvent(st, evGrow2, 0));
+            launch_grow_assemble(nf, st, true);
+        } else {
+            launch_prep(d_frames, nf, frame_stride, row_stride, st);
+            launch_grow_assemble(nf, st);
+        }
         if (fork) {
             PLVI_CHECK(hipStreamWaitEvent(st, evSobel, 0));
         } else {

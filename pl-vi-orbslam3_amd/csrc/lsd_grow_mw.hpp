@@ -56,6 +56,16 @@ constexpr int kMwLog = 256;         // dispatch log entries (seed order)
 #define PLVI_MW_GROWER_PRIO 3
 #endif
 constexpr int kMwLook = PLVI_MW_LOOK;  // dispatch-log entries ahead of the walk that growers revalidate (0 = off)
+#ifndef PLVI_MW_LATE
+#define PLVI_MW_LATE 0
+#endif
+// second-chance dispatch: an idle grower takes an undispatched seed just
+// ahead of the walk (skipped by the cursor because a dropped or regrown
+// region had claimed it, H) and files it in a small unordered "late" log
+constexpr int kMwLate = PLVI_MW_LATE;  // late-log entries (0 = off, the default: at 32 the undispatched
+                                       // seeds fall 119 -> 43 but dropped regions rise 338 -> 1036 and the
+                                       // kernel takes 10.9 instead of 7.1 ms per frame; <= 64)
+constexpr int kMwLateWords = 64;       // bitmap words ahead of the walk a grower scans for them
 
 // slot states; COMMITTED: validated and committed, a grower still copies
 // its points out (regions of more than kMwSP points); WALKING: the walker
@@ -79,6 +89,7 @@ struct MwCtl {
     int lock, dlock, head, cursor, finished, npts, nout, overflow;
     int dlog_n, wptr, ncommit, pad1;  // dispatch log: entries appended / next entry the walk examines;
                                       // regions committed so far (revalidation epoch)
+    int late_seed[kMwLate > 0 ? kMwLate : 1], late_slot[kMwLate > 0 ? kMwLate : 1];  // late log (seed -1: free)
     int stat[16];  // [0] dispatched [1] dropped [2] regrown [3] exact (undispatched) [4] trivial [5] committed
                    // speculative [6] walk cycles [7] walker growth cycles [8] walk entries [9] blocked on a
                    // growing head [10] kernel cycles (wave 0) [11] speculative growth cycles (sum over waves)
@@ -390,7 +401,20 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
         const int dn = mw_lds_load(&ctl->dlog_n);
         while (wp < dn && dlog[2 * (wp & (kMwLog - 1))] < q) ++wp;
         int si = -1;
-        if (wp < dn && dlog[2 * (wp & (kMwLog - 1))] == q) si = dlog[2 * (wp & (kMwLog - 1)) + 1];
+        bool fromLog = false;
+        if (wp < dn && dlog[2 * (wp & (kMwLog - 1))] == q) {
+            si = dlog[2 * (wp & (kMwLog - 1)) + 1];
+            fromLog = true;
+        } else if (kMwLate > 0) {
+            // a second-chance region (late log, unordered: lanes compare)
+            mw_cfence();
+            const bool hit = lane < kMwLate &&
+                             __hip_atomic_load(&ctl->late_seed[lane < kMwLate ? lane : 0], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP) == q;
+            const unsigned long long hb = __ballot(hit);
+            if (hb) si = ctl->late_slot[__ffsll((long long)hb) - 1];
+            mw_cfence();
+        }
         lds_slot* S = si >= 0 ? mw_slot(pool, si) : nullptr;
         int sst = si >= 0 ? mw_lds_load(&S->state) : kMwFree;
         if (sst == kMwDone) {
@@ -411,7 +435,7 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
             blocked = si;
             break;
         }
-        if (si >= 0) ++wp;
+        if (fromLog) ++wp;
         int n = 0;
         bool done = false;
         if (sst == kMwDone) {
@@ -584,6 +608,75 @@ __device__ __forceinline__ int mw_dispatch(const MwEnv& E, lds_u8* pool, int nsl
     return q;
 }
 
+// Second-chance dispatch (caller holds dlock): the first pixel at or after
+// the walk within kMwLateWords bitmap words that is neither committed /
+// NOTDEF nor trivial but claimed (H) and is no live slot's seed -- a seed the
+// cursor skipped because a region that was later dropped or regrown had
+// claimed it; the walker would grow it exactly.  It takes a free slot and a
+// free late-log entry (seed -1 or passed by the walk).  Returns the seed or -1.
+__device__ __forceinline__ int mw_second_chance(const MwEnv& E, lds_u8* pool, int nslots, int& slot, int lane) {
+    lds_ctl* ctl = E.ctl;
+    const int nwords = E.sh * E.wpr;
+    const int head = mw_lds_load(&ctl->head);
+    const int ls = lane < kMwLate ? ctl->late_seed[lane] : 0;
+    const unsigned long long lfree = __ballot(lane < kMwLate && ls < head);
+    if (!lfree) return -1;
+    const int le = __ffsll((long long)lfree) - 1;
+    slot = -1;
+    for (int b0 = 0; b0 < nslots && slot < 0; b0 += 64) {
+        const int si = b0 + lane;
+        bool ok = false;
+        if (si < nslots) {
+            lds_slot* S = mw_slot(pool, si);
+            const int st = S->state;
+            ok = st == kMwFree || (st == kMwDone && S->seed < head);
+        }
+        const unsigned long long b = __ballot(ok);
+        if (b) slot = b0 + __ffsll((long long)b) - 1;
+    }
+    if (slot < 0) return -1;
+    const int w0 = head >> 5;
+    for (int wb = w0; wb < min(nwords, w0 + kMwLateWords); wb += 64) {
+        const int w = wb + lane;
+        unsigned m = 0;
+        if (w < nwords && w < w0 + kMwLateWords) {
+            m = ~E.C[w] & ~E.T[w] & E.H[w];
+            if (w == w0) m &= ~0u << (head & 31);
+        }
+        unsigned long long has = __ballot(m != 0u);
+        while (has) {
+            const int l = __ffsll((long long)has) - 1;
+            has &= has - 1;
+            unsigned mm = (unsigned)readlane_i((int)m, l);
+            while (mm) {
+                const int q = (wb + l) * 32 + (__ffs((int)mm) - 1);
+                mm &= mm - 1;
+                // no live slot holds it (a dispatched seed keeps its slot until the walk passes it)
+                bool live = false;
+                for (int b0 = 0; b0 < nslots; b0 += 64) {
+                    const int si = b0 + lane;
+                    if (si < nslots) {
+                        lds_slot* S = mw_slot(pool, si);
+                        live |= S->seed == q && S->state != kMwFree;
+                    }
+                }
+                if (__ballot(live)) continue;
+                if (lane == 0) {
+                    lds_slot* S = mw_slot(pool, slot);
+                    S->seed = q;
+                    S->ovf = 0;
+                    S->chk = ctl->ncommit;
+                    S->state = kMwGrowing;  // before the late entry that names it
+                    ctl->late_slot[le] = slot;
+                    mw_lds_store(&ctl->late_seed[le], q);
+                }
+                return q;
+            }
+        }
+    }
+    return -1;
+}
+
 // Copy region points [0, n) from queue A to queue B (one wave).
 __device__ __forceinline__ void mw_copy_points(const MwQueue& A, const MwQueue& B, int n, int lane) {
     bool g = false;
@@ -682,6 +775,7 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
         ctl->lock = ctl->dlock = ctl->head = ctl->cursor = ctl->finished = 0;
         ctl->npts = ctl->nout = ctl->overflow = 0;
         ctl->dlog_n = ctl->wptr = ctl->ncommit = 0;
+        for (int i = 0; i < kMwLate; ++i) ctl->late_seed[i] = -1;
         for (int i = 0; i < 16; ++i) ctl->stat[i] = 0;
     }
     __syncthreads();
@@ -804,6 +898,10 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
             int q = -1, si = -1;
             if (mw_try_lock(&ctl->dlock, lane)) {
                 q = mw_dispatch<STATS>(E, pool, nslots, dlog, si, lane);
+                mw_unlock(&ctl->dlock, lane);
+            }
+            if (q < 0 && kMwLate > 0 && mw_try_lock(&ctl->dlock, lane)) {
+                q = mw_second_chance(E, pool, nslots, si, lane);
                 mw_unlock(&ctl->dlock, lane);
             }
             if (q < 0) {
