@@ -75,6 +75,7 @@ struct LinePipeline {
     bool growAfterBlur = true, sobelWithGrow = false, growSplit = false;
     hipStream_t critStream = nullptr;  // frame schedule: prep -> grow -> describe
     hipStream_t crit2 = nullptr;       // frame schedule: octave-1 region growing (split mode)
+    hipStream_t octStream = nullptr;   // small batches: prep + growth of octaves >= 1 beside octave 0's
     bool orbAfterPrep = false;
     std::vector<LineOctDev> oct;
     std::vector<float> scaleF, invScaleF;
@@ -125,6 +126,7 @@ struct LinePipeline {
             if (e) (void)hipEventDestroy(e);
         if (critStream) (void)hipStreamDestroy(critStream);
         if (crit2) (void)hipStreamDestroy(crit2);
+        if (octStream) (void)hipStreamDestroy(octStream);
         for (auto a : aux)
             if (a) (void)hipStreamDestroy(a);
         if (stream) (void)hipStreamDestroy(stream);
@@ -181,6 +183,9 @@ struct LinePipeline {
             // handles can put two streams of one schedule on one queue
             if (prio && growSplit)
                 PLVI_CHECK(hipStreamCreateWithPriority(&crit2, hipStreamNonBlocking, greatest));
+            // normal priority: the octave-1 growth is not the long pole, and the
+            // greatest-priority pool stays at two streams per handle
+            PLVI_CHECK(hipStreamCreateWithFlags(&octStream, hipStreamNonBlocking));
         }
         for (auto* e : {&evFork, &evPrep, &evSobel, &evOrb, &evCrit, &evBlur, &evGate, &evGrow2, &evPair})
             PLVI_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
@@ -614,8 +619,18 @@ struct LinePipeline {
         hipStream_t crit = critStream ? critStream : st;
         PLVI_CHECK(hipEventRecord(evFork, st));
         if (crit != st) PLVI_CHECK(hipStreamWaitEvent(crit, evFork, 0));
-        launch_prep(d_frames, nf, frame_stride, row_stride, crit);
+        // small batches (multi-wave growth): octave 0, the long pole, grows
+        // right after its own prep; the other octaves are prepared and grown
+        // on octStream beside it
+        const bool octFirst = nf <= mwMaxFrames && nOct > 1 && octStream;
+        launch_prep(d_frames, nf, frame_stride, row_stride, crit, 0, octFirst ? 1 : nOct);
         PLVI_CHECK(hipEventRecord(evPrep, crit));
+        if (octFirst) {
+            PLVI_CHECK(hipStreamWaitEvent(octStream, evPrep, 0));
+            launch_prep(d_frames, nf, frame_stride, row_stride, octStream, 1, nOct);
+            launch_grow(nf, 1, nOct - 1, octStream);
+            PLVI_CHECK(hipEventRecord(evGrow2, octStream));
+        }
         hipEvent_t auxStart = orbAfterPrep ? evPrep : evFork;
         PLVI_CHECK(hipStreamWaitEvent(aux[0], auxStart, 0));
         // only a batch whose region-growing waves fill the SIMDs (>= 2 per SIMD
@@ -646,7 +661,13 @@ struct LinePipeline {
             PLVI_CHECK(hipEventRecord(evGrow2, crit2));
             PLVI_CHECK(hipStreamWaitEvent(crit, evGrow2, 0));
         }
-        launch_grow_assemble(nf, crit, split);
+        if (octFirst) {
+            launch_grow(nf, 0, 1, crit);
+            PLVI_CHECK(hipStreamWaitEvent(crit, evGrow2, 0));
+            launch_grow_assemble(nf, crit, true);
+        } else {
+            launch_grow_assemble(nf, crit, split);
+        }
         PLVI_CHECK(hipStreamWaitEvent(crit, evSobel, 0));
         launch_describe(nf, crit);
         if (crit != st) {
