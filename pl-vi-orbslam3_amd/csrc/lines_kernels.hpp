@@ -956,7 +956,7 @@ __global__ __launch_bounds__(256) void line_assemble_kernel(const LineOctDev* __
                                                             plvi_keyline* __restrict__ kl_tmp, int* __restrict__ err) {
     __shared__ int s_scan[256];
     __shared__ int s_base;
-    __shared__ SortItem s_items[kKlCap];
+    __shared__ __align__(8) SortItem s_items[kKlCap];
     const int f = blockIdx.x;
     plvi_keyline* tmp = kl_tmp + (size_t)f * kKlCap;
     if (threadIdx.x == 0) s_base = 0;
@@ -1030,11 +1030,46 @@ __global__ __launch_bounds__(256) void line_assemble_kernel(const LineOctDev* __
     int nfinal = n;
     const bool truncate = n > nfeatures && nfeatures != 0;
     if (truncate) {
-        for (int i = threadIdx.x; i < n; i += 256) s_items[i] = SortItem{tmp[i].response, i};
-        __syncthreads();
-        if (threadIdx.x == 0) std_sort(s_items, s_items + n);
-        __syncthreads();
         nfinal = nfeatures;
+        // LineExtractor.cc:75-84 sorts by response, descending, with libstdc++
+        // std::sort.  Without equal keys among the kept lines (and the one
+        // after them) any sort gives its order: a block-wide bitonic sort of
+        // (response desc, index) keys, then a tie check; only a frame with
+        // such a tie replays the std::sort restatement on one thread.
+        int P = 256;
+        while (P < n) P <<= 1;
+        unsigned long long* K = reinterpret_cast<unsigned long long*>(s_items);
+        for (int i = threadIdx.x; i < P; i += 256)
+            K[i] = i < n ? ((0xFFFFFFFFull - (unsigned long long)__float_as_uint(tmp[i].response)) << 32) |
+                               (unsigned)i
+                         : ~0ull;
+        __syncthreads();
+        for (int k = 2; k <= P; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int t = threadIdx.x; t < P / 2; t += 256) {
+                    const int i = (t / j) * 2 * j + (t % j), ixj = i + j;
+                    const bool asc = (i & k) == 0;
+                    const unsigned long long x = K[i], y = K[ixj];
+                    if ((x > y) == asc) {
+                        K[i] = y;
+                        K[ixj] = x;
+                    }
+                }
+                __syncthreads();
+            }
+        bool tie = false;
+        for (int i = threadIdx.x; i < nfinal && i + 1 < n; i += 256) tie |= (K[i] >> 32) == (K[i + 1] >> 32);
+        if (__syncthreads_or(tie)) {
+            for (int i = threadIdx.x; i < n; i += 256) s_items[i] = SortItem{tmp[i].response, i};
+            __syncthreads();
+            if (threadIdx.x == 0) std_sort(s_items, s_items + n);
+        } else {
+            for (int i = threadIdx.x; i < nfinal; i += 256) {
+                const unsigned long long v = K[i];
+                s_items[i] = SortItem{tmp[(int)(v & 0xffffffffu)].response, (int)(v & 0xffffffffu)};
+            }
+        }
+        __syncthreads();
     }
     if (nfinal > fcap) {
         if (threadIdx.x == 0) { count_out[f] = 0; atomicOr(err + f, 8); }
@@ -1089,6 +1124,10 @@ __device__ __forceinline__ uint32_t lb_ld4(const uint8_t* p) {
     return v;
 }
 constexpr int kLbOutLanes = 62;  // output lanes per strip (4 columns each)
+#ifndef PLVI_LB_BANDS
+#define PLVI_LB_BANDS 4
+#endif
+constexpr int kLbBands = PLVI_LB_BANDS;  // row bands per strip of lbd_sobel0_kernel (more waves per frame)
 
 __global__ __launch_bounds__(64) void lbd_sobel0_kernel(const uint8_t* __restrict__ src, size_t s_frame, size_t s_row,
                                                         int w, int h, int strip_w, uint8_t* __restrict__ blur,
@@ -1097,6 +1136,12 @@ __global__ __launch_bounds__(64) void lbd_sobel0_kernel(const uint8_t* __restric
     const int f = blockIdx.y;
     const int lane = threadIdx.x;
     const int X0 = blockIdx.x * strip_w, X1 = min(X0 + strip_w, w);
+    // row band [Y0, Y1) of gridDim.z bands: blurred rows from Y0 - 1 (the
+    // Sobel of row Y0 needs it), input rows from Y0 - 3; reflection only at
+    // the image's own top and bottom
+    const int nb = gridDim.z, Y0 = (int)((long long)h * blockIdx.z / nb), Y1 = (int)((long long)h * (blockIdx.z + 1) / nb);
+    if (Y1 <= Y0) return;
+    const bool top = Y0 == 0, bottom = Y1 == h;
     const int c0 = X0 - 4 + 4 * lane;
     const bool need = c0 < X1 + 4;                      // output lanes and the two halo lanes
     const bool inner = need && c0 >= 0 && c0 + 4 <= w;  // a plain dword load
@@ -1134,7 +1179,7 @@ __global__ __launch_bounds__(64) void lbd_sobel0_kernel(const uint8_t* __restric
         const int gy1 = (int)(De & 0xffffu) + 2 * (int)(Do & 0xffffu) + (int)(De >> 16) - 1020;
         const int gy2 = (int)(Do & 0xffffu) + 2 * (int)(De >> 16) + (int)(Do >> 16) - 1020;
         const int gy3 = (int)(De >> 16) + 2 * (int)(Do >> 16) + (int)(Der & 0xffffu) - 1020;
-        if (!outl) return;
+        if (!outl || y < Y0 || y >= Y1) return;
         short2* o = Gp + (size_t)y * w + c0;
         const short2 g4[4] = {make_short2((short)gx0, (short)gy0), make_short2((short)gx1, (short)gy1),
                               make_short2((short)gx2, (short)gy2), make_short2((short)gx3, (short)gy3)};
@@ -1144,16 +1189,18 @@ __global__ __launch_bounds__(64) void lbd_sobel0_kernel(const uint8_t* __restric
             for (int j = 0; j < nout; ++j) o[j] = g4[j];
         }
     };
+    const int rS = top ? -2 : Y0 - 3, rE = bottom ? h + 2 : Y1 + 3;
+    const int yS = top ? 0 : Y0 - 1;
     uint32_t pv[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) pv[k] = load_row(k - 2);
-    for (int rb = -2; rb < h + 2; rb += 8) {
+    for (int k = 0; k < 8; ++k) pv[k] = rS + k < rE ? load_row(rS + k) : 0u;
+    for (int rb = rS; rb < rE; rb += 8) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const int r = rb + k;
-            if (r >= h + 2) break;
+            if (r >= rE) break;
             const uint32_t V = pv[k];
-            if (r + 8 < h + 2) pv[k] = load_row(r + 8);
+            if (r + 8 < rE) pv[k] = load_row(r + 8);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 pe[q] = pe[q + 1];
@@ -1162,7 +1209,7 @@ __global__ __launch_bounds__(64) void lbd_sobel0_kernel(const uint8_t* __restric
             pe[4] = V & 0x00ff00ffu;
             po[4] = (V >> 8) & 0x00ff00ffu;
             const int y = r - 2;  // blurred row from rows y-2 .. y+2
-            if (y < 0) continue;
+            if (y < yS) continue;
             // vertical: E = (c0, c0+2), O = (c0+1, c0+3); fields <= 255 * 256
             const uint32_t E = pk_madu16(T0, pe[0] + pe[4], pk_madu16(T1, pe[1] + pe[3], pk_madu16(T2, pe[2], 0u)));
             const uint32_t O = pk_madu16(T0, po[0] + po[4], pk_madu16(T1, po[1] + po[3], pk_madu16(T2, po[2], 0u)));
@@ -1175,7 +1222,7 @@ __global__ __launch_bounds__(64) void lbd_sobel0_kernel(const uint8_t* __restric
             const uint32_t h3 = lb_dot2(O, pk(t0, t2), lb_dot2(E, pk(0, t1), lb_dot2(Er, pk(t1, 0), lb_dot2(Or, pk(t0, 0), 0u))));
             const uint32_t Bv = min((h0 + 32768u) >> 16, 255u) | min((h1 + 32768u) >> 16, 255u) << 8 |
                                 min((h2 + 32768u) >> 16, 255u) << 16 | min((h3 + 32768u) >> 16, 255u) << 24;
-            if (outl) {
+            if (outl && y >= Y0 && y < Y1) {
                 uint8_t* o = Bp + (size_t)y * w + c0;
                 if (nout == 4 && (w & 3) == 0) {
                     *reinterpret_cast<uint32_t*>(o) = Bv;
@@ -1184,14 +1231,16 @@ __global__ __launch_bounds__(64) void lbd_sobel0_kernel(const uint8_t* __restric
                 }
             }
             // Sobel row y - 1 (needs blurred rows y-2 .. y; row -1 = row 1)
-            if (y == 1) sobel_row(0, Bv, b0, Bv);
-            else if (y >= 2) sobel_row(y - 1, bm1, b0, Bv);
+            if (top && y == 1) sobel_row(0, Bv, b0, Bv);
+            else if (y >= yS + 2) sobel_row(y - 1, bm1, b0, Bv);
             bm1 = b0;
             b0 = Bv;
         }
     }
-    if (h >= 2) sobel_row(h - 1, bm1, b0, bm1);  // row h = row h - 2
-    else sobel_row(0, b0, b0, b0);
+    if (bottom) {
+        if (h >= 2) sobel_row(h - 1, bm1, b0, bm1);  // row h = row h - 2
+        else sobel_row(0, b0, b0, b0);
+    }
 }
 
 // LB2: pyrDown(blurred octave 0) + Sobel.

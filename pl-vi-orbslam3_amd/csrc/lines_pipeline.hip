@@ -530,7 +530,7 @@ struct LinePipeline {
             // column strips of at most kLbOutLanes * 4 columns, balanced, multiples of 4
             const int ns = (d0.lw + 4 * kLbOutLanes - 1) / (4 * kLbOutLanes);
             const int sw4 = ((d0.lw + ns - 1) / ns + 3) & ~3;
-            hipLaunchKernelGGL(lbd_sobel0_kernel, dim3((d0.lw + sw4 - 1) / sw4, nf), dim3(64), 0, st, d_frames,
+            hipLaunchKernelGGL(lbd_sobel0_kernel, dim3((d0.lw + sw4 - 1) / sw4, nf, kLbBands), dim3(64), 0, st, d_frames,
                                frame_stride, row_stride, d0.lw, d0.lh, sw4, lbdBlur.as<uint8_t>(),
                                lbdG.as<short2>() + d0.loff, (size_t)d0.lplane, lbdTaps[0], lbdTaps[1], lbdTaps[2]);
         }

@@ -788,6 +788,76 @@ __global__ __launch_bounds__(64) void orb_sat_strip_kernel(const OrbLevelDev* __
     }
 }
 
+// The same table with four columns per lane: one wave covers four 64-column
+// strips (lanes 16g..16g+15 = strip 4w+g), one dword load per row and lane,
+// the strip-local prefix counts from four ballots masked to the lane's
+// 16-lane group, the four ushort entries of a lane stored as one 8-byte
+// store.  A quarter of the waves and load / store instructions.
+#ifndef PLVI_SAT_QUAD
+#define PLVI_SAT_QUAD 1
+#endif
+__global__ __launch_bounds__(64) void orb_sat_quad_kernel(const OrbLevelDev* __restrict__ lvs,
+                                                          const uint8_t* __restrict__ cand,
+                                                          unsigned short* __restrict__ lsat, int* __restrict__ carry) {
+    const int w = blockIdx.x, l = blockIdx.y, f = blockIdx.z;
+    const OrbLevelDev& L = lvs[l];
+    const int nS = L.satStrips;
+    if (4 * w >= nS) return;
+    const int lane = threadIdx.x, g = lane >> 4, s = 4 * w + g, xb = 256 * w + 4 * lane, pitch = 64 * nS;
+    const bool live = s < nS;
+    unsigned short* base = lsat + L.satOff + (size_t)f * L.satPlane;
+    int* T = carry + L.carryOff + (size_t)f * L.carryPlane;
+    const uint8_t* C0 = cand + L.boff + (size_t)f * L.bplane + (size_t)L.minB * L.bpitch + L.minB;
+    if (live) *reinterpret_cast<unsigned long long*>(base + xb) = 0ull;
+    if (live && (lane & 15) == 0) T[s + 1] = 0;
+    const unsigned long long below = ((1ull << lane) - 1ull) & ~((1ull << (16 * g)) - 1ull);
+    const unsigned long long group = 0xffffull << (16 * g);
+    const bool full = xb + 4 <= L.rw;
+    unsigned acc[4] = {0u, 0u, 0u, 0u};
+    int tot = 0;
+    for (int y0 = 1; y0 <= L.rh; y0 += kSatRowsPerWave) {
+        uint32_t v[kSatRowsPerWave];
+#pragma unroll
+        for (int k = 0; k < kSatRowsPerWave; ++k) {
+            const int y = y0 + k;  // SAT row y counts image row y-1 of the region
+            uint32_t u = 0u;
+            if (y <= L.rh && live && xb < L.rw) {
+                const uint8_t* r = C0 + (size_t)(y - 1) * L.bpitch + xb;
+                if (full) {
+                    u = ld_u32(r);
+                } else {
+                    for (int j = 0; j < 4; ++j)
+                        if (xb + j < L.rw) u |= (uint32_t)r[j] << (8 * j);
+                }
+            }
+            v[k] = u;
+        }
+#pragma unroll
+        for (int k = 0; k < kSatRowsPerWave; ++k) {
+            const uint32_t u = v[k];
+            const bool i0 = (u & 0xffu) != 0u, i1 = (u & 0xff00u) != 0u, i2 = (u & 0xff0000u) != 0u,
+                       i3 = (u & 0xff000000u) != 0u;
+            const unsigned long long m0 = __ballot(i0), m1 = __ballot(i1), m2 = __ballot(i2), m3 = __ballot(i3);
+            const unsigned cb = (unsigned)(__popcll(m0 & below) + __popcll(m1 & below) + __popcll(m2 & below) +
+                                           __popcll(m3 & below));
+            acc[0] += cb;
+            acc[1] += cb + (i0 ? 1u : 0u);
+            acc[2] += cb + (i0 ? 1u : 0u) + (i1 ? 1u : 0u);
+            acc[3] += cb + (i0 ? 1u : 0u) + (i1 ? 1u : 0u) + (i2 ? 1u : 0u);
+            tot += __popcll(m0 & group) + __popcll(m1 & group) + __popcll(m2 & group) + __popcll(m3 & group);
+            const int y = y0 + k;
+            if (y <= L.rh && live) {
+                const unsigned long long e = (unsigned long long)(acc[0] & 0xffffu) |
+                                             (unsigned long long)(acc[1] & 0xffffu) << 16 |
+                                             (unsigned long long)(acc[2] & 0xffffu) << 32 |
+                                             (unsigned long long)(acc[3] & 0xffffu) << 48;
+                *reinterpret_cast<unsigned long long*>(base + (size_t)y * pitch + xb) = e;
+                if ((lane & 15) == 0) T[(size_t)y * (nS + 1) + s + 1] = tot;
+            }
+        }
+    }
+}
+
 // Carry(s, y) = sum of the strip totals left of s (in place), one thread per row.
 __global__ __launch_bounds__(256) void orb_sat_carry_kernel(const OrbLevelDev* __restrict__ lvs,
                                                             int* __restrict__ carry) {

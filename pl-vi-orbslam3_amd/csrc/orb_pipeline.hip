@@ -341,8 +341,12 @@ struct OrbPipeline {
         // K3 SAT
         int maxRh = 0, maxStrips = 0;
         for (auto& d : lv) { maxRh = std::max(maxRh, d.rh); maxStrips = std::max(maxStrips, d.satStrips); }
-        hipLaunchKernelGGL(orb_sat_strip_kernel, dim3(maxStrips, L, nf), dim3(64), 0, st, d_lv.as<OrbLevelDev>(),
-                           (const uint8_t*)Cd, sat.as<unsigned short>(), carry.as<int>());
+        if (PLVI_SAT_QUAD)
+            hipLaunchKernelGGL(orb_sat_quad_kernel, dim3((maxStrips + 3) / 4, L, nf), dim3(64), 0, st,
+                               d_lv.as<OrbLevelDev>(), (const uint8_t*)Cd, sat.as<unsigned short>(), carry.as<int>());
+        else
+            hipLaunchKernelGGL(orb_sat_strip_kernel, dim3(maxStrips, L, nf), dim3(64), 0, st, d_lv.as<OrbLevelDev>(),
+                               (const uint8_t*)Cd, sat.as<unsigned short>(), carry.as<int>());
         hipLaunchKernelGGL(orb_sat_carry_kernel, dim3((maxRh + 1 + 255) / 256, L, nf), dim3(256), 0, st,
                            d_lv.as<OrbLevelDev>(), carry.as<int>());
         mark(3, st);
