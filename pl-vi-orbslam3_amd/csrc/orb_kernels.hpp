@@ -1168,7 +1168,10 @@ __constant__ int c_umax[16];
 constexpr int kDescR = 18, kDescP = 2 * kDescR + 1, kDescPitch = 40;
 constexpr int kAngR = 15, kAngRows = 2 * kAngR + 1, kAngPitch = 32;
 
-__global__ __launch_bounds__(256) void orb_describe_kernel(const OrbLevelDev* __restrict__ lvs, int L,
+#ifndef PLVI_DESC_WPE
+#define PLVI_DESC_WPE 5
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PLVI_DESC_WPE))) void orb_describe_kernel(const OrbLevelDev* __restrict__ lvs, int L,
                                                            const uint8_t* __restrict__ pyr,
                                                            const uint8_t* __restrict__ blur,
                                                            const int* __restrict__ rect_cnt,
@@ -1181,23 +1184,36 @@ __global__ __launch_bounds__(256) void orb_describe_kernel(const OrbLevelDev* __
     uint8_t* P = patch[wv];
     uint8_t* IP = ipatch[wv];
     const int half = lane >> 5, u = (lane & 31) - 15;
-    // this lane's four tests: (x0, y0, x1, y1) of tests lane + 64k
-    float px0[4], py0[4], px1[4], py1[4];
+    // this lane's four tests (x0, y0, x1, y1) of tests lane + 64k, packed as
+    // four signed bytes per test (4 VGPRs instead of 16: one more wave per SIMD)
+    uint32_t pat[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int j = lane + 64 * k;
-        px0[k] = c_pattern[4 * j];
-        py0[k] = c_pattern[4 * j + 1];
-        px1[k] = c_pattern[4 * j + 2];
-        py1[k] = c_pattern[4 * j + 3];
+        pat[k] = (uint32_t)(uint8_t)c_pattern[4 * j] | (uint32_t)(uint8_t)c_pattern[4 * j + 1] << 8 |
+                 (uint32_t)(uint8_t)c_pattern[4 * j + 2] << 16 | (uint32_t)(uint8_t)c_pattern[4 * j + 3] << 24;
     }
-    for (int slot = blockIdx.x * 4 + wv; slot < kpCapFrame; slot += gridDim.x * 4) {
-        int l = 0;
-        while (l + 1 < L && slot >= lvs[l + 1].kpOff) ++l;
+    // the next keypoint's coordinates are loaded one slot ahead, so each
+    // keypoint costs one dependent global round trip (its boxes), not two
+    const int stride = gridDim.x * 4;
+    const int* cnt = rect_cnt + (size_t)f * L;
+    auto next_slot = [&](int s, int& lvl) {
+        for (; s < kpCapFrame; s += stride) {
+            lvl = 0;
+            while (lvl + 1 < L && s >= lvs[lvl + 1].kpOff) ++lvl;
+            if (s - lvs[lvl].kpOff < cnt[lvl]) return s;
+        }
+        return kpCapFrame;
+    };
+    int lnext = 0;
+    int snext = next_slot(blockIdx.x * 4 + wv, lnext);
+    float4 kpn = snext < kpCapFrame ? lvkp[(size_t)f * kpCapFrame + snext] : make_float4(0.f, 0.f, 0.f, 0.f);
+    while (snext < kpCapFrame) {
+        const int slot = snext, l = lnext;
+        float4 kp = kpn;
+        snext = next_slot(slot + stride, lnext);
+        if (snext < kpCapFrame) kpn = lvkp[(size_t)f * kpCapFrame + snext];
         const OrbLevelDev& lv = lvs[l];
-        const int idx = slot - lv.kpOff;
-        if (idx >= rect_cnt[(size_t)f * L + l]) continue;  // wave-uniform
-        float4 kp = lvkp[(size_t)f * kpCapFrame + slot];
         const int cx = (int)kp.x, cy = (int)kp.y;  // integer-valued level coords (>= 19 from every border)
         const int W = lv.w, BW = lv.bpitch;
         // ---- stage both boxes: dword loads first, then LDS writes
@@ -1262,10 +1278,12 @@ __global__ __launch_bounds__(256) void orb_describe_kernel(const OrbLevelDev* __
         uint64_t* out = reinterpret_cast<uint64_t*>(lvdesc + ((size_t)f * kpCapFrame + slot) * 32);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int t0 = P[(cv_round_f(px0[k] * b + py0[k] * a) + kDescR) * kDescPitch +
-                             cv_round_f(px0[k] * a - py0[k] * b) + kDescR];
-            const int t1 = P[(cv_round_f(px1[k] * b + py1[k] * a) + kDescR) * kDescPitch +
-                             cv_round_f(px1[k] * a - py1[k] * b) + kDescR];
+            const float px0 = (float)(int8_t)(pat[k] & 0xffu), py0 = (float)(int8_t)((pat[k] >> 8) & 0xffu);
+            const float px1 = (float)(int8_t)((pat[k] >> 16) & 0xffu), py1 = (float)(int8_t)(pat[k] >> 24);
+            const int t0 = P[(cv_round_f(px0 * b + py0 * a) + kDescR) * kDescPitch + cv_round_f(px0 * a - py0 * b) +
+                             kDescR];
+            const int t1 = P[(cv_round_f(px1 * b + py1 * a) + kDescR) * kDescPitch + cv_round_f(px1 * a - py1 * b) +
+                             kDescR];
             const unsigned long long m = __ballot(t0 < t1);
             if (lane == 0) out[k] = m;
         }

@@ -78,6 +78,7 @@ struct OrbPipeline {
     bool ktime = false;
     int kn = 0;
     hipEvent_t evAfterBlur = nullptr;  // frame schedule hook (plvi_orb_internal_blur_event)
+    int gateStage = 1;  // PLVI_GROW_GATE: the hook fires after the pyramid (0), blur + FAST (1), NMS (2) or the SAT (3)
     std::vector<hipEvent_t> kev;
     int ktiming(int on) {
         if (on && kev.empty()) {
@@ -134,6 +135,7 @@ struct OrbPipeline {
             return PLVI_E_BADARG;
         prm = *p;
         W = width; H = height; Bcap = max_batch; device = dev; L = p->nlevels;
+        if (const char* e = getenv("PLVI_GROW_GATE")) gateStage = std::min(3, std::max(0, atoi(e)));
         PLVI_CHECK(hipSetDevice(device));
         PLVI_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         // ORBextractor ctor (ORBextractor.cc:413-444): scaleFactor is a double member.
@@ -320,6 +322,7 @@ struct OrbPipeline {
             hipLaunchKernelGGL(orb_pyramid_kernel, dim3((nf + kPyrFrames - 1) / kPyrFrames), dim3(64 * (kPyrFrames + 1)),
                                pyrSmem, st, d_lv.as<OrbLevelDev>(), L, d_frames, frame_stride, row_stride, nf, P,
                                (const uint32_t*)d_xtab.as<uint32_t>(), xtabN, pyrFrameLds, resizeGeneric);
+        if (evAfterBlur && gateStage == 0) PLVI_CHECK(hipEventRecord(evAfterBlur, st));
         // K1b: blur + FAST score of every level (level 0 also copies the frame into its plane)
         const bool kt = ktime && kn < kKRing;
         if (kt) PLVI_CHECK(hipEventRecord(kev[2 * kn], st));
@@ -330,7 +333,7 @@ struct OrbPipeline {
             PLVI_CHECK(hipEventRecord(kev[2 * kn + 1], st));
             ++kn;
         }
-        if (evAfterBlur) PLVI_CHECK(hipEventRecord(evAfterBlur, st));
+        if (evAfterBlur && gateStage == 1) PLVI_CHECK(hipEventRecord(evAfterBlur, st));
         mark(1, st);
         // K2 cell NMS -> candidate map (zeroed first: only detection windows are written)
         PLVI_CHECK(hipMemsetAsync(Cd, 0, candBytesTotal, st));
@@ -338,6 +341,7 @@ struct OrbPipeline {
                            dim3(64), 0, st, d_cells.as<OrbCellDev>(), (int)cells.size(), d_lv.as<OrbLevelDev>(),
                            (const uint8_t*)Sc, Cd, t1, t2);
         mark(2, st);
+        if (evAfterBlur && gateStage == 2) PLVI_CHECK(hipEventRecord(evAfterBlur, st));
         // K3 SAT
         int maxRh = 0, maxStrips = 0;
         for (auto& d : lv) { maxRh = std::max(maxRh, d.rh); maxStrips = std::max(maxStrips, d.satStrips); }
@@ -350,6 +354,7 @@ struct OrbPipeline {
         hipLaunchKernelGGL(orb_sat_carry_kernel, dim3((maxRh + 1 + 255) / 256, L, nf), dim3(256), 0, st,
                            d_lv.as<OrbLevelDev>(), carry.as<int>());
         mark(3, st);
+        if (evAfterBlur && gateStage == 3) PLVI_CHECK(hipEventRecord(evAfterBlur, st));
         // K4 octree
         const size_t smem = (size_t)nodeCapMax * (6 * 4 + 14 * 2 + 1) + 16;
         hipLaunchKernelGGL(orb_octree_kernel, dim3(L, nf), dim3(64), smem, st, d_lv.as<OrbLevelDev>(),
