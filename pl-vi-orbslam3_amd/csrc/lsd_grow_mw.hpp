@@ -53,7 +53,10 @@ constexpr int kMwLog = 256;         // dispatch log entries (seed order)
 #define PLVI_MW_WALKER_PRIO 3
 #endif
 #ifndef PLVI_MW_GROWER_PRIO
-#define PLVI_MW_GROWER_PRIO 3
+#define PLVI_MW_GROWER_PRIO 1
+#endif
+#ifndef PLVI_MW_BOOST
+#define PLVI_MW_BOOST 1  // a grower whose seed the walk has reached runs at priority 3
 #endif
 constexpr int kMwLook = PLVI_MW_LOOK;  // dispatch-log entries ahead of the walk that growers revalidate (0 = off)
 #ifndef PLVI_MW_LATE
@@ -222,10 +225,19 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
     int reg_size = 1;
     const int cap = Q.lcap + Q.gcap;
     for (int i = 0; i < reg_size;) {
-        if (SPEC && mw_lds_load(&E.ctl->head) > seedb) {
-            n_out = reg_size;
-            deg_out = reg_deg;
-            return 1;
+        if (SPEC) {
+            const int hd = mw_lds_load(&E.ctl->head);
+            if (hd > seedb) {
+                n_out = reg_size;
+                deg_out = reg_deg;
+                return 1;
+            }
+            // the walk waits on this region: let it win the SIMD's issue
+            // arbitration against the other growers until it is done
+            if (PLVI_MW_BOOST) {
+                if (hd == seedb) __builtin_amdgcn_s_setprio(3);
+                else __builtin_amdgcn_s_setprio(PLVI_MW_GROWER_PRIO);
+            }
         }
         const unsigned long long tb0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
         const int nb = min(7, reg_size - i);

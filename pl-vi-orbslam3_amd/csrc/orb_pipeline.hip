@@ -137,7 +137,19 @@ struct OrbPipeline {
         W = width; H = height; Bcap = max_batch; device = dev; L = p->nlevels;
         if (const char* e = getenv("PLVI_GROW_GATE")) gateStage = std::min(3, std::max(0, atoi(e)));
         PLVI_CHECK(hipSetDevice(device));
-        PLVI_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        {
+            // the handle's own stream (single-frame calls, batches without a
+            // caller stream) at the least priority (PLVI_ORB_STREAM_PRIO=0:
+            // normal): the runtime keeps a separate hardware-queue pool per
+            // priority, so the ORB thread of Frame does not share a queue with
+            // the line extractor's normal-priority stream and hold up its
+            // critical path (ORB finishes in half the lines' time anyway)
+            int least = 0, greatest = 0;
+            PLVI_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+            const char* e = getenv("PLVI_ORB_STREAM_PRIO");
+            const bool low = !e || atoi(e) != 0;
+            PLVI_CHECK(hipStreamCreateWithPriority(&stream, hipStreamNonBlocking, low ? least : 0));
+        }
         // ORBextractor ctor (ORBextractor.cc:413-444): scaleFactor is a double member.
         const double sf = (double)p->scale_factor;
         scale.assign(L, 1.f); sigma2.assign(L, 1.f);
