@@ -19,6 +19,7 @@
 
 // internal hook of the ORB pipeline (orb_pipeline.hip): event after the blur + FAST launch
 extern "C" int plvi_orb_internal_blur_event(plvi_orb_extractor* h, hipEvent_t ev);
+extern "C" int plvi_orb_internal_stage_event(plvi_orb_extractor* h, int stage, hipEvent_t ev);
 
 namespace plvi {
 
@@ -70,9 +71,11 @@ struct LinePipeline {
     int W = 0, H = 0, Bcap = 0, device = 0, nOct = 0, fcap = 0;
     hipStream_t stream = nullptr;
     hipStream_t aux[2] = {nullptr, nullptr};  // frame mode: ORB and LBD-Sobel streams
+    hipEvent_t evSobelGo = nullptr;
     hipEvent_t evFork = nullptr, evPrep = nullptr, evSobel = nullptr, evOrb = nullptr, evCrit = nullptr,
                evBlur = nullptr, evGate = nullptr, evGrow2 = nullptr, evPair = nullptr;
     bool growAfterBlur = true, sobelWithGrow = false, growSplit = false;
+    int sobelGate = -1;  // PLVI_SOBEL_GATE: ORB stage after which the Sobel pyramid starts (-1: with growth)
     hipStream_t critStream = nullptr;  // frame schedule: prep -> grow -> describe
     hipStream_t crit2 = nullptr;       // frame schedule: octave-1 region growing (split mode)
     hipStream_t octStream = nullptr;   // small batches: prep + growth of octaves >= 1 beside octave 0's
@@ -122,7 +125,7 @@ struct LinePipeline {
     ~LinePipeline() {
         for (auto e : kev) (void)hipEventDestroy(e);
         for (auto e : evs) (void)hipEventDestroy(e);
-        for (auto e : {evFork, evPrep, evSobel, evOrb, evCrit, evBlur, evGate, evGrow2, evPair})
+        for (auto e : {evFork, evPrep, evSobel, evOrb, evCrit, evBlur, evGate, evGrow2, evPair, evSobelGo})
             if (e) (void)hipEventDestroy(e);
         if (critStream) (void)hipStreamDestroy(critStream);
         if (crit2) (void)hipStreamDestroy(crit2);
@@ -172,6 +175,11 @@ struct LinePipeline {
             // of competing with the prep and the ORB pyramid
             const char* e5 = getenv("PLVI_SOBEL_WITH_GROW");
             sobelWithGrow = !e5 || atoi(e5) != 0;
+            // PLVI_SOBEL_GATE=k (batches from 1024 frames): the Sobel pyramid waits
+            // for ORB stage k instead (2: NMS, 3: SAT, 4: octree, 5: node best),
+            // so it does not take wave slots from the ORB chain while that chain
+            // runs beside region growing
+            if (const char* e7 = getenv("PLVI_SOBEL_GATE")) sobelGate = std::min(5, std::max(-1, atoi(e7)));
             if (prio) PLVI_CHECK(hipStreamCreateWithPriority(&critStream, hipStreamNonBlocking, greatest));
             // PLVI_GROW_SPLIT=1: octave 0 grows right after the prep, octave 1
             // after blur + FAST (batches from 1024 frames; +1 % in a 3-way
@@ -187,7 +195,7 @@ struct LinePipeline {
             // greatest-priority pool stays at two streams per handle
             PLVI_CHECK(hipStreamCreateWithFlags(&octStream, hipStreamNonBlocking));
         }
-        for (auto* e : {&evFork, &evPrep, &evSobel, &evOrb, &evCrit, &evBlur, &evGate, &evGrow2, &evPair})
+        for (auto* e : {&evFork, &evPrep, &evSobel, &evOrb, &evCrit, &evBlur, &evGate, &evGrow2, &evPair, &evSobelGo})
             PLVI_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
         fcap = p->nfeatures > 0 ? p->nfeatures : kKlCap;
         SCALE = (double)p->lsd_scale;  // LSDOptions::scale is float
@@ -637,9 +645,12 @@ struct LinePipeline {
         // from 1024 frames on) starves blur + FAST; a small batch is latency-bound
         // and starts region growing right after the prep
         const bool waitBlur = growAfterBlur && nf >= 1024;
+        const bool sobelLate = waitBlur && sobelGate >= 0;
         if (waitBlur) plvi_orb_internal_blur_event(orb, evBlur);
+        if (sobelLate) plvi_orb_internal_stage_event(orb, sobelGate, evSobelGo);
         int rc = plvi_orb_extract_batch(orb, d_frames, nf, frame_stride, row_stride, lap0, lap1, aux[0]);
         if (waitBlur) plvi_orb_internal_blur_event(orb, nullptr);
+        if (sobelLate) plvi_orb_internal_stage_event(orb, -1, nullptr);
         PLVI_CHECK(hipEventRecord(evOrb, aux[0]));
         // split: octave 0 (the long waves, 3 per SIMD at 3072 frames) grows
         // right after the prep and leaves room for the ORB pyramid and blur +
@@ -653,7 +664,7 @@ struct LinePipeline {
         if (waitBlur && !rc) PLVI_CHECK(hipStreamWaitEvent(gate, evBlur, 0));
         // evGate: everything the (last) region-growing launch waits for
         PLVI_CHECK(hipEventRecord(evGate, gate));
-        PLVI_CHECK(hipStreamWaitEvent(aux[1], sobelWithGrow ? evGate : auxStart, 0));
+        PLVI_CHECK(hipStreamWaitEvent(aux[1], sobelLate ? evSobelGo : sobelWithGrow ? evGate : auxStart, 0));
         if (!rc) rc = launch_sobel(d_frames, nf, frame_stride, row_stride, aux[1]);
         PLVI_CHECK(hipEventRecord(evSobel, aux[1]));
         if (split) {

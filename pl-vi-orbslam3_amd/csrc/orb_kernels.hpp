@@ -261,8 +261,16 @@ __global__ __launch_bounds__(64 * (kPyrFrames + 1)) void orb_pyramid_kernel(
 #ifndef PLVI_BF_SRING
 #define PLVI_BF_SRING 0
 #endif
+#ifndef PLVI_BF_PK
+#define PLVI_BF_PK 1  // candidates scored two per lane with packed 16-bit min / max (128 per flush)
+#endif
+constexpr int kBfFlush = PLVI_BF_PK ? 128 : 64;  // candidates scored per flush
+// ring rows 0..5 are mirrored after row kRingRows - 1, so the 7 rows around
+// any ring row are contiguous and a candidate's 17 taps are one base address
+// plus immediate offsets (no per-tap wrap arithmetic)
+constexpr int kRingMirror = PLVI_BF_PK ? 6 : 0;
 constexpr int kBfCols = (244 / kBfAlign) * kBfAlign, kBfRows = 128, kRingRows = PLVI_BF_LEAN ? 16 : 32, kRingW = 256,
-              kBfQCap = 320;
+              kBfQCap = kBfFlush - 1 + 256 + 1;  // a row adds <= 256 candidates to < kBfFlush queued
 
 __device__ __forceinline__ int lane_from_left(int v) {  // lane i <- lane i-1 (wave_shr:1)
     return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
@@ -328,6 +336,61 @@ __device__ __forceinline__ int fast_S_ring(const uint8_t (*rg)[kRingW], int y, i
     return max(A, -Bm);
 }
 
+// fast_S_ring for two pixels at once (a in the low, b in the high 16-bit
+// field of every value: v_pk_sub/min/max_i16).  Same arcs, regrouped: for an
+// even k the arcs starting at k and k+1 share inner_k = min(d[k+1..k+8]), and
+// max(min(d[k], in), min(in, d[k+9])) = min(in, max(d[k], d[k+9])); the eight
+// inner minima are built from pair then quad minima of odd-started runs
+// (d[j..j+1], d[j..j+3]), so each sense costs 47 packed ops for two pixels.
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ s16x2 fast_S_ring2(const uint8_t (*rg)[kRingW], int ya, int ca, int yb, int cb) {
+    const uint8_t* ra = &rg[(ya - 3) & (kRingRows - 1)][ca - 3];  // rows ya-3..ya+3 contiguous (mirror)
+    const uint8_t* rb = &rg[(yb - 3) & (kRingRows - 1)][cb - 3];
+#define RG2(dy, dx) \
+    (s16x2){(short)ra[((dy) + 3) * kRingW + (dx) + 3], (short)rb[((dy) + 3) * kRingW + (dx) + 3]}
+    const s16x2 v = RG2(0, 0);
+    s16x2 d[16];
+    d[0] = v - RG2(3, 0);
+    d[1] = v - RG2(3, 1);
+    d[2] = v - RG2(2, 2);
+    d[3] = v - RG2(1, 3);
+    d[4] = v - RG2(0, 3);
+    d[5] = v - RG2(-1, 3);
+    d[6] = v - RG2(-2, 2);
+    d[7] = v - RG2(-3, 1);
+    d[8] = v - RG2(-3, 0);
+    d[9] = v - RG2(-3, -1);
+    d[10] = v - RG2(-2, -2);
+    d[11] = v - RG2(-1, -3);
+    d[12] = v - RG2(0, -3);
+    d[13] = v - RG2(1, -3);
+    d[14] = v - RG2(2, -2);
+    d[15] = v - RG2(3, -1);
+#undef RG2
+    s16x2 pa[8], pb[8], qa[8], qb[8];  // index i <-> odd start j = 2i + 1
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int j = 2 * i + 1;
+        pa[i] = __builtin_elementwise_min(d[j], d[(j + 1) & 15]);
+        pb[i] = __builtin_elementwise_max(d[j], d[(j + 1) & 15]);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {  // runs d[j..j+3]
+        qa[i] = __builtin_elementwise_min(pa[i], pa[(i + 1) & 7]);
+        qb[i] = __builtin_elementwise_max(pb[i], pb[(i + 1) & 7]);
+    }
+    s16x2 A = (s16x2){-1000, -1000}, Bm = (s16x2){1000, 1000};
+#pragma unroll
+    for (int k = 0; k < 16; k += 2) {
+        const int i = k / 2;  // inner run d[k+1..k+8] = quads at k+1 and k+5
+        const s16x2 ia = __builtin_elementwise_min(qa[i], qa[(i + 2) & 7]);
+        const s16x2 ib = __builtin_elementwise_max(qb[i], qb[(i + 2) & 7]);
+        A = __builtin_elementwise_max(A, __builtin_elementwise_min(ia, __builtin_elementwise_max(d[k], d[(k + 9) & 15])));
+        Bm = __builtin_elementwise_min(Bm, __builtin_elementwise_max(ib, __builtin_elementwise_min(d[k], d[(k + 9) & 15])));
+    }
+    return __builtin_elementwise_max(A, -Bm);
+}
+
 __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __restrict__ lvs,
                                                            const OrbStripDev* __restrict__ strips,
                                                            const uint8_t* __restrict__ frames, size_t f_frame,
@@ -336,7 +399,7 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
                                                            int k0, int k1, int k2, int k3, int tmin, int nstrips,
                                                            int nf) {
     typedef typename std::conditional<PLVI_BF_LEAN != 0, unsigned short, unsigned>::type QT;
-    __shared__ __align__(16) uint8_t ring[kRingRows][kRingW];
+    __shared__ __align__(16) uint8_t ring[kRingRows + kRingMirror][kRingW];
     __shared__ QT q[kBfQCap];
 #if PLVI_BF_SRING
     // score rows of the last kRingRows output rows: candidates are scored into
@@ -380,30 +443,49 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
     int nq = 0;      // queued candidates (wave-uniform)
     int oldest = 0;  // row of the oldest queued candidate
     int ynew = 0;    // row of the newest queued candidate (queue rows are stored modulo 256)
-    auto flush = [&](int n, int ycur) {  // score the first n (<= 64) queued candidates (ycur: newest queued row)
+    auto flush = [&](int n, int ycur) {  // score the first n (<= kBfFlush) queued candidates (ycur: newest queued row)
         // one wave per block: wave-scope ordering only (no store drain).  The
         // candidate bytes below land after this wave's earlier zero stores of
         // the same pixels: a wavefront observes its own memory operations in
         // program order (wavefront-scope acquire/release needs no waits).
         wave_sync();
-        if (lane < n) {
-            const unsigned e = q[lane];
-            const int yy = ycur - (int)((((unsigned)ycur & 255u) - (e >> 8)) & 255u), rc = (int)(e & 255u);
-            const int Sv = fast_S_ring(ring, yy, rc);
+        auto put = [&](int yy, int rc, int Sv) {
 #if PLVI_BF_SRING
             sring[yy & (kRingRows - 1)][rc] = (uint8_t)(Sv >= T ? Sv - 1 : 0);
 #else
             Sp[(size_t)yy * bw + (sd.x0 - 4 + rc)] = (uint8_t)(Sv >= T ? Sv - 1 : 0);
 #endif
+        };
+        auto ent = [&](unsigned e, int& yy, int& rc) {
+            yy = ycur - (int)((((unsigned)ycur & 255u) - (e >> 8)) & 255u);
+            rc = (int)(e & 255u);
+        };
+#if PLVI_BF_PK
+        if (lane < n) {
+            int ya, ca, yb, cb;
+            ent(q[lane], ya, ca);
+            const bool hasb = lane + 64 < n;
+            ent(q[hasb ? lane + 64 : lane], yb, cb);
+            const s16x2 sv2 = fast_S_ring2(ring, ya, ca, yb, cb);
+            put(ya, ca, (int)sv2.x);
+            if (hasb) put(yb, cb, (int)sv2.y);
         }
+#else
+        if (lane < n) {
+            int yy, rc;
+            ent(q[lane], yy, rc);
+            put(yy, rc, fast_S_ring(ring, yy, rc));
+        }
+#endif
         wave_sync();
         const int rest = nq - n;
-        QT t[(kBfQCap - 64) / 64];
+        constexpr int kMove = (kBfQCap - kBfFlush + 63) / 64;  // rest < kBfQCap - kBfFlush + 1 entries
+        QT t[kMove];
 #pragma unroll
-        for (int k = 0; k < (kBfQCap - 64) / 64; ++k) t[k] = lane + 64 * k < rest ? q[n + lane + 64 * k] : (QT)0;
+        for (int k = 0; k < kMove; ++k) t[k] = lane + 64 * k < rest ? q[n + lane + 64 * k] : (QT)0;
         wave_sync();
 #pragma unroll
-        for (int k = 0; k < (kBfQCap - 64) / 64; ++k)
+        for (int k = 0; k < kMove; ++k)
             if (lane + 64 * k < rest) q[lane + 64 * k] = t[k];
         nq = rest;
         wave_sync();
@@ -446,8 +528,11 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
         // of the ring; a queued row yy needs rows yy-3..yy+3
         if (nq > 0 && oldest - 3 < rb - (kRingRows - 8)) flush(nq, ynew);
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-            *reinterpret_cast<uint32_t*>(&ring[(rb + k) & (kRingRows - 1)][4 * lane]) = pv[k];
+        for (int k = 0; k < 8; ++k) {
+            const int rr = (rb + k) & (kRingRows - 1);
+            *reinterpret_cast<uint32_t*>(&ring[rr][4 * lane]) = pv[k];
+            if (rr < kRingMirror) *reinterpret_cast<uint32_t*>(&ring[rr + kRingRows][4 * lane]) = pv[k];
+        }
         // next batch in flight while this one is filtered
         if (rb + 8 < y1 + 3) load_rows(rb + 8, pv);
 #pragma unroll 1
@@ -497,16 +582,15 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
             for (int e = 0; e < 2; ++e) {
                 const u16x2 c = as_u16x2(ce[e]);
                 const u16x2 q0 = as_u16x2(p0[e]), q4 = as_u16x2(p4[e]), q8 = as_u16x2(p8[e]), q12 = as_u16x2(p12[e]);
-                const u16x2 b0 = __builtin_elementwise_sub_sat(c, q0), b4 = __builtin_elementwise_sub_sat(c, q4);
-                const u16x2 b8 = __builtin_elementwise_sub_sat(c, q8), b12 = __builtin_elementwise_sub_sat(c, q12);
-                const u16x2 d0 = __builtin_elementwise_sub_sat(q0, c), d4 = __builtin_elementwise_sub_sat(q4, c);
-                const u16x2 d8 = __builtin_elementwise_sub_sat(q8, c), d12 = __builtin_elementwise_sub_sat(q12, c);
-                const u16x2 mb = __builtin_elementwise_max(
-                    __builtin_elementwise_max(__builtin_elementwise_min(b0, b4), __builtin_elementwise_min(b4, b8)),
-                    __builtin_elementwise_max(__builtin_elementwise_min(b8, b12), __builtin_elementwise_min(b12, b0)));
-                const u16x2 md = __builtin_elementwise_max(
-                    __builtin_elementwise_max(__builtin_elementwise_min(d0, d4), __builtin_elementwise_min(d4, d8)),
-                    __builtin_elementwise_max(__builtin_elementwise_min(d8, d12), __builtin_elementwise_min(d12, d0)));
+                // the 4 compass points form a cycle whose adjacent pairs are {0,8} x
+                // {4,12}: max over pairs of min(x, y) = min(max(x0, x8), max(x4, x12)),
+                // and max(c -sat q0, c -sat q8) = c -sat min(q0, q8)
+                const u16x2 n08 = __builtin_elementwise_min(q0, q8), n412 = __builtin_elementwise_min(q4, q12);
+                const u16x2 x08 = __builtin_elementwise_max(q0, q8), x412 = __builtin_elementwise_max(q4, q12);
+                const u16x2 mb = __builtin_elementwise_min(__builtin_elementwise_sub_sat(c, n08),
+                                                           __builtin_elementwise_sub_sat(c, n412));
+                const u16x2 md = __builtin_elementwise_min(__builtin_elementwise_sub_sat(x08, c),
+                                                           __builtin_elementwise_sub_sat(x412, c));
                 const uint32_t m = as_u32(__builtin_elementwise_max(mb, md));
                 candm |= ((m & 0xffffu) >= (unsigned)T ? 1u : 0u) << e;
                 candm |= ((m >> 16) >= (unsigned)T ? 4u : 0u) << e;
@@ -543,10 +627,10 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
             }
             if (nq0 == 0 && nq > 0) oldest = y;
             if (nq > nq0) ynew = y;
-            while (nq >= 64) flush(64, ynew);
+            while (nq >= kBfFlush) flush(kBfFlush, ynew);
         }
     }
-    while (nq > 0) flush(min(nq, 64), ynew);
+    while (nq > 0) flush(min(nq, kBfFlush), ynew);
 #if PLVI_BF_SRING
     wave_sync();
     for (int yy = max(y0, y1 - kRingRows); yy < y1; ++yy) store_score_row(yy);

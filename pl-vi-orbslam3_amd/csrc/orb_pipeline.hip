@@ -79,6 +79,8 @@ struct OrbPipeline {
     int kn = 0;
     hipEvent_t evAfterBlur = nullptr;  // frame schedule hook (plvi_orb_internal_blur_event)
     int gateStage = 1;  // PLVI_GROW_GATE: the hook fires after the pyramid (0), blur + FAST (1), NMS (2) or the SAT (3)
+    hipEvent_t evStage = nullptr;  // second hook (plvi_orb_internal_stage_event): fires after stage `evStageAt`
+    int evStageAt = -1;
     std::vector<hipEvent_t> kev;
     int ktiming(int on) {
         if (on && kev.empty()) {
@@ -328,13 +330,18 @@ struct OrbPipeline {
         uint8_t* Sc = score.as<uint8_t>();
         uint8_t* Cd = cand.as<uint8_t>();
         mark(0, st);
+        auto hook = [&](int k, hipStream_t s_) {
+            if (evAfterBlur && gateStage == k) PLVI_CHECK(hipEventRecord(evAfterBlur, s_));
+            if (evStage && evStageAt == k) PLVI_CHECK(hipEventRecord(evStage, s_));
+            return PLVI_OK;
+        };
         // K1a: the pyramid (ComputePyramid, chained resize: level l from l-1)
         // of every frame in one streaming launch, one wave per frame
         if (L > 1)
             hipLaunchKernelGGL(orb_pyramid_kernel, dim3((nf + kPyrFrames - 1) / kPyrFrames), dim3(64 * (kPyrFrames + 1)),
                                pyrSmem, st, d_lv.as<OrbLevelDev>(), L, d_frames, frame_stride, row_stride, nf, P,
                                (const uint32_t*)d_xtab.as<uint32_t>(), xtabN, pyrFrameLds, resizeGeneric);
-        if (evAfterBlur && gateStage == 0) PLVI_CHECK(hipEventRecord(evAfterBlur, st));
+        if (const int hrc = hook(0, st)) return hrc;
         // K1b: blur + FAST score of every level (level 0 also copies the frame into its plane)
         const bool kt = ktime && kn < kKRing;
         if (kt) PLVI_CHECK(hipEventRecord(kev[2 * kn], st));
@@ -345,7 +352,7 @@ struct OrbPipeline {
             PLVI_CHECK(hipEventRecord(kev[2 * kn + 1], st));
             ++kn;
         }
-        if (evAfterBlur && gateStage == 1) PLVI_CHECK(hipEventRecord(evAfterBlur, st));
+        if (const int hrc = hook(1, st)) return hrc;
         mark(1, st);
         // K2 cell NMS -> candidate map (zeroed first: only detection windows are written)
         PLVI_CHECK(hipMemsetAsync(Cd, 0, candBytesTotal, st));
@@ -353,7 +360,7 @@ struct OrbPipeline {
                            dim3(64), 0, st, d_cells.as<OrbCellDev>(), (int)cells.size(), d_lv.as<OrbLevelDev>(),
                            (const uint8_t*)Sc, Cd, t1, t2);
         mark(2, st);
-        if (evAfterBlur && gateStage == 2) PLVI_CHECK(hipEventRecord(evAfterBlur, st));
+        if (const int hrc = hook(2, st)) return hrc;
         // K3 SAT
         int maxRh = 0, maxStrips = 0;
         for (auto& d : lv) { maxRh = std::max(maxRh, d.rh); maxStrips = std::max(maxStrips, d.satStrips); }
@@ -366,7 +373,7 @@ struct OrbPipeline {
         hipLaunchKernelGGL(orb_sat_carry_kernel, dim3((maxRh + 1 + 255) / 256, L, nf), dim3(256), 0, st,
                            d_lv.as<OrbLevelDev>(), carry.as<int>());
         mark(3, st);
-        if (evAfterBlur && gateStage == 3) PLVI_CHECK(hipEventRecord(evAfterBlur, st));
+        if (const int hrc = hook(3, st)) return hrc;
         // K4 octree
         const size_t smem = (size_t)nodeCapMax * (6 * 4 + 14 * 2 + 1) + 16;
         hipLaunchKernelGGL(orb_octree_kernel, dim3(L, nf), dim3(64), smem, st, d_lv.as<OrbLevelDev>(),
@@ -374,11 +381,13 @@ struct OrbPipeline {
                            rects.as<short4>(), rectCnt.as<int>(), nodeCapMax, L,
                            err.as<int>());
         mark(4, st);
+        if (const int hrc = hook(4, st)) return hrc;
         // K5 best per node
         hipLaunchKernelGGL(orb_node_best_kernel, dim3(nodeCapMax, L, nf), dim3(64), 0, st, d_lv.as<OrbLevelDev>(),
                            (const uint8_t*)Cd, (const short4*)rects.as<short4>(), (const int*)rectCnt.as<int>(),
                            nodeCapMax, L, lvkp.as<float4>(), kpCapFrame);
         mark(5, st);
+        if (const int hrc = hook(5, st)) return hrc;
         // K6 orientation + rBRIEF
         hipLaunchKernelGGL(orb_describe_kernel, dim3((kpCapFrame + 15) / 16, nf), dim3(256), 0, st,
                            d_lv.as<OrbLevelDev>(), L, (const uint8_t*)P, (const uint8_t*)Bl,
@@ -569,6 +578,13 @@ extern "C" int plvi_orb_profile_read(plvi_orb_extractor* h, float* stage_ms, int
 
 // Internal (frame schedule): record `ev` on the batch stream right after the
 // blur + FAST launch of every later batch (nullptr: off).
+extern "C" int plvi_orb_internal_stage_event(plvi_orb_extractor* h, int stage, hipEvent_t ev) {
+    if (!h) return PLVI_E_BADARG;
+    h->p().evStage = ev;
+    h->p().evStageAt = stage;
+    return PLVI_OK;
+}
+
 extern "C" int plvi_orb_internal_blur_event(plvi_orb_extractor* h, hipEvent_t ev) {
     if (!h) return PLVI_E_BADARG;
     h->p().evAfterBlur = ev;
