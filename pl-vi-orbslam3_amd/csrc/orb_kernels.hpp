@@ -272,11 +272,16 @@ constexpr int kRingMirror = PLVI_BF_PK ? 6 : 0;
 constexpr int kBfCols = (244 / kBfAlign) * kBfAlign, kBfRows = 128, kRingRows = PLVI_BF_LEAN ? 16 : 32, kRingW = 256,
               kBfQCap = kBfFlush - 1 + 256 + 1;  // a row adds <= 256 candidates to < kBfFlush queued
 
-__device__ __forceinline__ int lane_from_left(int v) {  // lane i <- lane i-1 (wave_shr:1)
-    return __builtin_amdgcn_update_dpp(0, v, 0x138, 0xf, 0xf, false);
+// bound_ctrl: the lane past the wave's edge reads 0 without an `old` operand
+// (update_dpp(0, ...) costs a v_mov of the zero per shift)
+__device__ __forceinline__ int lane_from_left(int v) {  // lane i <- lane i-1 (wave_shr:1), lane 0 <- 0
+    return __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, true);
 }
-__device__ __forceinline__ int lane_from_right(int v) {  // lane i <- lane i+1 (wave_shl:1)
-    return __builtin_amdgcn_update_dpp(0, v, 0x130, 0xf, 0xf, false);
+__device__ __forceinline__ int lane_from_right(int v) {  // lane i <- lane i+1 (wave_shl:1), lane 63 <- 0
+    return __builtin_amdgcn_mov_dpp(v, 0x130, 0xf, 0xf, true);
+}
+__device__ __forceinline__ int orb_mbcnt(unsigned long long m) {  // set bits of m below this lane
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
 __device__ __forceinline__ uint32_t ld_u32(const uint8_t* p) {  // any alignment (gfx950 unaligned access)
     uint32_t v;
@@ -619,12 +624,30 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
                 }
             }
             const int nq0 = nq;
+#if PLVI_BF_PK
+            {
+                // lane-major queue order: the lane's candidate count (0..4) as three
+                // ballot bit planes gives every lane its exclusive prefix with mbcnt
+                (void)cand;
+                const unsigned cnt = (unsigned)__popc(candm);
+                const unsigned long long B0 = __ballot(cnt & 1u), B1 = __ballot(cnt & 2u), B2 = __ballot(cnt & 4u);
+                if ((B0 | B1 | B2) != 0ull) {
+                    const int pre = nq + orb_mbcnt(B0) + 2 * orb_mbcnt(B1) + 4 * orb_mbcnt(B2);
+                    const unsigned base = ((unsigned)y & 255u) << 8 | (unsigned)(4 * lane);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        if ((candm >> j) & 1u) q[pre + __popc(candm & ((1u << j) - 1u))] = (QT)(base | (unsigned)j);
+                    nq += __popcll(B0) + 2 * __popcll(B1) + 4 * __popcll(B2);
+                }
+            }
+#else
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const unsigned long long m = __ballot(cand[j]);
                 if (cand[j]) q[nq + __popcll(m & ((1ull << lane) - 1ull))] = (QT)(((unsigned)y & 255u) << 8 | (unsigned)(4 * lane + j));
                 nq += __popcll(m);
             }
+#endif
             if (nq0 == 0 && nq > 0) oldest = y;
             if (nq > nq0) ynew = y;
             while (nq >= kBfFlush) flush(kBfFlush, ynew);
