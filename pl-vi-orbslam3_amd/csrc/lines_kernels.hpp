@@ -1342,6 +1342,9 @@ __global__ __launch_bounds__(64) void lbd_sobel1_kernel(const uint8_t* __restric
 // normalises.  Gaussian coefficient tables come from the host (double exp,
 // cast to float at use, :1189/:1203).
 // ---------------------------------------------------------------------------
+#ifndef PLVI_LBD_XPOSE
+#define PLVI_LBD_XPOSE 1  // support-region gathers transposed through LDS (8 rows x 8 samples per instruction)
+#endif
 __constant__ float c_gaussG[63];
 __constant__ float c_gaussL[21];
 __constant__ unsigned char c_comb[64];
@@ -1371,6 +1374,69 @@ __global__ __launch_bounds__(64) void lbd_describe_kernel(const LineOctDev* __re
     const float dO0 = -dL1, dO1 = dL0;
     const int h = threadIdx.x;
     float pL = 0, nL = 0, pO = 0, nO = 0;
+#if PLVI_LBD_XPOSE
+    // The coordinates are walked per row lane (reference order), but the
+    // gathers are transposed through LDS: one gather instruction then covers
+    // 8 rows x 8 consecutive samples instead of 64 rows at one sample, so its
+    // lanes share cache lines (samples along a row are 1 px apart) and the
+    // vector-memory path is not one cache line per lane
+    // one array: each (row, sample) slot's index is read and its gathered
+    // value written back by the same lane, and row lane h writes / reads only
+    // its own row
+    __shared__ int sidx[64][9];
+    auto& sg = sidx;
+    {
+        float sX = -dL0 * halfWidth + dL1 * halfHeight + mX;
+        float sY = -dL1 * halfWidth - dL0 * halfHeight + mY;
+        for (int k = 0; k < h; ++k) {
+            sX -= dL1;
+            sY += dL0;
+        }
+        const int* pgi = reinterpret_cast<const int*>(pg);
+        const int kk = h & 7, rr = h >> 3;
+        for (int w0 = 0; w0 < lengthOfLSP; w0 += 8) {  // lengthOfLSP is wave-uniform
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                short t = (short)__builtin_roundf(sX);
+                const short xc = (t < 0) ? 0 : (t > imageWidth) ? imageWidth : t;
+                t = (short)__builtin_roundf(sY);
+                const short yc = (t < 0) ? 0 : (t > imageHeight) ? imageHeight : t;
+                sidx[h][k] = yc * realWidth + xc;
+                sX += dL0;
+                sY += dL1;
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            int gv[8];
+            const bool okk = w0 + kk < lengthOfLSP;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int r = 8 * i + rr;
+                gv[i] = (r < 63 && okk) ? pgi[sidx[r][kk]] : 0;
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) sg[8 * i + rr][kk] = gv[i];
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            if (h < 63) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    if (w0 + k >= lengthOfLSP) break;
+                    const short2 g = __builtin_bit_cast(short2, sg[h][k]);
+                    const short dx = g.x, dy = g.y;
+                    const float gDL = dx * dL0 + dy * dL1;
+                    const float gDO = dx * dO0 + dy * dO1;
+                    if (gDL > 0) pL += gDL;
+                    else nL -= gDL;
+                    if (gDO > 0) pO += gDO;
+                    else nO -= gDO;
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        }
+    }
+#else
     if (h < 63) {
         float sX0 = -dL0 * halfWidth + dL1 * halfHeight + mX;
         float sY0 = -dL1 * halfWidth - dL0 * halfHeight + mY;
@@ -1410,6 +1476,7 @@ __global__ __launch_bounds__(64) void lbd_describe_kernel(const LineOctDev* __re
             }
         }
     }
+#endif
     // row sums scaled by gaussCoefG_ (:1189-1197), per row lane
     if (h < 63) {
         const float c = c_gaussG[h];
