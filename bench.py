@@ -1027,6 +1027,18 @@ def extra_lines(args, torch, plvi, synth, lib, stream, W, H, seed0, orb, lx, ext
         "orb_median_ms": float(np.median(lo_)) * 1e3, "lines_median_ms": float(np.median(ll_)) * 1e3,
         "frames": len(lat), "how": "plvi_orb_extract || plvi_lines_extract on two host threads (Frame.cc:558-561), "
                                    "host frame in, host keypoints/keylines/descriptors out"}
+    # the same measurement in a child process that holds only the two
+    # extractors (a SLAM process's drop-in situation; this process holds ~20
+    # more handles whose streams share the runtime's hardware queues)
+    try:
+        cp = subprocess.run([sys.executable, str(ROOT / "tools" / "latency_pair.py"), "--json"], capture_output=True,
+                            text=True, timeout=180)
+        if cp.returncode == 0:
+            fp = json.loads(cp.stdout.strip().splitlines()[-1])
+            fp["how"] = "tools/latency_pair.py in a child process holding only the ORB and line extractors"
+            out["single_frame_latency"]["drop_in_process"] = fp
+    except (subprocess.SubprocessError, ValueError, IndexError) as e:
+        out["single_frame_latency"]["drop_in_process"] = {"error": str(e)[:200]}
     del so, sl
     # (3) pinned-H2D overlapped step (the main handles, two device buffers)
     host = torch.empty((B, H, W), dtype=torch.uint8, pin_memory=True)
