@@ -202,6 +202,41 @@ def cpu_baseline(frames, runs=5, par_s=5.0):
     return res
 
 
+def cgroup_cpu_quota():
+    """CPUs granted by the cgroup CPU quota (ceil(quota / period)), or None
+    when unlimited / unreadable.  cgroup v2: the tightest `cpu.max` on the
+    path from this process's cgroup (/proc/self/cgroup) up to the root;
+    cgroup v1: the cfs quota files."""
+    import math
+    best = None
+    try:
+        rel = ""
+        for line in pathlib.Path("/proc/self/cgroup").read_text().splitlines():
+            if line.startswith("0::"):
+                rel = line[3:].strip().strip("/")
+        d = pathlib.Path("/sys/fs/cgroup") / rel
+        while True:
+            f = d / "cpu.max"
+            if f.exists():
+                q, per = f.read_text().split()[:2]
+                if q != "max":
+                    n = max(1, math.ceil(int(q) / int(per)))
+                    best = n if best is None else min(best, n)
+            if d == pathlib.Path("/sys/fs/cgroup") or d == d.parent:
+                break
+            d = d.parent
+    except (OSError, ValueError):
+        pass
+    if best is not None:
+        return best
+    try:
+        q = int(pathlib.Path("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read_text())
+        per = int(pathlib.Path("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read_text())
+        return None if q <= 0 else max(1, math.ceil(q / per))
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline_child(frames_npy, out_json, runs, par_s):
     """The CPU-baseline measurement proper (child process, no GPU): per stage
     and end to end on the timed batch's frames, single thread pinned to one
@@ -243,19 +278,33 @@ def cpu_baseline_child(frames_npy, out_json, runs, par_s):
             tot.append(time.perf_counter() - t_run)
             for k in stages:
                 per[k].append(acc[k] * 1e3 / len(frames))
-        # BASELINE C0: 752x480, 1000 ORB features, 100 lines, extraction only
-        c0 = synth.device_sequence(16, 752, 480, seed=7).numpy()
-        c0t = []
-        for _ in range(3):
-            t0 = time.perf_counter()
-            for img in c0:
-                ol.orb_extract(img)
-                ol.line_extract(img, nfeatures=100)
-            c0t.append(time.perf_counter() - t0)
+        # BASELINE C0 as named (640x480, 1000 ORB features, 100 lines,
+        # extraction only), and the EuRoC frame shape (752x480) beside it
+        c0s = {}
+        for (cw, chh) in ((640, 480), (752, 480)):
+            c0 = synth.device_sequence(16, cw, chh, seed=7).numpy()
+            c0t = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                for img in c0:
+                    ol.orb_extract(img)
+                    ol.line_extract(img, nfeatures=100)
+                c0t.append(time.perf_counter() - t0)
+            c0s[(cw, chh)] = (len(c0), float(np.median(c0t)))
     finally:
         os.sched_setaffinity(0, set(cpus))
     med = float(np.median(tot))
-    nthr = len(cpus)
+    quota = cgroup_cpu_quota()
+    # frame-parallel leg: one thread per CPU the job may actually run on --
+    # the affinity set capped by the cgroup CPU quota (a GPU job on the box
+    # sees every CPU of the host but is granted far fewer).  Without a
+    # readable quota the job's declared CPU share (OMP_NUM_THREADS, which the
+    # GPU box sets to its per-GPU share) caps it instead.
+    share = quota
+    share_src = "cgroup cpu.max"
+    if not share and os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        share, share_src = int(os.environ["OMP_NUM_THREADS"]), "OMP_NUM_THREADS (no cgroup quota)"
+    nthr = max(1, min(len(cpus), share if share else len(cpus)))
     count = [0] * nthr
     stop = time.perf_counter() + par_s
 
@@ -285,14 +334,22 @@ def cpu_baseline_child(frames_npy, out_json, runs, par_s):
                      f"pinned to core {cpus[0]} (sched_setaffinity): ORB extract + LSD/LBD extract + ORB kNN-2 + "
                      f"LineMatcher::match vs previous frame, CPU restatement (oracle/)",
            "stage_ms_per_frame": {k: round(float(np.median(v)), 3) for k, v in per.items()},
-           "parallel": {"threads": nthr, "value": round(par_fps, 2), "unit": "frames/s",
-                        "sample": f"{sum(count)} frames in {par_s:.0f}s, one frame-parallel thread per CPU in "
-                                  f"this process's affinity set ({nthr})"},
-           "c0_752x480": {"value": round(len(c0) / float(np.median(c0t)), 3), "unit": "frames/s", "cores": 1,
-                          "sample": f"BASELINE C0 shape: {len(c0)} synthetic 752x480 EuRoC-shaped frames, "
+           "parallel": {"threads": nthr, "cores": nthr, "value": round(par_fps, 2), "unit": "frames/s",
+                        "sample": f"{sum(count)} frames in {par_s:.0f}s, one frame-parallel thread per CPU the "
+                                  f"job may use: min(affinity set {len(cpus)}, {share_src} "
+                                  f"{share if share else 'none'}) = {nthr}"},
+           "c0_640x480": {"value": round(c0s[(640, 480)][0] / c0s[(640, 480)][1], 3), "unit": "frames/s",
+                          "cores": 1,
+                          "sample": f"BASELINE configs[0] as named: {c0s[(640, 480)][0]} synthetic 640x480 frames, "
                                     "ORBextractor 1000 + Lineextractor 100 lines, extraction only, median of 3 "
                                     "single-thread runs"},
-           "host_cpu": _cpu_model(), "host_nproc": os.cpu_count(), "affinity_cpus": len(cpus)}
+           "c0_752x480": {"value": round(c0s[(752, 480)][0] / c0s[(752, 480)][1], 3), "unit": "frames/s",
+                          "cores": 1,
+                          "sample": f"EuRoC frame shape: {c0s[(752, 480)][0]} synthetic 752x480 frames, "
+                                    "ORBextractor 1000 + Lineextractor 100 lines, extraction only, median of 3 "
+                                    "single-thread runs"},
+           "host_cpu": _cpu_model(), "host_nproc": os.cpu_count(), "affinity_cpus": len(cpus),
+           "cgroup_cpu_quota": quota}
     pathlib.Path(out_json).write_text(json.dumps(res))
     return 0
 
@@ -966,9 +1023,11 @@ def extra_lines(args, torch, plvi, synth, lib, stream, W, H, seed0, orb, lx, ext
     v_api = timed_steps(step64k)
     # the same step replayed from HIP graphs, one capture per slot; the graph
     # holds the step on the slot's one stream (ORB extract, line extract,
-    # matches: the multi-stream frame schedule does not survive
-    # hipStreamEndCapture on this ROCm, a segfault inside the runtime), the
-    # 16 slots provide the concurrency
+    # matches).  This process imports torch, so the library runs on
+    # PyTorch's bundled HIP 7.0 runtime, which crashes capturing the
+    # multi-stream frame schedule's fork/join; plvi_frame_extract_batch
+    # refuses capture there (PLVI_E_CAPTURE), while ROCm 7.2's runtime
+    # captures it.  The 16 slots provide the concurrency.
     def step64g(q, sq):
         q.o.extract_batch(q.f, b64, W * H, W, (0, 0), stream=sq)
         q.l.extract_batch(q.f, b64, W * H, W, stream=sq)

@@ -403,7 +403,7 @@ struct LinePipeline {
                 const size_t tasks = (size_t)mwMaxFrames * nOct;
                 mwOwnTask = (size_t)kMwWaves * gbitsFrame;
                 if (mwOwn.alloc(sizeof(unsigned) * mwOwnTask * tasks) ||
-                    mwSlot.alloc(sizeof(unsigned) * (size_t)kMwMaxSlots * kMwSlotSpill * tasks) ||
+                    mwSlot.alloc(sizeof(unsigned) * (size_t)mwSlots * kMwSlotSpill * tasks) ||
                     mwGrow.alloc(sizeof(unsigned) * (size_t)kMwWaves * kMwGSpill * tasks))
                     return PLVI_E_HIP;
                 PLVI_CHECK(hipMemset(mwOwn.p, 0, mwOwn.bytes));  // kept zero by every launch

@@ -124,7 +124,29 @@ struct MwEnv {
     double prec;
 };
 
-__device__ __forceinline__ unsigned mw_word(const lds_u32* B, int wpr, int x, int y) { return B[y * wpr + (x >> 5)]; }
+// LDS hand-offs between the waves of the workgroup stay inside the HIP
+// memory model: a wave publishes data (slot records, dispatch-log entries,
+// the walk position) with a workgroup-scope RELEASE store of a flag and the
+// consumer reads the flag with an ACQUIRE load; locks are taken with an
+// acquire compare-and-swap and released with a release store.  Locations
+// several waves update concurrently (the C / H bitmaps, slot states scanned
+// as hints) are only accessed atomically -- relaxed where a later acquire or
+// a lock re-checks the value.  On gfx950 (no threadgroup split) a
+// workgroup-scope release or acquire on LDS costs an s_waitcnt lgkmcnt(0).
+// PLVI_MW_RELAXED=1 builds the r03 hand-offs (relaxed atomics + compiler
+// fences, relying on in-order DS execution) for A/B measurement only.
+#ifndef PLVI_MW_RELAXED
+#define PLVI_MW_RELAXED 0
+#endif
+__device__ __forceinline__ unsigned mw_peek(const lds_u32* p) {
+    return __hip_atomic_load(const_cast<lds_u32*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ int mw_peek(const lds_i32* p) {
+    return __hip_atomic_load(const_cast<lds_i32*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ unsigned mw_word(const lds_u32* B, int wpr, int x, int y) {
+    return mw_peek(B + y * wpr + (x >> 5));
+}
 __device__ __forceinline__ bool mw_bit(const lds_u32* B, int wpr, int x, int y) {
     return (mw_word(B, wpr, x, y) >> (x & 31)) & 1u;
 }
@@ -156,22 +178,33 @@ __device__ __forceinline__ void mw_wave_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-// LDS synchronisation: the LDS unit executes one wave's DS instructions in
-// issue order, so a flag written after data is seen by another wave only
-// after that data; compiler fences keep the program order.  (Workgroup-scope
-// acquire / release would also wait for this wave's outstanding global
-// stores, which nothing here needs: global spills are drained when written.)
+#if PLVI_MW_RELAXED
 __device__ __forceinline__ void mw_cfence() { __atomic_signal_fence(__ATOMIC_SEQ_CST); }
+#define PLVI_MW_ACQ __ATOMIC_RELAXED
+#define PLVI_MW_REL __ATOMIC_RELAXED
+#else
+__device__ __forceinline__ void mw_cfence() {}
+#define PLVI_MW_ACQ __ATOMIC_ACQUIRE
+#define PLVI_MW_REL __ATOMIC_RELEASE
+#endif
+// acquire load of a flag (pairs with mw_lds_store)
 __device__ __forceinline__ int mw_lds_load(lds_i32* p) {
     mw_cfence();
-    const int v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const int v = __hip_atomic_load(p, PLVI_MW_ACQ, __HIP_MEMORY_SCOPE_WORKGROUP);
     mw_cfence();
     return v;
 }
+// release store of a flag: everything this wave wrote before it (after a
+// mw_wave_sync when other lanes wrote) is visible to an acquiring wave
 __device__ __forceinline__ void mw_lds_store(lds_i32* p, int v) {
     mw_cfence();
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(p, v, PLVI_MW_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
     mw_cfence();
+}
+// compare-and-swap of a slot state / lock word: acquire on success
+__device__ __forceinline__ bool mw_lds_cas(lds_i32* p, int expected, int desired) {
+    return __hip_atomic_compare_exchange_strong(p, &expected, desired, PLVI_MW_ACQ, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void mw_stat(lds_ctl* c, int i, int v) {
     __hip_atomic_fetch_add(&c->stat[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -180,11 +213,7 @@ __device__ __forceinline__ void mw_stat(lds_ctl* c, int i, int v) {
 __device__ __forceinline__ bool mw_try_lock(lds_i32* l, int lane) {
     int got = 0;
     mw_cfence();
-    if (lane == 0) {
-        int e = 0;
-        got = __hip_atomic_compare_exchange_strong(l, &e, 1, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_WORKGROUP) ? 1 : 0;
-    }
+    if (lane == 0) got = mw_lds_cas(l, 0, 1) ? 1 : 0;
     got = __builtin_amdgcn_readfirstlane(got);
     mw_cfence();
     return got != 0;
@@ -376,14 +405,14 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
         // next unresolved pixel >= head: first zero bit of C
         int w = head >> 5;
         if (w >= nwords) break;
-        unsigned cw = E.C[w], tw = E.T[w];
+        unsigned cw = mw_peek(E.C + w), tw = E.T[w];  // T is static after the set-up
         unsigned m = ~cw & (~0u << (head & 31));
         if (!m) {
             // wave-parallel scan of the following words
             int found = -1;
             for (int w0 = w + 1; w0 < nwords && found < 0; w0 += 64) {
                 const int ww = w0 + lane;
-                const bool nz = ww < nwords && ~E.C[ww] != 0u;
+                const bool nz = ww < nwords && ~mw_peek(E.C + ww) != 0u;
                 const unsigned long long b = __ballot(nz);
                 if (b) found = w0 + __ffsll((long long)b) - 1;
             }
@@ -392,7 +421,7 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
                 break;
             }
             w = found;
-            cw = E.C[w];
+            cw = mw_peek(E.C + w);
             tw = E.T[w];
             m = ~cw;
         }
@@ -419,13 +448,9 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
             fromLog = true;
         } else if (kMwLate > 0) {
             // a second-chance region (late log, unordered: lanes compare)
-            mw_cfence();
-            const bool hit = lane < kMwLate &&
-                             __hip_atomic_load(&ctl->late_seed[lane < kMwLate ? lane : 0], __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP) == q;
+            const bool hit = lane < kMwLate && mw_lds_load(&ctl->late_seed[lane < kMwLate ? lane : 0]) == q;
             const unsigned long long hb = __ballot(hit);
             if (hb) si = ctl->late_slot[__ffsll((long long)hb) - 1];
-            mw_cfence();
         }
         lds_slot* S = si >= 0 ? mw_slot(pool, si) : nullptr;
         int sst = si >= 0 ? mw_lds_load(&S->state) : kMwFree;
@@ -433,11 +458,7 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
             // claim it against a grower's revalidation
             int got = 0;
             mw_cfence();
-            if (lane == 0) {
-                int e = kMwDone;
-                got = __hip_atomic_compare_exchange_strong(&S->state, &e, kMwWalking, __ATOMIC_RELAXED,
-                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ? 1 : 0;
-            }
+            if (lane == 0) got = mw_lds_cas(&S->state, kMwDone, kMwWalking) ? 1 : 0;
             got = __builtin_amdgcn_readfirstlane(got);
             mw_cfence();
             if (!got) sst = kMwGrowing;
@@ -545,12 +566,12 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
         }
         head = q + 1;
         if (lane == 0) {
-            ctl->wptr = wp;  // frees log entries for the dispatchers as the walk goes
+            mw_lds_store(&ctl->wptr, wp);  // frees log entries for the dispatchers as the walk goes
             mw_lds_store(&ctl->head, head);
         }
     }
     if (lane == 0) {
-        ctl->wptr = wp;
+        mw_lds_store(&ctl->wptr, wp);
         mw_lds_store(&ctl->head, head);
         if ((head >> 5) >= nwords) mw_lds_store(&ctl->finished, 1);
     }
@@ -567,7 +588,7 @@ __device__ __forceinline__ int mw_dispatch(const MwEnv& E, lds_u8* pool, int nsl
                                            int lane) {
     lds_ctl* ctl = E.ctl;
     const int nwords = E.sh * E.wpr;
-    const int dn = ctl->dlog_n;
+    const int dn = mw_peek(&ctl->dlog_n);  // written under dlock only (held)
     if (dn - mw_lds_load(&ctl->wptr) >= kMwLog - 1) return -1;  // log full: the walk is far behind
     const int head = mw_lds_load(&ctl->head);
     // a free slot (lanes scan the pool)
@@ -577,7 +598,7 @@ __device__ __forceinline__ int mw_dispatch(const MwEnv& E, lds_u8* pool, int nsl
         bool ok = false;
         if (si < nslots) {
             lds_slot* S = mw_slot(pool, si);
-            const int st = S->state;
+            const int st = mw_lds_load(&S->state);
             ok = st == kMwFree || (st == kMwDone && S->seed < head);
         }
         const unsigned long long b = __ballot(ok);
@@ -587,12 +608,12 @@ __device__ __forceinline__ int mw_dispatch(const MwEnv& E, lds_u8* pool, int nsl
     int cur = max(ctl->cursor, head);
     int w = cur >> 5;
     if (w >= nwords) return -1;
-    unsigned m = ~(E.C[w] | E.T[w] | E.H[w]) & (~0u << (cur & 31));
+    unsigned m = ~(mw_peek(E.C + w) | E.T[w] | mw_peek(E.H + w)) & (~0u << (cur & 31));
     if (!m) {
         int found = -1;
         for (int w0 = w + 1; w0 < nwords && found < 0; w0 += 64) {
             const int ww = w0 + lane;
-            const bool nz = ww < nwords && (E.C[ww] | E.T[ww] | E.H[ww]) != ~0u;
+            const bool nz = ww < nwords && (mw_peek(E.C + ww) | E.T[ww] | mw_peek(E.H + ww)) != ~0u;
             const unsigned long long b = __ballot(nz);
             if (b) found = w0 + __ffsll((long long)b) - 1;
         }
@@ -601,16 +622,16 @@ __device__ __forceinline__ int mw_dispatch(const MwEnv& E, lds_u8* pool, int nsl
             return -1;
         }
         w = found;
-        m = ~(E.C[w] | E.T[w] | E.H[w]);
+        m = ~(mw_peek(E.C + w) | E.T[w] | mw_peek(E.H + w));
     }
     const int q = w * 32 + (__ffs((int)m) - 1);
     if (lane == 0) {
         lds_slot* S = mw_slot(pool, slot);
-        if (STATS && S->state == kMwDone) mw_stat(ctl, 1, 1);  // a passed region, dropped
+        if (STATS && mw_peek(&S->state) == kMwDone) mw_stat(ctl, 1, 1);  // a passed region, dropped
         S->seed = q;
         S->ovf = 0;
-        S->chk = ctl->ncommit;
-        S->state = kMwGrowing;  // before the log entry that names it
+        S->chk = mw_peek(&ctl->ncommit);
+        mw_lds_store(&S->state, kMwGrowing);  // before the log entry that names it
         ctl->cursor = q + 1;
         dlog[2 * (dn & (kMwLog - 1))] = q;
         dlog[2 * (dn & (kMwLog - 1)) + 1] = slot;
@@ -630,7 +651,7 @@ __device__ __forceinline__ int mw_second_chance(const MwEnv& E, lds_u8* pool, in
     lds_ctl* ctl = E.ctl;
     const int nwords = E.sh * E.wpr;
     const int head = mw_lds_load(&ctl->head);
-    const int ls = lane < kMwLate ? ctl->late_seed[lane] : 0;
+    const int ls = lane < kMwLate ? mw_peek(&ctl->late_seed[lane]) : 0;
     const unsigned long long lfree = __ballot(lane < kMwLate && ls < head);
     if (!lfree) return -1;
     const int le = __ffsll((long long)lfree) - 1;
@@ -640,7 +661,7 @@ __device__ __forceinline__ int mw_second_chance(const MwEnv& E, lds_u8* pool, in
         bool ok = false;
         if (si < nslots) {
             lds_slot* S = mw_slot(pool, si);
-            const int st = S->state;
+            const int st = mw_lds_load(&S->state);
             ok = st == kMwFree || (st == kMwDone && S->seed < head);
         }
         const unsigned long long b = __ballot(ok);
@@ -652,7 +673,7 @@ __device__ __forceinline__ int mw_second_chance(const MwEnv& E, lds_u8* pool, in
         const int w = wb + lane;
         unsigned m = 0;
         if (w < nwords && w < w0 + kMwLateWords) {
-            m = ~E.C[w] & ~E.T[w] & E.H[w];
+            m = ~mw_peek(E.C + w) & ~E.T[w] & mw_peek(E.H + w);
             if (w == w0) m &= ~0u << (head & 31);
         }
         unsigned long long has = __ballot(m != 0u);
@@ -669,7 +690,7 @@ __device__ __forceinline__ int mw_second_chance(const MwEnv& E, lds_u8* pool, in
                     const int si = b0 + lane;
                     if (si < nslots) {
                         lds_slot* S = mw_slot(pool, si);
-                        live |= S->seed == q && S->state != kMwFree;
+                        live |= S->seed == q && mw_peek(&S->state) != kMwFree;
                     }
                 }
                 if (__ballot(live)) continue;
@@ -677,8 +698,8 @@ __device__ __forceinline__ int mw_second_chance(const MwEnv& E, lds_u8* pool, in
                     lds_slot* S = mw_slot(pool, slot);
                     S->seed = q;
                     S->ovf = 0;
-                    S->chk = ctl->ncommit;
-                    S->state = kMwGrowing;  // before the late entry that names it
+                    S->chk = mw_peek(&ctl->ncommit);
+                    mw_lds_store(&S->state, kMwGrowing);  // before the late entry that names it
                     ctl->late_slot[le] = slot;
                     mw_lds_store(&ctl->late_seed[le], q);
                 }
@@ -735,7 +756,7 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
     E.sw = sw; E.sh = sh; E.wpr = wpr; E.rowbits = wpr * 32;
     E.pdeg = (float)(prec / kD2R);
     E.prec = prec;
-    unsigned* sspill = slotspill + (size_t)task * kMwMaxSlots * kMwSlotSpill;
+    unsigned* sspill = slotspill + (size_t)task * nslots * kMwSlotSpill;  // the host sizes it by nslots
     // growth queue: LDS part + global part (the walker's spans a whole plane)
     const MwQueue GQ = wv == 0 ? MwQueue{gqAll, kMwGQ, xspill + (size_t)task * xspill_task,
                                          (int)min<size_t>(xspill_task, (size_t)sw * sh)}
@@ -815,11 +836,11 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
             if (mw_try_lock(&ctl->dlock, lane)) {
                 for (int b0 = 0; b0 < nslots && cs < 0; b0 += 64) {
                     const int si = b0 + lane;
-                    const bool ok = si < nslots && mw_slot(pool, si)->state == kMwCommitted;
+                    const bool ok = si < nslots && mw_lds_load(&mw_slot(pool, si)->state) == kMwCommitted;
                     const unsigned long long b = __ballot(ok);
                     if (b) cs = b0 + __ffsll((long long)b) - 1;
                 }
-                if (cs >= 0 && lane == 0) mw_slot(pool, cs)->state = kMwCopying;
+                if (cs >= 0 && lane == 0) mw_lds_store(&mw_slot(pool, cs)->state, kMwCopying);
                 mw_unlock(&ctl->dlock, lane);
             }
             if (cs >= 0) {
@@ -840,7 +861,7 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
             if (kMwLook > 0) {
                 int rs = -1;
                 if (mw_try_lock(&ctl->dlock, lane)) {
-                    const int wp = mw_lds_load(&ctl->wptr), dn = ctl->dlog_n;
+                    const int wp = mw_lds_load(&ctl->wptr), dn = mw_peek(&ctl->dlog_n);
                     const int nc = mw_lds_load(&ctl->ncommit), head = mw_lds_load(&ctl->head);
                     const int j = wp + lane;
                     int sj = -1;
@@ -849,18 +870,14 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
                         const int e = j & (kMwLog - 1);
                         sj = dlog[2 * e + 1];
                         lds_slot* S = mw_slot(pool, sj);
-                        ok = S->state == kMwDone && S->seed == dlog[2 * e] && S->seed >= head && S->chk < nc;
+                        ok = mw_lds_load(&S->state) == kMwDone && S->seed == dlog[2 * e] && S->seed >= head &&
+                             S->chk < nc;
                     }
                     const unsigned long long b = __ballot(ok);
                     if (b) {
                         const int cand = readlane_i(sj, __ffsll((long long)b) - 1);
                         int got = 0;
-                        if (lane == 0) {
-                            int e = kMwDone;
-                            got = __hip_atomic_compare_exchange_strong(&mw_slot(pool, cand)->state, &e, kMwGrowing,
-                                                                        __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                                        __HIP_MEMORY_SCOPE_WORKGROUP) ? 1 : 0;
-                        }
+                        if (lane == 0) got = mw_lds_cas(&mw_slot(pool, cand)->state, kMwDone, kMwGrowing) ? 1 : 0;
                         if (__builtin_amdgcn_readfirstlane(got)) rs = cand;
                     }
                     mw_unlock(&ctl->dlock, lane);

@@ -16,6 +16,7 @@ memory and streams; this module needs numpy only.
 """
 import ctypes
 import os
+import sys
 import pathlib
 
 import numpy as np
@@ -148,6 +149,7 @@ class LineParams(ctypes.Structure):
 
 
 _lib = None
+_runtime = None
 
 c_int_p = ctypes.POINTER(ctypes.c_int)
 c_void_pp = ctypes.POINTER(ctypes.c_void_p)
@@ -247,25 +249,55 @@ def _declare(lib):
     return lib
 
 
-def load():
-    """Load the HIP library (raises if it was not built: there is no fallback)."""
-    global _lib
+def load(runtime=None):
+    """Load the HIP library (raises if it was not built: there is no fallback).
+
+    Which HIP runtime the library binds to is decided here, once per process:
+    PyTorch's bundled libamdhip64 (HIP 7.0 on this image) and /opt/rocm's
+    (7.2) share the SONAME libamdhip64.so.7, so whichever loads first serves
+    both -- unless ours comes first and torch is imported later, in which case
+    torch loads its own copy by file name and that second runtime finds no
+    device.  `runtime`:
+
+    * "torch": import torch first (one runtime for both).  On the 7.0 runtime
+      `plvi_frame_extract_batch` / `plvi_stereo_frame_extract_batch` refuse
+      stream capture with PLVI_E_CAPTURE; everything else
+      behaves identically.
+    * "system": do not import torch; the library binds to /opt/rocm's runtime
+      (capture supported).  Do not import torch later in the same process.
+    * None (default): "torch" if torch is already imported, else the
+      PLVI_RUNTIME environment variable ("torch" / "system"; PLVI_NO_TORCH=1
+      means "system"), else "torch" when torch is installed -- the safe choice
+      for a process that may import torch later.
+    """
+    global _lib, _runtime
     if _lib is None:
-        # One HIP runtime per process: PyTorch's bundled libamdhip64 and
-        # /opt/rocm's share the SONAME libamdhip64.so.7, so whichever loads first
-        # serves both -- unless ours comes first, in which case torch later
-        # loads its own copy by file name and that second runtime finds no
-        # device.  Import torch (if installed) before the library; set
-        # PLVI_NO_TORCH=1 to run on the system runtime alone.
-        if not os.environ.get("PLVI_NO_TORCH"):
+        if runtime is None:
+            if "torch" in sys.modules:
+                runtime = "torch"
+            elif os.environ.get("PLVI_NO_TORCH"):
+                runtime = "system"
+            else:
+                runtime = os.environ.get("PLVI_RUNTIME", "torch")
+        if runtime not in ("torch", "system"):
+            raise ValueError(f"plvi.load: runtime must be 'torch' or 'system', not {runtime!r}")
+        if runtime == "torch":
             try:
                 import torch  # noqa: F401
             except ImportError:
-                pass
+                runtime = "system"
         if not LIB_PATH.exists():
             raise RuntimeError(f"{LIB_PATH} missing: build it with `make -C pl-vi-orbslam3_amd`")
         _lib = _declare(ctypes.CDLL(str(LIB_PATH)))
+        _runtime = runtime
+    elif runtime is not None and runtime != _runtime:
+        raise RuntimeError(f"plvi.load: library already bound to the {_runtime!r} HIP runtime")
     return _lib
+
+
+def bound_runtime():
+    """'torch' or 'system': the HIP runtime the loaded library is bound to (None before load())."""
+    return _runtime
 
 
 def exported_symbols():

@@ -58,8 +58,10 @@ class TableGather:
     code bench.py runs inside its timed region.
 
     `sizes` are the byte sizes of the tables (counts, keypoints, descriptors,
-    line counts, keylines, LBD descriptors).  `post(srcs, stream)` waits for
-    this gatherer's previous gathers, stages each source into its own byte
+    line counts, keylines, LBD descriptors).  `post(srcs, stream)` makes
+    `stream` wait for this gatherer's previous gathers (a stream-side wait
+    under RCCL, a host wait under gloo; the staging copies must be issued on
+    `stream` for that to order them), stages each source into its own byte
     buffer (`copy(dst_tensor, src)`: a device-pointer copy on the step's
     stream in the bench, a tensor copy on CPU) and issues one asynchronous
     `dist.gather` per table to rank 0 on `stream` (RCCL over xGMI on GPUs,
@@ -91,15 +93,22 @@ class TableGather:
         import torch
         if len(srcs) != len(self.stage):
             raise ValueError(f"TableGather.post: {len(srcs)} sources for {len(self.stage)} tables")
-        self.wait()
-        for src, t in zip(srcs, self.stage):
-            self.copy(t, src)
-        self.posted += 1
-        if self.world == 1:
-            return
-        import torch.distributed as dist
         ctx = torch.cuda.stream(stream) if stream is not None else contextlib.nullcontext()
         with ctx:
+            # Ordering: the staging buffers are still being read by the
+            # previous gathers.  Work.wait() under RCCL/NCCL does not block
+            # the host; it makes the CURRENT stream wait for the collective.
+            # Calling it inside `stream`'s context puts that wait on the
+            # stream the staging copies below are issued on, so they cannot
+            # overwrite a buffer an earlier gather is still sending (gloo's
+            # wait() blocks the host, which orders them as well).
+            self.wait()
+            for src, t in zip(srcs, self.stage):
+                self.copy(t, src)
+            self.posted += 1
+            if self.world == 1:
+                return
+            import torch.distributed as dist
             for i, t in enumerate(self.stage):
                 self.pending.append(dist.gather(t, self.recv[i] if self.rank == 0 else None, dst=0,
                                                 async_op=True))
