@@ -525,6 +525,57 @@ int plvi_search_by_projection(const plvi_proj_params* p, const plvi_keypoint* cu
                               const int* last_octave, const float* last_angle, const uint8_t* mp_desc,
                               const uint8_t* last_flags, int n_last, int* match);
 
+/* ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF,
+ * const set<MapPoint*>& sAlreadyFound, th, ORBdist) (src/ORBmatcher.cc:2180-2300):
+ * the relocalization guided search of Tracking::Relocalization
+ * (src/Tracking.cc:5857 th 10 / ORBdist 100, :5871 th 3 / ORBdist 64, with
+ * ORBmatcher(0.9, true)), single camera.  The MapPoint reads stay with the
+ * caller (they take the MapPoint mutexes): per KF MapPoint i, in
+ * pKF->GetMapPointMatches() order,
+ *   flags bit0 = pMP && !pMP->isBad() && !sAlreadyFound.count(pMP);
+ *   x3dc [3]   = Rcw*x3Dw + tcw (cv::Mat float gemm);
+ *   dist [3]   = { dist3D = cv::norm(x3Dw - Ow), GetMinDistanceInvariance(),
+ *                  GetMaxDistanceInvariance() };
+ *   level      = pMP->PredictScale(dist3D, &CurrentFrame);
+ *   angle      = pKF->mvKeysUn[i].angle;  desc = pMP->GetDescriptor().
+ * The device does the rest: Pinhole::project, the bounds and distance tests,
+ * GetFeaturesInArea(u, v, th*mvScaleFactors[level], level-1, level+1), the
+ * best candidate among keypoints whose mvpMapPoints[i2] is NULL (those
+ * assigned earlier in the same call included), bestDist <= ORBdist, and the
+ * rotation-histogram filter. */
+typedef struct plvi_reloc_params {
+  float fx, fy, cx, cy;             /* Pinhole mvParameters */
+  float min_x, max_x, min_y, max_y; /* mnMinX, mnMaxX, mnMinY, mnMaxY */
+  float inv_w, inv_h;               /* mfGridElementWidthInv / HeightInv */
+  float th;                         /* window radius at level 0 */
+  int orb_dist;                     /* ORBdist (< 256: at 256 an empty search would index mvpMapPoints[-1]) */
+  int check_orientation;            /* mbCheckOrientation */
+  int nlevels;                      /* CurrentFrame.mnScaleLevels (levels outside [0, nlevels) get no candidate) */
+  float scale_factors[16];          /* CurrentFrame.mvScaleFactors */
+} plvi_reloc_params;
+
+/* Batched over n_pairs (CurrentFrame, KeyFrame) pairs.  Current frame p:
+ * keypoints/descriptors [p][cur_cap] (mvKeysUn, counts d_cur_n), grid CSR from
+ * plvi_assign_grid_batch, blocked[i2] = mvpMapPoints[i2] != NULL on entry
+ * (NULL = none).  KeyFrame p: [p][kf_cap] flags, x3dc [3], dist [3], level,
+ * angle, desc [32] as above (counts d_kf_n).  Output match [p][cur_cap]: KF
+ * MapPoint index stored in mvpMapPoints[i2] by the call, -2 = set to NULL by
+ * the rotation filter, -1 = untouched; nmatches [p] = the return value.
+ * cur_cap, kf_cap <= 65535 and ~19 B per current + 8 B per KF point + 12 KB of
+ * LDS <= 160 KB.  Asynchronous on `stream`. */
+int plvi_search_reloc_batch(int n_pairs, const plvi_reloc_params* p, const plvi_keypoint* d_cur_kps,
+                            const uint8_t* d_cur_desc, const int* d_cur_n, int cur_cap, const uint8_t* d_cur_blocked,
+                            const int* d_cell_off, const int* d_cell_idx, const uint8_t* d_kf_flags,
+                            const float* d_x3dc, const float* d_dist, const int* d_level, const float* d_kf_angle,
+                            const uint8_t* d_mp_desc, const int* d_kf_n, int kf_cap, int* d_match, int* d_nmatches,
+                            void* stream);
+
+/* One pair from host memory, synchronous (grid built on the device).
+ * Returns nmatches (>= 0) or an error. */
+int plvi_search_reloc(const plvi_reloc_params* p, const plvi_keypoint* cur_kps, const uint8_t* cur_desc, int n_cur,
+                      const uint8_t* cur_blocked, const uint8_t* kf_flags, const float* x3dc, const float* dist,
+                      const int* level, const float* kf_angle, const uint8_t* mp_desc, int n_kf, int* match);
+
 /* ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>&
  * vpMapPoints, th, bFarPoints, thFarPoints) (src/ORBmatcher.cc:44-145,
  * F.Nleft == -1, RadiusByViewingCos :216-222): the local-map search of

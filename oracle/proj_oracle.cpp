@@ -10,6 +10,8 @@
 //   ORBmatcher::ComputeThreeMaxima   src/ORBmatcher.cc:2304-2345
 //   ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th, bFarPoints, thFarPoints)
 //                                    src/ORBmatcher.cc:44-145 (F.Nleft == -1) + RadiusByViewingCos :216-222
+//   ORBmatcher::SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist)
+//                                    src/ORBmatcher.cc:2180-2300 (relocalization)
 //   Pinhole::project                 src/CameraModels/Pinhole.cpp:30-39
 // The pose product x3Dc = Rcw*x3Dw + tcw (cv::Mat) is an input: it is taken
 // from the caller, as the drop-in shim keeps it on the host.
@@ -211,6 +213,85 @@ extern "C" int oracle_search_by_projection(
             nmatches++;
             if (check_ori) {
                 float rot = lang[i] - kps[bestIdx2].angle;
+                if (rot < 0.0) rot += 360.0f;
+                int bin = (int)std::round(rot * factor);
+                if (bin == kHisto) bin = 0;
+                rotHist[bin].push_back(bestIdx2);
+            }
+        }
+    }
+    std::vector<char> nulled(n_cur, 0);
+    if (check_ori) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        three_maxima(rotHist, kHisto, ind1, ind2, ind3);
+        for (int b = 0; b < kHisto; b++)
+            if (b != ind1 && b != ind2 && b != ind3)
+                for (int idx : rotHist[b]) {
+                    nulled[idx] = 1;
+                    nmatches--;
+                }
+    }
+    for (int i2 = 0; i2 < n_cur; ++i2) match[i2] = nulled[i2] ? -2 : mp[i2];
+    return nmatches;
+}
+
+// ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const
+// set<MapPoint*>& sAlreadyFound, th, ORBdist) (src/ORBmatcher.cc:2180-2300),
+// the relocalization guided search (Tracking.cc:5857, 5871).  Per KF MapPoint i
+// (GetMapPointMatches() order) the caller evaluates the MapPoint state:
+// kf_flags bit0 = pMP && !isBad() && !sAlreadyFound.count(pMP); x3dc =
+// Rcw*x3Dw+tcw; dist = {cv::norm(x3Dw-Ow), GetMinDistanceInvariance(),
+// GetMaxDistanceInvariance()}; level = PredictScale(dist3D, &CurrentFrame);
+// kf_angle = pKF->mvKeysUn[i].angle; mp_desc = GetDescriptor().  Frame:
+// mvKeysUn (x, y, octave, angle), descriptors, blocked = mvpMapPoints[i2] !=
+// NULL on entry.  Output match[i2] = KF index stored by this call, -2 = set to
+// NULL by the rotation filter, -1 = untouched.  Returns nmatches.
+extern "C" int oracle_search_reloc(int n_cur, const float* cx_, const float* cy_, const int* coct, const float* cang,
+                                   const uint8_t* cdesc, const uint8_t* cblocked, float minX, float maxX, float minY,
+                                   float maxY, float invW, float invH, const float* scale_factors, int nlevels,
+                                   float fx, float fy, float cxp, float cyp, int n_kf, const uint8_t* kf_flags,
+                                   const float* x3dc, const float* dist, const int* level, const float* kf_angle,
+                                   const uint8_t* mpdesc, float th, int ORBdist, int check_ori, int* match) {
+    const std::vector<Kp> kps = make_kps(n_cur, cx_, cy_, coct, cang);
+    Grid g;
+    assign_grid(kps, minX, minY, invW, invH, g);
+    std::vector<int> mp(n_cur, -1);
+    std::vector<char> nonnull(n_cur, 0);  // CurrentFrame.mvpMapPoints[i2] != NULL
+    for (int i = 0; i < n_cur; ++i) nonnull[i] = cblocked && cblocked[i] ? 1 : 0;
+    std::vector<int> rotHist[kHisto];
+    for (int i = 0; i < kHisto; i++) rotHist[i].reserve(500);
+    const float factor = 1.0f / kHisto;
+    int nmatches = 0;
+    for (int i = 0; i < n_kf; i++) {
+        if (!(kf_flags[i] & 1)) continue;  // pMP, !isBad(), !sAlreadyFound.count(pMP)
+        const float xc = x3dc[3 * i], yc = x3dc[3 * i + 1], zc = x3dc[3 * i + 2];
+        const float u = fx * xc / zc + cxp, v = fy * yc / zc + cyp;  // Pinhole::project
+        if (u < minX || u > maxX) continue;
+        if (v < minY || v > maxY) continue;
+        const float dist3D = dist[3 * i];
+        const float maxDistance = dist[3 * i + 2], minDistance = dist[3 * i + 1];
+        if (dist3D < minDistance || dist3D > maxDistance) continue;
+        const int nPredictedLevel = level[i];
+        if (nPredictedLevel < 0 || nPredictedLevel >= nlevels) continue;  // PredictScale's clamp range
+        const float radius = th * scale_factors[nPredictedLevel];
+        const std::vector<size_t> vIndices2 = features_in_area(g, kps, minX, minY, invW, invH, u, v, radius,
+                                                               nPredictedLevel - 1, nPredictedLevel + 1);
+        if (vIndices2.empty()) continue;
+        int bestDist = 256, bestIdx2 = -1;
+        for (size_t i2 : vIndices2) {
+            if (nonnull[i2]) continue;
+            const int d = dist256(mpdesc + 32 * (size_t)i, cdesc + 32 * i2);
+            if (d < bestDist) {
+                bestDist = d;
+                bestIdx2 = (int)i2;
+            }
+        }
+        if (bestDist <= ORBdist && bestIdx2 >= 0) {  // (ORBdist < 256: bestIdx2 >= 0 whenever bestDist <= ORBdist)
+            mp[bestIdx2] = i;
+            nonnull[bestIdx2] = 1;
+            nmatches++;
+            if (check_ori) {
+                float rot = kf_angle[i] - kps[bestIdx2].angle;
                 if (rot < 0.0) rot += 360.0f;
                 int bin = (int)std::round(rot * factor);
                 if (bin == kHisto) bin = 0;

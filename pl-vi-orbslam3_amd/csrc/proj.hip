@@ -3,6 +3,10 @@
 //   Frame::GetFeaturesInArea (src/Frame.cc:1006-1075)
 //   ORBmatcher::SearchByProjection(Frame&, const Frame&, th, bMono)
 //     (src/ORBmatcher.cc:1962-2178, Nleft == -1 branch) + ComputeThreeMaxima
+//   ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, ...)
+//     (src/ORBmatcher.cc:44-145, the local-map search)
+//   ORBmatcher::SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist)
+//     (src/ORBmatcher.cc:2180-2300, the relocalization guided search)
 // The pose product x3Dc = Rcw*x3Dw + tcw (cv::Mat float gemm) stays with the
 // caller (drop-in shim); everything after it runs here.
 //
@@ -435,6 +439,185 @@ __global__ __launch_bounds__(256) void search_local_kernel(
     for (int i = tid; i < nc; i += 256) M[i] = s.assign[i];
 }
 
+// ---------------------------------------------------------------------------
+// ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF,
+// const set<MapPoint*>& sAlreadyFound, th, ORBdist) (src/ORBmatcher.cc:2180-2300),
+// the relocalization guided search (Tracking.cc:5857, 5871).  Same schedule as
+// the frame-to-frame matcher: phase 1 finds every KF MapPoint's best candidate
+// in parallel against the NULL / non-NULL mvpMapPoints on entry; phase 2
+// walks the MapPoints in KF order -- every assignment blocks its keypoint for
+// the later points (:2240-2242), so a point whose best was taken meanwhile is
+// re-scanned -- and phase 3 is the rotation filter.
+__device__ unsigned reloc_scan(const plvi_reloc_params& p, const ProjLds& s, const unsigned char* blk, int i,
+                               const float* __restrict__ x3dc, const float* __restrict__ dist,
+                               const int* __restrict__ lvl, const uint8_t* __restrict__ mpdesc,
+                               const uint8_t* __restrict__ cdesc) {
+    const float xc = x3dc[3 * i], yc = x3dc[3 * i + 1], zc = x3dc[3 * i + 2];
+    const float u = p.fx * xc / zc + p.cx, v = p.fy * yc / zc + p.cy;  // Pinhole::project (no depth test here)
+    if (u < p.min_x || u > p.max_x) return 0xFFFFFFFFu;
+    if (v < p.min_y || v > p.max_y) return 0xFFFFFFFFu;
+    const float dist3D = dist[3 * i], minDistance = dist[3 * i + 1], maxDistance = dist[3 * i + 2];
+    if (dist3D < minDistance || dist3D > maxDistance) return 0xFFFFFFFFu;
+    const int L = lvl[i];
+    if (L < 0 || L >= p.nlevels) return 0xFFFFFFFFu;  // PredictScale clamps to [0, mnScaleLevels)
+    const float radius = p.th * p.scale_factors[L];
+    const int minLevel = L - 1, maxLevel = L + 1;
+    const int nMinCellX = max(0, (int)floorf((u - p.min_x - radius) * p.inv_w));
+    if (nMinCellX >= kGridCols) return 0xFFFFFFFFu;
+    const int nMaxCellX = min(kGridCols - 1, (int)ceilf((u - p.min_x + radius) * p.inv_w));
+    if (nMaxCellX < 0) return 0xFFFFFFFFu;
+    const int nMinCellY = max(0, (int)floorf((v - p.min_y - radius) * p.inv_h));
+    if (nMinCellY >= kGridRows) return 0xFFFFFFFFu;
+    const int nMaxCellY = min(kGridRows - 1, (int)ceilf((v - p.min_y + radius) * p.inv_h));
+    if (nMaxCellY < 0) return 0xFFFFFFFFu;
+    const uint4* dm = reinterpret_cast<const uint4*>(mpdesc + (size_t)32 * i);
+    const uint4 m0 = dm[0], m1 = dm[1];
+    int bestDist = 256, bestIdx2 = -1;
+    for (int ix = nMinCellX; ix <= nMaxCellX; ++ix) {
+        const int k0 = s.cell_off[ix * kGridRows + nMinCellY], k1 = s.cell_off[ix * kGridRows + nMaxCellY + 1];
+        for (int k = k0; k < k1; ++k) {
+            const int i2 = s.cell_idx[k];
+            const int o = s.koct[i2];  // bCheckLevels holds: maxLevel >= 0
+            if (o < minLevel || o > maxLevel) continue;
+            const float distx = s.kx[i2] - u, disty = s.ky[i2] - v;
+            if (!(fabsf(distx) < radius && fabsf(disty) < radius)) continue;
+            if (blk[i2]) continue;
+            const uint4* dc = reinterpret_cast<const uint4*>(cdesc + (size_t)32 * i2);
+            const uint4 c0 = dc[0], c1 = dc[1];
+            const int d = __popc(m0.x ^ c0.x) + __popc(m0.y ^ c0.y) + __popc(m0.z ^ c0.z) + __popc(m0.w ^ c0.w) +
+                          __popc(m1.x ^ c1.x) + __popc(m1.y ^ c1.y) + __popc(m1.z ^ c1.z) + __popc(m1.w ^ c1.w);
+            if (d < bestDist) {
+                bestDist = d;
+                bestIdx2 = i2;
+            }
+        }
+    }
+    if (bestIdx2 < 0) return 0xFFFFFFFFu;
+    return ((unsigned)bestDist << 16) | (unsigned)bestIdx2;
+}
+
+__global__ __launch_bounds__(256) void search_reloc_kernel(
+    plvi_reloc_params p, const plvi_keypoint* __restrict__ ckps, const uint8_t* __restrict__ cdesc_all,
+    const int* __restrict__ cur_n, int cur_cap, const uint8_t* __restrict__ cblocked,
+    const int* __restrict__ cell_off_all, const int* __restrict__ cell_idx_all, const uint8_t* __restrict__ kflags_all,
+    const float* __restrict__ x3dc_all, const float* __restrict__ dist_all, const int* __restrict__ lvl_all,
+    const float* __restrict__ kang_all, const uint8_t* __restrict__ mpdesc_all, const int* __restrict__ kf_n,
+    int kf_cap, int* __restrict__ match, int* __restrict__ nmatches) {
+    extern __shared__ __align__(16) unsigned char lds[];
+    const int pr = blockIdx.x, tid = threadIdx.x;
+    const int nc = min(cur_n[pr], cur_cap), nk = min(kf_n[pr], kf_cap);
+    ProjLds s;
+    {
+        unsigned char* q = lds;
+        s.kx = reinterpret_cast<float*>(q); q += 4 * cur_cap;
+        s.ky = reinterpret_cast<float*>(q); q += 4 * cur_cap;
+        s.assign = reinterpret_cast<int*>(q); q += 4 * cur_cap;
+        s.best = reinterpret_cast<int*>(q); q += 4 * kf_cap;
+        s.cell_off = reinterpret_cast<int*>(q); q += 4 * (kGridCells + 1);
+        s.cell_idx = reinterpret_cast<unsigned short*>(q); q += 2 * cur_cap;
+        s.ent = reinterpret_cast<unsigned short*>(q); q += 4 * kf_cap;  // [kf_cap] idx, [kf_cap] bin
+        s.koct = q; q += cur_cap;
+        s.blocked = q; q += cur_cap;
+        s.pre = q; q += cur_cap;
+        s.nulled = q;
+    }
+    __shared__ int s_hist[kProjHisto], s_keep[3], s_ne, s_nm;
+    const plvi_keypoint* K = ckps + (size_t)pr * cur_cap;
+    const uint8_t* cdesc = cdesc_all + (size_t)pr * cur_cap * 32;
+    for (int i = tid; i < nc; i += 256) {
+        s.kx[i] = K[i].x;
+        s.ky[i] = K[i].y;
+        s.koct[i] = (unsigned char)K[i].octave;
+        const unsigned char b = cblocked ? (cblocked[(size_t)pr * cur_cap + i] != 0) : 0;
+        s.blocked[i] = b;
+        s.pre[i] = b;
+        s.nulled[i] = 0;
+        s.assign[i] = -1;
+    }
+    const int* CO = cell_off_all + (size_t)pr * (kGridCells + 1);
+    for (int c = tid; c <= kGridCells; c += 256) s.cell_off[c] = CO[c];
+    const int ncell = CO[kGridCells];
+    for (int k = tid; k < ncell; k += 256) s.cell_idx[k] = (unsigned short)cell_idx_all[(size_t)pr * cur_cap + k];
+    if (tid < kProjHisto) s_hist[tid] = 0;
+    __syncthreads();
+    const float* x3dc = x3dc_all + (size_t)pr * kf_cap * 3;
+    const float* dist = dist_all + (size_t)pr * kf_cap * 3;
+    const int* lvl = lvl_all + (size_t)pr * kf_cap;
+    const uint8_t* mpdesc = mpdesc_all + (size_t)pr * kf_cap * 32;
+    const uint8_t* kfl = kflags_all + (size_t)pr * kf_cap;
+    // phase 1: every KF MapPoint against mvpMapPoints on entry
+    for (int i = tid; i < nk; i += 256)
+        s.best[i] = (kfl[i] & 1) ? (int)reloc_scan(p, s, s.pre, i, x3dc, dist, lvl, mpdesc, cdesc) : -1;
+    __syncthreads();
+    // phase 2: the assignment in KF order (:2260-2277)
+    if (tid == 0) {
+        const float factor = 1.0f / kProjHisto;
+        const float* kang = kang_all + (size_t)pr * kf_cap;
+        int nm = 0, ne = 0;
+        for (int i = 0; i < nk; ++i) {
+            unsigned b = (unsigned)s.best[i];
+            if (b == 0xFFFFFFFFu) continue;
+            if (s.blocked[b & 0xFFFFu] != s.pre[b & 0xFFFFu])  // its best was taken meanwhile: re-scan
+                b = reloc_scan(p, s, s.blocked, i, x3dc, dist, lvl, mpdesc, cdesc);
+            if (b == 0xFFFFFFFFu || (int)(b >> 16) > p.orb_dist) continue;
+            const int i2 = (int)(b & 0xFFFFu);
+            s.assign[i2] = i;
+            s.blocked[i2] = 1;
+            ++nm;
+            if (p.check_orientation) {
+                float rot = kang[i] - K[i2].angle;
+                if (rot < 0.0f) rot += 360.0f;
+                int bin = (int)roundf(rot * factor);
+                if (bin == kProjHisto) bin = 0;
+                s.ent[kf_cap + ne] = (unsigned short)bin;
+                s.ent[ne++] = (unsigned short)i2;
+                s_hist[bin]++;
+            }
+        }
+        s_ne = ne;
+        s_nm = nm;
+        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;  // ComputeThreeMaxima (:2304-2345)
+        for (int b = 0; b < kProjHisto; b++) {
+            const int c = s_hist[b];
+            if (c > max1) {
+                max3 = max2; max2 = max1; max1 = c;
+                ind3 = ind2; ind2 = ind1; ind1 = b;
+            } else if (c > max2) {
+                max3 = max2; max2 = c;
+                ind3 = ind2; ind2 = b;
+            } else if (c > max3) {
+                max3 = c;
+                ind3 = b;
+            }
+        }
+        if (max2 < 0.1f * (float)max1) {
+            ind2 = -1;
+            ind3 = -1;
+        } else if (max3 < 0.1f * (float)max1) {
+            ind3 = -1;
+        }
+        s_keep[0] = ind1; s_keep[1] = ind2; s_keep[2] = ind3;
+    }
+    __syncthreads();
+    // phase 3: entries in dropped bins set mvpMapPoints[idx] = NULL (:2284-2296)
+    if (p.check_orientation) {
+        const int ne = s_ne;
+        int dropped = 0;
+        for (int e = tid; e < ne; e += 256) {
+            const int bin = s.ent[kf_cap + e];
+            if (bin != s_keep[0] && bin != s_keep[1] && bin != s_keep[2]) {
+                s.nulled[s.ent[e]] = 1;
+                ++dropped;
+            }
+        }
+        if (dropped) atomicSub(&s_nm, dropped);
+        __syncthreads();
+    }
+    int* M = match + (size_t)pr * cur_cap;
+    for (int i = tid; i < nc; i += 256) M[i] = s.nulled[i] ? -2 : s.assign[i];
+    if (tid == 0) nmatches[pr] = s_nm;
+}
+
 static size_t local_smem(int cur_cap, int mp_cap) {
     return (size_t)cur_cap * (4 + 4 + 4 + 2 + 1 + 1 + 1) + (size_t)mp_cap * 8 + 4 * (kGridCells + 1) + 64;
 }
@@ -541,6 +724,83 @@ extern "C" int plvi_search_by_projection(const plvi_proj_params* p, const plvi_k
         reinterpret_cast<const int*>(B + off[oCI]), reinterpret_cast<const float*>(B + off[oX]),
         reinterpret_cast<const int*>(B + off[oLO]), reinterpret_cast<const float*>(B + off[oLA]), B + off[oMD],
         B + off[oLF], dN + 1, lc, reinterpret_cast<int*>(B + off[oM]), dN + 2, nullptr);
+    if (rc) return rc;
+    PLVI_CHECK(hipDeviceSynchronize());
+    int nm = 0;
+    PLVI_CHECK(hipMemcpy(match, B + off[oM], 4 * (size_t)n_cur, hipMemcpyDeviceToHost));
+    PLVI_CHECK(hipMemcpy(&nm, dN + 2, 4, hipMemcpyDeviceToHost));
+    return nm;
+}
+
+extern "C" int plvi_search_reloc_batch(int n_pairs, const plvi_reloc_params* p, const plvi_keypoint* d_cur_kps,
+                                       const uint8_t* d_cur_desc, const int* d_cur_n, int cur_cap,
+                                       const uint8_t* d_cur_blocked, const int* d_cell_off, const int* d_cell_idx,
+                                       const uint8_t* d_kf_flags, const float* d_x3dc, const float* d_dist,
+                                       const int* d_level, const float* d_kf_angle, const uint8_t* d_mp_desc,
+                                       const int* d_kf_n, int kf_cap, int* d_match, int* d_nmatches, void* stream) {
+    if (!p || n_pairs < 0 || cur_cap < 1 || kf_cap < 1 || cur_cap > 65535 || kf_cap > 65535) return PLVI_E_BADARG;
+    if (p->nlevels < 1 || p->nlevels > 16 || p->orb_dist < 0 || p->orb_dist > 255) return PLVI_E_BADARG;
+    if (n_pairs == 0) return PLVI_OK;
+    const size_t smem = proj_smem(cur_cap, kf_cap);  // same carve-up as the frame-to-frame matcher
+    if (smem > 160 * 1024) return PLVI_E_CAPACITY;
+    PLVI_CHECK(hipFuncSetAttribute((const void*)search_reloc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)smem));
+    hipLaunchKernelGGL(search_reloc_kernel, dim3(n_pairs), dim3(256), smem, (hipStream_t)stream, *p, d_cur_kps,
+                       d_cur_desc, d_cur_n, cur_cap, d_cur_blocked, d_cell_off, d_cell_idx, d_kf_flags, d_x3dc, d_dist,
+                       d_level, d_kf_angle, d_mp_desc, d_kf_n, kf_cap, d_match, d_nmatches);
+    PLVI_CHECK(hipGetLastError());
+    return PLVI_OK;
+}
+
+// One pair from host memory, synchronous (grid built on the device).
+extern "C" int plvi_search_reloc(const plvi_reloc_params* p, const plvi_keypoint* cur_kps, const uint8_t* cur_desc,
+                                 int n_cur, const uint8_t* cur_blocked, const uint8_t* kf_flags, const float* x3dc,
+                                 const float* dist, const int* level, const float* kf_angle, const uint8_t* mp_desc,
+                                 int n_kf, int* match) {
+    if (!p || n_cur < 0 || n_kf < 0 || (n_cur > 0 && (!cur_kps || !cur_desc || !match))) return PLVI_E_BADARG;
+    if (n_kf > 0 && (!kf_flags || !x3dc || !dist || !level || !kf_angle || !mp_desc)) return PLVI_E_BADARG;
+    if (p->nlevels < 1 || p->nlevels > 16 || p->orb_dist < 0 || p->orb_dist > 255) return PLVI_E_BADARG;
+    if (n_cur == 0) return 0;
+    const int cc = n_cur, kc = std::max(n_kf, 1);
+    std::vector<size_t> off;
+    size_t tot = 0;
+    auto put = [&](size_t bytes) {
+        off.push_back(tot);
+        tot += (bytes + 255) & ~size_t(255);
+        return off.size() - 1;
+    };
+    const size_t oK = put(sizeof(plvi_keypoint) * cc), oD = put(32 * (size_t)cc), oB = put(cc);
+    const size_t oCO = put(4 * (size_t)(kGridCells + 1)), oCI = put(4 * (size_t)cc), oF = put(kc);
+    const size_t oX = put(12 * (size_t)kc), oS = put(12 * (size_t)kc), oL = put(4 * (size_t)kc);
+    const size_t oA = put(4 * (size_t)kc), oMD = put(32 * (size_t)kc), oM = put(4 * (size_t)cc), oN = put(16);
+    DevBuf d;
+    if (d.alloc(tot)) return PLVI_E_HIP;
+    uint8_t* B = d.as<uint8_t>();
+    auto up = [&](size_t slot, const void* src, size_t bytes) -> int {
+        if (src && bytes) PLVI_CHECK(hipMemcpy(B + off[slot], src, bytes, hipMemcpyHostToDevice));
+        return PLVI_OK;
+    };
+    int rc = up(oK, cur_kps, sizeof(plvi_keypoint) * cc) | up(oD, cur_desc, 32 * (size_t)cc);
+    if (cur_blocked) rc |= up(oB, cur_blocked, cc);
+    else PLVI_CHECK(hipMemset(B + off[oB], 0, cc));
+    if (n_kf > 0)
+        rc |= up(oF, kf_flags, n_kf) | up(oX, x3dc, 12 * (size_t)n_kf) | up(oS, dist, 12 * (size_t)n_kf) |
+              up(oL, level, 4 * (size_t)n_kf) | up(oA, kf_angle, 4 * (size_t)n_kf) |
+              up(oMD, mp_desc, 32 * (size_t)n_kf);
+    if (rc) return PLVI_E_HIP;
+    int counts[2] = {n_cur, n_kf};
+    PLVI_CHECK(hipMemcpy(B + off[oN], counts, 8, hipMemcpyHostToDevice));
+    int* dN = reinterpret_cast<int*>(B + off[oN]);
+    plvi_grid_params gp{p->min_x, p->min_y, p->inv_w, p->inv_h};
+    rc = plvi_assign_grid_batch(reinterpret_cast<const plvi_keypoint*>(B + off[oK]), dN, cc, 1, &gp,
+                                reinterpret_cast<int*>(B + off[oCO]), reinterpret_cast<int*>(B + off[oCI]), nullptr);
+    if (rc) return rc;
+    rc = plvi_search_reloc_batch(1, p, reinterpret_cast<const plvi_keypoint*>(B + off[oK]), B + off[oD], dN, cc,
+                                 B + off[oB], reinterpret_cast<const int*>(B + off[oCO]),
+                                 reinterpret_cast<const int*>(B + off[oCI]), B + off[oF],
+                                 reinterpret_cast<const float*>(B + off[oX]), reinterpret_cast<const float*>(B + off[oS]),
+                                 reinterpret_cast<const int*>(B + off[oL]), reinterpret_cast<const float*>(B + off[oA]),
+                                 B + off[oMD], dN + 1, kc, reinterpret_cast<int*>(B + off[oM]), dN + 2, nullptr);
     if (rc) return rc;
     PLVI_CHECK(hipDeviceSynchronize());
     int nm = 0;

@@ -120,6 +120,16 @@ class LocalParams(ctypes.Structure):
                 ("nlevels", ctypes.c_int), ("scale_factors", ctypes.c_float * 16)]
 
 
+class RelocParams(ctypes.Structure):
+    """plvi_reloc_params (include/plvi_frontend.h): ORBmatcher::SearchByProjection(Frame&, KeyFrame*,
+    sAlreadyFound, th, ORBdist)."""
+    _fields_ = [("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
+                ("min_x", ctypes.c_float), ("max_x", ctypes.c_float), ("min_y", ctypes.c_float),
+                ("max_y", ctypes.c_float), ("inv_w", ctypes.c_float), ("inv_h", ctypes.c_float),
+                ("th", ctypes.c_float), ("orb_dist", ctypes.c_int), ("check_orientation", ctypes.c_int),
+                ("nlevels", ctypes.c_int), ("scale_factors", ctypes.c_float * 16)]
+
+
 class LineProjParams(ctypes.Structure):
     """plvi_line_proj_params (include/plvi_frontend.h): LineMatcher::SearchByProjection."""
     _fields_ = [("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
@@ -218,6 +228,8 @@ def _declare(lib):
         "plvi_line_search_init_batch": ([V, V, I, V, V, I, I, V, V, V, V, V], I),
         "plvi_search_local_batch": ([I, V, V, V, V, I, V, V, V, V, V, V, V, V, V, I, V, V, V], I),
         "plvi_search_local": ([V, V, V, I, V, V, V, V, V, V, I, V], I),
+        "plvi_search_reloc_batch": ([I, V, V, V, V, I, V, V, V, V, V, V, V, V, V, V, I, V, V, V], I),
+        "plvi_search_reloc": ([V, V, V, I, V, V, V, V, V, V, V, I, V], I),
         "plvi_line_search_projection_batch": ([I, V, V, V, V, V, I, V, V, I, V, V, V, V, V, I, V, V, V, V], I),
         "plvi_line_search_projection": ([V, V, V, V, I, V, V, V, V, V, V, I, V], I),
         "plvi_vocab_load_text": ([ctypes.c_char_p, I, I, c_void_pp], I),
@@ -808,6 +820,33 @@ class ORBmatcher:
                                                 _ptr(fl), _ptr(pr), _ptr(lv), _ptr(md), len(fl), _ptr(out)),
                     "plvi_search_local")
         return nm, out[:len(k)]
+
+    def SearchByProjectionKF(self, params, cur_kps, cur_desc, kf_flags, x3dc, dist, level, kf_angle, mp_desc,
+                             cur_blocked=None):
+        """SearchByProjection(CurrentFrame, pKF, sAlreadyFound, th, ORBdist) (src/ORBmatcher.cc:2180-2300),
+        the relocalization guided search, with mbCheckOrientation = checkOri of this matcher.  params:
+        RelocParams (camera, bounds, grid, th, orb_dist, scale factors); cur_kps: mvKeysUn; cur_blocked:
+        mvpMapPoints[i2] != NULL on entry; per KF MapPoint (GetMapPointMatches() order): flags (bit0 = live and
+        not in sAlreadyFound), x3dc (n x 3), dist (n x 3: dist3D, min / max distance invariance), level
+        (PredictScale), kf_angle (pKF->mvKeysUn[i].angle), descriptor.  Returns (nmatches, match) with
+        match[i2] = KF MapPoint index, -2 (nulled by the rotation filter) or -1 (untouched)."""
+        params.check_orientation = int(self.check_orientation)
+        ck = np.ascontiguousarray(cur_kps).view(KEYPOINT_DTYPE)
+        cd = np.ascontiguousarray(cur_desc, np.uint8).reshape(-1, 32)
+        n = len(ck)
+        fl = np.ascontiguousarray(kf_flags, np.uint8)
+        x3 = np.ascontiguousarray(x3dc, np.float32).reshape(-1, 3)
+        ds = np.ascontiguousarray(dist, np.float32).reshape(-1, 3)
+        lv = np.ascontiguousarray(level, np.int32)
+        ka = np.ascontiguousarray(kf_angle, np.float32)
+        md = np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32)
+        cb = None if cur_blocked is None else np.ascontiguousarray(cur_blocked, np.uint8)
+        out = np.full(max(n, 1), -1, np.int32)
+        nm = _check(self._lib.plvi_search_reloc(ctypes.byref(params), _ptr(ck), _ptr(cd), n,
+                                                None if cb is None else _ptr(cb), _ptr(fl), _ptr(x3), _ptr(ds),
+                                                _ptr(lv), _ptr(ka), _ptr(md), len(fl), _ptr(out)),
+                    "plvi_search_reloc")
+        return nm, out[:n]
 
     @staticmethod
     def DescriptorDistance(a, b, line_matcher_quirk=False):

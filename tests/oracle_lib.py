@@ -467,6 +467,34 @@ def search_by_projection(case, th, forward=0, backward=0, check_ori=1):
     return n, out[:len(kx)]
 
 
+def search_reloc(case, th, orb_dist, check_ori=1):
+    """ORBmatcher::SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist) restatement
+    -> (nmatches, match)."""
+    lib = load()
+    V, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    lib.oracle_search_reloc.argtypes = [I, V, V, V, V, V, V, F, F, F, F, F, F, V, I, F, F, F, F, I, V, V, V, V, V,
+                                        V, F, I, I, V]
+    lib.oracle_search_reloc.restype = I
+    c = case
+    k = c["cur_kps"]
+    kx = np.ascontiguousarray(k["x"], np.float32); ky = np.ascontiguousarray(k["y"], np.float32)
+    ko = np.ascontiguousarray(k["octave"], np.int32); ka = np.ascontiguousarray(k["angle"], np.float32)
+    cd = np.ascontiguousarray(c["cur_desc"], np.uint8)
+    cb = np.ascontiguousarray(c["cur_blocked"], np.uint8)
+    min_x, max_x, min_y, max_y, inv_w, inv_h = c["grid"]
+    sf = np.ascontiguousarray(c["scale_factors"], np.float32)
+    fl = np.ascontiguousarray(c["kf_flags"], np.uint8)
+    x3 = np.ascontiguousarray(c["x3dc"], np.float32); ds = np.ascontiguousarray(c["dist"], np.float32)
+    lv = np.ascontiguousarray(c["level"], np.int32); an = np.ascontiguousarray(c["kf_angle"], np.float32)
+    md = np.ascontiguousarray(c["mp_desc"], np.uint8)
+    fx, fy, cx, cy, _ = c["camera"]
+    out = np.full(max(len(kx), 1), -1, np.int32)
+    n = lib.oracle_search_reloc(len(kx), _p(kx), _p(ky), _p(ko), _p(ka), _p(cd), _p(cb), min_x, max_x, min_y, max_y,
+                                inv_w, inv_h, _p(sf), len(sf), fx, fy, cx, cy, len(fl), _p(fl), _p(x3), _p(ds), _p(lv),
+                                _p(an), _p(md), th, orb_dist, check_ori, _p(out))
+    return n, out[:len(kx)]
+
+
 def search_local(case, th, nnratio=0.8):
     """ORBmatcher::SearchByProjection(Frame&, const vector<MapPoint*>&, th, ...) restatement -> (nmatches, match)."""
     lib = load()

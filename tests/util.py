@@ -172,6 +172,61 @@ def projection_case(seed, n_cur=1000, n_last=900, W=752, H=480, uright=False, du
     return case
 
 
+def reloc_case(seed, n_cur=1000, n_kf=800, W=752, H=480, dup=0.08, pre_blocked=0.3):
+    """Synthetic relocalization-search input (ORBmatcher::SearchByProjection(Frame&, KeyFrame*, sAlreadyFound,
+    th, ORBdist), src/ORBmatcher.cc:2180-2300): current-frame keypoints (mvKeysUn) with descriptors, ~30 %
+    already holding a MapPoint (the PnP inliers); KF MapPoints that project near a keypoint (70 %) or anywhere,
+    descriptors = the keypoint's with ~6 % bit flips (or random), dist3D inside / outside the MapPoints'
+    distance invariance range, PredictScale levels = the keypoint's octave +-1 (a few at the clamp ends), some
+    points dead or already found, `dup` aimed at another point's keypoint (assignment conflicts), a global
+    rotation of 10 degrees plus noise, points behind the camera (the reloc search has no depth test)."""
+    from plvi import KEYPOINT_DTYPE, grid_geometry
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = np.float32(458.654), np.float32(457.296), np.float32(367.215), np.float32(248.375)
+    kps = np.zeros(n_cur, KEYPOINT_DTYPE)
+    kps["x"] = rng.uniform(-4, W + 4, n_cur).astype(np.float32)
+    kps["y"] = rng.uniform(-4, H + 4, n_cur).astype(np.float32)
+    kps["octave"] = np.minimum(rng.geometric(0.35, n_cur) - 1, 7)
+    kps["angle"] = rng.uniform(0, 360, n_cur).astype(np.float32)
+    kps["size"] = 31
+    kps["class_id"] = -1
+    desc = rng.integers(0, 256, (n_cur, 32), dtype=np.uint8)
+    near = rng.random(n_kf) < 0.7
+    src = rng.integers(0, n_cur, n_kf)
+    ndup = int(dup * n_kf)
+    src[:ndup] = src[ndup:2 * ndup]
+    u = np.where(near, kps["x"][src] + rng.normal(0, 2.0, n_kf), rng.uniform(-20, W + 20, n_kf))
+    v = np.where(near, kps["y"][src] + rng.normal(0, 2.0, n_kf), rng.uniform(-20, H + 20, n_kf))
+    z = rng.uniform(1.0, 20.0, n_kf)
+    z[rng.random(n_kf) < 0.02] *= -1
+    x3 = np.stack([(u - cx) * z / fx, (v - cy) * z / fy, z], 1).astype(np.float32)
+    d3 = np.abs(z * rng.uniform(1.0, 1.3, n_kf)).astype(np.float32)
+    lo = (d3 * rng.uniform(0.3, 1.02, n_kf)).astype(np.float32)
+    hi = (d3 * rng.uniform(0.98, 3.0, n_kf)).astype(np.float32)
+    dist = np.stack([d3, lo, hi], 1).astype(np.float32)
+    lvl = np.clip(np.where(near, kps["octave"][src] + rng.integers(-1, 2, n_kf), rng.integers(0, 8, n_kf)), 0, 7)
+    bits = np.unpackbits(desc[src], axis=1)
+    bits ^= (rng.random(bits.shape) < 0.06).astype(np.uint8)
+    mp = np.where(near[:, None], np.packbits(bits, axis=1), rng.integers(0, 256, (n_kf, 32), dtype=np.uint8))
+    ang = np.mod(kps["angle"][src] + 10 + rng.normal(0, 5, n_kf), 360).astype(np.float32)
+    return {"cur_kps": kps, "cur_desc": desc, "cur_blocked": (rng.random(n_cur) < pre_blocked).astype(np.uint8),
+            "grid": grid_geometry(W, H), "scale_factors": orb_scale_factors(), "x3dc": x3, "dist": dist,
+            "level": lvl.astype(np.int32), "kf_flags": (rng.random(n_kf) < 0.9).astype(np.uint8),
+            "kf_angle": ang, "mp_desc": mp.astype(np.uint8), "camera": (fx, fy, cx, cy, np.float32(0.0))}
+
+
+def reloc_params(case, th, orb_dist):
+    import plvi
+    p = plvi.RelocParams()
+    fx, fy, cx, cy, _ = case["camera"]
+    p.fx, p.fy, p.cx, p.cy, p.th, p.orb_dist = fx, fy, cx, cy, th, orb_dist
+    (p.min_x, p.max_x, p.min_y, p.max_y, p.inv_w, p.inv_h) = case["grid"]
+    p.nlevels = len(case["scale_factors"])
+    for i, s in enumerate(case["scale_factors"]):
+        p.scale_factors[i] = s
+    return p
+
+
 def local_case(seed, n_cur=1000, n_mp=1500, W=752, H=480, uright=False, dup=0.15):
     """Synthetic local-map search input (ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>...),
     SURVEY 8f / VERDICT r1 item 8): current-frame keypoints with octaves and descriptors; MapPoints whose
