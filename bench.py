@@ -92,6 +92,17 @@ def lsd_prep_bytes(w, h, scale=0.8, noct=2):
     return tot
 
 
+def lbd_sobel_bytes(w, h):
+    """SURVEY 8(d) LBD bytes/frame (2 918 400 at 640x480) split over the two
+    kernels that materialise them: lbd_sobel0_kernel = octave-0 5x5 blur
+    (read + write) + Sobel of it (u8 in, two int16 planes out: 5 B/px) =
+    2 150 400 B; lbd_sobel1_kernel = pyrDown (octave-0 blur read, quarter
+    write) + Sobel of octave 1 = 768 000 B."""
+    p0 = w * h
+    p1 = (w // 2) * (h // 2)
+    return (2 * p0 + 5 * p0, p0 + p1 + 5 * p1)
+
+
 def committed_traffic(batch, kernel):
     """HBM bytes per launch of `kernel` from the committed PMC passes
     (profiles/*/pmc_traffic*.json, tools/pmc_traffic.py), taken at this batch
@@ -598,6 +609,7 @@ def run(args, world, rank):
     f0 = seq.data_ptr()
     orb.profile(True)
     lx.profile(True)
+    lx.kernel_timing(True)  # isolated per-launch times of the LBD Gaussian + Sobel kernels
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     match_ms = 0.0
     nprof = max(3, min(args.steps, 10))
@@ -613,6 +625,8 @@ def run(args, world, rank):
         match_ms += ev0.elapsed_time(ev1)
     st_orb, runs = orb.profile_read()
     st_lines, lruns = lx.profile_read()
+    lbd_iso = [lx.kernel_timing_read(k) for k in (1, 2)]
+    lx.kernel_timing(False)
     orb.profile(False)
     lx.profile(False)
 
@@ -662,12 +676,17 @@ def run(args, world, rank):
     ms_step = el / args.steps * 1e3
     err = list(err_warm)
     ktot = kn = ltot = ln = 0
+    sob = [[0.0, 0], [0.0, 0]]  # LBD Gaussian + Sobel kernels: [total ms, launches] of octave 0 / 1
     for sl in slots:
         err[0] |= sl.orb.errors(sl.st)
         err[1] |= sl.lx.errors(sl.st)
         a, b = sl.orb.kernel_timing_read()
         c, d = sl.lx.kernel_timing_read()
         ktot, kn, ltot, ln = ktot + a, kn + b, ltot + c, ln + d
+        for k in (0, 1):
+            t_, n_ = sl.lx.kernel_timing_read(k + 1)
+            sob[k][0] += t_
+            sob[k][1] += n_
     # last timed batch's window (for the checks below)
     lo_last = ((step_no[0] - 1) % nwin) * (B - 1)
 
@@ -693,6 +712,24 @@ def run(args, world, rank):
                 "avg_launch_ms": lp_ms, "launches": ln}
     if roof_lsd["achieved"]:
         roof_lsd["frac"] = roof_lsd["achieved"] / HBM_PEAK_GBS
+    roof_lbd = {}
+    for k, (name, what) in enumerate((("lbd_sobel0_kernel", "octave-0 5x5 Gaussian + Sobel dx/dy"),
+                                      ("lbd_sobel1_kernel", "pyrDown + Sobel dx/dy of octave 1"))):
+        by = lbd_sobel_bytes(W, H)[k] * B
+        t_ms = sob[k][0] / max(sob[k][1], 1)
+        i_ms = lbd_iso[k][0] / max(lbd_iso[k][1], 1)
+        e = {"bound": "hbm", "kernel": f"{name} ({what})", "bytes_per_launch": by,
+             "bytes_model": "SURVEY 8(d) LBD split per octave (blur/pyrDown r+w, Sobel u8 in + 2 x i16 out)",
+             "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "traffic": committed_traffic(B, name) if (W, H) == (640, 480) else None,
+             "in_schedule": {"avg_launch_ms": t_ms, "launches": sob[k][1],
+                             "achieved": by / (t_ms * 1e-3) / 1e9 if sob[k][1] else None},
+             "isolated": {"avg_launch_ms": i_ms, "launches": lbd_iso[k][1],
+                          "achieved": by / (i_ms * 1e-3) / 1e9 if lbd_iso[k][1] else None}}
+        for part in ("in_schedule", "isolated"):
+            if e[part]["achieved"]:
+                e[part]["frac"] = e[part]["achieved"] / HBM_PEAK_GBS
+        roof_lbd[name] = e
     e2e_b = E2E_BYTES_640 if (W, H) == (640, 480) else E2E_BYTES_752 if (W, H) == (752, 480) else None
     e2e = None if e2e_b is None else {"bytes_per_frame": e2e_b, "achieved": e2e_b * value / world / 1e9,
                                       "unit": "GB/s per GPU", "frac": e2e_b * value / world / 1e9 / HBM_PEAK_GBS,
@@ -745,6 +782,7 @@ def run(args, world, rank):
                    "inflight": len(slots)},
         "roofline": roof,
         "roofline_lsd_prep": roof_lsd,
+        "roofline_lbd": roof_lbd,
         "end_to_end_hbm": e2e,
         "stage_ms": {k: round(v, 4) for k, v in stage_ms.items()},
         "dominant_stage": max(stage_ms, key=stage_ms.get),

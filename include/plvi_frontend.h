@@ -246,6 +246,9 @@ int plvi_lines_profile_read(plvi_line_extractor* h, float* stage_ms, int* runs);
  * launch per octave: as plvi_orb_kernel_timing / _read. */
 int plvi_lines_kernel_timing(plvi_line_extractor* h, int enable);
 int plvi_lines_kernel_timing_read(plvi_line_extractor* h, float* total_ms, int* launches);
+/* The same timing per kernel kind: 0 = lsd_prep_kernel, 1 = lbd_sobel0_kernel
+ * (octave-0 5x5 blur + Sobel), 2 = lbd_sobel1_kernel (pyrDown + Sobel). */
+int plvi_lines_kernel_timing_read_kind(plvi_line_extractor* h, int kind, float* total_ms, int* launches);
 
 /* ------------------------------------------------------------------ Hamming
  * ORBmatcher::DescriptorDistance (src/ORBmatcher.cc:2350-2366) over a batch. */
@@ -326,6 +329,29 @@ int plvi_search_by_bow_batch(int n_pairs, float nnratio, int check_orientation, 
                              const uint8_t* d_f_desc, const float* d_f_angle, const int* d_f_n, const int* d_f_node,
                              const int* d_f_off, const int* d_f_nnodes, const int* d_f_idx, int* d_match_kf,
                              int* d_nmatches, void* stream);
+
+/* The same with the two-camera branch of the reference (ORBmatcher.cc:321-420,
+ * F.Nleft != -1: KannalaBrandt8 stereo rigs): keypoints [0, Nleft) are the
+ * left camera's, [Nleft, N) the right one's (mvKeysRight); every KF keypoint
+ * keeps a best / second pair per camera, and when the left best passes
+ * TH_LOW the right best is also taken if it passes TH_LOW (its ratio test is
+ * `|| true` in the reference).  Angles are per keypoint index as the
+ * reference reads them (F: mvKeys for left indices, mvKeysRight[i - Nleft]
+ * for right ones; KF: mvKeysUn without a second camera, else mvKeys /
+ * mvKeysRight).  f_nleft = F.Nleft (-1 = one camera: plvi_search_by_bow);
+ * d_f_nleft [n_pairs] (NULL = all -1). */
+int plvi_search_by_bow_stereo(float nnratio, int check_orientation, const uint8_t* kf_desc, const float* kf_angle,
+                              const uint8_t* kf_live, int kf_n, const int* kf_node, const int* kf_off, int kf_nnodes,
+                              const int* kf_idx, const uint8_t* f_desc, const float* f_angle, int f_n,
+                              const int* f_node, const int* f_off, int f_nnodes, const int* f_idx, int f_nleft,
+                              int* match_kf);
+int plvi_search_by_bow_stereo_batch(int n_pairs, float nnratio, int check_orientation, int kf_cap, int f_cap,
+                                    int node_cap, const uint8_t* d_kf_desc, const float* d_kf_angle,
+                                    const uint8_t* d_kf_live, const int* d_kf_node, const int* d_kf_off,
+                                    const int* d_kf_nnodes, const int* d_kf_idx, const uint8_t* d_f_desc,
+                                    const float* d_f_angle, const int* d_f_n, const int* d_f_node, const int* d_f_off,
+                                    const int* d_f_nnodes, const int* d_f_idx, const int* d_f_nleft, int* d_match_kf,
+                                    int* d_nmatches, void* stream);
 
 /* ------------------------------------------------------------- matchGrid
  * LineMatcher::matchGrid(lines1, desc1, grid, desc2, directions2, w,

@@ -117,8 +117,8 @@ extern "C" int oracle_match(const uint8_t* d1, int n1, const uint8_t* d2, int n2
 }
 
 // ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)
-// (src/ORBmatcher.cc:269-471) + ComputeThreeMaxima (:2304-2345), monocular
-// branch (F.Nleft == -1, no second camera).  The FeatureVectors
+// (src/ORBmatcher.cc:269-471) + ComputeThreeMaxima (:2304-2345), one or two
+// cameras (F.Nleft, oracle_search_by_bow2).  The FeatureVectors
 // (std::map<NodeId, vector<unsigned>>) arrive as CSR arrays sorted by node
 // id; pMP != NULL && !pMP->isBad() arrives as kf_live[realIdxKF].  Output:
 // match_kf[iF] = KF keypoint index whose MapPoint the reference stores in
@@ -132,11 +132,30 @@ static int lower_bound_node(const int* ids, int lo, int hi, int key) {
     return lo;
 }
 
+// f_nleft = F.Nleft: -1 = one camera (:321-342); otherwise the two-camera
+// branch (:343-366, :404-431): keypoints [0, Nleft) left, [Nleft, N) right,
+// a best / second pair per camera, the right best taken (ratio test `|| true`)
+// inside the left best's TH_LOW test.
+extern "C" int oracle_search_by_bow2(const uint8_t* kf_desc, const float* kf_angle, const uint8_t* kf_live,
+                                     const int* kf_node, const int* kf_off, int kf_nnodes, const int* kf_idx,
+                                     const uint8_t* f_desc, const float* f_angle, int f_n, const int* f_node,
+                                     const int* f_off, int f_nnodes, const int* f_idx, float nnratio,
+                                     int check_orientation, int f_nleft, int* match_kf);
+
 extern "C" int oracle_search_by_bow(const uint8_t* kf_desc, const float* kf_angle, const uint8_t* kf_live,
                                     const int* kf_node, const int* kf_off, int kf_nnodes, const int* kf_idx,
                                     const uint8_t* f_desc, const float* f_angle, int f_n, const int* f_node,
                                     const int* f_off, int f_nnodes, const int* f_idx, float nnratio,
                                     int check_orientation, int* match_kf) {
+    return oracle_search_by_bow2(kf_desc, kf_angle, kf_live, kf_node, kf_off, kf_nnodes, kf_idx, f_desc, f_angle, f_n,
+                                 f_node, f_off, f_nnodes, f_idx, nnratio, check_orientation, -1, match_kf);
+}
+
+extern "C" int oracle_search_by_bow2(const uint8_t* kf_desc, const float* kf_angle, const uint8_t* kf_live,
+                                     const int* kf_node, const int* kf_off, int kf_nnodes, const int* kf_idx,
+                                     const uint8_t* f_desc, const float* f_angle, int f_n, const int* f_node,
+                                     const int* f_off, int f_nnodes, const int* f_idx, float nnratio,
+                                     int check_orientation, int f_nleft, int* match_kf) {
     const int TH_LOW = 50, HISTO_LENGTH = 30;
     for (int i = 0; i < f_n; ++i) match_kf[i] = -1;
     std::vector<std::vector<int>> rotHist(HISTO_LENGTH);
@@ -150,29 +169,53 @@ extern "C" int oracle_search_by_bow(const uint8_t* kf_desc, const float* kf_angl
                 if (!kf_live[realIdxKF]) continue;
                 const uint8_t* dKF = kf_desc + (size_t)realIdxKF * 32;
                 int bestDist1 = 256, bestIdxF = -1, bestDist2 = 256;
+                int bestDist1R = 256, bestIdxFR = -1, bestDist2R = 256;
                 for (int b = f_off[Fit]; b < f_off[Fit + 1]; ++b) {
-                    const int realIdxF = f_idx[b];
+                    const unsigned realIdxF = (unsigned)f_idx[b];
                     if (match_kf[realIdxF] >= 0) continue;
                     const int dist = descriptor_distance(dKF, f_desc + (size_t)realIdxF * 32, 24);
-                    if (dist < bestDist1) {
-                        bestDist2 = bestDist1;
-                        bestDist1 = dist;
-                        bestIdxF = realIdxF;
-                    } else if (dist < bestDist2) {
-                        bestDist2 = dist;
+                    if (f_nleft == -1) {
+                        if (dist < bestDist1) {
+                            bestDist2 = bestDist1;
+                            bestDist1 = dist;
+                            bestIdxF = (int)realIdxF;
+                        } else if (dist < bestDist2) {
+                            bestDist2 = dist;
+                        }
+                    } else {
+                        const unsigned nl = (unsigned)f_nleft;
+                        if (realIdxF < nl && dist < bestDist1) {
+                            bestDist2 = bestDist1;
+                            bestDist1 = dist;
+                            bestIdxF = (int)realIdxF;
+                        } else if (realIdxF < nl && dist < bestDist2) {
+                            bestDist2 = dist;
+                        }
+                        if (realIdxF >= nl && dist < bestDist1R) {
+                            bestDist2R = bestDist1R;
+                            bestDist1R = dist;
+                            bestIdxFR = (int)realIdxF;
+                        } else if (realIdxF >= nl && dist < bestDist2R) {
+                            bestDist2R = dist;
+                        }
                     }
                 }
+                auto take = [&](int idx) {
+                    match_kf[idx] = realIdxKF;
+                    if (check_orientation) {
+                        float rot = kf_angle[realIdxKF] - f_angle[idx];
+                        if (rot < 0.0) rot += 360.0f;
+                        int bin = (int)std::round(rot * factor);
+                        if (bin == HISTO_LENGTH) bin = 0;
+                        rotHist[bin].push_back(idx);
+                    }
+                    nmatches++;
+                };
                 if (bestDist1 <= TH_LOW) {
-                    if (static_cast<float>(bestDist1) < nnratio * static_cast<float>(bestDist2)) {
-                        match_kf[bestIdxF] = realIdxKF;
-                        if (check_orientation) {
-                            float rot = kf_angle[realIdxKF] - f_angle[bestIdxF];
-                            if (rot < 0.0) rot += 360.0f;
-                            int bin = (int)std::round(rot * factor);
-                            if (bin == HISTO_LENGTH) bin = 0;
-                            rotHist[bin].push_back(bestIdxF);
-                        }
-                        nmatches++;
+                    if (static_cast<float>(bestDist1) < nnratio * static_cast<float>(bestDist2)) take(bestIdxF);
+                    if (bestDist1R <= TH_LOW) {
+                        (void)bestDist2R;  // `static_cast<float>(bestDist1R) < mfNNratio * ... || true` (:411)
+                        take(bestIdxFR);
                     }
                 }
             }

@@ -1,6 +1,9 @@
 // bow.hip — ORBmatcher::SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&)
-// (src/ORBmatcher.cc:269-471) + ComputeThreeMaxima (:2304-2345), monocular
-// branch (F.Nleft == -1, no second camera), batched over (KF, F) pairs.
+// (src/ORBmatcher.cc:269-471) + ComputeThreeMaxima (:2304-2345), both the
+// single-camera branch (F.Nleft == -1) and the two-camera one (:321-420: a
+// best / second pair per camera, the right camera's match taken -- without
+// its ratio test (`|| true`, :411) -- only when the left best passed TH_LOW,
+// the enclosing `if` of the reference), batched over (KF, F) pairs.
 //
 // The two FeatureVectors (std::map<NodeId, vector<unsigned>>) arrive as CSR
 // arrays sorted by node id.  Each F keypoint lives in exactly one node, so
@@ -44,7 +47,8 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(
     const int* __restrict__ kf_off, const int* __restrict__ kf_nnodes, const int* __restrict__ kf_idx,
     const uint8_t* __restrict__ f_desc, const float* __restrict__ f_angle, const int* __restrict__ f_n,
     const int* __restrict__ f_node, const int* __restrict__ f_off, const int* __restrict__ f_nnodes,
-    const int* __restrict__ f_idx, int* __restrict__ match_kf, int* __restrict__ nmatches) {
+    const int* __restrict__ f_idx, const int* __restrict__ f_nleft, int* __restrict__ match_kf,
+    int* __restrict__ nmatches) {
     extern __shared__ __align__(16) int lds[];
     const int p = blockIdx.x;
     int* s_mk = lds;                                      // [f_cap] matched KF index or -1
@@ -52,6 +56,8 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(
     __shared__ int s_hist[kBowHisto], s_npairs, s_count, s_keep[3];
     const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
     const int nF = f_n[p];
+    // F.Nleft (-1: one camera, every keypoint is "left")
+    const int nLeft = (f_nleft && f_nleft[p] >= 0) ? f_nleft[p] : 0x7fffffff;
     const uint8_t* KD = kf_desc + (size_t)p * kf_cap * 32;
     const float* KA = kf_angle + (size_t)p * kf_cap;
     const uint8_t* KL = kf_live + (size_t)p * kf_cap;
@@ -99,7 +105,7 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(
             if (!KL[realIdxKF]) continue;
             const uint4* dk = reinterpret_cast<const uint4*>(KD + (size_t)realIdxKF * 32);
             const uint4 x0 = dk[0], x1 = dk[1];
-            BowBest bb{256, 0x7fffffff, 256};
+            BowBest bb{256, 0x7fffffff, 256}, br{256, 0x7fffffff, 256};  // left / right camera
             for (int j = lane; j < nfn; j += 64) {
                 const int realIdxF = FI[f0 + j];
                 if (s_mk[realIdxF] >= 0) continue;
@@ -108,12 +114,13 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(
                 const int d = __popc(x0.x ^ y0.x) + __popc(x0.y ^ y0.y) + __popc(x0.z ^ y0.z) + __popc(x0.w ^ y0.w) +
                               __popc(x1.x ^ y1.x) + __popc(x1.y ^ y1.y) + __popc(x1.z ^ y1.z) + __popc(x1.w ^ y1.w);
                 // lane-local scan in list order with the reference's update rule
-                if (d < bb.b1) {
-                    bb.b2 = bb.b1;
-                    bb.b1 = d;
-                    bb.p1 = j;
-                } else if (d < bb.b2) {
-                    bb.b2 = d;
+                BowBest& t = realIdxF < nLeft ? bb : br;
+                if (d < t.b1) {
+                    t.b2 = t.b1;
+                    t.b1 = d;
+                    t.p1 = j;
+                } else if (d < t.b2) {
+                    t.b2 = d;
                 }
             }
             for (int s = 32; s > 0; s >>= 1) {
@@ -122,9 +129,17 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(
                 o.p1 = __shfl_xor(bb.p1, s);
                 o.b2 = __shfl_xor(bb.b2, s);
                 bb = bow_combine(bb, o);
+                if (nLeft != 0x7fffffff) {
+                    o.b1 = __shfl_xor(br.b1, s);
+                    o.p1 = __shfl_xor(br.p1, s);
+                    o.b2 = __shfl_xor(br.b2, s);
+                    br = bow_combine(br, o);
+                }
             }
-            if (bb.b1 <= kBowTHLow && (float)bb.b1 < nnratio * (float)bb.b2) {
-                if (lane == 0) s_mk[FI[f0 + bb.p1]] = realIdxKF;
+            if (bb.b1 <= kBowTHLow && lane == 0) {
+                if ((float)bb.b1 < nnratio * (float)bb.b2) s_mk[FI[f0 + bb.p1]] = realIdxKF;
+                // the right camera's best, inside the left TH_LOW test, no ratio test (:404-430)
+                if (nLeft != 0x7fffffff && br.b1 <= kBowTHLow) s_mk[FI[f0 + br.p1]] = realIdxKF;
             }
             __builtin_amdgcn_wave_barrier();
         }
@@ -192,13 +207,14 @@ static size_t bow_smem(int f_cap, int node_cap) { return (size_t)f_cap * 4 + (si
 
 using namespace plvi;
 
-extern "C" int plvi_search_by_bow_batch(int n_pairs, float nnratio, int check_orientation, int kf_cap, int f_cap,
-                                        int node_cap, const uint8_t* d_kf_desc, const float* d_kf_angle,
-                                        const uint8_t* d_kf_live, const int* d_kf_node, const int* d_kf_off,
-                                        const int* d_kf_nnodes, const int* d_kf_idx, const uint8_t* d_f_desc,
-                                        const float* d_f_angle, const int* d_f_n, const int* d_f_node,
-                                        const int* d_f_off, const int* d_f_nnodes, const int* d_f_idx,
-                                        int* d_match_kf, int* d_nmatches, void* stream) {
+extern "C" int plvi_search_by_bow_stereo_batch(int n_pairs, float nnratio, int check_orientation, int kf_cap,
+                                               int f_cap, int node_cap, const uint8_t* d_kf_desc,
+                                               const float* d_kf_angle, const uint8_t* d_kf_live, const int* d_kf_node,
+                                               const int* d_kf_off, const int* d_kf_nnodes, const int* d_kf_idx,
+                                               const uint8_t* d_f_desc, const float* d_f_angle, const int* d_f_n,
+                                               const int* d_f_node, const int* d_f_off, const int* d_f_nnodes,
+                                               const int* d_f_idx, const int* d_f_nleft, int* d_match_kf,
+                                               int* d_nmatches, void* stream) {
     if (n_pairs < 0 || kf_cap < 1 || f_cap < 1 || node_cap < 1) return PLVI_E_BADARG;
     if (n_pairs == 0) return PLVI_OK;
     const size_t smem = bow_smem(f_cap, node_cap);
@@ -211,17 +227,31 @@ extern "C" int plvi_search_by_bow_batch(int n_pairs, float nnratio, int check_or
     hipLaunchKernelGGL(search_by_bow_kernel, dim3(n_pairs), dim3(256), smem, (hipStream_t)stream, nnratio,
                        check_orientation, kf_cap, f_cap, node_cap, d_kf_desc, d_kf_angle, d_kf_live, d_kf_node,
                        d_kf_off, d_kf_nnodes, d_kf_idx, d_f_desc, d_f_angle, d_f_n, d_f_node, d_f_off, d_f_nnodes,
-                       d_f_idx, d_match_kf, d_nmatches);
+                       d_f_idx, d_f_nleft, d_match_kf, d_nmatches);
     PLVI_CHECK(hipGetLastError());
     return PLVI_OK;
 }
 
+extern "C" int plvi_search_by_bow_batch(int n_pairs, float nnratio, int check_orientation, int kf_cap, int f_cap,
+                                        int node_cap, const uint8_t* d_kf_desc, const float* d_kf_angle,
+                                        const uint8_t* d_kf_live, const int* d_kf_node, const int* d_kf_off,
+                                        const int* d_kf_nnodes, const int* d_kf_idx, const uint8_t* d_f_desc,
+                                        const float* d_f_angle, const int* d_f_n, const int* d_f_node,
+                                        const int* d_f_off, const int* d_f_nnodes, const int* d_f_idx,
+                                        int* d_match_kf, int* d_nmatches, void* stream) {
+    return plvi_search_by_bow_stereo_batch(n_pairs, nnratio, check_orientation, kf_cap, f_cap, node_cap, d_kf_desc,
+                                           d_kf_angle, d_kf_live, d_kf_node, d_kf_off, d_kf_nnodes, d_kf_idx, d_f_desc,
+                                           d_f_angle, d_f_n, d_f_node, d_f_off, d_f_nnodes, d_f_idx, nullptr,
+                                           d_match_kf, d_nmatches, stream);
+}
+
 // Single pair from host memory, synchronous.  Returns nmatches (>= 0) or an error.
-extern "C" int plvi_search_by_bow(float nnratio, int check_orientation, const uint8_t* kf_desc, const float* kf_angle,
-                                  const uint8_t* kf_live, int kf_n, const int* kf_node, const int* kf_off,
-                                  int kf_nnodes, const int* kf_idx, const uint8_t* f_desc, const float* f_angle,
-                                  int f_n, const int* f_node, const int* f_off, int f_nnodes, const int* f_idx,
-                                  int* match_kf) {
+extern "C" int plvi_search_by_bow_stereo(float nnratio, int check_orientation, const uint8_t* kf_desc,
+                                         const float* kf_angle, const uint8_t* kf_live, int kf_n, const int* kf_node,
+                                         const int* kf_off, int kf_nnodes, const int* kf_idx, const uint8_t* f_desc,
+                                         const float* f_angle, int f_n, const int* f_node, const int* f_off,
+                                         int f_nnodes, const int* f_idx, int f_nleft, int* match_kf) {
+    if (f_nleft < -1 || f_nleft > f_n) return PLVI_E_BADARG;
     if (kf_n < 0 || f_n < 0 || kf_nnodes < 0 || f_nnodes < 0) return PLVI_E_BADARG;
     if (f_n == 0) return 0;
     const int kf_cap = std::max(kf_n, 1), f_cap = f_n, node_cap = std::max(std::max(kf_nnodes, f_nnodes), 1);
@@ -239,7 +269,7 @@ extern "C" int plvi_search_by_bow(float nnratio, int check_orientation, const ui
     const size_t oKC = put(&kf_nnodes, 1, 1), oKI = put(kf_idx, nkf_idx, kf_cap);
     const size_t oFN = put(f_node, f_nnodes, node_cap), oFO = put(f_off, f_nnodes + 1, node_cap + 1);
     const size_t oFC = put(&f_nnodes, 1, 1), oFI = put(f_idx, nf_idx, f_cap), oFn = put(&f_n, 1, 1);
-    const size_t oOut = put(nullptr, 0, f_cap), oCnt = put(nullptr, 0, 1);
+    const size_t oOut = put(nullptr, 0, f_cap), oCnt = put(nullptr, 0, 1), oNl = put(&f_nleft, 1, 1);
     const size_t bytes8 = (size_t)(kf_cap + f_cap) * 32 + (size_t)(kf_cap + f_cap) * 4 + (size_t)kf_cap;
     const size_t intOff = (bytes8 + 15) / 16 * 16;
     DevBuf d;
@@ -259,12 +289,22 @@ extern "C" int plvi_search_by_bow(float nnratio, int check_orientation, const ui
     PLVI_CHECK(hipMemcpy(dFD, f_desc, (size_t)f_n * 32, hipMemcpyHostToDevice));
     PLVI_CHECK(hipMemcpy(dFA, f_angle, (size_t)f_n * 4, hipMemcpyHostToDevice));
     PLVI_CHECK(hipMemcpy(dI, ints.data(), ints.size() * 4, hipMemcpyHostToDevice));
-    int rc = plvi_search_by_bow_batch(1, nnratio, check_orientation, kf_cap, f_cap, node_cap, dKD, dKA, dKL,
-                                      dI + oKN, dI + oKO, dI + oKC, dI + oKI, dFD, dFA, dI + oFn, dI + oFN, dI + oFO,
-                                      dI + oFC, dI + oFI, dI + oOut, dI + oCnt, nullptr);
+    int rc = plvi_search_by_bow_stereo_batch(1, nnratio, check_orientation, kf_cap, f_cap, node_cap, dKD, dKA, dKL,
+                                             dI + oKN, dI + oKO, dI + oKC, dI + oKI, dFD, dFA, dI + oFn, dI + oFN,
+                                             dI + oFO, dI + oFC, dI + oFI, dI + oNl, dI + oOut, dI + oCnt, nullptr);
     if (rc) return rc;
     int cnt = 0;
     PLVI_CHECK(hipMemcpy(match_kf, dI + oOut, (size_t)f_n * 4, hipMemcpyDeviceToHost));
     PLVI_CHECK(hipMemcpy(&cnt, dI + oCnt, 4, hipMemcpyDeviceToHost));
     return cnt;
+}
+
+extern "C" int plvi_search_by_bow(float nnratio, int check_orientation, const uint8_t* kf_desc, const float* kf_angle,
+                                  const uint8_t* kf_live, int kf_n, const int* kf_node, const int* kf_off,
+                                  int kf_nnodes, const int* kf_idx, const uint8_t* f_desc, const float* f_angle,
+                                  int f_n, const int* f_node, const int* f_off, int f_nnodes, const int* f_idx,
+                                  int* match_kf) {
+    return plvi_search_by_bow_stereo(nnratio, check_orientation, kf_desc, kf_angle, kf_live, kf_n, kf_node, kf_off,
+                                     kf_nnodes, kf_idx, f_desc, f_angle, f_n, f_node, f_off, f_nnodes, f_idx, -1,
+                                     match_kf);
 }

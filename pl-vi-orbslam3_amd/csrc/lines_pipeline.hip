@@ -100,13 +100,40 @@ struct LinePipeline {
     bool ktime = false;
     int kn = 0;
     std::vector<hipEvent_t> kev;
+    // and around every LBD Gaussian + Sobel launch: [0] lbd_sobel0_kernel, [1] lbd_sobel1_kernel
+    std::vector<hipEvent_t> kevS[2];
+    int knS[2] = {0, 0};
     int ktiming(int on) {
         if (on && kev.empty()) {
             kev.resize(2 * kKRing);
             for (auto& e : kev) PLVI_CHECK(hipEventCreate(&e));
+            for (auto& v : kevS) {
+                v.resize(2 * kKRing);
+                for (auto& e : v) PLVI_CHECK(hipEventCreate(&e));
+            }
         }
         ktime = on != 0;
-        if (on) kn = 0;
+        if (on) kn = knS[0] = knS[1] = 0;
+        return PLVI_OK;
+    }
+    void ktimeS(int k, int edge, hipStream_t st) {  // edge 0 = before, 1 = after launch k
+        if (!ktime || knS[k] >= kKRing) return;
+        (void)hipEventRecord(kevS[k][2 * knS[k] + edge], st);
+        if (edge) ++knS[k];
+    }
+    int ktiming_read_kind(int kind, float* total_ms, int* launches) {
+        if (kind == 0) return ktiming_read(total_ms, launches);
+        if (kind < 1 || kind > 2) return PLVI_E_BADARG;
+        const int k = kind - 1;
+        float tot = 0.f;
+        for (int i = 0; i < knS[k]; ++i) {
+            PLVI_CHECK(hipEventSynchronize(kevS[k][2 * i + 1]));
+            float t = 0.f;
+            PLVI_CHECK(hipEventElapsedTime(&t, kevS[k][2 * i], kevS[k][2 * i + 1]));
+            tot += t;
+        }
+        if (total_ms) *total_ms = tot;
+        if (launches) *launches = knS[k];
         return PLVI_OK;
     }
     int ktiming_read(float* total_ms, int* launches) {
@@ -538,18 +565,22 @@ struct LinePipeline {
             // column strips of at most kLbOutLanes * 4 columns, balanced, multiples of 4
             const int ns = (d0.lw + 4 * kLbOutLanes - 1) / (4 * kLbOutLanes);
             const int sw4 = ((d0.lw + ns - 1) / ns + 3) & ~3;
+            ktimeS(0, 0, st);
             hipLaunchKernelGGL(lbd_sobel0_kernel, dim3((d0.lw + sw4 - 1) / sw4, nf, kLbBands), dim3(64), 0, st, d_frames,
                                frame_stride, row_stride, d0.lw, d0.lh, sw4, lbdBlur.as<uint8_t>(),
                                lbdG.as<short2>() + d0.loff, (size_t)d0.lplane, lbdTaps[0], lbdTaps[1], lbdTaps[2]);
+            ktimeS(0, 1, st);
         }
         for (int l = 1; l < nOct; ++l) {
             const LineOctDev& d = oct[l];
             if (l > 1) return PLVI_E_BADARG;  // pyrDown chain beyond octave 1 not wired (config: 2 levels)
             const int ns = (d.lw + 2 * kLb2OutLanes - 1) / (2 * kLb2OutLanes);
             const int sw2 = ((d.lw + ns - 1) / ns + 1) & ~1;
+            ktimeS(1, 0, st);
             hipLaunchKernelGGL(lbd_sobel1_kernel, dim3((d.lw + sw2 - 1) / sw2, nf), dim3(64), 0, st,
                                (const uint8_t*)lbdBlur.as<uint8_t>(), d0.lw, d0.lh, (size_t)d0.lplane, d.lw, d.lh,
                                sw2, lbdG.as<short2>() + d.loff, (size_t)d.lplane);
+            ktimeS(1, 1, st);
         }
         return PLVI_OK;
     }
@@ -947,4 +978,10 @@ extern "C" int plvi_lines_kernel_timing_read(plvi_line_extractor* h, float* tota
     if (!h) return PLVI_E_BADARG;
     PLVI_CHECK(hipSetDevice(h->p().device));
     return h->p().ktiming_read(total_ms, launches);
+}
+
+extern "C" int plvi_lines_kernel_timing_read_kind(plvi_line_extractor* h, int kind, float* total_ms, int* launches) {
+    if (!h) return PLVI_E_BADARG;
+    PLVI_CHECK(hipSetDevice(h->p().device));
+    return h->p().ktiming_read_kind(kind, total_ms, launches);
 }

@@ -258,8 +258,12 @@ __global__ __launch_bounds__(64 * (kPyrFrames + 1)) void orb_pyramid_kernel(
 #ifndef PLVI_BF_LEAN
 #define PLVI_BF_LEAN 1
 #endif
-#ifndef PLVI_BF_SRING
-#define PLVI_BF_SRING 0
+// PLVI_BF_NMS=1: the per-cell NMS + threshold fallback inside this kernel
+// (bit-exact, but 8.8 vs 6.0 + 2.8 ms per 3072 frames at 3 instead of 8
+// waves per SIMD -- 13 KB of LDS -- and a slower step); the
+// default keeps the score plane + orb_cell_nms_kernel
+#ifndef PLVI_BF_NMS
+#define PLVI_BF_NMS 0
 #endif
 #ifndef PLVI_BF_PK
 #define PLVI_BF_PK 1  // candidates scored two per lane with packed 16-bit min / max (128 per flush)
@@ -269,8 +273,13 @@ constexpr int kBfFlush = PLVI_BF_PK ? 128 : 64;  // candidates scored per flush
 // any ring row are contiguous and a candidate's 17 taps are one base address
 // plus immediate offsets (no per-tap wrap arithmetic)
 constexpr int kRingMirror = PLVI_BF_PK ? 6 : 0;
-constexpr int kBfCols = (244 / kBfAlign) * kBfAlign, kBfRows = 128, kRingRows = PLVI_BF_LEAN ? 16 : 32, kRingW = 256,
+constexpr int kBfCols = 244, kBfRowsMax = 160, kRingRows = PLVI_BF_LEAN ? 16 : 32, kRingW = 256,
               kBfQCap = kBfFlush - 1 + 256 + 1;  // a row adds <= 256 candidates to < kBfFlush queued
+constexpr int kOrbCellsLevelMax = 1280;           // nRows * nCols of a level (LDS of the SAT kernel)
+// fused NMS: scores of the last kSRows output rows, the scored candidates
+// (score >= threshold) awaiting their NMS test as a ring of kNmsCap entries
+constexpr int kSRows = 16, kNmsCap = 1024;
+constexpr unsigned kCellIn = 0x80u, kEdgeHi = 0x40u, kEdgeLo = 0x20u;  // colinf / rowinf bits (low 5: local cell)
 
 // bound_ctrl: the lane past the wave's edge reads 0 without an `old` operand
 // (update_dpp(0, ...) costs a v_mov of the zero per shift)
@@ -396,21 +405,54 @@ __device__ __forceinline__ s16x2 fast_S_ring2(const uint8_t (*rg)[kRingW], int y
     return __builtin_elementwise_max(A, -Bm);
 }
 
+// FAST detection window along one axis (ORBextractor.cc:787-806): cell k
+// starts at minB + k*cell, its window is [start+3, min(start+cell+6, maxB)-3),
+// and cells with start >= maxB - skip do not exist (6 for columns, 3 for
+// rows).  Returns kCellIn | edge bits | (k - k0) for a coordinate inside a
+// window, 0 otherwise.
+__device__ __forceinline__ unsigned orb_cell_axis(int v, int minB, int cell, int n, int maxB, int skip, int k0) {
+    const int r = v - minB - 3;
+    if (r < 0) return 0u;
+    const int k = r / cell;
+    if (k >= n) return 0u;
+    const int start = minB + k * cell;
+    if (start >= maxB - skip) return 0u;
+    const int lo = start + 3, hi = min(start + cell + 6, maxB) - 3;
+    if (v >= hi) return 0u;
+    return kCellIn | ((unsigned)(k - k0) & 31u) | (v == lo ? kEdgeLo : 0u) | (v == hi - 1 ? kEdgeHi : 0u);
+}
+
+// PLVI_BF_NMS (default): the strip also runs K2, the per-cell FAST non-max
+// suppression with the iniThFAST -> minThFAST fallback (ORBextractor.cc:
+// 808-829; cv::FAST's NMS is local to the cell ROI).  Strips are
+// cut at cell boundaries, so a cell's whole detection window is scored by one
+// wave.  Scores go to an LDS ring of the last kSRows output rows instead of a
+// score plane; every scored candidate at or above threshold is queued for its
+// NMS test, which runs once the rows above and below it are final: a
+// candidate survives iff its score beats the raw scores of its 8 neighbours
+// inside the cell's window (a neighbour below threshold is below the
+// candidate anyway, so one test serves both thresholds).  Survivors (score >=
+// min(ini, min)) are written to the candidate plane, which the strip writes
+// densely (zero dwords, then survivors: wave-ordered), and each cell's
+// threshold -- iniThFAST if it has a survivor there, else minThFAST -- goes to
+// the per-frame cell table that the SAT and node-argmax kernels apply.  The
+// score plane, its zero fill and the NMS launch disappear.
 __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __restrict__ lvs,
                                                            const OrbStripDev* __restrict__ strips,
                                                            const uint8_t* __restrict__ frames, size_t f_frame,
                                                            size_t f_row, uint8_t* __restrict__ pyr,
                                                            uint8_t* __restrict__ blur, uint8_t* __restrict__ score,
-                                                           int k0, int k1, int k2, int k3, int tmin, int nstrips,
+                                                           uint8_t* __restrict__ cthr, int thrFrame, int k0, int k1,
+                                                           int k2, int k3, int tmin, int t1, int t2, int nstrips,
                                                            int nf) {
+    static_assert(!PLVI_BF_NMS || PLVI_BF_PK, "the fused NMS queues from the packed scorer");
     typedef typename std::conditional<PLVI_BF_LEAN != 0, unsigned short, unsigned>::type QT;
     __shared__ __align__(16) uint8_t ring[kRingRows + kRingMirror][kRingW];
     __shared__ QT q[kBfQCap];
-#if PLVI_BF_SRING
-    // score rows of the last kRingRows output rows: candidates are scored into
-    // LDS and a row is stored once, complete, when it leaves the window (no
-    // zero-then-candidate double writes of the score plane)
-    __shared__ __align__(16) uint8_t sring[kRingRows][kRingW];
+#if PLVI_BF_NMS
+    __shared__ __align__(16) uint8_t sring[kSRows][kRingW];  // scores (Sv - 1 or 0) of the last kSRows output rows
+    __shared__ QT nmsq[kNmsCap];                              // scored candidates awaiting NMS (ring, row order)
+    __shared__ uint8_t colinf[kRingW], rowinf[kBfRowsMax];
 #endif
     // XCD-affine mapping: blocks b and b + 8 share an XCD (and its L2), so
     // every strip of a frame goes to one XCD and the rows / columns two
@@ -422,24 +464,44 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
     const int lane = threadIdx.x;
     const OrbLevelDev& L = lvs[sd.level];
     const int w = L.w, h = L.h;
-    const int c0 = sd.x0 - 4 + 4 * lane;          // first of this lane's four columns
-    const bool need = lane <= (sd.x1 - sd.x0 + 3) / 4 + 1;  // output lanes and the two halo lanes
-    const bool inner = need && c0 >= 0 && c0 + 4 <= w;     // all four inside the row: one dword
+    const int ax = sd.x0 & ~3;                     // 4-aligned base of the strip's columns
+    const int c0 = ax - 4 + 4 * lane;              // first of this lane's four columns
     const int xe = min(sd.x1, w);
-    const bool outl = lane >= 1 && c0 < xe;        // output lane
-    const int nout = min(4, xe - c0);              // its output columns
+    const bool need = lane <= (xe - ax + 3) / 4 + 1;  // output lanes and the two halo lanes
+    const bool inner = need && c0 >= 0 && c0 + 4 <= w;  // all four inside the row: one dword
+    unsigned omask = 0;                            // this lane's output columns
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (c0 + j >= sd.x0 && c0 + j < xe) omask |= 1u << j;
+    const bool outl = omask != 0u;
     const uint8_t* src = sd.level == 0 ? frames + (size_t)f * f_frame : pyr + L.off + (size_t)f * L.plane;
     const size_t srow = sd.level == 0 ? f_row : (size_t)w;
     uint8_t* Dp = pyr + L.off + (size_t)f * L.plane;
     uint8_t* Bp = blur + L.boff + (size_t)f * L.bplane;
-    uint8_t* Sp = score + L.boff + (size_t)f * L.bplane;
+    uint8_t* Sp = score + L.boff + (size_t)f * L.bplane;  // the candidate plane when PLVI_BF_NMS
     const int bw = L.bpitch;
     const int T = max(tmin + 1, 1);
-    unsigned fastok = 0;  // pixel j may be a FAST candidate (column in [3, w-3), output column)
+    const int y0 = sd.y0, y1 = sd.y1;
+    unsigned fastok = 0;  // pixel j may be a FAST candidate
+#if PLVI_BF_NMS
+    const int maxBX = L.minB + L.rw, maxBY = L.minB + L.rh;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const unsigned ci = orb_cell_axis(c0 + j, L.minB, L.wCell, L.nCols, maxBX, 6, sd.cj0);
+        colinf[4 * lane + j] = (uint8_t)ci;
+        if (((omask >> j) & 1u) && (ci & kCellIn)) fastok |= 1u << j;  // only pixels of a detection window
+    }
+    for (int r = lane; r < y1 - y0; r += 64)
+        rowinf[r] = (uint8_t)orb_cell_axis(y0 + r, L.minB, L.hCell, L.nRows, maxBY, 3, sd.ci0);
+    int nh = 0, nt = 0;             // NMS queue head / tail (wave-uniform)
+    unsigned long long myt1 = 0;    // cells (local index) with a survivor >= iniThFAST
+    int ydone = y0 - 1;             // last output row whose candidates are all queued
+    wave_sync();
+#else
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-        if (outl && j < nout && c0 + j >= 3 && c0 + j < w - 3) fastok |= 1u << j;
-    const int y0 = sd.y0, y1 = sd.y1;
+        if (((omask >> j) & 1u) && c0 + j >= 3 && c0 + j < w - 3) fastok |= 1u << j;
+#endif
     // rows r-6..r as even bytes (columns c0, c0+2) and odd bytes (c0+1, c0+3) in 16-bit fields
     uint32_t pe[7] = {0, 0, 0, 0, 0, 0, 0}, po[7] = {0, 0, 0, 0, 0, 0, 0};
     const uint32_t kt[7] = {(uint32_t)k0, (uint32_t)k1, (uint32_t)k2, (uint32_t)k3,
@@ -448,38 +510,82 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
     int nq = 0;      // queued candidates (wave-uniform)
     int oldest = 0;  // row of the oldest queued candidate
     int ynew = 0;    // row of the newest queued candidate (queue rows are stored modulo 256)
+    auto ent = [&](unsigned e, int yref, int& yy, int& rc) {  // queue entry -> (row, strip column)
+        yy = yref - (int)((((unsigned)yref & 255u) - (e >> 8)) & 255u);
+        rc = (int)(e & 255u);
+    };
+#if PLVI_BF_NMS
+    // NMS of the queued scored candidates in rows <= lim (a prefix: the queue
+    // is in row order); yref >= every queued row
+    auto drain = [&](int lim, int yref) {
+        wave_sync();  // the flush's sring scores
+        while (nt - nh > 0) {
+            const int idx = nh + lane;
+            int yy = 0, rc = 0;
+            if (idx < nt) ent(nmsq[idx & (kNmsCap - 1)], yref, yy, rc);
+            const bool el = idx < nt && yy <= lim;
+            const unsigned long long E = __ballot(el);
+            if (el) {
+                const int rr = yy & (kSRows - 1), ru = (yy - 1) & (kSRows - 1), rd = (yy + 1) & (kSRows - 1);
+                const unsigned ci = colinf[rc], ri = rowinf[yy - y0];
+                const int s = sring[rr][rc];
+                const bool hl = !(ci & kEdgeLo), hr = !(ci & kEdgeHi);
+                int m = max(hl ? (int)sring[rr][rc - 1] : 0, hr ? (int)sring[rr][rc + 1] : 0);
+                if (!(ri & kEdgeLo))
+                    m = max(m, max((int)sring[ru][rc], max(hl ? (int)sring[ru][rc - 1] : 0, hr ? (int)sring[ru][rc + 1] : 0)));
+                if (!(ri & kEdgeHi))
+                    m = max(m, max((int)sring[rd][rc], max(hl ? (int)sring[rd][rc - 1] : 0, hr ? (int)sring[rd][rc + 1] : 0)));
+                if (s > m) {
+                    Sp[(size_t)yy * bw + (ax - 4 + rc)] = (uint8_t)s;  // after the row's zero dword (wave order)
+                    if (s >= t1) myt1 |= 1ull << (((ri & 31u) * (unsigned)sd.ncj + (ci & 31u)) & 63u);
+                }
+            }
+            const int ne = __popcll(E);
+            nh += ne;
+            if (ne < 64) break;
+        }
+    };
+#endif
     auto flush = [&](int n, int ycur) {  // score the first n (<= kBfFlush) queued candidates (ycur: newest queued row)
         // one wave per block: wave-scope ordering only (no store drain).  The
         // candidate bytes below land after this wave's earlier zero stores of
         // the same pixels: a wavefront observes its own memory operations in
         // program order (wavefront-scope acquire/release needs no waits).
         wave_sync();
-        auto put = [&](int yy, int rc, int Sv) {
-#if PLVI_BF_SRING
-            sring[yy & (kRingRows - 1)][rc] = (uint8_t)(Sv >= T ? Sv - 1 : 0);
-#else
-            Sp[(size_t)yy * bw + (sd.x0 - 4 + rc)] = (uint8_t)(Sv >= T ? Sv - 1 : 0);
-#endif
-        };
-        auto ent = [&](unsigned e, int& yy, int& rc) {
-            yy = ycur - (int)((((unsigned)ycur & 255u) - (e >> 8)) & 255u);
-            rc = (int)(e & 255u);
-        };
 #if PLVI_BF_PK
+        int sva = 0, svb = 0;
+        const bool hasb = lane + 64 < n;
         if (lane < n) {
             int ya, ca, yb, cb;
-            ent(q[lane], ya, ca);
-            const bool hasb = lane + 64 < n;
-            ent(q[hasb ? lane + 64 : lane], yb, cb);
+            ent(q[lane], ycur, ya, ca);
+            ent(q[hasb ? lane + 64 : lane], ycur, yb, cb);
             const s16x2 sv2 = fast_S_ring2(ring, ya, ca, yb, cb);
-            put(ya, ca, (int)sv2.x);
-            if (hasb) put(yb, cb, (int)sv2.y);
+            sva = (int)sv2.x;
+            svb = (int)sv2.y;
+#if PLVI_BF_NMS
+            sring[ya & (kSRows - 1)][ca] = (uint8_t)(sva >= T ? sva - 1 : 0);
+            if (hasb) sring[yb & (kSRows - 1)][cb] = (uint8_t)(svb >= T ? svb - 1 : 0);
+#else
+            Sp[(size_t)ya * bw + (ax - 4 + ca)] = (uint8_t)(sva >= T ? sva - 1 : 0);
+            if (hasb) Sp[(size_t)yb * bw + (ax - 4 + cb)] = (uint8_t)(svb >= T ? svb - 1 : 0);
+#endif
         }
+#if PLVI_BF_NMS
+        {
+            // candidates at or above threshold join the NMS queue in queue (= row) order
+            const bool va = lane < n && sva >= T, vb = lane < n && hasb && svb >= T;
+            const unsigned long long Ba = __ballot(va), Bb = __ballot(vb);
+            if (va) nmsq[(nt + orb_mbcnt(Ba)) & (kNmsCap - 1)] = q[lane];
+            if (vb) nmsq[(nt + __popcll(Ba) + orb_mbcnt(Bb)) & (kNmsCap - 1)] = q[lane + 64];
+            nt += __popcll(Ba) + __popcll(Bb);
+        }
+#endif
 #else
         if (lane < n) {
             int yy, rc;
-            ent(q[lane], yy, rc);
-            put(yy, rc, fast_S_ring(ring, yy, rc));
+            ent(q[lane], ycur, yy, rc);
+            const int sv = fast_S_ring(ring, yy, rc);
+            Sp[(size_t)yy * bw + (ax - 4 + rc)] = (uint8_t)(sv >= T ? sv - 1 : 0);
         }
 #endif
         wave_sync();
@@ -495,18 +601,12 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
         nq = rest;
         wave_sync();
         oldest = rest > 0 ? ycur - (int)((((unsigned)ycur & 255u) - ((unsigned)q[0] >> 8)) & 255u) : 0;
-    };
-#if PLVI_BF_SRING
-    auto store_score_row = [&](int yy) {  // LDS score row yy -> score plane (complete dwords)
-        if (outl) {
-            const uint32_t v = *reinterpret_cast<const uint32_t*>(&sring[yy & (kRingRows - 1)][4 * lane]);
-            const uint32_t ob = (uint32_t)(yy * bw + c0);
-            if (nout == 4) st_u32(Sp + ob, v);
-            else
-                for (int j = 0; j < nout; ++j) Sp[ob + j] = (uint8_t)byte_of(v, j);
-        }
-    };
+#if PLVI_BF_NMS
+        // rows before the oldest still-queued candidate are final: an entry
+        // can be tested once the row below it is
+        drain(rest > 0 ? oldest - 2 : ydone - 1, ydone);
 #endif
+    };
     // rows rb..rb+7 of the source (reflected), four columns per lane
     auto load_rows = [&](int rb, uint32_t* pv) {
 #pragma unroll
@@ -530,8 +630,13 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
     load_rows(y0 - 3, pv);
     for (int rb = y0 - 3; rb < y1 + 3; rb += 8) {
         // writing rows rb..rb+7 replaces rows rb-kRingRows..rb-kRingRows+7
-        // of the ring; a queued row yy needs rows yy-3..yy+3
+        // of the ring; a queued row yy needs rows yy-3..yy+3.  (The score ring
+        // zeroes output rows up to rb+4, i.e. rows <= rb+4-kSRows: after this
+        // every queued or NMS-pending row is >= rb-6.)
         if (nq > 0 && oldest - 3 < rb - (kRingRows - 8)) flush(nq, ynew);
+#if PLVI_BF_NMS
+        else if (nq == 0 && nt > nh) drain(ydone - 1, ydone);  // rows without candidates since the last flush
+#endif
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const int rr = (rb + k) & (kRingRows - 1);
@@ -600,27 +705,26 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
                 candm |= ((m & 0xffffu) >= (unsigned)T ? 1u : 0u) << e;
                 candm |= ((m >> 16) >= (unsigned)T ? 4u : 0u) << e;
             }
+#if PLVI_BF_NMS
+            if (!(rowinf[y - y0] & kCellIn)) candm = 0;  // only rows of a detection window
+            *reinterpret_cast<uint32_t*>(&sring[y & (kSRows - 1)][4 * lane]) = 0u;  // scores land by flush
+#else
             if (!(y >= 3 && y < h - 3)) candm = 0;
-            candm &= fastok;
-            bool cand[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) cand[j] = (candm >> j) & 1u;
-#if PLVI_BF_SRING
-            if (y - kRingRows >= y0) store_score_row(y - kRingRows);
-            *reinterpret_cast<uint32_t*>(&sring[y & (kRingRows - 1)][4 * lane]) = 0u;  // candidates land by flush
 #endif
+            candm &= fastok;
             if (outl) {
                 const uint32_t o = (uint32_t)(y * w + c0), ob = (uint32_t)(y * bw + c0);
-                if (nout == 4) {
+                if (omask == 15u) {
                     if (sd.level == 0) st_u32(Dp + o, cvw);
                     st_u32(Bp + ob, Bv);
-                    if (!PLVI_BF_SRING) st_u32(Sp + ob, 0u);  // candidates are overwritten by flush (wave-ordered)
+                    st_u32(Sp + ob, 0u);  // candidates / survivors are overwritten later (wave-ordered)
                 } else {
-                    for (int j = 0; j < nout; ++j) {
-                        if (sd.level == 0) Dp[o + j] = (uint8_t)byte_of(cvw, j);
-                        Bp[ob + j] = (uint8_t)byte_of(Bv, j);
-                        if (!PLVI_BF_SRING) Sp[ob + j] = 0;
-                    }
+                    for (int j = 0; j < 4; ++j)
+                        if ((omask >> j) & 1u) {
+                            if (sd.level == 0) Dp[o + j] = (uint8_t)byte_of(cvw, j);
+                            Bp[ob + j] = (uint8_t)byte_of(Bv, j);
+                            Sp[ob + j] = 0;
+                        }
                 }
             }
             const int nq0 = nq;
@@ -628,7 +732,6 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
             {
                 // lane-major queue order: the lane's candidate count (0..4) as three
                 // ballot bit planes gives every lane its exclusive prefix with mbcnt
-                (void)cand;
                 const unsigned cnt = (unsigned)__popc(candm);
                 const unsigned long long B0 = __ballot(cnt & 1u), B1 = __ballot(cnt & 2u), B2 = __ballot(cnt & 4u);
                 if ((B0 | B1 | B2) != 0ull) {
@@ -643,20 +746,31 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
 #else
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const unsigned long long m = __ballot(cand[j]);
-                if (cand[j]) q[nq + __popcll(m & ((1ull << lane) - 1ull))] = (QT)(((unsigned)y & 255u) << 8 | (unsigned)(4 * lane + j));
+                const bool cj = (candm >> j) & 1u;
+                const unsigned long long m = __ballot(cj);
+                if (cj) q[nq + __popcll(m & ((1ull << lane) - 1ull))] = (QT)(((unsigned)y & 255u) << 8 | (unsigned)(4 * lane + j));
                 nq += __popcll(m);
             }
 #endif
             if (nq0 == 0 && nq > 0) oldest = y;
             if (nq > nq0) ynew = y;
+#if PLVI_BF_NMS
+            ydone = y;
+#endif
             while (nq >= kBfFlush) flush(kBfFlush, ynew);
         }
     }
     while (nq > 0) flush(min(nq, kBfFlush), ynew);
-#if PLVI_BF_SRING
-    wave_sync();
-    for (int yy = max(y0, y1 - kRingRows); yy < y1; ++yy) store_score_row(yy);
+#if PLVI_BF_NMS
+    drain(INT_MAX, ydone);
+    // the strip's cells: iniThFAST where a survivor reached it, else minThFAST
+    unsigned long long m1 = myt1;
+    for (int o = 32; o > 0; o >>= 1) m1 |= __shfl_xor(m1, o);
+    if (lane < sd.ncj * sd.nci) {
+        const int il = lane / sd.ncj, jl = lane - il * sd.ncj;
+        cthr[(size_t)f * thrFrame + L.thrOff + (sd.ci0 + il) * L.nCols + sd.cj0 + jl] =
+            (uint8_t)(((m1 >> lane) & 1ull) ? t1 : t2);
+    }
 #endif
 }
 
@@ -678,6 +792,9 @@ constexpr int kNmsRows = 64;  // >= window height (hCell <= 58, orb_pipeline.hip
 #endif
 #ifndef PLVI_NMS_STREAM
 #define PLVI_NMS_STREAM 1  // rows streamed through registers, no LDS (0: the window staged in LDS)
+#endif
+#ifndef PLVI_NMS_DENSE
+#define PLVI_NMS_DENSE 1  // the NMS writes its whole window (no per-launch zero fill of the candidate plane)
 #endif
 
 __device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, const OrbLevelDev* __restrict__ lvs,
@@ -736,10 +853,16 @@ __device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, co
     const unsigned long long keep = __ballot(ka != 0ull) != 0ull ? ka : kb;
     if (!incol) return;
     uint8_t* C = cand + base;
+#if PLVI_NMS_DENSE
+    // the whole window, zeros included: the candidate plane needs no fill
+    // before the launch (pixels outside every window stay 0 from the init)
+    for (int r = 0; r < wh; ++r) C[(size_t)r * w] = ((keep >> r) & 1ull) ? S[(size_t)r * w] : (uint8_t)0;
+#else
     for (unsigned long long kk = keep; kk; kk &= kk - 1) {
         const int r = __ffsll((long long)kk) - 1;
         C[(size_t)r * w] = S[(size_t)r * w];
     }
+#endif
 #else
     // stage the window column-per-lane (rows beyond wh and lanes beyond ww hold 0)
     for (int r0 = 0; r0 < wh; r0 += 8) {
@@ -858,14 +981,38 @@ constexpr int kSatRowsPerWave = 8;
 // One wave per (strip, level, frame): lane = column, rows top-down, 8 rows'
 // loads in flight; per row a ballot gives the prefix counts (v_mbcnt) and the
 // row total (popcount) without any cross-lane scan; running column sums.
+// Per-cell candidate thresholds (K1b's fallback decision): a candidate byte v
+// counts iff v != 0 and v >= the threshold of its cell, cell (i, j) =
+// ((y - 3) / hCell, (x - 3) / wCell) in region coordinates (clamped: bytes
+// outside every detection window are 0).  The level's table is staged in LDS.
+struct OrbCellThr {
+    __device__ __forceinline__ static void stage(uint8_t* lds, const uint8_t* __restrict__ cthr, int thrFrame, int f,
+                                                 const OrbLevelDev& L) {
+        if (!PLVI_BF_NMS) return;  // the NMS kernel decided: every nonzero byte counts (table of zeros)
+        const uint8_t* g = cthr + (size_t)f * thrFrame + L.thrOff;
+        for (int k = threadIdx.x; k < L.nRows * L.nCols; k += blockDim.x) lds[k] = g[k];
+        __syncthreads();
+    }
+    __device__ __forceinline__ static int row(int yr, const OrbLevelDev& L) {  // cell row of region row yr
+        return yr < 3 ? 0 : min((yr - 3) / L.hCell, L.nRows - 1);
+    }
+    __device__ __forceinline__ static int col(int xr, const OrbLevelDev& L) {
+        return xr < 3 ? 0 : min((xr - 3) / L.wCell, L.nCols - 1);
+    }
+};
+
 __global__ __launch_bounds__(64) void orb_sat_strip_kernel(const OrbLevelDev* __restrict__ lvs,
                                                            const uint8_t* __restrict__ cand,
+                                                           const uint8_t* __restrict__ cthr, int thrFrame,
                                                            unsigned short* __restrict__ lsat, int* __restrict__ carry) {
+    __shared__ uint8_t sthr[PLVI_BF_NMS ? kOrbCellsLevelMax : 1];
     const int s = blockIdx.x, l = blockIdx.y, f = blockIdx.z;
     const OrbLevelDev& L = lvs[l];
     const int nS = L.satStrips;
     if (s >= nS) return;
+    OrbCellThr::stage(sthr, cthr, thrFrame, f, L);
     const int lane = threadIdx.x, x = 64 * s + lane, pitch = 64 * nS;
+    const int cj = OrbCellThr::col(x, L);
     unsigned short* base = lsat + L.satOff + (size_t)f * L.satPlane;
     int* T = carry + L.carryOff + (size_t)f * L.carryPlane;
     const uint8_t* C0 = cand + L.boff + (size_t)f * L.bplane + (size_t)L.minB * L.bpitch + L.minB;
@@ -877,7 +1024,8 @@ __global__ __launch_bounds__(64) void orb_sat_strip_kernel(const OrbLevelDev* __
 #pragma unroll
         for (int k = 0; k < kSatRowsPerWave; ++k) {
             const int y = y0 + k;  // SAT row y counts image row y-1 of the region
-            v[k] = (y <= L.rh && x < L.rw) ? (C0[(size_t)(y - 1) * L.bpitch + x] != 0) : 0;
+            const int c = (y <= L.rh && x < L.rw) ? (int)C0[(size_t)(y - 1) * L.bpitch + x] : 0;
+            v[k] = c != 0 && (!PLVI_BF_NMS || c >= (int)sthr[OrbCellThr::row(y - 1, L) * L.nCols + cj]);
         }
 #pragma unroll
         for (int k = 0; k < kSatRowsPerWave; ++k) {
@@ -905,11 +1053,14 @@ __global__ __launch_bounds__(64) void orb_sat_strip_kernel(const OrbLevelDev* __
 #endif
 __global__ __launch_bounds__(64) void orb_sat_quad_kernel(const OrbLevelDev* __restrict__ lvs,
                                                           const uint8_t* __restrict__ cand,
+                                                          const uint8_t* __restrict__ cthr, int thrFrame,
                                                           unsigned short* __restrict__ lsat, int* __restrict__ carry) {
+    __shared__ uint8_t sthr[PLVI_BF_NMS ? kOrbCellsLevelMax : 1];
     const int w = blockIdx.x, l = blockIdx.y, f = blockIdx.z;
     const OrbLevelDev& L = lvs[l];
     const int nS = L.satStrips;
     if (4 * w >= nS) return;
+    OrbCellThr::stage(sthr, cthr, thrFrame, f, L);
     const int lane = threadIdx.x, g = lane >> 4, s = 4 * w + g, xb = 256 * w + 4 * lane, pitch = 64 * nS;
     const bool live = s < nS;
     unsigned short* base = lsat + L.satOff + (size_t)f * L.satPlane;
@@ -920,6 +1071,11 @@ __global__ __launch_bounds__(64) void orb_sat_quad_kernel(const OrbLevelDev* __r
     const unsigned long long below = ((1ull << lane) - 1ull) & ~((1ull << (16 * g)) - 1ull);
     const unsigned long long group = 0xffffull << (16 * g);
     const bool full = xb + 4 <= L.rw;
+    int cj[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cj[j] = OrbCellThr::col(xb + j, L);
+    uint32_t thr = 0u;  // the four columns' thresholds (bytes) in the current cell row
+    int ci = -1;
     unsigned acc[4] = {0u, 0u, 0u, 0u};
     int tot = 0;
     for (int y0 = 1; y0 <= L.rh; y0 += kSatRowsPerWave) {
@@ -942,8 +1098,17 @@ __global__ __launch_bounds__(64) void orb_sat_quad_kernel(const OrbLevelDev* __r
 #pragma unroll
         for (int k = 0; k < kSatRowsPerWave; ++k) {
             const uint32_t u = v[k];
-            const bool i0 = (u & 0xffu) != 0u, i1 = (u & 0xff00u) != 0u, i2 = (u & 0xff0000u) != 0u,
-                       i3 = (u & 0xff000000u) != 0u;
+            const int cr = PLVI_BF_NMS ? OrbCellThr::row(y0 + k - 1, L) : 0;  // wave-uniform
+            if (PLVI_BF_NMS && cr != ci) {
+                ci = cr;
+                const uint8_t* tr = sthr + ci * L.nCols;
+                thr = (uint32_t)tr[cj[0]] | (uint32_t)tr[cj[1]] << 8 | (uint32_t)tr[cj[2]] << 16 |
+                      (uint32_t)tr[cj[3]] << 24;
+            }
+            const bool i0 = (u & 0xffu) != 0u && (u & 0xffu) >= (thr & 0xffu);
+            const bool i1 = (u & 0xff00u) != 0u && (u & 0xff00u) >= (thr & 0xff00u);
+            const bool i2 = (u & 0xff0000u) != 0u && (u & 0xff0000u) >= (thr & 0xff0000u);
+            const bool i3 = (u & 0xff000000u) != 0u && (u & 0xff000000u) >= (thr & 0xff000000u);
             const unsigned long long m0 = __ballot(i0), m1 = __ballot(i1), m2 = __ballot(i2), m3 = __ballot(i3);
             const unsigned cb = (unsigned)(__popcll(m0 & below) + __popcll(m1 & below) + __popcll(m2 & below) +
                                            __popcll(m3 & below));
@@ -1216,6 +1381,7 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void orb_node_best_kernel(const OrbLevelDev* __restrict__ lvs,
                                                            const uint8_t* __restrict__ cand,
+                                                           const uint8_t* __restrict__ cthr, int thrFrame,
                                                            const short4* __restrict__ rects,
                                                            const int* __restrict__ rect_cnt, int nodeCapMax, int L,
                                                            float4* __restrict__ lvkp, int kpCapFrame) {
@@ -1235,6 +1401,8 @@ __global__ __launch_bounds__(64) void orb_node_best_kernel(const OrbLevelDev* __
         const int resp = Cm[(size_t)(lv.minB + yy) * lv.bpitch + lv.minB + xx];
         if (!resp) continue;
         const unsigned ci = (unsigned)(yy - 3) / (unsigned)lv.hCell, cj = (unsigned)(xx - 3) / (unsigned)lv.wCell;
+        if (PLVI_BF_NMS && resp < (int)cthr[(size_t)f * thrFrame + lv.thrOff + ci * (unsigned)lv.nCols + cj])
+            continue;  // the cell's fallback threshold (fused NMS)
         const unsigned key = ((ci * (unsigned)lv.nCols + cj) * (unsigned)lv.rh + (unsigned)yy) * (unsigned)lv.rw + (unsigned)xx;
         const unsigned long long pk = ((unsigned long long)resp << 32) | (0xFFFFFFFFu - key);
         best = pk > best ? pk : best;

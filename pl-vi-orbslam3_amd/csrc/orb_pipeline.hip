@@ -41,6 +41,41 @@ static int append_xtab(std::vector<uint32_t>& tab, int sw, int dw) {
     return PLVI_OK;
 }
 
+// Split [0, n) into the fewest pieces whose interior cuts are taken from
+// `cand` (ascending) and that all satisfy fits(a, b), as even as possible:
+// the smallest piece-length bound for which the greedy cut still needs no
+// more pieces.  out = {0, cuts..., n}.
+template <class Fits>
+static int plan_splits(int n, const std::vector<int>& cand, Fits fits, std::vector<int>& out) {
+    auto greedy = [&](int bound, std::vector<int>& o) {
+        o.assign(1, 0);
+        int a = 0;
+        while (a < n) {
+            int b = -1;
+            if (fits(a, n) && n - a <= bound) b = n;
+            else
+                for (int c : cand)
+                    if (c > a && fits(a, c) && c - a <= bound) b = c;
+            if (b < 0) return false;
+            o.push_back(b);
+            a = b;
+        }
+        return true;
+    };
+    std::vector<int> best;
+    if (!greedy(n, best)) return PLVI_E_BADARG;
+    const size_t k = best.size();
+    int lo = 1, hi = n;  // smallest bound with <= k pieces
+    while (lo < hi) {
+        const int mid = (lo + hi) / 2;
+        std::vector<int> t;
+        if (greedy(mid, t) && t.size() <= k) hi = mid;
+        else lo = mid + 1;
+    }
+    if (!greedy(lo, out)) out = best;
+    return PLVI_OK;
+}
+
 struct OrbPipeline {
     plvi_orb_params prm{};
     int W = 0, H = 0, Bcap = 0, device = 0, L = 0;
@@ -54,9 +89,10 @@ struct OrbPipeline {
     int resizeGeneric = 0;  // A.1 vertical-pass switch (PLVI_COMPAT_RESIZE_V_GENERIC)
     int kpCapFrame = 0, nodeCapMax = 0;
     size_t pyrBytesFrameTotal = 0, candBytesTotal = 0, satIntsFrameTotal = 0;
+    int thrFrame = 0;  // bytes of cell thresholds per frame (all levels)
     size_t lvOff0 = 0;  // (unused)
-    DevBuf d_lv, d_cells, d_strips, d_xtab, pyr, blur, score, cand, sat, carry, rects, rectCnt, lvkp, lvdesc, okp, odesc, ocount,
-        omono, err, staging;
+    DevBuf d_lv, d_cells, d_strips, d_xtab, pyr, blur, score, cand, cthr, sat, carry, rects, rectCnt, lvkp, lvdesc, okp,
+        odesc, ocount, omono, err, staging;
     size_t pyrSmem = 0;  // orb_pyramid_kernel LDS: column table + source-level row rings
     int xtabN = 0, pyrFrameLds = 0;
     int lastFrames = 0;
@@ -274,17 +310,39 @@ struct OrbPipeline {
                 // LDS: a kPyrRing-row ring of level 0, two rows of every other source level
                 pyrSmem += (l == 1 ? kPyrRing : 2) * (size_t)((lv[l - 1].w + 3) & ~3);
             }
-            // strips of the blur + FAST kernel: columns split into kBfAlign-aligned
-            // strips of <= kBfCols, rows split evenly (<= kBfRows rows)
+            // strips of the blur + FAST (+ NMS) kernel, cut at cell boundaries so
+            // that every FAST detection window lies inside one strip: the valid
+            // cell columns / rows are a prefix of the grid (:796, :801 skip the rest)
             {
-                const int ncs = (d.w + kBfCols - 1) / kBfCols, nrs = (d.h + kBfRows - 1) / kBfRows;
-                const int cols = ((d.w + ncs - 1) / ncs + kBfAlign - 1) / kBfAlign * kBfAlign;
-                const int rows = (d.h + nrs - 1) / nrs;
-                if (cols > kBfCols) return PLVI_E_BADARG;
-                for (int y0 = 0; y0 < d.h; y0 += rows)
-                    for (int x0 = 0; x0 < d.w; x0 += cols)
-                        strips.push_back(OrbStripDev{l, x0, std::min(x0 + cols, d.w), y0, std::min(y0 + rows, d.h)});
+                int ncv = 0, nrv = 0;
+                for (int j = 0; j < d.nCols && d.minB + j * d.wCell < maxBX - 6; ++j) ncv = j + 1;
+                for (int i = 0; i < d.nRows && d.minB + i * d.hCell < maxBY - 3; ++i) nrv = i + 1;
+                std::vector<int> cx, cy;  // interior split candidates: window starts of cells 1..
+                for (int j = 1; j < ncv; ++j) cx.push_back(d.minB + j * d.wCell + 3);
+                for (int i = 1; i < nrv; ++i) cy.push_back(d.minB + i * d.hCell + 3);
+                std::vector<int> sx, sy;
+                if (plan_splits(d.w, cx, [](int a, int b) { return b - (a & ~3) <= kBfCols; }, sx) ||
+                    plan_splits(d.h, cy, [](int a, int b) { return b - a <= kBfRowsMax; }, sy))
+                    return PLVI_E_BADARG;
+                auto first_cell = [](int a, int n, int base, int step) {  // first cell index whose window starts >= a
+                    int k = 0;
+                    while (k < n && base + k * step + 3 < a) ++k;
+                    return k;
+                };
+                for (size_t ri = 0; ri + 1 < sy.size(); ++ri)
+                    for (size_t ci = 0; ci + 1 < sx.size(); ++ci) {
+                        OrbStripDev sd{l, sx[ci], sx[ci + 1], sy[ri], sy[ri + 1], 0, 0, 0, 0};
+                        sd.cj0 = first_cell(sd.x0, ncv, d.minB, d.wCell);
+                        sd.ncj = first_cell(sd.x1, ncv, d.minB, d.wCell) - sd.cj0;
+                        sd.ci0 = first_cell(sd.y0, nrv, d.minB, d.hCell);
+                        sd.nci = first_cell(sd.y1, nrv, d.minB, d.hCell) - sd.ci0;
+                        if (sd.ncj * sd.nci > 64) return PLVI_E_BADARG;
+                        strips.push_back(sd);
+                    }
             }
+            d.thrOff = thrFrame;
+            thrFrame += d.nRows * d.nCols;
+            if (d.nRows * d.nCols > kOrbCellsLevelMax) return PLVI_E_BADARG;
         }
         kpCapFrame = kpOff;
         pyrBytesFrameTotal = off;
@@ -306,7 +364,9 @@ struct OrbPipeline {
         PLVI_CHECK(hipMemcpy(d_xtab.p, xtab.data(), 4 * xtab.size(), hipMemcpyHostToDevice));
         PLVI_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax.data(), 16 * sizeof(int)));
         // work buffers
-        if (pyr.alloc(off) || blur.alloc(boffAll) || score.alloc(boffAll) || cand.alloc(boffAll) ||
+        // the score plane exists only without the fused NMS (PLVI_BF_NMS=0)
+        if (pyr.alloc(off) || blur.alloc(boffAll) || (!PLVI_BF_NMS && score.alloc(boffAll)) || cand.alloc(boffAll) ||
+            cthr.alloc((size_t)std::max(thrFrame, 1) * Bcap) ||
             sat.alloc(satOff * sizeof(unsigned short)) || carry.alloc(carryOff * sizeof(int)) || rects.alloc(sizeof(short4) * (size_t)nodeCapMax * L * Bcap) ||
             rectCnt.alloc(sizeof(int) * L * Bcap) || lvkp.alloc(sizeof(float4) * (size_t)kpCapFrame * Bcap) ||
             lvdesc.alloc((size_t)32 * kpCapFrame * Bcap) || okp.alloc(sizeof(plvi_keypoint) * (size_t)kpCapFrame * Bcap) ||
@@ -314,6 +374,10 @@ struct OrbPipeline {
             omono.alloc(sizeof(int) * Bcap) || err.alloc(sizeof(int) * Bcap) || staging.alloc((size_t)W * H))
             return PLVI_E_HIP;
         PLVI_CHECK(hipMemset(err.p, 0, sizeof(int) * Bcap));
+        // cell thresholds: written by every blur + FAST (+ NMS) launch; all 0
+        // (no per-cell filtering: the NMS kernel decides) with PLVI_BF_NMS=0
+        PLVI_CHECK(hipMemset(cthr.p, 0, cthr.bytes));
+        PLVI_CHECK(hipMemset(cand.p, 0, cand.bytes));  // outside the detection windows it stays 0
         return PLVI_OK;
     }
 
@@ -327,8 +391,9 @@ struct OrbPipeline {
         const int t1 = std::max(0, std::min(prm.ini_th_fast, 255)), t2 = std::max(0, std::min(prm.min_th_fast, 255));
         uint8_t* P = pyr.as<uint8_t>();
         uint8_t* Bl = blur.as<uint8_t>();
-        uint8_t* Sc = score.as<uint8_t>();
         uint8_t* Cd = cand.as<uint8_t>();
+        uint8_t* Sc = PLVI_BF_NMS ? Cd : score.as<uint8_t>();  // the fused kernel writes the candidate plane
+        uint8_t* Ct = cthr.as<uint8_t>();
         mark(0, st);
         auto hook = [&](int k, hipStream_t s_) {
             if (evAfterBlur && gateStage == k) PLVI_CHECK(hipEventRecord(evAfterBlur, s_));
@@ -347,18 +412,24 @@ struct OrbPipeline {
         if (kt) PLVI_CHECK(hipEventRecord(kev[2 * kn], st));
         hipLaunchKernelGGL(orb_blur_fast_kernel, dim3((unsigned)(strips.size() * 8 * ((nf + 7) / 8))), dim3(64), 0, st,
                            d_lv.as<OrbLevelDev>(), d_strips.as<OrbStripDev>(), d_frames, frame_stride, row_stride, P,
-                           Bl, Sc, taps[0], taps[1], taps[2], taps[3], tmin, (int)strips.size(), nf);
+                           Bl, Sc, Ct, thrFrame, taps[0], taps[1], taps[2], taps[3], tmin, t1, t2, (int)strips.size(),
+                           nf);
         if (kt) {
             PLVI_CHECK(hipEventRecord(kev[2 * kn + 1], st));
             ++kn;
         }
         if (const int hrc = hook(1, st)) return hrc;
         mark(1, st);
-        // K2 cell NMS -> candidate map (zeroed first: only detection windows are written)
-        PLVI_CHECK(hipMemsetAsync(Cd, 0, candBytesTotal, st));
-        hipLaunchKernelGGL(orb_cell_nms_kernel, dim3((unsigned)((cells.size() + kNmsCells - 1) / kNmsCells), nf),
-                           dim3(64), 0, st, d_cells.as<OrbCellDev>(), (int)cells.size(), d_lv.as<OrbLevelDev>(),
-                           (const uint8_t*)Sc, Cd, t1, t2);
+        if (!PLVI_BF_NMS) {
+            // K2 cell NMS -> candidate map.  PLVI_NMS_DENSE: every detection
+            // window is written whole and the rest of the plane stays 0 from
+            // the init; otherwise only survivors are written, on a zeroed plane
+            if (!PLVI_NMS_DENSE || !(PLVI_NMS_MAXONLY && PLVI_NMS_STREAM))
+                PLVI_CHECK(hipMemsetAsync(Cd, 0, candBytesTotal, st));
+            hipLaunchKernelGGL(orb_cell_nms_kernel, dim3((unsigned)((cells.size() + kNmsCells - 1) / kNmsCells), nf),
+                               dim3(64), 0, st, d_cells.as<OrbCellDev>(), (int)cells.size(), d_lv.as<OrbLevelDev>(),
+                               (const uint8_t*)Sc, Cd, t1, t2);
+        }
         mark(2, st);
         if (const int hrc = hook(2, st)) return hrc;
         // K3 SAT
@@ -366,10 +437,12 @@ struct OrbPipeline {
         for (auto& d : lv) { maxRh = std::max(maxRh, d.rh); maxStrips = std::max(maxStrips, d.satStrips); }
         if (PLVI_SAT_QUAD)
             hipLaunchKernelGGL(orb_sat_quad_kernel, dim3((maxStrips + 3) / 4, L, nf), dim3(64), 0, st,
-                               d_lv.as<OrbLevelDev>(), (const uint8_t*)Cd, sat.as<unsigned short>(), carry.as<int>());
+                               d_lv.as<OrbLevelDev>(), (const uint8_t*)Cd, (const uint8_t*)Ct, thrFrame,
+                               sat.as<unsigned short>(), carry.as<int>());
         else
             hipLaunchKernelGGL(orb_sat_strip_kernel, dim3(maxStrips, L, nf), dim3(64), 0, st, d_lv.as<OrbLevelDev>(),
-                               (const uint8_t*)Cd, sat.as<unsigned short>(), carry.as<int>());
+                               (const uint8_t*)Cd, (const uint8_t*)Ct, thrFrame, sat.as<unsigned short>(),
+                               carry.as<int>());
         hipLaunchKernelGGL(orb_sat_carry_kernel, dim3((maxRh + 1 + 255) / 256, L, nf), dim3(256), 0, st,
                            d_lv.as<OrbLevelDev>(), carry.as<int>());
         mark(3, st);
@@ -384,7 +457,7 @@ struct OrbPipeline {
         if (const int hrc = hook(4, st)) return hrc;
         // K5 best per node
         hipLaunchKernelGGL(orb_node_best_kernel, dim3(nodeCapMax, L, nf), dim3(64), 0, st, d_lv.as<OrbLevelDev>(),
-                           (const uint8_t*)Cd, (const short4*)rects.as<short4>(), (const int*)rectCnt.as<int>(),
+                           (const uint8_t*)Cd, (const uint8_t*)Ct, thrFrame, (const short4*)rects.as<short4>(), (const int*)rectCnt.as<int>(),
                            nodeCapMax, L, lvkp.as<float4>(), kpCapFrame);
         mark(5, st);
         if (const int hrc = hook(5, st)) return hrc;

@@ -179,6 +179,7 @@ def _declare(lib):
         "plvi_lines_errors": ([V, V, P, V], I),
         "plvi_lines_kernel_timing": ([V, I], I),
         "plvi_lines_kernel_timing_read": ([V, V, P], I),
+        "plvi_lines_kernel_timing_read_kind": ([V, I, V, P], I),
         "plvi_line_match_nnr_inout": ([V, I, V, I, F, V, I], I),
         "plvi_line_match_inout": ([V, I, V, I, F, V, I], I),
         "plvi_orb_pyramid_level": ([V, I, I, V, P, P], I),
@@ -209,6 +210,9 @@ def _declare(lib):
         "plvi_lines_debug_sobel": ([V, I, I, V, P, P], I),
         "plvi_descriptor_distance_batch": ([V, V, I, I, V, V], I),
         "plvi_search_by_bow": ([F, I, V, V, V, I, V, V, I, V, V, V, I, V, V, I, V, V], I),
+        "plvi_search_by_bow_stereo": ([F, I, V, V, V, I, V, V, I, V, V, V, I, V, V, I, V, I, V], I),
+        "plvi_search_by_bow_stereo_batch": ([I, F, I, I, I, I, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V,
+                                             V], I),
         "plvi_search_by_bow_batch": ([I, F, I, I, I, I, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V, V], I),
         "plvi_line_match_grid": ([V, V, I, I, I, V, V, V, V, I, I, I, I, I, I, V], I),
         "plvi_line_match_grid_batch": ([I, V, V, V, I, I, I, V, V, I, V, V, V, I, I, I, I, I, I, V, V, V, V], I),
@@ -597,14 +601,16 @@ class Lineextractor:
         return dict(zip(self.STAGES, ms.tolist())), runs.value
 
     def kernel_timing(self, enable=True):
-        """Event pair around every lsd_prep_kernel launch (LSD-pass roofline)."""
+        """Event pair around every lsd_prep_kernel and LBD Gaussian + Sobel launch (rooflines)."""
         _check(self._lib.plvi_lines_kernel_timing(self._h, int(enable)), "plvi_lines_kernel_timing")
 
-    def kernel_timing_read(self):
+    def kernel_timing_read(self, kind=0):
+        """(total ms, launches) since kernel_timing(True): kind 0 = lsd_prep_kernel, 1 = lbd_sobel0_kernel,
+        2 = lbd_sobel1_kernel."""
         tot = ctypes.c_float()
         n = ctypes.c_int()
-        _check(self._lib.plvi_lines_kernel_timing_read(self._h, ctypes.byref(tot), ctypes.byref(n)),
-               "plvi_lines_kernel_timing_read")
+        _check(self._lib.plvi_lines_kernel_timing_read_kind(self._h, int(kind), ctypes.byref(tot), ctypes.byref(n)),
+               "plvi_lines_kernel_timing_read_kind")
         return tot.value, n.value
 
     def pyramid_level(self, level, frame=0):
@@ -755,9 +761,10 @@ class ORBmatcher:
         self.nnratio = float(nnratio)
         self.check_orientation = bool(checkOri)
 
-    def SearchByBoW(self, kf_desc, kf_angle, kf_live, kf_featvec, f_desc, f_angle, f_featvec):
-        """SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&) (src/ORBmatcher.cc:269-471).
-        Returns (nmatches, match_kf) with match_kf[iF] = KF keypoint index or -1."""
+    def SearchByBoW(self, kf_desc, kf_angle, kf_live, kf_featvec, f_desc, f_angle, f_featvec, f_nleft=-1):
+        """SearchByBoW(KeyFrame*, Frame&, vector<MapPoint*>&) (src/ORBmatcher.cc:269-471); f_nleft = F.Nleft
+        (-1: one camera; else the two-camera branch, :321-420).  Returns (nmatches, match_kf) with
+        match_kf[iF] = KF keypoint index or -1."""
         kd = np.ascontiguousarray(kf_desc, np.uint8)
         ka = np.ascontiguousarray(kf_angle, np.float32)
         kl = np.ascontiguousarray(kf_live, np.uint8)
@@ -766,10 +773,11 @@ class ORBmatcher:
         kn, ko, ki = feature_vector_csr(kf_featvec)
         fn, fo, fi = feature_vector_csr(f_featvec)
         out = np.full(max(len(fd), 1), -1, np.int32)
-        n = _check(self._lib.plvi_search_by_bow(self.nnratio, int(self.check_orientation), _ptr(kd), _ptr(ka),
-                                                _ptr(kl), len(kd), _ptr(kn), _ptr(ko), len(kn), _ptr(ki), _ptr(fd),
-                                                _ptr(fa), len(fd), _ptr(fn), _ptr(fo), len(fn), _ptr(fi), _ptr(out)),
-                   "plvi_search_by_bow")
+        n = _check(self._lib.plvi_search_by_bow_stereo(self.nnratio, int(self.check_orientation), _ptr(kd),
+                                                       _ptr(ka), _ptr(kl), len(kd), _ptr(kn), _ptr(ko), len(kn),
+                                                       _ptr(ki), _ptr(fd), _ptr(fa), len(fd), _ptr(fn), _ptr(fo),
+                                                       len(fn), _ptr(fi), int(f_nleft), _ptr(out)),
+                   "plvi_search_by_bow_stereo")
         return n, out[:len(fd)]
 
     def SearchByProjection(self, params, cur_kps, cur_desc, last_x3dc, last_octave, last_angle, mp_desc,

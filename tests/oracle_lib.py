@@ -282,8 +282,9 @@ def line_iterator_count(W, H, x1, y1, x2, y2):
     return lib.oracle_line_iterator_count(W, H, x1, y1, x2, y2)
 
 
-def search_by_bow(kf_desc, kf_angle, kf_live, kf_fv, f_desc, f_angle, f_fv, nnratio, check_orientation=True):
-    """ORBmatcher::SearchByBoW restatement; fv = dict {node: [indices]}."""
+def search_by_bow(kf_desc, kf_angle, kf_live, kf_fv, f_desc, f_angle, f_fv, nnratio, check_orientation=True,
+                  f_nleft=-1):
+    """ORBmatcher::SearchByBoW restatement; fv = dict {node: [indices]}; f_nleft = F.Nleft (-1: one camera)."""
     lib = load()
     def csr(fv):
         nodes = np.array(sorted(fv), dtype=np.int32)
@@ -299,8 +300,12 @@ def search_by_bow(kf_desc, kf_angle, kf_live, kf_fv, f_desc, f_angle, f_fv, nnra
     kl = np.ascontiguousarray(kf_live, np.uint8); fd = np.ascontiguousarray(f_desc, np.uint8)
     fa = np.ascontiguousarray(f_angle, np.float32)
     out = np.full(max(len(fd), 1), -1, np.int32)
-    n = lib.oracle_search_by_bow(_p(kd), _p(ka), _p(kl), _p(kn), _p(ko), len(kn), _p(ki), _p(fd), _p(fa), len(fd),
-                                 _p(fn), _p(fo), len(fn), _p(fi), float(nnratio), int(check_orientation), _p(out))
+    V, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    lib.oracle_search_by_bow2.argtypes = [V, V, V, V, V, I, V, V, V, I, V, V, I, V, F, I, I, V]
+    lib.oracle_search_by_bow2.restype = I
+    n = lib.oracle_search_by_bow2(_p(kd), _p(ka), _p(kl), _p(kn), _p(ko), len(kn), _p(ki), _p(fd), _p(fa), len(fd),
+                                  _p(fn), _p(fo), len(fn), _p(fi), float(nnratio), int(check_orientation),
+                                  int(f_nleft), _p(out))
     return n, out[:len(fd)]
 
 

@@ -62,3 +62,13 @@ def test_committed_traffic_is_calibrated_and_near_algorithmic():
     assert 1.0 <= t / alg < 1.3  # measured 1.20
     assert 1.0 <= t / (b.blur_fast_bytes(640, 480) * 3072) < 1.45  # vs the SURVEY model: 1.36
     assert b.committed_traffic(3071, "orb_blur_fast_kernel") is None
+
+
+def test_lbd_sobel_bytes_split_survey_lbd_total():
+    b = _bench()
+    # LBD blur/pyrDown 998 400 + Sobel 1 920 000 = 2 918 400 B/frame,
+    # split over the two kernels that materialise them (roofline_lbd)
+    s0, s1 = b.lbd_sobel_bytes(640, 480)
+    assert s0 == 2 * 307_200 + 5 * 307_200 == 2_150_400  # blur r+w, Sobel u8 in + 2 x int16 out
+    assert s1 == 307_200 + 76_800 + 5 * 76_800 == 768_000  # pyrDown r+w, Sobel of octave 1
+    assert s0 + s1 == 2_918_400 == 998_400 + 1_920_000

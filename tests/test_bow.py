@@ -42,6 +42,31 @@ def test_oracle_search_by_bow_known_answers():
     assert n2 == 2 and (m2 == m).all()
 
 
+def test_oracle_search_by_bow_two_cameras_known_answers():
+    """The two-camera branch (ORBmatcher.cc:321-420, F.Nleft != -1): a best / second pair per camera; the right
+    best is taken without a ratio test, but only inside the left best's TH_LOW test."""
+    rng = np.random.default_rng(9)
+    kf = _desc(rng, 3)
+    # F: left keypoints 0..2, right keypoints 3..5 (Nleft = 3)
+    f = np.stack([_flip(kf[0], 10, rng), _flip(kf[0], 11, rng), _flip(kf[1], 8, rng),    # left
+                  _flip(kf[0], 20, rng), _flip(kf[1], 90, rng), _flip(kf[2], 4, rng)])   # right
+    kf_angle = np.zeros(3, np.float32)
+    f_angle = np.zeros(6, np.float32)
+    live = np.ones(3, np.uint8)
+    kf_fv = {5: [0, 1, 2]}
+    f_fv = {5: [0, 1, 2, 3, 4, 5]}
+    n, m = oracle_lib.search_by_bow(kf, kf_angle, live, kf_fv, f, f_angle, f_fv, 0.75, check_orientation=False,
+                                    f_nleft=3)
+    # KF0: left best F0 (10) fails the ratio vs F1 (11), yet its right best F3 (20 <= 50) is taken (`|| true`).
+    # KF1: left best F2 (8) passes; its right side holds only F4 (~90 > TH_LOW): left only.
+    # KF2: no left candidate within TH_LOW (F1 ~ random vs KF2) -> its right best F5 (4 bits) is NOT taken.
+    assert list(m) == [-1, -1, 1, 0, -1, -1]
+    assert n == 2
+    # one camera (Nleft = -1): all six compete; KF0 -> F0 (10 < 0.75 * 11 fails) ... the same rule as before
+    n1, m1 = oracle_lib.search_by_bow(kf, kf_angle, live, kf_fv, f, f_angle, f_fv, 0.75, check_orientation=False)
+    assert m1[3] == -1 and m1[5] == 2
+
+
 def test_oracle_descriptor_distance_quirk():
     lib = oracle_lib.load()
     a = np.zeros(32, np.uint8)
@@ -65,6 +90,20 @@ def test_search_by_bow_matches_oracle(seed, nnratio, ori):
     assert n == n_ref
     np.testing.assert_array_equal(m, m_ref)
     assert n_ref > 50  # the synthetic case does exercise matching
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(4))
+@pytest.mark.parametrize("nleft_frac,ori", [(0.5, True), (0.3, False), (1.0, True), (0.0, True)])
+def test_search_by_bow_two_cameras_matches_oracle(seed, nleft_frac, ori):
+    import plvi
+    case = util.bow_case(40 + seed, n_kf=600 + 29 * seed, n_f=900 + 17 * seed, dup=0.8)
+    nleft = int(nleft_frac * len(case[4]))
+    n_ref, m_ref = oracle_lib.search_by_bow(*case, 0.75, ori, f_nleft=nleft)
+    n, m = plvi.ORBmatcher(0.75, ori).SearchByBoW(*case, f_nleft=nleft)
+    assert n == n_ref
+    np.testing.assert_array_equal(m, m_ref)
+    assert n_ref > 30
 
 
 @pytest.mark.gpu
