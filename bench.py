@@ -457,7 +457,7 @@ def main():
     ap.add_argument("--no-check", action="store_true", help="skip the oracle check of the timed batch")
     ap.add_argument("--no-extra", action="store_true", help="skip the batch-64 / latency / H2D lines")
     ap.add_argument("--no-side", action="store_true", help="skip the BoW / projection / stereo stage timings")
-    ap.add_argument("--inflight", type=int, default=1,
+    ap.add_argument("--inflight", type=int, default=2,
                     help="batches in flight: consecutive steps alternate over this many extractor/stream slots, "
                          "so one batch's ORB tail overlaps the next batch's LSD front")
     args = ap.parse_args()

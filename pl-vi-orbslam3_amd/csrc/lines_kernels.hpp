@@ -947,6 +947,9 @@ __device__ inline int line_iter_count(int W, int H, float fx1, float fy1, float 
 }
 
 constexpr int kKlCap = 4096;  // keylines per frame before the top-k filter
+#ifndef PLVI_TIE_SERIAL
+#define PLVI_TIE_SERIAL 0
+#endif
 
 __global__ __launch_bounds__(256) void line_assemble_kernel(const LineOctDev* __restrict__ octs, int nOct,
                                                             const LsdLine* __restrict__ lines,
@@ -1060,9 +1063,18 @@ __global__ __launch_bounds__(256) void line_assemble_kernel(const LineOctDev* __
         bool tie = false;
         for (int i = threadIdx.x; i < nfinal && i + 1 < n; i += 256) tie |= (K[i] >> 32) == (K[i + 1] >> 32);
         if (__syncthreads_or(tie)) {
+            __shared__ SortRange s_rng[2][256];
+            __shared__ unsigned s_seg[kKlCap / 32];
+            __shared__ int s_ctl[4];
             for (int i = threadIdx.x; i < n; i += 256) s_items[i] = SortItem{tmp[i].response, i};
             __syncthreads();
-            if (threadIdx.x == 0) std_sort(s_items, s_items + n);
+            // the libstdc++ std::sort permutation, replayed by the whole block
+            // (std_sort.h: std_sort_block; PLVI_TIE_SERIAL=1: one thread)
+            if (PLVI_TIE_SERIAL) {
+                if (threadIdx.x == 0) std_sort(s_items, s_items + n);
+            } else {
+                std_sort_block(s_items, n, s_rng[0], s_rng[1], s_seg, s_ctl);
+            }
         } else {
             for (int i = threadIdx.x; i < nfinal; i += 256) {
                 const unsigned long long v = K[i];

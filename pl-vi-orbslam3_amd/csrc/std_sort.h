@@ -168,6 +168,78 @@ PLVI_SORT_HD inline void introsort_loop(SortItem* first, SortItem* last, int dep
     }
 }
 
+#ifdef __HIPCC__
+// The same permutation as std_sort, replayed by a whole workgroup: every
+// partition of __introsort_loop reads and writes only its own range, so the
+// ranges of one recursion level are independent -- one thread per range,
+// level by level (both children carry the decremented depth, as in the
+// reference loop; a range at depth 0 is heap-sorted by its thread).  The
+// final insertion sort never moves an element across a partition boundary
+// (left parts hold keys >= the pivot's, right parts <=, so comp(right,
+// left) is false and the linear inserts stop there), so it runs per final
+// range, in parallel.  ~2n sequential element steps instead of n log n.
+// Any block size; LDS scratch: rng0 / rng1 of 256 ranges each (a level holds
+// < n / 17 ranges longer than 16: n <= 4352), `segbits` (n bits), 4 ints.
+struct SortRange {
+    int first, last, depth;
+};
+__device__ inline void std_sort_block(SortItem* a, int n, SortRange* rng0, SortRange* rng1, unsigned* segbits,
+                                      int* ctl, int depth0 = -1) {  // depth0 >= 0: test override of 2 lg n
+    const int tid = threadIdx.x, nt = blockDim.x;
+    for (int w = tid; w < (n + 31) / 32; w += nt) segbits[w] = 0u;
+    if (tid == 0) {
+        ctl[0] = 0;
+        if (n > 16) {
+            rng0[0] = SortRange{0, n, depth0 >= 0 ? depth0 : lg2(n) * 2};
+            ctl[0] = 1;
+        } else if (n > 0) {
+            segbits[0] = 1u;  // one final range [0, n)
+        }
+    }
+    __syncthreads();
+    SortRange* cur = rng0;
+    SortRange* nxt = rng1;
+    int nr = ctl[0];
+    while (nr > 0) {
+        if (tid == 0) ctl[1] = 0;
+        __syncthreads();
+        for (int r = tid; r < nr; r += nt) {
+            const SortRange R = cur[r];
+            SortItem* f = a + R.first;
+            SortItem* l = a + R.last;
+            if (R.depth == 0) {  // __partial_sort(first, last, last)
+                heap_sort_range(f, l);
+                atomicOr(&segbits[R.first >> 5], 1u << (R.first & 31));
+                continue;
+            }
+            SortItem* mid = f + (l - f) / 2;
+            move_median_to_first(f, f + 1, mid, l - 1);
+            SortItem* cut = unguarded_partition(f + 1, l, f);
+            const int c = (int)(cut - a);
+            const SortRange kids[2] = {SortRange{R.first, c, R.depth - 1}, SortRange{c, R.last, R.depth - 1}};
+            for (const SortRange& k : kids) {
+                if (k.last - k.first > 16) nxt[atomicAdd(&ctl[1], 1)] = k;
+                else if (k.last > k.first) atomicOr(&segbits[k.first >> 5], 1u << (k.first & 31));
+            }
+        }
+        __syncthreads();
+        nr = ctl[1];
+        SortRange* t = cur;
+        cur = nxt;
+        nxt = t;
+        __syncthreads();
+    }
+    // __final_insertion_sort, one thread per final range
+    for (int i = tid; i < n; i += nt) {
+        if (!((segbits[i >> 5] >> (i & 31)) & 1u)) continue;
+        int e = i + 1;
+        while (e < n && !((segbits[e >> 5] >> (e & 31)) & 1u)) ++e;
+        insertion_sort(a + i, a + e);
+    }
+    __syncthreads();
+}
+#endif
+
 PLVI_SORT_HD inline void std_sort(SortItem* first, SortItem* last) {
     if (first == last) return;
     introsort_loop(first, last, lg2(last - first) * 2);

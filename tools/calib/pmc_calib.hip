@@ -7,6 +7,7 @@
 //   calib_dword_copy   4 B per lane loads and stores
 //   calib_byte_copy    1 B per lane loads and stores
 //   calib_dwordx2_store 8 B per lane stores (no loads)
+//   calib_dwordx4_store 16 B per lane stores (no loads; the LBD Sobel kernels' int4 stores)
 // build: hipcc --offload-arch=gfx950 -O3 -shared -fPIC -o ../lib/libplvi_calib.so pmc_calib.hip
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -28,7 +29,12 @@ __global__ __launch_bounds__(256) void calib_dwordx2_store(uint2* __restrict__ d
         d[i] = make_uint2((unsigned)i, (unsigned)(i >> 32));
 }
 
-// mode 0..3 as listed above; n = bytes read (modes 0-2) or written (mode 3)
+__global__ __launch_bounds__(256) void calib_dwordx4_store(uint4* __restrict__ d, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        d[i] = make_uint4((unsigned)i, (unsigned)(i >> 32), 1u, 2u);
+}
+
+// mode 0..4 as listed above; n = bytes read (modes 0-2) or written (modes 3-4)
 extern "C" int calib_run(int mode, const void* src, void* dst, size_t n, void* stream) {
     const dim3 g(4096), b(256);
     hipStream_t st = (hipStream_t)stream;
@@ -36,6 +42,7 @@ extern "C" int calib_run(int mode, const void* src, void* dst, size_t n, void* s
     else if (mode == 1) hipLaunchKernelGGL(calib_dword_copy, g, b, 0, st, (const uint32_t*)src, (uint32_t*)dst, n / 4);
     else if (mode == 2) hipLaunchKernelGGL(calib_byte_copy, g, b, 0, st, (const uint8_t*)src, (uint8_t*)dst, n);
     else if (mode == 3) hipLaunchKernelGGL(calib_dwordx2_store, g, b, 0, st, (uint2*)dst, n / 8);
+    else if (mode == 4) hipLaunchKernelGGL(calib_dwordx4_store, g, b, 0, st, (uint4*)dst, n / 16);
     else return 1;
     return hipGetLastError() == hipSuccess ? 0 : 2;
 }

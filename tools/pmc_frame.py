@@ -20,7 +20,7 @@ cal = ctypes.CDLL(str(ROOT / "tools" / "lib" / "libplvi_calib.so"))
 cal.calib_run.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
 src = torch.randint(0, 255, (CAL_BYTES,), dtype=torch.uint8, device="cuda")
 dst = torch.empty(CAL_BYTES, dtype=torch.uint8, device="cuda")
-for mode in range(4):
+for mode in range(5):
     assert cal.calib_run(mode, src.data_ptr(), dst.data_ptr(), CAL_BYTES, None) == 0
 torch.cuda.synchronize()
 del src, dst

@@ -8,6 +8,9 @@ with the widths the kernels use and give the bytes-per-counted-byte factor:
   writes of orb_blur_fast_kernel: dword stores -> calib_dword_copy (writes)
   reads  of lsd_prep_kernel:      dword loads  -> calib_dword_read
   writes of lsd_prep_kernel:      4/8-B stores -> calib_dword_copy / calib_dwordx2_store (mean)
+  reads  of lbd_sobel0/1_kernel:  dword loads  -> calib_dword_read
+  writes of lbd_sobel0_kernel:    dword blur stores (1 B/px) + 16-B Sobel stores (4 B/px): 1/5 dword, 4/5 dwordx4
+  writes of lbd_sobel1_kernel:    4-B Sobel stores (short2 per pixel) -> calib_dword_copy
 Writes profiles/<round>/pmc_traffic.json (a list, one entry per kernel) for bench.py.
 usage: python tools/pmc_traffic.py <pmc_dir> profiles/r03 BATCH CAL_BYTES"""
 import csv
@@ -37,10 +40,13 @@ def main():
     f_wr8 = cal_bytes / mean(wr["calib_dwordx2_store"])
     f_rd1 = cal_bytes / mean(fe["calib_byte_copy"])
     f_wr1 = cal_bytes / mean(wr["calib_byte_copy"])
-    calib = {"read_dword": f_rd, "read_byte": f_rd1, "write_dword": f_wr4, "write_dwordx2": f_wr8, "write_byte": f_wr1,
+    f_wr16 = cal_bytes / mean(wr["calib_dwordx4_store"]) if "calib_dwordx4_store" in wr else f_wr8
+    calib = {"read_dword": f_rd, "read_byte": f_rd1, "write_dword": f_wr4, "write_dwordx2": f_wr8,
+             "write_dwordx4": f_wr16, "write_byte": f_wr1,
              "note": "true bytes per counted byte, from calibration kernels streaming %d B" % cal_bytes}
     entries = []
-    for k, fr, fw in (("orb_blur_fast_kernel", f_rd, f_wr4), ("lsd_prep_kernel", f_rd, (f_wr4 + f_wr8) / 2)):
+    for k, fr, fw in (("orb_blur_fast_kernel", f_rd, f_wr4), ("lsd_prep_kernel", f_rd, (f_wr4 + f_wr8) / 2),
+                      ("lbd_sobel0_kernel", f_rd, 0.2 * f_wr4 + 0.8 * f_wr16), ("lbd_sobel1_kernel", f_rd, f_wr4)):
         if k not in fe or k not in wr:
             continue
         if k == "lsd_prep_kernel":  # two launches per batch (octaves): mean of the first pair
