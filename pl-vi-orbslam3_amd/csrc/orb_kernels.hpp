@@ -794,7 +794,18 @@ constexpr int kNmsRows = 64;  // >= window height (hCell <= 58, orb_pipeline.hip
 #define PLVI_NMS_STREAM 1  // rows streamed through registers, no LDS (0: the window staged in LDS)
 #endif
 #ifndef PLVI_NMS_DENSE
-#define PLVI_NMS_DENSE 1  // the NMS writes its whole window (no per-launch zero fill of the candidate plane)
+// 1: the NMS writes its whole window, zeros included (no fill needed).  Off:
+// 4.7 vs 2.8 ms for the stage at B = 3072, 41K vs 44K FPS (column-per-lane
+// byte stores of every window row cost more than the sparse survivors)
+#define PLVI_NMS_DENSE 0
+#endif
+#ifndef PLVI_NMS_CLEAR
+// Consume and clear: orb_node_best_kernel, the last reader of the candidate
+// plane, zeroes each candidate it reads (the octree's membership rectangles
+// cover every candidate of a level; on an octree overflow the octree kernel
+// zeroes the level's region), so the NMS writes survivors only onto a plane
+// that is already zero and the per-launch fill of the plane goes away
+#define PLVI_NMS_CLEAR 1
 #endif
 
 __device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, const OrbLevelDev* __restrict__ lvs,
@@ -1177,7 +1188,7 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
                                                         const unsigned short* __restrict__ lsat,
                                                         const int* __restrict__ carry, short4* __restrict__ out_rect,
                                                         int* __restrict__ out_cnt, int nodeCapMax, int L,
-                                                        int* __restrict__ err) {
+                                                        int* __restrict__ err, uint8_t* __restrict__ cand) {
     extern __shared__ __align__(16) unsigned char smem[];
     // blocks are dealt round-robin over the 8 XCDs: with l = blockIdx.x every
     // XCD would own one level (level 0, the heaviest, on one XCD); rotating
@@ -1371,6 +1382,12 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
         out_cnt[(size_t)f * L + l] = overflow ? 0 : cntOut;
         if (overflow) atomicOr(err + f, 1);
     }
+    if (PLVI_NMS_CLEAR && !PLVI_BF_NMS && overflow) {
+        // no node list for orb_node_best_kernel to clear from: zero the region here
+        uint8_t* Cm = cand + lv.boff + (size_t)f * lv.bplane + (size_t)lv.minB * lv.bpitch + lv.minB;
+        for (int y = 0; y < RH; ++y)
+            for (int x = lane; x < RW; x += 64) Cm[(size_t)y * lv.bpitch + x] = 0;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1380,7 +1397,7 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
 // keypoint (x, y, response) in level coordinates.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void orb_node_best_kernel(const OrbLevelDev* __restrict__ lvs,
-                                                           const uint8_t* __restrict__ cand,
+                                                           uint8_t* __restrict__ cand,
                                                            const uint8_t* __restrict__ cthr, int thrFrame,
                                                            const short4* __restrict__ rects,
                                                            const int* __restrict__ rect_cnt, int nodeCapMax, int L,
@@ -1390,7 +1407,7 @@ __global__ __launch_bounds__(64) void orb_node_best_kernel(const OrbLevelDev* __
     if (node >= ncnt) return;
     const OrbLevelDev& lv = lvs[l];
     const short4 r = rects[((size_t)f * L + l) * nodeCapMax + node];
-    const uint8_t* Cm = cand + lv.boff + (size_t)f * lv.bplane;
+    uint8_t* Cm = cand + lv.boff + (size_t)f * lv.bplane;
     const int lane = threadIdx.x;
     const int rx0 = r.x, ry0 = r.y, rx1 = r.z, ry1 = r.w;
     const int wdt = rx1 - rx0;
@@ -1398,8 +1415,10 @@ __global__ __launch_bounds__(64) void orb_node_best_kernel(const OrbLevelDev* __
     const int total = wdt * (ry1 - ry0);
     for (int i = lane; i < total; i += 64) {
         const int yy = ry0 + i / wdt, xx = rx0 + i % wdt;
-        const int resp = Cm[(size_t)(lv.minB + yy) * lv.bpitch + lv.minB + xx];
+        uint8_t* cp = Cm + (size_t)(lv.minB + yy) * lv.bpitch + lv.minB + xx;
+        const int resp = *cp;
         if (!resp) continue;
+        if (PLVI_NMS_CLEAR && !PLVI_BF_NMS) *cp = 0;  // consumed: the next batch's NMS finds the plane zero
         const unsigned ci = (unsigned)(yy - 3) / (unsigned)lv.hCell, cj = (unsigned)(xx - 3) / (unsigned)lv.wCell;
         if (PLVI_BF_NMS && resp < (int)cthr[(size_t)f * thrFrame + lv.thrOff + ci * (unsigned)lv.nCols + cj])
             continue;  // the cell's fallback threshold (fused NMS)

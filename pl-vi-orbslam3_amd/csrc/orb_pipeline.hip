@@ -421,10 +421,11 @@ struct OrbPipeline {
         if (const int hrc = hook(1, st)) return hrc;
         mark(1, st);
         if (!PLVI_BF_NMS) {
-            // K2 cell NMS -> candidate map.  PLVI_NMS_DENSE: every detection
-            // window is written whole and the rest of the plane stays 0 from
-            // the init; otherwise only survivors are written, on a zeroed plane
-            if (!PLVI_NMS_DENSE || !(PLVI_NMS_MAXONLY && PLVI_NMS_STREAM))
+            // K2 cell NMS -> candidate map: only survivors are written, onto a
+            // zero plane.  PLVI_NMS_CLEAR: the previous batch's node-best pass
+            // zeroed every candidate it read (and the init zeroed the plane);
+            // otherwise a fill per launch, or PLVI_NMS_DENSE (whole windows)
+            if (!PLVI_NMS_CLEAR && (!PLVI_NMS_DENSE || !(PLVI_NMS_MAXONLY && PLVI_NMS_STREAM)))
                 PLVI_CHECK(hipMemsetAsync(Cd, 0, candBytesTotal, st));
             hipLaunchKernelGGL(orb_cell_nms_kernel, dim3((unsigned)((cells.size() + kNmsCells - 1) / kNmsCells), nf),
                                dim3(64), 0, st, d_cells.as<OrbCellDev>(), (int)cells.size(), d_lv.as<OrbLevelDev>(),
@@ -452,12 +453,12 @@ struct OrbPipeline {
         hipLaunchKernelGGL(orb_octree_kernel, dim3(L, nf), dim3(64), smem, st, d_lv.as<OrbLevelDev>(),
                            (const unsigned short*)sat.as<unsigned short>(), (const int*)carry.as<int>(),
                            rects.as<short4>(), rectCnt.as<int>(), nodeCapMax, L,
-                           err.as<int>());
+                           err.as<int>(), Cd);
         mark(4, st);
         if (const int hrc = hook(4, st)) return hrc;
         // K5 best per node
         hipLaunchKernelGGL(orb_node_best_kernel, dim3(nodeCapMax, L, nf), dim3(64), 0, st, d_lv.as<OrbLevelDev>(),
-                           (const uint8_t*)Cd, (const uint8_t*)Ct, thrFrame, (const short4*)rects.as<short4>(), (const int*)rectCnt.as<int>(),
+                           Cd, (const uint8_t*)Ct, thrFrame, (const short4*)rects.as<short4>(), (const int*)rectCnt.as<int>(),
                            nodeCapMax, L, lvkp.as<float4>(), kpCapFrame);
         mark(5, st);
         if (const int hrc = hook(5, st)) return hrc;

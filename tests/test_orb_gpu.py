@@ -109,3 +109,25 @@ def test_orb_batch_equals_single(orb640):
 def test_orb_structured_extremes(orb640, name):
     img = structured_frames()[name]
     _assert_same(orb640(img), ol.orb_extract(img), name)
+
+
+def test_orb_candidate_plane_reuse_across_batches(orb640):
+    """The candidate plane is cleared by the node-best pass that reads it (PLVI_NMS_CLEAR), not filled per
+    launch: a batch after a larger, candidate-dense one (binary noise) and a shorter batch after it must
+    still match the oracle frame by frame."""
+    noise = np.random.default_rng(3).integers(0, 256, size=(8, 480, 640), dtype=np.uint8)
+    frames = synth.batch(8, seed0=40)
+    for batch in (noise, frames[:3], frames[3:8], noise[:1], frames[:8]):
+        n = len(batch)
+        buf = plvi.DeviceBuffer(batch.nbytes)
+        buf.upload(np.ascontiguousarray(batch))
+        orb640.extract_batch(buf.ptr, n, 640 * 480, 640)
+        plvi.load().plvi_device_synchronize()
+        kp_p, de_p, co_p, mo_p, cap = orb640.outputs()
+        cnt = plvi.download(co_p, np.zeros(n, np.int32))
+        mono = plvi.download(mo_p, np.zeros(n, np.int32))
+        kps = plvi.download(kp_p, np.zeros(n * cap, plvi.KEYPOINT_DTYPE))
+        desc = plvi.download(de_p, np.zeros((n * cap, 32), np.uint8))
+        for f in range(n):
+            got = (int(mono[f]), kps[f * cap:f * cap + cnt[f]], desc[f * cap:f * cap + cnt[f]])
+            _assert_same(got, ol.orb_extract(batch[f]), f"reuse n={n} f={f}")
