@@ -637,6 +637,41 @@ int plvi_search_local(const plvi_local_params* p, const plvi_keypoint* kps, cons
                       const uint8_t* blocked, const float* uright, const uint8_t* mp_flags, const float* mp_proj,
                       const int* mp_level, const uint8_t* mp_desc, int n_mp, int* match);
 
+/* The same search on a two-camera Frame (F.Nleft != -1, src/ORBmatcher.cc:
+ * 44-214; replaces the reference's loop for KannalaBrandt8 stereo rigs).
+ * Left side: mvKeys [f][cap] (counts d_n) with their descriptors (rows
+ * 0..Nleft-1 of mDescriptors), blocked (mvpMapPoints[idx] && Observations()
+ * > 0), mvLeftToRightMatch (NULL = all -1) and the left grid (mGrid,
+ * plvi_assign_grid_batch over the left keypoints); right side: mvKeysRight
+ * [f][cap_r] (counts d_n_r), descriptors rows Nleft.., blocked of
+ * mvpMapPoints[Nleft + idx], mvRightToLeftMatch and mGridRight (the grid
+ * kernel over the right keypoints: right-relative indices).  MapPoints:
+ * flags bit0 = searched left (mbTrackInView && not far && !isBad()), bit1 =
+ * Observations() > 0, bit2 = searched right (mbTrackInViewR && not far &&
+ * !isBad()); proj [4] = mTrackProjX, mTrackProjY, (unused), mTrackViewCos;
+ * level = mnTrackScaleLevel; proj_r [4] = mTrackProjXR, mTrackProjYR,
+ * (unused), mTrackViewCosR; level_r = mnTrackScaleLevelR (-1: no right
+ * search).  Outputs match [f][cap] / match_r [f][cap_r] = the MapPoint
+ * index stored in mvpMapPoints[idx] / mvpMapPoints[Nleft + idx] by the
+ * call, or -1; nmatches [f] = the return value.  Asynchronous on `stream`. */
+int plvi_search_local_stereo_batch(int n_frames, const plvi_local_params* p, const plvi_keypoint* d_kps,
+                                   const uint8_t* d_desc, const int* d_n, int cap, const uint8_t* d_blocked,
+                                   const int* d_l2r, const int* d_cell_off, const int* d_cell_idx,
+                                   const plvi_keypoint* d_kps_r, const uint8_t* d_desc_r, const int* d_n_r, int cap_r,
+                                   const uint8_t* d_blocked_r, const int* d_r2l, const int* d_cell_off_r,
+                                   const int* d_cell_idx_r, const uint8_t* d_mp_flags, const float* d_mp_proj,
+                                   const int* d_mp_level, const float* d_mp_proj_r, const int* d_mp_level_r,
+                                   const uint8_t* d_mp_desc, const int* d_mp_n, int mp_cap, int* d_match,
+                                   int* d_match_r, int* d_nmatches, void* stream);
+
+/* One two-camera frame from host memory, synchronous.  Returns nmatches or
+ * an error. */
+int plvi_search_local_stereo(const plvi_local_params* p, const plvi_keypoint* kps, const uint8_t* desc, int n,
+                             const uint8_t* blocked, const int* l2r, const plvi_keypoint* kps_r, const uint8_t* desc_r,
+                             int n_r, const uint8_t* blocked_r, const int* r2l, const uint8_t* mp_flags,
+                             const float* mp_proj, const int* mp_level, const float* mp_proj_r, const int* mp_level_r,
+                             const uint8_t* mp_desc, int n_mp, int* match, int* match_r);
+
 /* ---------------------------------------------------------------- Stereo
  * Rectified stereo of the stereo Frame constructors (src/Frame.cc:95-140,
  * :225-300). */

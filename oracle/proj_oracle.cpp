@@ -378,6 +378,114 @@ extern "C" int oracle_search_local(int n_cur, const float* cx_, const float* cy_
     return nmatches;
 }
 
+// The same function on a two-camera Frame (F.Nleft != -1, src/ORBmatcher.cc:
+// 44-214).  Restated with the reference's indexing: one mvpMapPoints /
+// mDescriptors space of N = Nleft + Nright entries, left keypoints mvKeys
+// [0, Nleft) in mGrid, right keypoints mvKeysRight in mGridRight with
+// right-relative indices (Frame.cc:661-674).  blocked[N] = mvpMapPoints[i]
+// && Observations() > 0 on entry; l2r[Nleft] / r2l[Nright] =
+// mvLeftToRightMatch / mvRightToLeftMatch.  MapPoint flags: bit0 =
+// mbTrackInView (and not far, not bad), bit1 = Observations() > 0, bit2 =
+// mbTrackInViewR (and not far, not bad).  match[N] = the MapPoint index left
+// in mvpMapPoints by the call or -1; returns nmatches.
+extern "C" int oracle_search_local2(int n_left, const float* lx, const float* ly, const int* loct, int n_right,
+                                    const float* rx, const float* ry, const int* roct, const uint8_t* desc,
+                                    const uint8_t* blocked_in, const int* l2r, const int* r2l, float minX, float minY,
+                                    float invW, float invH, const float* scale_factors, float nnratio, float th,
+                                    int n_mp, const uint8_t* mp_flags, const float* px, const float* py,
+                                    const float* view_cos, const int* level, const float* pxr, const float* pyr,
+                                    const float* view_cos_r, const int* level_r, const uint8_t* mpdesc, int* match) {
+    const int Nleft = n_left, N = n_left + n_right;
+    const std::vector<Kp> keys = make_kps(n_left, lx, ly, loct, nullptr);        // mvKeys
+    const std::vector<Kp> keysRight = make_kps(n_right, rx, ry, roct, nullptr);  // mvKeysRight
+    Grid grid, gridRight;
+    assign_grid(keys, minX, minY, invW, invH, grid);
+    assign_grid(keysRight, minX, minY, invW, invH, gridRight);
+    std::vector<char> blocked(blocked_in, blocked_in + N);  // mvpMapPoints[i] && ->Observations() > 0
+    for (int i = 0; i < N; ++i) match[i] = -1;
+    const bool bFactor = th != 1.0;
+    int nmatches = 0;
+    auto store = [&](int i, int iMP) {  // F.mvpMapPoints[i] = pMP
+        match[i] = iMP;
+        blocked[i] = (mp_flags[iMP] & 2) ? 1 : 0;
+    };
+    for (int iMP = 0; iMP < n_mp; iMP++) {
+        const bool inView = mp_flags[iMP] & 1, inViewR = mp_flags[iMP] & 4;
+        if (!inView && !inViewR) continue;
+        if (inView) {
+            const int nPredictedLevel = level[iMP];
+            float r = view_cos[iMP] > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos
+            if (bFactor) r *= th;
+            const std::vector<size_t> vIndices =
+                features_in_area(grid, keys, minX, minY, invW, invH, px[iMP], py[iMP], r * scale_factors[nPredictedLevel],
+                                 nPredictedLevel - 1, nPredictedLevel);
+            if (!vIndices.empty()) {
+                int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+                for (size_t idx : vIndices) {
+                    if (blocked[idx]) continue;
+                    const int dist = dist256(mpdesc + 32 * (size_t)iMP, desc + 32 * idx);
+                    if (dist < bestDist) {
+                        bestDist2 = bestDist;
+                        bestDist = dist;
+                        bestLevel2 = bestLevel;
+                        bestLevel = keys[idx].octave;
+                        bestIdx = (int)idx;
+                    } else if (dist < bestDist2) {
+                        bestLevel2 = keys[idx].octave;
+                        bestDist2 = dist;
+                    }
+                }
+                if (bestDist <= kThHigh) {
+                    if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;  // the next MapPoint
+                    if (bestLevel != bestLevel2 || bestDist <= nnratio * bestDist2) {
+                        store(bestIdx, iMP);
+                        if (l2r && l2r[bestIdx] != -1) {  // also the stereo observation in the right camera
+                            store(l2r[bestIdx] + Nleft, iMP);
+                            nmatches++;
+                        }
+                        nmatches++;
+                    }
+                }
+            }
+        }
+        if (inViewR) {
+            const int nPredictedLevel = level_r[iMP];
+            if (nPredictedLevel != -1) {
+                const float r = view_cos_r[iMP] > 0.998 ? 2.5f : 4.0f;
+                const std::vector<size_t> vIndices =
+                    features_in_area(gridRight, keysRight, minX, minY, invW, invH, pxr[iMP], pyr[iMP],
+                                     r * scale_factors[nPredictedLevel], nPredictedLevel - 1, nPredictedLevel);
+                if (vIndices.empty()) continue;
+                int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+                for (size_t idx : vIndices) {
+                    if (blocked[idx + Nleft]) continue;
+                    const int dist = dist256(mpdesc + 32 * (size_t)iMP, desc + 32 * (idx + Nleft));
+                    if (dist < bestDist) {
+                        bestDist2 = bestDist;
+                        bestDist = dist;
+                        bestLevel2 = bestLevel;
+                        bestLevel = keysRight[idx].octave;
+                        bestIdx = (int)idx;
+                    } else if (dist < bestDist2) {
+                        bestLevel2 = keysRight[idx].octave;
+                        bestDist2 = dist;
+                    }
+                }
+                if (bestDist <= kThHigh) {
+                    if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
+                    if (r2l && r2l[bestIdx] != -1) {
+                        store(r2l[bestIdx], iMP);
+                        nmatches++;
+                    }
+                    store(bestIdx + Nleft, iMP);
+                    nmatches++;
+                }
+            }
+        }
+    }
+    return nmatches;
+}
+
 // ORBmatcher::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12,
 // windowSize) (src/ORBmatcher.cc:705-814), the monocular initializer's matcher
 // (Tracking::MonocularInitialization, Tracking.cc:3023/3111: ORBmatcher(0.9,

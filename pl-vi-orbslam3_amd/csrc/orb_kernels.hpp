@@ -273,7 +273,7 @@ constexpr int kBfFlush = PLVI_BF_PK ? 128 : 64;  // candidates scored per flush
 // any ring row are contiguous and a candidate's 17 taps are one base address
 // plus immediate offsets (no per-tap wrap arithmetic)
 constexpr int kRingMirror = PLVI_BF_PK ? 6 : 0;
-constexpr int kBfCols = 244, kBfRowsMax = 160, kRingRows = PLVI_BF_LEAN ? 16 : 32, kRingW = 256,
+constexpr int kBfCols = 244, kBfRowsMax = 160, kBfRowsPlain = 128, kRingRows = PLVI_BF_LEAN ? 16 : 32, kRingW = 256,
               kBfQCap = kBfFlush - 1 + 256 + 1;  // a row adds <= 256 candidates to < kBfFlush queued
 constexpr int kOrbCellsLevelMax = 1280;           // nRows * nCols of a level (LDS of the SAT kernel)
 // fused NMS: scores of the last kSRows output rows, the scored candidates

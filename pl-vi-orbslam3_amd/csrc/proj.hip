@@ -299,18 +299,20 @@ __global__ __launch_bounds__(256) void search_by_projection_kernel(
 // re-scans only one whose best or second candidate was blocked meanwhile
 // (removing any other candidate leaves both unchanged), then applies the
 // level-aware ratio test and the assignment.
+// fbit: the MapPoint flag that enables this scan; use_th: the radius is
+// scaled by th (the left camera's branch only, :69-70 -- not :148)
 __device__ void local_scan(const plvi_local_params& p, const ProjLds& s, const unsigned char* blk, int m,
                            const unsigned char* __restrict__ fl, const float* __restrict__ proj,
                            const int* __restrict__ lvl, const uint8_t* __restrict__ mpdesc,
                            const uint8_t* __restrict__ cdesc, const float* __restrict__ uright, unsigned* b1,
-                           unsigned* b2) {
+                           unsigned* b2, unsigned char fbit = 1, bool use_th = true) {
     *b1 = *b2 = 0xFFFFFFFFu;
-    if (!(fl[m] & 1)) return;
+    if (!(fl[m] & fbit)) return;
     const float x = proj[4 * m], y = proj[4 * m + 1], xr = proj[4 * m + 2], vcos = proj[4 * m + 3];
     const int L = lvl[m];
     if (L < 0 || L >= p.nlevels) return;  // no scale factor for that level: no candidate
     float r = vcos > 0.998 ? 2.5f : 4.0f;  // RadiusByViewingCos (:216-222)
-    if (p.th != 1.0) r *= p.th;
+    if (use_th && p.th != 1.0) r *= p.th;
     const float radius = r * p.scale_factors[L];
     const int minLevel = L - 1, maxLevel = L;
     const int nMinCellX = max(0, (int)floorf((x - p.min_x - radius) * p.inv_w));
@@ -437,6 +439,140 @@ __global__ __launch_bounds__(256) void search_local_kernel(
     __syncthreads();
     int* M = match + (size_t)fr * cur_cap;
     for (int i = tid; i < nc; i += 256) M[i] = s.assign[i];
+}
+
+// ---------------------------------------------------------------------------
+// The same search on a two-camera Frame (F.Nleft != -1: the KannalaBrandt8
+// stereo rigs, ORBmatcher.cc:44-214).  Left keypoints mvKeys [0, Nleft) with
+// grid mGrid, right keypoints mvKeysRight with mGridRight (right-relative
+// indices, Frame.cc:661-674); a MapPoint is searched in the left image when
+// mbTrackInView (flag bit0) and in the right image when mbTrackInViewR (bit2)
+// -- the right radius is not scaled by th (:148) and there is no mvuRight
+// test.  Assignments follow the stereo pairs: a left match also stores the
+// MapPoint at mvLeftToRightMatch[idx] + Nleft (:132-136), a right match at
+// mvRightToLeftMatch[idx] (:199-203), and both block those keypoints for the
+// later MapPoints.  A left ratio-test failure skips the MapPoint's right
+// search too (the `continue` at :127).  Same schedule: phase 1 scans both
+// sides of every MapPoint in parallel against the entry flags, phase 2 walks
+// the MapPoints in order, left then right, re-scanning a side whose best or
+// second candidate was blocked meanwhile.
+struct LocalSide {
+    ProjLds s;
+    const uint8_t* desc;
+    const int* pair;  // mvLeftToRightMatch / mvRightToLeftMatch (NULL = none)
+    int n;
+};
+
+__device__ void local_side_load(LocalSide& d, unsigned char*& q, int cap, const plvi_keypoint* K,
+                                const uint8_t* blocked, const int* CO, const int* CI, int tid) {
+    d.s.kx = reinterpret_cast<float*>(q); q += 4 * cap;
+    d.s.ky = reinterpret_cast<float*>(q); q += 4 * cap;
+    d.s.assign = reinterpret_cast<int*>(q); q += 4 * cap;
+    d.s.cell_off = reinterpret_cast<int*>(q); q += 4 * (kGridCells + 1);
+    d.s.cell_idx = reinterpret_cast<unsigned short*>(q); q += 2 * cap;
+    d.s.koct = q; q += cap;
+    d.s.blocked = q; q += cap;
+    d.s.pre = q; q += cap;
+    q = reinterpret_cast<unsigned char*>(((uintptr_t)q + 15) & ~(uintptr_t)15);
+    for (int i = tid; i < d.n; i += 256) {
+        d.s.kx[i] = K[i].x;
+        d.s.ky[i] = K[i].y;
+        d.s.koct[i] = (unsigned char)K[i].octave;
+        const unsigned char b = blocked ? blocked[i] : 0;
+        d.s.blocked[i] = b;
+        d.s.pre[i] = b;
+        d.s.assign[i] = -1;
+    }
+    for (int c = tid; c <= kGridCells; c += 256) d.s.cell_off[c] = CO[c];
+    const int ncell = CO[kGridCells];
+    for (int k = tid; k < ncell; k += 256) d.s.cell_idx[k] = (unsigned short)CI[k];
+}
+
+__global__ __launch_bounds__(256) void search_local2_kernel(
+    plvi_local_params p, const plvi_keypoint* __restrict__ lkps, const uint8_t* __restrict__ ldesc_all,
+    const int* __restrict__ l_n, int l_cap, const uint8_t* __restrict__ lblocked, const int* __restrict__ l2r_all,
+    const int* __restrict__ lcell_off_all, const int* __restrict__ lcell_idx_all, const plvi_keypoint* __restrict__ rkps,
+    const uint8_t* __restrict__ rdesc_all, const int* __restrict__ r_n, int r_cap, const uint8_t* __restrict__ rblocked,
+    const int* __restrict__ r2l_all, const int* __restrict__ rcell_off_all, const int* __restrict__ rcell_idx_all,
+    const uint8_t* __restrict__ flags_all, const float* __restrict__ proj_all, const int* __restrict__ level_all,
+    const float* __restrict__ projr_all, const int* __restrict__ levelr_all, const uint8_t* __restrict__ mpdesc_all,
+    const int* __restrict__ mp_n, int mp_cap, int* __restrict__ match_l, int* __restrict__ match_r,
+    int* __restrict__ nmatches) {
+    extern __shared__ __align__(16) unsigned char lds[];
+    const int fr = blockIdx.x, tid = threadIdx.x;
+    const int nm = min(mp_n[fr], mp_cap);
+    LocalSide S[2];
+    S[0].n = min(l_n[fr], l_cap);
+    S[1].n = min(r_n[fr], r_cap);
+    S[0].desc = ldesc_all + (size_t)fr * l_cap * 32;
+    S[1].desc = rdesc_all + (size_t)fr * r_cap * 32;
+    S[0].pair = l2r_all ? l2r_all + (size_t)fr * l_cap : nullptr;
+    S[1].pair = r2l_all ? r2l_all + (size_t)fr * r_cap : nullptr;
+    unsigned* best;  // [4][mp_cap]: left best / second, right best / second
+    {
+        unsigned char* q = lds;
+        best = reinterpret_cast<unsigned*>(q); q += 16 * (size_t)mp_cap;
+        local_side_load(S[0], q, l_cap, lkps + (size_t)fr * l_cap, lblocked ? lblocked + (size_t)fr * l_cap : nullptr,
+                        lcell_off_all + (size_t)fr * (kGridCells + 1), lcell_idx_all + (size_t)fr * l_cap, tid);
+        local_side_load(S[1], q, r_cap, rkps + (size_t)fr * r_cap, rblocked ? rblocked + (size_t)fr * r_cap : nullptr,
+                        rcell_off_all + (size_t)fr * (kGridCells + 1), rcell_idx_all + (size_t)fr * r_cap, tid);
+    }
+    __syncthreads();
+    const unsigned char* fl = flags_all + (size_t)fr * mp_cap;
+    const float* proj[2] = {proj_all + (size_t)fr * mp_cap * 4, projr_all + (size_t)fr * mp_cap * 4};
+    const int* lvl[2] = {level_all + (size_t)fr * mp_cap, levelr_all + (size_t)fr * mp_cap};
+    const uint8_t* mpdesc = mpdesc_all + (size_t)fr * mp_cap * 32;
+    const unsigned char fbit[2] = {1, 4};
+    // phase 1: both sides of every MapPoint against the flags on entry
+    for (int m = tid; m < nm; m += 256)
+        for (int c = 0; c < 2; ++c)
+            local_scan(p, S[c].s, S[c].s.pre, m, fl, proj[c], lvl[c], mpdesc, S[c].desc, nullptr,
+                       &best[(2 * c) * mp_cap + m], &best[(2 * c + 1) * mp_cap + m], fbit[c], c == 0);
+    __syncthreads();
+    // phase 2: vpMapPoints order, left (:62-143) then right (:145-211)
+    // A stereo partner is overwritten unchecked (:133, :200), so a keypoint
+    // blocked on entry can become a candidate again (stored MapPoint without
+    // observations): from then on every scan of that image is redone (rare).
+    if (tid == 0) {
+        int nmt = 0;
+        bool unblocked[2] = {false, false};
+        for (int m = 0; m < nm; ++m) {
+            const unsigned char obs = (fl[m] & 2) ? 1 : 0;  // the stored MapPoint's Observations() > 0
+            for (int c = 0; c < 2; ++c) {
+                LocalSide& A = S[c];
+                LocalSide& B = S[1 - c];
+                unsigned b1 = best[(2 * c) * mp_cap + m], b2 = best[(2 * c + 1) * mp_cap + m];
+                if (b1 == 0xFFFFFFFFu && !unblocked[c]) continue;
+                const int i1 = (int)(b1 & 0xFFFFu), i2 = b2 == 0xFFFFFFFFu ? -1 : (int)(b2 & 0xFFFFu);
+                if (unblocked[c] || A.s.blocked[i1] != A.s.pre[i1] || (i2 >= 0 && A.s.blocked[i2] != A.s.pre[i2])) {
+                    local_scan(p, A.s, A.s.blocked, m, fl, proj[c], lvl[c], mpdesc, A.desc, nullptr, &b1, &b2, fbit[c],
+                               c == 0);  // blocked meanwhile
+                    if (b1 == 0xFFFFFFFFu) continue;
+                }
+                const int bestDist = (int)(b1 >> 16), bestIdx = (int)(b1 & 0xFFFFu);
+                const int bestDist2 = b2 == 0xFFFFFFFFu ? 256 : (int)(b2 >> 16);
+                const int bestLevel = A.s.koct[bestIdx], bestLevel2 = b2 == 0xFFFFFFFFu ? -1 : A.s.koct[b2 & 0xFFFFu];
+                if (bestDist > kProjThHigh) continue;
+                if (bestLevel == bestLevel2 && bestDist > p.nnratio * bestDist2) break;  // :127 / :197: next MapPoint
+                A.s.assign[bestIdx] = m;
+                A.s.blocked[bestIdx] = obs;
+                ++nmt;
+                const int o = A.pair ? A.pair[bestIdx] : -1;
+                if (o >= 0 && o < B.n) {  // the stereo observation in the other image
+                    B.s.assign[o] = m;
+                    if (B.s.blocked[o] && !obs) unblocked[1 - c] = true;
+                    B.s.blocked[o] = obs;
+                    ++nmt;
+                }
+            }
+        }
+        nmatches[fr] = nmt;
+    }
+    __syncthreads();
+    int* ML = match_l + (size_t)fr * l_cap;
+    int* MR = match_r + (size_t)fr * r_cap;
+    for (int i = tid; i < S[0].n; i += 256) ML[i] = S[0].s.assign[i];
+    for (int i = tid; i < S[1].n; i += 256) MR[i] = S[1].s.assign[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -620,6 +756,11 @@ __global__ __launch_bounds__(256) void search_reloc_kernel(
 
 static size_t local_smem(int cur_cap, int mp_cap) {
     return (size_t)cur_cap * (4 + 4 + 4 + 2 + 1 + 1 + 1) + (size_t)mp_cap * 8 + 4 * (kGridCells + 1) + 64;
+}
+
+static size_t local2_smem(int l_cap, int r_cap, int mp_cap) {
+    auto side = [](int cap) { return ((size_t)cap * (4 + 4 + 4 + 2 + 1 + 1 + 1) + 4 * (kGridCells + 1) + 15) & ~size_t(15); };
+    return 16 * (size_t)mp_cap + side(l_cap) + side(r_cap) + 64;
 }
 
 static size_t proj_smem(int cur_cap, int last_cap) {
@@ -881,5 +1022,101 @@ extern "C" int plvi_search_local(const plvi_local_params* p, const plvi_keypoint
     int nmt = 0;
     PLVI_CHECK(hipMemcpy(match, B + off[oM], 4 * (size_t)n, hipMemcpyDeviceToHost));
     PLVI_CHECK(hipMemcpy(&nmt, dN + 2, 4, hipMemcpyDeviceToHost));
+    return nmt;
+}
+
+extern "C" int plvi_search_local_stereo_batch(
+    int n_frames, const plvi_local_params* p, const plvi_keypoint* d_kps, const uint8_t* d_desc, const int* d_n,
+    int cap, const uint8_t* d_blocked, const int* d_l2r, const int* d_cell_off, const int* d_cell_idx,
+    const plvi_keypoint* d_kps_r, const uint8_t* d_desc_r, const int* d_n_r, int cap_r, const uint8_t* d_blocked_r,
+    const int* d_r2l, const int* d_cell_off_r, const int* d_cell_idx_r, const uint8_t* d_mp_flags,
+    const float* d_mp_proj, const int* d_mp_level, const float* d_mp_proj_r, const int* d_mp_level_r,
+    const uint8_t* d_mp_desc, const int* d_mp_n, int mp_cap, int* d_match, int* d_match_r, int* d_nmatches,
+    void* stream) {
+    if (!p || n_frames < 0 || cap < 1 || cap_r < 1 || mp_cap < 1 || cap > 65535 || cap_r > 65535)
+        return PLVI_E_BADARG;
+    if (p->nlevels < 1 || p->nlevels > 16) return PLVI_E_BADARG;
+    if (n_frames == 0) return PLVI_OK;
+    const size_t smem = local2_smem(cap, cap_r, mp_cap);
+    if (smem > 160 * 1024) return PLVI_E_CAPACITY;
+    PLVI_CHECK(hipFuncSetAttribute((const void*)search_local2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)smem));
+    hipLaunchKernelGGL(search_local2_kernel, dim3(n_frames), dim3(256), smem, (hipStream_t)stream, *p, d_kps, d_desc,
+                       d_n, cap, d_blocked, d_l2r, d_cell_off, d_cell_idx, d_kps_r, d_desc_r, d_n_r, cap_r,
+                       d_blocked_r, d_r2l, d_cell_off_r, d_cell_idx_r, d_mp_flags, d_mp_proj, d_mp_level, d_mp_proj_r,
+                       d_mp_level_r, d_mp_desc, d_mp_n, mp_cap, d_match, d_match_r, d_nmatches);
+    PLVI_CHECK(hipGetLastError());
+    return PLVI_OK;
+}
+
+// One two-camera frame from host memory, synchronous (both grids built on the device).
+extern "C" int plvi_search_local_stereo(const plvi_local_params* p, const plvi_keypoint* kps, const uint8_t* desc,
+                                        int n, const uint8_t* blocked, const int* l2r, const plvi_keypoint* kps_r,
+                                        const uint8_t* desc_r, int n_r, const uint8_t* blocked_r, const int* r2l,
+                                        const uint8_t* mp_flags, const float* mp_proj, const int* mp_level,
+                                        const float* mp_proj_r, const int* mp_level_r, const uint8_t* mp_desc,
+                                        int n_mp, int* match, int* match_r) {
+    if (!p || n < 0 || n_r < 0 || n_mp < 0) return PLVI_E_BADARG;
+    if ((n > 0 && (!kps || !desc || !match)) || (n_r > 0 && (!kps_r || !desc_r || !match_r))) return PLVI_E_BADARG;
+    if (n_mp > 0 && (!mp_flags || !mp_proj || !mp_level || !mp_proj_r || !mp_level_r || !mp_desc))
+        return PLVI_E_BADARG;
+    if (n + n_r == 0) return 0;
+    const int cl = std::max(n, 1), cr = std::max(n_r, 1), mc = std::max(n_mp, 1);
+    std::vector<size_t> off;
+    size_t tot = 0;
+    auto put = [&](size_t bytes) {
+        off.push_back(tot);
+        tot += (bytes + 255) & ~size_t(255);
+        return off.size() - 1;
+    };
+    const size_t oK = put(sizeof(plvi_keypoint) * cl), oD = put(32 * (size_t)cl), oB = put(cl), oP2 = put(4 * (size_t)cl);
+    const size_t oCO = put(4 * (size_t)(kGridCells + 1)), oCI = put(4 * (size_t)cl), oM = put(4 * (size_t)cl);
+    const size_t rK = put(sizeof(plvi_keypoint) * cr), rD = put(32 * (size_t)cr), rB = put(cr), rP2 = put(4 * (size_t)cr);
+    const size_t rCO = put(4 * (size_t)(kGridCells + 1)), rCI = put(4 * (size_t)cr), rM = put(4 * (size_t)cr);
+    const size_t oF = put(mc), oP = put(16 * (size_t)mc), oL = put(4 * (size_t)mc), oPR = put(16 * (size_t)mc),
+                 oLR = put(4 * (size_t)mc), oMD = put(32 * (size_t)mc), oN = put(16);
+    DevBuf d;
+    if (d.alloc(tot)) return PLVI_E_HIP;
+    uint8_t* B = d.as<uint8_t>();
+    PLVI_CHECK(hipMemset(B, 0, tot));
+    auto up = [&](size_t slot, const void* src, size_t bytes) -> int {
+        if (src && bytes) PLVI_CHECK(hipMemcpy(B + off[slot], src, bytes, hipMemcpyHostToDevice));
+        return PLVI_OK;
+    };
+    int rc = up(oK, kps, sizeof(plvi_keypoint) * n) | up(oD, desc, 32 * (size_t)n) | up(oB, blocked, n) |
+             up(rK, kps_r, sizeof(plvi_keypoint) * n_r) | up(rD, desc_r, 32 * (size_t)n_r) | up(rB, blocked_r, n_r);
+    // no stereo pairs = every entry -1
+    std::vector<int> none(std::max(n, n_r), -1);
+    rc |= up(oP2, l2r ? l2r : none.data(), 4 * (size_t)n) | up(rP2, r2l ? r2l : none.data(), 4 * (size_t)n_r);
+    if (n_mp > 0)
+        rc |= up(oF, mp_flags, n_mp) | up(oP, mp_proj, 16 * (size_t)n_mp) | up(oL, mp_level, 4 * (size_t)n_mp) |
+              up(oPR, mp_proj_r, 16 * (size_t)n_mp) | up(oLR, mp_level_r, 4 * (size_t)n_mp) |
+              up(oMD, mp_desc, 32 * (size_t)n_mp);
+    if (rc) return PLVI_E_HIP;
+    int counts[4] = {n, n_r, n_mp, 0};
+    PLVI_CHECK(hipMemcpy(B + off[oN], counts, 16, hipMemcpyHostToDevice));
+    int* dN = reinterpret_cast<int*>(B + off[oN]);
+    plvi_grid_params gp{p->min_x, p->min_y, p->inv_w, p->inv_h};
+    rc = plvi_assign_grid_batch(reinterpret_cast<const plvi_keypoint*>(B + off[oK]), dN, cl, 1, &gp,
+                                reinterpret_cast<int*>(B + off[oCO]), reinterpret_cast<int*>(B + off[oCI]), nullptr);
+    if (rc) return rc;
+    rc = plvi_assign_grid_batch(reinterpret_cast<const plvi_keypoint*>(B + off[rK]), dN + 1, cr, 1, &gp,
+                                reinterpret_cast<int*>(B + off[rCO]), reinterpret_cast<int*>(B + off[rCI]), nullptr);
+    if (rc) return rc;
+    rc = plvi_search_local_stereo_batch(
+        1, p, reinterpret_cast<const plvi_keypoint*>(B + off[oK]), B + off[oD], dN, cl, B + off[oB],
+        reinterpret_cast<const int*>(B + off[oP2]), reinterpret_cast<const int*>(B + off[oCO]),
+        reinterpret_cast<const int*>(B + off[oCI]), reinterpret_cast<const plvi_keypoint*>(B + off[rK]), B + off[rD],
+        dN + 1, cr, B + off[rB], reinterpret_cast<const int*>(B + off[rP2]), reinterpret_cast<const int*>(B + off[rCO]),
+        reinterpret_cast<const int*>(B + off[rCI]), B + off[oF], reinterpret_cast<const float*>(B + off[oP]),
+        reinterpret_cast<const int*>(B + off[oL]), reinterpret_cast<const float*>(B + off[oPR]),
+        reinterpret_cast<const int*>(B + off[oLR]), B + off[oMD], dN + 2, mc, reinterpret_cast<int*>(B + off[oM]),
+        reinterpret_cast<int*>(B + off[rM]), dN + 3, nullptr);
+    if (rc) return rc;
+    PLVI_CHECK(hipDeviceSynchronize());
+    int nmt = 0;
+    if (n) PLVI_CHECK(hipMemcpy(match, B + off[oM], 4 * (size_t)n, hipMemcpyDeviceToHost));
+    if (n_r) PLVI_CHECK(hipMemcpy(match_r, B + off[rM], 4 * (size_t)n_r, hipMemcpyDeviceToHost));
+    PLVI_CHECK(hipMemcpy(&nmt, dN + 3, 4, hipMemcpyDeviceToHost));
     return nmt;
 }

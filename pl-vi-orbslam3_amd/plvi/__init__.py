@@ -232,6 +232,9 @@ def _declare(lib):
         "plvi_line_search_init_batch": ([V, V, I, V, V, I, I, V, V, V, V, V], I),
         "plvi_search_local_batch": ([I, V, V, V, V, I, V, V, V, V, V, V, V, V, V, I, V, V, V], I),
         "plvi_search_local": ([V, V, V, I, V, V, V, V, V, V, I, V], I),
+        "plvi_search_local_stereo_batch": ([I, V, V, V, V, I, V, V, V, V, V, V, V, I, V, V, V, V, V, V, V, V, V, V,
+                                            V, I, V, V, V, V], I),
+        "plvi_search_local_stereo": ([V, V, V, I, V, V, V, V, I, V, V, V, V, V, V, V, V, I, V, V], I),
         "plvi_search_reloc_batch": ([I, V, V, V, V, I, V, V, V, V, V, V, V, V, V, V, I, V, V, V], I),
         "plvi_search_reloc": ([V, V, V, I, V, V, V, V, V, V, V, I, V], I),
         "plvi_line_search_projection_batch": ([I, V, V, V, V, V, I, V, V, I, V, V, V, V, V, I, V, V, V, V], I),
@@ -828,6 +831,39 @@ class ORBmatcher:
                                                 _ptr(fl), _ptr(pr), _ptr(lv), _ptr(md), len(fl), _ptr(out)),
                     "plvi_search_local")
         return nm, out[:len(k)]
+
+    def SearchByProjectionLocalStereo(self, params, kps, desc, kps_r, desc_r, mp_flags, mp_proj, mp_level,
+                                      mp_proj_r, mp_level_r, mp_desc, blocked=None, blocked_r=None, l2r=None,
+                                      r2l=None):
+        """SearchByProjection(Frame&, const vector<MapPoint*>&, ...) on a two-camera Frame (F.Nleft != -1,
+        src/ORBmatcher.cc:44-214).  kps / desc: mvKeys and descriptor rows 0..Nleft-1; kps_r / desc_r:
+        mvKeysRight and rows Nleft..; blocked / blocked_r: mvpMapPoints[idx] (resp. [Nleft + idx]) with
+        Observations() > 0 on entry; l2r / r2l: mvLeftToRightMatch / mvRightToLeftMatch; per MapPoint: flags
+        (bit0 searched left, bit1 Observations() > 0, bit2 searched right), proj (n x 4: mTrackProjX,
+        mTrackProjY, -, mTrackViewCos), mnTrackScaleLevel, proj_r (mTrackProjXR, mTrackProjYR, -,
+        mTrackViewCosR), mnTrackScaleLevelR, descriptor.  Returns (nmatches, match, match_r)."""
+        params.nnratio = self.nnratio
+        k = np.ascontiguousarray(kps).view(KEYPOINT_DTYPE)
+        kr = np.ascontiguousarray(kps_r).view(KEYPOINT_DTYPE)
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        dr = np.ascontiguousarray(desc_r, np.uint8).reshape(-1, 32)
+        fl = np.ascontiguousarray(mp_flags, np.uint8)
+        pr = np.ascontiguousarray(mp_proj, np.float32).reshape(-1, 4)
+        lv = np.ascontiguousarray(mp_level, np.int32)
+        prr = np.ascontiguousarray(mp_proj_r, np.float32).reshape(-1, 4)
+        lvr = np.ascontiguousarray(mp_level_r, np.int32)
+        md = np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32)
+        opt = lambda a, t: None if a is None else np.ascontiguousarray(a, t)  # noqa: E731
+        cb, cbr, a, b = opt(blocked, np.uint8), opt(blocked_r, np.uint8), opt(l2r, np.int32), opt(r2l, np.int32)
+        pp = lambda a: None if a is None else _ptr(a)  # noqa: E731
+        out = np.full(max(len(k), 1), -1, np.int32)
+        outr = np.full(max(len(kr), 1), -1, np.int32)
+        nm = _check(self._lib.plvi_search_local_stereo(ctypes.byref(params), _ptr(k), _ptr(d), len(k), pp(cb), pp(a),
+                                                       _ptr(kr), _ptr(dr), len(kr), pp(cbr), pp(b), _ptr(fl), _ptr(pr),
+                                                       _ptr(lv), _ptr(prr), _ptr(lvr), _ptr(md), len(fl), _ptr(out),
+                                                       _ptr(outr)),
+                    "plvi_search_local_stereo")
+        return nm, out[:len(k)], outr[:len(kr)]
 
     def SearchByProjectionKF(self, params, cur_kps, cur_desc, kf_flags, x3dc, dist, level, kf_angle, mp_desc,
                              cur_blocked=None):

@@ -527,6 +527,39 @@ def search_local(case, th, nnratio=0.8):
     return n, out[:len(kx)]
 
 
+def search_local_stereo(case, th, nnratio=0.8):
+    """Two-camera SearchByProjection(Frame&, const vector<MapPoint*>&, ...) restatement
+    -> (nmatches, match_left, match_right)."""
+    lib = load()
+    V, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    lib.oracle_search_local2.argtypes = [I, V, V, V, I, V, V, V, V, V, V, V, F, F, F, F, V, F, F, I, V, V, V, V, V,
+                                         V, V, V, V, V, V]
+    lib.oracle_search_local2.restype = I
+    c = case
+    f32 = lambda a: np.ascontiguousarray(a, np.float32)  # noqa: E731
+    i32 = lambda a: np.ascontiguousarray(a, np.int32)  # noqa: E731
+    kl, kr = c["kps"], c["kps_r"]
+    nl, nr = len(kl), len(kr)
+    desc = np.ascontiguousarray(np.concatenate([c["desc"], c["desc_r"]]), np.uint8)
+    blk = np.ascontiguousarray(np.concatenate([c["blocked"], c["blocked_r"]]), np.uint8)
+    l2r, r2l = i32(c["l2r"]), i32(c["r2l"])
+    min_x, _, min_y, _, inv_w, inv_h = c["grid"]
+    sf = f32(c["scale_factors"])
+    fl = np.ascontiguousarray(c["mp_flags"], np.uint8)
+    pr, prr = f32(c["mp_proj"]), f32(c["mp_proj_r"])
+    lv, lvr = i32(c["mp_level"]), i32(c["mp_level_r"])
+    md = np.ascontiguousarray(c["mp_desc"], np.uint8)
+    cols = [f32(pr[:, j]) for j in range(4)] + [f32(prr[:, j]) for j in range(4)]
+    lx, ly, lo = f32(kl["x"]), f32(kl["y"]), i32(kl["octave"])
+    rx, ry, ro = f32(kr["x"]), f32(kr["y"]), i32(kr["octave"])
+    out = np.full(max(nl + nr, 1), -1, np.int32)
+    n = lib.oracle_search_local2(nl, _p(lx), _p(ly), _p(lo), nr, _p(rx), _p(ry), _p(ro), _p(desc), _p(blk), _p(l2r),
+                                 _p(r2l), min_x, min_y, inv_w, inv_h, _p(sf), nnratio, th, len(fl), _p(fl),
+                                 _p(cols[0]), _p(cols[1]), _p(cols[3]), _p(lv), _p(cols[4]), _p(cols[5]), _p(cols[7]),
+                                 _p(lvr), _p(md), _p(out))
+    return n, out[:nl], out[nl:nl + nr]
+
+
 def line_search_projection(case, th, angth, range_hint=1):
     """LineMatcher::SearchByProjection restatement -> (count, match)."""
     lib = load()

@@ -269,6 +269,79 @@ def local_case(seed, n_cur=1000, n_mp=1500, W=752, H=480, uright=False, dup=0.15
     return case
 
 
+def local_stereo_case(seed, n_left=900, n_right=850, n_mp=1400, W=752, H=480, pair_frac=0.6, dup=0.15):
+    """Two-camera local-map search input (F.Nleft != -1): left / right keypoint sets with descriptors, a
+    fraction of them paired (mvLeftToRightMatch / mvRightToLeftMatch, mutually consistent, right
+    descriptor = the left one with a few flipped bits); MapPoints seen in the left image, the right image or
+    both (bit0 / bit2), each aiming near a keypoint of that image (its predicted level = the keypoint's
+    octave +-1, the right level sometimes -1), duplicates aiming at an earlier MapPoint's keypoints so the
+    sequential blocking and the stereo cross-assignments matter."""
+    from plvi import KEYPOINT_DTYPE, grid_geometry
+    rng = np.random.default_rng(seed)
+
+    def kset(n):
+        k = np.zeros(n, KEYPOINT_DTYPE)
+        k["x"] = rng.uniform(-3, W + 3, n).astype(np.float32)
+        k["y"] = rng.uniform(-3, H + 3, n).astype(np.float32)
+        k["octave"] = np.minimum(rng.geometric(0.35, n) - 1, 7)
+        k["size"] = 31
+        k["class_id"] = -1
+        return k
+    kl, kr = kset(n_left), kset(n_right)
+    dl = rng.integers(0, 256, (n_left, 32), dtype=np.uint8)
+    dr = rng.integers(0, 256, (n_right, 32), dtype=np.uint8)
+    npair = int(pair_frac * min(n_left, n_right))
+    li = rng.choice(n_left, npair, replace=False)
+    ri = rng.choice(n_right, npair, replace=False)
+    l2r = np.full(n_left, -1, np.int32)
+    r2l = np.full(n_right, -1, np.int32)
+    l2r[li] = ri
+    r2l[ri] = li
+    bits = np.unpackbits(dl[li], axis=1)
+    bits ^= (rng.random(bits.shape) < 0.03).astype(np.uint8)
+    dr[ri] = np.packbits(bits, axis=1)
+    kr["octave"][ri] = kl["octave"][li]
+
+    def aim(k, d, n):
+        near = rng.random(n_mp) < 0.8
+        src = rng.integers(0, n, n_mp)
+        nd = int(dup * n_mp)
+        if nd:
+            src[-nd:] = src[rng.integers(0, n_mp - nd, nd)]
+        px = np.where(near, k["x"][src] + rng.normal(0, 1.5, n_mp), rng.uniform(0, W, n_mp)).astype(np.float32)
+        py = np.where(near, k["y"][src] + rng.normal(0, 1.5, n_mp), rng.uniform(0, H, n_mp)).astype(np.float32)
+        vc = np.where(rng.random(n_mp) < 0.5, rng.uniform(0.999, 1.0, n_mp), rng.uniform(0.5, 0.998, n_mp))
+        lvl = np.clip(np.where(near, k["octave"][src] + rng.integers(-1, 2, n_mp), rng.integers(0, 8, n_mp)), 0, 7)
+        return src, near, np.stack([px, py, np.zeros(n_mp), vc], 1).astype(np.float32), lvl.astype(np.int32)
+    srcl, nearl, prl, lvl = aim(kl, dl, n_left)
+    srcr, nearr, prr, lvr = aim(kr, dr, n_right)
+    side = rng.random(n_mp)  # left only / right only / both
+    bl = side < 0.75
+    br = side > 0.45
+    # a MapPoint seen in both images aims at a stereo pair's two keypoints when its left target has one
+    both = bl & br & (l2r[srcl] >= 0)
+    srcr = np.where(both, l2r[srcl], srcr)
+    prr[both, 0] = kr["x"][srcr[both]] + rng.normal(0, 1.5, both.sum()).astype(np.float32)
+    prr[both, 1] = kr["y"][srcr[both]] + rng.normal(0, 1.5, both.sum()).astype(np.float32)
+    nearr = nearr | both
+    lvr = np.where(both, np.clip(kr["octave"][srcr] + rng.integers(-1, 2, n_mp), 0, 7), lvr).astype(np.int32)
+    lvr = np.where(rng.random(n_mp) < 0.05, -1, lvr).astype(np.int32)
+    base = np.where(bl, dl[srcl].T, dr[srcr].T).T
+    bits = np.unpackbits(base, axis=1)
+    bits ^= (rng.random(bits.shape) < 0.06).astype(np.uint8)
+    md = np.where((nearl | nearr)[:, None], np.packbits(bits, axis=1),
+                  rng.integers(0, 256, (n_mp, 32), dtype=np.uint8))
+    alive = rng.random(n_mp) < 0.92
+    obs = rng.random(n_mp) < 0.85
+    flags = ((bl & alive).astype(np.uint8) | (obs.astype(np.uint8) << 1) | ((br & alive).astype(np.uint8) << 2))
+    return {"kps": kl, "desc": dl, "kps_r": kr, "desc_r": dr, "l2r": l2r, "r2l": r2l,
+            "blocked": (rng.random(n_left) < 0.04).astype(np.uint8),
+            "blocked_r": (rng.random(n_right) < 0.04).astype(np.uint8),
+            "grid": grid_geometry(W, H), "scale_factors": orb_scale_factors(),
+            "mp_flags": flags, "mp_proj": prl, "mp_level": lvl, "mp_proj_r": prr, "mp_level_r": lvr,
+            "mp_desc": md.astype(np.uint8)}
+
+
 def local_params(case, th):
     import plvi
     p = plvi.LocalParams()
