@@ -551,6 +551,40 @@ int plvi_search_by_projection(const plvi_proj_params* p, const plvi_keypoint* cu
                               const int* last_octave, const float* last_angle, const uint8_t* mp_desc,
                               const uint8_t* last_flags, int n_last, int* match);
 
+/* The same search with a two-camera CurrentFrame (CurrentFrame.Nleft != -1,
+ * src/ORBmatcher.cc:1985-2153).  kb8 = KannalaBrandt8 k1..k4 of
+ * CurrentFrame.mpCamera (fx, fy, cx, cy from p; NULL = Pinhole).  Left:
+ * mvKeys [p][cap] (counts d_n), descriptor rows 0..Nleft-1, blocked, mGrid
+ * (plvi_assign_grid_batch over the left keypoints); right: mvKeysRight
+ * [p][cap_r], rows Nleft.., blocked of mvpMapPoints[Nleft + idx], mGridRight
+ * (the grid kernel over the right keypoints).  LastFrame point i: x3Dc, x3Dr
+ * = mTrl * x3Dc (the caller's cv::Mat products), octave (mvKeys[i] or
+ * mvKeysRight[i - Nleft] of LastFrame), angle (mvKeysUn / mvKeys /
+ * mvKeysRight as :2067-2069), descriptor, flags as above.  A point is
+ * searched in the right image only when its left pass did not end early
+ * (behind the camera, outside mnMin/MaxX/Y, empty window: :2000-2026).
+ * Outputs match [p][cap] / match_r [p][cap_r] (-2 = NULL by the rotation
+ * filter, which sees both images' matches in one histogram), nmatches [p].
+ * p->mbf is unused.  Asynchronous on `stream`. */
+int plvi_search_by_projection_stereo_batch(int n_pairs, const plvi_proj_params* p, const float* kb8,
+                                           const plvi_keypoint* d_kps, const uint8_t* d_desc, const int* d_n, int cap,
+                                           const uint8_t* d_blocked, const int* d_cell_off, const int* d_cell_idx,
+                                           const plvi_keypoint* d_kps_r, const uint8_t* d_desc_r, const int* d_n_r,
+                                           int cap_r, const uint8_t* d_blocked_r, const int* d_cell_off_r,
+                                           const int* d_cell_idx_r, const float* d_x3dc, const float* d_x3dr,
+                                           const int* d_last_octave, const float* d_last_angle,
+                                           const uint8_t* d_mp_desc, const uint8_t* d_last_flags, const int* d_last_n,
+                                           int last_cap, int* d_match, int* d_match_r, int* d_nmatches, void* stream);
+
+/* One pair from host memory, synchronous.  Returns nmatches or an error
+ * (PLVI_E_BADARG for a searched point's octave outside [0, nlevels)). */
+int plvi_search_by_projection_stereo(const plvi_proj_params* p, const float* kb8, const plvi_keypoint* kps,
+                                     const uint8_t* desc, int n, const uint8_t* blocked, const plvi_keypoint* kps_r,
+                                     const uint8_t* desc_r, int n_r, const uint8_t* blocked_r, const float* x3dc,
+                                     const float* x3dr, const int* last_octave, const float* last_angle,
+                                     const uint8_t* mp_desc, const uint8_t* last_flags, int n_last, int* match,
+                                     int* match_r);
+
 /* ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF,
  * const set<MapPoint*>& sAlreadyFound, th, ORBdist) (src/ORBmatcher.cc:2180-2300):
  * the relocalization guided search of Tracking::Relocalization

@@ -235,6 +235,132 @@ extern "C" int oracle_search_by_projection(
     return nmatches;
 }
 
+// CameraModels: Pinhole::project (Pinhole.cpp:30-33) and
+// KannalaBrandt8::project(const cv::Point3f&) (KannalaBrandt8.cpp:33-48),
+// the host libm as the reference calls it (atan2f, sqrtf; `cos(psi)` with a
+// float psi under `using namespace std` is std::cos(float)).
+static void project_cam(const float* kb8, float fx, float fy, float cxp, float cyp, float x, float y, float z,
+                        float& u, float& v) {
+    if (!kb8) {
+        u = fx * x / z + cxp;
+        v = fy * y / z + cyp;
+        return;
+    }
+    const float x2_plus_y2 = x * x + y * y;
+    const float theta = atan2f(sqrtf(x2_plus_y2), z);
+    const float psi = atan2f(y, x);
+    const float theta2 = theta * theta;
+    const float theta3 = theta * theta2;
+    const float theta5 = theta3 * theta2;
+    const float theta7 = theta5 * theta2;
+    const float theta9 = theta7 * theta2;
+    const float r = theta + kb8[0] * theta3 + kb8[1] * theta5 + kb8[2] * theta7 + kb8[3] * theta9;
+    u = fx * r * std::cos(psi) + cxp;
+    v = fy * r * std::sin(psi) + cyp;
+}
+
+// SearchByProjection(CurrentFrame, LastFrame, th, bMono) with a two-camera
+// CurrentFrame (CurrentFrame.Nleft != -1, src/ORBmatcher.cc:1985-2175),
+// restated with the reference's indexing: mvpMapPoints / mDescriptors over N
+// = Nleft + Nright, mvKeys in mGrid, mvKeysRight in mGridRight
+// (right-relative).  kb8 = KannalaBrandt8 k1..k4 (NULL = Pinhole).  LastFrame
+// point i: x3Dc, x3Dr = mTrl * x3Dc, octave, angle, descriptor, flags (bit0
+// MapPoint and not an outlier, bit1 Observations() > 0).  match[N]: LastFrame
+// index held by mvpMapPoints[idx], -2 = NULL by the rotation filter, -1.
+extern "C" int oracle_search_by_projection2(
+    int n_left, const float* lx, const float* ly, const int* loct_c, const float* lang_c, int n_right, const float* rx,
+    const float* ry, const int* roct_c, const float* rang_c, const uint8_t* cdesc, const uint8_t* cblocked,
+    float minX, float maxX, float minY, float maxY, float invW, float invH, const float* scale_factors, float fx,
+    float fy, float cxp, float cyp, const float* kb8, int n_last, const uint8_t* lflags, const float* x3dc,
+    const float* x3dr, const int* loct, const float* lang, const uint8_t* mpdesc, float th, int bForward,
+    int bBackward, int check_ori, int* match) {
+    const int Nleft = n_left, N = n_left + n_right;
+    const std::vector<Kp> keys = make_kps(n_left, lx, ly, loct_c, lang_c);            // mvKeys
+    const std::vector<Kp> keysRight = make_kps(n_right, rx, ry, roct_c, rang_c);     // mvKeysRight
+    Grid grid, gridRight;
+    assign_grid(keys, minX, minY, invW, invH, grid);
+    assign_grid(keysRight, minX, minY, invW, invH, gridRight);
+    std::vector<int> mp(N, -1);
+    std::vector<char> blocked(cblocked, cblocked + N);
+    std::vector<int> rotHist[kHisto];
+    const float factor = 1.0f / kHisto;
+    int nmatches = 0;
+    auto area = [&](const Grid& g, const std::vector<Kp>& k, float u, float v, float radius, int nLastOctave) {
+        if (bForward) return features_in_area(g, k, minX, minY, invW, invH, u, v, radius, nLastOctave, -1);
+        if (bBackward) return features_in_area(g, k, minX, minY, invW, invH, u, v, radius, 0, nLastOctave);
+        return features_in_area(g, k, minX, minY, invW, invH, u, v, radius, nLastOctave - 1, nLastOctave + 1);
+    };
+    auto bin_of = [&](float a, float b) {
+        float rot = a - b;
+        if (rot < 0.0) rot += 360.0f;
+        int bin = (int)std::round(rot * factor);
+        if (bin == kHisto) bin = 0;
+        return bin;
+    };
+    for (int i = 0; i < n_last; i++) {
+        if (!(lflags[i] & 1)) continue;
+        const float xc = x3dc[3 * i], yc = x3dc[3 * i + 1], zc = x3dc[3 * i + 2];
+        const float invzc = 1.0 / zc;
+        if (invzc < 0) continue;
+        float u, v;
+        project_cam(kb8, fx, fy, cxp, cyp, xc, yc, zc, u, v);
+        if (u < minX || u > maxX) continue;
+        if (v < minY || v > maxY) continue;
+        const int nLastOctave = loct[i];
+        const float radius = th * scale_factors[nLastOctave];
+        const std::vector<size_t> vIndices2 = area(grid, keys, u, v, radius, nLastOctave);
+        if (vIndices2.empty()) continue;
+        int bestDist = 256, bestIdx2 = -1;
+        for (size_t i2 : vIndices2) {
+            if (blocked[i2]) continue;
+            const int dist = dist256(mpdesc + 32 * (size_t)i, cdesc + 32 * i2);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx2 = (int)i2;
+            }
+        }
+        if (bestDist <= kThHigh) {
+            mp[bestIdx2] = i;
+            blocked[bestIdx2] = (lflags[i] & 2) ? 1 : 0;
+            nmatches++;
+            if (check_ori) rotHist[bin_of(lang[i], keys[bestIdx2].angle)].push_back(bestIdx2);
+        }
+        // the right camera (:2084-2150)
+        float ur, vr;
+        project_cam(kb8, fx, fy, cxp, cyp, x3dr[3 * i], x3dr[3 * i + 1], x3dr[3 * i + 2], ur, vr);
+        const std::vector<size_t> vIndicesR = area(gridRight, keysRight, ur, vr, radius, nLastOctave);
+        bestDist = 256;
+        bestIdx2 = -1;
+        for (size_t i2 : vIndicesR) {
+            if (blocked[i2 + Nleft]) continue;
+            const int dist = dist256(mpdesc + 32 * (size_t)i, cdesc + 32 * (i2 + Nleft));
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx2 = (int)i2;
+            }
+        }
+        if (bestDist <= kThHigh) {
+            mp[bestIdx2 + Nleft] = i;
+            blocked[bestIdx2 + Nleft] = (lflags[i] & 2) ? 1 : 0;
+            nmatches++;
+            if (check_ori) rotHist[bin_of(lang[i], keysRight[bestIdx2].angle)].push_back(bestIdx2 + Nleft);
+        }
+    }
+    std::vector<char> nulled(N, 0);
+    if (check_ori) {
+        int ind1 = -1, ind2 = -1, ind3 = -1;
+        three_maxima(rotHist, kHisto, ind1, ind2, ind3);
+        for (int b = 0; b < kHisto; b++)
+            if (b != ind1 && b != ind2 && b != ind3)
+                for (int idx : rotHist[b]) {
+                    nulled[idx] = 1;
+                    nmatches--;
+                }
+    }
+    for (int k = 0; k < N; ++k) match[k] = nulled[k] ? -2 : mp[k];
+    return nmatches;
+}
+
 // ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const
 // set<MapPoint*>& sAlreadyFound, th, ORBdist) (src/ORBmatcher.cc:2180-2300),
 // the relocalization guided search (Tracking.cc:5857, 5871).  Per KF MapPoint i

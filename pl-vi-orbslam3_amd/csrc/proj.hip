@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "plvi_common.h"
+#include "plvi_math.h"
 
 namespace plvi {
 
@@ -285,6 +286,275 @@ __global__ __launch_bounds__(256) void search_by_projection_kernel(
     }
     int* M = match + (size_t)pr * cur_cap;
     for (int i = tid; i < nc; i += 256) M[i] = s.nulled[i] ? -2 : s.assign[i];
+    if (tid == 0) nmatches[pr] = s_nm;
+}
+
+// ---------------------------------------------------------------------------
+// SearchByProjection(CurrentFrame, LastFrame, th, bMono) on a two-camera
+// CurrentFrame (CurrentFrame.Nleft != -1, :1985-2153): every LastFrame point
+// is projected with CurrentFrame.mpCamera into the left image (x3Dc) and,
+// when the left pass did not `continue` (:2000-2026: behind the camera,
+// outside the image bounds, empty window), into the right image (x3Dr =
+// mTrl * x3Dc, no bounds test, mGridRight); no mvuRight test.  Both
+// assignments feed one rotation histogram (right entries at idx + Nleft).
+// mpCamera is Pinhole (:30-33) or KannalaBrandt8 (:33-48 of
+// CameraModels/KannalaBrandt8.cpp, glibc atan2f / cosf / sinf restated in
+// plvi_math.h).  Same schedule as the one-camera kernel, per side.
+struct CamModel {
+    int kb;  // 0 = Pinhole, 1 = KannalaBrandt8 (k1..k4 below)
+    float k0, k1, k2, k3;
+};
+
+__device__ __forceinline__ void cam_project(const plvi_proj_params& p, const CamModel& cm, float x, float y, float z,
+                                            float& u, float& v) {
+    if (!cm.kb) {  // Pinhole::project
+        u = p.fx * x / z + p.cx;
+        v = p.fy * y / z + p.cy;
+        return;
+    }
+    // KannalaBrandt8::project(const cv::Point3f&)
+    const float x2_plus_y2 = x * x + y * y;
+    const float theta = plvi::plvi_atan2f(__builtin_sqrtf(x2_plus_y2), z);
+    const float psi = plvi::plvi_atan2f(y, x);
+    const float theta2 = theta * theta;
+    const float theta3 = theta * theta2;
+    const float theta5 = theta3 * theta2;
+    const float theta7 = theta5 * theta2;
+    const float theta9 = theta7 * theta2;
+    const float r = theta + cm.k0 * theta3 + cm.k1 * theta5 + cm.k2 * theta7 + cm.k3 * theta9;
+    u = p.fx * r * plvi::plvi_cosf(psi) + p.cx;
+    v = p.fy * r * plvi::plvi_sinf(psi) + p.cy;
+}
+
+constexpr unsigned kScanSkip = 0xFFFFFFFFu;   // left pass `continue`d: no right pass either
+constexpr unsigned kScanNone = 0xFFFFFFFEu;   // window searched, no candidate (bestIdx2 == -1)
+
+// GetFeaturesInArea(u, v, radius, levels, bRight) + the candidate loop
+// (:2033-2058 / :2109-2125) of point i on one side.
+__device__ unsigned proj2_scan(const plvi_proj_params& p, const ProjLds& s, const unsigned char* blk, float u, float v,
+                               int nLastOctave, const uint8_t* __restrict__ mpd, const uint8_t* __restrict__ cdesc,
+                               bool left) {
+    const float radius = p.th * p.scale_factors[nLastOctave];
+    int minLevel, maxLevel;
+    if (p.forward) { minLevel = nLastOctave; maxLevel = -1; }
+    else if (p.backward) { minLevel = 0; maxLevel = nLastOctave; }
+    else { minLevel = nLastOctave - 1; maxLevel = nLastOctave + 1; }
+    const unsigned empty = left ? kScanSkip : kScanNone;
+    const int nMinCellX = max(0, (int)floorf((u - p.min_x - radius) * p.inv_w));
+    if (nMinCellX >= kGridCols) return empty;
+    const int nMaxCellX = min(kGridCols - 1, (int)ceilf((u - p.min_x + radius) * p.inv_w));
+    if (nMaxCellX < 0) return empty;
+    const int nMinCellY = max(0, (int)floorf((v - p.min_y - radius) * p.inv_h));
+    if (nMinCellY >= kGridRows) return empty;
+    const int nMaxCellY = min(kGridRows - 1, (int)ceilf((v - p.min_y + radius) * p.inv_h));
+    if (nMaxCellY < 0) return empty;
+    const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+    const uint4* dm = reinterpret_cast<const uint4*>(mpd);
+    const uint4 m0 = dm[0], m1 = dm[1];
+    int bestDist = 256, bestIdx2 = -1;
+    bool any = false;  // vIndices2 non-empty
+    for (int ix = nMinCellX; ix <= nMaxCellX; ++ix) {
+        const int k0 = s.cell_off[ix * kGridRows + nMinCellY], k1 = s.cell_off[ix * kGridRows + nMaxCellY + 1];
+        for (int k = k0; k < k1; ++k) {
+            const int i2 = s.cell_idx[k];
+            if (bCheckLevels) {
+                const int o = s.koct[i2];
+                if (o < minLevel) continue;
+                if (maxLevel >= 0 && o > maxLevel) continue;
+            }
+            const float distx = s.kx[i2] - u, disty = s.ky[i2] - v;
+            if (!(fabsf(distx) < radius && fabsf(disty) < radius)) continue;
+            any = true;
+            if (blk[i2]) continue;
+            const uint4* dc = reinterpret_cast<const uint4*>(cdesc + (size_t)32 * i2);
+            const uint4 c0 = dc[0], c1 = dc[1];
+            const int dist = __popc(m0.x ^ c0.x) + __popc(m0.y ^ c0.y) + __popc(m0.z ^ c0.z) + __popc(m0.w ^ c0.w) +
+                             __popc(m1.x ^ c1.x) + __popc(m1.y ^ c1.y) + __popc(m1.z ^ c1.z) + __popc(m1.w ^ c1.w);
+            if (dist < bestDist) {
+                bestDist = dist;
+                bestIdx2 = i2;
+            }
+        }
+    }
+    if (!any) return empty;
+    if (bestIdx2 < 0) return kScanNone;
+    return ((unsigned)bestDist << 16) | (unsigned)bestIdx2;
+}
+
+struct ProjSide {
+    ProjLds s;
+    const plvi_keypoint* K;
+    const uint8_t* desc;
+    int n;
+};
+
+__device__ void proj_side_load(ProjSide& d, unsigned char*& q, int cap, const uint8_t* blocked, const int* CO,
+                               const int* CI, int tid) {
+    d.s.kx = reinterpret_cast<float*>(q); q += 4 * cap;
+    d.s.ky = reinterpret_cast<float*>(q); q += 4 * cap;
+    d.s.assign = reinterpret_cast<int*>(q); q += 4 * cap;
+    d.s.cell_off = reinterpret_cast<int*>(q); q += 4 * (kGridCells + 1);
+    d.s.cell_idx = reinterpret_cast<unsigned short*>(q); q += 2 * cap;
+    d.s.koct = q; q += cap;
+    d.s.blocked = q; q += cap;
+    d.s.pre = q; q += cap;
+    d.s.nulled = q; q += cap;
+    q = reinterpret_cast<unsigned char*>(((uintptr_t)q + 15) & ~(uintptr_t)15);
+    for (int i = tid; i < d.n; i += 256) {
+        d.s.kx[i] = d.K[i].x;
+        d.s.ky[i] = d.K[i].y;
+        d.s.koct[i] = (unsigned char)d.K[i].octave;
+        const unsigned char b = blocked ? (blocked[i] != 0) : 0;
+        d.s.blocked[i] = b;
+        d.s.pre[i] = b;
+        d.s.nulled[i] = 0;
+        d.s.assign[i] = -1;
+    }
+    for (int c = tid; c <= kGridCells; c += 256) d.s.cell_off[c] = CO[c];
+    const int ncell = CO[kGridCells];
+    for (int k = tid; k < ncell; k += 256) d.s.cell_idx[k] = (unsigned short)CI[k];
+}
+
+__global__ __launch_bounds__(256) void search_by_projection2_kernel(
+    plvi_proj_params p, CamModel cm, const plvi_keypoint* __restrict__ lkps, const uint8_t* __restrict__ ldesc_all,
+    const int* __restrict__ l_n, int l_cap, const uint8_t* __restrict__ lblocked, const int* __restrict__ lcell_off_all,
+    const int* __restrict__ lcell_idx_all, const plvi_keypoint* __restrict__ rkps, const uint8_t* __restrict__ rdesc_all,
+    const int* __restrict__ r_n, int r_cap, const uint8_t* __restrict__ rblocked, const int* __restrict__ rcell_off_all,
+    const int* __restrict__ rcell_idx_all, const float* __restrict__ x3dc_all, const float* __restrict__ x3dr_all,
+    const int* __restrict__ loct_all, const float* __restrict__ lang_all, const uint8_t* __restrict__ mpdesc_all,
+    const uint8_t* __restrict__ lflags_all, const int* __restrict__ last_n, int last_cap, int* __restrict__ match_l,
+    int* __restrict__ match_r, int* __restrict__ nmatches) {
+    extern __shared__ __align__(16) unsigned char lds[];
+    const int pr = blockIdx.x, tid = threadIdx.x;
+    const int nl = min(last_n[pr], last_cap);
+    ProjSide S[2];
+    S[0].n = min(l_n[pr], l_cap);
+    S[1].n = min(r_n[pr], r_cap);
+    S[0].K = lkps + (size_t)pr * l_cap;
+    S[1].K = rkps + (size_t)pr * r_cap;
+    S[0].desc = ldesc_all + (size_t)pr * l_cap * 32;
+    S[1].desc = rdesc_all + (size_t)pr * r_cap * 32;
+    unsigned* best;          // [2][last_cap]
+    unsigned short* ent;     // [2 * last_cap] keypoint, [2 * last_cap] bin | side << 15
+    {
+        unsigned char* q = lds;
+        best = reinterpret_cast<unsigned*>(q); q += 8 * (size_t)last_cap;
+        ent = reinterpret_cast<unsigned short*>(q); q += 8 * (size_t)last_cap;
+        proj_side_load(S[0], q, l_cap, lblocked ? lblocked + (size_t)pr * l_cap : nullptr,
+                       lcell_off_all + (size_t)pr * (kGridCells + 1), lcell_idx_all + (size_t)pr * l_cap, tid);
+        proj_side_load(S[1], q, r_cap, rblocked ? rblocked + (size_t)pr * r_cap : nullptr,
+                       rcell_off_all + (size_t)pr * (kGridCells + 1), rcell_idx_all + (size_t)pr * r_cap, tid);
+    }
+    __shared__ int s_hist[kProjHisto], s_keep[3], s_ne, s_nm;
+    if (tid < kProjHisto) s_hist[tid] = 0;
+    __syncthreads();
+    const float* x3dc = x3dc_all + (size_t)pr * last_cap * 3;
+    const float* x3dr = x3dr_all + (size_t)pr * last_cap * 3;
+    const int* loct = loct_all + (size_t)pr * last_cap;
+    const uint8_t* mpdesc = mpdesc_all + (size_t)pr * last_cap * 32;
+    const uint8_t* lflags = lflags_all + (size_t)pr * last_cap;
+    // the projections of point i (left pass exits: invzc < 0, outside the bounds)
+    auto project = [&](int i, float& ul, float& vl, float& ur, float& vr) -> bool {
+        const float xc = x3dc[3 * i], yc = x3dc[3 * i + 1], zc = x3dc[3 * i + 2];
+        const float invzc = (float)(1.0 / (double)zc);
+        if (invzc < 0) return false;
+        cam_project(p, cm, xc, yc, zc, ul, vl);
+        if (ul < p.min_x || ul > p.max_x) return false;
+        if (vl < p.min_y || vl > p.max_y) return false;
+        cam_project(p, cm, x3dr[3 * i], x3dr[3 * i + 1], x3dr[3 * i + 2], ur, vr);
+        return true;
+    };
+    // phase 1: both sides of every point against the flags on entry
+    for (int i = tid; i < nl; i += 256) {
+        unsigned bl = kScanSkip, br = kScanSkip;
+        float ul, vl, ur, vr;
+        if ((lflags[i] & 1) && project(i, ul, vl, ur, vr)) {
+            const uint8_t* mpd = mpdesc + (size_t)32 * i;
+            bl = proj2_scan(p, S[0].s, S[0].s.pre, ul, vl, loct[i], mpd, S[0].desc, true);
+            if (bl != kScanSkip) br = proj2_scan(p, S[1].s, S[1].s.pre, ur, vr, loct[i], mpd, S[1].desc, false);
+        }
+        best[i] = bl;
+        best[last_cap + i] = br;
+    }
+    __syncthreads();
+    // phase 2: LastFrame order, left (:2060-2083) then right (:2127-2148)
+    if (tid == 0) {
+        const float factor = 1.0f / kProjHisto;
+        const float* lang = lang_all + (size_t)pr * last_cap;
+        int nm = 0, ne = 0;
+        for (int i = 0; i < nl; ++i) {
+            if (best[i] == kScanSkip) continue;
+            float ul, vl, ur, vr;
+            bool projected = false;
+            for (int c = 0; c < 2; ++c) {
+                ProjSide& A = S[c];
+                unsigned b = best[c * last_cap + i];
+                if (b == kScanSkip || b == kScanNone) continue;  // no unblocked candidate stays so
+                if (A.s.blocked[b & 0xFFFFu] != A.s.pre[b & 0xFFFFu]) {  // its best was taken meanwhile: re-scan
+                    if (!projected) projected = project(i, ul, vl, ur, vr);
+                    b = proj2_scan(p, A.s, A.s.blocked, c ? ur : ul, c ? vr : vl, loct[i], mpdesc + (size_t)32 * i,
+                                   A.desc, c == 0);
+                    if (b == kScanSkip || b == kScanNone) continue;
+                }
+                if ((int)(b >> 16) > kProjThHigh) continue;
+                const int i2 = (int)(b & 0xFFFFu);
+                A.s.assign[i2] = i;
+                A.s.blocked[i2] = (lflags[i] & 2) ? 1 : 0;  // the stored MapPoint's Observations() > 0
+                ++nm;
+                if (p.check_orientation) {
+                    float rot = lang[i] - A.K[i2].angle;
+                    if (rot < 0.0f) rot += 360.0f;
+                    int bin = (int)roundf(rot * factor);
+                    if (bin == kProjHisto) bin = 0;
+                    ent[2 * last_cap + ne] = (unsigned short)(bin | c << 15);
+                    ent[ne++] = (unsigned short)i2;
+                    s_hist[bin]++;
+                }
+            }
+        }
+        s_ne = ne;
+        s_nm = nm;
+        int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;  // ComputeThreeMaxima (:2304-2345)
+        for (int b = 0; b < kProjHisto; b++) {
+            const int c = s_hist[b];
+            if (c > max1) {
+                max3 = max2; max2 = max1; max1 = c;
+                ind3 = ind2; ind2 = ind1; ind1 = b;
+            } else if (c > max2) {
+                max3 = max2; max2 = c;
+                ind3 = ind2; ind2 = b;
+            } else if (c > max3) {
+                max3 = c;
+                ind3 = b;
+            }
+        }
+        if (max2 < 0.1f * (float)max1) {
+            ind2 = -1;
+            ind3 = -1;
+        } else if (max3 < 0.1f * (float)max1) {
+            ind3 = -1;
+        }
+        s_keep[0] = ind1; s_keep[1] = ind2; s_keep[2] = ind3;
+    }
+    __syncthreads();
+    // phase 3: entries in dropped bins set mvpMapPoints[idx] = NULL (:2155-2175)
+    if (p.check_orientation) {
+        const int ne = s_ne;
+        int dropped = 0;
+        for (int e = tid; e < ne; e += 256) {
+            const int code = ent[2 * last_cap + e], bin = code & 0x7FFF;
+            if (bin != s_keep[0] && bin != s_keep[1] && bin != s_keep[2]) {
+                S[code >> 15].s.nulled[ent[e]] = 1;
+                ++dropped;
+            }
+        }
+        if (dropped) atomicSub(&s_nm, dropped);
+        __syncthreads();
+    }
+    int* ML = match_l + (size_t)pr * l_cap;
+    int* MR = match_r + (size_t)pr * r_cap;
+    for (int i = tid; i < S[0].n; i += 256) ML[i] = S[0].s.nulled[i] ? -2 : S[0].s.assign[i];
+    for (int i = tid; i < S[1].n; i += 256) MR[i] = S[1].s.nulled[i] ? -2 : S[1].s.assign[i];
     if (tid == 0) nmatches[pr] = s_nm;
 }
 
@@ -763,6 +1033,13 @@ static size_t local2_smem(int l_cap, int r_cap, int mp_cap) {
     return 16 * (size_t)mp_cap + side(l_cap) + side(r_cap) + 64;
 }
 
+static size_t proj2_smem(int l_cap, int r_cap, int last_cap) {
+    auto side = [](int cap) {
+        return ((size_t)cap * (4 + 4 + 4 + 2 + 1 + 1 + 1 + 1) + 4 * (kGridCells + 1) + 15) & ~size_t(15);
+    };
+    return 16 * (size_t)last_cap + side(l_cap) + side(r_cap) + 64;
+}
+
 static size_t proj_smem(int cur_cap, int last_cap) {
     return (size_t)cur_cap * (4 + 4 + 4 + 2 + 1 + 1 + 1 + 1) + (size_t)last_cap * (4 + 4) + 4 * (kGridCells + 1) + 64;
 }
@@ -1112,6 +1389,102 @@ extern "C" int plvi_search_local_stereo(const plvi_local_params* p, const plvi_k
         reinterpret_cast<const int*>(B + off[oL]), reinterpret_cast<const float*>(B + off[oPR]),
         reinterpret_cast<const int*>(B + off[oLR]), B + off[oMD], dN + 2, mc, reinterpret_cast<int*>(B + off[oM]),
         reinterpret_cast<int*>(B + off[rM]), dN + 3, nullptr);
+    if (rc) return rc;
+    PLVI_CHECK(hipDeviceSynchronize());
+    int nmt = 0;
+    if (n) PLVI_CHECK(hipMemcpy(match, B + off[oM], 4 * (size_t)n, hipMemcpyDeviceToHost));
+    if (n_r) PLVI_CHECK(hipMemcpy(match_r, B + off[rM], 4 * (size_t)n_r, hipMemcpyDeviceToHost));
+    PLVI_CHECK(hipMemcpy(&nmt, dN + 3, 4, hipMemcpyDeviceToHost));
+    return nmt;
+}
+
+extern "C" int plvi_search_by_projection_stereo_batch(
+    int n_pairs, const plvi_proj_params* p, const float* kb8, const plvi_keypoint* d_kps, const uint8_t* d_desc,
+    const int* d_n, int cap, const uint8_t* d_blocked, const int* d_cell_off, const int* d_cell_idx,
+    const plvi_keypoint* d_kps_r, const uint8_t* d_desc_r, const int* d_n_r, int cap_r, const uint8_t* d_blocked_r,
+    const int* d_cell_off_r, const int* d_cell_idx_r, const float* d_x3dc, const float* d_x3dr,
+    const int* d_last_octave, const float* d_last_angle, const uint8_t* d_mp_desc, const uint8_t* d_last_flags,
+    const int* d_last_n, int last_cap, int* d_match, int* d_match_r, int* d_nmatches, void* stream) {
+    if (!p || n_pairs < 0 || cap < 1 || cap_r < 1 || last_cap < 1 || cap > 65535 || cap_r > 65535 ||
+        last_cap > 65535)
+        return PLVI_E_BADARG;
+    if (p->nlevels < 1 || p->nlevels > 16) return PLVI_E_BADARG;
+    if (n_pairs == 0) return PLVI_OK;
+    const size_t smem = proj2_smem(cap, cap_r, last_cap);
+    if (smem > 160 * 1024) return PLVI_E_CAPACITY;
+    CamModel cm{0, 0.f, 0.f, 0.f, 0.f};
+    if (kb8) cm = CamModel{1, kb8[0], kb8[1], kb8[2], kb8[3]};
+    PLVI_CHECK(hipFuncSetAttribute((const void*)search_by_projection2_kernel,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
+    hipLaunchKernelGGL(search_by_projection2_kernel, dim3(n_pairs), dim3(256), smem, (hipStream_t)stream, *p, cm, d_kps,
+                       d_desc, d_n, cap, d_blocked, d_cell_off, d_cell_idx, d_kps_r, d_desc_r, d_n_r, cap_r,
+                       d_blocked_r, d_cell_off_r, d_cell_idx_r, d_x3dc, d_x3dr, d_last_octave, d_last_angle, d_mp_desc,
+                       d_last_flags, d_last_n, last_cap, d_match, d_match_r, d_nmatches);
+    PLVI_CHECK(hipGetLastError());
+    return PLVI_OK;
+}
+
+// One pair from host memory, synchronous (both grids built on the device).
+extern "C" int plvi_search_by_projection_stereo(const plvi_proj_params* p, const float* kb8, const plvi_keypoint* kps,
+                                                const uint8_t* desc, int n, const uint8_t* blocked,
+                                                const plvi_keypoint* kps_r, const uint8_t* desc_r, int n_r,
+                                                const uint8_t* blocked_r, const float* x3dc, const float* x3dr,
+                                                const int* last_octave, const float* last_angle,
+                                                const uint8_t* mp_desc, const uint8_t* last_flags, int n_last,
+                                                int* match, int* match_r) {
+    if (!p || n < 0 || n_r < 0 || n_last < 0) return PLVI_E_BADARG;
+    if ((n > 0 && (!kps || !desc || !match)) || (n_r > 0 && (!kps_r || !desc_r || !match_r))) return PLVI_E_BADARG;
+    if (n_last > 0 && (!x3dc || !x3dr || !last_octave || !last_angle || !mp_desc || !last_flags)) return PLVI_E_BADARG;
+    if (n_last > 0)
+        for (int i = 0; i < n_last; ++i)
+            if ((last_flags[i] & 1) && (last_octave[i] < 0 || last_octave[i] >= p->nlevels)) return PLVI_E_BADARG;
+    const int cl = std::max(n, 1), cr = std::max(n_r, 1), lc = std::max(n_last, 1);
+    std::vector<size_t> off;
+    size_t tot = 0;
+    auto put = [&](size_t bytes) {
+        off.push_back(tot);
+        tot += (bytes + 255) & ~size_t(255);
+        return off.size() - 1;
+    };
+    const size_t oK = put(sizeof(plvi_keypoint) * cl), oD = put(32 * (size_t)cl), oB = put(cl);
+    const size_t oCO = put(4 * (size_t)(kGridCells + 1)), oCI = put(4 * (size_t)cl), oM = put(4 * (size_t)cl);
+    const size_t rK = put(sizeof(plvi_keypoint) * cr), rD = put(32 * (size_t)cr), rB = put(cr);
+    const size_t rCO = put(4 * (size_t)(kGridCells + 1)), rCI = put(4 * (size_t)cr), rM = put(4 * (size_t)cr);
+    const size_t oX = put(12 * (size_t)lc), oXR = put(12 * (size_t)lc), oO = put(4 * (size_t)lc),
+                 oA = put(4 * (size_t)lc), oMD = put(32 * (size_t)lc), oF = put(lc), oN = put(16);
+    DevBuf d;
+    if (d.alloc(tot)) return PLVI_E_HIP;
+    uint8_t* B = d.as<uint8_t>();
+    PLVI_CHECK(hipMemset(B, 0, tot));
+    auto up = [&](size_t slot, const void* src, size_t bytes) -> int {
+        if (src && bytes) PLVI_CHECK(hipMemcpy(B + off[slot], src, bytes, hipMemcpyHostToDevice));
+        return PLVI_OK;
+    };
+    int rc = up(oK, kps, sizeof(plvi_keypoint) * n) | up(oD, desc, 32 * (size_t)n) | up(oB, blocked, n) |
+             up(rK, kps_r, sizeof(plvi_keypoint) * n_r) | up(rD, desc_r, 32 * (size_t)n_r) | up(rB, blocked_r, n_r) |
+             up(oX, x3dc, 12 * (size_t)n_last) | up(oXR, x3dr, 12 * (size_t)n_last) |
+             up(oO, last_octave, 4 * (size_t)n_last) | up(oA, last_angle, 4 * (size_t)n_last) |
+             up(oMD, mp_desc, 32 * (size_t)n_last) | up(oF, last_flags, n_last);
+    if (rc) return PLVI_E_HIP;
+    int counts[4] = {n, n_r, n_last, 0};
+    PLVI_CHECK(hipMemcpy(B + off[oN], counts, 16, hipMemcpyHostToDevice));
+    int* dN = reinterpret_cast<int*>(B + off[oN]);
+    plvi_grid_params gp{p->min_x, p->min_y, p->inv_w, p->inv_h};
+    rc = plvi_assign_grid_batch(reinterpret_cast<const plvi_keypoint*>(B + off[oK]), dN, cl, 1, &gp,
+                                reinterpret_cast<int*>(B + off[oCO]), reinterpret_cast<int*>(B + off[oCI]), nullptr);
+    if (rc) return rc;
+    rc = plvi_assign_grid_batch(reinterpret_cast<const plvi_keypoint*>(B + off[rK]), dN + 1, cr, 1, &gp,
+                                reinterpret_cast<int*>(B + off[rCO]), reinterpret_cast<int*>(B + off[rCI]), nullptr);
+    if (rc) return rc;
+    rc = plvi_search_by_projection_stereo_batch(
+        1, p, kb8, reinterpret_cast<const plvi_keypoint*>(B + off[oK]), B + off[oD], dN, cl, B + off[oB],
+        reinterpret_cast<const int*>(B + off[oCO]), reinterpret_cast<const int*>(B + off[oCI]),
+        reinterpret_cast<const plvi_keypoint*>(B + off[rK]), B + off[rD], dN + 1, cr, B + off[rB],
+        reinterpret_cast<const int*>(B + off[rCO]), reinterpret_cast<const int*>(B + off[rCI]),
+        reinterpret_cast<const float*>(B + off[oX]), reinterpret_cast<const float*>(B + off[oXR]),
+        reinterpret_cast<const int*>(B + off[oO]), reinterpret_cast<const float*>(B + off[oA]), B + off[oMD],
+        B + off[oF], dN + 2, lc, reinterpret_cast<int*>(B + off[oM]), reinterpret_cast<int*>(B + off[rM]), dN + 3,
+        nullptr);
     if (rc) return rc;
     PLVI_CHECK(hipDeviceSynchronize());
     int nmt = 0;

@@ -232,6 +232,9 @@ def _declare(lib):
         "plvi_line_search_init_batch": ([V, V, I, V, V, I, I, V, V, V, V, V], I),
         "plvi_search_local_batch": ([I, V, V, V, V, I, V, V, V, V, V, V, V, V, V, I, V, V, V], I),
         "plvi_search_local": ([V, V, V, I, V, V, V, V, V, V, I, V], I),
+        "plvi_search_by_projection_stereo_batch": ([I, V, V, V, V, V, I, V, V, V, V, V, V, I, V, V, V, V, V, V, V, V,
+                                                    V, V, I, V, V, V, V], I),
+        "plvi_search_by_projection_stereo": ([V, V, V, V, I, V, V, V, I, V, V, V, V, V, V, V, I, V, V], I),
         "plvi_search_local_stereo_batch": ([I, V, V, V, V, I, V, V, V, V, V, V, V, I, V, V, V, V, V, V, V, V, V, V,
                                             V, I, V, V, V, V], I),
         "plvi_search_local_stereo": ([V, V, V, I, V, V, V, V, I, V, V, V, V, V, V, V, V, I, V, V], I),
@@ -831,6 +834,37 @@ class ORBmatcher:
                                                 _ptr(fl), _ptr(pr), _ptr(lv), _ptr(md), len(fl), _ptr(out)),
                     "plvi_search_local")
         return nm, out[:len(k)]
+
+    def SearchByProjectionStereo(self, params, kps, desc, kps_r, desc_r, x3dc, x3dr, last_octave, last_angle,
+                                 mp_desc, last_flags, kb8=None, blocked=None, blocked_r=None):
+        """SearchByProjection(CurrentFrame, LastFrame, th, bMono) with a two-camera CurrentFrame
+        (CurrentFrame.Nleft != -1, src/ORBmatcher.cc:1985-2175), rotation check = checkOri of this matcher.
+        params: ProjParams (camera fx/fy/cx/cy, bounds, grid, th, forward / backward, scale factors); kb8:
+        KannalaBrandt8 k1..k4 (None = Pinhole); kps / desc: mvKeys and descriptor rows 0..Nleft-1; kps_r /
+        desc_r: mvKeysRight and rows Nleft..; per LastFrame point: x3Dc, x3Dr = mTrl * x3Dc, octave, angle,
+        descriptor, flags (bit0 MapPoint and not an outlier, bit1 Observations() > 0).  Returns (nmatches,
+        match, match_r) with -2 = set to NULL by the rotation filter."""
+        params.check_orientation = int(self.check_orientation)
+        k = np.ascontiguousarray(kps).view(KEYPOINT_DTYPE)
+        kr = np.ascontiguousarray(kps_r).view(KEYPOINT_DTYPE)
+        d = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        dr = np.ascontiguousarray(desc_r, np.uint8).reshape(-1, 32)
+        x3 = np.ascontiguousarray(x3dc, np.float32).reshape(-1, 3)
+        x3r = np.ascontiguousarray(x3dr, np.float32).reshape(-1, 3)
+        lo = np.ascontiguousarray(last_octave, np.int32)
+        la = np.ascontiguousarray(last_angle, np.float32)
+        md = np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32)
+        lf = np.ascontiguousarray(last_flags, np.uint8)
+        opt = lambda a, t: None if a is None else np.ascontiguousarray(a, t)  # noqa: E731
+        kb, cb, cbr = opt(kb8, np.float32), opt(blocked, np.uint8), opt(blocked_r, np.uint8)
+        pp = lambda a: None if a is None else _ptr(a)  # noqa: E731
+        out = np.full(max(len(k), 1), -1, np.int32)
+        outr = np.full(max(len(kr), 1), -1, np.int32)
+        nm = _check(self._lib.plvi_search_by_projection_stereo(
+            ctypes.byref(params), pp(kb), _ptr(k), _ptr(d), len(k), pp(cb), _ptr(kr), _ptr(dr), len(kr), pp(cbr),
+            _ptr(x3), _ptr(x3r), _ptr(lo), _ptr(la), _ptr(md), _ptr(lf), len(lf), _ptr(out), _ptr(outr)),
+            "plvi_search_by_projection_stereo")
+        return nm, out[:len(k)], outr[:len(kr)]
 
     def SearchByProjectionLocalStereo(self, params, kps, desc, kps_r, desc_r, mp_flags, mp_proj, mp_level,
                                       mp_proj_r, mp_level_r, mp_desc, blocked=None, blocked_r=None, l2r=None,

@@ -472,6 +472,39 @@ def search_by_projection(case, th, forward=0, backward=0, check_ori=1):
     return n, out[:len(kx)]
 
 
+def search_by_projection_stereo(case, th, forward=0, backward=0, check_ori=1):
+    """Two-camera SearchByProjection(CurrentFrame, LastFrame, th, bMono) restatement
+    -> (nmatches, match_left, match_right)."""
+    lib = load()
+    V, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    lib.oracle_search_by_projection2.argtypes = [I, V, V, V, V, I, V, V, V, V, V, V, F, F, F, F, F, F, V, F, F, F,
+                                                 F, V, I, V, V, V, V, V, V, F, I, I, I, V]
+    lib.oracle_search_by_projection2.restype = I
+    c = case
+    f32 = lambda a: np.ascontiguousarray(a, np.float32)  # noqa: E731
+    i32 = lambda a: np.ascontiguousarray(a, np.int32)  # noqa: E731
+    kl, kr = c["kps"], c["kps_r"]
+    nl, nr = len(kl), len(kr)
+    lx, ly, lo, la = f32(kl["x"]), f32(kl["y"]), i32(kl["octave"]), f32(kl["angle"])
+    rx, ry, ro, ra = f32(kr["x"]), f32(kr["y"]), i32(kr["octave"]), f32(kr["angle"])
+    desc = np.ascontiguousarray(np.concatenate([c["desc"], c["desc_r"]]), np.uint8)
+    blk = np.ascontiguousarray(np.concatenate([c["blocked"], c["blocked_r"]]), np.uint8)
+    min_x, max_x, min_y, max_y, inv_w, inv_h = c["grid"]
+    sf = f32(c["scale_factors"])
+    fx, fy, cx, cy, _ = c["camera"]
+    kb = None if c.get("kb8") is None else f32(c["kb8"])
+    lf = np.ascontiguousarray(c["flags"], np.uint8)
+    x3, x3r = f32(c["x3dc"]), f32(c["x3dr"])
+    oc, an = i32(c["last_octave"]), f32(c["last_angle"])
+    md = np.ascontiguousarray(c["mp_desc"], np.uint8)
+    out = np.full(max(nl + nr, 1), -1, np.int32)
+    n = lib.oracle_search_by_projection2(nl, _p(lx), _p(ly), _p(lo), _p(la), nr, _p(rx), _p(ry), _p(ro), _p(ra),
+                                         _p(desc), _p(blk), min_x, max_x, min_y, max_y, inv_w, inv_h, _p(sf), fx, fy,
+                                         cx, cy, None if kb is None else _p(kb), len(lf), _p(lf), _p(x3), _p(x3r),
+                                         _p(oc), _p(an), _p(md), th, forward, backward, check_ori, _p(out))
+    return n, out[:nl], out[nl:nl + nr]
+
+
 def search_reloc(case, th, orb_dist, check_ori=1):
     """ORBmatcher::SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist) restatement
     -> (nmatches, match)."""

@@ -172,6 +172,107 @@ def projection_case(seed, n_cur=1000, n_last=900, W=752, H=480, uright=False, du
     return case
 
 
+KB8_TUMVI = (np.float32(190.978), np.float32(190.973), np.float32(254.932), np.float32(256.897),
+             np.float32(0.0034823894), np.float32(0.00071503044), np.float32(-0.0020532361), np.float32(0.00020293143))
+
+
+def _kb8_unproject(u, v, cam):
+    """Rays (x/z, y/z) of pixels under KannalaBrandt8 (Newton on r(theta) = theta_d, float64)."""
+    fx, fy, cx, cy, k1, k2, k3, k4 = (float(t) for t in cam)
+    px, py = (u - cx) / fx, (v - cy) / fy
+    td = np.minimum(np.hypot(px, py), np.pi / 2 - 1e-3)
+    th = td.copy()
+    for _ in range(20):
+        t2 = th * th
+        f = th * (1 + k1 * t2 + k2 * t2 ** 2 + k3 * t2 ** 3 + k4 * t2 ** 4) - td
+        fd = 1 + 3 * k1 * t2 + 5 * k2 * t2 ** 2 + 7 * k3 * t2 ** 3 + 9 * k4 * t2 ** 4
+        th = th - f / fd
+    sc = np.where(td > 1e-8, np.tan(th) / np.maximum(td, 1e-12), 1.0)
+    return px * sc, py * sc
+
+
+def _kb8_project(x3, cam):
+    fx, fy, cx, cy, k1, k2, k3, k4 = (float(t) for t in cam)
+    x, y, z = x3[:, 0].astype(np.float64), x3[:, 1].astype(np.float64), x3[:, 2].astype(np.float64)
+    th = np.arctan2(np.hypot(x, y), z)
+    psi = np.arctan2(y, x)
+    r = th + k1 * th ** 3 + k2 * th ** 5 + k3 * th ** 7 + k4 * th ** 9
+    return fx * r * np.cos(psi) + cx, fy * r * np.sin(psi) + cy
+
+
+def projection_stereo_case(seed, n_left=900, n_right=850, n_last=800, kb8=True, dup=0.05):
+    """Two-camera SearchByProjection(CurrentFrame, LastFrame) input (CurrentFrame.Nleft != -1): a
+    KannalaBrandt8 rig (TUM-VI-like intrinsics, 512 x 512, or a Pinhole one), left / right keypoints with
+    descriptors, LastFrame points whose x3Dc project near a left keypoint (70 %) and whose x3Dr = Rrl x3Dc +
+    trl project near a right keypoint placed there for 60 % of them (descriptor = the same source with flipped
+    bits), a global 10-degree rotation, some points behind the camera / outliers / with Observations() == 0,
+    pre-blocked keypoints on both sides, `dup` aimed at another point's keypoints."""
+    from plvi import KEYPOINT_DTYPE
+    rng = np.random.default_rng(seed)
+    W = H = 512
+    cam = KB8_TUMVI if kb8 else (np.float32(190.978), np.float32(190.973), np.float32(254.932),
+                                 np.float32(256.897))
+
+    def kset(n):
+        k = np.zeros(n, KEYPOINT_DTYPE)
+        k["x"] = rng.uniform(-4, W + 4, n).astype(np.float32)
+        k["y"] = rng.uniform(-4, H + 4, n).astype(np.float32)
+        k["octave"] = np.minimum(rng.geometric(0.35, n) - 1, 7)
+        k["angle"] = rng.uniform(0, 360, n).astype(np.float32)
+        k["size"] = 31
+        k["class_id"] = -1
+        return k
+    kl, kr = kset(n_left), kset(n_right)
+    dl = rng.integers(0, 256, (n_left, 32), dtype=np.uint8)
+    dr = rng.integers(0, 256, (n_right, 32), dtype=np.uint8)
+    near = rng.random(n_last) < 0.7
+    src = rng.integers(0, n_left, n_last)
+    nd = int(dup * n_last)
+    src[:nd] = src[nd:2 * nd]
+    u = np.where(near, kl["x"][src] + rng.normal(0, 2.0, n_last), rng.uniform(0, W, n_last))
+    v = np.where(near, kl["y"][src] + rng.normal(0, 2.0, n_last), rng.uniform(0, H, n_last))
+    z = rng.uniform(1.0, 20.0, n_last)
+    if kb8:
+        rx_, ry_ = _kb8_unproject(u, v, cam)
+    else:
+        rx_, ry_ = (u - float(cam[2])) / float(cam[0]), (v - float(cam[3])) / float(cam[1])
+    x3 = np.stack([rx_ * z, ry_ * z, z], 1)
+    x3[rng.random(n_last) < 0.02] *= -1
+    x3 = x3.astype(np.float32)
+    a = np.deg2rad(2.0)
+    R = np.array([[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]])
+    x3r = (x3.astype(np.float64) @ R.T + np.array([-0.11, 0.002, 0.001])).astype(np.float32)
+    if kb8:
+        ur, vr = _kb8_project(x3r, cam)
+    else:
+        ur = float(cam[0]) * x3r[:, 0] / x3r[:, 2] + float(cam[2])
+        vr = float(cam[1]) * x3r[:, 1] / x3r[:, 2] + float(cam[3])
+    # right keypoints at the right projections of 60 % of the near points
+    put = np.nonzero(near & (rng.random(n_last) < 0.6) & (x3[:, 2] > 0))[0][:n_right]
+    slots = rng.choice(n_right, len(put), replace=False)
+    kr["x"][slots] = (ur[put] + rng.normal(0, 1.5, len(put))).astype(np.float32)
+    kr["y"][slots] = (vr[put] + rng.normal(0, 1.5, len(put))).astype(np.float32)
+    kr["octave"][slots] = kl["octave"][src[put]]
+    kr["angle"][slots] = np.mod(kl["angle"][src[put]] + rng.normal(0, 3, len(put)), 360).astype(np.float32)
+    bits = np.unpackbits(dl[src[put]], axis=1)
+    bits ^= (rng.random(bits.shape) < 0.04).astype(np.uint8)
+    dr[slots] = np.packbits(bits, axis=1)
+    oct_ = np.clip(np.where(near, kl["octave"][src] + rng.integers(-1, 2, n_last), rng.integers(0, 8, n_last)), 0, 7)
+    bits = np.unpackbits(dl[src], axis=1)
+    bits ^= (rng.random(bits.shape) < 0.05).astype(np.uint8)
+    mp = np.where(near[:, None], np.packbits(bits, axis=1), rng.integers(0, 256, (n_last, 32), dtype=np.uint8))
+    ang = np.mod(kl["angle"][src] + 10 + rng.normal(0, 5, n_last), 360).astype(np.float32)
+    flags = ((rng.random(n_last) < 0.92).astype(np.uint8) | ((rng.random(n_last) < 0.85).astype(np.uint8) << 1))
+    cols, rows = 64, 48
+    grid = (np.float32(0), np.float32(W), np.float32(0), np.float32(H), np.float32(cols / W), np.float32(rows / H))
+    return {"kps": kl, "desc": dl, "kps_r": kr, "desc_r": dr,
+            "blocked": (rng.random(n_left) < 0.05).astype(np.uint8),
+            "blocked_r": (rng.random(n_right) < 0.05).astype(np.uint8), "grid": grid,
+            "scale_factors": orb_scale_factors(), "x3dc": x3, "x3dr": x3r, "flags": flags,
+            "last_octave": oct_.astype(np.int32), "last_angle": ang, "mp_desc": mp.astype(np.uint8),
+            "camera": tuple(cam[:4]) + (np.float32(0.0),), "kb8": np.array(cam[4:], np.float32) if kb8 else None}
+
+
 def reloc_case(seed, n_cur=1000, n_kf=800, W=752, H=480, dup=0.08, pre_blocked=0.3):
     """Synthetic relocalization-search input (ORBmatcher::SearchByProjection(Frame&, KeyFrame*, sAlreadyFound,
     th, ORBdist), src/ORBmatcher.cc:2180-2300): current-frame keypoints (mvKeysUn) with descriptors, ~30 %
