@@ -79,7 +79,7 @@ struct LinePipeline {
     hipStream_t critStream = nullptr;  // frame schedule: prep -> grow -> describe
     hipStream_t crit2 = nullptr;       // frame schedule: octave-1 region growing (split mode)
     hipStream_t octStream = nullptr;   // small batches: prep + growth of octaves >= 1 beside octave 0's
-    bool orbAfterPrep = false;
+    int orbAfterPrep = 1;
     std::vector<LineOctDev> oct;
     std::vector<float> scaleF, invScaleF;
     double SCALE = 0.8, prec = 0, rho = 0, min_length = 0;
@@ -177,13 +177,16 @@ struct LinePipeline {
             PLVI_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
             const char* e1 = getenv("PLVI_STREAM_PRIO");
             const bool prio = !e1 || atoi(e1) != 0;
-            // PLVI_ORB_AFTER_PREP (default 1): ORB waits for the LSD prep.  With
-            // the faster ORB chain of r03 the pyramid otherwise ends while the
-            // prep still runs and blur + FAST shares the CUs with it (9-12 ms
-            // instead of 7.4 per 3072 frames); the step time is the same either
-            // way (region growing waits for blur + FAST from 1024 frames on)
+            // PLVI_ORB_AFTER_PREP: ORB waits for the LSD prep -- 1 (default) in
+            // batches below 1024 frames, 2 in every batch, 0 never.  With one
+            // 3072-frame batch in flight waiting is ~1 % faster (the pyramid
+            // otherwise ends while the prep still runs and blur + FAST shares
+            // the CUs with it); with two in flight (bench default) starting ORB
+            // at once is 2-3 % faster (47.9K vs 46.6K FPS, 47.3K vs 46.2K,
+            // profiles/r04/ab_sched_inflight2.txt): the next batch's pyramid and
+            // blur + FAST no longer wait for its prep while the other batch grows
             const char* e2 = getenv("PLVI_ORB_AFTER_PREP");
-            orbAfterPrep = !e2 || atoi(e2) != 0;
+            orbAfterPrep = e2 ? atoi(e2) : 1;
             // PLVI_GROW_AFTER_BLUR=0: region growing starts right after the prep
             // (default 1: it waits for the ORB blur + FAST launch, whose 81-VGPR /
             // 9 KB-LDS waves cannot share a CU with the region-growing waves; the
@@ -670,7 +673,7 @@ struct LinePipeline {
             launch_grow(nf, 1, nOct - 1, octStream);
             PLVI_CHECK(hipEventRecord(evGrow2, octStream));
         }
-        hipEvent_t auxStart = orbAfterPrep ? evPrep : evFork;
+        hipEvent_t auxStart = (orbAfterPrep >= 2 || (orbAfterPrep == 1 && nf < 1024)) ? evPrep : evFork;
         PLVI_CHECK(hipStreamWaitEvent(aux[0], auxStart, 0));
         // only a batch whose region-growing waves fill the SIMDs (>= 2 per SIMD
         // from 1024 frames on) starves blur + FAST; a small batch is latency-bound

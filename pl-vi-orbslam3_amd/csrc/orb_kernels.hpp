@@ -1396,25 +1396,51 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
 // raster within a cell).  One wave per (node, level, frame).  Output level
 // keypoint (x, y, response) in level coordinates.
 // ---------------------------------------------------------------------------
+#ifndef PLVI_BEST_NODES
+#define PLVI_BEST_NODES 1
+#endif
+constexpr int kBestNodes = PLVI_BEST_NODES;  // nodes per wave (the grid's x extent is nodeCapMax / kBestNodes)
+
+__device__ __forceinline__ void orb_node_best_one(const OrbLevelDev& lv, uint8_t* __restrict__ Cm,
+                                                  const uint8_t* __restrict__ cthr, int thrFrame, int f, const short4 r,
+                                                  float4* __restrict__ out);
+
 __global__ __launch_bounds__(64) void orb_node_best_kernel(const OrbLevelDev* __restrict__ lvs,
                                                            uint8_t* __restrict__ cand,
                                                            const uint8_t* __restrict__ cthr, int thrFrame,
                                                            const short4* __restrict__ rects,
                                                            const int* __restrict__ rect_cnt, int nodeCapMax, int L,
                                                            float4* __restrict__ lvkp, int kpCapFrame) {
-    const int node = blockIdx.x, l = blockIdx.y, f = blockIdx.z;
+    const int l = blockIdx.y, f = blockIdx.z;
     const int ncnt = rect_cnt[(size_t)f * L + l];
-    if (node >= ncnt) return;
     const OrbLevelDev& lv = lvs[l];
-    const short4 r = rects[((size_t)f * L + l) * nodeCapMax + node];
     uint8_t* Cm = cand + lv.boff + (size_t)f * lv.bplane;
+    for (int k = 0; k < kBestNodes; ++k) {
+        const int node = blockIdx.x * kBestNodes + k;
+        if (node >= ncnt) return;
+        orb_node_best_one(lv, Cm, cthr, thrFrame, f, rects[((size_t)f * L + l) * nodeCapMax + node],
+                          lvkp + (size_t)f * kpCapFrame + lv.kpOff + node);
+    }
+}
+
+__device__ __forceinline__ void orb_node_best_one(const OrbLevelDev& lv, uint8_t* __restrict__ Cm,
+                                                  const uint8_t* __restrict__ cthr, int thrFrame, int f, const short4 r,
+                                                  float4* __restrict__ out) {
     const int lane = threadIdx.x;
     const int rx0 = r.x, ry0 = r.y, rx1 = r.z, ry1 = r.w;
     const int wdt = rx1 - rx0;
     unsigned long long best = 0;
     const int total = wdt * (ry1 - ry0);
-    for (int i = lane; i < total; i += 64) {
-        const int yy = ry0 + i / wdt, xx = rx0 + i % wdt;
+    // i = lane + 64 t walks the rectangle row-major; (yy, xx) advance by
+    // 64 = q rows + rr columns per step (no division in the loop)
+    const int wd = max(wdt, 1);  // (an empty rectangle has total 0)
+    const int q = 64 / wd, rr = 64 - q * wd;
+    int yy = ry0 + lane / wd, xx = rx0 + lane % wd;
+    for (int i = lane; i < total; i += 64, yy += q, xx += rr) {
+        if (xx >= rx1) {
+            xx -= wdt;
+            ++yy;
+        }
         uint8_t* cp = Cm + (size_t)(lv.minB + yy) * lv.bpitch + lv.minB + xx;
         const int resp = *cp;
         if (!resp) continue;
@@ -1434,8 +1460,7 @@ __global__ __launch_bounds__(64) void orb_node_best_kernel(const OrbLevelDev* __
         const unsigned key = 0xFFFFFFFFu - (unsigned)(best & 0xFFFFFFFFu);
         const unsigned xx = key % (unsigned)lv.rw;
         const unsigned yy = (key / (unsigned)lv.rw) % (unsigned)lv.rh;
-        lvkp[(size_t)f * kpCapFrame + lv.kpOff + node] =
-            make_float4((float)(xx + lv.minB), (float)(yy + lv.minB), (float)(best >> 32), 0.f);
+        *out = make_float4((float)(xx + lv.minB), (float)(yy + lv.minB), (float)(best >> 32), 0.f);
     }
 }
 

@@ -468,7 +468,8 @@ struct OrbPipeline {
         mark(4, st);
         if (const int hrc = hook(4, st)) return hrc;
         // K5 best per node
-        hipLaunchKernelGGL(orb_node_best_kernel, dim3(nodeCapMax, L, nf), dim3(64), 0, st, d_lv.as<OrbLevelDev>(),
+        hipLaunchKernelGGL(orb_node_best_kernel, dim3((nodeCapMax + kBestNodes - 1) / kBestNodes, L, nf), dim3(64), 0, st,
+                           d_lv.as<OrbLevelDev>(),
                            Cd, (const uint8_t*)Ct, thrFrame, (const short4*)rects.as<short4>(), (const int*)rectCnt.as<int>(),
                            nodeCapMax, L, lvkp.as<float4>(), kpCapFrame);
         mark(5, st);
