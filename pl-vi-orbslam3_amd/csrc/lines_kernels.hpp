@@ -420,9 +420,10 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
     unsigned long long s_setup = 0, s_round = 0, s_rect = 0, n_seed = 0, n_block = 0, n_round = 0, n_rpt = 0,
                        n_commit = 0;
     unsigned long long s_ph[4] = {0, 0, 0, 0};
-    unsigned long long n_dy[3] = {0, 0, 0};
+    unsigned long long s_scan = 0, s_seed = 0, s_init = 0;  // seed scan, per-seed start, init
     constexpr bool do_stats = STATS;  // diagnostic variant only (keeps SGPRs free in the product kernel)
     const unsigned long long t_begin = do_stats ? __builtin_amdgcn_s_memtime() : 0;
+    unsigned long long t_mark = t_begin;
     const int half = R / 2, halfb = RB / 2;
     // Seed-chunk angles, prefetched one chunk ahead from the (static) angle
     // plane: (x, y), (x-1, y), (x+1, y), (x-1, y+1), (x, y+1), (x+1, y+1)
@@ -433,8 +434,22 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
         v[0] = r0[xx]; v[1] = r0[xm]; v[2] = r0[xp];
         v[3] = r1[xm]; v[4] = r1[xx]; v[5] = r1[xp];
     };
-    float nv[6];
+    // two chunks in flight ahead of the one being scanned (a chunk without
+    // seeds takes less time than one load round trip)
+    auto chunk_next = [&](int& cy, int& cxb) {
+        if (cxb + 64 < sw - 1) {
+            cxb += 64;
+        } else {
+            cxb = 0;
+            ++cy;
+        }
+    };
+    float nv[6], nv2[6];
+    int py2 = 0, px2 = 0;  // chunk of nv2
     chunk_load(0, 0, nv);
+    chunk_next(py2, px2);
+    if (py2 < sh - 1) chunk_load(py2, px2, nv2);
+    if (do_stats) s_init = __builtin_amdgcn_s_memtime() - t_begin;
     for (int y = 0; y < sh - 1; ++y) {
         // slide each window by half its height once row y is past its middle;
         // the rows leaving it are above y and never read again
@@ -457,13 +472,15 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
         }
         g.ys = y;
         for (int xb = 0; xb < sw - 1; xb += 64) {
+            if (do_stats) t_mark = __builtin_amdgcn_s_memtime();
             float cv[6];
 #pragma unroll
-            for (int k = 0; k < 6; ++k) cv[k] = nv[k];
-            {
-                const int nxb = xb + 64 < sw - 1 ? xb + 64 : 0, ny = xb + 64 < sw - 1 ? y : y + 1;
-                if (ny < sh - 1) chunk_load(ny, nxb, nv);
+            for (int k = 0; k < 6; ++k) {
+                cv[k] = nv[k];
+                nv[k] = nv2[k];
             }
+            chunk_next(py2, px2);
+            if (py2 < sh - 1) chunk_load(py2, px2, nv2);
             const int x = xb + lane;
             bool cand = false, grow = false;
             if (x < sw - 1) {
@@ -480,6 +497,7 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
                            is_aligned_fast(cv[5], d0, pdeg, prec);
             }
             unsigned long long m = __ballot(cand);
+            if (do_stats) s_scan += __builtin_amdgcn_s_memtime() - t_mark;
             if (!m) continue;
             const unsigned long long gm = __ballot(grow);
             // USED bits of seeds that cannot grow, set before the next seed grows
@@ -490,6 +508,7 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
                 const int b = __ffsll((long long)m) - 1;
                 m &= m - 1;
                 const int sx = xb + b;
+                if (do_stats) t_mark = __builtin_amdgcn_s_memtime();
                 const unsigned long long before = pend & ((1ull << b) - 1ull);
                 if (before) {
                     used_set_chunk(g, xb, y, before, lane);
@@ -497,22 +516,20 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
                 }
                 if (used_get(g, sx, y)) continue;  // absorbed by an earlier region of this chunk
                 // ---- region_grow (lsd.cpp:635-686)
-                float reg_deg = deg_at(g, sx, y);  // reg_angle = (double)reg_deg * DEG_TO_RADS
-                // seed direction: sumdx = (float)cos(reg_angle), sumdy = (float)sin(reg_angle)
-                // (lsd.cpp:648-649), double libm restated (plvi_math.h), wave-uniform
-                float sumdx, sumdy;
-                {
-                    double ds, dc;
-                    plvi_sincos((double)reg_deg * kD2R, &ds, &dc);
-                    sumdx = (float)dc;
-                    sumdy = (float)ds;
-                }
+                // the seed's angle is lane b's value of the scanned chunk (no reload)
+                float reg_deg = readlane_f(cv[0], b);  // reg_angle = (double)reg_deg * DEG_TO_RADS
+                // seed direction sumdx / sumdy: computed in the first block, while
+                // its neighbourhood loads are in flight
+                float sumdx = 0.f, sumdy = 0.f;
                 if (lane == 0) {
                     used_set(g, sx, y);
                     g.qlds[0] = (unsigned)sx | ((unsigned)y << 16);
                 }
                 __syncthreads();
-                if (do_stats) n_seed++;
+                if (do_stats) {
+                    n_seed++;
+                    s_seed += __builtin_amdgcn_s_memtime() - t_mark;
+                }
                 int reg_size = 1;
                 for (int i = 0; i < reg_size;) {
                     const unsigned long long t0 = do_stats ? __builtin_amdgcn_s_memtime() : 0;
@@ -531,6 +548,14 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
                         cc = cs2.x;
                         ss = cs2.y;
                     }
+                    if (i == 0) {
+                        // sumdx = (float)cos(reg_angle), sumdy = (float)sin(reg_angle)
+                        // (lsd.cpp:648-649), double libm restated (plvi_math.h), wave-uniform
+                        double ds, dc;
+                        plvi_sincos((double)reg_deg * kD2R, &ds, &dc);
+                        sumdx = (float)dc;
+                        sumdy = (float)ds;
+                    }
                     // lanes of earlier block points that test the same pixel
                     unsigned long long dup = 0;
                     for (int p2 = 0; p2 < nb - 1; ++p2) {
@@ -542,10 +567,6 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
                     unsigned long long t1 = 0;
                     if (do_stats) {
                         t1 = __builtin_amdgcn_s_memtime(); s_setup += t1 - t0; n_block++;
-                        // rows below the seed row of the tested neighbours: 0-1 / 2-7 / 8+
-                        n_dy[0] += __popcll(__ballot(valid && ny - y <= 1));
-                        n_dy[1] += __popcll(__ballot(valid && ny - y >= 2 && ny - y < 8));
-                        n_dy[2] += __popcll(__ballot(valid && ny - y >= 8));
                     }
                     // USED is read once per block: within the block a lane's pixel
                     // only becomes USED through a commit of an earlier lane testing
@@ -639,7 +660,7 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
         S[1] = s_setup; S[2] = s_round; S[3] = s_rect; S[4] = n_seed;
         S[5] = n_block; S[6] = n_round; S[7] = n_rpt; S[8] = n_commit;
         S[9] = s_ph[0]; S[10] = s_ph[1]; S[11] = s_ph[2]; S[12] = s_ph[3];
-        S[13] = n_dy[0]; S[14] = n_dy[1]; S[15] = n_dy[2];
+        S[13] = s_scan; S[14] = s_seed; S[15] = s_init;
     }
 }
 

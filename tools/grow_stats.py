@@ -27,7 +27,10 @@ lib.plvi_device_synchronize()
 lib.plvi_lines_debug_stats(lx._h, ctypes.c_void_p(0))
 s = st.cpu().numpy().reshape(B, 2, 16).astype(np.float64)
 names = ["total", "block_setup", "rounds", "rect", "seeds", "blocks", "rounds_n", "rect_pts", "commits", "ph_decide",
-         "ph_angles", "ph_verify", "ph_commit", "dy_0_1", "dy_2_7", "dy_8p"]
+         "ph_angles", "ph_verify", "ph_commit", "seed_scan", "seed_start", "init"]
+# 64-pixel chunks of the seed scan per octave (octave 0 = 0.8 x 640 x 480, octave 1 half of it)
+dims = [(512, 384), (256, 192)]
+names_chunks = [((w - 1 + 63) // 64) * (h - 1) for w, h in dims]
 print(f"B = {B}")
 for o in range(2):
     print(f"octave {o}:")
@@ -41,6 +44,9 @@ for o in range(2):
               (t[:, 0] / np.maximum(t[:, 8], 1)).mean()))
     print("  per round: decide %.0f  angles %.0f  verify %.0f  commit %.0f" % tuple(
         (t[:, 9 + k] / t[:, 6]).mean() for k in range(4)))
-    dy = t[:, 13:16].sum(axis=0)
-    print("  tested neighbours by rows below the seed: 0-1 %.1f%%  2-7 %.1f%%  8+ %.1f%%" % tuple(100 * dy / dy.sum()))
+    print("  seed scan %.0f (%.1f %%, %.0f per 64-pixel chunk)  seed starts %.0f (%.0f per seed)  init %.0f" % (
+        t[:, 13].mean(), 100 * (t[:, 13] / t[:, 0]).mean(), t[:, 13].mean() / max(1, names_chunks[o]),
+        t[:, 14].mean(), (t[:, 14] / np.maximum(t[:, 4], 1)).mean(), t[:, 15].mean()))
+    print("  unaccounted %.1f %%" % (100 * ((t[:, 0] - t[:, 1] - t[:, 2] - t[:, 3] - t[:, 13] - t[:, 14] - t[:, 15])
+                                          / t[:, 0]).mean()))
     print("  wave time: mean %.0f  max %.0f cycles" % (t[:, 0].mean(), t[:, 0].max()))
