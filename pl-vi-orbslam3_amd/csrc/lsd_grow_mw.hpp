@@ -237,13 +237,9 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
     const int bp = lane / 9, bk = lane % 9;
     const int kdx = bk % 3 - 1, kdy = bk / 3 - 1;
     float reg_deg = E.P[(size_t)sy * sw + sx];
-    float sumdx, sumdy;
-    {
-        double ds, dc;
-        plvi_sincos((double)reg_deg * kD2R, &ds, &dc);
-        sumdx = (float)dc;
-        sumdy = (float)ds;
-    }
+    // the seed direction (lsd.cpp:648-649) is computed in the first block,
+    // while its neighbourhood loads are in flight
+    float sumdx = 0.f, sumdy = 0.f;
     if (lane == 0) {
         mw_own_set(E, sx, sy, sy);
         mw_or(E.H, E.wpr, sx, sy);
@@ -282,6 +278,12 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
             deg = E.P[(size_t)ny * sw + nx];
             cc = cs2.x;
             ss = cs2.y;
+        }
+        if (i == 0) {
+            double ds, dc;
+            plvi_sincos((double)reg_deg * kD2R, &ds, &dc);
+            sumdx = (float)dc;
+            sumdy = (float)ds;
         }
         unsigned long long dup = 0;
         for (int p2 = 0; p2 < nb - 1; ++p2) {
