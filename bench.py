@@ -610,6 +610,7 @@ def run(args, world, rank):
     orb.profile(True)
     lx.profile(True)
     lx.kernel_timing(True)  # isolated per-launch times of the LBD Gaussian + Sobel kernels
+    orb.kernel_timing(True)  # and of blur + FAST (the roofline kernel) with nothing beside it
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     match_ms = 0.0
     nprof = max(3, min(args.steps, 10))
@@ -626,6 +627,8 @@ def run(args, world, rank):
     st_orb, runs = orb.profile_read()
     st_lines, lruns = lx.profile_read()
     lbd_iso = [lx.kernel_timing_read(k) for k in (1, 2)]
+    bf_iso = orb.kernel_timing_read()
+    orb.kernel_timing(False)
     lx.kernel_timing(False)
     orb.profile(False)
     lx.profile(False)
@@ -702,6 +705,12 @@ def run(args, world, rank):
             "kernel_bytes_frac": blur_fast_kernel_bytes(W, H) * B / (bf_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "avg_launch_ms": bf_ms, "launches": kn}
     roof["frac"] = roof["achieved"] / roof["peak"]
+    if bf_iso[1]:
+        # the same launch with nothing beside it (stage-timing runs): the timed
+        # figure above shares the CUs with region growing and the other batch
+        i_ms = bf_iso[0] / bf_iso[1]
+        roof["isolated"] = {"avg_launch_ms": i_ms, "launches": bf_iso[1], "achieved": bf_bytes / (i_ms * 1e-3) / 1e9,
+                            "frac": bf_bytes / (i_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
     lp_ms = ltot / max(ln, 1)
     roof_lsd = {"bound": "hbm", "kernel": "lsd_prep_kernel (u8 -> f64 blur 7x7, resize x0.8, ll_angle; one launch "
                                           "per octave)",
