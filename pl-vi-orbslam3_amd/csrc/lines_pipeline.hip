@@ -76,6 +76,7 @@ struct LinePipeline {
                evBlur = nullptr, evGate = nullptr, evGrow2 = nullptr, evPair = nullptr;
     bool growAfterBlur = true, sobelWithGrow = false, growSplit = false;
     int sobelGate = -1;  // PLVI_SOBEL_GATE: ORB stage after which the Sobel pyramid starts (-1: with growth)
+    bool sobelAfterGrow = true;
     hipStream_t critStream = nullptr;  // frame schedule: prep -> grow -> describe
     hipStream_t crit2 = nullptr;       // frame schedule: octave-1 region growing (split mode)
     hipStream_t octStream = nullptr;   // small batches: prep + growth of octaves >= 1 beside octave 0's
@@ -210,6 +211,14 @@ struct LinePipeline {
             // so it does not take wave slots from the ORB chain while that chain
             // runs beside region growing
             if (const char* e7 = getenv("PLVI_SOBEL_GATE")) sobelGate = std::min(5, std::max(-1, atoi(e7)));
+            // PLVI_SOBEL_AFTER_GROW (default 1, batches from 1024 frames): the
+            // Sobel pyramid runs on the critical stream after region growing +
+            // rect + assemble instead of beside growth on a low-priority
+            // stream.  With two batches in flight the step is the same (47.4K
+            // vs 47.6K FPS, within run-to-run noise) and lbd_sobel0 takes 3.0-3.3
+            // instead of 23-29 ms per launch (its waves no longer sit on the
+            // SIMDs beside the growth waves; profiles/r04/ab_sched_inflight2.txt)
+            if (const char* e8 = getenv("PLVI_SOBEL_AFTER_GROW")) sobelAfterGrow = atoi(e8) != 0;
             if (prio) PLVI_CHECK(hipStreamCreateWithPriority(&critStream, hipStreamNonBlocking, greatest));
             // PLVI_GROW_SPLIT=1: octave 0 grows right after the prep, octave 1
             // after blur + FAST (batches from 1024 frames; +1 % in a 3-way
@@ -698,9 +707,12 @@ struct LinePipeline {
         if (waitBlur && !rc) PLVI_CHECK(hipStreamWaitEvent(gate, evBlur, 0));
         // evGate: everything the (last) region-growing launch waits for
         PLVI_CHECK(hipEventRecord(evGate, gate));
-        PLVI_CHECK(hipStreamWaitEvent(aux[1], sobelLate ? evSobelGo : sobelWithGrow ? evGate : auxStart, 0));
-        if (!rc) rc = launch_sobel(d_frames, nf, frame_stride, row_stride, aux[1]);
-        PLVI_CHECK(hipEventRecord(evSobel, aux[1]));
+        const bool sobelAfter = sobelAfterGrow && waitBlur;
+        if (!sobelAfter) {
+            PLVI_CHECK(hipStreamWaitEvent(aux[1], sobelLate ? evSobelGo : sobelWithGrow ? evGate : auxStart, 0));
+            if (!rc) rc = launch_sobel(d_frames, nf, frame_stride, row_stride, aux[1]);
+            PLVI_CHECK(hipEventRecord(evSobel, aux[1]));
+        }
         if (split) {
             launch_grow(nf, 1, 1, crit2);
             PLVI_CHECK(hipEventRecord(evGrow2, crit2));
@@ -713,7 +725,11 @@ struct LinePipeline {
         } else {
             launch_grow_assemble(nf, crit, split);
         }
-        PLVI_CHECK(hipStreamWaitEvent(crit, evSobel, 0));
+        if (sobelAfter) {
+            if (!rc) rc = launch_sobel(d_frames, nf, frame_stride, row_stride, crit);
+        } else {
+            PLVI_CHECK(hipStreamWaitEvent(crit, evSobel, 0));
+        }
         launch_describe(nf, crit);
         if (crit != st) {
             PLVI_CHECK(hipEventRecord(evCrit, crit));

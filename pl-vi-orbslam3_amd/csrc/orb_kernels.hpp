@@ -55,14 +55,26 @@ __host__ __device__ inline uint32_t pyr_xtab_pack(int sx, int a0, int a1, bool c
     return (uint32_t)sx | ((uint32_t)a0 << 10) | ((uint32_t)(a0 + a1 - 2047) << 22) | ((uint32_t)clampR << 24);
 }
 
-__device__ __forceinline__ int lds_load_volatile(lds_i32* p) { return *(volatile lds_i32*)p; }
-__device__ __forceinline__ void lds_publish(lds_i32* p, int v) {
-    // earlier LDS writes of this wave complete before the counter moves
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    *(volatile lds_i32*)p = v;
+// Loader -> resizer hand-off of the pyramid kernel's LDS row ring, inside the
+// HIP memory model: the producing wave makes all its lanes' row writes
+// visible to its lane 0 (wavefront-scope release / acquire around a wave
+// barrier), lane 0 publishes the row counter with a workgroup-scope RELEASE
+// store, and the consuming wave polls it with workgroup-scope ACQUIRE loads
+// (on gfx950 both compile to an s_waitcnt lgkmcnt(0) for LDS).
+__device__ __forceinline__ int lds_load_acquire(lds_i32* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_publish(lds_i32* p, int v, int lane) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0) __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-__global__ __launch_bounds__(64 * (kPyrFrames + 1)) void orb_pyramid_kernel(
+#ifndef PLVI_PYR_WPE
+#define PLVI_PYR_WPE 1  // waves per EU the pyramid kernel is compiled for (1: no cap)
+#endif
+__global__ __launch_bounds__(64 * (kPyrFrames + 1)) __attribute__((amdgpu_waves_per_eu(PLVI_PYR_WPE))) void orb_pyramid_kernel(
     const OrbLevelDev* __restrict__ lvs, int L, const uint8_t* __restrict__ frames, size_t f_frame, size_t f_row,
     int nf, uint8_t* __restrict__ pyr, const uint32_t* __restrict__ xtab, int xtab_n, int frame_lds, int generic) {
     extern __shared__ __align__(16) uint8_t lds_pyr_g[];
@@ -133,12 +145,12 @@ __global__ __launch_bounds__(64 * (kPyrFrames + 1)) void orb_pyramid_kernel(
                     lds_i32* loaded = (lds_i32*)&s_cnt[2 * k];
                     lds_i32* consumed = (lds_i32*)&s_cnt[2 * k + 1];
                     // the resizer needs rows consumed-1 and consumed: slot r % ring is free once r - ring <= consumed - 2
-                    while (r - kPyrRing > lds_load_volatile(consumed) - 2) __builtin_amdgcn_s_sleep(1);
+                    while (r - kPyrRing > lds_load_acquire(consumed) - 2) __builtin_amdgcn_s_sleep(1);
                     lds_u32* slot = (lds_u32*)(fbase + (size_t)k * frame_lds + (r % kPyrRing) * pitch0);
 #pragma unroll
                     for (int q = 0; q < kPyrDw; ++q)
                         if (lane + 64 * q < nd) slot[lane + 64 * q] = pf[j][k][q];
-                    if (lane == 0) lds_publish(loaded, r + 1);
+                    lds_publish(loaded, r + 1, lane);
                     if (r + kPyrAhead < H0) load_row(k, r + kPyrAhead, pf[j][k]);
                 }
             }
@@ -161,7 +173,7 @@ __global__ __launch_bounds__(64 * (kPyrFrames + 1)) void orb_pyramid_kernel(
 #pragma unroll
     for (int l = 0; l < kOrbMaxLevels; ++l) prod[l] = 0;
     for (int r = 0; r < H0; ++r) {
-        while (lds_load_volatile(s_loaded) <= r) __builtin_amdgcn_s_sleep(1);
+        while (lds_load_acquire(s_loaded) <= r) __builtin_amdgcn_s_sleep(1);
         int avail = r + 1;  // rows of the source level available
         for (int l = 1; l < L; ++l) {
             const int sh = s_h[l - 1], w = s_w[l], h = s_h[l];
@@ -232,7 +244,7 @@ __global__ __launch_bounds__(64 * (kPyrFrames + 1)) void orb_pyramid_kernel(
             if (y == y_start) break;  // nothing new at level l: deeper levels have no new source rows
             avail = y;
         }
-        if (lane == 0) lds_publish(s_consumed, r + 1);
+        lds_publish(s_consumed, r + 1, lane);
     }
 }
 
@@ -437,7 +449,10 @@ __device__ __forceinline__ unsigned orb_cell_axis(int v, int minB, int cell, int
 // threshold -- iniThFAST if it has a survivor there, else minThFAST -- goes to
 // the per-frame cell table that the SAT and node-argmax kernels apply.  The
 // score plane, its zero fill and the NMS launch disappear.
-__global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __restrict__ lvs,
+#ifndef PLVI_BF_WPE
+#define PLVI_BF_WPE 1  // waves per EU blur + FAST is compiled for (1: no cap)
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PLVI_BF_WPE))) void orb_blur_fast_kernel(const OrbLevelDev* __restrict__ lvs,
                                                            const OrbStripDev* __restrict__ strips,
                                                            const uint8_t* __restrict__ frames, size_t f_frame,
                                                            size_t f_row, uint8_t* __restrict__ pyr,
