@@ -222,8 +222,9 @@ int plvi_lines_scale_tables(plvi_line_extractor* h, float* scale, float* inv_sca
  * [2] region growing + rect, [3] keyline assembly + top-k, [4] LBD. */
 int plvi_lines_profile(plvi_line_extractor* h, int enable);
 /* Diagnostic cycle accounting inside the region-growing kernel (s_memtime):
- * per (frame, octave) 16 uint64 = [total, pop-prep, commit rounds, rect,
- * seeds, pops, commits, rect points, slow-path loads]; NULL disables. */
+ * per (frame, octave) 24 uint64 = [total, block setup, rounds, rect, seeds,
+ * blocks, rounds, rect points, commits, 4 round phases, seed scan, seed
+ * starts, init, HW_ID, XCC_ID, start time, -]; NULL disables. */
 int plvi_lines_debug_stats(plvi_line_extractor* h, unsigned long long* d_stats);
 /* Diagnostic counters of the multi-wave (small-batch) region-growing kernel:
  * per (frame, octave) 16 int32 = [regions dispatched speculatively, dropped,

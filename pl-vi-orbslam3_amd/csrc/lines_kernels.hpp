@@ -361,8 +361,29 @@ __device__ __forceinline__ void bits_load_rows(const GrowCtx& g, int r0, int r1,
 #ifndef PLVI_GROW_WPE
 #define PLVI_GROW_WPE 8
 #endif
+// waves (tasks) per workgroup of the region-growing kernel: with single-wave
+// workgroups the dispatcher put 7 growth waves on 33 of the 1024 SIMDs and 5
+// on 33 others at 3072 frames (every CU holds 24), and the waves on the
+// 7-wave SIMDs set the launch time (max 87.9M vs 79.7M cycles on 6-wave
+// SIMDs, tools/grow_stats.py); a 4-wave workgroup puts one task on each SIMD
+#ifndef PLVI_GROW_WG_WAVES
+#define PLVI_GROW_WG_WAVES 4
+#endif
+constexpr int kGrowWaves = PLVI_GROW_WG_WAVES;
+
+// the waves of a workgroup share nothing (each has its own LDS partition):
+// a wave-level barrier orders its own lanes' LDS accesses
+// (the scheduling barrier keeps the code motion of the workgroup barrier it
+// replaces: without it the compiler hoists loads across and spills VGPRs)
+__device__ __forceinline__ void grow_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 template <bool STATS>
-__global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineOctDev* __restrict__ octs,
+__global__ __launch_bounds__(64 * kGrowWaves, PLVI_GROW_WPE) void lsd_grow_kernel(const LineOctDev* __restrict__ octs,
                                                       const float* __restrict__ pix,
                                                       const double* __restrict__ modgrad,
                                                       const float2* __restrict__ pixcs,
@@ -371,8 +392,9 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
                                                       double prec, LsdRegion* __restrict__ regs, unsigned* __restrict__ regpts,
                                                       size_t regpts_frame, int* __restrict__ nlines,
                                                       int* __restrict__ err, int R, int RB, int QL, int nOct,
-                                                      int oBase, int oCount, unsigned long long* __restrict__ stats) {
-    extern __shared__ __align__(16) unsigned lds_u[];
+                                                      int oBase, int oCount, unsigned long long* __restrict__ stats,
+                                                      int nf, int ldsWave, int wpw) {
+    extern __shared__ __align__(16) unsigned lds_all[];
     // latency-bound serial chain: win the SIMD arbiter against co-resident
     // throughput kernels (ORB / LBD on the other stream)
     __builtin_amdgcn_s_setprio(PLVI_GROW_SETPRIO);
@@ -380,12 +402,19 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
     // octave 1.  Blocks are dealt round-robin over the 8 XCDs, so every XCD
     // gets the same mix (a (nOct, nf) grid put every octave-0 task on the
     // even XCDs) and the heavy tasks are dispatched first.
-    // this launch covers octaves oBase .. oBase + oCount - 1
-    const int nf = gridDim.x / oCount;
-    const int o = oBase + blockIdx.x / nf, f = blockIdx.x - (o - oBase) * nf;
+    // this launch covers octaves oBase .. oBase + oCount - 1; task = (octave,
+    // frame) in that order, wpw (<= kGrowWaves, LDS permitting) consecutive
+    // tasks per workgroup; the wave index is read uniformly (readfirstlane)
+    // so that everything derived from the task stays scalar
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int task = blockIdx.x * wpw + wv;
+    if (task >= nf * oCount) return;  // no workgroup barrier below: the other waves go on
+    const int o = oBase + task / nf, f = task - (o - oBase) * nf;
+    // this wave's LDS partition, addressed as LDS (32-bit) from the start
+    lds_u32* lds_w = (lds_u32*)lds_all + wv * (ldsWave >> 2);
     const LineOctDev& od = octs[o];
     const int sw = od.sw, sh = od.sh;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
     GrowCtx g;
     g.sw = sw; g.sh = sh; g.R = R; g.RB = RB; g.QL = QL;
     g.wpr = (sw + 31) >> 5;
@@ -397,7 +426,7 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
     g.gbits = gbits_all + (size_t)(f * nOct + o) * gbits_frame;
     g.qglob = qspill + (size_t)(f * nOct + o) * qspill_frame;
     // LDS: USED ring | queue | angle ring
-    g.bits = (lds_u32*)lds_u;
+    g.bits = lds_w;
     g.qlds = g.bits + RB * g.wpr;
     g.win = (lds_f32*)(g.qlds + QL);
     g.wb = 0;
@@ -407,7 +436,7 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
     for (int i = lane; i < RB * g.wpr; i += 64) g.bits[i] = 0u;
     if (R) win_load_rows(g, 0, min(R, sh), lane);
     vm_drain();
-    __syncthreads();
+    grow_wave_sync();
     int nout = 0;
     bool overflow = false;
     const float pdeg = (float)(prec / kD2R);  // ANG_TH in degrees
@@ -468,7 +497,7 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
         }
         if (slid) {
             vm_drain();
-            __syncthreads();
+            grow_wave_sync();
         }
         g.ys = y;
         for (int xb = 0; xb < sw - 1; xb += 64) {
@@ -525,7 +554,7 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
                     used_set(g, sx, y);
                     g.qlds[0] = (unsigned)sx | ((unsigned)y << 16);
                 }
-                __syncthreads();
+                grow_wave_sync();
                 if (do_stats) {
                     n_seed++;
                     s_seed += __builtin_amdgcn_s_memtime() - t_mark;
@@ -655,12 +684,16 @@ __global__ __launch_bounds__(64, PLVI_GROW_WPE) void lsd_grow_kernel(const LineO
         if (overflow) atomicOr(err + f, 4);
     }
     if (do_stats && lane == 0) {
-        unsigned long long* S = stats + (size_t)(f * nOct + o) * 16;
+        unsigned long long* S = stats + (size_t)(f * nOct + o) * 24;
         S[0] = __builtin_amdgcn_s_memtime() - t_begin;
         S[1] = s_setup; S[2] = s_round; S[3] = s_rect; S[4] = n_seed;
         S[5] = n_block; S[6] = n_round; S[7] = n_rpt; S[8] = n_commit;
         S[9] = s_ph[0]; S[10] = s_ph[1]; S[11] = s_ph[2]; S[12] = s_ph[3];
         S[13] = s_scan; S[14] = s_seed; S[15] = s_init;
+        // where the wave ran: HW_ID (wave / SIMD / CU / SH / SE) and XCC_ID
+        S[16] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        S[17] = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+        S[18] = t_begin;
     }
 }
 

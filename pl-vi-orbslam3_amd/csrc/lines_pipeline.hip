@@ -413,10 +413,13 @@ struct LinePipeline {
         }
         if (const char* e = getenv("PLVI_GROW_RD")) growR = atoi(e);
         if (growR < 0 || (growR & (growR - 1)) || growR == 1 || growR > 1024) return PLVI_E_BADARG;
-        growSmem = fixed + perRow * growR;
+        growSmem = (fixed + perRow * growR + 15) & ~size_t(15);  // per wave
         if (growSmem > 160 * 1024) return PLVI_E_BADARG;
+        // tasks (waves) per workgroup: kGrowWaves, fewer when their LDS
+        // partitions would not fit one CU (large PLVI_GROW_LDS budgets)
+        growWPW = (int)std::max<size_t>(1, std::min<size_t>(kGrowWaves, (160 * 1024) / growSmem));
         for (const void* k : {(const void*)lsd_grow_kernel<false>, (const void*)lsd_grow_kernel<true>})
-            PLVI_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)growSmem));
+            PLVI_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(growSmem * growWPW)));
         // region2rect: PLVI_RECT_LANES=1 (default) lane = region
         // (lsd_rect_lanes_kernel), 0 = wave = region (lsd_rect_kernel)
         rectLanes = true;
@@ -462,6 +465,7 @@ struct LinePipeline {
     size_t mwSmem = 0, mwOwnTask = 0;
     int* mwStats = nullptr;  // diagnostic counters (plvi_lines_debug_mw_stats)
     size_t growSmem = 0;
+    int growWPW = 1;  // region-growing tasks (waves) per workgroup
     int growR = 0, growRB = 0, growQL = 0;
     unsigned long long* growStats = nullptr;  // diagnostic cycle counters (plvi_lines_debug_stats)
 
@@ -540,12 +544,13 @@ struct LinePipeline {
             return;
         }
         auto growK = growStats ? lsd_grow_kernel<true> : lsd_grow_kernel<false>;
-        hipLaunchKernelGGL(growK, dim3(oCount * nf), dim3(64), growSmem, st, d_oct.as<LineOctDev>(),
+        hipLaunchKernelGGL(growK, dim3((oCount * nf + growWPW - 1) / growWPW), dim3(64 * growWPW),
+                           growSmem * growWPW, st, d_oct.as<LineOctDev>(),
                            (const float*)pix.as<float>(), (const double*)modg.as<double>(),
                            (const float2*)seedcs.as<float2>(), gbits.as<unsigned>(), gbitsFrame,
                            qspill.as<unsigned>(), qspillFrame, prec, regs.as<LsdRegion>(), regpts.as<unsigned>(),
                            qspillFrame, nlines.as<int>(), err.as<int>(), growR, growRB, growQL, nOct, oBase, oCount,
-                           growStats);
+                           growStats, nf, (int)growSmem, growWPW);
     }
     void launch_grow_assemble(int nf, hipStream_t st, bool grown = false) {
         if (!grown) launch_grow(nf, 0, nOct, st);
@@ -936,7 +941,8 @@ extern "C" int plvi_lines_profile_read(plvi_line_extractor* h, float* stage_ms, 
 }
 
 // Diagnostic: enable per-task cycle accounting of the region-growing kernel
-// into a caller-provided device buffer of n_frames*nlevels*16 uint64 (NULL disables).
+// into a caller-provided device buffer of n_frames*nlevels*24 uint64 (NULL disables):
+// [0..15] cycle counters, [16] HW_ID, [17] XCC_ID, [18] start time (s_memtime).
 extern "C" int plvi_lines_debug_stats(plvi_line_extractor* h, unsigned long long* d_stats) {
     if (!h) return PLVI_E_BADARG;
     h->p().growStats = d_stats;

@@ -17,7 +17,7 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 16
 seq = synth.device_sequence(B, 640, 480, seed=0, device="cuda:0")
 torch.cuda.synchronize()
 lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 640, 480, max_batch=B)
-st = torch.zeros(B * 2 * 16, dtype=torch.int64, device="cuda:0")
+st = torch.zeros(B * 2 * 24, dtype=torch.int64, device="cuda:0")
 lib = plvi.load()
 lx.extract_batch(seq.data_ptr(), B, 640 * 480, 640)
 lib.plvi_device_synchronize()
@@ -25,7 +25,8 @@ lib.plvi_lines_debug_stats(lx._h, ctypes.c_void_p(st.data_ptr()))
 lx.extract_batch(seq.data_ptr(), B, 640 * 480, 640)
 lib.plvi_device_synchronize()
 lib.plvi_lines_debug_stats(lx._h, ctypes.c_void_p(0))
-s = st.cpu().numpy().reshape(B, 2, 16).astype(np.float64)
+raw = st.cpu().numpy().reshape(B, 2, 24)
+s = raw[:, :, :16].astype(np.float64)
 names = ["total", "block_setup", "rounds", "rect", "seeds", "blocks", "rounds_n", "rect_pts", "commits", "ph_decide",
          "ph_angles", "ph_verify", "ph_commit", "seed_scan", "seed_start", "init"]
 # 64-pixel chunks of the seed scan per octave (octave 0 = 0.8 x 640 x 480, octave 1 half of it)
@@ -50,3 +51,47 @@ for o in range(2):
     print("  unaccounted %.1f %%" % (100 * ((t[:, 0] - t[:, 1] - t[:, 2] - t[:, 3] - t[:, 13] - t[:, 14] - t[:, 15])
                                           / t[:, 0]).mean()))
     print("  wave time: mean %.0f  max %.0f cycles" % (t[:, 0].mean(), t[:, 0].max()))
+# work vs time: is the slowest wave the one with the most work, or a contended one?
+for o in range(2):
+    t = s[:, o]
+    cyc, blk = t[:, 0], t[:, 5]
+    r = np.corrcoef(cyc, blk)[0, 1]
+    per = cyc / np.maximum(blk, 1)
+    top = np.argsort(cyc)[-5:][::-1]
+    print(f"octave {o}: corr(cycles, blocks) {r:.3f}; cycles/block mean {per.mean():.0f} min {per.min():.0f} "
+          f"max {per.max():.0f}; blocks max {blk.max():.0f} (wave {int(np.argmax(blk))})")
+    for i in top:
+        print(f"   wave {i:5d} cycles {cyc[i]:12.0f} blocks {blk[i]:6.0f} cycles/block {per[i]:6.0f} "
+              f"seeds {t[i, 4]:5.0f}")
+
+# placement: waves per SIMD (same XCC / SE / SH / CU / SIMD) vs cycles per block
+hw = raw[:, :, 16].astype(np.int64) & 0xFFFFFFFF
+xcc = raw[:, :, 17].astype(np.int64) & 0xF
+simd = (hw >> 4) & 3
+cu = (hw >> 8) & 15
+sh = (hw >> 12) & 1
+se = (hw >> 13) & 7
+key = ((xcc * 8 + se) * 2 + sh) * 16 * 4 + cu * 4 + simd
+cuk = key // 4
+uk, cnt = np.unique(key, return_counts=True)
+ucu, ccnt = np.unique(cuk, return_counts=True)
+print(f"placement: {len(uk)} SIMDs and {len(ucu)} CUs used; waves per SIMD min {cnt.min()} max {cnt.max()} "
+      f"mean {cnt.mean():.2f}; waves per CU min {ccnt.min()} max {ccnt.max()}")
+hist = np.bincount(cnt)
+print("  SIMDs by wave count:", {i: int(h) for i, h in enumerate(hist) if h})
+per_simd = dict(zip(uk, cnt))
+for o in range(2):
+    c = np.array([per_simd[k] for k in key[:, o]])
+    cpb = s[:, o, 0] / np.maximum(s[:, o, 5], 1)
+    for n in sorted(set(c)):
+        m = c == n
+        print(f"  octave {o}: waves on a SIMD with {n} grow waves: {m.sum():5d}, cycles/block {cpb[m].mean():6.0f}, "
+              f"wave cycles mean {s[m, o, 0].mean():12.0f} max {s[m, o, 0].max():12.0f}")
+    oc = np.array([np.sum((key[:, 0] == k)) for k in key[:, o]])
+    for n in sorted(set(oc)):
+        m = oc == n
+        print(f"  octave {o}: SIMD holding {n} octave-0 waves: {m.sum():5d}, wave cycles mean {s[m, o, 0].mean():12.0f}")
+t0 = raw[:, :, 18].astype(np.float64)
+t0 -= t0.min()
+print("  start-time spread (cycles): octave 0 max %.0f, octave 1 min %.0f max %.0f" % (
+    t0[:, 0].max(), t0[:, 1].min(), t0[:, 1].max()))
