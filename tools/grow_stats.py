@@ -95,3 +95,38 @@ t0 = raw[:, :, 18].astype(np.float64)
 t0 -= t0.min()
 print("  start-time spread (cycles): octave 0 max %.0f, octave 1 min %.0f max %.0f" % (
     t0[:, 0].max(), t0[:, 1].min(), t0[:, 1].max()))
+
+# drains: commit rounds with USED rows beyond the LDS window (global atomics) or a queue spill
+for o in range(2):
+    far, sp = raw[:, o, 19].astype(np.float64), raw[:, o, 20].astype(np.float64)
+    cyc = s[:, o, 0]
+    print(f"octave {o}: far-row drains mean {far.mean():.0f} max {far.max():.0f}, spill drains mean {sp.mean():.0f} "
+          f"max {sp.max():.0f}; corr(cycles, far) {np.corrcoef(cyc, far)[0, 1]:.3f} corr(cycles, spill) "
+          f"{np.corrcoef(cyc, sp)[0, 1] if sp.std() > 0 else 0:.3f}")
+    top = np.argsort(cyc)[-3:][::-1]
+    print("   slowest:", [(int(i), int(far[i]), int(sp[i])) for i in top])
+
+# start / end on the 100 MHz clock (s_memrealtime): do the slowest tasks start late?
+r0, r1 = raw[:, :, 21].astype(np.float64), raw[:, :, 22].astype(np.float64)
+base = r0.min()
+for o in range(2):
+    st, en = (r0[:, o] - base) / 100.0, (r1[:, o] - base) / 100.0  # microseconds
+    cyc = s[:, o, 0]
+    top = np.argsort(en)[-5:][::-1]
+    print(f"octave {o}: start us mean {st.mean():.0f} max {st.max():.0f}; end us mean {en.mean():.0f} max {en.max():.0f}; "
+          f"latest ends: {[(int(i), round(float(st[i])), round(float(en[i]))) for i in top]}")
+    late = st > 100
+    print(f"   tasks starting > 100 us late: {int(late.sum())}; their mean cycles/block "
+          f"{(cyc[late] / np.maximum(s[late, o, 5], 1)).mean() if late.any() else 0:.0f}")
+# end time by hardware location (averaged over the 8 XCCs): is the tail tied to particular CUs?
+for o in range(2):
+    en = (r1[:, o] - base) / 100.0
+    loc = (se[:, o] * 2 + sh[:, o]) * 16 + cu[:, o]
+    ul = np.unique(loc)
+    means = sorted(((float(en[loc == u].mean()), int(u)) for u in ul), reverse=True)
+    print(f"octave {o}: end us by (SE, SH, CU): slowest {[(round(m), u // 32, (u // 16) % 2, u % 16) for m, u in means[:4]]} "
+          f"fastest {[(round(m), u // 32, (u // 16) % 2, u % 16) for m, u in means[-3:]]}")
+    xs = np.unique(xcc[:, o])
+    print(f"   by XCC: {[(int(x), round(float(en[xcc[:, o] == x].mean()))) for x in xs]}")
+    top = np.argsort(en)[-6:]
+    print(f"   slowest tasks at (XCC, SE, SH, CU, SIMD): {[(int(xcc[i, o]), int(se[i, o]), int(sh[i, o]), int(cu[i, o]), int(simd[i, o])) for i in top]}")
