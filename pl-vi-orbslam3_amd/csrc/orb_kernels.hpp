@@ -71,12 +71,21 @@ __device__ __forceinline__ void lds_publish(lds_i32* p, int v, int lane) {
     if (lane == 0) __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+#ifndef PLVI_ORB_SETPRIO
+#define PLVI_ORB_SETPRIO 0  // s_setprio of the ORB chain's waves (0: hardware default, no instruction)
+#endif
+#define PLVI_ORB_PRIO_SET()                                                      \
+    do {                                                                         \
+        if (PLVI_ORB_SETPRIO) __builtin_amdgcn_s_setprio(PLVI_ORB_SETPRIO);      \
+    } while (0)
+
 #ifndef PLVI_PYR_WPE
 #define PLVI_PYR_WPE 1  // waves per EU the pyramid kernel is compiled for (1: no cap)
 #endif
 __global__ __launch_bounds__(64 * (kPyrFrames + 1)) __attribute__((amdgpu_waves_per_eu(PLVI_PYR_WPE))) void orb_pyramid_kernel(
     const OrbLevelDev* __restrict__ lvs, int L, const uint8_t* __restrict__ frames, size_t f_frame, size_t f_row,
     int nf, uint8_t* __restrict__ pyr, const uint32_t* __restrict__ xtab, int xtab_n, int frame_lds, int generic) {
+    PLVI_ORB_PRIO_SET();
     extern __shared__ __align__(16) uint8_t lds_pyr_g[];
     __shared__ int s_w[kOrbMaxLevels], s_h[kOrbMaxLevels], s_roff[kOrbMaxLevels], s_xoff[kOrbMaxLevels];
     __shared__ double s_sy[kOrbMaxLevels];
@@ -460,6 +469,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PLVI_BF_WPE)
                                                            uint8_t* __restrict__ cthr, int thrFrame, int k0, int k1,
                                                            int k2, int k3, int tmin, int t1, int t2, int nstrips,
                                                            int nf) {
+    PLVI_ORB_PRIO_SET();
     static_assert(!PLVI_BF_NMS || PLVI_BF_PK, "the fused NMS queues from the packed scorer");
     typedef typename std::conditional<PLVI_BF_LEAN != 0, unsigned short, unsigned>::type QT;
     __shared__ __align__(16) uint8_t ring[kRingRows + kRingMirror][kRingW];
@@ -984,6 +994,7 @@ __global__ __launch_bounds__(64) void orb_cell_nms_kernel(const OrbCellDev* __re
                                                           const OrbLevelDev* __restrict__ lvs,
                                                           const uint8_t* __restrict__ score,
                                                           uint8_t* __restrict__ cand, int t1, int t2) {
+    PLVI_ORB_PRIO_SET();
     __shared__ uint8_t sv[kNmsRows * 64];
     const int f = blockIdx.y;
     for (int ci = blockIdx.x; ci < ncells; ci += gridDim.x) {
@@ -1081,6 +1092,7 @@ __global__ __launch_bounds__(64) void orb_sat_quad_kernel(const OrbLevelDev* __r
                                                           const uint8_t* __restrict__ cand,
                                                           const uint8_t* __restrict__ cthr, int thrFrame,
                                                           unsigned short* __restrict__ lsat, int* __restrict__ carry) {
+    PLVI_ORB_PRIO_SET();
     __shared__ uint8_t sthr[PLVI_BF_NMS ? kOrbCellsLevelMax : 1];
     const int w = blockIdx.x, l = blockIdx.y, f = blockIdx.z;
     const OrbLevelDev& L = lvs[l];
@@ -1204,6 +1216,7 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
                                                         const int* __restrict__ carry, short4* __restrict__ out_rect,
                                                         int* __restrict__ out_cnt, int nodeCapMax, int L,
                                                         int* __restrict__ err, uint8_t* __restrict__ cand) {
+    PLVI_ORB_PRIO_SET();
     extern __shared__ __align__(16) unsigned char smem[];
     // blocks are dealt round-robin over the 8 XCDs: with l = blockIdx.x every
     // XCD would own one level (level 0, the heaviest, on one XCD); rotating
@@ -1426,6 +1439,7 @@ __global__ __launch_bounds__(64) void orb_node_best_kernel(const OrbLevelDev* __
                                                            const short4* __restrict__ rects,
                                                            const int* __restrict__ rect_cnt, int nodeCapMax, int L,
                                                            float4* __restrict__ lvkp, int kpCapFrame) {
+    PLVI_ORB_PRIO_SET();
     const int l = blockIdx.y, f = blockIdx.z;
     const int ncnt = rect_cnt[(size_t)f * L + l];
     const OrbLevelDev& lv = lvs[l];
@@ -1511,6 +1525,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PLVI_DESC_W
                                                            const int* __restrict__ rect_cnt,
                                                            float4* __restrict__ lvkp, uint8_t* __restrict__ lvdesc,
                                                            int kpCapFrame) {
+    PLVI_ORB_PRIO_SET();
     __shared__ __align__(16) uint8_t patch[4][kDescP * kDescPitch];
     __shared__ __align__(16) uint8_t ipatch[4][kAngRows * kAngPitch];
     const int f = blockIdx.y;

@@ -207,3 +207,59 @@ def test_local_stereo_degenerate():
                                                     c["mp_proj_r"], c["mp_level_r"], c["mp_desc"], c["blocked"],
                                                     c["blocked_r"])
     assert ng == ne and np.array_equal(mlg, mle) and np.array_equal(mrg, mre)
+
+
+@pytest.mark.gpu
+def test_local_stereo_batch_device():
+    """Several two-camera frames in one launch through plvi_search_local_stereo_batch (device tables, both
+    grids built on the device), each compared with the oracle."""
+    import ctypes
+    import plvi
+    lib = plvi.load()
+    cases = [util.local_stereo_case(70 + i, n_left=500 + 60 * i, n_right=450 + 50 * i, n_mp=700 + 80 * i)
+             for i in range(3)]
+    P, cl, cr, mc = len(cases), 700, 600, 900
+    kl = np.zeros((P, cl), plvi.KEYPOINT_DTYPE); kr = np.zeros((P, cr), plvi.KEYPOINT_DTYPE)
+    dl = np.zeros((P, cl, 32), np.uint8); dr = np.zeros((P, cr, 32), np.uint8)
+    bl = np.zeros((P, cl), np.uint8); br = np.zeros((P, cr), np.uint8)
+    l2r = np.full((P, cl), -1, np.int32); r2l = np.full((P, cr), -1, np.int32)
+    nl = np.zeros(P, np.int32); nr = np.zeros(P, np.int32); nm = np.zeros(P, np.int32)
+    fl = np.zeros((P, mc), np.uint8); pr = np.zeros((P, mc, 4), np.float32); lv = np.zeros((P, mc), np.int32)
+    prr = np.zeros((P, mc, 4), np.float32); lvr = np.zeros((P, mc), np.int32); md = np.zeros((P, mc, 32), np.uint8)
+    for p, c in enumerate(cases):
+        a, b, m = len(c["kps"]), len(c["kps_r"]), len(c["mp_flags"])
+        kl[p, :a] = c["kps"]; dl[p, :a] = c["desc"]; bl[p, :a] = c["blocked"]; l2r[p, :a] = c["l2r"]; nl[p] = a
+        kr[p, :b] = c["kps_r"]; dr[p, :b] = c["desc_r"]; br[p, :b] = c["blocked_r"]; r2l[p, :b] = c["r2l"]
+        nr[p] = b
+        fl[p, :m] = c["mp_flags"]; pr[p, :m] = c["mp_proj"]; lv[p, :m] = c["mp_level"]
+        prr[p, :m] = c["mp_proj_r"]; lvr[p, :m] = c["mp_level_r"]; md[p, :m] = c["mp_desc"]; nm[p] = m
+    bufs = []
+
+    def dev(x):
+        b = plvi.DeviceBuffer(max(x.nbytes, 4)); b.upload(np.ascontiguousarray(x)); bufs.append(b)
+        return b.ptr
+    g = cases[0]["grid"]
+    gp = plvi.GridParams(g[0], g[2], g[4], g[5])
+    dkl, dnl, dkr, dnr = dev(kl), dev(nl), dev(kr), dev(nr)
+    col = plvi.DeviceBuffer(P * 3073 * 4); cil = plvi.DeviceBuffer(P * cl * 4)
+    cor = plvi.DeviceBuffer(P * 3073 * 4); cir = plvi.DeviceBuffer(P * cr * 4)
+    plvi.assign_grid_batch(dkl, dnl, cl, P, gp, col.ptr, cil.ptr)
+    plvi.assign_grid_batch(dkr, dnr, cr, P, gp, cor.ptr, cir.ptr)
+    prm = util.local_params(cases[0], 1.0)
+    prm.nnratio = 0.8
+    ml = plvi.DeviceBuffer(P * cl * 4); mr = plvi.DeviceBuffer(P * cr * 4); nmt = plvi.DeviceBuffer(P * 4)
+    V = ctypes.c_void_p
+    rc = lib.plvi_search_local_stereo_batch(P, ctypes.byref(prm), V(dkl), V(dev(dl)), V(dnl), cl, V(dev(bl)),
+                                            V(dev(l2r)), V(col.ptr), V(cil.ptr), V(dkr), V(dev(dr)), V(dnr), cr,
+                                            V(dev(br)), V(dev(r2l)), V(cor.ptr), V(cir.ptr), V(dev(fl)), V(dev(pr)),
+                                            V(dev(lv)), V(dev(prr)), V(dev(lvr)), V(dev(md)), V(dev(nm)), mc,
+                                            V(ml.ptr), V(mr.ptr), V(nmt.ptr), None)
+    assert rc == 0
+    lib.plvi_device_synchronize()
+    ML = ml.download(np.zeros((P, cl), np.int32)); MR = mr.download(np.zeros((P, cr), np.int32))
+    N = nmt.download(np.zeros(P, np.int32))
+    for p, c in enumerate(cases):
+        ne, mle, mre = oracle_lib.search_local_stereo(c, 1.0)
+        assert N[p] == ne
+        np.testing.assert_array_equal(ML[p, :len(mle)], mle)
+        np.testing.assert_array_equal(MR[p, :len(mre)], mre)

@@ -85,3 +85,57 @@ def test_stereo_projection_no_rotation_check_and_degenerate():
             util.proj_params(d, 7.0), d["kps"], d["desc"], d["kps_r"], d["desc_r"], d["x3dc"], d["x3dr"],
             d["last_octave"], d["last_angle"], d["mp_desc"], d["flags"], d["kb8"], d["blocked"], d["blocked_r"])
         assert ng == ne and np.array_equal(mlg, mle) and np.array_equal(mrg, mre), cut
+
+
+@pytest.mark.gpu
+def test_stereo_projection_batch_device():
+    """Several (CurrentFrame, LastFrame) pairs in one plvi_search_by_projection_stereo_batch launch."""
+    import ctypes
+    import plvi
+    lib = plvi.load()
+    cases = [util.projection_stereo_case(80 + i, n_left=600 + 50 * i, n_right=550 + 40 * i, n_last=500 + 60 * i)
+             for i in range(3)]
+    P, cl, cr, lc = len(cases), 800, 700, 700
+    kl = np.zeros((P, cl), plvi.KEYPOINT_DTYPE); kr = np.zeros((P, cr), plvi.KEYPOINT_DTYPE)
+    dl = np.zeros((P, cl, 32), np.uint8); dr = np.zeros((P, cr, 32), np.uint8)
+    bl = np.zeros((P, cl), np.uint8); br = np.zeros((P, cr), np.uint8)
+    nl = np.zeros(P, np.int32); nr = np.zeros(P, np.int32); nlast = np.zeros(P, np.int32)
+    x3 = np.zeros((P, lc, 3), np.float32); x3r = np.zeros((P, lc, 3), np.float32)
+    oc = np.zeros((P, lc), np.int32); an = np.zeros((P, lc), np.float32)
+    md = np.zeros((P, lc, 32), np.uint8); lf = np.zeros((P, lc), np.uint8)
+    for p, c in enumerate(cases):
+        a, b, m = len(c["kps"]), len(c["kps_r"]), len(c["flags"])
+        kl[p, :a] = c["kps"]; dl[p, :a] = c["desc"]; bl[p, :a] = c["blocked"]; nl[p] = a
+        kr[p, :b] = c["kps_r"]; dr[p, :b] = c["desc_r"]; br[p, :b] = c["blocked_r"]; nr[p] = b
+        x3[p, :m] = c["x3dc"]; x3r[p, :m] = c["x3dr"]; oc[p, :m] = c["last_octave"]; an[p, :m] = c["last_angle"]
+        md[p, :m] = c["mp_desc"]; lf[p, :m] = c["flags"]; nlast[p] = m
+    bufs = []
+
+    def dev(x):
+        b = plvi.DeviceBuffer(max(x.nbytes, 4)); b.upload(np.ascontiguousarray(x)); bufs.append(b)
+        return b.ptr
+    g = cases[0]["grid"]
+    gp = plvi.GridParams(g[0], g[2], g[4], g[5])
+    dkl, dnl, dkr, dnr = dev(kl), dev(nl), dev(kr), dev(nr)
+    col = plvi.DeviceBuffer(P * 3073 * 4); cil = plvi.DeviceBuffer(P * cl * 4)
+    cor = plvi.DeviceBuffer(P * 3073 * 4); cir = plvi.DeviceBuffer(P * cr * 4)
+    plvi.assign_grid_batch(dkl, dnl, cl, P, gp, col.ptr, cil.ptr)
+    plvi.assign_grid_batch(dkr, dnr, cr, P, gp, cor.ptr, cir.ptr)
+    prm = util.proj_params(cases[0], 7.0)
+    prm.check_orientation = 1
+    kb = np.ascontiguousarray(cases[0]["kb8"], np.float32)
+    ml = plvi.DeviceBuffer(P * cl * 4); mr = plvi.DeviceBuffer(P * cr * 4); nmt = plvi.DeviceBuffer(P * 4)
+    V = ctypes.c_void_p
+    rc = lib.plvi_search_by_projection_stereo_batch(
+        P, ctypes.byref(prm), kb.ctypes.data_as(V), V(dkl), V(dev(dl)), V(dnl), cl, V(dev(bl)), V(col.ptr),
+        V(cil.ptr), V(dkr), V(dev(dr)), V(dnr), cr, V(dev(br)), V(cor.ptr), V(cir.ptr), V(dev(x3)), V(dev(x3r)),
+        V(dev(oc)), V(dev(an)), V(dev(md)), V(dev(lf)), V(dev(nlast)), lc, V(ml.ptr), V(mr.ptr), V(nmt.ptr), None)
+    assert rc == 0
+    lib.plvi_device_synchronize()
+    ML = ml.download(np.zeros((P, cl), np.int32)); MR = mr.download(np.zeros((P, cr), np.int32))
+    N = nmt.download(np.zeros(P, np.int32))
+    for p, c in enumerate(cases):
+        ne, mle, mre = oracle_lib.search_by_projection_stereo(c, 7.0)
+        assert N[p] == ne
+        np.testing.assert_array_equal(ML[p, :len(mle)], mle)
+        np.testing.assert_array_equal(MR[p, :len(mre)], mre)
