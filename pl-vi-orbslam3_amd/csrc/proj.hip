@@ -118,6 +118,7 @@ __device__ unsigned proj_scan(const plvi_proj_params& p, const ProjLds& s, const
     if (u < p.min_x || u > p.max_x) return 0xFFFFFFFFu;
     if (v < p.min_y || v > p.max_y) return 0xFFFFFFFFu;
     const int nLastOctave = loct[i];
+    if (nLastOctave < 0 || nLastOctave >= p.nlevels) return 0xFFFFFFFFu;  // no scale factor: no candidate
     const float radius = p.th * p.scale_factors[nLastOctave];
     int minLevel, maxLevel;
     if (p.forward) { minLevel = nLastOctave; maxLevel = -1; }
@@ -334,6 +335,7 @@ constexpr unsigned kScanNone = 0xFFFFFFFEu;   // window searched, no candidate (
 __device__ unsigned proj2_scan(const plvi_proj_params& p, const ProjLds& s, const unsigned char* blk, float u, float v,
                                int nLastOctave, const uint8_t* __restrict__ mpd, const uint8_t* __restrict__ cdesc,
                                bool left) {
+    if (nLastOctave < 0 || nLastOctave >= p.nlevels) return left ? kScanSkip : kScanNone;  // no scale factor
     const float radius = p.th * p.scale_factors[nLastOctave];
     int minLevel, maxLevel;
     if (p.forward) { minLevel = nLastOctave; maxLevel = -1; }
