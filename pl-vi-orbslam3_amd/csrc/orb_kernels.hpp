@@ -1519,7 +1519,17 @@ constexpr int kAngR = 15, kAngRows = 2 * kAngR + 1, kAngPitch = 32;
 #ifndef PLVI_DESC_WPE
 #define PLVI_DESC_WPE 5
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PLVI_DESC_WPE))) void orb_describe_kernel(const OrbLevelDev* __restrict__ lvs, int L,
+// PLVI_DESC_SPLIT=1: IC_Angle and rBRIEF as two launches of this kernel
+// (PART 1: orientation only, PART 2: descriptor only, reading the angle
+// PART 1 stored), each with about half the registers of the fused PART 0
+#ifndef PLVI_DESC_SPLIT
+#define PLVI_DESC_SPLIT 0
+#endif
+#ifndef PLVI_DESC_SPLIT_WPE
+#define PLVI_DESC_SPLIT_WPE 8
+#endif
+template <int PART>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PART ? PLVI_DESC_SPLIT_WPE : PLVI_DESC_WPE))) void orb_describe_kernel(const OrbLevelDev* __restrict__ lvs, int L,
                                                            const uint8_t* __restrict__ pyr,
                                                            const uint8_t* __restrict__ blur,
                                                            const int* __restrict__ rect_cnt,
@@ -1568,32 +1578,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PLVI_DESC_W
         // ---- stage both boxes: dword loads first, then LDS writes
         const uint8_t* I0 = pyr + lv.off + (size_t)f * lv.plane + (size_t)(cy - kAngR) * W + (cx - kAngR);
         const uint8_t* B0 = blur + lv.boff + (size_t)f * lv.bplane + (size_t)(cy - kDescR) * BW + (cx - kDescR);
+        constexpr bool doAng = PART != 2, doDesc = PART != 1;
         uint32_t iv[4], bv[6];
         uint8_t blast = 0;
+        if (doAng) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {  // 31 rows x 8 dwords (columns cx-15 .. cx+16)
-            const int i = lane + 64 * k;
-            iv[k] = i < kAngRows * 8 ? ld_u32(I0 + (size_t)(i >> 3) * W + 4 * (i & 7)) : 0u;
+            for (int k = 0; k < 4; ++k) {  // 31 rows x 8 dwords (columns cx-15 .. cx+16)
+                const int i = lane + 64 * k;
+                iv[k] = i < kAngRows * 8 ? ld_u32(I0 + (size_t)(i >> 3) * W + 4 * (i & 7)) : 0u;
+            }
         }
+        if (doDesc) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) {  // 37 rows x 9 dwords (columns cx-18 .. cx+17)
-            const int i = lane + 64 * k, r = i / 9;
-            bv[k] = i < kDescP * 9 ? ld_u32(B0 + (size_t)r * BW + 4 * (i - 9 * r)) : 0u;
+            for (int k = 0; k < 6; ++k) {  // 37 rows x 9 dwords (columns cx-18 .. cx+17)
+                const int i = lane + 64 * k, r = i / 9;
+                bv[k] = i < kDescP * 9 ? ld_u32(B0 + (size_t)r * BW + 4 * (i - 9 * r)) : 0u;
+            }
+            if (lane < kDescP) blast = B0[(size_t)lane * BW + 36];  // column cx+18
         }
-        if (lane < kDescP) blast = B0[(size_t)lane * BW + 36];  // column cx+18
+        if (doAng) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int i = lane + 64 * k;
-            if (i < kAngRows * 8) *reinterpret_cast<uint32_t*>(IP + (i >> 3) * kAngPitch + 4 * (i & 7)) = iv[k];
+            for (int k = 0; k < 4; ++k) {
+                const int i = lane + 64 * k;
+                if (i < kAngRows * 8) *reinterpret_cast<uint32_t*>(IP + (i >> 3) * kAngPitch + 4 * (i & 7)) = iv[k];
+            }
         }
+        if (doDesc) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            const int i = lane + 64 * k, r = i / 9;
-            if (i < kDescP * 9) *reinterpret_cast<uint32_t*>(P + r * kDescPitch + 4 * (i - 9 * r)) = bv[k];
+            for (int k = 0; k < 6; ++k) {
+                const int i = lane + 64 * k, r = i / 9;
+                if (i < kDescP * 9) *reinterpret_cast<uint32_t*>(P + r * kDescPitch + 4 * (i - 9 * r)) = bv[k];
+            }
+            if (lane < kDescP) P[lane * kDescPitch + 36] = blast;
         }
-        if (lane < kDescP) P[lane * kDescPitch + 36] = blast;
         wave_sync();
         // ---- IC_Angle (ORBextractor.cc:75-102)
+        float angle = kp.w;  // PART 2: stored by the PART 1 launch
+        if (doAng) {
         const uint8_t* center = IP + kAngR * kAngPitch + kAngR;
         int m_01 = 0, m_10 = 0;
         if (u <= 15) {
@@ -1611,10 +1632,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PLVI_DESC_W
             m_01 += __shfl_xor(m_01, s2);
             m_10 += __shfl_xor(m_10, s2);
         }
-        const float angle = plvi_fast_atan2((float)m_01, (float)m_10);
+        angle = plvi_fast_atan2((float)m_01, (float)m_10);
         if (lane == 0) {
             kp.w = angle;
             lvkp[(size_t)f * kpCapFrame + slot] = kp;
+        }
+        }
+        if (!doDesc) {
+            wave_sync();  // the next slot's staging overwrites the box
+            continue;
         }
         // ---- rBRIEF (computeOrbDescriptor, ORBextractor.cc:106-145)
         const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);

@@ -475,9 +475,18 @@ struct OrbPipeline {
         mark(5, st);
         if (const int hrc = hook(5, st)) return hrc;
         // K6 orientation + rBRIEF
-        hipLaunchKernelGGL(orb_describe_kernel, dim3((kpCapFrame + 15) / 16, nf), dim3(256), 0, st,
-                           d_lv.as<OrbLevelDev>(), L, (const uint8_t*)P, (const uint8_t*)Bl,
-                           (const int*)rectCnt.as<int>(), lvkp.as<float4>(), lvdesc.as<uint8_t>(), kpCapFrame);
+        if (PLVI_DESC_SPLIT) {
+            hipLaunchKernelGGL(orb_describe_kernel<1>, dim3((kpCapFrame + 15) / 16, nf), dim3(256), 0, st,
+                               d_lv.as<OrbLevelDev>(), L, (const uint8_t*)P, (const uint8_t*)Bl,
+                               (const int*)rectCnt.as<int>(), lvkp.as<float4>(), lvdesc.as<uint8_t>(), kpCapFrame);
+            hipLaunchKernelGGL(orb_describe_kernel<2>, dim3((kpCapFrame + 15) / 16, nf), dim3(256), 0, st,
+                               d_lv.as<OrbLevelDev>(), L, (const uint8_t*)P, (const uint8_t*)Bl,
+                               (const int*)rectCnt.as<int>(), lvkp.as<float4>(), lvdesc.as<uint8_t>(), kpCapFrame);
+        } else {
+            hipLaunchKernelGGL(orb_describe_kernel<0>, dim3((kpCapFrame + 15) / 16, nf), dim3(256), 0, st,
+                               d_lv.as<OrbLevelDev>(), L, (const uint8_t*)P, (const uint8_t*)Bl,
+                               (const int*)rectCnt.as<int>(), lvkp.as<float4>(), lvdesc.as<uint8_t>(), kpCapFrame);
+        }
         mark(6, st);
         // K7 assemble
         hipLaunchKernelGGL(orb_assemble_kernel, dim3(nf), dim3(256), 0, st, d_lv.as<OrbLevelDev>(), L,
