@@ -87,7 +87,7 @@ struct LinePipeline {
     double gk[7]{};
     int lbdTaps[3] = {14, 62, 104};
     DevBuf d_oct, d_tabs, octImg, pix, modg, seedcs, gbits, qspill, regs, regpts, rawLines, nlines, klTmp, klOut, fnOut, cntOut, descOut, lbdBlur,
-        lbdG, err, staging, mwOwn, mwSlot, mwGrow;
+        lbdG, err, staging, mwOwn, mwSlot, mwGrow, mwHMap, mwHRec, mwHPts, mwHCur, mwHOwn, mwHGq;
     size_t qspillFrame = 0, gbitsFrame = 0, lbdPlaneTotal = 0;
     int lastFrames = 0;
     static constexpr int kStages = 5, kRing = 512;
@@ -449,6 +449,31 @@ struct LinePipeline {
                     mwGrow.alloc(sizeof(unsigned) * (size_t)kMwWaves * kMwGSpill * tasks))
                     return PLVI_E_HIP;
                 PLVI_CHECK(hipMemset(mwOwn.p, 0, mwOwn.bytes));  // kept zero by every launch
+                // helper workgroups (octave 0 of small batches, on the CUs the
+                // tasks leave idle): PLVI_MW_HELP = most helpers per task (0 = off)
+                mwHelpMax = 0;
+                if (const char* e = getenv("PLVI_MW_HELP")) mwHelpMax = std::max(0, std::min(kMwHelpMax, atoi(e)));
+                if (!PLVI_MW_HELPERS) mwHelpMax = 0;  // built without the helper role
+                mwHMapTask = gbitsFrame * 32;  // bit indices of the largest octave
+                if (mwHelpMax > 0 && mwHMapTask < (1u << 20)) {
+                    int dev = 0;
+                    PLVI_CHECK(hipGetDevice(&dev));
+                    PLVI_CHECK(hipDeviceGetAttribute(&mwCUs, hipDeviceAttributeMultiprocessorCount, dev));
+                    mwHelpWgs = std::max(8, mwCUs / 2);
+                    const size_t W = (size_t)mwHelpWgs;
+                    if (mwHMap.alloc(sizeof(unsigned) * mwHMapTask * W) ||
+                        mwHRec.alloc(sizeof(MwHelpRec) * kMwHelpRecCap * W) ||
+                        mwHPts.alloc(sizeof(unsigned) * mwHMapTask * W) || mwHCur.alloc(sizeof(unsigned) * W) ||
+                        mwHOwn.alloc(sizeof(unsigned) * mwOwnTask * W) ||
+                        mwHGq.alloc(sizeof(unsigned) * (size_t)kMwWaves * kMwGSpill * W))
+                        return PLVI_E_HIP;
+                    PLVI_CHECK(hipMemset(mwHMap.p, 0, mwHMap.bytes));
+                    PLVI_CHECK(hipMemset(mwHRec.p, 0, mwHRec.bytes));
+                    PLVI_CHECK(hipMemset(mwHCur.p, 0, mwHCur.bytes));
+                    PLVI_CHECK(hipMemset(mwHOwn.p, 0, mwHOwn.bytes));  // kept zero by every launch
+                } else {
+                    mwHelpMax = 0;
+                }
                 for (const void* k : {(const void*)lsd_grow_mw_kernel<kMwWaves, false>,
                                       (const void*)lsd_grow_mw_kernel<kMwWaves, true>})
                     PLVI_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mwSmem));
@@ -463,6 +488,9 @@ struct LinePipeline {
     bool rectLanes = true;
     int mwMaxFrames = 0, mwSlots = 0;
     size_t mwSmem = 0, mwOwnTask = 0;
+    int mwHelpMax = 0, mwHelpWgs = 0, mwCUs = 0;  // helpers per task (most), helper workgroups buffered, CUs
+    size_t mwHMapTask = 0;
+    unsigned mwEpoch = 0;
     int* mwStats = nullptr;  // diagnostic counters (plvi_lines_debug_mw_stats)
     size_t growSmem = 0;
     int growWPW = 1;  // region-growing tasks (waves) per workgroup
@@ -536,11 +564,23 @@ struct LinePipeline {
     void launch_grow(int nf, int oBase, int oCount, hipStream_t st) {
         if (nf <= mwMaxFrames) {
             auto mwK = mwStats ? lsd_grow_mw_kernel<kMwWaves, true> : lsd_grow_mw_kernel<kMwWaves, false>;
-            hipLaunchKernelGGL(mwK, dim3(oCount * nf), dim3(kMwWaves * 64), mwSmem, st, d_oct.as<LineOctDev>(),
+            // helpers for the launches that grow octave 0: as many per task as
+            // the CUs left by every octave's tasks allow (one workgroup per CU)
+            const int nT = oCount * nf, nTp = (nT + 7) & ~7;
+            int K = 0;
+            if (mwHelpMax > 0 && oBase == 0) {
+                K = std::min(mwHelpMax, (mwCUs - nf * nOct) / nT);
+                K = std::max(0, std::min(K, mwHelpWgs / nTp));
+            }
+            MwHelp Hp{mwHMap.as<unsigned>(), mwHMapTask, mwHRec.as<MwHelpRec>(), mwHPts.as<unsigned>(),
+                      mwHCur.as<unsigned>(), mwHOwn.as<unsigned>(), mwOwnTask, mwHGq.as<unsigned>(), K, nTp,
+                      (int)mwHMapTask, ++mwEpoch};
+            hipLaunchKernelGGL(mwK, dim3(nTp * (K + 1)), dim3(kMwWaves * 64), mwSmem, st, d_oct.as<LineOctDev>(),
                                (const float*)pix.as<float>(), (const float2*)seedcs.as<float2>(),
                                mwOwn.as<unsigned>(), mwOwnTask, mwGrow.as<unsigned>(), mwSlot.as<unsigned>(),
                                qspill.as<unsigned>(), qspillFrame, prec, regs.as<LsdRegion>(), regpts.as<unsigned>(),
-                               qspillFrame, nlines.as<int>(), err.as<int>(), mwSlots, nOct, oBase, oCount, mwStats);
+                               qspillFrame, nlines.as<int>(), err.as<int>(), mwSlots, nOct, oBase, oCount, mwStats, nf,
+                               Hp);
             return;
         }
         auto growK = growStats ? lsd_grow_kernel<true> : lsd_grow_kernel<false>;

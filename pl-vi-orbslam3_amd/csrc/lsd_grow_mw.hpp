@@ -32,6 +32,15 @@
 // speculative seeds in increasing order with their slots).  Commit order =
 // raster seed order, so the region list handed to lsd_rect_kernel is the
 // sequential kernel's.
+//
+// Helper workgroups (nHelp per task, on other CUs): helper k grows the seeds
+// of row band k + 1 of nHelp + 1 ahead of the task's own growers with the
+// same rule and no committed bitmap at all (an empty C is a subset of the
+// walk's, so the validation above still decides), and publishes each region
+// in global memory behind an agent-scope release; a grower of the task whose
+// cursor reaches that seed imports it (agent-scope acquire) into a slot
+// instead of growing it, marked for revalidation.  A seed no helper has
+// published yet is grown as before, so helpers only move work off the CU.
 // ---------------------------------------------------------------------------
 #pragma once
 
@@ -96,7 +105,7 @@ struct MwCtl {
     int stat[16];  // [0] dispatched [1] dropped [2] regrown [3] exact (undispatched) [4] trivial [5] committed
                    // speculative [6] walk cycles [7] walker growth cycles [8] walk entries [9] blocked on a
                    // growing head [10] kernel cycles (wave 0) [11] speculative growth cycles (sum over waves)
-                   // [12] idle polls [13] blocks (completed regions) [14] block setup cycles / 16
+                   // [12] regions imported from helpers [13] blocks (completed regions) [14] block setup cycles / 16
                    // [15] block round cycles / 16
 };
 
@@ -226,7 +235,7 @@ __device__ __forceinline__ void mw_unlock(lds_i32* l, int lane) {
 // Grow the region of seed (sx, sy) into Q (region_grow, lsd.cpp:635-686).
 // SPEC: abandon when the walk passes the seed.  Returns 0 = grown, 1 =
 // abandoned, 2 = queue overflow; n = points in Q (own marks set for them).
-template <bool SPEC, bool STATS = false>
+template <bool SPEC, bool STATS = false, bool HELP = false>
 __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_out, float& deg_out, bool& spilled,
                        int lane) {
     unsigned long long c_setup = 0, c_round = 0, n_blk = 0;
@@ -294,7 +303,9 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
         // own marks and the committed bitmap, read once per block (within the
         // block a lane's pixel only changes through an earlier lane's commit
         // of the same pixel: dup / Ccum)
-        const bool live0 = valid && deg != kNotdefF && !mw_bit(E.C, E.wpr, nx, ny) && !mw_own_get(E, nx, ny, sy);
+        // (a helper has no committed bitmap: HELP)
+        const bool live0 =
+            valid && deg != kNotdefF && (HELP || !mw_bit(E.C, E.wpr, nx, ny)) && !mw_own_get(E, nx, ny, sy);
         unsigned long long tb1 = 0;
         if (STATS) {
             tb1 = __builtin_amdgcn_s_memtime();
@@ -587,7 +598,7 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
 // dispatch log with its slot.  Returns the seed (-1: none) and the slot.
 template <bool STATS>
 __device__ __forceinline__ int mw_dispatch(const MwEnv& E, lds_u8* pool, int nslots, lds_i32* dlog, int& slot,
-                                           int lane) {
+                                           unsigned* hcur, unsigned ctag, int lane) {
     lds_ctl* ctl = E.ctl;
     const int nwords = E.sh * E.wpr;
     const int dn = mw_peek(&ctl->dlog_n);  // written under dlock only (held)
@@ -635,6 +646,7 @@ __device__ __forceinline__ int mw_dispatch(const MwEnv& E, lds_u8* pool, int nsl
         S->chk = mw_peek(&ctl->ncommit);
         mw_lds_store(&S->state, kMwGrowing);  // before the log entry that names it
         ctl->cursor = q + 1;
+        if (hcur) gstore_l2(hcur, ctag | (unsigned)q);  // where the helpers' work starts to pay (a hint)
         dlog[2 * (dn & (kMwLog - 1))] = q;
         dlog[2 * (dn & (kMwLog - 1)) + 1] = slot;
         mw_lds_store(&ctl->dlog_n, dn + 1);
@@ -722,18 +734,239 @@ __device__ __forceinline__ void mw_copy_points(const MwQueue& A, const MwQueue& 
     if (__ballot(g)) vm_drain();
 }
 
+
+// ---------------------------------------------------------------------------
+// Helper workgroups.  Records and points of the regions a helper grew live in
+// global memory; the task's per-pixel map names the record of a seed.  Map
+// entries and the cursor hint carry the launch epoch, so no buffer is cleared
+// between launches (a stale entry fails the epoch or the record's seed check).
+struct MwHelpRec {
+    int seed, n, off;  // seed bit index, points, offset in the helper's point area
+    float deg;         // final region angle (float degrees)
+    unsigned epoch;
+    int pad[3];
+};
+// Compiled out by default: with up to 7 helpers per task the task's growers
+// import most regions (1 439 of 1 742 dispatched at one frame) but region
+// growing stays at 7.0-7.5 ms per frame and 8.6-10 ms per 64 frames -- the
+// walk's own chain (exact growth of invalidated and undispatched seeds,
+// ~7M of 18M cycles, plus the commits) bounds the kernel, not the growers
+// (profiles/r04/mw_helpers_ab.txt); compiled in, the extra kernel state
+// costs 1-2 % even with no helper launched.  PLVI_MW_HELPERS=1 builds it.
+#ifndef PLVI_MW_HELPERS
+#define PLVI_MW_HELPERS 0
+#endif
+constexpr int kMwHelpRecCap = 4096;  // records per helper workgroup (map ids: 16 bits, nHelp <= 15)
+constexpr int kMwHelpMax = 15;
+struct MwHelp {
+    unsigned* map;     // per task: bit index -> (epoch & 0xffff) << 16 | (k * kMwHelpRecCap + record + 1)
+    size_t mapTask;    // entries per task
+    MwHelpRec* rec;    // per helper workgroup: kMwHelpRecCap records
+    unsigned* pts;     // per helper workgroup: ptsCap points
+    unsigned* cur;     // per task: (epoch & 0xfff) << 20 | the task's dispatch cursor (a hint)
+    unsigned* own;     // per helper workgroup: NW own-mark spills (sh x wpr words each)
+    size_t ownWg;      // words per helper workgroup
+    unsigned* gq;      // per helper workgroup: NW growth-queue spills (kMwGSpill each)
+    int nHelp, nTp;    // helpers per task; tasks padded to a multiple of 8 (grid sections)
+    int ptsCap;
+    unsigned epoch;
+};
+
+// A grower of the task took seed q into slot si: import the region a helper
+// published for it, if any (agent-scope acquire after the map entry is seen).
+// The region was grown with an empty committed bitmap: chk = -1 sends it
+// through revalidation; the walker validates it like any other.
+__device__ __forceinline__ bool mw_import(const MwEnv& E, const MwHelp& Hp, int t, lds_u8* pool, unsigned* sspill,
+                                          int si, int q, int lane) {
+    const unsigned hv = gload_l2(Hp.map + (size_t)t * Hp.mapTask + q);
+    if ((hv >> 16) != (Hp.epoch & 0xffffu) || (hv & 0xffffu) == 0u) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const int g = (int)(hv & 0xffffu) - 1, k = g / kMwHelpRecCap, r = g - k * kMwHelpRecCap;
+    const size_t hwg = (size_t)k * Hp.nTp + t;
+    const MwHelpRec R = Hp.rec[hwg * kMwHelpRecCap + r];
+    if (R.seed != q || R.epoch != Hp.epoch || R.n > kMwSP + kMwSlotSpill) return false;
+    const unsigned* P = Hp.pts + hwg * Hp.ptsCap + R.off;
+    const MwQueue Q = mw_slot_queue(pool, sspill, si);
+    bool gl = false;
+    for (int j = lane; j < R.n; j += 64) {
+        const unsigned v = P[j];
+        mw_qput(Q, j, v);
+        mw_or(E.H, E.wpr, (int)(v & 0xffffu), (int)(v >> 16));  // claimed: the cursor skips seeds inside it
+        gl |= j >= Q.lcap;
+    }
+    if (__ballot(gl)) vm_drain();
+    if (lane == 0) {
+        lds_slot* S = mw_slot(pool, si);
+        S->n = R.n;
+        S->deg = R.deg;
+        S->ovf = 0;
+        S->chk = -1;
+    }
+    return true;
+}
+
+// Helper dispatch (caller holds the helper's lock): the next seed of the band
+// [cursor, yEnd) that is neither NOTDEF / trivial (T) nor inside a region this
+// helper grew (H); a cursor the task's own growers passed moves ahead of them.
+__device__ __forceinline__ int mw_help_dispatch(const MwEnv& E, int yEnd, const unsigned* hcur, unsigned ctag,
+                                                int lane) {
+    lds_ctl* ctl = E.ctl;
+    const int nwords = min(E.sh, yEnd) * E.wpr;
+    int cur = ctl->cursor;
+    const unsigned mc = gload_l2(const_cast<unsigned*>(hcur));
+    if ((mc & 0xfff00000u) == ctag && (int)(mc & 0xfffffu) + 2 * E.rowbits > cur)
+        cur = (int)(mc & 0xfffffu) + 2 * E.rowbits;  // two rows ahead of the task's cursor
+    int w = cur >> 5;
+    if (w >= nwords) return -1;
+    unsigned m = ~(E.T[w] | mw_peek(E.H + w)) & (~0u << (cur & 31));
+    if (!m) {
+        int found = -1;
+        for (int w0 = w + 1; w0 < nwords && found < 0; w0 += 64) {
+            const int ww = w0 + lane;
+            const bool nz = ww < nwords && (E.T[ww] | mw_peek(E.H + ww)) != ~0u;
+            const unsigned long long b = __ballot(nz);
+            if (b) found = w0 + __ffsll((long long)b) - 1;
+        }
+        if (found < 0) {
+            if (lane == 0) ctl->cursor = nwords * 32;
+            return -1;
+        }
+        w = found;
+        m = ~(E.T[w] | mw_peek(E.H + w));
+    }
+    const int q = w * 32 + (__ffs((int)m) - 1);
+    if (lane == 0) ctl->cursor = q + 1;
+    return q;
+}
+
+// A helper workgroup (NW grower waves): grows the seeds of its band and
+// publishes every region it completes.
+template <int NW, bool STATS>
+__device__ void mw_helper(const LineOctDev& od, const float* P, const float2* SC, double prec, const MwHelp& Hp, int k,
+                          int t, unsigned* lds_u) {
+    const int sw = od.sw, sh = od.sh, wpr = (sw + 31) >> 5;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int y0 = sh * (k + 1) / (Hp.nHelp + 1), y1 = sh * (k + 2) / (Hp.nHelp + 1);
+    // LDS: ctl | T (NOTDEF or trivial) | H | own windows | growth queues
+    lds_ctl* ctl = (lds_ctl*)lds_u;
+    const int nwords = sh * wpr;
+    lds_u32* T = (lds_u32*)(lds_u + sizeof(MwCtl) / 4);
+    lds_u32* H = T + nwords;
+    lds_u32* ownAll = H + nwords;
+    lds_u32* gqAll = ownAll + NW * kMwRB * wpr;
+    const size_t hwg = (size_t)k * Hp.nTp + t;
+    MwEnv E;
+    E.P = P;
+    E.SC = SC;
+    E.C = nullptr;
+    E.T = T;
+    E.H = H;
+    E.own = ownAll + wv * kMwRB * wpr;
+    E.ownG = Hp.own + hwg * Hp.ownWg + (size_t)wv * sh * wpr;
+    E.ctl = ctl;
+    E.sw = sw; E.sh = sh; E.wpr = wpr; E.rowbits = wpr * 32;
+    E.pdeg = (float)(prec / kD2R);
+    E.prec = prec;
+    const MwQueue GQ{gqAll + wv * kMwGQ, kMwGQ, Hp.gq + (hwg * NW + wv) * kMwGSpill, kMwGSpill};
+    const unsigned ctag = (Hp.epoch & 0xfffu) << 20;
+    const unsigned* hcur = Hp.cur + t;
+    const float pdeg = E.pdeg;
+    const int min_reg = od.min_reg_size;
+    for (int i = threadIdx.x; i < 2 * nwords; i += NW * 64) T[i] = i < nwords ? ~0u : 0u;  // T outside the band: no seed
+    for (int i = threadIdx.x; i < NW * kMwRB * wpr; i += NW * 64) ownAll[i] = 0u;
+    if (threadIdx.x == 0) {
+        ctl->lock = ctl->dlock = 0;
+        ctl->cursor = y0 * E.rowbits;
+        ctl->npts = ctl->nout = 0;
+        for (int i = 0; i < 16; ++i) ctl->stat[i] = 0;
+    }
+    __syncthreads();
+    // T over the band (the task's C | T set-up restricted to its rows)
+    for (int kk = wv; kk < (y1 - y0) * ((wpr + 1) >> 1); kk += NW) {
+        const int y = y0 + kk / ((wpr + 1) >> 1), xb = (kk - (y - y0) * ((wpr + 1) >> 1)) * 64;
+        const int x = xb + lane;
+        const float* r0 = P + (size_t)y * sw;
+        float d0 = kNotdefF, dr = kNotdefF, dbl = kNotdefF, db = kNotdefF, dbr = kNotdefF;
+        if (x < sw) {
+            d0 = r0[x];
+            if (x + 1 < sw) dr = r0[x + 1];
+            if (y + 1 < sh) {
+                const float* r1 = r0 + sw;
+                if (x > 0) dbl = r1[x - 1];
+                db = r1[x];
+                if (x + 1 < sw) dbr = r1[x + 1];
+            }
+        }
+        const bool def = x < sw && d0 != kNotdefF;
+        const bool grows = is_aligned_fast(dr, d0, pdeg, prec) || is_aligned_fast(dbl, d0, pdeg, prec) ||
+                           is_aligned_fast(db, d0, pdeg, prec) || is_aligned_fast(dbr, d0, pdeg, prec);
+        const unsigned long long tm = __ballot(!def || (!grows && min_reg > 1));
+        if (lane < 2 && (xb >> 5) + lane < wpr) T[y * wpr + (xb >> 5) + lane] = lane == 0 ? (unsigned)tm : (unsigned)(tm >> 32);
+    }
+    __syncthreads();
+    unsigned* map = Hp.map + (size_t)t * Hp.mapTask;
+    while (true) {
+        int q = -1;
+        while (true) {  // the lock (no other work to do meanwhile)
+            if (mw_try_lock(&ctl->dlock, lane)) {
+                q = mw_help_dispatch(E, y1, hcur, ctag, lane);
+                mw_unlock(&ctl->dlock, lane);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (q < 0) break;
+        int n = 0;
+        float deg = 0.f;
+        bool spilled = false;
+        const int rc = mw_grow<false, STATS, true>(E, q % E.rowbits, q / E.rowbits, GQ, n, deg, spilled, lane);
+        int r = 0, off = 0;
+        if (rc == 0 && lane == 0) {
+            r = __hip_atomic_fetch_add(&ctl->nout, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            off = __hip_atomic_fetch_add(&ctl->npts, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        r = __builtin_amdgcn_readfirstlane(r);
+        off = __builtin_amdgcn_readfirstlane(off);
+        if (rc == 0 && r < kMwHelpRecCap && off + n <= Hp.ptsCap) {
+            unsigned* dst = Hp.pts + hwg * Hp.ptsCap + off;
+            for (int j = lane; j < n; j += 64) dst[j] = mw_qget(GQ, j);
+            if (lane == 0) Hp.rec[hwg * kMwHelpRecCap + r] = MwHelpRec{q, n, off, deg, Hp.epoch, {0, 0, 0}};
+            // publish: this wave's stores, then an agent-scope release, then the map entry
+            __builtin_amdgcn_s_waitcnt(0);
+            if (lane == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(map + q, ((Hp.epoch & 0xffffu) << 16) | (unsigned)(k * kMwHelpRecCap + r + 1),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        mw_own_clear(E, q / E.rowbits, GQ, n, spilled, lane);
+    }
+}
+
 template <int NW, bool STATS>
 __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
     const LineOctDev* __restrict__ octs, const float* __restrict__ pix, const float2* __restrict__ pixcs,
     unsigned* __restrict__ ownspill, size_t ownspill_task, unsigned* __restrict__ gspill, unsigned* __restrict__ slotspill,
     unsigned* __restrict__ xspill, size_t xspill_task, double prec, LsdRegion* __restrict__ regs,
     unsigned* __restrict__ regpts, size_t regpts_frame, int* __restrict__ nlines, int* __restrict__ err, int nslots,
-    int nOct, int oBase, int oCount, int* __restrict__ stats) {
+    int nOct, int oBase, int oCount, int* __restrict__ stats, int nf, MwHelp Hp) {
     extern __shared__ __align__(16) unsigned lds_u[];
     __builtin_amdgcn_s_setprio(PLVI_GROW_SETPRIO);
-    const int nf = gridDim.x / oCount;
-    const int o = oBase + blockIdx.x / nf, f = blockIdx.x - (o - oBase) * nf;
+    // grid: nHelp + 1 sections of nTp blocks (tasks padded to a multiple of 8,
+    // so that a task's helpers share its XCD when blocks are dealt round-robin
+    // over the XCDs); section 0 = the tasks, section k + 1 = helper k
+    const int sec = blockIdx.x / Hp.nTp, t = blockIdx.x - sec * Hp.nTp;
+    if (t >= nf * oCount) return;
+    const int o = oBase + t / nf, f = t - (o - oBase) * nf;
     const int task = f * nOct + o;
+    if (PLVI_MW_HELPERS && sec > 0) {
+        const LineOctDev& hod = octs[o];
+        __builtin_amdgcn_s_setprio(PLVI_MW_GROWER_PRIO);
+        mw_helper<NW, STATS>(hod, pix + hod.soff + (size_t)f * hod.splane, pixcs + hod.soff + (size_t)f * hod.splane,
+                             prec, Hp, sec - 1, t, lds_u);
+        return;
+    }
     const LineOctDev& od = octs[o];
     const int sw = od.sw, sh = od.sh, wpr = (sw + 31) >> 5;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -766,6 +999,10 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
                                          gspill + ((size_t)task * NW + wv) * kMwGSpill, kMwGSpill};
     LsdRegion* outR = regs + (size_t)task * kLsdRawCap;
     unsigned* outP = regpts + (size_t)task * regpts_frame;
+    // helpers of this task: the dispatch cursor hint and the first seed of their bands
+    unsigned* hcur = PLVI_MW_HELPERS && Hp.nHelp > 0 ? Hp.cur + t : nullptr;
+    const unsigned ctag = (Hp.epoch & 0xfffu) << 20;
+    const int helpStart = (sh / (Hp.nHelp + 1)) * E.rowbits;
 
     const unsigned long long t_kernel = STATS ? __builtin_amdgcn_s_memtime() : 0;
     // ---- init: C = NOTDEF (and row padding), T = trivial seeds, H = 0
@@ -928,7 +1165,7 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
             // a new speculative region
             int q = -1, si = -1;
             if (mw_try_lock(&ctl->dlock, lane)) {
-                q = mw_dispatch<STATS>(E, pool, nslots, dlog, si, lane);
+                q = mw_dispatch<STATS>(E, pool, nslots, dlog, si, hcur, ctag, lane);
                 mw_unlock(&ctl->dlock, lane);
             }
             if (q < 0 && kMwLate > 0 && mw_try_lock(&ctl->dlock, lane)) {
@@ -936,8 +1173,14 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
                 mw_unlock(&ctl->dlock, lane);
             }
             if (q < 0) {
-                if (STATS && lane == 0) mw_stat(ctl, 12, 1);
                 __builtin_amdgcn_s_sleep(2);
+                continue;
+            }
+            // a region a helper already grew for this seed
+            if (hcur && q >= helpStart && mw_import(E, Hp, t, pool, sspill, si, q, lane)) {
+                if (STATS && lane == 0) mw_stat(ctl, 12, 1);
+                mw_wave_sync();
+                if (lane == 0) mw_lds_store(&mw_slot(pool, si)->state, kMwDone);
                 continue;
             }
             int n = 0;

@@ -461,7 +461,12 @@ __device__ __forceinline__ unsigned orb_cell_axis(int v, int minB, int cell, int
 #ifndef PLVI_BF_WPE
 #define PLVI_BF_WPE 1  // waves per EU blur + FAST is compiled for (1: no cap)
 #endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PLVI_BF_WPE))) void orb_blur_fast_kernel(const OrbLevelDev* __restrict__ lvs,
+#ifdef PLVI_BF_VGPR  // hard VGPR cap (A/B builds)
+#define PLVI_BF_NUMVGPR __attribute__((amdgpu_num_vgpr(PLVI_BF_VGPR)))
+#else
+#define PLVI_BF_NUMVGPR
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PLVI_BF_WPE))) PLVI_BF_NUMVGPR void orb_blur_fast_kernel(const OrbLevelDev* __restrict__ lvs,
                                                            const OrbStripDev* __restrict__ strips,
                                                            const uint8_t* __restrict__ frames, size_t f_frame,
                                                            size_t f_row, uint8_t* __restrict__ pyr,
@@ -1521,9 +1526,12 @@ constexpr int kAngR = 15, kAngRows = 2 * kAngR + 1, kAngPitch = 32;
 #endif
 // PLVI_DESC_SPLIT=1: IC_Angle and rBRIEF as two launches of this kernel
 // (PART 1: orientation only, PART 2: descriptor only, reading the angle
-// PART 1 stored), each with about half the registers of the fused PART 0
+// PART 1 stored), each with about half the registers of the fused PART 0.
+// Default: beside the growth waves (6 per SIMD) the fused kernel's 96 VGPRs
+// fit one wave per SIMD, the parts' 44 / 64 fit two or more; at two batches
+// in flight the step measured 48.5K vs 47.8K FPS (profiles/r04/ab_sched_inflight2.txt)
 #ifndef PLVI_DESC_SPLIT
-#define PLVI_DESC_SPLIT 0
+#define PLVI_DESC_SPLIT 1
 #endif
 #ifndef PLVI_DESC_SPLIT_WPE
 #define PLVI_DESC_SPLIT_WPE 8

@@ -108,3 +108,44 @@ def test_rect_lane_per_region_equals_wave_per_region(plvi_lib, monkeypatch, mw):
             assert _same(lanes[f], waves[f]), f"n={n} frame {f}: lane-per-region != wave-per-region"
     kl, de, fn = ol.line_extract(frames[0])
     assert _same(lanes[0], (kl.astype(plvi.KEYLINE_DTYPE), de, fn))
+
+
+@pytest.mark.parametrize("helpers", [0, 1, 7, 15])
+def test_mw_helper_workgroups(plvi_lib, monkeypatch, helpers):
+    """Helper workgroups (a PLVI_MW_HELPERS=1 build; PLVI_MW_HELP: up to that
+    many per octave-0 task on idle CUs) grow the seeds of later row bands with an empty committed bitmap
+    and publish them; the task's growers import them, the walker validates
+    them.  The lines stay the oracle's bit for bit, and with helpers some
+    regions come from them (counter 12)."""
+    monkeypatch.setenv("PLVI_MW_HELP", str(helpers))
+    frames = np.concatenate([synth.batch(3, seed0=410), structured_frames()["checker"][None]])
+    mw, st = _run(monkeypatch, frames, 256, stats=True)
+    for f in range(len(frames)):
+        assert _same(mw[f], ol.line_extract(frames[f])), f"helpers={helpers} frame {f}"
+    imported = int(st[:3, 0, 12].sum())
+    if helpers > 0 and imported == 0:
+        pytest.skip("library built without helper workgroups (PLVI_MW_HELPERS=0, the default)")
+    assert (imported > 0) == (helpers > 0), st[:, 0, 12]
+
+
+def test_mw_helpers_across_launches(plvi_lib, monkeypatch):
+    """One extractor, consecutive launches over different frames: the helpers'
+    per-pixel map and records are not cleared between launches (the launch
+    epoch tags them), so a region published for another frame is never
+    imported."""
+    monkeypatch.setenv("PLVI_GROW_MW", "256")
+    monkeypatch.setenv("PLVI_MW_HELP", "3")
+    frames = synth.batch(4, seed0=520)
+    lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 640, 480, max_batch=2)
+    lib = plvi.load()
+    buf = plvi.DeviceBuffer(frames.nbytes)
+    buf.upload(frames)
+    for rep in range(2):
+        for i in (0, 2, 1):  # frame pairs (0, 1), (2, 3), (1, 2)
+            lx.extract_batch(buf.ptr + i * 640 * 480, 2, 640 * 480, 640)
+            lib.plvi_device_synchronize()
+            assert lx.errors() == 0
+            out = _tables(lx, 2)
+            for f in range(2):
+                assert _same(out[f], ol.line_extract(frames[i + f])), f"rep {rep} pair {i} frame {f}"
+    lx.close()
