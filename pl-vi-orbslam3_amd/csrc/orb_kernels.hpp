@@ -78,6 +78,9 @@ __device__ __forceinline__ void lds_publish(lds_i32* p, int v, int lane) {
     do {                                                                         \
         if (PLVI_ORB_SETPRIO) __builtin_amdgcn_s_setprio(PLVI_ORB_SETPRIO);      \
     } while (0)
+#ifndef PLVI_BF_SETPRIO
+#define PLVI_BF_SETPRIO 0  // s_setprio of the blur + FAST waves alone (0: as the ORB chain)
+#endif
 
 #ifndef PLVI_PYR_WPE
 #define PLVI_PYR_WPE 1  // waves per EU the pyramid kernel is compiled for (1: no cap)
@@ -474,7 +477,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PLVI_BF_WPE)
                                                            uint8_t* __restrict__ cthr, int thrFrame, int k0, int k1,
                                                            int k2, int k3, int tmin, int t1, int t2, int nstrips,
                                                            int nf) {
-    PLVI_ORB_PRIO_SET();
+    if (PLVI_BF_SETPRIO) __builtin_amdgcn_s_setprio(PLVI_BF_SETPRIO);
+    else PLVI_ORB_PRIO_SET();
     static_assert(!PLVI_BF_NMS || PLVI_BF_PK, "the fused NMS queues from the packed scorer");
     typedef typename std::conditional<PLVI_BF_LEAN != 0, unsigned short, unsigned>::type QT;
     __shared__ __align__(16) uint8_t ring[kRingRows + kRingMirror][kRingW];
@@ -1527,11 +1531,14 @@ constexpr int kAngR = 15, kAngRows = 2 * kAngR + 1, kAngPitch = 32;
 // PLVI_DESC_SPLIT=1: IC_Angle and rBRIEF as two launches of this kernel
 // (PART 1: orientation only, PART 2: descriptor only, reading the angle
 // PART 1 stored), each with about half the registers of the fused PART 0.
-// Default: beside the growth waves (6 per SIMD) the fused kernel's 96 VGPRs
-// fit one wave per SIMD, the parts' 44 / 64 fit two or more; at two batches
-// in flight the step measured 48.5K vs 47.8K FPS (profiles/r04/ab_sched_inflight2.txt)
+// Beside the growth waves (6 per SIMD) the fused kernel's 96 VGPRs fit one
+// wave per SIMD, the parts' 44 / 64 fit two or more: at two batches in
+// flight the step is 0.7-1.5 % faster (within the spread between boxes), but
+// the extra describe waves slow the other batch's blur + FAST launches from
+// 9-11 to 15-16 ms in the timed window (profiles/r04/ab_sched_inflight2.txt),
+// so the fused kernel stays the default
 #ifndef PLVI_DESC_SPLIT
-#define PLVI_DESC_SPLIT 1
+#define PLVI_DESC_SPLIT 0
 #endif
 #ifndef PLVI_DESC_SPLIT_WPE
 #define PLVI_DESC_SPLIT_WPE 8
