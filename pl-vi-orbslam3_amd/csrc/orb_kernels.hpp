@@ -1554,7 +1554,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PART ? PLVI
     __shared__ __align__(16) uint8_t patch[4][kDescP * kDescPitch];
     __shared__ __align__(16) uint8_t ipatch[4][kAngRows * kAngPitch];
     const int f = blockIdx.y;
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the wave index read uniformly: the slot walk, the level record and the
+    // box bases derived from it stay scalar (SGPR addresses, not 64-bit VGPR pairs)
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
     uint8_t* P = patch[wv];
     uint8_t* IP = ipatch[wv];
     const int half = lane >> 5, u = (lane & 31) - 15;
