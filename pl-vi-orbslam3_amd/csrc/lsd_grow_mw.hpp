@@ -845,7 +845,7 @@ template <int NW, bool STATS>
 __device__ void mw_helper(const LineOctDev& od, const float* P, const float2* SC, double prec, const MwHelp& Hp, int k,
                           int t, unsigned* lds_u) {
     const int sw = od.sw, sh = od.sh, wpr = (sw + 31) >> 5;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int y0 = sh * (k + 1) / (Hp.nHelp + 1), y1 = sh * (k + 2) / (Hp.nHelp + 1);
     // LDS: ctl | T (NOTDEF or trivial) | H | own windows | growth queues
     lds_ctl* ctl = (lds_ctl*)lds_u;
@@ -969,7 +969,9 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
     }
     const LineOctDev& od = octs[o];
     const int sw = od.sw, sh = od.sh, wpr = (sw + 31) >> 5;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // the wave index read uniformly: the role (walker / grower) and this wave's
+    // LDS partitions and spill areas stay scalar
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     // LDS carve-up: ctl | dispatch log | C | T | H | own windows | growth queues | slot pool
     lds_ctl* ctl = (lds_ctl*)lds_u;
     lds_i32* dlog = (lds_i32*)(lds_u + sizeof(MwCtl) / 4);

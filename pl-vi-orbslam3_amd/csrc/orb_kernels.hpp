@@ -93,7 +93,7 @@ __global__ __launch_bounds__(64 * (kPyrFrames + 1)) __attribute__((amdgpu_waves_
     __shared__ int s_w[kOrbMaxLevels], s_h[kOrbMaxLevels], s_roff[kOrbMaxLevels], s_xoff[kOrbMaxLevels];
     __shared__ double s_sy[kOrbMaxLevels];
     __shared__ int s_cnt[2 * kPyrFrames];  // per frame: rows loaded, rows consumed
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // uniform: scalar role / frame
     const int f0 = blockIdx.x * kPyrFrames;
     const int nfw = min(kPyrFrames, nf - f0);  // frames of this workgroup
     lds_u32* ltab = (lds_u32*)lds_pyr_g;     // column table first (xtab_n words)
