@@ -54,7 +54,7 @@ __global__ __launch_bounds__(256) void search_by_bow_kernel(
     int* s_mk = lds;                                      // [f_cap] matched KF index or -1
     int2* s_pairs = reinterpret_cast<int2*>(lds + f_cap);  // [node_cap] shared (KF node, F node)
     __shared__ int s_hist[kBowHisto], s_npairs, s_count, s_keep[3];
-    const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x, wv = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const int nF = f_n[p];
     // F.Nleft (-1: one camera, every keypoint is "left")
     const int nLeft = (f_nleft && f_nleft[p] >= 0) ? f_nleft[p] : 0x7fffffff;

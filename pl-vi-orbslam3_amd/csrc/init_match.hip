@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void search_init_kernel(
     const uint8_t* __restrict__ desc2_all, const int* __restrict__ n2_all, int cap2, const int* __restrict__ cell_off_all,
     const int* __restrict__ cell_idx_all, int* __restrict__ m12_all, int* __restrict__ nmatch_all) {
     extern __shared__ __align__(16) unsigned char lds[];
-    const int pr = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int pr = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int n1 = min(n1_all[pr], cap1), n2 = min(n2_all[pr], cap2);
     InitLds s;
     {

@@ -57,7 +57,7 @@ __device__ __forceinline__ int hamming32(const uint4* a, const uint4* b) {
 
 // Exclusive scan of s[0..n) in place over the 256-thread block; returns the total.
 __device__ int block_scan_excl(int* s, int n, int* s_tmp) {
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
     const int per = (n + kStThreads - 1) / kStThreads, b0 = min(n, t * per), b1 = min(n, b0 + per);
     int local = 0;
     for (int i = b0; i < b1; ++i) local += s[i];
@@ -96,7 +96,7 @@ __global__ __launch_bounds__(kStThreads) void stereo_orb_kernel(
     extern __shared__ __align__(16) int lds_s[];
     __shared__ int s_tmp[kStThreads / 64], s_njob, s_nacc, s_fail, s_hist[256], s_sel[2];
     __shared__ int s_part[kStThreads / 64][121], s_dist[kStThreads / 64][11];
-    const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int f = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);
     const int nL = nLs[f], nR = nRs[f];
     const int nRows = lv.h[0];
     int* s_row = lds_s;                                        // nRows + 1 (counts -> offsets)

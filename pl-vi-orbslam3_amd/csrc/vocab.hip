@@ -53,7 +53,7 @@ __device__ __forceinline__ int popc256(const uint4& a0, const uint4& a1, const u
 
 // Exclusive scan of one int per thread over the 256-thread block.
 __device__ int block_excl_scan(int v, int* s_tmp, int* total) {
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     int x = v;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
