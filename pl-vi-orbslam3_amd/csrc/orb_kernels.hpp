@@ -1543,6 +1543,11 @@ constexpr int kAngR = 15, kAngRows = 2 * kAngR + 1, kAngPitch = 32;
 #ifndef PLVI_DESC_SPLIT_WPE
 #define PLVI_DESC_SPLIT_WPE 8
 #endif
+#ifndef PLVI_DESC_UNROLL
+#define PLVI_DESC_UNROLL 4  // rBRIEF loop unroll (1 or 2: 78 instead of 92 VGPRs)
+#endif
+#define PLVI_PRAGMA(x) _Pragma(#x)
+#define PLVI_UNROLL(n) PLVI_PRAGMA(unroll n)
 template <int PART>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PART ? PLVI_DESC_SPLIT_WPE : PLVI_DESC_WPE))) void orb_describe_kernel(const OrbLevelDev* __restrict__ lvs, int L,
                                                            const uint8_t* __restrict__ pyr,
@@ -1668,7 +1673,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PART ? PLVI
         float a, b;
         plvi_sincosf_pos(ang, &b, &a);
         uint64_t* out = reinterpret_cast<uint64_t*>(lvdesc + ((size_t)f * kpCapFrame + slot) * 32);
-#pragma unroll
+        PLVI_UNROLL(PLVI_DESC_UNROLL)
         for (int k = 0; k < 4; ++k) {
             const float px0 = (float)(int8_t)(pat[k] & 0xffu), py0 = (float)(int8_t)((pat[k] >> 8) & 0xffu);
             const float px1 = (float)(int8_t)((pat[k] >> 16) & 0xffu), py1 = (float)(int8_t)(pat[k] >> 24);
