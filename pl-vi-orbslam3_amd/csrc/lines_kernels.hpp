@@ -354,6 +354,9 @@ __device__ __forceinline__ void bits_load_rows(const GrowCtx& g, int r0, int r1,
 #ifndef PLVI_GROW_SETPRIO
 #define PLVI_GROW_SETPRIO 3  // wave priority of the region-growing waves (s_setprio)
 #endif
+#ifndef PLVI_GROW_OCT1_PRIO
+#define PLVI_GROW_OCT1_PRIO PLVI_GROW_SETPRIO  // priority of the octave >= 1 growth waves
+#endif
 
 // waves per SIMD the region-growing kernel is compiled for: 8 caps it at 64
 // VGPRs, so its 6 resident waves per SIMD (a 3072-frame batch) leave room for
@@ -412,6 +415,9 @@ __global__ __launch_bounds__(64 * kGrowWaves, PLVI_GROW_WPE) void lsd_grow_kerne
     // consecutive frames per workgroup (spreading frames over the workgroups
     // by a stride permutation was slower: 35.3 vs 33.2 ms per 3072 frames)
     const int o = oBase + task / nf, f = task - (o - oBase) * nf;
+    // the octave-0 waves carry the launch (4x the pixels): PLVI_GROW_OCT1_PRIO
+    // lowers the other octaves' priority below theirs
+    if (PLVI_GROW_OCT1_PRIO != PLVI_GROW_SETPRIO && o > 0) __builtin_amdgcn_s_setprio(PLVI_GROW_OCT1_PRIO);
     // this wave's LDS partition, addressed as LDS (32-bit) from the start
     lds_u32* lds_w = (lds_u32*)lds_all + wv * (ldsWave >> 2);
     const LineOctDev& od = octs[o];
