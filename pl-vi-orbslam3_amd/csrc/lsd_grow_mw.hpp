@@ -78,6 +78,14 @@ constexpr int kMwLate = PLVI_MW_LATE;  // late-log entries (0 = off, the default
                                        // seeds fall 119 -> 43 but dropped regions rise 338 -> 1036 and the
                                        // kernel takes 10.9 instead of 7.1 ms per frame; <= 64)
 constexpr int kMwLateWords = 64;       // bitmap words ahead of the walk a grower scans for them
+// PLVI_MW_ORPHAN (with PLVI_MW_LATE > 0): a region that will not be committed
+// as grown (invalid at the walk, dropped, regrown by revalidation) gives up
+// its H claims outside C, and the second-chance dispatch takes only such
+// orphans -- pixels between the walk and the cursor that are neither
+// committed, trivial nor claimed -- instead of every claimed pixel
+#ifndef PLVI_MW_ORPHAN
+#define PLVI_MW_ORPHAN 0
+#endif
 
 // slot states; COMMITTED: validated and committed, a grower still copies
 // its points out (regions of more than kMwSP points); WALKING: the walker
@@ -93,7 +101,7 @@ struct MwSlot {
     int ovf;    // queue overflow: the walker regrows it
     int out;    // COMMITTED: offset of its points in the task's point list
     int chk;    // ctl->ncommit when the region was last grown / found valid
-    int pad;
+    int dead;   // PLVI_MW_ORPHAN: FREE after a region that was not committed (its claims not yet released)
 };
 constexpr int kMwSlotBytes = sizeof(MwSlot) + 4 * kMwSP;
 // control block (LDS)
@@ -393,6 +401,18 @@ __device__ __forceinline__ void mw_own_clear(const MwEnv& E, int sy, const MwQue
     mw_wave_sync();
 }
 
+// Release the H claims of a region that will not be committed as grown
+// (points outside C only: a committed pixel stays claimed).
+__device__ __forceinline__ void mw_unclaim(const MwEnv& E, const MwQueue& Q, int n, int lane) {
+    for (int j = lane; j < n; j += 64) {
+        const unsigned v = mw_qget(Q, j);
+        const int x = (int)(v & 0xffffu), y = (int)(v >> 16);
+        if (!mw_bit(E.C, E.wpr, x, y))
+            __hip_atomic_fetch_and(&E.H[y * E.wpr + (x >> 5)], ~(1u << (x & 31)), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
 // A slot's points: the first kMwSP in LDS after its header, the rest in
 // global memory.
 __device__ __forceinline__ MwQueue mw_slot_queue(lds_u8* pool, unsigned* slotspill, int si) {
@@ -539,6 +559,7 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
                 done = true;
             } else {
                 if (STATS && lane == 0) mw_stat(ctl, 2, 1);
+                if (PLVI_MW_ORPHAN && S->ovf == 0) mw_unclaim(E, Q, n, lane);  // before the exact regrowth claims its own
                 mw_wave_sync();
                 if (lane == 0) mw_lds_store(&S->state, kMwFree);
             }
@@ -640,7 +661,11 @@ __device__ __forceinline__ int mw_dispatch(const MwEnv& E, lds_u8* pool, int nsl
     const int q = w * 32 + (__ffs((int)m) - 1);
     if (lane == 0) {
         lds_slot* S = mw_slot(pool, slot);
-        if (STATS && mw_peek(&S->state) == kMwDone) mw_stat(ctl, 1, 1);  // a passed region, dropped
+        const int st0 = mw_peek(&S->state);
+        if (STATS && st0 == kMwDone) mw_stat(ctl, 1, 1);  // a passed region, dropped
+        // a dropped region (or one left dead by revalidation) gives up its claims
+        // when the slot is reused (by the grower that took it, outside the lock)
+        S->dead = PLVI_MW_ORPHAN && (st0 == kMwDone || S->dead) && S->ovf == 0 ? 1 : 0;
         S->seed = q;
         S->ovf = 0;
         S->chk = mw_peek(&ctl->ncommit);
@@ -683,11 +708,19 @@ __device__ __forceinline__ int mw_second_chance(const MwEnv& E, lds_u8* pool, in
     }
     if (slot < 0) return -1;
     const int w0 = head >> 5;
+    const int cur = ctl->cursor;  // under dlock
     for (int wb = w0; wb < min(nwords, w0 + kMwLateWords); wb += 64) {
         const int w = wb + lane;
         unsigned m = 0;
         if (w < nwords && w < w0 + kMwLateWords) {
-            m = ~mw_peek(E.C + w) & ~E.T[w] & mw_peek(E.H + w);
+            if (PLVI_MW_ORPHAN) {
+                // orphans: passed by the cursor, now neither committed, trivial nor claimed
+                m = ~mw_peek(E.C + w) & ~E.T[w] & ~mw_peek(E.H + w);
+                if (w > (cur >> 5)) m = 0;
+                else if (w == (cur >> 5)) m &= (1u << (cur & 31)) - 1u;
+            } else {
+                m = ~mw_peek(E.C + w) & ~E.T[w] & mw_peek(E.H + w);
+            }
             if (w == w0) m &= ~0u << (head & 31);
         }
         unsigned long long has = __ballot(m != 0u);
@@ -1044,6 +1077,9 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
     for (int k = threadIdx.x; k < nslots; k += NW * 64) {
         mw_slot(pool, k)->state = kMwFree;
         mw_slot(pool, k)->seed = -1;
+        mw_slot(pool, k)->n = 0;
+        mw_slot(pool, k)->ovf = 0;
+        mw_slot(pool, k)->dead = 0;
     }
     if (threadIdx.x == 0) {
         ctl->lock = ctl->dlock = ctl->head = ctl->cursor = ctl->finished = 0;
@@ -1137,12 +1173,14 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
                     int nst = kMwDone;
                     if (mw_bit(E.C, E.wpr, sx, sy)) {
                         nst = kMwFree;  // the seed itself was taken: the walk never visits it
+                        if (lane == 0) S->dead = PLVI_MW_ORPHAN && S->ovf == 0 ? 1 : 0;
                     } else if (__ballot(bad) == 0ull) {
                         if (lane == 0) S->chk = nc0;
                     } else {
                         int n = 0;
                         float deg = 0.f;
                         bool spilled = false;
+                        if (PLVI_MW_ORPHAN && S->ovf == 0) mw_unclaim(E, Q, n0, lane);
                         const unsigned long long ts0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
                         int rc = mw_grow<true, STATS>(E, sx, sy, GQ, n, deg, spilled, lane);
                         mw_own_clear(E, sy, GQ, n, spilled, lane);
@@ -1177,6 +1215,14 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
             if (q < 0) {
                 __builtin_amdgcn_s_sleep(2);
                 continue;
+            }
+            if (PLVI_MW_ORPHAN) {
+                lds_slot* S0 = mw_slot(pool, si);
+                if (__builtin_amdgcn_readfirstlane(S0->dead)) {
+                    mw_unclaim(E, mw_slot_queue(pool, sspill, si), S0->n, lane);
+                    mw_wave_sync();
+                    if (lane == 0) S0->dead = 0;
+                }
             }
             // a region a helper already grew for this seed
             if (hcur && q >= helpStart && mw_import(E, Hp, t, pool, sspill, si, q, lane)) {
