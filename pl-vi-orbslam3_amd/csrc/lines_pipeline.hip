@@ -566,12 +566,13 @@ struct LinePipeline {
             auto mwK = mwStats ? lsd_grow_mw_kernel<kMwWaves, true> : lsd_grow_mw_kernel<kMwWaves, false>;
             // helpers for the launches that grow octave 0: as many per task as
             // the CUs left by every octave's tasks allow (one workgroup per CU)
-            const int nT = oCount * nf, nTp = (nT + 7) & ~7;
+            const int nT = oCount * nf, nT8 = (nT + 7) & ~7;
             int K = 0;
             if (mwHelpMax > 0 && oBase == 0) {
                 K = std::min(mwHelpMax, (mwCUs - nf * nOct) / nT);
-                K = std::max(0, std::min(K, mwHelpWgs / nTp));
+                K = std::max(0, std::min(K, mwHelpWgs / nT8));
             }
+            const int nTp = K > 0 ? nT8 : nT;  // sections padded to 8 blocks only with helpers
             MwHelp Hp{mwHMap.as<unsigned>(), mwHMapTask, mwHRec.as<MwHelpRec>(), mwHPts.as<unsigned>(),
                       mwHCur.as<unsigned>(), mwHOwn.as<unsigned>(), mwOwnTask, mwHGq.as<unsigned>(), K, nTp,
                       (int)mwHMapTask, ++mwEpoch};
