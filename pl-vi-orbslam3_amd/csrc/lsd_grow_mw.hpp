@@ -64,6 +64,13 @@ constexpr int kMwLog = 256;         // dispatch log entries (seed order)
 #ifndef PLVI_MW_GROWER_PRIO
 #define PLVI_MW_GROWER_PRIO 1
 #endif
+// a grower reads the walk position (relaxed) at the top of each block and
+// tests it once the block's loads are issued, instead of an acquire load
+// that stalls the block first: region growing 6.40 -> 6.27 ms (one frame),
+// 7.97 -> 7.86 ms (64 frames), profiles/r04/mw_helpers_ab.txt
+#ifndef PLVI_MW_LATECHK
+#define PLVI_MW_LATECHK 1
+#endif
 #ifndef PLVI_MW_BOOST
 #define PLVI_MW_BOOST 1  // a grower whose seed the walk has reached runs at priority 3
 #endif
@@ -267,7 +274,10 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
     int reg_size = 1;
     const int cap = Q.lcap + Q.gcap;
     for (int i = 0; i < reg_size;) {
-        if (SPEC) {
+        // PLVI_MW_LATECHK: the walk position is read at the top of the block
+        // (relaxed: a hint) and tested once the block's loads are in flight
+        const int hd0 = SPEC && PLVI_MW_LATECHK ? mw_peek(&E.ctl->head) : 0;
+        if (SPEC && !PLVI_MW_LATECHK) {
             const int hd = mw_lds_load(&E.ctl->head);
             if (hd > seedb) {
                 n_out = reg_size;
@@ -307,6 +317,17 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
             const unsigned q2 = (unsigned)readlane_i((int)pv, 9 * p2);
             const int ddx = nx - (int)(q2 & 0xffffu) + 1, ddy = ny - (int)(q2 >> 16) + 1;
             if (p2 < bp && ddx >= 0 && ddx <= 2 && ddy >= 0 && ddy <= 2) dup |= 1ull << (9 * p2 + ddy * 3 + ddx);
+        }
+        if (SPEC && PLVI_MW_LATECHK) {
+            if (hd0 > seedb) {
+                n_out = reg_size;
+                deg_out = reg_deg;
+                return 1;
+            }
+            if (PLVI_MW_BOOST) {
+                if (hd0 == seedb) __builtin_amdgcn_s_setprio(3);
+                else __builtin_amdgcn_s_setprio(PLVI_MW_GROWER_PRIO);
+            }
         }
         // own marks and the committed bitmap, read once per block (within the
         // block a lane's pixel only changes through an earlier lane's commit
