@@ -68,6 +68,9 @@ constexpr int kMwLog = 256;         // dispatch log entries (seed order)
 // tests it once the block's loads are issued, instead of an acquire load
 // that stalls the block first: region growing 6.40 -> 6.27 ms (one frame),
 // 7.97 -> 7.86 ms (64 frames), profiles/r04/mw_helpers_ab.txt
+#ifndef PLVI_MW_WALKFAST
+#define PLVI_MW_WALKFAST 0
+#endif
 #ifndef PLVI_MW_LATECHK
 #define PLVI_MW_LATECHK 1
 #endif
@@ -459,6 +462,9 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
         // next unresolved pixel >= head: first zero bit of C
         int w = head >> 5;
         if (w >= nwords) break;
+        // PLVI_MW_WALKFAST: the dispatch-log count is read (relaxed) beside the
+        // bitmap words and acquired by a fence once the seed is known
+        const int dnr = PLVI_MW_WALKFAST ? mw_peek(&ctl->dlog_n) : 0;
         unsigned cw = mw_peek(E.C + w), tw = E.T[w];  // T is static after the set-up
         unsigned m = ~cw & (~0u << (head & 31));
         if (!m) {
@@ -493,7 +499,13 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
         const int q = w * 32 + (__ffs((int)nt) - 1);
         head = q;
         // the speculative region of seed q, if one was dispatched
-        const int dn = mw_lds_load(&ctl->dlog_n);
+        int dn;
+        if (PLVI_MW_WALKFAST) {
+            dn = dnr;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // pairs with the dispatcher's release of dlog_n
+        } else {
+            dn = mw_lds_load(&ctl->dlog_n);
+        }
         while (wp < dn && dlog[2 * (wp & (kMwLog - 1))] < q) ++wp;
         int si = -1;
         bool fromLog = false;
@@ -621,8 +633,15 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
         }
         head = q + 1;
         if (lane == 0) {
-            mw_lds_store(&ctl->wptr, wp);  // frees log entries for the dispatchers as the walk goes
-            mw_lds_store(&ctl->head, head);
+            if (PLVI_MW_WALKFAST) {
+                // one release for both (the slot / log reads above are done before either is seen)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __hip_atomic_store(&ctl->wptr, wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(&ctl->head, head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+                mw_lds_store(&ctl->wptr, wp);  // frees log entries for the dispatchers as the walk goes
+                mw_lds_store(&ctl->head, head);
+            }
         }
     }
     if (lane == 0) {
