@@ -173,6 +173,11 @@ int plvi_orb_profile_read(plvi_orb_extractor* h, float* stage_ms, int* runs);
  * summed milliseconds and the launch count. */
 int plvi_orb_kernel_timing(plvi_orb_extractor* h, int enable);
 int plvi_orb_kernel_timing_read(plvi_orb_extractor* h, float* total_ms, int* launches);
+/* Diagnostic: cap every level's octree node capacity at `cap` (<= 0 restores
+ * the planned capacities).  A level whose DistributeOctTree needs more nodes
+ * flags its frame (plvi_orb_errors bit 1) and yields no keypoints; the test
+ * hook for that path (the candidate plane it must leave zero). */
+int plvi_orb_debug_node_cap(plvi_orb_extractor* h, int cap);
 
 /* ------------------------------------------------------------------ Lines
  * Replaces ORB_SLAM3::Lineextractor (include/LineExtractor.h:49-93,

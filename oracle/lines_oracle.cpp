@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "cvprim.h"
+#include "ref_fma.h"
 
 namespace oracle {
 
@@ -157,7 +158,7 @@ struct LSD {
                 double DA = scaled.px[addr + img_width + 1] - scaled.px[addr];
                 double BC = scaled.px[addr + 1] - scaled.px[addr + img_width];
                 double gx = DA + BC, gy = DA - BC;
-                double norm = std::sqrt((gx * gx + gy * gy) / 4);
+                double norm = std::sqrt(ref_fma(gx, gx, gy * gy) / 4);  // fused in lsd.cpp.o
                 modgrad.px[addr] = norm;
                 if (norm <= threshold) angles.px[addr] = NOTDEF;
                 else angles.px[addr] = fast_atan2((float)gx, (float)-gy) * DEG_TO_RADS;
@@ -210,11 +211,12 @@ struct LSD {
         for (int i = 0; i < reg_size; ++i) {
             const double regx = reg[i].x, regy = reg[i].y, weight = reg[i].modgrad;
             double dx = regx - x, dy = regy - y;
-            Ixx += dy * dy * weight;
-            Iyy += dx * dx * weight;
-            Ixy -= dx * dy * weight;
+            // lsd.cpp.o get_theta: three fused accumulations + the root's
+            Ixx = ref_fma(dy * dy, weight, Ixx);
+            Iyy = ref_fma(dx * dx, weight, Iyy);
+            Ixy = ref_fma(-(dx * dy), weight, Ixy);
         }
-        double lambda = 0.5 * (Ixx + Iyy - std::sqrt((Ixx - Iyy) * (Ixx - Iyy) + 4.0 * Ixy * Ixy));
+        double lambda = 0.5 * (Ixx + Iyy - std::sqrt(ref_fma(Ixx - Iyy, Ixx - Iyy, 4.0 * Ixy * Ixy)));
         double theta = (std::fabs(Ixx) > std::fabs(Iyy)) ? (double)fast_atan2((float)(lambda - Ixx), (float)Ixy)
                                                          : (double)fast_atan2((float)Ixy, (float)(lambda - Iyy));
         theta *= DEG_TO_RADS;
@@ -226,8 +228,8 @@ struct LSD {
         double x = 0, y = 0, sum = 0;
         for (int i = 0; i < reg_size; ++i) {
             const double weight = reg[i].modgrad;
-            x += (double)reg[i].x * weight;
-            y += (double)reg[i].y * weight;
+            x = ref_fma((double)reg[i].x, weight, x);  // fused in lsd.cpp.o region2rect
+            y = ref_fma((double)reg[i].y, weight, y);
             sum += weight;
         }
         x /= sum;
@@ -237,17 +239,17 @@ struct LSD {
         double l_min = 0, l_max = 0, w_min = 0, w_max = 0;
         for (int i = 0; i < reg_size; ++i) {
             double regdx = (double)reg[i].x - x, regdy = (double)reg[i].y - y;
-            double l = regdx * dx + regdy * dy;
-            double w = -regdx * dy + regdy * dx;
+            double l = ref_fma(regdx, dx, regdy * dy);
+            double w = ref_fma(-regdx, dy, regdy * dx);
             if (l > l_max) l_max = l;
             else if (l < l_min) l_min = l;
             if (w > w_max) w_max = w;
             else if (w < w_min) w_min = w;
         }
-        r[0] = x + l_min * dx;
-        r[1] = y + l_min * dy;
-        r[2] = x + l_max * dx;
-        r[3] = y + l_max * dy;
+        r[0] = ref_fma(l_min, dx, x);  // one vfmadd132pd over the four
+        r[1] = ref_fma(l_min, dy, y);
+        r[2] = ref_fma(l_max, dx, x);
+        r[3] = ref_fma(l_max, dy, y);
     }
 
     // LineSegmentDetectorImpl::detect + flsd (:412-534), refine = LSD_REFINE_NONE.
@@ -270,7 +272,11 @@ struct LSD {
             scaled = image;
         }
         ll_angle(rho);
-        const double LOG_NT = 5 * (std::log10((double)img_width) + std::log10((double)img_height)) / 2 + std::log10(11.0);
+        // lsd.cpp.o: fma(5*(lw + lh), 0.5, log10(11.0) folded by GCC); the
+        // literal below is that .rodata constant (glibc's log10(11.0) is one
+        // ulp lower)
+        const double LOG_NT = ref_fma(5 * (std::log10((double)img_width) + std::log10((double)img_height)), 0.5,
+                                      0x1.0a98b6050c56fp+0);
         const int min_reg_size = (int)(-LOG_NT / std::log10(p));
         used.assign((size_t)img_width * img_height, 0);
         reg.assign((size_t)img_width * img_height, RegionPoint{0, 0, 0, 0});
@@ -607,8 +613,8 @@ static void line_extract(const ImageU8& img, const LineParams& P, LinesResult& R
     R.lineFns.clear();
     for (auto& k : kls) {
         double sx = k.startPointX, sy = k.startPointY, ex = k.endPointX, ey = k.endPointY;
-        double a = sy * 1.0 - 1.0 * ey, b = 1.0 * ex - sx * 1.0, c = sx * ey - sy * ex;
-        double n = std::sqrt(a * a + b * b);
+        double a = sy * 1.0 - 1.0 * ey, b = 1.0 * ex - sx * 1.0, c = ref_fma(sx, ey, -(sy * ex));
+        double n = std::sqrt(ref_fma(a, a, b * b));  // both fused in LineExtractor.cc.o
         R.lineFns.push_back(a / n);
         R.lineFns.push_back(b / n);
         R.lineFns.push_back(c / n);

@@ -15,6 +15,7 @@
 #include <cstdint>
 #include <cstring>
 #include <vector>
+#include "ref_fma.h"
 
 static int descriptor_distance(const uint8_t* a, const uint8_t* b, int shift) {
     int dist = 0;
@@ -298,24 +299,55 @@ static void insert_range_gcc10(std::unordered_set<int>& indices, const std::list
     indices.merge(src);
 }
 
+// GridStructure(rows, cols) filled from CSR cells (x * rows + y) in list order
+using GridLists = std::vector<std::vector<std::list<int>>>;
+static GridLists grid_lists(int cols, int rows, const int* cell_off, const int* cell_idx) {
+    GridLists grid(cols, std::vector<std::list<int>>(rows));
+    for (int x = 0; x < cols; ++x)
+        for (int y = 0; y < rows; ++y)
+            for (int k = cell_off[x * rows + y]; k < cell_off[x * rows + y + 1]; ++k) grid[x][y].push_back(cell_idx[k]);
+    return grid;
+}
+
+// GridStructure::get (src/gridStructure.cpp:67-78)
+static void grid_get(const GridLists& grid, int cols, int rows, int x, int y, int w0, int w1, int h0, int h1,
+                     int range_hint, std::unordered_set<int>& indices) {
+    int min_x = std::max(0, x - w0);
+    int max_x = std::min(cols, x + w1 + 1);
+    int min_y = std::max(0, y - h0);
+    int max_y = std::min(rows, y + h1 + 1);
+    for (int x_ = min_x; x_ < max_x; ++x_)
+        for (int y_ = min_y; y_ < max_y; ++y_) {
+            if (range_hint) insert_range_gcc10(indices, grid[x_][y_]);
+            else indices.insert(grid[x_][y_].begin(), grid[x_][y_].end());
+        }
+}
+
+// The candidate set of one matchGrid line (get at sp, then at ep, into one
+// set) in iteration order: the restatement tests/test_ref_grid.py compares
+// with the reference's own gridStructure.cpp (oracle/_ref).
+extern "C" int oracle_grid_candidates(int cols, int rows, const int* cell_off, const int* cell_idx, int spx, int spy,
+                                      int epx, int epy, int w0, int w1, int h0, int h1, int range_hint, int* out,
+                                      int cap) {
+    const GridLists grid = grid_lists(cols, rows, cell_off, cell_idx);
+    std::unordered_set<int> c;
+    grid_get(grid, cols, rows, spx, spy, w0, w1, h0, h1, range_hint, c);
+    grid_get(grid, cols, rows, epx, epy, w0, w1, h0, h1, range_hint, c);
+    int n = 0;
+    for (int v : c) {
+        if (n < cap) out[n] = v;
+        ++n;
+    }
+    return n;
+}
+
 extern "C" int oracle_match_grid2(const int* lines1, const uint8_t* desc1, int n1, int cols, int rows,
                                   const int* cell_off, const int* cell_idx, const uint8_t* desc2,
                                   const double* directions2, int n2, int w0, int w1, int h0, int h1,
                                   int range_hint, int* matches_12) {
-    std::vector<std::vector<std::list<int>>> grid(cols, std::vector<std::list<int>>(rows));
-    for (int x = 0; x < cols; ++x)
-        for (int y = 0; y < rows; ++y)
-            for (int k = cell_off[x * rows + y]; k < cell_off[x * rows + y + 1]; ++k) grid[x][y].push_back(cell_idx[k]);
+    const GridLists grid = grid_lists(cols, rows, cell_off, cell_idx);
     auto get = [&](int x, int y, std::unordered_set<int>& indices) {
-        int min_x = std::max(0, x - w0);
-        int max_x = std::min(cols, x + w1 + 1);
-        int min_y = std::max(0, y - h0);
-        int max_y = std::min(rows, y + h1 + 1);
-        for (int x_ = min_x; x_ < max_x; ++x_)
-            for (int y_ = min_y; y_ < max_y; ++y_) {
-                if (range_hint) insert_range_gcc10(indices, grid[x_][y_]);
-                else indices.insert(grid[x_][y_].begin(), grid[x_][y_].end());
-            }
+        grid_get(grid, cols, rows, x, y, w0, w1, h0, h1, range_hint, indices);
     };
     const double lineSimTh = 0.75, minRatio12L = 0.9;
     int matches = 0;
@@ -325,7 +357,7 @@ extern "C" int oracle_match_grid2(const int* lines1, const uint8_t* desc1, int n
         int best_d = std::numeric_limits<int>::max(), best_d2 = std::numeric_limits<int>::max(), best_idx = -1;
         const int spx = lines1[4 * i1], spy = lines1[4 * i1 + 1], epx = lines1[4 * i1 + 2], epy = lines1[4 * i1 + 3];
         double vx = (double)(epx - spx), vy = (double)(epy - spy);
-        const double magnitude = std::sqrt(vx * vx + vy * vy);
+        const double magnitude = std::sqrt(ref_fma(vx, vx, vy * vy));  // normalize / dot: fused in LineMatcher.cpp.o
         vx /= magnitude;
         vy /= magnitude;
         std::unordered_set<int> candidates;
@@ -334,7 +366,7 @@ extern "C" int oracle_match_grid2(const int* lines1, const uint8_t* desc1, int n
         if (candidates.empty()) continue;
         for (const int& i2 : candidates) {
             if (i2 < 0 || i2 >= n2) continue;
-            if (std::abs(vx * directions2[2 * i2] + vy * directions2[2 * i2 + 1]) < lineSimTh) continue;
+            if (std::abs(ref_fma(vx, directions2[2 * i2], vy * directions2[2 * i2 + 1])) < lineSimTh) continue;
             const int d = descriptor_distance(desc1 + (size_t)i1 * 32, desc2 + (size_t)i2 * 32, 24);
             if (d < distances[i2]) {
                 distances[i2] = d;

@@ -17,6 +17,7 @@
 
 #include "cvprim.h"
 #include "oracle_api.h"
+#include "ref_fma.h"
 
 namespace oracle {
 
@@ -286,8 +287,9 @@ static void orb_descriptor(const KP& kpt, const ImageU8& img, uint8_t* desc) {
     const int cx = cv_round(kpt.x), cy = cv_round(kpt.y);
     auto get = [&](int idx) -> int {
         int x = kPattern[2 * idx], y = kPattern[2 * idx + 1];
-        int r = cv_round((float)x * b + (float)y * a);
-        int c = cv_round((float)x * a - (float)y * b);
+        // GET_VALUE (:116-118): the left product fused (ORBextractor.cc.o)
+        int r = cv_round(ref_fmaf((float)x, b, (float)y * a));
+        int c = cv_round(ref_fmaf((float)x, a, -((float)y * b)));
         return img.at(cx + c, cy + r);
     };
     for (int i = 0; i < 32; ++i) {

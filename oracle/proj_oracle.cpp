@@ -21,6 +21,8 @@
 #include <cstring>
 #include <vector>
 
+#include "ref_fma.h"
+
 namespace {
 
 constexpr int kCols = 64, kRows = 48;  // FRAME_GRID_COLS / FRAME_GRID_ROWS (include/Frame.h:47-48)
@@ -197,7 +199,7 @@ extern "C" int oracle_search_by_projection(
         for (size_t i2 : vIndices2) {
             if (blocked[i2]) continue;
             if (curight && curight[i2] > 0) {
-                const float ur = u - mbf * invzc;
+                const float ur = ref_fmaf(-mbf, invzc, u);  // fused in ORBmatcher.cc.o
                 const float er = std::fabs(ur - curight[i2]);
                 if (er > radius) continue;
             }
@@ -246,7 +248,9 @@ static void project_cam(const float* kb8, float fx, float fy, float cxp, float c
         v = fy * y / z + cyp;
         return;
     }
-    const float x2_plus_y2 = x * x + y * y;
+    // the seven multiply-adds KannalaBrandt8.cpp.o fuses: x*x + y*y, the four
+    // r terms, u and v
+    const float x2_plus_y2 = ref_fmaf(x, x, y * y);
     const float theta = atan2f(sqrtf(x2_plus_y2), z);
     const float psi = atan2f(y, x);
     const float theta2 = theta * theta;
@@ -254,9 +258,10 @@ static void project_cam(const float* kb8, float fx, float fy, float cxp, float c
     const float theta5 = theta3 * theta2;
     const float theta7 = theta5 * theta2;
     const float theta9 = theta7 * theta2;
-    const float r = theta + kb8[0] * theta3 + kb8[1] * theta5 + kb8[2] * theta7 + kb8[3] * theta9;
-    u = fx * r * std::cos(psi) + cxp;
-    v = fy * r * std::sin(psi) + cyp;
+    const float r =
+        ref_fmaf(kb8[3], theta9, ref_fmaf(kb8[2], theta7, ref_fmaf(kb8[1], theta5, ref_fmaf(kb8[0], theta3, theta))));
+    u = ref_fmaf(fx * r, std::cos(psi), cxp);
+    v = ref_fmaf(fy * r, std::sin(psi), cyp);
 }
 
 // SearchByProjection(CurrentFrame, LastFrame, th, bMono) with a two-camera

@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "oracle_api.h"
+#include "ref_fma.h"
 
 extern "C" int oracle_match_grid2(const int* lines1, const uint8_t* desc1, int n1, int cols, int rows,
                                   const int* cell_off, const int* cell_idx, const uint8_t* desc2,
@@ -103,6 +104,20 @@ double overlap_stereo(double spl_obs, double epl_obs, double spl_proj, double ep
 
 }  // namespace
 
+// getLineCoords (src/gridStructure.cpp:32-40): the pixels of LineIterator in
+// order, as (x, y) pairs; tests/test_ref_grid.py compares it with the
+// reference's own LineIterator.cpp (oracle/_ref).
+extern "C" int oracle_line_coords(double x1, double y1, double x2, double y2, int* out_xy, int cap) {
+    std::list<std::pair<int, int>> l;
+    line_coords(x1, y1, x2, y2, l);
+    int n = 0;
+    for (auto& p : l) {
+        if (n < cap) { out_xy[2 * n] = p.first; out_xy[2 * n + 1] = p.second; }
+        ++n;
+    }
+    return n;
+}
+
 // Frame::ComputeStereoMatches (src/Frame.cc:1228-1406).  kps*: mvKeys /
 // mvKeysRight (cv::KeyPoint layout), desc*: 32 B rows; pyramids: level l of
 // each side at pyr + lvl_off[l], lvl_w[l] x lvl_h[l] (mvImagePyramid of the
@@ -120,9 +135,9 @@ extern "C" int oracle_stereo_match(const plvi_keypoint* kpsL, const uint8_t* des
     for (int iR = 0; iR < nR; iR++) {
         const plvi_keypoint& kp = kpsR[iR];
         const float& kpY = kp.y;
-        const float r = 2.0f * scale[kp.octave];
-        const int maxr = std::ceil(kpY + r);
-        const int minr = std::floor(kpY - r);
+        // kpY + r / kpY - r with r = 2*scale: fused in Frame.cc.o
+        const int maxr = std::ceil(ref_fmaf(2.0f, scale[kp.octave], kpY));
+        const int minr = std::floor(ref_fmaf(-2.0f, scale[kp.octave], kpY));
         if (minr < 0 || maxr >= nRows) return -1;  // vRowIndices[yi] out of range (UB in the reference)
         for (int yi = minr; yi <= maxr; yi++) vRowIndices[yi].push_back(iR);
     }
@@ -199,7 +214,7 @@ extern "C" int oracle_stereo_match(const plvi_keypoint* kpsL, const uint8_t* des
             const float dist1 = vDists[L + bestincR - 1];
             const float dist2 = vDists[L + bestincR];
             const float dist3 = vDists[L + bestincR + 1];
-            const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+            const float deltaR = (dist1 - dist3) / (2.0f * ref_fmaf(-2.0f, dist2, dist1 + dist3));
             if (deltaR < -1 || deltaR > 1) continue;
             float bestuR = scale[kpL.octave] * ((float)scaleduR0 + (float)bestincR + deltaR);
             float disparity = (uL - bestuR);
@@ -276,7 +291,7 @@ extern "C" int oracle_stereo_lines(const float* klL, const uint8_t* descL, int n
     std::list<std::pair<int, int>> lc;
     for (int idx = 0; idx < nR; ++idx) {
         double vx = (R[idx].ex - R[idx].sx) * inv_width, vy = (R[idx].ey - R[idx].sy) * inv_height;
-        const double magnitude = std::sqrt(vx * vx + vy * vy);
+        const double magnitude = std::sqrt(ref_fma(vx, vx, vy * vy));  // fused in Frame.cc.o
         vx /= magnitude;
         vy /= magnitude;
         directions[2 * idx] = vx;
@@ -303,9 +318,9 @@ extern "C" int oracle_stereo_lines(const float* klL, const uint8_t* descL, int n
         double spr0 = R[i2].sx, spr1 = R[i2].sy, epr0 = R[i2].ex, epr1 = R[i2].ey;
         const double overlap = overlap_stereo(spl1, epl1, spr1, epr1);
         // sp_r << ..., sp_l(1), 1.0;  then ep_r << ... reads the UPDATED sp_r
-        spr0 = (spr0 * (spl1 - epr1) + epr0 * (spr1 - spl1)) / (spr1 - epr1);
+        spr0 = ref_fma(spr0, spl1 - epr1, epr0 * (spr1 - spl1)) / (spr1 - epr1);  // left products fused
         spr1 = spl1;
-        epr0 = (spr0 * (epl1 - epr1) + epr0 * (spr1 - epl1)) / (spr1 - epr1);
+        epr0 = ref_fma(spr0, epl1 - epr1, epr0 * (spr1 - epl1)) / (spr1 - epr1);
         epr1 = epl1;
         double disp_s = spl0 - spr0, disp_e = epl0 - epr0;  // filterLineSegmentDisparity (:1531-1542)
         float lsMinDispRatio = 0.7;
@@ -327,8 +342,8 @@ extern "C" int oracle_stereo_lines(const float* klL, const uint8_t* descL, int n
     }
     for (int i = 0; i < nL; i++) {  // mvle_l from mvKeysUn_Line (Eigen cross + normalise)
         const double a0 = U[i].sx, a1 = U[i].sy, a2 = 1.0, b0 = U[i].ex, b1 = U[i].ey, b2 = 1.0;
-        double l0 = a1 * b2 - a2 * b1, l1 = a2 * b0 - a0 * b2, l2 = a0 * b1 - a1 * b0;
-        const double s = std::sqrt(l0 * l0 + l1 * l1);
+        double l0 = a1 * b2 - a2 * b1, l1 = a2 * b0 - a0 * b2, l2 = ref_fma(a0, b1, -(a1 * b0));
+        const double s = std::sqrt(ref_fma(l0, l0, l1 * l1));  // both fused in Frame.cc.o
         le[3 * i] = l0 / s;
         le[3 * i + 1] = l1 / s;
         le[3 * i + 2] = l2 / s;

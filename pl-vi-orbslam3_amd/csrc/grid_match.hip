@@ -77,9 +77,10 @@ __global__ __launch_bounds__(64) void line_match_grid_kernel(
         __syncthreads();
         const int K = s_ncand;
         // std::pair normalize / dot (LineMatcher.h:44-52): a zero-length line
-        // gives NaN, whose |dot| < 0.75 test is false (candidate kept)
+        // gives NaN, whose |dot| < 0.75 test is false (candidate kept).  Both
+        // are fused in the reference build (LineMatcher.cpp.o matchGrid)
         double vx = (double)(epx - spx), vy = (double)(epy - spy);
-        const double mag = __builtin_sqrt(vx * vx + vy * vy);
+        const double mag = __builtin_sqrt(rfma(vx, vx, vy * vy));
         vx /= mag;
         vy /= mag;
         uint4 a0, a1;
@@ -92,7 +93,7 @@ __global__ __launch_bounds__(64) void line_match_grid_kernel(
         for (int c = lane; c < K; c += 64) {
             const int i2 = s_cand[c];
             if (i2 < 0 || i2 >= n2) continue;
-            const double dt = vx * V2[2 * i2] + vy * V2[2 * i2 + 1];
+            const double dt = rfma(vx, V2[2 * i2], vy * V2[2 * i2 + 1]);
             if (__builtin_fabs(dt) < 0.75) continue;
             const uint4* pb = reinterpret_cast<const uint4*>(D2 + (size_t)i2 * 32);
             const uint4 c0 = pb[0], c1 = pb[1];

@@ -16,6 +16,9 @@ constexpr double kNotdef = -1024.0;
 constexpr float kNotdefF = -1024.0f;
 constexpr double kD2R = 3.14159265358979323846 / 180;  // DEG_TO_RADS (lsd.cpp)
 constexpr double kPi = 3.14159265358979323846;
+// log10(11.0) as GCC folds it (MPFR, correctly rounded) into lsd.cpp.o's
+// LOG_NT (.rodata 1.0413926851582251); glibc's log10(11.0) is one ulp lower
+constexpr double kLog10Of11 = 0x1.0a98b6050c56fp+0;
 
 // ---------------------------------------------------------------------------
 // LK1: LSDDetectorC::ComputePyramid level 1 = resize(level0, (w/2,h/2)).
@@ -133,7 +136,7 @@ __global__ __launch_bounds__(64) void lsd_prep_kernel(const uint8_t* __restrict_
             const double DA = Scn - Sp;
             const double BC = Spn - Sc;
             const double gx = DA + BC, gy = DA - BC;
-            norm = __builtin_sqrt((gx * gx + gy * gy) / 4);
+            norm = __builtin_sqrt(rfma(gx, gx, gy * gy) / 4);  // fused in lsd.cpp.o ll_angle
             if (!(norm <= rho)) deg = plvi_fast_atan2((float)gx, (float)-gy);
         }
         const size_t o = (size_t)y * sw + lane;
@@ -682,7 +685,7 @@ __global__ __launch_bounds__(64 * kGrowWaves, PLVI_GROW_WPE) void lsd_grow_kerne
                 if (reg_size < min_reg) continue;
                 const unsigned long long tr0 = do_stats ? __builtin_amdgcn_s_memtime() : 0;
                 if (do_stats) n_rpt += reg_size;
-                // region2rect runs in lsd_rect_kernel (one lane per region): hand
+                // region2rect runs in lsd_rect_lanes_kernel (one lane per region): hand
                 // over the region's points in queue order and its angle
                 if (nout < kLsdRawCap) {
                     for (int j = lane; j < reg_size; j += 64) outP[npts + j] = q_get(g, j);
@@ -719,135 +722,13 @@ __global__ __launch_bounds__(64 * kGrowWaves, PLVI_GROW_WPE) void lsd_grow_kerne
 }
 
 // ---------------------------------------------------------------------------
-// LK3b: region2rect (lsd.cpp:688-744) + get_theta (:746-782) of every region
-// lsd_grow_kernel kept (reg_size >= min_reg_size), one wave per region: the
-// lanes gather the points and weights (many loads in flight) and form the
-// per-point products, lane 0 adds them from LDS in region order (the
-// reference's double summation order, no contraction); the l extents are
-// order-free max/min reductions.  Emits the Vec4f of flsd (:506-518) at the
-// region's index.
-// ---------------------------------------------------------------------------
-#ifndef PLVI_RECT_BLOCKS
-#define PLVI_RECT_BLOCKS 32
-#endif
-constexpr int kRectBlocks = PLVI_RECT_BLOCKS;  // 4-wave workgroups per (octave, frame); waves stride over the regions
-
-__global__ __launch_bounds__(256) void lsd_rect_kernel(const LineOctDev* __restrict__ octs,
-                                                       const double* __restrict__ modgrad,
-                                                       const LsdRegion* __restrict__ regs,
-                                                       const unsigned* __restrict__ regpts, size_t regpts_frame,
-                                                       const int* __restrict__ nlines, double prec, double scale_lsd,
-                                                       LsdLine* __restrict__ lines) {
-    __shared__ double rs[4][3][64];
-    const int o = blockIdx.y, f = blockIdx.z, nOct = gridDim.y;
-    const int task = f * nOct + o;
-    const int n = min(nlines[task], kLsdRawCap);
-    const LineOctDev& od = octs[o];
-    const int sw = od.sw;
-    const double* M = modgrad + od.soff + (size_t)f * od.splane;
-    const unsigned* P = regpts + (size_t)task * regpts_frame;
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    double* R0 = rs[wv][0];
-    double* R1 = rs[wv][1];
-    double* R2 = rs[wv][2];
-    for (int k = blockIdx.x * 4 + wv; k < n; k += gridDim.x * 4) {
-        const LsdRegion r = regs[(size_t)task * kLsdRawCap + k];
-        const unsigned* q = P + r.start;
-        unsigned v0 = 0u;
-        double w0 = 0.0;
-        if (lane < r.n) {
-            v0 = q[lane];
-            w0 = M[(size_t)(v0 >> 16) * sw + (v0 & 0xffffu)];
-        }
-        double xs = 0, ys = 0, sum = 0, Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
-        for (int pass = 0; pass < 2; ++pass) {
-            for (int base = 0; base < r.n; base += 64) {
-                const int j = base + lane;
-                if (j < r.n) {
-                    const unsigned v = base == 0 ? v0 : q[j];
-                    const double w = base == 0 ? w0 : M[(size_t)(v >> 16) * sw + (v & 0xffffu)];
-                    const double rx = (double)(int)(v & 0xffffu), ry = (double)(int)(v >> 16);
-                    if (pass == 0) {
-                        R0[lane] = rx * w;
-                        R1[lane] = ry * w;
-                        R2[lane] = w;
-                    } else {
-                        const double dx = rx - xs, dy = ry - ys;
-                        R0[lane] = dy * dy * w;
-                        R1[lane] = dx * dx * w;
-                        R2[lane] = dx * dy * w;
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                if (lane == 0) {
-                    const int nn = min(64, r.n - base);
-                    if (pass == 0) {
-#pragma unroll 4
-                        for (int t = 0; t < nn; ++t) {
-                            xs += R0[t];
-                            ys += R1[t];
-                            sum += R2[t];
-                        }
-                    } else {
-#pragma unroll 4
-                        for (int t = 0; t < nn; ++t) {
-                            Ixx += R0[t];
-                            Iyy += R1[t];
-                            Ixy -= R2[t];
-                        }
-                    }
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            }
-            if (pass == 0) {
-                xs = readlane_d(xs, 0) / readlane_d(sum, 0);
-                ys = readlane_d(ys, 0) / readlane_d(sum, 0);
-            }
-        }
-        Ixx = readlane_d(Ixx, 0);
-        Iyy = readlane_d(Iyy, 0);
-        Ixy = readlane_d(Ixy, 0);
-        const double lambda = 0.5 * (Ixx + Iyy - __builtin_sqrt((Ixx - Iyy) * (Ixx - Iyy) + 4.0 * Ixy * Ixy));
-        double theta = (__builtin_fabs(Ixx) > __builtin_fabs(Iyy))
-                           ? (double)plvi_fast_atan2((float)(lambda - Ixx), (float)Ixy)
-                           : (double)plvi_fast_atan2((float)Ixy, (float)(lambda - Iyy));
-        theta *= kD2R;
-        if (angle_diff(theta, r.angle) > prec) theta += kPi;
-        const double dxv = plvi_cos(theta), dyv = plvi_sin(theta);
-        // l extents: the reference's if/else-if max/min is equivalent to
-        // independent max(0, .)/min(0, .) (l_min <= 0 <= l_max throughout).
-        double lmax = 0, lmin = 0;
-        for (int j = lane; j < r.n; j += 64) {
-            const unsigned v = j < 64 ? v0 : q[j];
-            const double l = ((double)(int)(v & 0xffffu) - xs) * dxv + ((double)(int)(v >> 16) - ys) * dyv;
-            lmax = l > lmax ? l : lmax;
-            lmin = l < lmin ? l : lmin;
-        }
-        for (int s2 = 32; s2 > 0; s2 >>= 1) {
-            const double a2 = __shfl_xor(lmax, s2), b2 = __shfl_xor(lmin, s2);
-            lmax = a2 > lmax ? a2 : lmax;
-            lmin = b2 < lmin ? b2 : lmin;
-        }
-        double x1 = xs + lmin * dxv, y1 = ys + lmin * dyv;
-        double x2 = xs + lmax * dxv, y2 = ys + lmax * dyv;
-        x1 += 0.5; y1 += 0.5; x2 += 0.5; y2 += 0.5;
-        if (scale_lsd != 1) {
-            x1 /= scale_lsd; y1 /= scale_lsd; x2 /= scale_lsd; y2 /= scale_lsd;
-        }
-        if (lane == 0) lines[(size_t)task * kLsdRawCap + k] = LsdLine{(float)x1, (float)y1, (float)x2, (float)y2};
-    }
-}
-
-// ---------------------------------------------------------------------------
-// LK3c: the same region2rect + get_theta with lane = region.  Each lane walks
-// its own region's points in region order through the reference's three
-// loops (centroid sums, inertia sums, l extents; lsd.cpp:697-744, :755-771):
-// the identical sequence of double products and adds per region, with no
-// LDS round trip and no idle lanes behind a serial lane 0.  Points and
+// LK3: region2rect (lsd.cpp:688-744) + get_theta (:746-782) with lane =
+// region.  Each lane walks its own region's points in region order through
+// the reference's three loops (centroid sums, inertia sums, l extents;
+// lsd.cpp:697-744, :755-771): the identical sequence of double operations per
+// region -- including the nine multiply-adds lsd.cpp.o fuses (x / y sums,
+// Ixx / Iyy / Ixy, the eigenvalue root, l, the endpoints) -- with no LDS
+// round trip and no idle lanes behind a serial lane 0.  Points and
 // weights are fetched kRectU at a time so each lane keeps several loads in
 // flight; regions of one wave are consecutive indices of one (frame, octave).
 // ---------------------------------------------------------------------------
@@ -888,16 +769,16 @@ __global__ __launch_bounds__(256) void lsd_rect_lanes_kernel(const LineOctDev* _
             for (int u = 0; u < kRectU; ++u) w[u] = M[(size_t)(v[u] >> 16) * sw + (v[u] & 0xffffu)];
 #pragma unroll
             for (int u = 0; u < kRectU; ++u) {
-                xs += (double)(int)(v[u] & 0xffffu) * w[u];
-                ys += (double)(int)(v[u] >> 16) * w[u];
+                xs = rfma((double)(int)(v[u] & 0xffffu), w[u], xs);
+                ys = rfma((double)(int)(v[u] >> 16), w[u], ys);
                 sum += w[u];
             }
         }
         for (; i < rn; ++i) {
             const unsigned v = q[i];
             const double w = M[(size_t)(v >> 16) * sw + (v & 0xffffu)];
-            xs += (double)(int)(v & 0xffffu) * w;
-            ys += (double)(int)(v >> 16) * w;
+            xs = rfma((double)(int)(v & 0xffffu), w, xs);
+            ys = rfma((double)(int)(v >> 16), w, ys);
             sum += w;
         }
         xs /= sum;
@@ -915,20 +796,20 @@ __global__ __launch_bounds__(256) void lsd_rect_lanes_kernel(const LineOctDev* _
 #pragma unroll
             for (int u = 0; u < kRectU; ++u) {
                 const double dx = (double)(int)(v[u] & 0xffffu) - xs, dy = (double)(int)(v[u] >> 16) - ys;
-                Ixx += dy * dy * w[u];
-                Iyy += dx * dx * w[u];
-                Ixy -= dx * dy * w[u];
+                Ixx = rfma(dy * dy, w[u], Ixx);
+                Iyy = rfma(dx * dx, w[u], Iyy);
+                Ixy = rfma(-(dx * dy), w[u], Ixy);
             }
         }
         for (; i < rn; ++i) {
             const unsigned v = q[i];
             const double w = M[(size_t)(v >> 16) * sw + (v & 0xffffu)];
             const double dx = (double)(int)(v & 0xffffu) - xs, dy = (double)(int)(v >> 16) - ys;
-            Ixx += dy * dy * w;
-            Iyy += dx * dx * w;
-            Ixy -= dx * dy * w;
+            Ixx = rfma(dy * dy, w, Ixx);
+            Iyy = rfma(dx * dx, w, Iyy);
+            Ixy = rfma(-(dx * dy), w, Ixy);
         }
-        const double lambda = 0.5 * (Ixx + Iyy - __builtin_sqrt((Ixx - Iyy) * (Ixx - Iyy) + 4.0 * Ixy * Ixy));
+        const double lambda = 0.5 * (Ixx + Iyy - __builtin_sqrt(rfma(Ixx - Iyy, Ixx - Iyy, 4.0 * Ixy * Ixy)));
         double theta = (__builtin_fabs(Ixx) > __builtin_fabs(Iyy))
                            ? (double)plvi_fast_atan2((float)(lambda - Ixx), (float)Ixy)
                            : (double)plvi_fast_atan2((float)Ixy, (float)(lambda - Iyy));
@@ -944,19 +825,19 @@ __global__ __launch_bounds__(256) void lsd_rect_lanes_kernel(const LineOctDev* _
             for (int u = 0; u < kRectU; ++u) v[u] = q[i + u];
 #pragma unroll
             for (int u = 0; u < kRectU; ++u) {
-                const double l = ((double)(int)(v[u] & 0xffffu) - xs) * dxv + ((double)(int)(v[u] >> 16) - ys) * dyv;
+                const double l = rfma((double)(int)(v[u] & 0xffffu) - xs, dxv, ((double)(int)(v[u] >> 16) - ys) * dyv);
                 lmax = l > lmax ? l : lmax;
                 lmin = l < lmin ? l : lmin;
             }
         }
         for (; i < rn; ++i) {
             const unsigned v = q[i];
-            const double l = ((double)(int)(v & 0xffffu) - xs) * dxv + ((double)(int)(v >> 16) - ys) * dyv;
+            const double l = rfma((double)(int)(v & 0xffffu) - xs, dxv, ((double)(int)(v >> 16) - ys) * dyv);
             lmax = l > lmax ? l : lmax;
             lmin = l < lmin ? l : lmin;
         }
-        double x1 = xs + lmin * dxv, y1 = ys + lmin * dyv;
-        double x2 = xs + lmax * dxv, y2 = ys + lmax * dyv;
+        double x1 = rfma(lmin, dxv, xs), y1 = rfma(lmin, dyv, ys);
+        double x2 = rfma(lmax, dxv, xs), y2 = rfma(lmax, dyv, ys);
         x1 += 0.5; y1 += 0.5; x2 += 0.5; y2 += 0.5;
         if (scale_lsd != 1) {
             x1 /= scale_lsd; y1 /= scale_lsd; x2 /= scale_lsd; y2 /= scale_lsd;
@@ -1022,9 +903,6 @@ __device__ inline int line_iter_count(int W, int H, float fx1, float fy1, float 
 }
 
 constexpr int kKlCap = 4096;  // keylines per frame before the top-k filter
-#ifndef PLVI_TIE_SERIAL
-#define PLVI_TIE_SERIAL 0
-#endif
 
 __global__ __launch_bounds__(256) void line_assemble_kernel(const LineOctDev* __restrict__ octs, int nOct,
                                                             const LsdLine* __restrict__ lines,
@@ -1144,12 +1022,8 @@ __global__ __launch_bounds__(256) void line_assemble_kernel(const LineOctDev* __
             for (int i = threadIdx.x; i < n; i += 256) s_items[i] = SortItem{tmp[i].response, i};
             __syncthreads();
             // the libstdc++ std::sort permutation, replayed by the whole block
-            // (std_sort.h: std_sort_block; PLVI_TIE_SERIAL=1: one thread)
-            if (PLVI_TIE_SERIAL) {
-                if (threadIdx.x == 0) std_sort(s_items, s_items + n);
-            } else {
-                std_sort_block(s_items, n, s_rng[0], s_rng[1], s_seg, s_ctl);
-            }
+            // (std_sort.h: std_sort_block)
+            std_sort_block(s_items, n, s_rng[0], s_rng[1], s_seg, s_ctl);
         } else {
             for (int i = threadIdx.x; i < nfinal; i += 256) {
                 const unsigned long long v = K[i];
@@ -1170,8 +1044,9 @@ __global__ __launch_bounds__(256) void line_assemble_kernel(const LineOctDev* __
         outk[i] = kl;
         // lineF = (sp x ep) / sqrt(l0^2 + l1^2), Eigen Vector3d (LineExtractor.cc:106-115)
         const double sx = kl.startPointX, sy = kl.startPointY, ex = kl.endPointX, ey = kl.endPointY;
-        const double a = sy * 1.0 - 1.0 * ey, b = 1.0 * ex - sx * 1.0, c = sx * ey - sy * ex;
-        const double nrm = __builtin_sqrt(a * a + b * b);
+        // LineExtractor.cc.o fuses sx*ey - sy*ex and a*a + b*b
+        const double a = sy * 1.0 - 1.0 * ey, b = 1.0 * ex - sx * 1.0, c = rfma(sx, ey, -(sy * ex));
+        const double nrm = __builtin_sqrt(rfma(a, a, b * b));
         outf[3 * i] = a / nrm;
         outf[3 * i + 1] = b / nrm;
         outf[3 * i + 2] = c / nrm;
@@ -1429,9 +1304,6 @@ __global__ __launch_bounds__(64) void lbd_sobel1_kernel(const uint8_t* __restric
 // normalises.  Gaussian coefficient tables come from the host (double exp,
 // cast to float at use, :1189/:1203).
 // ---------------------------------------------------------------------------
-#ifndef PLVI_LBD_XPOSE
-#define PLVI_LBD_XPOSE 1  // support-region gathers transposed through LDS (8 rows x 8 samples per instruction)
-#endif
 __constant__ float c_gaussG[63];
 __constant__ float c_gaussL[21];
 __constant__ unsigned char c_comb[64];
@@ -1461,7 +1333,6 @@ __global__ __launch_bounds__(64) void lbd_describe_kernel(const LineOctDev* __re
     const float dO0 = -dL1, dO1 = dL0;
     const int h = threadIdx.x;
     float pL = 0, nL = 0, pO = 0, nO = 0;
-#if PLVI_LBD_XPOSE
     // The coordinates are walked per row lane (reference order), but the
     // gathers are transposed through LDS: one gather instruction then covers
     // 8 rows x 8 consecutive samples instead of 64 rows at one sample, so its
@@ -1523,47 +1394,6 @@ __global__ __launch_bounds__(64) void lbd_describe_kernel(const LineOctDev* __re
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         }
     }
-#else
-    if (h < 63) {
-        float sX0 = -dL0 * halfWidth + dL1 * halfHeight + mX;
-        float sY0 = -dL1 * halfWidth - dL0 * halfHeight + mY;
-        for (int k = 0; k < h; ++k) {
-            sX0 -= dL1;
-            sY0 += dL0;
-        }
-        float sX = sX0, sY = sY0;
-        // samples in batches of 8: the coordinate sequence (sequential float
-        // steps) and the sums stay in reference order; the 8 gathers are in
-        // flight together
-        for (int w0 = 0; w0 < lengthOfLSP; w0 += 8) {
-            int idx[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                short t = (short)__builtin_roundf(sX);
-                const short xc = (t < 0) ? 0 : (t > imageWidth) ? imageWidth : t;
-                t = (short)__builtin_roundf(sY);
-                const short yc = (t < 0) ? 0 : (t > imageHeight) ? imageHeight : t;
-                idx[k] = yc * realWidth + xc;
-                sX += dL0;
-                sY += dL1;
-            }
-            short2 g[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) g[k] = w0 + k < lengthOfLSP ? pg[idx[k]] : make_short2(0, 0);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                if (w0 + k >= lengthOfLSP) break;
-                const short dx = g[k].x, dy = g[k].y;
-                const float gDL = dx * dL0 + dy * dL1;
-                const float gDO = dx * dO0 + dy * dO1;
-                if (gDL > 0) pL += gDL;
-                else nL -= gDL;
-                if (gDO > 0) pO += gDO;
-                else nO -= gDO;
-            }
-        }
-    }
-#endif
     // row sums scaled by gaussCoefG_ (:1189-1197), per row lane
     if (h < 63) {
         const float c = c_gaussG[h];

@@ -87,7 +87,7 @@ struct LinePipeline {
     double gk[7]{};
     int lbdTaps[3] = {14, 62, 104};
     DevBuf d_oct, d_tabs, octImg, pix, modg, seedcs, gbits, qspill, regs, regpts, rawLines, nlines, klTmp, klOut, fnOut, cntOut, descOut, lbdBlur,
-        lbdG, err, staging, mwOwn, mwSlot, mwGrow, mwHMap, mwHRec, mwHPts, mwHCur, mwHOwn, mwHGq;
+        lbdG, err, staging, mwOwn, mwSlot, mwGrow;
     size_t qspillFrame = 0, gbitsFrame = 0, lbdPlaneTotal = 0;
     int lastFrames = 0;
     static constexpr int kStages = 5, kRing = 512;
@@ -289,7 +289,10 @@ struct LinePipeline {
             d.soff = (long long)sOff;
             sOff += (size_t)d.splane * Bcap;
             maxSplane = std::max(maxSplane, (size_t)d.splane);
-            const double LOG_NT = 5 * (std::log10((double)d.sw) + std::log10((double)d.sh)) / 2 + std::log10(11.0);
+            // lsd.cpp.o computes 5*(.)/2 + log10(11.0) as one fused
+            // multiply-add by 0.5 with GCC's folded constant log10(11.0)
+            const double LOG_NT = rfma(5 * (std::log10((double)d.sw) + std::log10((double)d.sh)), 0.5,
+                                       kLog10Of11);
             d.min_reg_size = (int)(-LOG_NT / std::log10(pp));
             d.octaveScale = (float)std::pow(p->scale, l);
             d.maxWH = std::max(d.w, d.h);
@@ -420,10 +423,6 @@ struct LinePipeline {
         growWPW = (int)std::max<size_t>(1, std::min<size_t>(kGrowWaves, (160 * 1024) / growSmem));
         for (const void* k : {(const void*)lsd_grow_kernel<false>, (const void*)lsd_grow_kernel<true>})
             PLVI_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(growSmem * growWPW)));
-        // region2rect: PLVI_RECT_LANES=1 (default) lane = region
-        // (lsd_rect_lanes_kernel), 0 = wave = region (lsd_rect_kernel)
-        rectLanes = true;
-        if (const char* e = getenv("PLVI_RECT_LANES")) rectLanes = atoi(e) != 0;
         // Small batches (latency): lsd_grow_mw_kernel, kMwWaves waves per
         // (frame, octave) growing regions of one frame concurrently.
         // PLVI_GROW_MW = largest batch that takes it (default 256; 0 = off).
@@ -449,31 +448,6 @@ struct LinePipeline {
                     mwGrow.alloc(sizeof(unsigned) * (size_t)kMwWaves * kMwGSpill * tasks))
                     return PLVI_E_HIP;
                 PLVI_CHECK(hipMemset(mwOwn.p, 0, mwOwn.bytes));  // kept zero by every launch
-                // helper workgroups (octave 0 of small batches, on the CUs the
-                // tasks leave idle): PLVI_MW_HELP = most helpers per task (0 = off)
-                mwHelpMax = 0;
-                if (const char* e = getenv("PLVI_MW_HELP")) mwHelpMax = std::max(0, std::min(kMwHelpMax, atoi(e)));
-                if (!PLVI_MW_HELPERS) mwHelpMax = 0;  // built without the helper role
-                mwHMapTask = gbitsFrame * 32;  // bit indices of the largest octave
-                if (mwHelpMax > 0 && mwHMapTask < (1u << 20)) {
-                    int dev = 0;
-                    PLVI_CHECK(hipGetDevice(&dev));
-                    PLVI_CHECK(hipDeviceGetAttribute(&mwCUs, hipDeviceAttributeMultiprocessorCount, dev));
-                    mwHelpWgs = std::max(8, mwCUs / 2);
-                    const size_t W = (size_t)mwHelpWgs;
-                    if (mwHMap.alloc(sizeof(unsigned) * mwHMapTask * W) ||
-                        mwHRec.alloc(sizeof(MwHelpRec) * kMwHelpRecCap * W) ||
-                        mwHPts.alloc(sizeof(unsigned) * mwHMapTask * W) || mwHCur.alloc(sizeof(unsigned) * W) ||
-                        mwHOwn.alloc(sizeof(unsigned) * mwOwnTask * W) ||
-                        mwHGq.alloc(sizeof(unsigned) * (size_t)kMwWaves * kMwGSpill * W))
-                        return PLVI_E_HIP;
-                    PLVI_CHECK(hipMemset(mwHMap.p, 0, mwHMap.bytes));
-                    PLVI_CHECK(hipMemset(mwHRec.p, 0, mwHRec.bytes));
-                    PLVI_CHECK(hipMemset(mwHCur.p, 0, mwHCur.bytes));
-                    PLVI_CHECK(hipMemset(mwHOwn.p, 0, mwHOwn.bytes));  // kept zero by every launch
-                } else {
-                    mwHelpMax = 0;
-                }
                 for (const void* k : {(const void*)lsd_grow_mw_kernel<kMwWaves, false>,
                                       (const void*)lsd_grow_mw_kernel<kMwWaves, true>})
                     PLVI_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)mwSmem));
@@ -485,12 +459,8 @@ struct LinePipeline {
 #define PLVI_MW_WAVES 16
 #endif
     static constexpr int kMwWaves = PLVI_MW_WAVES;  // waves per (frame, octave) of the multi-wave kernel
-    bool rectLanes = true;
     int mwMaxFrames = 0, mwSlots = 0;
     size_t mwSmem = 0, mwOwnTask = 0;
-    int mwHelpMax = 0, mwHelpWgs = 0, mwCUs = 0;  // helpers per task (most), helper workgroups buffered, CUs
-    size_t mwHMapTask = 0;
-    unsigned mwEpoch = 0;
     int* mwStats = nullptr;  // diagnostic counters (plvi_lines_debug_mw_stats)
     size_t growSmem = 0;
     int growWPW = 1;  // region-growing tasks (waves) per workgroup
@@ -564,24 +534,11 @@ struct LinePipeline {
     void launch_grow(int nf, int oBase, int oCount, hipStream_t st) {
         if (nf <= mwMaxFrames) {
             auto mwK = mwStats ? lsd_grow_mw_kernel<kMwWaves, true> : lsd_grow_mw_kernel<kMwWaves, false>;
-            // helpers for the launches that grow octave 0: as many per task as
-            // the CUs left by every octave's tasks allow (one workgroup per CU)
-            const int nT = oCount * nf, nT8 = (nT + 7) & ~7;
-            int K = 0;
-            if (mwHelpMax > 0 && oBase == 0) {
-                K = std::min(mwHelpMax, (mwCUs - nf * nOct) / nT);
-                K = std::max(0, std::min(K, mwHelpWgs / nT8));
-            }
-            const int nTp = K > 0 ? nT8 : nT;  // sections padded to 8 blocks only with helpers
-            MwHelp Hp{mwHMap.as<unsigned>(), mwHMapTask, mwHRec.as<MwHelpRec>(), mwHPts.as<unsigned>(),
-                      mwHCur.as<unsigned>(), mwHOwn.as<unsigned>(), mwOwnTask, mwHGq.as<unsigned>(), K, nTp,
-                      (int)mwHMapTask, ++mwEpoch};
-            hipLaunchKernelGGL(mwK, dim3(nTp * (K + 1)), dim3(kMwWaves * 64), mwSmem, st, d_oct.as<LineOctDev>(),
+            hipLaunchKernelGGL(mwK, dim3(oCount * nf), dim3(kMwWaves * 64), mwSmem, st, d_oct.as<LineOctDev>(),
                                (const float*)pix.as<float>(), (const float2*)seedcs.as<float2>(),
                                mwOwn.as<unsigned>(), mwOwnTask, mwGrow.as<unsigned>(), mwSlot.as<unsigned>(),
                                qspill.as<unsigned>(), qspillFrame, prec, regs.as<LsdRegion>(), regpts.as<unsigned>(),
-                               qspillFrame, nlines.as<int>(), err.as<int>(), mwSlots, nOct, oBase, oCount, mwStats, nf,
-                               Hp);
+                               qspillFrame, nlines.as<int>(), err.as<int>(), mwSlots, nOct, oBase, oCount, mwStats, nf);
             return;
         }
         auto growK = growStats ? lsd_grow_kernel<true> : lsd_grow_kernel<false>;
@@ -595,18 +552,14 @@ struct LinePipeline {
     }
     void launch_grow_assemble(int nf, hipStream_t st, bool grown = false) {
         if (!grown) launch_grow(nf, 0, nOct, st);
-        if (rectLanes) {
-            // small batches spread a frame's regions over more workgroups (latency)
+        {
+            // region2rect, lane = region; small batches spread a frame's
+            // regions over more workgroups (latency)
             const int bx = nf <= 16 ? 8 : kRectLaneBlocks;
             hipLaunchKernelGGL(lsd_rect_lanes_kernel, dim3(bx, nOct, nf), dim3(256), 0, st, d_oct.as<LineOctDev>(),
                                (const double*)modg.as<double>(), (const LsdRegion*)regs.as<LsdRegion>(),
                                (const unsigned*)regpts.as<unsigned>(), qspillFrame, (const int*)nlines.as<int>(),
                                prec, SCALE, rawLines.as<LsdLine>());
-        } else {
-            hipLaunchKernelGGL(lsd_rect_kernel, dim3(kRectBlocks, nOct, nf), dim3(256), 0, st,
-                               d_oct.as<LineOctDev>(), (const double*)modg.as<double>(),
-                               (const LsdRegion*)regs.as<LsdRegion>(), (const unsigned*)regpts.as<unsigned>(),
-                               qspillFrame, (const int*)nlines.as<int>(), prec, SCALE, rawLines.as<LsdLine>());
         }
         mark(3, st);
         hipLaunchKernelGGL(line_assemble_kernel, dim3(nf), dim3(256), 0, st, d_oct.as<LineOctDev>(), nOct,

@@ -30,17 +30,9 @@
 // of kMwRB rows from the seed row (rows below it spill to a global bitmap)
 // and a growth queue (spill to global), the slot pool, the dispatch log (the
 // speculative seeds in increasing order with their slots).  Commit order =
-// raster seed order, so the region list handed to lsd_rect_kernel is the
+// raster seed order, so the region list handed to lsd_rect_lanes_kernel is the
 // sequential kernel's.
 //
-// Helper workgroups (nHelp per task, on other CUs): helper k grows the seeds
-// of row band k + 1 of nHelp + 1 ahead of the task's own growers with the
-// same rule and no committed bitmap at all (an empty C is a subset of the
-// walk's, so the validation above still decides), and publishes each region
-// in global memory behind an agent-scope release; a grower of the task whose
-// cursor reaches that seed imports it (agent-scope acquire) into a slot
-// instead of growing it, marked for revalidation.  A seed no helper has
-// published yet is grown as before, so helpers only move work off the CU.
 // ---------------------------------------------------------------------------
 #pragma once
 
@@ -64,38 +56,7 @@ constexpr int kMwLog = 256;         // dispatch log entries (seed order)
 #ifndef PLVI_MW_GROWER_PRIO
 #define PLVI_MW_GROWER_PRIO 1
 #endif
-// a grower reads the walk position (relaxed) at the top of each block and
-// tests it once the block's loads are issued, instead of an acquire load
-// that stalls the block first: region growing 6.40 -> 6.27 ms (one frame),
-// 7.97 -> 7.86 ms (64 frames), profiles/r04/mw_helpers_ab.txt
-#ifndef PLVI_MW_WALKFAST
-#define PLVI_MW_WALKFAST 0
-#endif
-#ifndef PLVI_MW_LATECHK
-#define PLVI_MW_LATECHK 1
-#endif
-#ifndef PLVI_MW_BOOST
-#define PLVI_MW_BOOST 1  // a grower whose seed the walk has reached runs at priority 3
-#endif
 constexpr int kMwLook = PLVI_MW_LOOK;  // dispatch-log entries ahead of the walk that growers revalidate (0 = off)
-#ifndef PLVI_MW_LATE
-#define PLVI_MW_LATE 0
-#endif
-// second-chance dispatch: an idle grower takes an undispatched seed just
-// ahead of the walk (skipped by the cursor because a dropped or regrown
-// region had claimed it, H) and files it in a small unordered "late" log
-constexpr int kMwLate = PLVI_MW_LATE;  // late-log entries (0 = off, the default: at 32 the undispatched
-                                       // seeds fall 119 -> 43 but dropped regions rise 338 -> 1036 and the
-                                       // kernel takes 10.9 instead of 7.1 ms per frame; <= 64)
-constexpr int kMwLateWords = 64;       // bitmap words ahead of the walk a grower scans for them
-// PLVI_MW_ORPHAN (with PLVI_MW_LATE > 0): a region that will not be committed
-// as grown (invalid at the walk, dropped, regrown by revalidation) gives up
-// its H claims outside C, and the second-chance dispatch takes only such
-// orphans -- pixels between the walk and the cursor that are neither
-// committed, trivial nor claimed -- instead of every claimed pixel
-#ifndef PLVI_MW_ORPHAN
-#define PLVI_MW_ORPHAN 0
-#endif
 
 // slot states; COMMITTED: validated and committed, a grower still copies
 // its points out (regions of more than kMwSP points); WALKING: the walker
@@ -111,7 +72,6 @@ struct MwSlot {
     int ovf;    // queue overflow: the walker regrows it
     int out;    // COMMITTED: offset of its points in the task's point list
     int chk;    // ctl->ncommit when the region was last grown / found valid
-    int dead;   // PLVI_MW_ORPHAN: FREE after a region that was not committed (its claims not yet released)
 };
 constexpr int kMwSlotBytes = sizeof(MwSlot) + 4 * kMwSP;
 // control block (LDS)
@@ -119,11 +79,10 @@ struct MwCtl {
     int lock, dlock, head, cursor, finished, npts, nout, overflow;
     int dlog_n, wptr, ncommit, pad1;  // dispatch log: entries appended / next entry the walk examines;
                                       // regions committed so far (revalidation epoch)
-    int late_seed[kMwLate > 0 ? kMwLate : 1], late_slot[kMwLate > 0 ? kMwLate : 1];  // late log (seed -1: free)
     int stat[16];  // [0] dispatched [1] dropped [2] regrown [3] exact (undispatched) [4] trivial [5] committed
                    // speculative [6] walk cycles [7] walker growth cycles [8] walk entries [9] blocked on a
                    // growing head [10] kernel cycles (wave 0) [11] speculative growth cycles (sum over waves)
-                   // [12] regions imported from helpers [13] blocks (completed regions) [14] block setup cycles / 16
+                   // [12] unused [13] blocks (completed regions) [14] block setup cycles / 16
                    // [15] block round cycles / 16
 };
 
@@ -160,11 +119,6 @@ struct MwEnv {
 // as hints) are only accessed atomically -- relaxed where a later acquire or
 // a lock re-checks the value.  On gfx950 (no threadgroup split) a
 // workgroup-scope release or acquire on LDS costs an s_waitcnt lgkmcnt(0).
-// PLVI_MW_RELAXED=1 builds the r03 hand-offs (relaxed atomics + compiler
-// fences, relying on in-order DS execution) for A/B measurement only.
-#ifndef PLVI_MW_RELAXED
-#define PLVI_MW_RELAXED 0
-#endif
 __device__ __forceinline__ unsigned mw_peek(const lds_u32* p) {
     return __hip_atomic_load(const_cast<lds_u32*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -205,32 +159,19 @@ __device__ __forceinline__ void mw_wave_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
-#if PLVI_MW_RELAXED
-__device__ __forceinline__ void mw_cfence() { __atomic_signal_fence(__ATOMIC_SEQ_CST); }
-#define PLVI_MW_ACQ __ATOMIC_RELAXED
-#define PLVI_MW_REL __ATOMIC_RELAXED
-#else
-__device__ __forceinline__ void mw_cfence() {}
-#define PLVI_MW_ACQ __ATOMIC_ACQUIRE
-#define PLVI_MW_REL __ATOMIC_RELEASE
-#endif
 // acquire load of a flag (pairs with mw_lds_store)
 __device__ __forceinline__ int mw_lds_load(lds_i32* p) {
-    mw_cfence();
-    const int v = __hip_atomic_load(p, PLVI_MW_ACQ, __HIP_MEMORY_SCOPE_WORKGROUP);
-    mw_cfence();
+    const int v = __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
     return v;
 }
 // release store of a flag: everything this wave wrote before it (after a
 // mw_wave_sync when other lanes wrote) is visible to an acquiring wave
 __device__ __forceinline__ void mw_lds_store(lds_i32* p, int v) {
-    mw_cfence();
-    __hip_atomic_store(p, v, PLVI_MW_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-    mw_cfence();
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 // compare-and-swap of a slot state / lock word: acquire on success
 __device__ __forceinline__ bool mw_lds_cas(lds_i32* p, int expected, int desired) {
-    return __hip_atomic_compare_exchange_strong(p, &expected, desired, PLVI_MW_ACQ, __ATOMIC_RELAXED,
+    return __hip_atomic_compare_exchange_strong(p, &expected, desired, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void mw_stat(lds_ctl* c, int i, int v) {
@@ -239,10 +180,8 @@ __device__ __forceinline__ void mw_stat(lds_ctl* c, int i, int v) {
 // wave-uniform try-lock (lane 0 does the CAS)
 __device__ __forceinline__ bool mw_try_lock(lds_i32* l, int lane) {
     int got = 0;
-    mw_cfence();
     if (lane == 0) got = mw_lds_cas(l, 0, 1) ? 1 : 0;
     got = __builtin_amdgcn_readfirstlane(got);
-    mw_cfence();
     return got != 0;
 }
 __device__ __forceinline__ void mw_unlock(lds_i32* l, int lane) {
@@ -253,7 +192,7 @@ __device__ __forceinline__ void mw_unlock(lds_i32* l, int lane) {
 // Grow the region of seed (sx, sy) into Q (region_grow, lsd.cpp:635-686).
 // SPEC: abandon when the walk passes the seed.  Returns 0 = grown, 1 =
 // abandoned, 2 = queue overflow; n = points in Q (own marks set for them).
-template <bool SPEC, bool STATS = false, bool HELP = false>
+template <bool SPEC, bool STATS = false>
 __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_out, float& deg_out, bool& spilled,
                        int lane) {
     unsigned long long c_setup = 0, c_round = 0, n_blk = 0;
@@ -277,23 +216,11 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
     int reg_size = 1;
     const int cap = Q.lcap + Q.gcap;
     for (int i = 0; i < reg_size;) {
-        // PLVI_MW_LATECHK: the walk position is read at the top of the block
-        // (relaxed: a hint) and tested once the block's loads are in flight
-        const int hd0 = SPEC && PLVI_MW_LATECHK ? mw_peek(&E.ctl->head) : 0;
-        if (SPEC && !PLVI_MW_LATECHK) {
-            const int hd = mw_lds_load(&E.ctl->head);
-            if (hd > seedb) {
-                n_out = reg_size;
-                deg_out = reg_deg;
-                return 1;
-            }
-            // the walk waits on this region: let it win the SIMD's issue
-            // arbitration against the other growers until it is done
-            if (PLVI_MW_BOOST) {
-                if (hd == seedb) __builtin_amdgcn_s_setprio(3);
-                else __builtin_amdgcn_s_setprio(PLVI_MW_GROWER_PRIO);
-            }
-        }
+        // the walk position is read at the top of the block (relaxed: a hint)
+        // and tested once the block's loads are in flight, instead of an
+        // acquire load that stalls the block first (6.40 -> 6.27 ms at one
+        // frame, profiles/r04/mw_helpers_ab.txt)
+        const int hd0 = SPEC ? mw_peek(&E.ctl->head) : 0;
         const unsigned long long tb0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
         const int nb = min(7, reg_size - i);
         const bool active = lane < 9 * nb;
@@ -321,23 +248,21 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
             const int ddx = nx - (int)(q2 & 0xffffu) + 1, ddy = ny - (int)(q2 >> 16) + 1;
             if (p2 < bp && ddx >= 0 && ddx <= 2 && ddy >= 0 && ddy <= 2) dup |= 1ull << (9 * p2 + ddy * 3 + ddx);
         }
-        if (SPEC && PLVI_MW_LATECHK) {
+        if (SPEC) {
             if (hd0 > seedb) {
                 n_out = reg_size;
                 deg_out = reg_deg;
                 return 1;
             }
-            if (PLVI_MW_BOOST) {
-                if (hd0 == seedb) __builtin_amdgcn_s_setprio(3);
-                else __builtin_amdgcn_s_setprio(PLVI_MW_GROWER_PRIO);
-            }
+            // the walk waits on this region: let it win the SIMD's issue
+            // arbitration against the other growers until it is done
+            if (hd0 == seedb) __builtin_amdgcn_s_setprio(3);
+            else __builtin_amdgcn_s_setprio(PLVI_MW_GROWER_PRIO);
         }
         // own marks and the committed bitmap, read once per block (within the
         // block a lane's pixel only changes through an earlier lane's commit
         // of the same pixel: dup / Ccum)
-        // (a helper has no committed bitmap: HELP)
-        const bool live0 =
-            valid && deg != kNotdefF && (HELP || !mw_bit(E.C, E.wpr, nx, ny)) && !mw_own_get(E, nx, ny, sy);
+        const bool live0 = valid && deg != kNotdefF && !mw_bit(E.C, E.wpr, nx, ny) && !mw_own_get(E, nx, ny, sy);
         unsigned long long tb1 = 0;
         if (STATS) {
             tb1 = __builtin_amdgcn_s_memtime();
@@ -425,18 +350,6 @@ __device__ __forceinline__ void mw_own_clear(const MwEnv& E, int sy, const MwQue
     mw_wave_sync();
 }
 
-// Release the H claims of a region that will not be committed as grown
-// (points outside C only: a committed pixel stays claimed).
-__device__ __forceinline__ void mw_unclaim(const MwEnv& E, const MwQueue& Q, int n, int lane) {
-    for (int j = lane; j < n; j += 64) {
-        const unsigned v = mw_qget(Q, j);
-        const int x = (int)(v & 0xffffu), y = (int)(v >> 16);
-        if (!mw_bit(E.C, E.wpr, x, y))
-            __hip_atomic_fetch_and(&E.H[y * E.wpr + (x >> 5)], ~(1u << (x & 31)), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-}
-
 // A slot's points: the first kMwSP in LDS after its header, the rest in
 // global memory.
 __device__ __forceinline__ MwQueue mw_slot_queue(lds_u8* pool, unsigned* slotspill, int si) {
@@ -462,9 +375,6 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
         // next unresolved pixel >= head: first zero bit of C
         int w = head >> 5;
         if (w >= nwords) break;
-        // PLVI_MW_WALKFAST: the dispatch-log count is read (relaxed) beside the
-        // bitmap words and acquired by a fence once the seed is known
-        const int dnr = PLVI_MW_WALKFAST ? mw_peek(&ctl->dlog_n) : 0;
         unsigned cw = mw_peek(E.C + w), tw = E.T[w];  // T is static after the set-up
         unsigned m = ~cw & (~0u << (head & 31));
         if (!m) {
@@ -499,35 +409,22 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
         const int q = w * 32 + (__ffs((int)nt) - 1);
         head = q;
         // the speculative region of seed q, if one was dispatched
-        int dn;
-        if (PLVI_MW_WALKFAST) {
-            dn = dnr;
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // pairs with the dispatcher's release of dlog_n
-        } else {
-            dn = mw_lds_load(&ctl->dlog_n);
-        }
+        const int dn = mw_lds_load(&ctl->dlog_n);
         while (wp < dn && dlog[2 * (wp & (kMwLog - 1))] < q) ++wp;
         int si = -1;
         bool fromLog = false;
         if (wp < dn && dlog[2 * (wp & (kMwLog - 1))] == q) {
             si = dlog[2 * (wp & (kMwLog - 1)) + 1];
             fromLog = true;
-        } else if (kMwLate > 0) {
-            // a second-chance region (late log, unordered: lanes compare)
-            const bool hit = lane < kMwLate && mw_lds_load(&ctl->late_seed[lane < kMwLate ? lane : 0]) == q;
-            const unsigned long long hb = __ballot(hit);
-            if (hb) si = ctl->late_slot[__ffsll((long long)hb) - 1];
         }
         lds_slot* S = si >= 0 ? mw_slot(pool, si) : nullptr;
         int sst = si >= 0 ? mw_lds_load(&S->state) : kMwFree;
         if (sst == kMwDone) {
             // claim it against a grower's revalidation
             int got = 0;
-            mw_cfence();
-            if (lane == 0) got = mw_lds_cas(&S->state, kMwDone, kMwWalking) ? 1 : 0;
+                    if (lane == 0) got = mw_lds_cas(&S->state, kMwDone, kMwWalking) ? 1 : 0;
             got = __builtin_amdgcn_readfirstlane(got);
-            mw_cfence();
-            if (!got) sst = kMwGrowing;
+                    if (!got) sst = kMwGrowing;
         }
         if (sst == kMwGrowing) {  // wait for it
             if (STATS && lane == 0) mw_stat(ctl, 9, 1);
@@ -592,7 +489,6 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
                 done = true;
             } else {
                 if (STATS && lane == 0) mw_stat(ctl, 2, 1);
-                if (PLVI_MW_ORPHAN && S->ovf == 0) mw_unclaim(E, Q, n, lane);  // before the exact regrowth claims its own
                 mw_wave_sync();
                 if (lane == 0) mw_lds_store(&S->state, kMwFree);
             }
@@ -615,7 +511,7 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
             }
             mw_wave_sync();
             if (lane == 0) mw_lds_store(&ctl->ncommit, ctl->ncommit + 1);
-            // region2rect input for lsd_rect_kernel (flsd :500-518 order)
+            // region2rect input for lsd_rect_lanes_kernel (flsd :500-518 order)
             if (n >= min_reg) {
                 const int nout = ctl->nout, npts = ctl->npts;
                 if (nout < kLsdRawCap) {
@@ -633,15 +529,8 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
         }
         head = q + 1;
         if (lane == 0) {
-            if (PLVI_MW_WALKFAST) {
-                // one release for both (the slot / log reads above are done before either is seen)
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                __hip_atomic_store(&ctl->wptr, wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_store(&ctl->head, head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            } else {
-                mw_lds_store(&ctl->wptr, wp);  // frees log entries for the dispatchers as the walk goes
-                mw_lds_store(&ctl->head, head);
-            }
+            mw_lds_store(&ctl->wptr, wp);  // frees log entries for the dispatchers as the walk goes
+            mw_lds_store(&ctl->head, head);
         }
     }
     if (lane == 0) {
@@ -659,7 +548,7 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
 // dispatch log with its slot.  Returns the seed (-1: none) and the slot.
 template <bool STATS>
 __device__ __forceinline__ int mw_dispatch(const MwEnv& E, lds_u8* pool, int nslots, lds_i32* dlog, int& slot,
-                                           unsigned* hcur, unsigned ctag, int lane) {
+                                           int lane) {
     lds_ctl* ctl = E.ctl;
     const int nwords = E.sh * E.wpr;
     const int dn = mw_peek(&ctl->dlog_n);  // written under dlock only (held)
@@ -703,98 +592,17 @@ __device__ __forceinline__ int mw_dispatch(const MwEnv& E, lds_u8* pool, int nsl
         lds_slot* S = mw_slot(pool, slot);
         const int st0 = mw_peek(&S->state);
         if (STATS && st0 == kMwDone) mw_stat(ctl, 1, 1);  // a passed region, dropped
-        // a dropped region (or one left dead by revalidation) gives up its claims
-        // when the slot is reused (by the grower that took it, outside the lock)
-        S->dead = PLVI_MW_ORPHAN && (st0 == kMwDone || S->dead) && S->ovf == 0 ? 1 : 0;
         S->seed = q;
         S->ovf = 0;
         S->chk = mw_peek(&ctl->ncommit);
         mw_lds_store(&S->state, kMwGrowing);  // before the log entry that names it
         ctl->cursor = q + 1;
-        if (hcur) gstore_l2(hcur, ctag | (unsigned)q);  // where the helpers' work starts to pay (a hint)
         dlog[2 * (dn & (kMwLog - 1))] = q;
         dlog[2 * (dn & (kMwLog - 1)) + 1] = slot;
         mw_lds_store(&ctl->dlog_n, dn + 1);
         if (STATS) mw_stat(ctl, 0, 1);
     }
     return q;
-}
-
-// Second-chance dispatch (caller holds dlock): the first pixel at or after
-// the walk within kMwLateWords bitmap words that is neither committed /
-// NOTDEF nor trivial but claimed (H) and is no live slot's seed -- a seed the
-// cursor skipped because a region that was later dropped or regrown had
-// claimed it; the walker would grow it exactly.  It takes a free slot and a
-// free late-log entry (seed -1 or passed by the walk).  Returns the seed or -1.
-__device__ __forceinline__ int mw_second_chance(const MwEnv& E, lds_u8* pool, int nslots, int& slot, int lane) {
-    lds_ctl* ctl = E.ctl;
-    const int nwords = E.sh * E.wpr;
-    const int head = mw_lds_load(&ctl->head);
-    const int ls = lane < kMwLate ? mw_peek(&ctl->late_seed[lane]) : 0;
-    const unsigned long long lfree = __ballot(lane < kMwLate && ls < head);
-    if (!lfree) return -1;
-    const int le = __ffsll((long long)lfree) - 1;
-    slot = -1;
-    for (int b0 = 0; b0 < nslots && slot < 0; b0 += 64) {
-        const int si = b0 + lane;
-        bool ok = false;
-        if (si < nslots) {
-            lds_slot* S = mw_slot(pool, si);
-            const int st = mw_lds_load(&S->state);
-            ok = st == kMwFree || (st == kMwDone && S->seed < head);
-        }
-        const unsigned long long b = __ballot(ok);
-        if (b) slot = b0 + __ffsll((long long)b) - 1;
-    }
-    if (slot < 0) return -1;
-    const int w0 = head >> 5;
-    const int cur = ctl->cursor;  // under dlock
-    for (int wb = w0; wb < min(nwords, w0 + kMwLateWords); wb += 64) {
-        const int w = wb + lane;
-        unsigned m = 0;
-        if (w < nwords && w < w0 + kMwLateWords) {
-            if (PLVI_MW_ORPHAN) {
-                // orphans: passed by the cursor, now neither committed, trivial nor claimed
-                m = ~mw_peek(E.C + w) & ~E.T[w] & ~mw_peek(E.H + w);
-                if (w > (cur >> 5)) m = 0;
-                else if (w == (cur >> 5)) m &= (1u << (cur & 31)) - 1u;
-            } else {
-                m = ~mw_peek(E.C + w) & ~E.T[w] & mw_peek(E.H + w);
-            }
-            if (w == w0) m &= ~0u << (head & 31);
-        }
-        unsigned long long has = __ballot(m != 0u);
-        while (has) {
-            const int l = __ffsll((long long)has) - 1;
-            has &= has - 1;
-            unsigned mm = (unsigned)readlane_i((int)m, l);
-            while (mm) {
-                const int q = (wb + l) * 32 + (__ffs((int)mm) - 1);
-                mm &= mm - 1;
-                // no live slot holds it (a dispatched seed keeps its slot until the walk passes it)
-                bool live = false;
-                for (int b0 = 0; b0 < nslots; b0 += 64) {
-                    const int si = b0 + lane;
-                    if (si < nslots) {
-                        lds_slot* S = mw_slot(pool, si);
-                        live |= S->seed == q && mw_peek(&S->state) != kMwFree;
-                    }
-                }
-                if (__ballot(live)) continue;
-                if (lane == 0) {
-                    lds_slot* S = mw_slot(pool, slot);
-                    S->seed = q;
-                    S->ovf = 0;
-                    S->chk = mw_peek(&ctl->ncommit);
-                    mw_lds_store(&S->state, kMwGrowing);  // before the late entry that names it
-                    ctl->late_slot[le] = slot;
-                    mw_lds_store(&ctl->late_seed[le], q);
-                }
-                return q;
-            }
-        }
-    }
-    return -1;
 }
 
 // Copy region points [0, n) from queue A to queue B (one wave).
@@ -808,238 +616,19 @@ __device__ __forceinline__ void mw_copy_points(const MwQueue& A, const MwQueue& 
 }
 
 
-// ---------------------------------------------------------------------------
-// Helper workgroups.  Records and points of the regions a helper grew live in
-// global memory; the task's per-pixel map names the record of a seed.  Map
-// entries and the cursor hint carry the launch epoch, so no buffer is cleared
-// between launches (a stale entry fails the epoch or the record's seed check).
-struct MwHelpRec {
-    int seed, n, off;  // seed bit index, points, offset in the helper's point area
-    float deg;         // final region angle (float degrees)
-    unsigned epoch;
-    int pad[3];
-};
-// Compiled out by default: with up to 7 helpers per task the task's growers
-// import most regions (1 439 of 1 742 dispatched at one frame) but region
-// growing stays at 7.0-7.5 ms per frame and 8.6-10 ms per 64 frames -- the
-// walk's own chain (exact growth of invalidated and undispatched seeds,
-// ~7M of 18M cycles, plus the commits) bounds the kernel, not the growers
-// (profiles/r04/mw_helpers_ab.txt); compiled in, the extra kernel state
-// costs 1-2 % even with no helper launched.  PLVI_MW_HELPERS=1 builds it.
-#ifndef PLVI_MW_HELPERS
-#define PLVI_MW_HELPERS 0
-#endif
-constexpr int kMwHelpRecCap = 4096;  // records per helper workgroup (map ids: 16 bits, nHelp <= 15)
-constexpr int kMwHelpMax = 15;
-struct MwHelp {
-    unsigned* map;     // per task: bit index -> (epoch & 0xffff) << 16 | (k * kMwHelpRecCap + record + 1)
-    size_t mapTask;    // entries per task
-    MwHelpRec* rec;    // per helper workgroup: kMwHelpRecCap records
-    unsigned* pts;     // per helper workgroup: ptsCap points
-    unsigned* cur;     // per task: (epoch & 0xfff) << 20 | the task's dispatch cursor (a hint)
-    unsigned* own;     // per helper workgroup: NW own-mark spills (sh x wpr words each)
-    size_t ownWg;      // words per helper workgroup
-    unsigned* gq;      // per helper workgroup: NW growth-queue spills (kMwGSpill each)
-    int nHelp, nTp;    // helpers per task; tasks padded to a multiple of 8 (grid sections)
-    int ptsCap;
-    unsigned epoch;
-};
-
-// A grower of the task took seed q into slot si: import the region a helper
-// published for it, if any (agent-scope acquire after the map entry is seen).
-// The region was grown with an empty committed bitmap: chk = -1 sends it
-// through revalidation; the walker validates it like any other.
-__device__ __forceinline__ bool mw_import(const MwEnv& E, const MwHelp& Hp, int t, lds_u8* pool, unsigned* sspill,
-                                          int si, int q, int lane) {
-    const unsigned hv = gload_l2(Hp.map + (size_t)t * Hp.mapTask + q);
-    if ((hv >> 16) != (Hp.epoch & 0xffffu) || (hv & 0xffffu) == 0u) return false;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    const int g = (int)(hv & 0xffffu) - 1, k = g / kMwHelpRecCap, r = g - k * kMwHelpRecCap;
-    const size_t hwg = (size_t)k * Hp.nTp + t;
-    const MwHelpRec R = Hp.rec[hwg * kMwHelpRecCap + r];
-    if (R.seed != q || R.epoch != Hp.epoch || R.n > kMwSP + kMwSlotSpill) return false;
-    const unsigned* P = Hp.pts + hwg * Hp.ptsCap + R.off;
-    const MwQueue Q = mw_slot_queue(pool, sspill, si);
-    bool gl = false;
-    for (int j = lane; j < R.n; j += 64) {
-        const unsigned v = P[j];
-        mw_qput(Q, j, v);
-        mw_or(E.H, E.wpr, (int)(v & 0xffffu), (int)(v >> 16));  // claimed: the cursor skips seeds inside it
-        gl |= j >= Q.lcap;
-    }
-    if (__ballot(gl)) vm_drain();
-    if (lane == 0) {
-        lds_slot* S = mw_slot(pool, si);
-        S->n = R.n;
-        S->deg = R.deg;
-        S->ovf = 0;
-        S->chk = -1;
-    }
-    return true;
-}
-
-// Helper dispatch (caller holds the helper's lock): the next seed of the band
-// [cursor, yEnd) that is neither NOTDEF / trivial (T) nor inside a region this
-// helper grew (H); a cursor the task's own growers passed moves ahead of them.
-__device__ __forceinline__ int mw_help_dispatch(const MwEnv& E, int yEnd, const unsigned* hcur, unsigned ctag,
-                                                int lane) {
-    lds_ctl* ctl = E.ctl;
-    const int nwords = min(E.sh, yEnd) * E.wpr;
-    int cur = ctl->cursor;
-    const unsigned mc = gload_l2(const_cast<unsigned*>(hcur));
-    if ((mc & 0xfff00000u) == ctag && (int)(mc & 0xfffffu) + 2 * E.rowbits > cur)
-        cur = (int)(mc & 0xfffffu) + 2 * E.rowbits;  // two rows ahead of the task's cursor
-    int w = cur >> 5;
-    if (w >= nwords) return -1;
-    unsigned m = ~(E.T[w] | mw_peek(E.H + w)) & (~0u << (cur & 31));
-    if (!m) {
-        int found = -1;
-        for (int w0 = w + 1; w0 < nwords && found < 0; w0 += 64) {
-            const int ww = w0 + lane;
-            const bool nz = ww < nwords && (E.T[ww] | mw_peek(E.H + ww)) != ~0u;
-            const unsigned long long b = __ballot(nz);
-            if (b) found = w0 + __ffsll((long long)b) - 1;
-        }
-        if (found < 0) {
-            if (lane == 0) ctl->cursor = nwords * 32;
-            return -1;
-        }
-        w = found;
-        m = ~(E.T[w] | mw_peek(E.H + w));
-    }
-    const int q = w * 32 + (__ffs((int)m) - 1);
-    if (lane == 0) ctl->cursor = q + 1;
-    return q;
-}
-
-// A helper workgroup (NW grower waves): grows the seeds of its band and
-// publishes every region it completes.
-template <int NW, bool STATS>
-__device__ void mw_helper(const LineOctDev& od, const float* P, const float2* SC, double prec, const MwHelp& Hp, int k,
-                          int t, unsigned* lds_u) {
-    const int sw = od.sw, sh = od.sh, wpr = (sw + 31) >> 5;
-    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int y0 = sh * (k + 1) / (Hp.nHelp + 1), y1 = sh * (k + 2) / (Hp.nHelp + 1);
-    // LDS: ctl | T (NOTDEF or trivial) | H | own windows | growth queues
-    lds_ctl* ctl = (lds_ctl*)lds_u;
-    const int nwords = sh * wpr;
-    lds_u32* T = (lds_u32*)(lds_u + sizeof(MwCtl) / 4);
-    lds_u32* H = T + nwords;
-    lds_u32* ownAll = H + nwords;
-    lds_u32* gqAll = ownAll + NW * kMwRB * wpr;
-    const size_t hwg = (size_t)k * Hp.nTp + t;
-    MwEnv E;
-    E.P = P;
-    E.SC = SC;
-    E.C = nullptr;
-    E.T = T;
-    E.H = H;
-    E.own = ownAll + wv * kMwRB * wpr;
-    E.ownG = Hp.own + hwg * Hp.ownWg + (size_t)wv * sh * wpr;
-    E.ctl = ctl;
-    E.sw = sw; E.sh = sh; E.wpr = wpr; E.rowbits = wpr * 32;
-    E.pdeg = (float)(prec / kD2R);
-    E.prec = prec;
-    const MwQueue GQ{gqAll + wv * kMwGQ, kMwGQ, Hp.gq + (hwg * NW + wv) * kMwGSpill, kMwGSpill};
-    const unsigned ctag = (Hp.epoch & 0xfffu) << 20;
-    const unsigned* hcur = Hp.cur + t;
-    const float pdeg = E.pdeg;
-    const int min_reg = od.min_reg_size;
-    for (int i = threadIdx.x; i < 2 * nwords; i += NW * 64) T[i] = i < nwords ? ~0u : 0u;  // T outside the band: no seed
-    for (int i = threadIdx.x; i < NW * kMwRB * wpr; i += NW * 64) ownAll[i] = 0u;
-    if (threadIdx.x == 0) {
-        ctl->lock = ctl->dlock = 0;
-        ctl->cursor = y0 * E.rowbits;
-        ctl->npts = ctl->nout = 0;
-        for (int i = 0; i < 16; ++i) ctl->stat[i] = 0;
-    }
-    __syncthreads();
-    // T over the band (the task's C | T set-up restricted to its rows)
-    for (int kk = wv; kk < (y1 - y0) * ((wpr + 1) >> 1); kk += NW) {
-        const int y = y0 + kk / ((wpr + 1) >> 1), xb = (kk - (y - y0) * ((wpr + 1) >> 1)) * 64;
-        const int x = xb + lane;
-        const float* r0 = P + (size_t)y * sw;
-        float d0 = kNotdefF, dr = kNotdefF, dbl = kNotdefF, db = kNotdefF, dbr = kNotdefF;
-        if (x < sw) {
-            d0 = r0[x];
-            if (x + 1 < sw) dr = r0[x + 1];
-            if (y + 1 < sh) {
-                const float* r1 = r0 + sw;
-                if (x > 0) dbl = r1[x - 1];
-                db = r1[x];
-                if (x + 1 < sw) dbr = r1[x + 1];
-            }
-        }
-        const bool def = x < sw && d0 != kNotdefF;
-        const bool grows = is_aligned_fast(dr, d0, pdeg, prec) || is_aligned_fast(dbl, d0, pdeg, prec) ||
-                           is_aligned_fast(db, d0, pdeg, prec) || is_aligned_fast(dbr, d0, pdeg, prec);
-        const unsigned long long tm = __ballot(!def || (!grows && min_reg > 1));
-        if (lane < 2 && (xb >> 5) + lane < wpr) T[y * wpr + (xb >> 5) + lane] = lane == 0 ? (unsigned)tm : (unsigned)(tm >> 32);
-    }
-    __syncthreads();
-    unsigned* map = Hp.map + (size_t)t * Hp.mapTask;
-    while (true) {
-        int q = -1;
-        while (true) {  // the lock (no other work to do meanwhile)
-            if (mw_try_lock(&ctl->dlock, lane)) {
-                q = mw_help_dispatch(E, y1, hcur, ctag, lane);
-                mw_unlock(&ctl->dlock, lane);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        if (q < 0) break;
-        int n = 0;
-        float deg = 0.f;
-        bool spilled = false;
-        const int rc = mw_grow<false, STATS, true>(E, q % E.rowbits, q / E.rowbits, GQ, n, deg, spilled, lane);
-        int r = 0, off = 0;
-        if (rc == 0 && lane == 0) {
-            r = __hip_atomic_fetch_add(&ctl->nout, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            off = __hip_atomic_fetch_add(&ctl->npts, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        r = __builtin_amdgcn_readfirstlane(r);
-        off = __builtin_amdgcn_readfirstlane(off);
-        if (rc == 0 && r < kMwHelpRecCap && off + n <= Hp.ptsCap) {
-            unsigned* dst = Hp.pts + hwg * Hp.ptsCap + off;
-            for (int j = lane; j < n; j += 64) dst[j] = mw_qget(GQ, j);
-            if (lane == 0) Hp.rec[hwg * kMwHelpRecCap + r] = MwHelpRec{q, n, off, deg, Hp.epoch, {0, 0, 0}};
-            // publish: this wave's stores, then an agent-scope release, then the map entry
-            __builtin_amdgcn_s_waitcnt(0);
-            if (lane == 0) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(map + q, ((Hp.epoch & 0xffffu) << 16) | (unsigned)(k * kMwHelpRecCap + r + 1),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        mw_own_clear(E, q / E.rowbits, GQ, n, spilled, lane);
-    }
-}
-
 template <int NW, bool STATS>
 __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
     const LineOctDev* __restrict__ octs, const float* __restrict__ pix, const float2* __restrict__ pixcs,
     unsigned* __restrict__ ownspill, size_t ownspill_task, unsigned* __restrict__ gspill, unsigned* __restrict__ slotspill,
     unsigned* __restrict__ xspill, size_t xspill_task, double prec, LsdRegion* __restrict__ regs,
     unsigned* __restrict__ regpts, size_t regpts_frame, int* __restrict__ nlines, int* __restrict__ err, int nslots,
-    int nOct, int oBase, int oCount, int* __restrict__ stats, int nf, MwHelp Hp) {
+    int nOct, int oBase, int oCount, int* __restrict__ stats, int nf) {
     extern __shared__ __align__(16) unsigned lds_u[];
     __builtin_amdgcn_s_setprio(PLVI_GROW_SETPRIO);
-    // grid: nHelp + 1 sections of nTp blocks (tasks padded to a multiple of 8,
-    // so that a task's helpers share its XCD when blocks are dealt round-robin
-    // over the XCDs); section 0 = the tasks, section k + 1 = helper k
-    const int sec = blockIdx.x / Hp.nTp, t = blockIdx.x - sec * Hp.nTp;
+    const int t = blockIdx.x;
     if (t >= nf * oCount) return;
     const int o = oBase + t / nf, f = t - (o - oBase) * nf;
     const int task = f * nOct + o;
-    if (PLVI_MW_HELPERS && sec > 0) {
-        const LineOctDev& hod = octs[o];
-        __builtin_amdgcn_s_setprio(PLVI_MW_GROWER_PRIO);
-        mw_helper<NW, STATS>(hod, pix + hod.soff + (size_t)f * hod.splane, pixcs + hod.soff + (size_t)f * hod.splane,
-                             prec, Hp, sec - 1, t, lds_u);
-        return;
-    }
     const LineOctDev& od = octs[o];
     const int sw = od.sw, sh = od.sh, wpr = (sw + 31) >> 5;
     // the wave index read uniformly: the role (walker / grower) and this wave's
@@ -1074,10 +663,6 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
                                          gspill + ((size_t)task * NW + wv) * kMwGSpill, kMwGSpill};
     LsdRegion* outR = regs + (size_t)task * kLsdRawCap;
     unsigned* outP = regpts + (size_t)task * regpts_frame;
-    // helpers of this task: the dispatch cursor hint and the first seed of their bands
-    unsigned* hcur = PLVI_MW_HELPERS && Hp.nHelp > 0 ? Hp.cur + t : nullptr;
-    const unsigned ctag = (Hp.epoch & 0xfffu) << 20;
-    const int helpStart = (sh / (Hp.nHelp + 1)) * E.rowbits;
 
     const unsigned long long t_kernel = STATS ? __builtin_amdgcn_s_memtime() : 0;
     // ---- init: C = NOTDEF (and row padding), T = trivial seeds, H = 0
@@ -1119,13 +704,11 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
         mw_slot(pool, k)->seed = -1;
         mw_slot(pool, k)->n = 0;
         mw_slot(pool, k)->ovf = 0;
-        mw_slot(pool, k)->dead = 0;
     }
     if (threadIdx.x == 0) {
         ctl->lock = ctl->dlock = ctl->head = ctl->cursor = ctl->finished = 0;
         ctl->npts = ctl->nout = ctl->overflow = 0;
         ctl->dlog_n = ctl->wptr = ctl->ncommit = 0;
-        for (int i = 0; i < kMwLate; ++i) ctl->late_seed[i] = -1;
         for (int i = 0; i < 16; ++i) ctl->stat[i] = 0;
     }
     __syncthreads();
@@ -1213,14 +796,12 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
                     int nst = kMwDone;
                     if (mw_bit(E.C, E.wpr, sx, sy)) {
                         nst = kMwFree;  // the seed itself was taken: the walk never visits it
-                        if (lane == 0) S->dead = PLVI_MW_ORPHAN && S->ovf == 0 ? 1 : 0;
                     } else if (__ballot(bad) == 0ull) {
                         if (lane == 0) S->chk = nc0;
                     } else {
                         int n = 0;
                         float deg = 0.f;
                         bool spilled = false;
-                        if (PLVI_MW_ORPHAN && S->ovf == 0) mw_unclaim(E, Q, n0, lane);
                         const unsigned long long ts0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
                         int rc = mw_grow<true, STATS>(E, sx, sy, GQ, n, deg, spilled, lane);
                         mw_own_clear(E, sy, GQ, n, spilled, lane);
@@ -1245,30 +826,11 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
             // a new speculative region
             int q = -1, si = -1;
             if (mw_try_lock(&ctl->dlock, lane)) {
-                q = mw_dispatch<STATS>(E, pool, nslots, dlog, si, hcur, ctag, lane);
-                mw_unlock(&ctl->dlock, lane);
-            }
-            if (q < 0 && kMwLate > 0 && mw_try_lock(&ctl->dlock, lane)) {
-                q = mw_second_chance(E, pool, nslots, si, lane);
+                q = mw_dispatch<STATS>(E, pool, nslots, dlog, si, lane);
                 mw_unlock(&ctl->dlock, lane);
             }
             if (q < 0) {
                 __builtin_amdgcn_s_sleep(2);
-                continue;
-            }
-            if (PLVI_MW_ORPHAN) {
-                lds_slot* S0 = mw_slot(pool, si);
-                if (__builtin_amdgcn_readfirstlane(S0->dead)) {
-                    mw_unclaim(E, mw_slot_queue(pool, sspill, si), S0->n, lane);
-                    mw_wave_sync();
-                    if (lane == 0) S0->dead = 0;
-                }
-            }
-            // a region a helper already grew for this seed
-            if (hcur && q >= helpStart && mw_import(E, Hp, t, pool, sspill, si, q, lane)) {
-                if (STATS && lane == 0) mw_stat(ctl, 12, 1);
-                mw_wave_sync();
-                if (lane == 0) mw_lds_store(&mw_slot(pool, si)->state, kMwDone);
                 continue;
             }
             int n = 0;

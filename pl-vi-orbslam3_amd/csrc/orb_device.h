@@ -40,18 +40,13 @@ struct OrbLevelDev {
     int rootB[kOrbMaxRoots + 1];   // membership: root i holds x in [rootB[i], rootB[i+1])
     double rsx, rsy;               // cv::resize scale_x / scale_y from level l-1 (1 / ((double)dw / sw))
     int xtab;                      // offset of this level's packed column table (orb_pyramid_kernel)
-    int thrOff;                    // byte offset of this level's cell thresholds in a frame's table
 };
 
-// One strip of a level for the blur + FAST (+ NMS) kernel: output columns
-// [x0, x1), rows [y0, y1).  Lane L holds the four columns (x0 & ~3) - 4 + 4L
-// .. +3 (x1 - (x0 & ~3) <= kBfCols).  Strips are cut at cell boundaries, so
-// every FAST detection window (cell) of the level lies inside one strip: the
-// strip holds cell columns [cj0, cj0 + ncj) and rows [ci0, ci0 + nci)
-// (ncj * nci <= 64).
+// One strip of a level for the blur + FAST kernel: output columns [x0, x1),
+// rows [y0, y1).  Lane L holds the four columns (x0 & ~3) - 4 + 4L .. +3
+// (x1 - (x0 & ~3) <= kBfCols).  Strips are cut at kBfAlign-aligned columns.
 struct OrbStripDev {
     int level, x0, x1, y0, y1;
-    int cj0, ncj, ci0, nci;
 };
 
 struct OrbCellDev {

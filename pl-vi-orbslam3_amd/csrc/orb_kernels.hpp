@@ -276,34 +276,18 @@ __global__ __launch_bounds__(64 * (kPyrFrames + 1)) __attribute__((amdgpu_waves_
 // T) rejects ~90 % of pixels; survivors are queued (row, column) and scored
 // 64 at a time from an LDS ring of the last 32 raw rows.
 // ---------------------------------------------------------------------------
-// PLVI_BF_LEAN (default): a 16-row ring and 16-bit queue entries (row modulo
-// 256: queued rows are never 256 rows old), 4.6 KB of LDS and <= 64 VGPRs, so 8
-// waves fit a SIMD and the launch can share CUs with region growing
-#ifndef PLVI_BF_LEAN
-#define PLVI_BF_LEAN 1
-#endif
-// PLVI_BF_NMS=1: the per-cell NMS + threshold fallback inside this kernel
-// (bit-exact, but 8.8 vs 6.0 + 2.8 ms per 3072 frames at 3 instead of 8
-// waves per SIMD -- 13 KB of LDS -- and a slower step); the
-// default keeps the score plane + orb_cell_nms_kernel
-#ifndef PLVI_BF_NMS
-#define PLVI_BF_NMS 0
-#endif
-#ifndef PLVI_BF_PK
-#define PLVI_BF_PK 1  // candidates scored two per lane with packed 16-bit min / max (128 per flush)
-#endif
-constexpr int kBfFlush = PLVI_BF_PK ? 128 : 64;  // candidates scored per flush
+// A 16-row ring and 16-bit queue entries (row modulo 256: queued rows are
+// never 256 rows old), 4.6 KB of LDS and <= 64 VGPRs, so 8 waves fit a SIMD
+// and the launch can share CUs with region growing.  (The per-cell NMS folded
+// into this kernel was bit-exact but slower at 13 KB of LDS, DESIGN.md §4;
+// r05 removed it.)
+constexpr int kBfFlush = 1 ? 128 : 64;  // candidates scored per flush
 // ring rows 0..5 are mirrored after row kRingRows - 1, so the 7 rows around
 // any ring row are contiguous and a candidate's 17 taps are one base address
 // plus immediate offsets (no per-tap wrap arithmetic)
-constexpr int kRingMirror = PLVI_BF_PK ? 6 : 0;
-constexpr int kBfCols = 244, kBfRowsMax = 160, kBfRowsPlain = 128, kRingRows = PLVI_BF_LEAN ? 16 : 32, kRingW = 256,
+constexpr int kRingMirror = 1 ? 6 : 0;
+constexpr int kBfCols = 244, kBfRowsPlain = 128, kRingRows = 16, kRingW = 256,
               kBfQCap = kBfFlush - 1 + 256 + 1;  // a row adds <= 256 candidates to < kBfFlush queued
-constexpr int kOrbCellsLevelMax = 1280;           // nRows * nCols of a level (LDS of the SAT kernel)
-// fused NMS: scores of the last kSRows output rows, the scored candidates
-// (score >= threshold) awaiting their NMS test as a ring of kNmsCap entries
-constexpr int kSRows = 16, kNmsCap = 1024;
-constexpr unsigned kCellIn = 0x80u, kEdgeHi = 0x40u, kEdgeLo = 0x20u;  // colinf / rowinf bits (low 5: local cell)
 
 // bound_ctrl: the lane past the wave's edge reads 0 without an `old` operand
 // (update_dpp(0, ...) costs a v_mov of the zero per shift)
@@ -429,38 +413,6 @@ __device__ __forceinline__ s16x2 fast_S_ring2(const uint8_t (*rg)[kRingW], int y
     return __builtin_elementwise_max(A, -Bm);
 }
 
-// FAST detection window along one axis (ORBextractor.cc:787-806): cell k
-// starts at minB + k*cell, its window is [start+3, min(start+cell+6, maxB)-3),
-// and cells with start >= maxB - skip do not exist (6 for columns, 3 for
-// rows).  Returns kCellIn | edge bits | (k - k0) for a coordinate inside a
-// window, 0 otherwise.
-__device__ __forceinline__ unsigned orb_cell_axis(int v, int minB, int cell, int n, int maxB, int skip, int k0) {
-    const int r = v - minB - 3;
-    if (r < 0) return 0u;
-    const int k = r / cell;
-    if (k >= n) return 0u;
-    const int start = minB + k * cell;
-    if (start >= maxB - skip) return 0u;
-    const int lo = start + 3, hi = min(start + cell + 6, maxB) - 3;
-    if (v >= hi) return 0u;
-    return kCellIn | ((unsigned)(k - k0) & 31u) | (v == lo ? kEdgeLo : 0u) | (v == hi - 1 ? kEdgeHi : 0u);
-}
-
-// PLVI_BF_NMS (default): the strip also runs K2, the per-cell FAST non-max
-// suppression with the iniThFAST -> minThFAST fallback (ORBextractor.cc:
-// 808-829; cv::FAST's NMS is local to the cell ROI).  Strips are
-// cut at cell boundaries, so a cell's whole detection window is scored by one
-// wave.  Scores go to an LDS ring of the last kSRows output rows instead of a
-// score plane; every scored candidate at or above threshold is queued for its
-// NMS test, which runs once the rows above and below it are final: a
-// candidate survives iff its score beats the raw scores of its 8 neighbours
-// inside the cell's window (a neighbour below threshold is below the
-// candidate anyway, so one test serves both thresholds).  Survivors (score >=
-// min(ini, min)) are written to the candidate plane, which the strip writes
-// densely (zero dwords, then survivors: wave-ordered), and each cell's
-// threshold -- iniThFAST if it has a survivor there, else minThFAST -- goes to
-// the per-frame cell table that the SAT and node-argmax kernels apply.  The
-// score plane, its zero fill and the NMS launch disappear.
 #ifndef PLVI_BF_WPE
 #define PLVI_BF_WPE 1  // waves per EU blur + FAST is compiled for (1: no cap)
 #endif
@@ -474,20 +426,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PLVI_BF_WPE)
                                                            const uint8_t* __restrict__ frames, size_t f_frame,
                                                            size_t f_row, uint8_t* __restrict__ pyr,
                                                            uint8_t* __restrict__ blur, uint8_t* __restrict__ score,
-                                                           uint8_t* __restrict__ cthr, int thrFrame, int k0, int k1,
+                                                           int k0, int k1,
                                                            int k2, int k3, int tmin, int t1, int t2, int nstrips,
                                                            int nf) {
     if (PLVI_BF_SETPRIO) __builtin_amdgcn_s_setprio(PLVI_BF_SETPRIO);
     else PLVI_ORB_PRIO_SET();
-    static_assert(!PLVI_BF_NMS || PLVI_BF_PK, "the fused NMS queues from the packed scorer");
-    typedef typename std::conditional<PLVI_BF_LEAN != 0, unsigned short, unsigned>::type QT;
+    typedef unsigned short QT;
     __shared__ __align__(16) uint8_t ring[kRingRows + kRingMirror][kRingW];
     __shared__ QT q[kBfQCap];
-#if PLVI_BF_NMS
-    __shared__ __align__(16) uint8_t sring[kSRows][kRingW];  // scores (Sv - 1 or 0) of the last kSRows output rows
-    __shared__ QT nmsq[kNmsCap];                              // scored candidates awaiting NMS (ring, row order)
-    __shared__ uint8_t colinf[kRingW], rowinf[kBfRowsMax];
-#endif
     // XCD-affine mapping: blocks b and b + 8 share an XCD (and its L2), so
     // every strip of a frame goes to one XCD and the rows / columns two
     // strips share are fetched from HBM once
@@ -512,30 +458,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PLVI_BF_WPE)
     const size_t srow = sd.level == 0 ? f_row : (size_t)w;
     uint8_t* Dp = pyr + L.off + (size_t)f * L.plane;
     uint8_t* Bp = blur + L.boff + (size_t)f * L.bplane;
-    uint8_t* Sp = score + L.boff + (size_t)f * L.bplane;  // the candidate plane when PLVI_BF_NMS
+    uint8_t* Sp = score + L.boff + (size_t)f * L.bplane;
     const int bw = L.bpitch;
     const int T = max(tmin + 1, 1);
     const int y0 = sd.y0, y1 = sd.y1;
     unsigned fastok = 0;  // pixel j may be a FAST candidate
-#if PLVI_BF_NMS
-    const int maxBX = L.minB + L.rw, maxBY = L.minB + L.rh;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const unsigned ci = orb_cell_axis(c0 + j, L.minB, L.wCell, L.nCols, maxBX, 6, sd.cj0);
-        colinf[4 * lane + j] = (uint8_t)ci;
-        if (((omask >> j) & 1u) && (ci & kCellIn)) fastok |= 1u << j;  // only pixels of a detection window
-    }
-    for (int r = lane; r < y1 - y0; r += 64)
-        rowinf[r] = (uint8_t)orb_cell_axis(y0 + r, L.minB, L.hCell, L.nRows, maxBY, 3, sd.ci0);
-    int nh = 0, nt = 0;             // NMS queue head / tail (wave-uniform)
-    unsigned long long myt1 = 0;    // cells (local index) with a survivor >= iniThFAST
-    int ydone = y0 - 1;             // last output row whose candidates are all queued
-    wave_sync();
-#else
 #pragma unroll
     for (int j = 0; j < 4; ++j)
         if (((omask >> j) & 1u) && c0 + j >= 3 && c0 + j < w - 3) fastok |= 1u << j;
-#endif
     // rows r-6..r as even bytes (columns c0, c0+2) and odd bytes (c0+1, c0+3) in 16-bit fields
     uint32_t pe[7] = {0, 0, 0, 0, 0, 0, 0}, po[7] = {0, 0, 0, 0, 0, 0, 0};
     const uint32_t kt[7] = {(uint32_t)k0, (uint32_t)k1, (uint32_t)k2, (uint32_t)k3,
@@ -548,45 +478,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PLVI_BF_WPE)
         yy = yref - (int)((((unsigned)yref & 255u) - (e >> 8)) & 255u);
         rc = (int)(e & 255u);
     };
-#if PLVI_BF_NMS
-    // NMS of the queued scored candidates in rows <= lim (a prefix: the queue
-    // is in row order); yref >= every queued row
-    auto drain = [&](int lim, int yref) {
-        wave_sync();  // the flush's sring scores
-        while (nt - nh > 0) {
-            const int idx = nh + lane;
-            int yy = 0, rc = 0;
-            if (idx < nt) ent(nmsq[idx & (kNmsCap - 1)], yref, yy, rc);
-            const bool el = idx < nt && yy <= lim;
-            const unsigned long long E = __ballot(el);
-            if (el) {
-                const int rr = yy & (kSRows - 1), ru = (yy - 1) & (kSRows - 1), rd = (yy + 1) & (kSRows - 1);
-                const unsigned ci = colinf[rc], ri = rowinf[yy - y0];
-                const int s = sring[rr][rc];
-                const bool hl = !(ci & kEdgeLo), hr = !(ci & kEdgeHi);
-                int m = max(hl ? (int)sring[rr][rc - 1] : 0, hr ? (int)sring[rr][rc + 1] : 0);
-                if (!(ri & kEdgeLo))
-                    m = max(m, max((int)sring[ru][rc], max(hl ? (int)sring[ru][rc - 1] : 0, hr ? (int)sring[ru][rc + 1] : 0)));
-                if (!(ri & kEdgeHi))
-                    m = max(m, max((int)sring[rd][rc], max(hl ? (int)sring[rd][rc - 1] : 0, hr ? (int)sring[rd][rc + 1] : 0)));
-                if (s > m) {
-                    Sp[(size_t)yy * bw + (ax - 4 + rc)] = (uint8_t)s;  // after the row's zero dword (wave order)
-                    if (s >= t1) myt1 |= 1ull << (((ri & 31u) * (unsigned)sd.ncj + (ci & 31u)) & 63u);
-                }
-            }
-            const int ne = __popcll(E);
-            nh += ne;
-            if (ne < 64) break;
-        }
-    };
-#endif
     auto flush = [&](int n, int ycur) {  // score the first n (<= kBfFlush) queued candidates (ycur: newest queued row)
         // one wave per block: wave-scope ordering only (no store drain).  The
         // candidate bytes below land after this wave's earlier zero stores of
         // the same pixels: a wavefront observes its own memory operations in
         // program order (wavefront-scope acquire/release needs no waits).
         wave_sync();
-#if PLVI_BF_PK
         int sva = 0, svb = 0;
         const bool hasb = lane + 64 < n;
         if (lane < n) {
@@ -596,32 +493,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PLVI_BF_WPE)
             const s16x2 sv2 = fast_S_ring2(ring, ya, ca, yb, cb);
             sva = (int)sv2.x;
             svb = (int)sv2.y;
-#if PLVI_BF_NMS
-            sring[ya & (kSRows - 1)][ca] = (uint8_t)(sva >= T ? sva - 1 : 0);
-            if (hasb) sring[yb & (kSRows - 1)][cb] = (uint8_t)(svb >= T ? svb - 1 : 0);
-#else
             Sp[(size_t)ya * bw + (ax - 4 + ca)] = (uint8_t)(sva >= T ? sva - 1 : 0);
             if (hasb) Sp[(size_t)yb * bw + (ax - 4 + cb)] = (uint8_t)(svb >= T ? svb - 1 : 0);
-#endif
         }
-#if PLVI_BF_NMS
-        {
-            // candidates at or above threshold join the NMS queue in queue (= row) order
-            const bool va = lane < n && sva >= T, vb = lane < n && hasb && svb >= T;
-            const unsigned long long Ba = __ballot(va), Bb = __ballot(vb);
-            if (va) nmsq[(nt + orb_mbcnt(Ba)) & (kNmsCap - 1)] = q[lane];
-            if (vb) nmsq[(nt + __popcll(Ba) + orb_mbcnt(Bb)) & (kNmsCap - 1)] = q[lane + 64];
-            nt += __popcll(Ba) + __popcll(Bb);
-        }
-#endif
-#else
-        if (lane < n) {
-            int yy, rc;
-            ent(q[lane], ycur, yy, rc);
-            const int sv = fast_S_ring(ring, yy, rc);
-            Sp[(size_t)yy * bw + (ax - 4 + rc)] = (uint8_t)(sv >= T ? sv - 1 : 0);
-        }
-#endif
         wave_sync();
         const int rest = nq - n;
         constexpr int kMove = (kBfQCap - kBfFlush + 63) / 64;  // rest < kBfQCap - kBfFlush + 1 entries
@@ -635,11 +509,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PLVI_BF_WPE)
         nq = rest;
         wave_sync();
         oldest = rest > 0 ? ycur - (int)((((unsigned)ycur & 255u) - ((unsigned)q[0] >> 8)) & 255u) : 0;
-#if PLVI_BF_NMS
-        // rows before the oldest still-queued candidate are final: an entry
-        // can be tested once the row below it is
-        drain(rest > 0 ? oldest - 2 : ydone - 1, ydone);
-#endif
     };
     // rows rb..rb+7 of the source (reflected), four columns per lane
     auto load_rows = [&](int rb, uint32_t* pv) {
@@ -668,9 +537,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PLVI_BF_WPE)
         // zeroes output rows up to rb+4, i.e. rows <= rb+4-kSRows: after this
         // every queued or NMS-pending row is >= rb-6.)
         if (nq > 0 && oldest - 3 < rb - (kRingRows - 8)) flush(nq, ynew);
-#if PLVI_BF_NMS
-        else if (nq == 0 && nt > nh) drain(ydone - 1, ydone);  // rows without candidates since the last flush
-#endif
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const int rr = (rb + k) & (kRingRows - 1);
@@ -739,12 +605,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PLVI_BF_WPE)
                 candm |= ((m & 0xffffu) >= (unsigned)T ? 1u : 0u) << e;
                 candm |= ((m >> 16) >= (unsigned)T ? 4u : 0u) << e;
             }
-#if PLVI_BF_NMS
-            if (!(rowinf[y - y0] & kCellIn)) candm = 0;  // only rows of a detection window
-            *reinterpret_cast<uint32_t*>(&sring[y & (kSRows - 1)][4 * lane]) = 0u;  // scores land by flush
-#else
             if (!(y >= 3 && y < h - 3)) candm = 0;
-#endif
             candm &= fastok;
             if (outl) {
                 const uint32_t o = (uint32_t)(y * w + c0), ob = (uint32_t)(y * bw + c0);
@@ -762,7 +623,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PLVI_BF_WPE)
                 }
             }
             const int nq0 = nq;
-#if PLVI_BF_PK
             {
                 // lane-major queue order: the lane's candidate count (0..4) as three
                 // ballot bit planes gives every lane its exclusive prefix with mbcnt
@@ -777,35 +637,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PLVI_BF_WPE)
                     nq += __popcll(B0) + 2 * __popcll(B1) + 4 * __popcll(B2);
                 }
             }
-#else
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const bool cj = (candm >> j) & 1u;
-                const unsigned long long m = __ballot(cj);
-                if (cj) q[nq + __popcll(m & ((1ull << lane) - 1ull))] = (QT)(((unsigned)y & 255u) << 8 | (unsigned)(4 * lane + j));
-                nq += __popcll(m);
-            }
-#endif
             if (nq0 == 0 && nq > 0) oldest = y;
             if (nq > nq0) ynew = y;
-#if PLVI_BF_NMS
-            ydone = y;
-#endif
             while (nq >= kBfFlush) flush(kBfFlush, ynew);
         }
     }
     while (nq > 0) flush(min(nq, kBfFlush), ynew);
-#if PLVI_BF_NMS
-    drain(INT_MAX, ydone);
-    // the strip's cells: iniThFAST where a survivor reached it, else minThFAST
-    unsigned long long m1 = myt1;
-    for (int o = 32; o > 0; o >>= 1) m1 |= __shfl_xor(m1, o);
-    if (lane < sd.ncj * sd.nci) {
-        const int il = lane / sd.ncj, jl = lane - il * sd.ncj;
-        cthr[(size_t)f * thrFrame + L.thrOff + (sd.ci0 + il) * L.nCols + sd.cj0 + jl] =
-            (uint8_t)(((m1 >> lane) & 1ull) ? t1 : t2);
-    }
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -815,48 +652,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PLVI_BF_WPE)
 // cell's detection window count as 0 (cv::FAST on the cell ROI), a
 // neighbour below the threshold counts as 0, and a survivor is strictly
 // greater than all 8 (A.3).
-// One wave per (cell, frame), lane = window column (windows are < 64 wide):
-// the window is staged column-per-lane in LDS, each row's 8 neighbours come
-// from the rows above / below and DPP lane shifts, and both thresholds are
-// decided in the same sweep, so there is no per-pixel index arithmetic.
+// One wave per (cell, frame), lane = window column (windows are < 64 wide),
+// each row's 8 neighbours from the rows above / below and DPP lane shifts.
 // ---------------------------------------------------------------------------
-constexpr int kNmsRows = 64;  // >= window height (hCell <= 58, orb_pipeline.hip plan checks)
-#ifndef PLVI_NMS_MAXONLY
-#define PLVI_NMS_MAXONLY 1  // one strict-local-max sweep, survivors-only writes (0: both thresholds per row)
-#endif
-#ifndef PLVI_NMS_STREAM
-#define PLVI_NMS_STREAM 1  // rows streamed through registers, no LDS (0: the window staged in LDS)
-#endif
-#ifndef PLVI_NMS_DENSE
-// 1: the NMS writes its whole window, zeros included (no fill needed).  Off:
-// 4.7 vs 2.8 ms for the stage at B = 3072, 41K vs 44K FPS (column-per-lane
-// byte stores of every window row cost more than the sparse survivors)
-#define PLVI_NMS_DENSE 0
-#endif
-#ifndef PLVI_NMS_CLEAR
-// Consume and clear: orb_node_best_kernel, the last reader of the candidate
-// plane, zeroes each candidate it reads (the octree's membership rectangles
-// cover every candidate of a level; on an octree overflow the octree kernel
-// zeroes the level's region), so the NMS writes survivors only onto a plane
-// that is already zero and the per-launch fill of the plane goes away
-#define PLVI_NMS_CLEAR 1
-#endif
-
 __device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, const OrbLevelDev* __restrict__ lvs,
                                              const uint8_t* __restrict__ score, uint8_t* __restrict__ cand, int t1,
-                                             int t2, uint8_t* sv) {
+                                             int t2) {
     const OrbLevelDev& L = lvs[c.level];
     const int ww = c.x1 - c.x0, wh = c.y1 - c.y0, w = L.bpitch;
     const int lane = threadIdx.x;
     const bool incol = lane < ww;
     const size_t base = L.boff + (size_t)f * L.bplane + (size_t)c.y0 * w + c.x0 + lane;
     const uint8_t* S = score + base;
-#if PLVI_NMS_MAXONLY && PLVI_NMS_STREAM
     // Register streaming, no LDS: rows come straight from the score plane,
     // eight in flight (the next chunk is loaded while this one is swept), so
     // the kernel occupies no LDS next to the region-growing waves it runs
     // with; survivors are re-read from the (L2-resident) plane when written.
-    (void)sv;
     unsigned long long ka = 0, kb = 0;
     {
         auto ld = [&](int r) -> int { return (incol && r < wh) ? (int)S[(size_t)r * w] : 0; };
@@ -898,100 +709,10 @@ __device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, co
     const unsigned long long keep = __ballot(ka != 0ull) != 0ull ? ka : kb;
     if (!incol) return;
     uint8_t* C = cand + base;
-#if PLVI_NMS_DENSE
-    // the whole window, zeros included: the candidate plane needs no fill
-    // before the launch (pixels outside every window stay 0 from the init)
-    for (int r = 0; r < wh; ++r) C[(size_t)r * w] = ((keep >> r) & 1ull) ? S[(size_t)r * w] : (uint8_t)0;
-#else
     for (unsigned long long kk = keep; kk; kk &= kk - 1) {
         const int r = __ffsll((long long)kk) - 1;
         C[(size_t)r * w] = S[(size_t)r * w];
     }
-#endif
-#else
-    // stage the window column-per-lane (rows beyond wh and lanes beyond ww hold 0)
-    for (int r0 = 0; r0 < wh; r0 += 8) {
-        uint8_t v[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = (incol && r0 + k < wh) ? S[(size_t)(r0 + k) * w] : (uint8_t)0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) sv[(r0 + k) * 64 + lane] = v[k];
-    }
-    sv[wh * 64 + lane] = 0;  // row wh (wh < kNmsRows) is the bottom neighbour of the last row
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-#if PLVI_NMS_MAXONLY
-    // A pixel at or above threshold t survives iff its score is strictly
-    // greater than all 8 RAW neighbour scores: a neighbour below t counts as 0
-    // in the reference's buffer but is then below the pixel's score anyway,
-    // and one at or above t is compared as it is.  So one sweep finds the
-    // strict local maxima (s > 0) and the thresholds only filter the pixel
-    // itself; the cand plane is zeroed beforehand, only survivors are written.
-    unsigned long long ka = 0, kb = 0;
-    {
-        int s = sv[lane];
-        int hp = 0;  // max over columns c-1..c+1 of row r-1
-        int hc = max(s, max(lane_from_left(s), lane_from_right(s)));
-        int lr = max(lane_from_left(s), lane_from_right(s));
-        for (int r = 0; r < wh; ++r) {
-            const int sn = sv[(r + 1) * 64 + lane];
-            const int lrn = max(lane_from_left(sn), lane_from_right(sn));
-            const int hn = max(sn, lrn);
-            const int m = max(max(hp, hn), lr);
-            if (s > m) {
-                if (s >= t1) ka |= 1ull << r;
-                if (s >= t2) kb |= 1ull << r;
-            }
-            hp = hc;
-            hc = hn;
-            lr = lrn;
-            s = sn;
-        }
-    }
-    const unsigned long long keep = __ballot(ka != 0ull) != 0ull ? ka : kb;
-    if (!incol) return;
-    uint8_t* C = cand + base;
-    for (unsigned long long kk = keep; kk; kk &= kk - 1) {
-        const int r = __ffsll((long long)kk) - 1;
-        C[(size_t)r * w] = sv[r * 64 + lane];
-    }
-#else
-    // both thresholds in one sweep: a = iniThFAST, b = minThFAST
-    unsigned long long ka = 0, kb = 0;
-    int s = sv[lane];
-    int ac = s >= t1 ? s : 0, bc = s >= t2 ? s : 0;
-    int ahp = 0, bhp = 0;  // max over columns c-1..c+1 of row r-1
-    for (int r = 0; r < wh; ++r) {
-        const int sn = sv[(r + 1) * 64 + lane];
-        const int an = sn >= t1 ? sn : 0, bn = sn >= t2 ? sn : 0;
-        const int alc = lane_from_left(ac), arc = lane_from_right(ac);
-        const int aln = lane_from_left(an), arn = lane_from_right(an);
-        const int blc = lane_from_left(bc), brc = lane_from_right(bc);
-        const int bln = lane_from_left(bn), brn = lane_from_right(bn);
-        const int ah = max(alc, arc), bh = max(blc, brc);
-        const int am = max(max(ahp, ah), max(max(aln, arn), an));
-        const int bm = max(max(bhp, bh), max(max(bln, brn), bn));
-        // s > m >= 0 also excludes s == 0
-        if (s >= t1 && s > am) ka |= 1ull << r;
-        if (s >= t2 && s > bm) kb |= 1ull << r;
-        ahp = max(ah, ac);
-        bhp = max(bh, bc);
-        ac = an;
-        bc = bn;
-        s = sn;
-    }
-    const unsigned long long keep = __ballot(ka != 0ull) != 0ull ? ka : kb;
-    if (!incol) return;
-    uint8_t* C = cand + base;
-    for (int r0 = 0; r0 < wh; r0 += 8) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int r = r0 + k;
-            if (r < wh) C[(size_t)r * w] = ((keep >> r) & 1ull) ? sv[r * 64 + lane] : (uint8_t)0;
-        }
-    }
-#endif
-#endif
 }
 
 #ifndef PLVI_NMS_CELLS
@@ -1004,13 +725,8 @@ __global__ __launch_bounds__(64) void orb_cell_nms_kernel(const OrbCellDev* __re
                                                           const uint8_t* __restrict__ score,
                                                           uint8_t* __restrict__ cand, int t1, int t2) {
     PLVI_ORB_PRIO_SET();
-    __shared__ uint8_t sv[kNmsRows * 64];
     const int f = blockIdx.y;
-    for (int ci = blockIdx.x; ci < ncells; ci += gridDim.x) {
-        orb_nms_cell(cells[ci], f, lvs, score, cand, t1, t2, sv);
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // the next cell's staging overwrites sv
-    }
+    for (int ci = blockIdx.x; ci < ncells; ci += gridDim.x) orb_nms_cell(cells[ci], f, lvs, score, cand, t1, t2);
 }
 
 // ---------------------------------------------------------------------------
@@ -1024,90 +740,21 @@ __global__ __launch_bounds__(64) void orb_cell_nms_kernel(const OrbCellDev* __re
 // ---------------------------------------------------------------------------
 constexpr int kSatRowsPerWave = 8;
 
-// One wave per (strip, level, frame): lane = column, rows top-down, 8 rows'
-// loads in flight; per row a ballot gives the prefix counts (v_mbcnt) and the
-// row total (popcount) without any cross-lane scan; running column sums.
-// Per-cell candidate thresholds (K1b's fallback decision): a candidate byte v
-// counts iff v != 0 and v >= the threshold of its cell, cell (i, j) =
-// ((y - 3) / hCell, (x - 3) / wCell) in region coordinates (clamped: bytes
-// outside every detection window are 0).  The level's table is staged in LDS.
-struct OrbCellThr {
-    __device__ __forceinline__ static void stage(uint8_t* lds, const uint8_t* __restrict__ cthr, int thrFrame, int f,
-                                                 const OrbLevelDev& L) {
-        if (!PLVI_BF_NMS) return;  // the NMS kernel decided: every nonzero byte counts (table of zeros)
-        const uint8_t* g = cthr + (size_t)f * thrFrame + L.thrOff;
-        for (int k = threadIdx.x; k < L.nRows * L.nCols; k += blockDim.x) lds[k] = g[k];
-        __syncthreads();
-    }
-    __device__ __forceinline__ static int row(int yr, const OrbLevelDev& L) {  // cell row of region row yr
-        return yr < 3 ? 0 : min((yr - 3) / L.hCell, L.nRows - 1);
-    }
-    __device__ __forceinline__ static int col(int xr, const OrbLevelDev& L) {
-        return xr < 3 ? 0 : min((xr - 3) / L.wCell, L.nCols - 1);
-    }
-};
-
-__global__ __launch_bounds__(64) void orb_sat_strip_kernel(const OrbLevelDev* __restrict__ lvs,
-                                                           const uint8_t* __restrict__ cand,
-                                                           const uint8_t* __restrict__ cthr, int thrFrame,
-                                                           unsigned short* __restrict__ lsat, int* __restrict__ carry) {
-    __shared__ uint8_t sthr[PLVI_BF_NMS ? kOrbCellsLevelMax : 1];
-    const int s = blockIdx.x, l = blockIdx.y, f = blockIdx.z;
-    const OrbLevelDev& L = lvs[l];
-    const int nS = L.satStrips;
-    if (s >= nS) return;
-    OrbCellThr::stage(sthr, cthr, thrFrame, f, L);
-    const int lane = threadIdx.x, x = 64 * s + lane, pitch = 64 * nS;
-    const int cj = OrbCellThr::col(x, L);
-    unsigned short* base = lsat + L.satOff + (size_t)f * L.satPlane;
-    int* T = carry + L.carryOff + (size_t)f * L.carryPlane;
-    const uint8_t* C0 = cand + L.boff + (size_t)f * L.bplane + (size_t)L.minB * L.bpitch + L.minB;
-    base[x] = 0;
-    if (lane == 0) T[s + 1] = 0;
-    int colacc = 0, tot = 0;
-    for (int y0 = 1; y0 <= L.rh; y0 += kSatRowsPerWave) {
-        int v[kSatRowsPerWave];
-#pragma unroll
-        for (int k = 0; k < kSatRowsPerWave; ++k) {
-            const int y = y0 + k;  // SAT row y counts image row y-1 of the region
-            const int c = (y <= L.rh && x < L.rw) ? (int)C0[(size_t)(y - 1) * L.bpitch + x] : 0;
-            v[k] = c != 0 && (!PLVI_BF_NMS || c >= (int)sthr[OrbCellThr::row(y - 1, L) * L.nCols + cj]);
-        }
-#pragma unroll
-        for (int k = 0; k < kSatRowsPerWave; ++k) {
-            // the row's indicator as a wave mask: candidates left of x within the
-            // strip = set bits below this lane (v_mbcnt), the row total = popcount
-            const unsigned long long m = __ballot(v[k] != 0);
-            colacc += (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-            tot += __popcll(m);
-            const int y = y0 + k;
-            if (y <= L.rh) {
-                base[(size_t)y * pitch + x] = (unsigned short)colacc;
-                if (lane == 0) T[(size_t)y * (nS + 1) + s + 1] = tot;
-            }
-        }
-    }
-}
-
-// The same table with four columns per lane: one wave covers four 64-column
+// Rows top-down, 8 rows' loads in flight; per row ballots give the prefix
+// counts (v_mbcnt) and the row total (popcount) without any cross-lane scan;
+// running column sums.  Four columns per lane: one wave covers four 64-column
 // strips (lanes 16g..16g+15 = strip 4w+g), one dword load per row and lane,
 // the strip-local prefix counts from four ballots masked to the lane's
 // 16-lane group, the four ushort entries of a lane stored as one 8-byte
 // store.  A quarter of the waves and load / store instructions.
-#ifndef PLVI_SAT_QUAD
-#define PLVI_SAT_QUAD 1
-#endif
 __global__ __launch_bounds__(64) void orb_sat_quad_kernel(const OrbLevelDev* __restrict__ lvs,
                                                           const uint8_t* __restrict__ cand,
-                                                          const uint8_t* __restrict__ cthr, int thrFrame,
                                                           unsigned short* __restrict__ lsat, int* __restrict__ carry) {
     PLVI_ORB_PRIO_SET();
-    __shared__ uint8_t sthr[PLVI_BF_NMS ? kOrbCellsLevelMax : 1];
     const int w = blockIdx.x, l = blockIdx.y, f = blockIdx.z;
     const OrbLevelDev& L = lvs[l];
     const int nS = L.satStrips;
     if (4 * w >= nS) return;
-    OrbCellThr::stage(sthr, cthr, thrFrame, f, L);
     const int lane = threadIdx.x, g = lane >> 4, s = 4 * w + g, xb = 256 * w + 4 * lane, pitch = 64 * nS;
     const bool live = s < nS;
     unsigned short* base = lsat + L.satOff + (size_t)f * L.satPlane;
@@ -1118,11 +765,6 @@ __global__ __launch_bounds__(64) void orb_sat_quad_kernel(const OrbLevelDev* __r
     const unsigned long long below = ((1ull << lane) - 1ull) & ~((1ull << (16 * g)) - 1ull);
     const unsigned long long group = 0xffffull << (16 * g);
     const bool full = xb + 4 <= L.rw;
-    int cj[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) cj[j] = OrbCellThr::col(xb + j, L);
-    uint32_t thr = 0u;  // the four columns' thresholds (bytes) in the current cell row
-    int ci = -1;
     unsigned acc[4] = {0u, 0u, 0u, 0u};
     int tot = 0;
     for (int y0 = 1; y0 <= L.rh; y0 += kSatRowsPerWave) {
@@ -1145,17 +787,8 @@ __global__ __launch_bounds__(64) void orb_sat_quad_kernel(const OrbLevelDev* __r
 #pragma unroll
         for (int k = 0; k < kSatRowsPerWave; ++k) {
             const uint32_t u = v[k];
-            const int cr = PLVI_BF_NMS ? OrbCellThr::row(y0 + k - 1, L) : 0;  // wave-uniform
-            if (PLVI_BF_NMS && cr != ci) {
-                ci = cr;
-                const uint8_t* tr = sthr + ci * L.nCols;
-                thr = (uint32_t)tr[cj[0]] | (uint32_t)tr[cj[1]] << 8 | (uint32_t)tr[cj[2]] << 16 |
-                      (uint32_t)tr[cj[3]] << 24;
-            }
-            const bool i0 = (u & 0xffu) != 0u && (u & 0xffu) >= (thr & 0xffu);
-            const bool i1 = (u & 0xff00u) != 0u && (u & 0xff00u) >= (thr & 0xff00u);
-            const bool i2 = (u & 0xff0000u) != 0u && (u & 0xff0000u) >= (thr & 0xff0000u);
-            const bool i3 = (u & 0xff000000u) != 0u && (u & 0xff000000u) >= (thr & 0xff000000u);
+            const bool i0 = (u & 0xffu) != 0u, i1 = (u & 0xff00u) != 0u, i2 = (u & 0xff0000u) != 0u,
+                       i3 = (u & 0xff000000u) != 0u;
             const unsigned long long m0 = __ballot(i0), m1 = __ballot(i1), m2 = __ballot(i2), m3 = __ballot(i3);
             const unsigned cb = (unsigned)(__popcll(m0 & below) + __popcll(m1 & below) + __popcll(m2 & below) +
                                            __popcll(m3 & below));
@@ -1419,7 +1052,7 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
         out_cnt[(size_t)f * L + l] = overflow ? 0 : cntOut;
         if (overflow) atomicOr(err + f, 1);
     }
-    if (PLVI_NMS_CLEAR && !PLVI_BF_NMS && overflow) {
+    if (overflow) {
         // no node list for orb_node_best_kernel to clear from: zero the region here
         uint8_t* Cm = cand + lv.boff + (size_t)f * lv.bplane + (size_t)lv.minB * lv.bpitch + lv.minB;
         for (int y = 0; y < RH; ++y)
@@ -1438,13 +1071,11 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
 #endif
 constexpr int kBestNodes = PLVI_BEST_NODES;  // nodes per wave (the grid's x extent is nodeCapMax / kBestNodes)
 
-__device__ __forceinline__ void orb_node_best_one(const OrbLevelDev& lv, uint8_t* __restrict__ Cm,
-                                                  const uint8_t* __restrict__ cthr, int thrFrame, int f, const short4 r,
+__device__ __forceinline__ void orb_node_best_one(const OrbLevelDev& lv, uint8_t* __restrict__ Cm, const short4 r,
                                                   float4* __restrict__ out);
 
 __global__ __launch_bounds__(64) void orb_node_best_kernel(const OrbLevelDev* __restrict__ lvs,
                                                            uint8_t* __restrict__ cand,
-                                                           const uint8_t* __restrict__ cthr, int thrFrame,
                                                            const short4* __restrict__ rects,
                                                            const int* __restrict__ rect_cnt, int nodeCapMax, int L,
                                                            float4* __restrict__ lvkp, int kpCapFrame) {
@@ -1456,13 +1087,12 @@ __global__ __launch_bounds__(64) void orb_node_best_kernel(const OrbLevelDev* __
     for (int k = 0; k < kBestNodes; ++k) {
         const int node = blockIdx.x * kBestNodes + k;
         if (node >= ncnt) return;
-        orb_node_best_one(lv, Cm, cthr, thrFrame, f, rects[((size_t)f * L + l) * nodeCapMax + node],
+        orb_node_best_one(lv, Cm, rects[((size_t)f * L + l) * nodeCapMax + node],
                           lvkp + (size_t)f * kpCapFrame + lv.kpOff + node);
     }
 }
 
-__device__ __forceinline__ void orb_node_best_one(const OrbLevelDev& lv, uint8_t* __restrict__ Cm,
-                                                  const uint8_t* __restrict__ cthr, int thrFrame, int f, const short4 r,
+__device__ __forceinline__ void orb_node_best_one(const OrbLevelDev& lv, uint8_t* __restrict__ Cm, const short4 r,
                                                   float4* __restrict__ out) {
     const int lane = threadIdx.x;
     const int rx0 = r.x, ry0 = r.y, rx1 = r.z, ry1 = r.w;
@@ -1482,10 +1112,8 @@ __device__ __forceinline__ void orb_node_best_one(const OrbLevelDev& lv, uint8_t
         uint8_t* cp = Cm + (size_t)(lv.minB + yy) * lv.bpitch + lv.minB + xx;
         const int resp = *cp;
         if (!resp) continue;
-        if (PLVI_NMS_CLEAR && !PLVI_BF_NMS) *cp = 0;  // consumed: the next batch's NMS finds the plane zero
+        *cp = 0;  // consumed: the next batch's NMS finds the plane zero
         const unsigned ci = (unsigned)(yy - 3) / (unsigned)lv.hCell, cj = (unsigned)(xx - 3) / (unsigned)lv.wCell;
-        if (PLVI_BF_NMS && resp < (int)cthr[(size_t)f * thrFrame + lv.thrOff + ci * (unsigned)lv.nCols + cj])
-            continue;  // the cell's fallback threshold (fused NMS)
         const unsigned key = ((ci * (unsigned)lv.nCols + cj) * (unsigned)lv.rh + (unsigned)yy) * (unsigned)lv.rw + (unsigned)xx;
         const unsigned long long pk = ((unsigned long long)resp << 32) | (0xFFFFFFFFu - key);
         best = pk > best ? pk : best;
@@ -1528,28 +1156,12 @@ constexpr int kAngR = 15, kAngRows = 2 * kAngR + 1, kAngPitch = 32;
 #ifndef PLVI_DESC_WPE
 #define PLVI_DESC_WPE 5
 #endif
-// PLVI_DESC_SPLIT=1: IC_Angle and rBRIEF as two launches of this kernel
-// (PART 1: orientation only, PART 2: descriptor only, reading the angle
-// PART 1 stored), each with about half the registers of the fused PART 0.
-// Beside the growth waves (6 per SIMD) the fused kernel's 96 VGPRs fit one
-// wave per SIMD, the parts' 44 / 64 fit two or more: at two batches in
-// flight the step is 0.7-1.5 % faster (within the spread between boxes), but
-// the extra describe waves slow the other batch's blur + FAST launches from
-// 9-11 to 15-16 ms in the timed window (profiles/r04/ab_sched_inflight2.txt),
-// so the fused kernel stays the default
-#ifndef PLVI_DESC_SPLIT
-#define PLVI_DESC_SPLIT 0
-#endif
-#ifndef PLVI_DESC_SPLIT_WPE
-#define PLVI_DESC_SPLIT_WPE 8
-#endif
 #ifndef PLVI_DESC_UNROLL
 #define PLVI_DESC_UNROLL 4  // rBRIEF loop unroll (1 or 2: 78 instead of 92 VGPRs)
 #endif
 #define PLVI_PRAGMA(x) _Pragma(#x)
 #define PLVI_UNROLL(n) PLVI_PRAGMA(unroll n)
-template <int PART>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PART ? PLVI_DESC_SPLIT_WPE : PLVI_DESC_WPE))) void orb_describe_kernel(const OrbLevelDev* __restrict__ lvs, int L,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PLVI_DESC_WPE))) void orb_describe_kernel(const OrbLevelDev* __restrict__ lvs, int L,
                                                            const uint8_t* __restrict__ pyr,
                                                            const uint8_t* __restrict__ blur,
                                                            const int* __restrict__ rect_cnt,
@@ -1600,17 +1212,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PART ? PLVI
         // ---- stage both boxes: dword loads first, then LDS writes
         const uint8_t* I0 = pyr + lv.off + (size_t)f * lv.plane + (size_t)(cy - kAngR) * W + (cx - kAngR);
         const uint8_t* B0 = blur + lv.boff + (size_t)f * lv.bplane + (size_t)(cy - kDescR) * BW + (cx - kDescR);
-        constexpr bool doAng = PART != 2, doDesc = PART != 1;
         uint32_t iv[4], bv[6];
         uint8_t blast = 0;
-        if (doAng) {
+        {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {  // 31 rows x 8 dwords (columns cx-15 .. cx+16)
                 const int i = lane + 64 * k;
                 iv[k] = i < kAngRows * 8 ? ld_u32(I0 + (size_t)(i >> 3) * W + 4 * (i & 7)) : 0u;
             }
         }
-        if (doDesc) {
+        {
 #pragma unroll
             for (int k = 0; k < 6; ++k) {  // 37 rows x 9 dwords (columns cx-18 .. cx+17)
                 const int i = lane + 64 * k, r = i / 9;
@@ -1618,14 +1229,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PART ? PLVI
             }
             if (lane < kDescP) blast = B0[(size_t)lane * BW + 36];  // column cx+18
         }
-        if (doAng) {
+        {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const int i = lane + 64 * k;
                 if (i < kAngRows * 8) *reinterpret_cast<uint32_t*>(IP + (i >> 3) * kAngPitch + 4 * (i & 7)) = iv[k];
             }
         }
-        if (doDesc) {
+        {
 #pragma unroll
             for (int k = 0; k < 6; ++k) {
                 const int i = lane + 64 * k, r = i / 9;
@@ -1635,8 +1246,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PART ? PLVI
         }
         wave_sync();
         // ---- IC_Angle (ORBextractor.cc:75-102)
-        float angle = kp.w;  // PART 2: stored by the PART 1 launch
-        if (doAng) {
+        float angle;
+        {
         const uint8_t* center = IP + kAngR * kAngPitch + kAngR;
         int m_01 = 0, m_10 = 0;
         if (u <= 15) {
@@ -1660,10 +1271,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PART ? PLVI
             lvkp[(size_t)f * kpCapFrame + slot] = kp;
         }
         }
-        if (!doDesc) {
-            wave_sync();  // the next slot's staging overwrites the box
-            continue;
-        }
         // ---- rBRIEF (computeOrbDescriptor, ORBextractor.cc:106-145)
         const float factorPI = (float)(3.1415926535897932384626433832795 / 180.f);
         const float ang = angle * factorPI;
@@ -1677,10 +1284,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PART ? PLVI
         for (int k = 0; k < 4; ++k) {
             const float px0 = (float)(int8_t)(pat[k] & 0xffu), py0 = (float)(int8_t)((pat[k] >> 8) & 0xffu);
             const float px1 = (float)(int8_t)((pat[k] >> 16) & 0xffu), py1 = (float)(int8_t)(pat[k] >> 24);
-            const int t0 = P[(cv_round_f(px0 * b + py0 * a) + kDescR) * kDescPitch + cv_round_f(px0 * a - py0 * b) +
-                             kDescR];
-            const int t1 = P[(cv_round_f(px1 * b + py1 * a) + kDescR) * kDescPitch + cv_round_f(px1 * a - py1 * b) +
-                             kDescR];
+            // GET_VALUE's x*b + y*a and x*a - y*b: the left product fused
+            // (ORBextractor.cc.o, 16 vfmadd/vfmsub pairs per descriptor byte)
+            const int t0 = P[(cv_round_f(rfmaf(px0, b, py0 * a)) + kDescR) * kDescPitch +
+                             cv_round_f(rfmaf(px0, a, -(py0 * b))) + kDescR];
+            const int t1 = P[(cv_round_f(rfmaf(px1, b, py1 * a)) + kDescR) * kDescPitch +
+                             cv_round_f(rfmaf(px1, a, -(py1 * b))) + kDescR];
             const unsigned long long m = __ballot(t0 < t1);
             if (lane == 0) out[k] = m;
         }

@@ -89,9 +89,9 @@ struct OrbPipeline {
     int resizeGeneric = 0;  // A.1 vertical-pass switch (PLVI_COMPAT_RESIZE_V_GENERIC)
     int kpCapFrame = 0, nodeCapMax = 0;
     size_t pyrBytesFrameTotal = 0, candBytesTotal = 0, satIntsFrameTotal = 0;
-    int thrFrame = 0;  // bytes of cell thresholds per frame (all levels)
     size_t lvOff0 = 0;  // (unused)
-    DevBuf d_lv, d_cells, d_strips, d_xtab, pyr, blur, score, cand, cthr, sat, carry, rects, rectCnt, lvkp, lvdesc, okp,
+    bool candDirty = false;  // survivors of an aborted run() may still be in the candidate plane
+    DevBuf d_lv, d_cells, d_strips, d_xtab, pyr, blur, score, cand, sat, carry, rects, rectCnt, lvkp, lvdesc, okp,
         odesc, ocount, omono, err, staging;
     size_t pyrSmem = 0;  // orb_pyramid_kernel LDS: column table + source-level row rings
     int xtabN = 0, pyrFrameLds = 0;
@@ -310,50 +310,23 @@ struct OrbPipeline {
                 // LDS: a kPyrRing-row ring of level 0, two rows of every other source level
                 pyrSmem += (l == 1 ? kPyrRing : 2) * (size_t)((lv[l - 1].w + 3) & ~3);
             }
-            // strips of the blur + FAST kernel.  With the fused NMS
-            // (PLVI_BF_NMS) they are cut at cell boundaries so that every FAST
-            // detection window lies inside one strip (the valid cell columns /
-            // rows are a prefix of the grid, :796, :801 skip the rest);
-            // otherwise at kBfAlign-aligned columns, so that each strip writes
-            // whole aligned segments of the blur / score rows (cuts at cell
-            // windows leave partial segments that two strips write at
-            // different times: 12.48 vs 11.57 GB of HBM traffic per launch)
+            // strips of the blur + FAST kernel, cut at kBfAlign-aligned columns
+            // so that each strip writes whole aligned segments of the blur /
+            // score rows (cuts at cell windows leave partial segments that two
+            // strips write at different times: 12.48 vs 11.57 GB of HBM
+            // traffic per launch)
             {
-                int ncv = 0, nrv = 0;
-                for (int j = 0; j < d.nCols && d.minB + j * d.wCell < maxBX - 6; ++j) ncv = j + 1;
-                for (int i = 0; i < d.nRows && d.minB + i * d.hCell < maxBY - 3; ++i) nrv = i + 1;
                 std::vector<int> cx, cy;  // interior split candidates
-                if (PLVI_BF_NMS) {        // window starts of cells 1..
-                    for (int j = 1; j < ncv; ++j) cx.push_back(d.minB + j * d.wCell + 3);
-                    for (int i = 1; i < nrv; ++i) cy.push_back(d.minB + i * d.hCell + 3);
-                } else {
-                    for (int x = kBfAlign; x < d.w; x += kBfAlign) cx.push_back(x);
-                    for (int y = 1; y < d.h; ++y) cy.push_back(y);
-                }
-                constexpr int rowsMax = PLVI_BF_NMS ? kBfRowsMax : kBfRowsPlain;
+                for (int x = kBfAlign; x < d.w; x += kBfAlign) cx.push_back(x);
+                for (int y = 1; y < d.h; ++y) cy.push_back(y);
                 std::vector<int> sx, sy;
                 if (plan_splits(d.w, cx, [](int a, int b) { return b - (a & ~3) <= kBfCols; }, sx) ||
-                    plan_splits(d.h, cy, [](int a, int b) { return b - a <= rowsMax; }, sy))
+                    plan_splits(d.h, cy, [](int a, int b) { return b - a <= kBfRowsPlain; }, sy))
                     return PLVI_E_BADARG;
-                auto first_cell = [](int a, int n, int base, int step) {  // first cell index whose window starts >= a
-                    int k = 0;
-                    while (k < n && base + k * step + 3 < a) ++k;
-                    return k;
-                };
                 for (size_t ri = 0; ri + 1 < sy.size(); ++ri)
-                    for (size_t ci = 0; ci + 1 < sx.size(); ++ci) {
-                        OrbStripDev sd{l, sx[ci], sx[ci + 1], sy[ri], sy[ri + 1], 0, 0, 0, 0};
-                        sd.cj0 = first_cell(sd.x0, ncv, d.minB, d.wCell);
-                        sd.ncj = first_cell(sd.x1, ncv, d.minB, d.wCell) - sd.cj0;
-                        sd.ci0 = first_cell(sd.y0, nrv, d.minB, d.hCell);
-                        sd.nci = first_cell(sd.y1, nrv, d.minB, d.hCell) - sd.ci0;
-                        if (PLVI_BF_NMS && sd.ncj * sd.nci > 64) return PLVI_E_BADARG;
-                        strips.push_back(sd);
-                    }
+                    for (size_t ci = 0; ci + 1 < sx.size(); ++ci)
+                        strips.push_back(OrbStripDev{l, sx[ci], sx[ci + 1], sy[ri], sy[ri + 1]});
             }
-            d.thrOff = thrFrame;
-            thrFrame += d.nRows * d.nCols;
-            if (d.nRows * d.nCols > kOrbCellsLevelMax) return PLVI_E_BADARG;
         }
         kpCapFrame = kpOff;
         pyrBytesFrameTotal = off;
@@ -375,9 +348,7 @@ struct OrbPipeline {
         PLVI_CHECK(hipMemcpy(d_xtab.p, xtab.data(), 4 * xtab.size(), hipMemcpyHostToDevice));
         PLVI_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax.data(), 16 * sizeof(int)));
         // work buffers
-        // the score plane exists only without the fused NMS (PLVI_BF_NMS=0)
-        if (pyr.alloc(off) || blur.alloc(boffAll) || (!PLVI_BF_NMS && score.alloc(boffAll)) || cand.alloc(boffAll) ||
-            cthr.alloc((size_t)std::max(thrFrame, 1) * Bcap) ||
+        if (pyr.alloc(off) || blur.alloc(boffAll) || score.alloc(boffAll) || cand.alloc(boffAll) ||
             sat.alloc(satOff * sizeof(unsigned short)) || carry.alloc(carryOff * sizeof(int)) || rects.alloc(sizeof(short4) * (size_t)nodeCapMax * L * Bcap) ||
             rectCnt.alloc(sizeof(int) * L * Bcap) || lvkp.alloc(sizeof(float4) * (size_t)kpCapFrame * Bcap) ||
             lvdesc.alloc((size_t)32 * kpCapFrame * Bcap) || okp.alloc(sizeof(plvi_keypoint) * (size_t)kpCapFrame * Bcap) ||
@@ -385,9 +356,6 @@ struct OrbPipeline {
             omono.alloc(sizeof(int) * Bcap) || err.alloc(sizeof(int) * Bcap) || staging.alloc((size_t)W * H))
             return PLVI_E_HIP;
         PLVI_CHECK(hipMemset(err.p, 0, sizeof(int) * Bcap));
-        // cell thresholds: written by every blur + FAST (+ NMS) launch; all 0
-        // (no per-cell filtering: the NMS kernel decides) with PLVI_BF_NMS=0
-        PLVI_CHECK(hipMemset(cthr.p, 0, cthr.bytes));
         PLVI_CHECK(hipMemset(cand.p, 0, cand.bytes));  // outside the detection windows it stays 0
         return PLVI_OK;
     }
@@ -403,8 +371,13 @@ struct OrbPipeline {
         uint8_t* P = pyr.as<uint8_t>();
         uint8_t* Bl = blur.as<uint8_t>();
         uint8_t* Cd = cand.as<uint8_t>();
-        uint8_t* Sc = PLVI_BF_NMS ? Cd : score.as<uint8_t>();  // the fused kernel writes the candidate plane
-        uint8_t* Ct = cthr.as<uint8_t>();
+        uint8_t* Sc = score.as<uint8_t>();
+        // The candidate plane must be zero when the NMS writes its survivors:
+        // orb_node_best_kernel clears every candidate it reads (the octree
+        // kernel the region of a level that overflowed).  A run that returned
+        // between the two launches left survivors behind: clear it once.
+        if (candDirty) PLVI_CHECK(hipMemsetAsync(Cd, 0, candBytesTotal, st));
+        candDirty = false;
         mark(0, st);
         auto hook = [&](int k, hipStream_t s_) {
             if (evAfterBlur && gateStage == k) PLVI_CHECK(hipEventRecord(evAfterBlur, s_));
@@ -423,7 +396,7 @@ struct OrbPipeline {
         if (kt) PLVI_CHECK(hipEventRecord(kev[2 * kn], st));
         hipLaunchKernelGGL(orb_blur_fast_kernel, dim3((unsigned)(strips.size() * 8 * ((nf + 7) / 8))), dim3(64), 0, st,
                            d_lv.as<OrbLevelDev>(), d_strips.as<OrbStripDev>(), d_frames, frame_stride, row_stride, P,
-                           Bl, Sc, Ct, thrFrame, taps[0], taps[1], taps[2], taps[3], tmin, t1, t2, (int)strips.size(),
+                           Bl, Sc, taps[0], taps[1], taps[2], taps[3], tmin, t1, t2, (int)strips.size(),
                            nf);
         if (kt) {
             PLVI_CHECK(hipEventRecord(kev[2 * kn + 1], st));
@@ -431,30 +404,19 @@ struct OrbPipeline {
         }
         if (const int hrc = hook(1, st)) return hrc;
         mark(1, st);
-        if (!PLVI_BF_NMS) {
-            // K2 cell NMS -> candidate map: only survivors are written, onto a
-            // zero plane.  PLVI_NMS_CLEAR: the previous batch's node-best pass
-            // zeroed every candidate it read (and the init zeroed the plane);
-            // otherwise a fill per launch, or PLVI_NMS_DENSE (whole windows)
-            if (!PLVI_NMS_CLEAR && (!PLVI_NMS_DENSE || !(PLVI_NMS_MAXONLY && PLVI_NMS_STREAM)))
-                PLVI_CHECK(hipMemsetAsync(Cd, 0, candBytesTotal, st));
-            hipLaunchKernelGGL(orb_cell_nms_kernel, dim3((unsigned)((cells.size() + kNmsCells - 1) / kNmsCells), nf),
-                               dim3(64), 0, st, d_cells.as<OrbCellDev>(), (int)cells.size(), d_lv.as<OrbLevelDev>(),
-                               (const uint8_t*)Sc, Cd, t1, t2);
-        }
+        // K2 cell NMS -> candidate map: only survivors are written, onto the
+        // zero plane (no fill per launch: see candDirty above)
+        candDirty = true;
+        hipLaunchKernelGGL(orb_cell_nms_kernel, dim3((unsigned)((cells.size() + kNmsCells - 1) / kNmsCells), nf),
+                           dim3(64), 0, st, d_cells.as<OrbCellDev>(), (int)cells.size(), d_lv.as<OrbLevelDev>(),
+                           (const uint8_t*)Sc, Cd, t1, t2);
         mark(2, st);
         if (const int hrc = hook(2, st)) return hrc;
         // K3 SAT
         int maxRh = 0, maxStrips = 0;
         for (auto& d : lv) { maxRh = std::max(maxRh, d.rh); maxStrips = std::max(maxStrips, d.satStrips); }
-        if (PLVI_SAT_QUAD)
-            hipLaunchKernelGGL(orb_sat_quad_kernel, dim3((maxStrips + 3) / 4, L, nf), dim3(64), 0, st,
-                               d_lv.as<OrbLevelDev>(), (const uint8_t*)Cd, (const uint8_t*)Ct, thrFrame,
-                               sat.as<unsigned short>(), carry.as<int>());
-        else
-            hipLaunchKernelGGL(orb_sat_strip_kernel, dim3(maxStrips, L, nf), dim3(64), 0, st, d_lv.as<OrbLevelDev>(),
-                               (const uint8_t*)Cd, (const uint8_t*)Ct, thrFrame, sat.as<unsigned short>(),
-                               carry.as<int>());
+        hipLaunchKernelGGL(orb_sat_quad_kernel, dim3((maxStrips + 3) / 4, L, nf), dim3(64), 0, st,
+                           d_lv.as<OrbLevelDev>(), (const uint8_t*)Cd, sat.as<unsigned short>(), carry.as<int>());
         hipLaunchKernelGGL(orb_sat_carry_kernel, dim3((maxRh + 1 + 255) / 256, L, nf), dim3(256), 0, st,
                            d_lv.as<OrbLevelDev>(), carry.as<int>());
         mark(3, st);
@@ -470,23 +432,15 @@ struct OrbPipeline {
         // K5 best per node
         hipLaunchKernelGGL(orb_node_best_kernel, dim3((nodeCapMax + kBestNodes - 1) / kBestNodes, L, nf), dim3(64), 0, st,
                            d_lv.as<OrbLevelDev>(),
-                           Cd, (const uint8_t*)Ct, thrFrame, (const short4*)rects.as<short4>(), (const int*)rectCnt.as<int>(),
+                           Cd, (const short4*)rects.as<short4>(), (const int*)rectCnt.as<int>(),
                            nodeCapMax, L, lvkp.as<float4>(), kpCapFrame);
+        candDirty = false;  // node-best (or the octree on overflow) consumed every survivor
         mark(5, st);
         if (const int hrc = hook(5, st)) return hrc;
         // K6 orientation + rBRIEF
-        if (PLVI_DESC_SPLIT) {
-            hipLaunchKernelGGL(orb_describe_kernel<1>, dim3((kpCapFrame + 15) / 16, nf), dim3(256), 0, st,
-                               d_lv.as<OrbLevelDev>(), L, (const uint8_t*)P, (const uint8_t*)Bl,
-                               (const int*)rectCnt.as<int>(), lvkp.as<float4>(), lvdesc.as<uint8_t>(), kpCapFrame);
-            hipLaunchKernelGGL(orb_describe_kernel<2>, dim3((kpCapFrame + 15) / 16, nf), dim3(256), 0, st,
-                               d_lv.as<OrbLevelDev>(), L, (const uint8_t*)P, (const uint8_t*)Bl,
-                               (const int*)rectCnt.as<int>(), lvkp.as<float4>(), lvdesc.as<uint8_t>(), kpCapFrame);
-        } else {
-            hipLaunchKernelGGL(orb_describe_kernel<0>, dim3((kpCapFrame + 15) / 16, nf), dim3(256), 0, st,
-                               d_lv.as<OrbLevelDev>(), L, (const uint8_t*)P, (const uint8_t*)Bl,
-                               (const int*)rectCnt.as<int>(), lvkp.as<float4>(), lvdesc.as<uint8_t>(), kpCapFrame);
-        }
+        hipLaunchKernelGGL(orb_describe_kernel, dim3((kpCapFrame + 15) / 16, nf), dim3(256), 0, st,
+                           d_lv.as<OrbLevelDev>(), L, (const uint8_t*)P, (const uint8_t*)Bl,
+                           (const int*)rectCnt.as<int>(), lvkp.as<float4>(), lvdesc.as<uint8_t>(), kpCapFrame);
         mark(6, st);
         // K7 assemble
         hipLaunchKernelGGL(orb_assemble_kernel, dim3(nf), dim3(256), 0, st, d_lv.as<OrbLevelDev>(), L,
@@ -696,4 +650,16 @@ extern "C" int plvi_orb_kernel_timing_read(plvi_orb_extractor* h, float* total_m
     if (!h) return PLVI_E_BADARG;
     PLVI_CHECK(hipSetDevice(h->p().device));
     return h->p().ktiming_read(total_ms, launches);
+}
+
+extern "C" int plvi_orb_debug_node_cap(plvi_orb_extractor* h, int cap) {
+    if (!h) return PLVI_E_BADARG;
+    OrbPipeline& p = h->p();
+    PLVI_CHECK(hipSetDevice(p.device));
+    PLVI_CHECK(hipStreamSynchronize(p.stream));
+    std::vector<plvi::OrbLevelDev> v = p.lv;
+    if (cap > 0)
+        for (auto& d : v) d.nodeCap = std::min(d.nodeCap, cap);
+    PLVI_CHECK(hipMemcpy(p.d_lv.p, v.data(), sizeof(plvi::OrbLevelDev) * v.size(), hipMemcpyHostToDevice));
+    return PLVI_OK;
 }

@@ -38,6 +38,17 @@ PLVI_HD uint64_t d2u(double d) { uint64_t u; memcpy(&u, &d, 8); return u; }
 PLVI_HD double u2d(uint64_t u) { double d; memcpy(&d, &u, 8); return d; }
 PLVI_HD double fmad(double a, double b, double c) { return __builtin_fma(a, b, c); }
 
+// The reference's own sources are built by GCC 9.4 with `-O3 -march=native`
+// (CMakeLists.txt; build/CMakeFiles/ORB_SLAM3-Relocalization.dir/flags.make)
+// and GCC's C++ front end contracts `a*b + c` into one fused multiply-add
+// even under -std=c++11.  The shipped objects show exactly which expressions
+// were fused (tests/test_ref_objects.py pins every site on the path); those
+// sites call rfma / rfmaf, everything else stays one IEEE op per operator
+// (-ffp-contract=off).  For `a*b + c*d` GCC fuses the left product:
+// rfma(a, b, c*d).
+PLVI_HD double rfma(double a, double b, double c) { return __builtin_fma(a, b, c); }
+PLVI_HD float rfmaf(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+
 // ------------------------------------------------------------ sinf / cosf
 // __sincosf_table (values dumped from the glibc 2.35 libm used by the
 // reference host).  Entry 1 = entry 0 with the cosine polynomial negated.

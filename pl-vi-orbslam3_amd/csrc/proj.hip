@@ -149,7 +149,7 @@ __device__ unsigned proj_scan(const plvi_proj_params& p, const ProjLds& s, const
             if (!(fabsf(distx) < radius && fabsf(disty) < radius)) continue;
             if (blk[i2]) continue;
             if (uright && uright[i2] > 0) {
-                const float ur = u - p.mbf * invzc;
+                const float ur = rfmaf(-p.mbf, invzc, u);  // fused in ORBmatcher.cc.o
                 const float er = fabsf(ur - uright[i2]);
                 if (er > radius) continue;
             }
@@ -313,8 +313,9 @@ __device__ __forceinline__ void cam_project(const plvi_proj_params& p, const Cam
         v = p.fy * y / z + p.cy;
         return;
     }
-    // KannalaBrandt8::project(const cv::Point3f&)
-    const float x2_plus_y2 = x * x + y * y;
+    // KannalaBrandt8::project(const cv::Point3f&); its 7 fused multiply-adds
+    // as in KannalaBrandt8.cpp.o (x*x + y*y, the four r terms, u, v)
+    const float x2_plus_y2 = rfmaf(x, x, y * y);
     const float theta = plvi::plvi_atan2f(__builtin_sqrtf(x2_plus_y2), z);
     const float psi = plvi::plvi_atan2f(y, x);
     const float theta2 = theta * theta;
@@ -322,9 +323,9 @@ __device__ __forceinline__ void cam_project(const plvi_proj_params& p, const Cam
     const float theta5 = theta3 * theta2;
     const float theta7 = theta5 * theta2;
     const float theta9 = theta7 * theta2;
-    const float r = theta + cm.k0 * theta3 + cm.k1 * theta5 + cm.k2 * theta7 + cm.k3 * theta9;
-    u = p.fx * r * plvi::plvi_cosf(psi) + p.cx;
-    v = p.fy * r * plvi::plvi_sinf(psi) + p.cy;
+    const float r = rfmaf(cm.k3, theta9, rfmaf(cm.k2, theta7, rfmaf(cm.k1, theta5, rfmaf(cm.k0, theta3, theta))));
+    u = rfmaf(p.fx * r, plvi::plvi_cosf(psi), p.cx);
+    v = rfmaf(p.fy * r, plvi::plvi_sinf(psi), p.cy);
 }
 
 constexpr unsigned kScanSkip = 0xFFFFFFFFu;   // left pass `continue`d: no right pass either

@@ -120,9 +120,9 @@ __global__ __launch_bounds__(kStThreads) void stereo_orb_kernel(
     // vRowIndices (:1238-1255)
     for (int iR = t; iR < nR; iR += kStThreads) {
         const plvi_keypoint kp = KR[iR];
-        const float r = 2.0f * prm.scale[kp.octave];
-        const int maxr = (int)__builtin_ceilf(kp.y + r);
-        const int minr = (int)__builtin_floorf(kp.y - r);
+        // ceil(kpY + r) / floor(kpY - r), r = 2*scale: fused in Frame.cc.o
+        const int maxr = (int)__builtin_ceilf(rfmaf(2.0f, prm.scale[kp.octave], kp.y));
+        const int minr = (int)__builtin_floorf(rfmaf(-2.0f, prm.scale[kp.octave], kp.y));
         s_rx[iR] = kp.x;
         s_roct[iR] = kp.octave;
         if (minr < 0 || maxr >= nRows) { s_fail = 1; continue; }  // vRowIndices[yi] out of range (UB)
@@ -141,8 +141,8 @@ __global__ __launch_bounds__(kStThreads) void stereo_orb_kernel(
         return;
     }
     for (int iR = t; iR < nR; iR += kStThreads) {
-        const float y = KR[iR].y, r = 2.0f * prm.scale[s_roct[iR]];
-        const int maxr = (int)__builtin_ceilf(y + r), minr = (int)__builtin_floorf(y - r);
+        const float y = KR[iR].y, sc = prm.scale[s_roct[iR]];
+        const int maxr = (int)__builtin_ceilf(rfmaf(2.0f, sc, y)), minr = (int)__builtin_floorf(rfmaf(-2.0f, sc, y));
         for (int yi = minr; yi <= maxr; ++yi) s_idx[s_row[yi] + atomicAdd(&s_cur[yi], 1)] = (unsigned short)iR;
     }
     __syncthreads();
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(kStThreads) void stereo_orb_kernel(
                         const float dist1 = (float)s_dist[wv][L + bestincR - 1];
                         const float dist2 = (float)s_dist[wv][L + bestincR];
                         const float dist3 = (float)s_dist[wv][L + bestincR + 1];
-                        const float deltaR = (dist1 - dist3) / (2.0f * (dist1 + dist3 - 2.0f * dist2));
+                        const float deltaR = (dist1 - dist3) / (2.0f * rfmaf(-2.0f, dist2, dist1 + dist3));
                         if (!(deltaR < -1 || deltaR > 1)) {
                             float bestuR = prm.scale[oct] * ((float)scaleduR0 + (float)bestincR + deltaR);
                             float disparity = kp.x - bestuR;
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(kStThreads) void stereo_line_grid_kernel(
     for (int i = t; i < nR; i += kStThreads) {  // directions + grid (:1431-1442)
         const plvi_keyline k = R[i];
         double vx = (double)(k.endPointX - k.startPointX) * inv_w, vy = (double)(k.endPointY - k.startPointY) * inv_h;
-        const double m = sqrt(vx * vx + vy * vy);
+        const double m = sqrt(rfma(vx, vx, vy * vy));  // normalize, fused in Frame.cc.o
         vx /= m;
         vy /= m;
         v2[2 * i] = vx;
@@ -443,9 +443,10 @@ __global__ __launch_bounds__(kStThreads) void stereo_line_disparity_kernel(
                 const double spl0 = a.startPointX, spl1 = a.startPointY, epl0 = a.endPointX, epl1 = a.endPointY;
                 double spr0 = b.startPointX, spr1 = b.startPointY, epr0 = b.endPointX, epr1 = b.endPointY;
                 const double overlap = overlap_stereo(spl1, epl1, spr1, epr1);
-                spr0 = (spr0 * (spl1 - epr1) + epr0 * (spr1 - spl1)) / (spr1 - epr1);
+                // the left product of each numerator is fused (Frame.cc.o)
+                spr0 = rfma(spr0, spl1 - epr1, epr0 * (spr1 - spl1)) / (spr1 - epr1);
                 spr1 = spl1;
-                epr0 = (spr0 * (epl1 - epr1) + epr0 * (spr1 - epl1)) / (spr1 - epr1);
+                epr0 = rfma(spr0, epl1 - epr1, epr0 * (spr1 - epl1)) / (spr1 - epr1);
                 epr1 = epl1;
                 double disp_s = spl0 - spr0, disp_e = epl0 - epr0;
                 const float lsMinDispRatio = 0.7f;
@@ -466,8 +467,8 @@ __global__ __launch_bounds__(kStThreads) void stereo_line_disparity_kernel(
                          b2 = 1.0;
             l0 = a1 * b2 - a2 * b1;
             l1 = a2 * b0 - a0 * b2;
-            l2 = a0 * b1 - a1 * b0;
-            const double s = sqrt(l0 * l0 + l1 * l1);
+            l2 = rfma(a0, b1, -(a1 * b0));  // Eigen cross + norm, fused in Frame.cc.o
+            const double s = sqrt(rfma(l0, l0, l1 * l1));
             l0 = l0 / s;
             l1 = l1 / s;
             l2 = l2 / s;

@@ -190,6 +190,7 @@ def _declare(lib):
         "plvi_orb_profile_read": ([V, V, P], I),
         "plvi_orb_kernel_timing": ([V, I], I),
         "plvi_orb_kernel_timing_read": ([V, V, P], I),
+        "plvi_orb_debug_node_cap": ([V, I], I),
         "plvi_hamming_knn2_batch": ([V, V, I, V, V, I, I, V, V, V, V, V], I),
         "plvi_hamming_knn2": ([V, I, V, I, V, V, V, V], I),
         "plvi_line_match_nnr": ([V, I, V, I, F, V], I),

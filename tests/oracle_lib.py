@@ -68,6 +68,10 @@ def load():
     lib.oracle_match_grid2.restype = I
     lib.oracle_uset_order.argtypes = [V, V, I, I, V]
     lib.oracle_uset_order.restype = I
+    lib.oracle_grid_candidates.argtypes = [I, I, V, V, I, I, I, I, I, I, I, I, I, V, I]
+    lib.oracle_grid_candidates.restype = I
+    lib.oracle_line_coords.argtypes = [D, D, D, D, V, I]
+    lib.oracle_line_coords.restype = I
     lib.oracle_fast_score.argtypes = [V, I]
     lib.oracle_fast_score.restype = I
     lib.oracle_set_compat.argtypes = [ctypes.c_uint]
@@ -343,6 +347,44 @@ def match_grid(lines1, desc1, grid, desc2, directions2, window=((7, 0), (2, 2)),
     n = lib.oracle_match_grid2(_p(l1), _p(d1), len(l1), cols, rows, _p(off), _p(idx), _p(d2), _p(v2), len(d2),
                                w0, w1, h0, h1, range_hint, _p(m))
     return n, m[:len(l1)]
+
+
+def _grid_csr(grid):
+    cols, rows = len(grid), len(grid[0])
+    off = np.zeros(cols * rows + 1, np.int32)
+    idx = []
+    for x in range(cols):
+        for y in range(rows):
+            idx.extend(grid[x][y])
+            off[x * rows + y + 1] = len(idx)
+    return cols, rows, off, np.array(idx if idx else [0], np.int32)
+
+
+def grid_candidates(grid, sp, ep, window=((7, 0), (2, 2)), range_hint=0, lib=None, fn="oracle_grid_candidates"):
+    """Iteration order of matchGrid's candidate set for one line (GridStructure::get
+    at sp then ep, gridStructure.cpp:67-78).  `lib`/`fn` select another
+    implementation with the same signature minus range_hint (oracle/_ref)."""
+    cols, rows, off, idx = _grid_csr(grid)
+    (w0, w1), (h0, h1) = window
+    out = np.zeros(4096, np.int32)
+    if lib is None:
+        lib = load()
+        n = lib.oracle_grid_candidates(cols, rows, _p(off), _p(idx), sp[0], sp[1], ep[0], ep[1], w0, w1, h0, h1,
+                                       range_hint, _p(out), len(out))
+    else:
+        n = getattr(lib, fn)(cols, rows, _p(off), _p(idx), sp[0], sp[1], ep[0], ep[1], w0, w1, h0, h1, _p(out),
+                             len(out))
+    assert n <= len(out)
+    return out[:n].tolist()
+
+
+def line_coords(x1, y1, x2, y2, lib=None, fn="oracle_line_coords"):
+    """getLineCoords (gridStructure.cpp:32-40) as (x, y) pairs."""
+    lib = lib or load()
+    out = np.zeros(2 * 8192, np.int32)
+    n = getattr(lib, fn)(float(x1), float(y1), float(x2), float(y2), _p(out), 8192)
+    assert n <= 8192
+    return [(int(out[2 * i]), int(out[2 * i + 1])) for i in range(n)]
 
 
 def _declare_vocab(lib):

@@ -91,50 +91,25 @@ def test_mw_flat_and_single_frame(plvi_lib, monkeypatch):
 
 
 @pytest.mark.parametrize("mw", [256, 0])
-def test_rect_lane_per_region_equals_wave_per_region(plvi_lib, monkeypatch, mw):
-    """region2rect + get_theta (lsd.cpp:688-782): lsd_rect_lanes_kernel (lane =
-    region, the default) and lsd_rect_kernel (wave = region,
-    PLVI_RECT_LANES=0) give the same lines bit for bit, behind either
-    region-growing kernel; frame 0 equals the oracle.  Includes the small-batch
-    grid (8 workgroups per (frame, octave)) and the batch grid."""
+def test_rect_lanes_small_and_batch_grid(plvi_lib, monkeypatch, mw):
+    """region2rect + get_theta (lsd.cpp:688-782) in lsd_rect_lanes_kernel
+    (lane = region, with the nine multiply-adds lsd.cpp.o fuses) behind
+    either region-growing kernel, at the small-batch grid (8 workgroups per
+    (frame, octave)) and the batch grid: every frame equals the oracle."""
     st_ = structured_frames()
     frames = np.concatenate([synth.batch(17, seed0=900), np.stack([st_["checker"], st_["stripes"]])])
     for n in (2, len(frames)):
-        monkeypatch.setenv("PLVI_RECT_LANES", "1")
-        lanes = _run(monkeypatch, frames[:n], mw)
-        monkeypatch.setenv("PLVI_RECT_LANES", "0")
-        waves = _run(monkeypatch, frames[:n], mw)
+        got = _run(monkeypatch, frames[:n], mw)
         for f in range(n):
-            assert _same(lanes[f], waves[f]), f"n={n} frame {f}: lane-per-region != wave-per-region"
-    kl, de, fn = ol.line_extract(frames[0])
-    assert _same(lanes[0], (kl.astype(plvi.KEYLINE_DTYPE), de, fn))
+            kl, de, fn = ol.line_extract(frames[f])
+            assert _same(got[f], (kl.astype(plvi.KEYLINE_DTYPE), de, fn)), f"n={n} frame {f}"
 
 
-@pytest.mark.parametrize("helpers", [0, 1, 7, 15])
-def test_mw_helper_workgroups(plvi_lib, monkeypatch, helpers):
-    """Helper workgroups (a PLVI_MW_HELPERS=1 build; PLVI_MW_HELP: up to that
-    many per octave-0 task on idle CUs) grow the seeds of later row bands with an empty committed bitmap
-    and publish them; the task's growers import them, the walker validates
-    them.  The lines stay the oracle's bit for bit, and with helpers some
-    regions come from them (counter 12)."""
-    monkeypatch.setenv("PLVI_MW_HELP", str(helpers))
-    frames = np.concatenate([synth.batch(3, seed0=410), structured_frames()["checker"][None]])
-    mw, st = _run(monkeypatch, frames, 256, stats=True)
-    for f in range(len(frames)):
-        assert _same(mw[f], ol.line_extract(frames[f])), f"helpers={helpers} frame {f}"
-    imported = int(st[:3, 0, 12].sum())
-    if helpers > 0 and imported == 0:
-        pytest.skip("library built without helper workgroups (PLVI_MW_HELPERS=0, the default)")
-    assert (imported > 0) == (helpers > 0), st[:, 0, 12]
-
-
-def test_mw_helpers_across_launches(plvi_lib, monkeypatch):
-    """One extractor, consecutive launches over different frames: the helpers'
-    per-pixel map and records are not cleared between launches (the launch
-    epoch tags them), so a region published for another frame is never
-    imported."""
+def test_mw_consecutive_launches(plvi_lib, monkeypatch):
+    """One extractor, consecutive launches over different frames: the own-mark
+    spill bitmaps are kept zero by every launch (never cleared in between),
+    so no launch sees another frame's marks."""
     monkeypatch.setenv("PLVI_GROW_MW", "256")
-    monkeypatch.setenv("PLVI_MW_HELP", "3")
     frames = synth.batch(4, seed0=520)
     lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 640, 480, max_batch=2)
     lib = plvi.load()

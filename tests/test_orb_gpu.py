@@ -111,9 +111,42 @@ def test_orb_structured_extremes(orb640, name):
     _assert_same(orb640(img), ol.orb_extract(img), name)
 
 
+def _batch_tables(orb, batch):
+    n = len(batch)
+    buf = plvi.DeviceBuffer(batch.nbytes)
+    buf.upload(np.ascontiguousarray(batch))
+    orb.extract_batch(buf.ptr, n, 640 * 480, 640)
+    plvi.load().plvi_device_synchronize()
+    kp_p, de_p, co_p, mo_p, cap = orb.outputs()
+    cnt = plvi.download(co_p, np.zeros(n, np.int32))
+    mono = plvi.download(mo_p, np.zeros(n, np.int32))
+    kps = plvi.download(kp_p, np.zeros(n * cap, plvi.KEYPOINT_DTYPE))
+    desc = plvi.download(de_p, np.zeros((n * cap, 32), np.uint8))
+    return [(int(mono[f]), kps[f * cap:f * cap + cnt[f]], desc[f * cap:f * cap + cnt[f]]) for f in range(n)]
+
+
+def test_orb_octree_overflow_leaves_candidate_plane_clean(plvi_lib):
+    """An octree overflow (forced with the plvi_orb_debug_node_cap hook) flags
+    its frames and has no node list for orb_node_best_kernel to clear the
+    candidate plane from: the octree kernel zeroes the level's region itself.
+    The next normal batch through the same handle is the oracle's bit for bit."""
+    orb = plvi.ORBextractor(1000, 1.2, 8, 20, 7, 640, 480, max_batch=4)
+    lib = plvi.load()
+    noise = np.random.default_rng(5).integers(0, 256, size=(4, 480, 640), dtype=np.uint8)
+    frames = synth.batch(4, seed0=60)
+    assert lib.plvi_orb_debug_node_cap(orb._h, 6) == 0
+    _batch_tables(orb, noise)
+    flags = orb.errors(per_frame=True)
+    assert all(int(v) & 1 for v in np.atleast_1d(flags)[:4]), flags
+    assert lib.plvi_orb_debug_node_cap(orb._h, 0) == 0
+    for f, got in enumerate(_batch_tables(orb, frames)):
+        _assert_same(got, ol.orb_extract(frames[f]), f"after overflow f={f}")
+    assert orb.errors() == 0
+    orb.close()
+
+
 def test_orb_candidate_plane_reuse_across_batches(orb640):
-    """The candidate plane is cleared by the node-best pass that reads it (PLVI_NMS_CLEAR), not filled per
-    launch: a batch after a larger, candidate-dense one (binary noise) and a shorter batch after it must
+    """The candidate plane is cleared by the node-best pass that reads it, not filled per launch: a batch after a larger, candidate-dense one (binary noise) and a shorter batch after it must
     still match the oracle frame by frame."""
     noise = np.random.default_rng(3).integers(0, 256, size=(8, 480, 640), dtype=np.uint8)
     frames = synth.batch(8, seed0=40)

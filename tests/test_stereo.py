@@ -45,8 +45,8 @@ def _py_stereo(kL, dL, kR, dR, pyrL, pyrR, scale, inv, mb, mbf):
     rows = [[] for _ in range(nRows)]
     for iR in range(len(kR)):
         y = f32(kR["y"][iR])
-        r = f32(f32(2.0) * scale[kR["octave"][iR]])
-        maxr, minr = int(math.ceil(f32(y + r))), int(math.floor(f32(y - r)))
+        sc = f32(scale[kR["octave"][iR]])  # kpY +/- 2*scale, fused in Frame.cc.o
+        maxr, minr = int(math.ceil(util.fmaf(2.0, sc, y))), int(math.floor(util.fmaf(-2.0, sc, y)))
         for yi in range(minr, maxr + 1):
             rows[yi].append(iR)
     minD, maxD = f32(0), f32(mbf / mb)
@@ -90,7 +90,7 @@ def _py_stereo(kL, dL, kR, dR, pyrL, pyrR, scale, inv, mb, mbf):
             continue
         d1, d2, d3 = dists[bi - 1], dists[bi], dists[bi + 1]
         with np.errstate(divide="ignore", invalid="ignore"):
-            delta = f32(f32(d1 - d3) / f32(f32(2.0) * f32(f32(d1 + d3) - f32(f32(2.0) * d2))))
+            delta = f32(f32(d1 - d3) / f32(f32(2.0) * util.fmaf(-2.0, d2, f32(d1 + d3))))
         if delta < -1 or delta > 1:
             continue
         bu = f32(scale[lev] * f32(f32(suR0 + f32(binc)) + delta))
@@ -174,7 +174,7 @@ def _py_stereo_lines(klL, dL, klR, dR, W, H, mbf):
         k = klR[i]
         vx = float(f32(k["endPointX"] - k["startPointX"])) * iw
         vy = float(f32(k["endPointY"] - k["startPointY"])) * ih
-        m = math.sqrt(vx * vx + vy * vy)
+        m = math.sqrt(util.fma(vx, vx, vy * vy))
         dirs[i] = (vx / m, vy / m)
         for (x, y) in util.line_iterator(float(k["startPointX"]) * iw, float(k["startPointY"]) * ih,
                                          float(k["endPointX"]) * iw, float(k["endPointY"]) * ih):
@@ -193,9 +193,9 @@ def _py_stereo_lines(klL, dL, klR, dR, W, H, mbf):
         epr0, epr1 = float(r["endPointX"]), float(r["endPointY"])
         ov = _py_overlap(spl1, epl1, spr1, epr1)
         with np.errstate(divide="ignore", invalid="ignore"):
-            spr0 = float(np.float64(spr0 * (spl1 - epr1) + epr0 * (spr1 - spl1)) / np.float64(spr1 - epr1))
+            spr0 = float(np.float64(util.fma(spr0, spl1 - epr1, epr0 * (spr1 - spl1))) / np.float64(spr1 - epr1))
             spr1 = spl1
-            epr0 = float(np.float64(spr0 * (epl1 - epr1) + epr0 * (spr1 - epl1)) / np.float64(spr1 - epr1))
+            epr0 = float(np.float64(util.fma(spr0, epl1 - epr1, epr0 * (spr1 - epl1))) / np.float64(spr1 - epr1))
             epr1 = epl1
             ds, de = spl0 - spr0, epl0 - epr0
             mn = de if de < ds else ds

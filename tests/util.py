@@ -532,3 +532,25 @@ def structured_frames(w=640, h=480):
     rng = np.random.default_rng(11)
     out["binary_noise"] = (rng.integers(0, 2, size=(h, w)) * 255).astype(np.uint8)
     return out
+
+
+# Exact fused multiply-add (Python 3.10 has no math.fma): the reference build
+# fuses some `a*b + c` sites (oracle/ref_fma.h, tests/test_ref_objects.py);
+# the pure-Python restatements use these at the same sites.
+def fma(a, b, c):
+    """a*b + c rounded once to double (float(Fraction) is correctly rounded)."""
+    from fractions import Fraction
+    return float(Fraction(float(a)) * Fraction(float(b)) + Fraction(float(c)))
+
+
+def fmaf(a, b, c):
+    """a*b + c on float32 operands rounded once to float32 (ties to even)."""
+    from fractions import Fraction
+    exact = Fraction(float(np.float32(a))) * Fraction(float(np.float32(b))) + Fraction(float(np.float32(c)))
+    f = np.float32(float(exact))  # double then float32: may double-round, fixed below
+    best = f
+    for g in (np.nextafter(f, np.float32(-np.inf)), np.nextafter(f, np.float32(np.inf))):
+        dg, db = abs(Fraction(float(g)) - exact), abs(Fraction(float(best)) - exact)
+        if dg < db or (dg == db and (int(np.float32(g).view(np.uint32)) & 1) == 0):
+            best = g
+    return np.float32(best)

@@ -1,6 +1,6 @@
 """Region-growing stage time, sequential kernel vs the multi-wave kernel, at
 small batches, plus the multi-wave counters (diagnostic).
-usage: python tools/mw_probe.py [B,...] [helpers,...]  (PLVI_MW_HELP values for the multi-wave runs)"""
+usage: python tools/mw_probe.py [B,...]"""
 import ctypes
 import os
 import pathlib
@@ -20,13 +20,10 @@ W, H = 640, 480
 allf = synth.device_sequence(max(batches), W, H, 0, "cuda")
 lib = plvi.load()
 names = ["disp", "drop", "regrow", "exact", "trivial", "spec_ok", "walk_cyc", "wgrow_cyc", "walks", "blocked",
-         "kern_cyc", "spec_cyc", "import", "blocks", "setup16", "round16"]
-helps = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [None]
+         "kern_cyc", "spec_cyc", "unused", "blocks", "setup16", "round16"]
 for B in batches:
-    for mw, hp in [(0, None)] + [(256, h) for h in helps]:
+    for mw in (0, 256):
         os.environ["PLVI_GROW_MW"] = str(mw)
-        if hp is not None:
-            os.environ["PLVI_MW_HELP"] = str(hp)
         lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=B)
         lx.extract_batch(allf.data_ptr(), B, W * H, W)
         torch.cuda.synchronize()
@@ -35,7 +32,7 @@ for B in batches:
             lx.extract_batch(allf.data_ptr(), B, W * H, W)
         st, runs = lx.profile_read()
         lx.profile(False)
-        line = f"B={B} mw={mw} help={hp} " + " ".join(f"{k}={v / runs:.2f}" for k, v in st.items())
+        line = f"B={B} mw={mw} " + " ".join(f"{k}={v / runs:.2f}" for k, v in st.items())
         if mw:
             s = torch.zeros(B * 2 * 16, dtype=torch.int32, device="cuda")
             lib.plvi_lines_debug_mw_stats(lx._h, ctypes.c_void_p(s.data_ptr()))
