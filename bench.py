@@ -72,6 +72,14 @@ def blur_fast_bytes(w, h):
     return 3 * sum(planes)
 
 
+def pyramid_bytes(w, h):
+    """SURVEY 8(d) algorithmic bytes/frame of the ORB resize pass
+    (ComputePyramid, orb_pyramid_kernel): level l >= 1 reads level l-1 and
+    writes level l once = 1 569 878 B at 640x480."""
+    planes = [a * b for a, b in level_dims(w, h)]
+    return sum(planes[:-1]) + sum(planes[1:])
+
+
 def blur_fast_kernel_bytes(w, h):
     """What orb_blur_fast_kernel itself materialises per frame (reported next
     to the SURVEY model, not used for frac): every level read once, its blur
@@ -381,7 +389,7 @@ def dry_run(args, world, rank):
     nwin = 2 if args.c4 else 1
     seq = synth.device_sequence(B + (nwin - 1) * (B - 1), W, H, seed=pdist.shard_seed(rank))
     digest = hashlib.sha256(seq[:B].numpy().tobytes()).hexdigest()[:16]
-    gather = args.c4 and world > 1 if args.gather is None else args.gather
+    gather = world > 1 if args.gather is None else args.gather
 
     def tables(lo):
         # stand-ins for the per-frame tables (counts, keypoints, descriptors,
@@ -446,8 +454,8 @@ def main():
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--c4", action="store_true", help="BASELINE C4: 752x480 sequences, RCCL gather to rank 0")
     ap.add_argument("--gather", dest="gather", action="store_true", default=None,
-                    help="gather every step's per-frame tables to rank 0 over RCCL (timed; default: on for --c4 "
-                         "with world > 1)")
+                    help="gather every step's per-frame tables to rank 0 over RCCL (timed; default: on whenever "
+                         "world > 1, the north_star's gather of the descriptor tables)")
     ap.add_argument("--no-gather", dest="gather", action="store_false")
     ap.add_argument("--dry-run", action="store_true", help="launcher + reductions on CPU (gloo), no GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -483,7 +491,7 @@ def main():
     if args.c4:
         args.width, args.height = 752, 480
     if args.gather is None:
-        args.gather = bool(args.c4 and world > 1)
+        args.gather = world > 1
     return run(args, world, rank)
 
 
@@ -628,6 +636,7 @@ def run(args, world, rank):
     st_lines, lruns = lx.profile_read()
     lbd_iso = [lx.kernel_timing_read(k) for k in (1, 2)]
     bf_iso = orb.kernel_timing_read()
+    pyr_iso = orb.kernel_timing_read(1)
     orb.kernel_timing(False)
     lx.kernel_timing(False)
     orb.profile(False)
@@ -678,14 +687,15 @@ def run(args, world, rank):
     value = frames_total / el
     ms_step = el / args.steps * 1e3
     err = list(err_warm)
-    ktot = kn = ltot = ln = 0
+    ktot = kn = ltot = ln = ptot = pn = 0
     sob = [[0.0, 0], [0.0, 0]]  # LBD Gaussian + Sobel kernels: [total ms, launches] of octave 0 / 1
     for sl in slots:
         err[0] |= sl.orb.errors(sl.st)
         err[1] |= sl.lx.errors(sl.st)
         a, b = sl.orb.kernel_timing_read()
         c, d = sl.lx.kernel_timing_read()
-        ktot, kn, ltot, ln = ktot + a, kn + b, ltot + c, ln + d
+        p_, q_ = sl.orb.kernel_timing_read(1)
+        ktot, kn, ltot, ln, ptot, pn = ktot + a, kn + b, ltot + c, ln + d, ptot + p_, pn + q_
         for k in (0, 1):
             t_, n_ = sl.lx.kernel_timing_read(k + 1)
             sob[k][0] += t_
@@ -711,6 +721,23 @@ def run(args, world, rank):
         i_ms = bf_iso[0] / bf_iso[1]
         roof["isolated"] = {"avg_launch_ms": i_ms, "launches": bf_iso[1], "achieved": bf_bytes / (i_ms * 1e-3) / 1e9,
                             "frac": bf_bytes / (i_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    # the ORB resize pass (north_star: "pyramid" passes), same pricing
+    py_bytes = pyramid_bytes(W, H) * B
+    py_ms = ptot / max(pn, 1)
+    roof_pyr = {"bound": "hbm", "kernel": "orb_pyramid_kernel (ComputePyramid: 7 chained INTER_LINEAR 8U resizes, "
+                                          "one streaming launch)",
+                "achieved": py_bytes / (py_ms * 1e-3) / 1e9 if pn else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "traffic": committed_traffic(B, "orb_pyramid_kernel") if (W, H) == (640, 480) else None,
+                "bytes_per_launch": py_bytes,
+                "bytes_model": "SURVEY 8(d): level l-1 read + level l written, l = 1..7 (1 569 878 B/frame)",
+                "avg_launch_ms": py_ms, "launches": pn}
+    if roof_pyr["achieved"]:
+        roof_pyr["frac"] = roof_pyr["achieved"] / HBM_PEAK_GBS
+    if pyr_iso[1]:
+        i_ms = pyr_iso[0] / pyr_iso[1]
+        roof_pyr["isolated"] = {"avg_launch_ms": i_ms, "launches": pyr_iso[1],
+                                "achieved": py_bytes / (i_ms * 1e-3) / 1e9,
+                                "frac": py_bytes / (i_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
     lp_ms = ltot / max(ln, 1)
     roof_lsd = {"bound": "hbm", "kernel": "lsd_prep_kernel (u8 -> f64 blur 7x7, resize x0.8, ll_angle; one launch "
                                           "per octave)",
@@ -790,6 +817,7 @@ def run(args, world, rank):
                    "parallelism": f"sequence-sharded x{world}", "gather": bool(args.gather),
                    "inflight": len(slots)},
         "roofline": roof,
+        "roofline_pyramid": roof_pyr,
         "roofline_lsd_prep": roof_lsd,
         "roofline_lbd": roof_lbd,
         "end_to_end_hbm": e2e,

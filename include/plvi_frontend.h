@@ -168,11 +168,13 @@ int plvi_orb_profile(plvi_orb_extractor* h, int enable);
 int plvi_orb_profile_read(plvi_orb_extractor* h, float* stage_ms, int* runs);
 
 /* Per-launch timing of the pyramid blur + FAST kernel (bench.py's roofline
- * kernel): enable=1 resets and records an event pair around every launch on
+ * kernel) and of the pyramid kernel: enable=1 resets and records an event pair around every launch on
  * its launch stream (up to 4096 launches); read synchronises and returns the
  * summed milliseconds and the launch count. */
 int plvi_orb_kernel_timing(plvi_orb_extractor* h, int enable);
 int plvi_orb_kernel_timing_read(plvi_orb_extractor* h, float* total_ms, int* launches);
+/* The same for kind 0 = blur + FAST, 1 = orb_pyramid_kernel (roofline_pyramid). */
+int plvi_orb_kernel_timing_read_kind(plvi_orb_extractor* h, int kind, float* total_ms, int* launches);
 /* Diagnostic: cap every level's octree node capacity at `cap` (<= 0 restores
  * the planned capacities).  A level whose DistributeOctTree needs more nodes
  * flags its frame (plvi_orb_errors bit 1) and yields no keypoints; the test

@@ -105,38 +105,45 @@ struct OrbPipeline {
     ~OrbPipeline() {
         for (auto e : evs) (void)hipEventDestroy(e);
         for (auto e : kev) (void)hipEventDestroy(e);
+        for (auto e : kevP) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
     }
 
-    // Per-launch timing of the blur + FAST kernel (bench.py's roofline kernel):
-    // an event pair on the launch stream around every launch while enabled.
+    // Per-launch timing of the blur + FAST kernel (bench.py's roofline kernel)
+    // and of the pyramid kernel (roofline_pyramid): an event pair on the
+    // launch stream around every launch while enabled.
     static constexpr int kKRing = 4096;
     bool ktime = false;
-    int kn = 0;
+    int kn = 0, knP = 0;
     hipEvent_t evAfterBlur = nullptr;  // frame schedule hook (plvi_orb_internal_blur_event)
     int gateStage = 1;  // PLVI_GROW_GATE: the hook fires after the pyramid (0), blur + FAST (1), NMS (2) or the SAT (3)
     hipEvent_t evStage = nullptr;  // second hook (plvi_orb_internal_stage_event): fires after stage `evStageAt`
     int evStageAt = -1;
-    std::vector<hipEvent_t> kev;
+    std::vector<hipEvent_t> kev, kevP;
     int ktiming(int on) {
         if (on && kev.empty()) {
             kev.resize(2 * kKRing);
+            kevP.resize(2 * kKRing);
             for (auto& e : kev) PLVI_CHECK(hipEventCreate(&e));
+            for (auto& e : kevP) PLVI_CHECK(hipEventCreate(&e));
         }
         ktime = on != 0;
-        if (on) kn = 0;
+        if (on) kn = knP = 0;
         return PLVI_OK;
     }
-    int ktiming_read(float* total_ms, int* launches) {
+    // kind 0: blur + FAST, 1: pyramid
+    int ktiming_read(int kind, float* total_ms, int* launches) {
+        const std::vector<hipEvent_t>& E = kind ? kevP : kev;
+        const int n = kind ? knP : kn;
         float tot = 0.f;
-        for (int i = 0; i < kn; ++i) {
-            PLVI_CHECK(hipEventSynchronize(kev[2 * i + 1]));
+        for (int i = 0; i < n; ++i) {
+            PLVI_CHECK(hipEventSynchronize(E[2 * i + 1]));
             float t = 0.f;
-            PLVI_CHECK(hipEventElapsedTime(&t, kev[2 * i], kev[2 * i + 1]));
+            PLVI_CHECK(hipEventElapsedTime(&t, E[2 * i], E[2 * i + 1]));
             tot += t;
         }
         if (total_ms) *total_ms = tot;
-        if (launches) *launches = kn;
+        if (launches) *launches = n;
         return PLVI_OK;
     }
 
@@ -386,10 +393,17 @@ struct OrbPipeline {
         };
         // K1a: the pyramid (ComputePyramid, chained resize: level l from l-1)
         // of every frame in one streaming launch, one wave per frame
-        if (L > 1)
+        if (L > 1) {
+            const bool ktP = ktime && knP < kKRing;
+            if (ktP) PLVI_CHECK(hipEventRecord(kevP[2 * knP], st));
             hipLaunchKernelGGL(orb_pyramid_kernel, dim3((nf + kPyrFrames - 1) / kPyrFrames), dim3(64 * (kPyrFrames + 1)),
                                pyrSmem, st, d_lv.as<OrbLevelDev>(), L, d_frames, frame_stride, row_stride, nf, P,
                                (const uint32_t*)d_xtab.as<uint32_t>(), xtabN, pyrFrameLds, resizeGeneric);
+            if (ktP) {
+                PLVI_CHECK(hipEventRecord(kevP[2 * knP + 1], st));
+                ++knP;
+            }
+        }
         if (const int hrc = hook(0, st)) return hrc;
         // K1b: blur + FAST score of every level (level 0 also copies the frame into its plane)
         const bool kt = ktime && kn < kKRing;
@@ -649,7 +663,13 @@ extern "C" int plvi_orb_kernel_timing(plvi_orb_extractor* h, int enable) {
 extern "C" int plvi_orb_kernel_timing_read(plvi_orb_extractor* h, float* total_ms, int* launches) {
     if (!h) return PLVI_E_BADARG;
     PLVI_CHECK(hipSetDevice(h->p().device));
-    return h->p().ktiming_read(total_ms, launches);
+    return h->p().ktiming_read(0, total_ms, launches);
+}
+
+extern "C" int plvi_orb_kernel_timing_read_kind(plvi_orb_extractor* h, int kind, float* total_ms, int* launches) {
+    if (!h || kind < 0 || kind > 1) return PLVI_E_BADARG;
+    PLVI_CHECK(hipSetDevice(h->p().device));
+    return h->p().ktiming_read(kind, total_ms, launches);
 }
 
 extern "C" int plvi_orb_debug_node_cap(plvi_orb_extractor* h, int cap) {

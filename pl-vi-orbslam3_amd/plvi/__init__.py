@@ -190,6 +190,7 @@ def _declare(lib):
         "plvi_orb_profile_read": ([V, V, P], I),
         "plvi_orb_kernel_timing": ([V, I], I),
         "plvi_orb_kernel_timing_read": ([V, V, P], I),
+        "plvi_orb_kernel_timing_read_kind": ([V, I, V, P], I),
         "plvi_orb_debug_node_cap": ([V, I], I),
         "plvi_hamming_knn2_batch": ([V, V, I, V, V, I, I, V, V, V, V, V], I),
         "plvi_hamming_knn2": ([V, I, V, I, V, V, V, V], I),
@@ -469,14 +470,15 @@ class ORBextractor:
         return dict(zip(self.ORB_STAGES, ms.tolist())), runs.value
 
     def kernel_timing(self, enable=True):
-        """Event pair around every blur + FAST kernel launch (roofline kernel)."""
+        """Event pair around every blur + FAST and pyramid kernel launch (rooflines)."""
         _check(self._lib.plvi_orb_kernel_timing(self._h, int(enable)), "plvi_orb_kernel_timing")
 
-    def kernel_timing_read(self):
+    def kernel_timing_read(self, kind=0):
+        """(total ms, launches) since kernel_timing(True): kind 0 = orb_blur_fast_kernel, 1 = orb_pyramid_kernel."""
         tot = ctypes.c_float()
         n = ctypes.c_int()
-        _check(self._lib.plvi_orb_kernel_timing_read(self._h, ctypes.byref(tot), ctypes.byref(n)),
-               "plvi_orb_kernel_timing_read")
+        _check(self._lib.plvi_orb_kernel_timing_read_kind(self._h, int(kind), ctypes.byref(tot), ctypes.byref(n)),
+               "plvi_orb_kernel_timing_read_kind")
         return tot.value, n.value
 
     # --- reference getters ---------------------------------------------------

@@ -72,3 +72,12 @@ def test_lbd_sobel_bytes_split_survey_lbd_total():
     assert s0 == 2 * 307_200 + 5 * 307_200 == 2_150_400  # blur r+w, Sobel u8 in + 2 x int16 out
     assert s1 == 307_200 + 76_800 + 5 * 76_800 == 768_000  # pyrDown r+w, Sobel of octave 1
     assert s0 + s1 == 2_918_400 == 998_400 + 1_920_000
+
+
+def test_pyramid_bytes_are_survey_orb_resize():
+    """roofline_pyramid's numerator: SURVEY 8(d) 'ORB resize 1,569,878' B/frame
+    at 640x480 -- each level l >= 1 reads level l-1 and writes level l once;
+    with blur + FAST read it makes the survey's ORB total of 4,421,474."""
+    b = _bench()
+    assert b.pyramid_bytes(640, 480) == 1569878
+    assert b.pyramid_bytes(640, 480) + b.blur_fast_bytes(640, 480) == 4421474

@@ -94,6 +94,17 @@ def test_bench_gpus_n_launches_n_ranks():
     assert out["n_gpus"] == 2 and out["frames_total"] == 2 * 2 * 3
     d = out["rank_digests"]
     assert len(d) == 2 and d[0] != d[1]
+    # the default (non-C4) multi-rank run gathers every step's per-frame
+    # tables to rank 0 too (north_star: RCCL gather of the descriptor tables)
+    g = out["gather"]
+    assert g is not None and g["posts"] == 2
+    assert g["received"] == g["rank_tables"] and g["rank_tables"][0] != g["rank_tables"][1]
+
+
+def test_bench_no_gather_opt_out():
+    out = _bench("--gpus", "2", "--dry-run", "--no-gather", "--batch", "3", "--steps", "2", "--width", "64",
+                 "--height", "48")
+    assert out["gather"] is None
 
 
 def test_bench_c4_dry_run_world2():
