@@ -50,11 +50,16 @@ enum {
  *                  (ORBextractor.cc:1165)
  *  EXP_CV_TABLE    A.6: the f64 7-tap LSD Gaussian (lsd.cpp:455) built with
  *                  OpenCV's table + polynomial exp (EXPTAB_SCALE 6) instead of
- *                  glibc exp (which equals the correctly rounded exp there) */
+ *                  glibc exp (which equals the correctly rounded exp there)
+ *  GEMM_FMA        the pose product Rcw*P + tcw of the frustum tests (cv::gemm,
+ *                  3x3 * 3x1 + 3x1 float) as OpenCV's AVX2-dispatched build
+ *                  contracts it, fma(a2,b2, fma(a0,b0, a1*b1)), instead of the
+ *                  baseline (a0*b0 + a1*b1) + a2*b2 (plvi_frustum_params.compat) */
 enum {
   PLVI_COMPAT_GAUSS_ROUNDED = 1,
   PLVI_COMPAT_RESIZE_V_GENERIC = 2,
   PLVI_COMPAT_EXP_CV_TABLE = 4,
+  PLVI_COMPAT_GEMM_FMA = 8,
 };
 
 /* Per-frame device error flags of a batch (plvi_orb_errors / plvi_lines_errors). */
@@ -713,6 +718,119 @@ int plvi_search_local_stereo(const plvi_local_params* p, const plvi_keypoint* kp
                              int n_r, const uint8_t* blocked_r, const int* r2l, const uint8_t* mp_flags,
                              const float* mp_proj, const int* mp_level, const float* mp_proj_r, const int* mp_level_r,
                              const uint8_t* mp_desc, int n_mp, int* match, int* match_r);
+
+/* --------------------------------------------------------------- Frustum
+ * The local-map visibility test of Tracking::SearchLocalPoints /
+ * SearchLocalPointsAndLines (src/Tracking.cc:5074-5092, :5166-5184,
+ * :5219-5234): Frame::isInFrustum (src/Frame.cc:758-835, Nleft == -1;
+ * :836-846 + isInFrustumChecks :1751-1824, Nleft != -1), Frame::isInFrustum_l
+ * (:849-933), MapPoint::PredictScale(dist, Frame*) (src/MapPoint.cc:531-546),
+ * Get{Min,Max}DistanceInvariance (MapPoint.cc:502-512, MapLine.cc:384-394).
+ * The outputs are the MapPoint fields the local search reads, in the layout
+ * of plvi_search_local_batch / plvi_search_local_stereo_batch, so the two run
+ * back to back on the device.
+ *
+ * One camera of a frame: the world->camera pose of the product Pc = R*P + t
+ * and the centre O of the distance test.  Left / one-camera frames: R = mRcw,
+ * t = mtcw, O = mOw, the camera mpCamera.  Right camera of a two-camera frame:
+ * R = Rrl*mRcw, t = Rrl*mtcw + trl, O = mRwc*tlr + mOw (Frame.cc:1757-1761,
+ * per frame, the caller's cv::Mat products), the camera mpCamera2. */
+typedef struct plvi_frustum_camera {
+  float R[9]; /* row-major */
+  float t[3];
+  float O[3];
+  float fx, fy, cx, cy; /* Pinhole / KannalaBrandt8 mvParameters[0..3]; lines: Frame::fx, fy, cx, cy */
+  float kb[4];          /* KannalaBrandt8 k1..k4 (mvParameters[4..7]) */
+  int model;            /* 0 = Pinhole, 1 = KannalaBrandt8 */
+} plvi_frustum_camera;
+
+typedef struct plvi_frustum_params {
+  plvi_frustum_camera cam[2];       /* cam[1] only with two_camera */
+  int two_camera;                   /* F.Nleft != -1 */
+  float mbf;                        /* Frame::mbf (mTrackProjXR of a one-camera frame) */
+  float min_x, max_x, min_y, max_y; /* mnMinX, mnMaxX, mnMinY, mnMaxY */
+  float view_cos_limit;             /* 0.5 in SearchLocalPoints */
+  int far_points;                   /* mpLocalMapper->mbFarPoints */
+  float far_th;                     /* mpLocalMapper->mThFarPoints */
+  int nlevels;                      /* mnScaleLevels (1..16) */
+  float log_scale_factor;           /* mfLogScaleFactor */
+  float level_ratio[16];            /* filled by plvi_frustum_params_init */
+  unsigned compat;                  /* PLVI_COMPAT_GEMM_FMA */
+} plvi_frustum_params;
+
+/* PredictScale as a table: level_ratio[n] = the least float ratio =
+ * mfMaxDistance/dist with ceil(logf(ratio)/mfLogScaleFactor) >= n (host glibc
+ * logf, as MapPoint.cc.o calls it); +inf when none.  Call once per
+ * (nlevels, log_scale_factor) before uploading the params.  PLVI_E_BADARG for
+ * nlevels outside 1..16 or a negative / NaN log_scale_factor. */
+int plvi_frustum_params_init(plvi_frustum_params* p);
+
+/* Output flags of plvi_frustum_points_batch. */
+enum {
+  PLVI_FRUSTUM_SEARCH = 1,    /* searched by SearchByProjection (left): in view, not far (== local bit0) */
+  PLVI_FRUSTUM_OBS = 2,       /* Observations() > 0, copied from the input (== local bit1) */
+  PLVI_FRUSTUM_SEARCH_R = 4,  /* two-camera: searched right (== local-stereo bit2) */
+  PLVI_FRUSTUM_VISIBLE = 8,   /* isInFrustum returned true: IncreaseVisible, nToMatch */
+  PLVI_FRUSTUM_TRACK = 16,    /* mbTrackInView after the call: mmProjectPoints[mnId] = (ProjX, ProjY) */
+};
+
+/* Per frame f (d_params[f] on the device), its local MapPoints [f][cap] in
+ * mvpLocalMapPoints order (counts d_n): pos [3] = GetWorldPos(), normal [3] =
+ * GetNormal(), dist [2] = {mfMinDistance, mfMaxDistance}, in_flags bit0 =
+ * the loop reaches isInFrustum (mnLastFrameSeen != mnId && !isBad()), bit1 =
+ * Observations() > 0.  Outputs, for evaluated MapPoints only (others keep the
+ * buffers' contents, flags 0 apart from OBS): proj [4] = {mTrackProjX,
+ * mTrackProjY, mTrackProjXR, mTrackViewCos}, level = mnTrackScaleLevel, depth
+ * = mTrackDepth (in/out: a two-camera far test reads the entry value when the
+ * left test fails); two-camera frames: proj[2] untouched, proj_r [4] =
+ * {mTrackProjXR, mTrackProjYR, -, mTrackViewCosR}, level_r =
+ * mnTrackScaleLevelR (-1 = not in view).  Fields the reference leaves stale
+ * are left as they were.  nvisible [f] = nToMatch.  proj_r / level_r may be
+ * NULL for one-camera batches, nvisible may be NULL.  Asynchronous. */
+int plvi_frustum_points_batch(int n_frames, const plvi_frustum_params* d_params, const float* d_pos,
+                              const float* d_normal, const float* d_dist, const uint8_t* d_in_flags, const int* d_n,
+                              int cap, uint8_t* d_flags, float* d_proj, int* d_level, float* d_proj_r, int* d_level_r,
+                              float* d_depth, int* d_nvisible, void* stream);
+
+/* One frame from host memory, synchronous.  Returns nToMatch or an error. */
+int plvi_frustum_points(const plvi_frustum_params* p, const float* pos, const float* normal, const float* dist,
+                        const uint8_t* in_flags, int n, uint8_t* flags, float* proj, int* level, float* proj_r,
+                        int* level_r, float* depth);
+
+/* isInFrustum_l over frame f's local MapLines [f][cap] (mvpLocalMapLines
+ * order, counts d_n): sep [6] = GetWorldPos() (double), normal [3] =
+ * GetNormal(), dist [2] = {mfMinDistance, mfMaxDistance}, in_flags bit0 =
+ * evaluated (mnLastFrameSeen != mnId && !isBad()), desc [32] =
+ * GetDescriptor() (NULL: no gather).  Outputs: inview = mbTrackInView (0 for
+ * lines not evaluated), proj [4] = {mTrackProjsX, mTrackProjsY, mTrackProjeX,
+ * mTrackProjeY} (each pair written once its endpoint passes, as the
+ * reference does), angle = mnTrackangle (in view only); the order-preserving
+ * list mvpLocalMapLines_InFrustum as local indices compact [f][cap] (count
+ * ncompact [f] = nToMatch) and their descriptors compact_desc [f][cap][32],
+ * the desc1 of LineMatcher::match (plvi_line_match_batch).  Asynchronous. */
+int plvi_frustum_lines_batch(int n_frames, const plvi_frustum_params* d_params, const double* d_sep,
+                             const float* d_normal, const float* d_dist, const uint8_t* d_in_flags,
+                             const uint8_t* d_desc, const int* d_n, int cap, uint8_t* d_inview, float* d_proj,
+                             double* d_angle, int* d_compact, uint8_t* d_compact_desc, int* d_ncompact, void* stream);
+
+/* One frame from host memory, synchronous.  Returns nToMatch or an error. */
+int plvi_frustum_lines(const plvi_frustum_params* p, const double* sep, const float* normal, const float* dist,
+                       const uint8_t* in_flags, const uint8_t* desc, int n, uint8_t* inview, float* proj,
+                       double* angle, int* compact, uint8_t* compact_desc);
+
+/* The orientation / position filter after LineMatcher::match in
+ * SearchLocalPointsAndLines (src/Tracking.cc:5244-5292).  Frame f: matches_12
+ * [f][cap] over its ncompact [f] in-frustum lines (in/out: rejected entries
+ * set to -1, as the reference does), compact / proj / angle from
+ * plvi_frustum_lines_batch, the frame's mvKeysUn_Line [f][kl_cap] (counts
+ * d_nkl), blocked [f][kl_cap] = mvpMapLines[i2] && Observations() > 0 on
+ * entry (NULL = none).  Output assign [f][kl_cap] = the local MapLine index
+ * stored in mvpMapLines[i2] by the loop, or -1; nassigned [f] = their count.
+ * The bounds for deltaWidth / deltaHeight come from d_params[f]. */
+int plvi_local_lines_filter_batch(int n_frames, const plvi_frustum_params* d_params, int* d_matches_12,
+                                  const int* d_ncompact, const int* d_compact, int cap, const float* d_proj,
+                                  const double* d_angle, const plvi_keyline* d_kl, const int* d_nkl, int kl_cap,
+                                  const uint8_t* d_blocked, int* d_assign, int* d_nassigned, void* stream);
 
 /* ---------------------------------------------------------------- Stereo
  * Rectified stereo of the stereo Frame constructors (src/Frame.cc:95-140,

@@ -140,6 +140,76 @@ class LineProjParams(ctypes.Structure):
                 ("scale_l", ctypes.c_float * 8)]
 
 
+class FrustumCamera(ctypes.Structure):
+    """plvi_frustum_camera (include/plvi_frontend.h): one camera of a frame for the frustum tests."""
+    _fields_ = [("R", ctypes.c_float * 9), ("t", ctypes.c_float * 3), ("O", ctypes.c_float * 3),
+                ("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
+                ("kb", ctypes.c_float * 4), ("model", ctypes.c_int)]
+
+
+class FrustumParams(ctypes.Structure):
+    """plvi_frustum_params (include/plvi_frontend.h): Frame::isInFrustum / isInFrustum_l of one frame."""
+    _fields_ = [("cam", FrustumCamera * 2), ("two_camera", ctypes.c_int), ("mbf", ctypes.c_float),
+                ("min_x", ctypes.c_float), ("max_x", ctypes.c_float), ("min_y", ctypes.c_float),
+                ("max_y", ctypes.c_float), ("view_cos_limit", ctypes.c_float), ("far_points", ctypes.c_int),
+                ("far_th", ctypes.c_float), ("nlevels", ctypes.c_int), ("log_scale_factor", ctypes.c_float),
+                ("level_ratio", ctypes.c_float * 16), ("compat", ctypes.c_uint)]
+
+
+FRUSTUM_SEARCH, FRUSTUM_OBS, FRUSTUM_SEARCH_R, FRUSTUM_VISIBLE, FRUSTUM_TRACK = 1, 2, 4, 8, 16
+
+
+def frustum_params_init(p):
+    """plvi_frustum_params_init: PredictScale's level_ratio table from nlevels / log_scale_factor."""
+    _check(load().plvi_frustum_params_init(ctypes.byref(p)), "plvi_frustum_params_init")
+    return p
+
+
+def frustum_points(params, pos, normal, dist, in_flags, proj=None, level=None, depth=None, proj_r=None,
+                   level_r=None):
+    """Frame::isInFrustum over one frame's local MapPoints (src/Frame.cc:758-847) from host memory.
+    proj / level / depth (/ proj_r / level_r) are the MapPoint fields on entry (stale values are kept
+    where the reference keeps them).  Returns (nToMatch, flags, proj, level, depth, proj_r, level_r)."""
+    pos = np.ascontiguousarray(pos, np.float32).reshape(-1, 3)
+    n = len(pos)
+    nr = np.ascontiguousarray(normal, np.float32).reshape(-1, 3)
+    ds = np.ascontiguousarray(dist, np.float32).reshape(-1, 2)
+    fi = np.ascontiguousarray(in_flags, np.uint8)
+    pr = np.zeros((n, 4), np.float32) if proj is None else np.array(proj, np.float32).reshape(-1, 4)
+    lv = np.zeros(n, np.int32) if level is None else np.array(level, np.int32)
+    de = np.zeros(n, np.float32) if depth is None else np.array(depth, np.float32)
+    two = bool(params.two_camera)
+    prr = (np.zeros((n, 4), np.float32) if proj_r is None else np.array(proj_r, np.float32).reshape(-1, 4)) \
+        if two else None
+    lvr = (np.zeros(n, np.int32) if level_r is None else np.array(level_r, np.int32)) if two else None
+    fo = np.zeros(max(n, 1), np.uint8)
+    nv = _check(load().plvi_frustum_points(ctypes.byref(params), _ptr(pos), _ptr(nr), _ptr(ds), _ptr(fi), n,
+                                           _ptr(fo), _ptr(pr), _ptr(lv), None if prr is None else _ptr(prr),
+                                           None if lvr is None else _ptr(lvr), _ptr(de)), "plvi_frustum_points")
+    return nv, fo[:n], pr, lv, de, prr, lvr
+
+
+def frustum_lines(params, sep, normal, dist, in_flags, desc=None, proj=None, angle=None):
+    """Frame::isInFrustum_l over one frame's local MapLines (src/Frame.cc:849-933) from host memory.
+    Returns (inview, proj, angle, compact, compact_desc): compact = mvpLocalMapLines_InFrustum as local
+    indices, compact_desc = their descriptors (None without desc)."""
+    sp = np.ascontiguousarray(sep, np.float64).reshape(-1, 6)
+    n = len(sp)
+    nr = np.ascontiguousarray(normal, np.float32).reshape(-1, 3)
+    ds = np.ascontiguousarray(dist, np.float32).reshape(-1, 2)
+    fi = np.ascontiguousarray(in_flags, np.uint8)
+    de = None if desc is None else np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    pr = np.zeros((n, 4), np.float32) if proj is None else np.array(proj, np.float32).reshape(-1, 4)
+    an = np.zeros(n, np.float64) if angle is None else np.array(angle, np.float64)
+    iv = np.zeros(max(n, 1), np.uint8)
+    cp = np.zeros(max(n, 1), np.int32)
+    cd = np.zeros((max(n, 1), 32), np.uint8)
+    nc = _check(load().plvi_frustum_lines(ctypes.byref(params), _ptr(sp), _ptr(nr), _ptr(ds), _ptr(fi),
+                                          None if de is None else _ptr(de), n, _ptr(iv), _ptr(pr), _ptr(an),
+                                          _ptr(cp), _ptr(cd)), "plvi_frustum_lines")
+    return iv[:n], pr, an, cp[:nc], (None if de is None else cd[:nc])
+
+
 def grid_geometry(width, height):
     """Frame ctor grid geometry without distortion (mnMinX = 0, mnMaxX = cols, ...;
     Frame.cc:156-157): (min_x, max_x, min_y, max_y, inv_w, inv_h) as float32."""
@@ -256,6 +326,12 @@ def _declare(lib):
         "plvi_stereo_lines_scratch_bytes": ([I, I, I, I], S),
         "plvi_stereo_lines_batch": ([I, V, V, V, I, V, V, V, I, V, I, I, F, I, I, V, S, V, V, V, V, V, V, V], I),
         "plvi_stereo_lines": ([V, V, I, V, V, I, V, I, I, F, I, V, V, V, V], I),
+        "plvi_frustum_params_init": ([V], I),
+        "plvi_frustum_points_batch": ([I, V, V, V, V, V, V, I, V, V, V, V, V, V, V, V], I),
+        "plvi_frustum_points": ([V, V, V, V, V, I, V, V, V, V, V, V], I),
+        "plvi_frustum_lines_batch": ([I, V, V, V, V, V, V, V, I, V, V, V, V, V, V, V], I),
+        "plvi_frustum_lines": ([V, V, V, V, V, V, I, V, V, V, V, V], I),
+        "plvi_local_lines_filter_batch": ([I, V, V, V, V, I, V, V, V, V, I, V, V, V, V], I),
         "plvi_device_malloc": ([c_void_pp, S], I),
         "plvi_device_free": ([V], I),
         "plvi_memcpy": ([V, V, S, I], I),

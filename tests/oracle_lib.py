@@ -788,3 +788,86 @@ def line_search_init(d1, d2):
     mad = np.zeros(2, np.float64)
     n = lib.oracle_line_search_init(_p(d1), len(d1), _p(d2), len(d2), _p(q), _p(t), _p(mad))
     return np.stack([q[:n], t[:n]], 1), (float(mad[0]), float(mad[1]))
+
+
+# ------------------------------------------------- frustum (oracle/frustum_oracle.cpp)
+def _frustum_fns():
+    lib = load()
+    V, I, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    lib.oracle_predict_scale.argtypes = [F, F, F, I]
+    lib.oracle_predict_scale.restype = I
+    lib.oracle_level_table_check.argtypes = [V, F, I, F, F, ctypes.POINTER(ctypes.c_uint32)]
+    lib.oracle_level_table_check.restype = ctypes.c_longlong
+    lib.oracle_frustum_points.argtypes = [V, V, V, V, V, I, V, V, V, V, V, V]
+    lib.oracle_frustum_points.restype = I
+    lib.oracle_frustum_lines.argtypes = [V, V, V, V, V, I, V, V, V, V]
+    lib.oracle_frustum_lines.restype = I
+    lib.oracle_local_lines_filter.argtypes = [V, V, I, V, V, V, V, I, V, V]
+    lib.oracle_local_lines_filter.restype = I
+    return lib
+
+
+def predict_scale(max_distance, dist, log_scale_factor, nlevels):
+    """MapPoint::PredictScale (MapPoint.cc:531-546) with the host glibc logf."""
+    return _frustum_fns().oracle_predict_scale(max_distance, dist, log_scale_factor, nlevels)
+
+
+def level_table_check(thr, lsf, nlevels, lo, hi):
+    """Mismatches of the threshold rule vs PredictScale over every float ratio in [lo, hi]."""
+    t = np.ascontiguousarray(thr, np.float32)
+    first = ctypes.c_uint32(0)
+    bad = _frustum_fns().oracle_level_table_check(_p(t), float(lsf), int(nlevels), float(lo), float(hi),
+                                                  ctypes.byref(first))
+    return bad, first.value
+
+
+def frustum_points(params, case):
+    """Tracking.cc:5074-5092 over one frame (Frame::isInFrustum) -> dict of the MapPoint fields after it."""
+    lib = _frustum_fns()
+    n = len(case["pos"])
+    pos = np.ascontiguousarray(case["pos"], np.float32)
+    nr = np.ascontiguousarray(case["normal"], np.float32)
+    ds = np.ascontiguousarray(case["dist"], np.float32)
+    fi = np.ascontiguousarray(case["in_flags"], np.uint8)
+    pr = np.array(case["proj"], np.float32)
+    lv = np.array(case["level"], np.int32)
+    de = np.array(case["depth"], np.float32)
+    prr = np.array(case["proj_r"], np.float32)
+    lvr = np.array(case["level_r"], np.int32)
+    fo = np.zeros(max(n, 1), np.uint8)
+    nv = lib.oracle_frustum_points(ctypes.byref(params), _p(pos), _p(nr), _p(ds), _p(fi), n, _p(fo), _p(pr), _p(lv),
+                                   _p(prr), _p(lvr), _p(de))
+    return {"nvisible": nv, "flags": fo[:n], "proj": pr, "level": lv, "depth": de, "proj_r": prr, "level_r": lvr}
+
+
+def frustum_lines(params, case):
+    """Tracking.cc:5219-5234 over one frame (Frame::isInFrustum_l) -> (inview, proj, angle, compact)."""
+    lib = _frustum_fns()
+    n = len(case["sep"])
+    sp = np.ascontiguousarray(case["sep"], np.float64)
+    nr = np.ascontiguousarray(case["normal"], np.float32)
+    ds = np.ascontiguousarray(case["dist"], np.float32)
+    fi = np.ascontiguousarray(case["in_flags"], np.uint8)
+    pr = np.array(case["proj"], np.float32)
+    an = np.array(case["angle"], np.float64)
+    iv = np.zeros(max(n, 1), np.uint8)
+    cp = np.zeros(max(n, 1), np.int32)
+    nc = lib.oracle_frustum_lines(ctypes.byref(params), _p(sp), _p(nr), _p(ds), _p(fi), n, _p(iv), _p(pr), _p(an),
+                                  _p(cp))
+    return iv[:n], pr, an, cp[:nc].copy()
+
+
+def local_lines_filter(params, matches_12, compact, proj, angle, keylines, blocked=None):
+    """Tracking.cc:5244-5292 -> (nassigned, assign, matches_12 after)."""
+    lib = _frustum_fns()
+    m = np.array(matches_12, np.int32)
+    cp = np.ascontiguousarray(compact, np.int32)
+    pr = np.ascontiguousarray(proj, np.float32)
+    an = np.ascontiguousarray(angle, np.float64)
+    kl = np.ascontiguousarray(np.stack([keylines["startPointX"], keylines["startPointY"], keylines["endPointX"],
+                                        keylines["endPointY"]], 1), np.float32)
+    bl = None if blocked is None else np.ascontiguousarray(blocked, np.uint8)
+    asg = np.full(max(len(kl), 1), -1, np.int32)
+    na = lib.oracle_local_lines_filter(ctypes.byref(params), _p(m), len(cp), _p(cp), _p(pr), _p(an), _p(kl), len(kl),
+                                       None if bl is None else _p(bl), _p(asg))
+    return na, asg[:len(kl)], m

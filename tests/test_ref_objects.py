@@ -132,6 +132,8 @@ O_OM = MAIN / "src/ORBmatcher.cc.o"
 O_FR = MAIN / "src/Frame.cc.o"
 O_KB8 = MAIN / "src/CameraModels/KannalaBrandt8.cpp.o"
 O_PIN = MAIN / "src/CameraModels/Pinhole.cpp.o"
+O_MP = MAIN / "src/MapPoint.cc.o"
+O_TR = MAIN / "src/Tracking.cc.o"
 O_GRID = MAIN / "src/gridStructure.cpp.o"
 O_LIT = MAIN / "src/LineIterator.cpp.o"
 O_LSDDET = LINEDESC / "src/LSDDetector_custom.cpp.o"
@@ -223,6 +225,9 @@ UNFUSED = {
            "ORB_SLAM3::Frame::ComputeImageBounds(", "ORB_SLAM3::Frame::ComputeBoW(",
            "ORB_SLAM3::Frame::lineDescriptorMAD(", "ORB_SLAM3::Frame::isInFrustumChecks("],
     O_PIN: ["ORB_SLAM3::Pinhole::project(cv::Point3_<float> const&)"],
+    O_MP: ["ORB_SLAM3::MapPoint::PredictScale(float const&, ORB_SLAM3::Frame*)",
+           "ORB_SLAM3::MapPoint::GetMinDistanceInvariance(", "ORB_SLAM3::MapPoint::GetMaxDistanceInvariance("],
+    O_TR: ["ORB_SLAM3::Tracking::SearchLocalPointsAndLines("],
     O_GRID: ["ORB_SLAM3::GridStructure::get(", "ORB_SLAM3::getLineCoords("],
     O_LIT: ["ORB_SLAM3::LineIterator::LineIterator(", "ORB_SLAM3::LineIterator::getNext("],
 }
@@ -350,6 +355,46 @@ def test_projection_and_stereo_fused_sites():
     assert _find(cl, ["vmulsd %xmm0,%xmm1,%xmm5", "vsubsd %xmm2,%xmm0,%xmm0", "vsubsd %xmm4,%xmm1,%xmm1",
                       "vfmsub231sd %xmm4,%xmm2,%xmm5", "vmulsd %xmm1,%xmm1,%xmm1", "vfmadd132sd %xmm0,%xmm1,%xmm0",
                       "vsqrtsd %xmm0,%xmm0,%xmm1"], gap=6) == 1
+
+
+def test_frustum_sites():
+    """Frame::isInFrustum (Frame.cc:777, :810, :823): invz = 1.0f/PcZ, viewCos
+    = (float)(PO.dot(Pn) / (double)dist), mTrackProjXR = fma(-mbf, invz, u);
+    isInFrustum_l (:871-873, :895-897, :930): u = fma(fx*PcX, invz, cx) per
+    coordinate, mnTrackangle = (double)atan2f(eY - sY, eX - sX);
+    MapPoint::PredictScale (MapPoint.cc:539-545): logf, a float division,
+    ceil (vroundss $0xa), cvttss2si, the clamp (negative -> 0 first); the
+    line filter of SearchLocalPointsAndLines calls atan2f (Tracking.cc:5260)."""
+    fr = _fn(O_FR, "ORB_SLAM3::Frame::isInFrustum(")
+    assert _find(fr, ["vdivss -0x408(%rbp),%xmm0,%xmm0", "vmovss -0x420(%rbp),%xmm7", "vmovss %xmm1,0x1c(%rbx)",
+                      "vfnmadd132ss 0x1c0(%r12),%xmm1,%xmm0"], gap=3) == 1
+    assert _find(fr, ["vcvtss2sd -0x3fc(%rbp),%xmm0,%xmm0", "vdivsd %xmm0,%xmm1,%xmm0",
+                      "vcvtsd2ss %xmm0,%xmm0,%xmm6"], gap=1) == 1
+    calls = [c for c in fr if c.startswith("call [") and c.split("[")[1].rstrip("]") in (
+        "cv::norm", "cv::Mat::dot", "ORB_SLAM3::MapPoint::PredictScale", "cv::operator*", "cv::operator+",
+        "cv::operator-")]
+    assert calls == ["call [cv::operator*]", "call [cv::operator+]", "call [cv::norm]", "call [cv::operator-]",
+                     "call [cv::norm]", "call [cv::Mat::dot]", "call [ORB_SLAM3::MapPoint::PredictScale]"]
+    fl = _fn(O_FR, "ORB_SLAM3::Frame::isInFrustum_l(")
+    for c in ("cx", "cy"):
+        reg = "%xmm0" if c == "cx" else "%xmm2"
+        acc = "%xmm1,%xmm0" if c == "cx" else "%xmm2,%xmm1"
+        assert _find(fl, ["vmulss (%rax)," + reg + "," + reg, "mov 0x0(%rip),%rax [ORB_SLAM3::Frame::" + c + "]",
+                          "vfmadd213ss (%rax)," + acc], gap=1) == 2
+    assert _find(fl, ["vsubss 0x68(%r14),%xmm0,%xmm0", "vsubss 0x64(%r14),%xmm1,%xmm1", "call [atan2f]",
+                      "vcvtss2sd %xmm0,%xmm0,%xmm0"], gap=1) == 1
+    assert _find(fl, ["vcvtss2sd -0x4e8(%rbp),%xmm0,%xmm0", "vmovss -0x50c(%rbp),%xmm7", "vdivsd %xmm0,%xmm1,%xmm0",
+                      "vcvtsd2ss %xmm0,%xmm0,%xmm0"], gap=1) == 1
+    ps = _fn(O_MP, "ORB_SLAM3::MapPoint::PredictScale(float const&, ORB_SLAM3::Frame*)")
+    assert _find(ps, ["call [logf]", "vdivss 0x129b8(%rbp),%xmm0,%xmm0", "vroundss $0xa,%xmm0,%xmm0,%xmm0",
+                      "vcvttss2si %xmm0,%eax", "test %eax,%eax", "js"], gap=1) == 1
+    assert _find(ps, ["cmp %eax,%edx", "lea -0x1(%rdx),%ecx", "cmovle %ecx,%eax"], gap=1) == 1
+    assert "call [atan2f]" in _fn(O_TR, "ORB_SLAM3::Tracking::SearchLocalPointsAndLines(")
+    for name, want in (("GetMinDistanceInvariance", 0.8), ("GetMaxDistanceInvariance", 1.2)):
+        f = _fn(O_MP, "ORB_SLAM3::MapPoint::" + name + "(")
+        lc = [re.search(r"\[(\.LC\d+)\]", s).group(1) for s in f if s.startswith("vmovss 0x0(%rip)")]
+        assert len(lc) == 1 and any(s.startswith("vmulss") for s in f), name
+        assert _rodata(O_MP, lc[0], "f") == struct.unpack("<f", struct.pack("<f", want))[0], name
 
 
 def test_grid_get_passes_the_range_length_as_rehash_hint():

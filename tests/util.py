@@ -554,3 +554,125 @@ def fmaf(a, b, c):
         if dg < db or (dg == db and (int(np.float32(g).view(np.uint32)) & 1) == 0):
             best = g
     return np.float32(best)
+
+
+# ------------------------------------------------------------- frustum cases
+def _rotation(rng):
+    q = rng.normal(size=4)
+    q /= np.linalg.norm(q)
+    w, x, y, z = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def frustum_params(seed, model=0, two_camera=False, far_points=False, compat=0, nlevels=8, scale=1.2):
+    """plvi_frustum_params of a synthetic frame: random pose (Rcw, tcw, Ow = -Rcw^T tcw as float), EuRoC-like
+    Pinhole (752 x 480, mbf = 0.11 fx) or TUM-VI-like KannalaBrandt8 (512 x 512); two_camera adds a right
+    camera 0.1 m to the side (R = Rrl Rcw, t = Rrl tcw + trl, O = Rwc tlr + Ow) with a slight rotation."""
+    import plvi
+    rng = np.random.default_rng(seed)
+    p = plvi.FrustumParams()
+    R = _rotation(rng)
+    t = rng.normal(0, 2, 3)
+    Ow = -R.T @ t
+
+    def set_cam(c, R_, t_, O_):
+        for i in range(9):
+            c.R[i] = np.float32(R_.flat[i])
+        for i in range(3):
+            c.t[i] = np.float32(t_[i])
+            c.O[i] = np.float32(O_[i])
+        if model == 0:
+            c.fx, c.fy, c.cx, c.cy = 458.654, 457.296, 367.215, 248.375
+        else:
+            c.fx, c.fy, c.cx, c.cy = (float(v) for v in KB8_TUMVI[:4])
+            for i in range(4):
+                c.kb[i] = KB8_TUMVI[4 + i]
+        c.model = model
+
+    set_cam(p.cam[0], R, t, Ow)
+    if two_camera:
+        a = 0.02
+        Rrl = np.array([[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]])
+        trl = np.array([-0.101, 0.002, 0.001])
+        tlr = -Rrl.T @ trl
+        set_cam(p.cam[1], Rrl @ R, Rrl @ t + trl, R.T @ tlr + Ow)
+    p.two_camera = int(two_camera)
+    p.mbf = np.float32(0.11) * np.float32(p.cam[0].fx) if model == 0 else 0.0
+    if model == 0:
+        p.min_x, p.max_x, p.min_y, p.max_y = -0.75, 752.5, 0.25, 479.25
+    else:
+        p.min_x, p.max_x, p.min_y, p.max_y = 0.0, 512.0, 0.0, 512.0
+    p.view_cos_limit = 0.5
+    p.far_points, p.far_th = int(far_points), 9.0
+    p.nlevels = nlevels
+    p.log_scale_factor = float(np.float32(np.log(np.float32(scale))))
+    p.compat = compat
+    plvi.frustum_params_init(p)
+    return p
+
+
+def _cam_points(rng, n, model):
+    """Camera-frame points: most in front and inside / around the field of view, some behind."""
+    z = np.where(rng.random(n) < 0.1, rng.uniform(-3, 0, n), rng.uniform(0.05, 25, n))
+    s = 0.9 if model == 0 else 2.5
+    return np.stack([z * rng.uniform(-s, s, n), z * rng.uniform(-s * 0.7, s * 0.7, n), z], 1)
+
+
+def _world(p, pc, cam=0):
+    c = p.cam[cam]
+    R = np.array(c.R[:], np.float64).reshape(3, 3)
+    t = np.array(c.t[:], np.float64)
+    return (pc - t) @ R  # R^T (pc - t)
+
+
+def _normals(rng, po):
+    """Unit normals at ~0-90 degrees from the viewing ray PO (the view cos straddles 0.5)."""
+    u = po / np.maximum(np.linalg.norm(po, axis=1, keepdims=True), 1e-12)
+    perp = np.cross(u, rng.normal(size=u.shape))
+    perp /= np.maximum(np.linalg.norm(perp, axis=1, keepdims=True), 1e-12)
+    a = rng.uniform(0, np.pi / 2, len(u))
+    return (u * np.cos(a)[:, None] + perp * np.sin(a)[:, None]).astype(np.float32)
+
+
+def frustum_case(seed, p, n=3000):
+    """Local MapPoints of frame p (Tracking::SearchLocalPoints input): world positions, normals, {mfMinDistance,
+    mfMaxDistance} straddling the 0.8 / 1.2 invariance bounds with max/dist ratios over every level, flags,
+    and stale MapPoint fields from an earlier frame; plus degenerate points (camera centre, zero depth)."""
+    rng = np.random.default_rng(seed)
+    model = p.cam[0].model
+    pw = _world(p, _cam_points(rng, n, model)).astype(np.float32)
+    O = np.array(p.cam[0].O[:], np.float32)
+    d = np.linalg.norm(pw.astype(np.float64) - O, axis=1)
+    mx = d * 1.2 ** rng.uniform(-1.3, 8.5, n)
+    mn = d / 0.8 * 1.2 ** rng.uniform(-8, 0.4, n)
+    # degenerate: the camera centre itself (Pc ~ 0, dist 0), zero max / min distance
+    pw[:4] = O
+    mx[:2], mn[:4] = 0.0, 0.0
+    dist = np.stack([mn, mx], 1).astype(np.float32)
+    case = {"pos": pw, "normal": _normals(rng, pw.astype(np.float64) - O), "dist": dist,
+            "in_flags": ((rng.random(n) < 0.9).astype(np.uint8) | ((rng.random(n) < 0.85).astype(np.uint8) << 1)),
+            "proj": rng.uniform(-5, 800, (n, 4)).astype(np.float32), "level": rng.integers(-1, 8, n).astype(np.int32),
+            "depth": rng.uniform(0, 30, n).astype(np.float32),
+            "proj_r": rng.uniform(-5, 800, (n, 4)).astype(np.float32),
+            "level_r": rng.integers(-1, 8, n).astype(np.int32)}
+    case["in_flags"][:4] |= 1
+    return case
+
+
+def frustum_line_case(seed, p, n=800):
+    """Local MapLines of frame p: world endpoints (double) of segments in front / behind / across the image
+    border, float normals, {mfMinDistance, mfMaxDistance}, evaluated flags, descriptors, stale fields."""
+    rng = np.random.default_rng(seed)
+    a = _cam_points(rng, n, 0)
+    b = a + rng.normal(0, 1.0, (n, 3)) * np.maximum(a[:, 2:3], 0.5) * 0.3
+    sp, ep = _world(p, a), _world(p, b)
+    O = np.array(p.cam[0].O[:], np.float64)
+    mid = (sp + ep) / 2 - O
+    d = np.linalg.norm(mid, axis=1)
+    dist = np.stack([d / 0.8 * 1.2 ** rng.uniform(-6, 0.4, n), d * 1.2 ** rng.uniform(-1.3, 6, n)], 1)
+    return {"sep": np.concatenate([sp, ep], 1), "normal": _normals(rng, mid), "dist": dist.astype(np.float32),
+            "in_flags": (rng.random(n) < 0.9).astype(np.uint8),
+            "desc": rng.integers(0, 256, (n, 32), dtype=np.uint8),
+            "proj": rng.uniform(-5, 800, (n, 4)).astype(np.float32), "angle": rng.uniform(-3, 3, n)}
