@@ -444,6 +444,27 @@ def dry_run(args, world, rank):
 
 
 # ------------------------------------------------------------------ main
+# The frame schedule's environment knobs (csrc/lines_pipeline.hip init(),
+# csrc/orb_pipeline.hip) and the batch-size rules they select, recorded in the
+# bench line so numbers from different schedules are not compared as like for
+# like (r04 moved --inflight from 1 to 2 and made the ORB start depend on the
+# batch size).
+SCHEDULE_ENV = ("PLVI_STREAM_PRIO", "PLVI_ORB_AFTER_PREP", "PLVI_GROW_AFTER_BLUR", "PLVI_ORB_PRIO",
+                "PLVI_SOBEL_WITH_GROW", "PLVI_SOBEL_GATE", "PLVI_SOBEL_AFTER_GROW", "PLVI_GROW_SPLIT", "PLVI_GROW_LDS",
+                "PLVI_GROW_RB", "PLVI_GROW_RD", "PLVI_GROW_MW", "PLVI_GROW_GATE", "PLVI_ORB_STREAM_PRIO")
+
+
+def schedule_knobs(batch):
+    env = {k: os.environ[k] for k in SCHEDULE_ENV if k in os.environ}
+    after_prep = int(os.environ.get("PLVI_ORB_AFTER_PREP", "1"))
+    big = batch >= 1024
+    return {"env": env,
+            "orb_waits_for_lsd_prep": after_prep >= 2 or (after_prep == 1 and batch < 1024),
+            "growth_waits_for_blur_fast": os.environ.get("PLVI_GROW_AFTER_BLUR", "1") != "0" and big,
+            "sobel_after_growth": os.environ.get("PLVI_SOBEL_AFTER_GROW", "1") != "0" and
+            os.environ.get("PLVI_GROW_AFTER_BLUR", "1") != "0" and big}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -815,7 +836,7 @@ def run(args, world, rank):
                                                    else ""),
                    "batch": B, "frames_per_step": new_frames, "width": W, "height": H,
                    "parallelism": f"sequence-sharded x{world}", "gather": bool(args.gather),
-                   "inflight": len(slots)},
+                   "inflight": len(slots), "schedule": schedule_knobs(B)},
         "roofline": roof,
         "roofline_pyramid": roof_pyr,
         "roofline_lsd_prep": roof_lsd,

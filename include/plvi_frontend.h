@@ -578,6 +578,8 @@ int plvi_search_by_projection(const plvi_proj_params* p, const plvi_keypoint* cu
  * (behind the camera, outside mnMin/MaxX/Y, empty window: :2000-2026).
  * Outputs match [p][cap] / match_r [p][cap_r] (-2 = NULL by the rotation
  * filter, which sees both images' matches in one histogram), nmatches [p].
+ * A searched point whose octave is outside [0, nlevels) gets no candidate in
+ * either image (the reference would index mvScaleFactors out of range).
  * p->mbf is unused.  Asynchronous on `stream`. */
 int plvi_search_by_projection_stereo_batch(int n_pairs, const plvi_proj_params* p, const float* kb8,
                                            const plvi_keypoint* d_kps, const uint8_t* d_desc, const int* d_n, int cap,
@@ -589,8 +591,9 @@ int plvi_search_by_projection_stereo_batch(int n_pairs, const plvi_proj_params* 
                                            const uint8_t* d_mp_desc, const uint8_t* d_last_flags, const int* d_last_n,
                                            int last_cap, int* d_match, int* d_match_r, int* d_nmatches, void* stream);
 
-/* One pair from host memory, synchronous.  Returns nmatches or an error
- * (PLVI_E_BADARG for a searched point's octave outside [0, nlevels)). */
+/* One pair from host memory, synchronous; the same contract as the batch
+ * (an octave outside [0, nlevels): no candidate).  Returns nmatches or an
+ * error. */
 int plvi_search_by_projection_stereo(const plvi_proj_params* p, const float* kb8, const plvi_keypoint* kps,
                                      const uint8_t* desc, int n, const uint8_t* blocked, const plvi_keypoint* kps_r,
                                      const uint8_t* desc_r, int n_r, const uint8_t* blocked_r, const float* x3dc,

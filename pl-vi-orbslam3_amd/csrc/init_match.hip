@@ -364,14 +364,8 @@ extern "C" int plvi_search_for_initialization_batch(int n_pairs, const plvi_init
     if (!(p->window > 0)) return PLVI_E_BADARG;
     if (n_pairs == 0) return PLVI_OK;
     const size_t smem = init_smem(cap1, cap2);
-    // the kernel's static __shared__ data (histogram, kept bins, counters)
-    // shares the 160 KB with the dynamic part: query it once
-    static const size_t static_lds = [] {
-        hipFuncAttributes fa{};
-        return hipFuncGetAttributes(&fa, (const void*)search_init_kernel) == hipSuccess ? fa.sharedSizeBytes
-                                                                                        : (size_t)1024;
-    }();
-    if (smem + static_lds > 160 * 1024) return PLVI_E_CAPACITY;
+    // (with the kernel's static __shared__ histogram, kept bins, counters)
+    if (!lds_fits<search_init_kernel>(smem)) return PLVI_E_CAPACITY;
     PLVI_CHECK(hipFuncSetAttribute((const void*)search_init_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)smem));
     hipLaunchKernelGGL(search_init_kernel, dim3(n_pairs), dim3(256), smem, (hipStream_t)stream, *p, d_kps1, d_desc1,

@@ -77,6 +77,17 @@ struct DevBuf {
     T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+// Does a launch with `dyn` bytes of dynamic LDS fit the 160 KB of a CU? The
+// kernel's static __shared__ data shares the budget (queried once per kernel).
+template <auto Kernel>
+inline bool lds_fits(size_t dyn) {
+    static const size_t static_lds = [] {
+        hipFuncAttributes fa{};
+        return hipFuncGetAttributes(&fa, (const void*)Kernel) == hipSuccess ? fa.sharedSizeBytes : (size_t)1024;
+    }();
+    return dyn + static_lds <= 160 * 1024;
+}
+
 // Read and clear a pipeline's per-frame device error flags (orb_pipeline.hip).
 int read_frame_errors(int* d_err, int nslots, int* frame_flags, int* any, hipStream_t st);
 

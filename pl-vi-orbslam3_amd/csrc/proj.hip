@@ -1085,7 +1085,7 @@ extern "C" int plvi_search_by_projection_batch(int n_pairs, const plvi_proj_para
     if (p->nlevels < 1 || p->nlevels > 16) return PLVI_E_BADARG;
     if (n_pairs == 0) return PLVI_OK;
     const size_t smem = proj_smem(cur_cap, last_cap);
-    if (smem > 160 * 1024) return PLVI_E_CAPACITY;
+    if (!lds_fits<search_by_projection_kernel>(smem)) return PLVI_E_CAPACITY;
     PLVI_CHECK(hipFuncSetAttribute((const void*)search_by_projection_kernel,
                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));
     hipLaunchKernelGGL(search_by_projection_kernel, dim3(n_pairs), dim3(256), smem, (hipStream_t)stream, *p, d_cur_kps,
@@ -1163,7 +1163,7 @@ extern "C" int plvi_search_reloc_batch(int n_pairs, const plvi_reloc_params* p, 
     if (p->nlevels < 1 || p->nlevels > 16 || p->orb_dist < 0 || p->orb_dist > 255) return PLVI_E_BADARG;
     if (n_pairs == 0) return PLVI_OK;
     const size_t smem = proj_smem(cur_cap, kf_cap);  // same carve-up as the frame-to-frame matcher
-    if (smem > 160 * 1024) return PLVI_E_CAPACITY;
+    if (!lds_fits<search_reloc_kernel>(smem)) return PLVI_E_CAPACITY;
     PLVI_CHECK(hipFuncSetAttribute((const void*)search_reloc_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)smem));
     hipLaunchKernelGGL(search_reloc_kernel, dim3(n_pairs), dim3(256), smem, (hipStream_t)stream, *p, d_cur_kps,
@@ -1240,7 +1240,7 @@ extern "C" int plvi_search_local_batch(int n_frames, const plvi_local_params* p,
     if (p->nlevels < 1 || p->nlevels > 16) return PLVI_E_BADARG;
     if (n_frames == 0) return PLVI_OK;
     const size_t smem = local_smem(cap, mp_cap);
-    if (smem > 160 * 1024) return PLVI_E_CAPACITY;
+    if (!lds_fits<search_local_kernel>(smem)) return PLVI_E_CAPACITY;
     PLVI_CHECK(hipFuncSetAttribute((const void*)search_local_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)smem));
     hipLaunchKernelGGL(search_local_kernel, dim3(n_frames), dim3(256), smem, (hipStream_t)stream, *p, d_kps, d_desc,
@@ -1318,7 +1318,7 @@ extern "C" int plvi_search_local_stereo_batch(
     if (p->nlevels < 1 || p->nlevels > 16) return PLVI_E_BADARG;
     if (n_frames == 0) return PLVI_OK;
     const size_t smem = local2_smem(cap, cap_r, mp_cap);
-    if (smem > 160 * 1024) return PLVI_E_CAPACITY;
+    if (!lds_fits<search_local2_kernel>(smem)) return PLVI_E_CAPACITY;
     PLVI_CHECK(hipFuncSetAttribute((const void*)search_local2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)smem));
     hipLaunchKernelGGL(search_local2_kernel, dim3(n_frames), dim3(256), smem, (hipStream_t)stream, *p, d_kps, d_desc,
@@ -1414,7 +1414,7 @@ extern "C" int plvi_search_by_projection_stereo_batch(
     if (p->nlevels < 1 || p->nlevels > 16) return PLVI_E_BADARG;
     if (n_pairs == 0) return PLVI_OK;
     const size_t smem = proj2_smem(cap, cap_r, last_cap);
-    if (smem > 160 * 1024) return PLVI_E_CAPACITY;
+    if (!lds_fits<search_by_projection2_kernel>(smem)) return PLVI_E_CAPACITY;
     CamModel cm{0, 0.f, 0.f, 0.f, 0.f};
     if (kb8) cm = CamModel{1, kb8[0], kb8[1], kb8[2], kb8[3]};
     PLVI_CHECK(hipFuncSetAttribute((const void*)search_by_projection2_kernel,
@@ -1438,9 +1438,6 @@ extern "C" int plvi_search_by_projection_stereo(const plvi_proj_params* p, const
     if (!p || n < 0 || n_r < 0 || n_last < 0) return PLVI_E_BADARG;
     if ((n > 0 && (!kps || !desc || !match)) || (n_r > 0 && (!kps_r || !desc_r || !match_r))) return PLVI_E_BADARG;
     if (n_last > 0 && (!x3dc || !x3dr || !last_octave || !last_angle || !mp_desc || !last_flags)) return PLVI_E_BADARG;
-    if (n_last > 0)
-        for (int i = 0; i < n_last; ++i)
-            if ((last_flags[i] & 1) && (last_octave[i] < 0 || last_octave[i] >= p->nlevels)) return PLVI_E_BADARG;
     const int cl = std::max(n, 1), cr = std::max(n_r, 1), lc = std::max(n_last, 1);
     std::vector<size_t> off;
     size_t tot = 0;

@@ -509,7 +509,7 @@ extern "C" int plvi_vocab_transform_batch(plvi_vocabulary* h, const uint8_t* d_d
     }
     const int P = bow_pow2(cap);
     const size_t smem = bow_smem(P);
-    if (smem > 160 * 1024) return PLVI_E_CAPACITY;
+    if (!lds_fits<bow_transform_kernel>(smem)) return PLVI_E_CAPACITY;
     PLVI_CHECK(hipFuncSetAttribute((const void*)bow_transform_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    (int)smem));
     const int must = v.scoring != 5, l2 = v.scoring == 1, tf = v.weighting == 0 || v.weighting == 1;

@@ -3,7 +3,12 @@ distances (ORBmatcher.cc:2350-2366, LineMatcher.cpp:487-499).
 
 Parity unpinned: the reference has no tests for SearchByBoW (SURVEY §8c);
 the oracle restates the cited lines and is checked here on hand-built known
-answers, then the HIP kernel is compared with it on synthetic FeatureVectors."""
+answers, then the HIP kernel is compared with it on synthetic FeatureVectors.
+
+Two-camera Frames (F.Nleft != -1, ORBmatcher.cc:321-420): the right-image
+ratio test is `... || true` (ORBmatcher.cc:405), i.e. every right best match
+within TH_LOW is kept; the oracle (match_oracle.cpp) and the kernel (bow.hip)
+both encode that (test_oracle_search_by_bow_two_cameras_known_answers)."""
 import numpy as np
 import pytest
 

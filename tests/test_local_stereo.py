@@ -8,7 +8,11 @@ mvRightToLeftMatch), and a left ratio-test failure skips the MapPoint's right se
 Parity unpinned: the reference has no tests for it.  The C++ oracle (oracle/proj_oracle.cpp:
 oracle_search_local2) restates the cited lines and is checked here against a pure-Python restatement; the
 HIP path (search_local2_kernel, csrc/proj.hip) is compared with the oracle exactly (both match tables incl.
-overwrites, nmatches)."""
+overwrites, nmatches).
+
+Reference quirks encoded by both: a left ratio-test failure `continue`s past the right search
+(ORBmatcher.cc:126-127); the far-point test reads the left mTrackDepth for both images (:56; stale when only
+the right camera sees the point -- plvi_frustum_points_batch keeps that value, tests/test_frustum.py)."""
 import math
 
 import numpy as np

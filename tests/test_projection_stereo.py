@@ -9,7 +9,13 @@ oracle_search_by_projection2, host libm for atan2f / cosf / sinf as the referenc
 cited lines; with a Pinhole rig it is checked here against the one-camera oracle on a frame whose right image
 is empty, and its KannalaBrandt8 projection against a float64 model; the HIP path (search_by_projection2_kernel,
 csrc/proj.hip, glibc atan2f / cosf / sinf restated in csrc/plvi_math.h) is compared with the oracle exactly
-(both match tables incl. overwrites and the rotation filter's NULLs, nmatches)."""
+(both match tables incl. overwrites and the rotation filter's NULLs, nmatches).
+
+Reference quirks the oracle and the kernel both encode (a change to either
+must keep them): the right pass projects x3Dr with CurrentFrame.mpCamera, not
+mpCamera2 (ORBmatcher.cc:2087); the right projection has no mnMin/MaxX/Y
+bounds test (:2085-2093, unlike the left one at :2005-2008); the right window
+uses the LastFrame point's own octave (:2089-2090)."""
 import numpy as np
 import pytest
 
@@ -85,6 +91,65 @@ def test_stereo_projection_no_rotation_check_and_degenerate():
             util.proj_params(d, 7.0), d["kps"], d["desc"], d["kps_r"], d["desc_r"], d["x3dc"], d["x3dr"],
             d["last_octave"], d["last_angle"], d["mp_desc"], d["flags"], d["kb8"], d["blocked"], d["blocked_r"])
         assert ng == ne and np.array_equal(mlg, mle) and np.array_equal(mrg, mre), cut
+
+
+@pytest.mark.gpu
+def test_stereo_projection_invalid_octave_is_no_candidate():
+    """A searched LastFrame point whose octave is outside [0, nlevels) (the reference would index
+    mvScaleFactors out of range, ORBmatcher.cc:2029) gets no candidate in either image, in the one-pair
+    and the batched entry point alike (the one-pair wrapper runs the batch kernel): the result equals the
+    oracle's with those points unflagged."""
+    import plvi
+    c = util.projection_stereo_case(41)
+    rng = np.random.default_rng(5)
+    bad = np.nonzero(c["flags"] & 1)[0]
+    bad = rng.choice(bad, 40, replace=False)
+    d = dict(c)
+    d["last_octave"] = c["last_octave"].copy()
+    d["last_octave"][bad[:20]] = -1
+    d["last_octave"][bad[20:]] = 8
+    e = dict(c)
+    e["flags"] = c["flags"].copy()
+    e["flags"][bad] &= ~np.uint8(1)
+    ne, mle, mre = oracle_lib.search_by_projection_stereo(e, 7.0)
+    ng, mlg, mrg = plvi.ORBmatcher(0.9, True).SearchByProjectionStereo(
+        util.proj_params(d, 7.0), d["kps"], d["desc"], d["kps_r"], d["desc_r"], d["x3dc"], d["x3dr"],
+        d["last_octave"], d["last_angle"], d["mp_desc"], d["flags"], d["kb8"], d["blocked"], d["blocked_r"])
+    assert ng == ne and np.array_equal(mlg, mle) and np.array_equal(mrg, mre)
+
+
+@pytest.mark.gpu
+def test_stereo_lds_check_counts_static_shared():
+    """The LDS capacity checks count the kernels' static __shared__ data (the rotation histogram and
+    counters of the two-camera and relocalization SearchByProjection kernels): a configuration whose
+    dynamic LDS alone is exactly 160 KB returns PLVI_E_CAPACITY; the local-map stereo kernel has no static
+    LDS, so 160 KB launches and 16 B more is refused.  Every pointer is one zeroed device buffer (all
+    counts 0), so a launch is harmless."""
+    import ctypes
+    import plvi
+    lib = plvi.load()
+    z = plvi.DeviceBuffer(1 << 20)
+    z.upload(np.zeros(1 << 20, np.uint8))
+    Z = ctypes.c_void_p(z.ptr)
+    pp = plvi.ProjParams()
+    pp.nlevels = 8
+    # proj2: 16*last + 2*((18*cap + 4*3073 + 15) & ~15) + 64 == 163840 at cap 2000, last 4198
+    rc = lib.plvi_search_by_projection_stereo_batch(1, ctypes.byref(pp), None, Z, Z, Z, 2000, *([Z] * 6), 2000,
+                                                    *([Z] * 10), 4198, Z, Z, Z, None)
+    assert rc == plvi.PLVI_E_CAPACITY
+    rp = plvi.RelocParams()
+    rp.nlevels, rp.orb_dist = 8, 50
+    # reloc: 17*cur + 8*kf + 4*3073 + 64 == 163840 at cur 4004, kf 10427
+    rc = lib.plvi_search_reloc_batch(1, ctypes.byref(rp), Z, Z, Z, 4004, *([Z] * 10), 10427, Z, Z, None)
+    assert rc == plvi.PLVI_E_CAPACITY
+    lp = plvi.LocalParams()
+    lp.nlevels = 8
+    # local2: 16*mp + 2*((17*cap + 4*3073 + 15) & ~15) + 64 == 163840 at cap 2000, mp 4448
+    for mp, want in ((4449, plvi.PLVI_E_CAPACITY), (4448, 0)):
+        rc = lib.plvi_search_local_stereo_batch(1, ctypes.byref(lp), Z, Z, Z, 2000, *([Z] * 7), 2000, *([Z] * 11),
+                                                mp, Z, Z, Z, None)
+        assert rc == want, mp
+    lib.plvi_device_synchronize()
 
 
 @pytest.mark.gpu
