@@ -133,6 +133,42 @@ def committed_traffic(batch, kernel):
     return v
 
 
+def committed_pmc(batch, kernel, field):
+    """A per-launch PMC field (e.g. valu_insts_per_launch) of `kernel` from the
+    committed passes (profiles/*/pmc_traffic*.json), taken at this batch size."""
+    best = None
+    for f in sorted(ROOT.glob("profiles/*/pmc_traffic*.json")):
+        try:
+            d = json.loads(f.read_text())
+        except ValueError:
+            continue
+        for e in d if isinstance(d, list) else [d]:
+            if e.get("batch") == batch and e.get("kernel") == kernel and field in e:
+                best = e[field]
+    return best
+
+
+# VALU issue peak: 256 CUs x 4 SIMDs, a wave64 VALU instruction issues over 2
+# cycles on a SIMD-32 (MI355X_MICROARCH.md, execution model), 2.4 GHz
+VALU_PEAK_WIPS = 256 * 4 * 2.4e9 / 2
+
+
+def valu_roof(batch, kernel, ms_timed, ms_iso):
+    """roofline.valu: the kernel's VALU wave-instructions per launch (committed
+    PMC pass) / launch duration / the chip's VALU issue peak."""
+    n = committed_pmc(batch, kernel, "valu_insts_per_launch")
+    if not n:
+        return None
+    r = {"insts_per_launch": n, "peak": VALU_PEAK_WIPS, "unit": "wave-instructions/s",
+         "source": "SQ_INSTS_VALU, tools/gpu_traffic.sh pass 3 (profiles/*/pmc_traffic.json)"}
+    if ms_timed:
+        r["achieved"] = n / (ms_timed * 1e-3)
+        r["frac"] = r["achieved"] / VALU_PEAK_WIPS
+    if ms_iso:
+        r["isolated_frac"] = n / (ms_iso * 1e-3) / VALU_PEAK_WIPS
+    return r
+
+
 def free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -736,6 +772,9 @@ def run(args, world, rank):
             "kernel_bytes_frac": blur_fast_kernel_bytes(W, H) * B / (bf_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "avg_launch_ms": bf_ms, "launches": kn}
     roof["frac"] = roof["achieved"] / roof["peak"]
+    if (W, H) == (640, 480):
+        roof["valu"] = valu_roof(B, "orb_blur_fast_kernel", bf_ms if kn else None,
+                                 bf_iso[0] / bf_iso[1] if bf_iso[1] else None)
     if bf_iso[1]:
         # the same launch with nothing beside it (stage-timing runs): the timed
         # figure above shares the CUs with region growing and the other batch
@@ -754,6 +793,9 @@ def run(args, world, rank):
                 "avg_launch_ms": py_ms, "launches": pn}
     if roof_pyr["achieved"]:
         roof_pyr["frac"] = roof_pyr["achieved"] / HBM_PEAK_GBS
+    if (W, H) == (640, 480):
+        roof_pyr["valu"] = valu_roof(B, "orb_pyramid_kernel", py_ms if pn else None,
+                                     pyr_iso[0] / pyr_iso[1] if pyr_iso[1] else None)
     if pyr_iso[1]:
         i_ms = pyr_iso[0] / pyr_iso[1]
         roof_pyr["isolated"] = {"avg_launch_ms": i_ms, "launches": pyr_iso[1],

@@ -81,3 +81,21 @@ def test_pyramid_bytes_are_survey_orb_resize():
     b = _bench()
     assert b.pyramid_bytes(640, 480) == 1569878
     assert b.pyramid_bytes(640, 480) + b.blur_fast_bytes(640, 480) == 4421474
+
+
+def test_valu_roof_is_pmc_instructions_over_launch_over_issue_peak(tmp_path, monkeypatch):
+    """roofline.valu = SQ_INSTS_VALU per launch (committed pass) / launch time / the chip's VALU issue
+    peak: 256 CUs x 4 SIMD-32 x 2.4 GHz / 2 cycles per wave64 instruction."""
+    import json
+    b = _bench()
+    assert b.VALU_PEAK_WIPS == 256 * 4 * 2.4e9 / 2
+    (tmp_path / "profiles" / "rX").mkdir(parents=True)
+    (tmp_path / "profiles" / "rX" / "pmc_traffic.json").write_text(json.dumps(
+        [{"kernel": "orb_blur_fast_kernel", "batch": 3072, "bytes_per_launch": 1.0, "unit": "bytes per launch",
+          "valu_insts_per_launch": 6.0e9}]))
+    monkeypatch.setattr(b, "ROOT", tmp_path)
+    r = b.valu_roof(3072, "orb_blur_fast_kernel", 10.0, 5.0)
+    assert r["insts_per_launch"] == 6.0e9
+    assert abs(r["frac"] - 6.0e9 / 10e-3 / b.VALU_PEAK_WIPS) < 1e-12
+    assert abs(r["isolated_frac"] - 6.0e9 / 5e-3 / b.VALU_PEAK_WIPS) < 1e-12
+    assert b.valu_roof(64, "orb_blur_fast_kernel", 10.0, 5.0) is None  # other batch size: not measured

@@ -11,6 +11,11 @@ with the widths the kernels use and give the bytes-per-counted-byte factor:
   reads  of lbd_sobel0/1_kernel:  dword loads  -> calib_dword_read
   writes of lbd_sobel0_kernel:    dword blur stores (1 B/px) + 16-B Sobel stores (4 B/px): 1/5 dword, 4/5 dwordx4
   writes of lbd_sobel1_kernel:    4-B Sobel stores (short2 per pixel) -> calib_dword_copy
+  reads  of orb_pyramid_kernel:   dword loads of level 0 -> calib_dword_read
+  writes of orb_pyramid_kernel:   1 B per lane stores (levels 1..7) -> calib_byte_copy
+A third pass (SQ_INSTS_VALU, SQ_INSTS_SALU, SQ_INSTS_LDS, SQ_WAVES; pmc_VALU/)
+adds the per-launch wave-instruction counts of each kernel (valu_insts_per_launch
+...), the numerator of bench.py's roofline.valu.
 Writes profiles/<round>/pmc_traffic.json (a list, one entry per kernel) for bench.py.
 usage: python tools/pmc_traffic.py <pmc_dir> profiles/r03 BATCH CAL_BYTES"""
 import csv
@@ -30,6 +35,15 @@ def per_kernel(path, counter):
     return out
 
 
+def per_kernel_all(path):
+    """{counter: {kernel: [value per dispatch]}} of one pass."""
+    out = defaultdict(lambda: defaultdict(list))
+    for r in csv.DictReader(open(path)):
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("plvi::", "")
+        out[r["Counter_Name"]][name].append(float(r["Counter_Value"]))
+    return out
+
+
 def main():
     d, dst, batch, cal_bytes = pathlib.Path(sys.argv[1]), pathlib.Path(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
     fe = per_kernel(next(d.glob("pmc_FETCH_SIZE/**/*counter_collection.csv")), "FETCH_SIZE")
@@ -45,8 +59,11 @@ def main():
              "write_dwordx4": f_wr16, "write_byte": f_wr1,
              "note": "true bytes per counted byte, from calibration kernels streaming %d B" % cal_bytes}
     entries = []
+    vp = list(d.glob("pmc_VALU/**/*counter_collection.csv"))
+    sq = per_kernel_all(vp[0]) if vp else {}
     for k, fr, fw in (("orb_blur_fast_kernel", f_rd, f_wr4), ("lsd_prep_kernel", f_rd, (f_wr4 + f_wr8) / 2),
-                      ("lbd_sobel0_kernel", f_rd, 0.2 * f_wr4 + 0.8 * f_wr16), ("lbd_sobel1_kernel", f_rd, f_wr4)):
+                      ("lbd_sobel0_kernel", f_rd, 0.2 * f_wr4 + 0.8 * f_wr16), ("lbd_sobel1_kernel", f_rd, f_wr4),
+                      ("orb_pyramid_kernel", f_rd, f_wr1)):
         if k not in fe or k not in wr:
             continue
         if k == "lsd_prep_kernel":  # two launches per batch (octaves): mean of the first pair
@@ -58,6 +75,12 @@ def main():
                         "fetch_bytes": rf * fr, "write_bytes": rw * fw, "bytes_per_launch": rf * fr + rw * fw,
                         "unit": "bytes per launch",
                         "calibration": calib})
+        for c, field in (("SQ_INSTS_VALU", "valu_insts_per_launch"), ("SQ_INSTS_SALU", "salu_insts_per_launch"),
+                         ("SQ_INSTS_LDS", "lds_insts_per_launch"), ("SQ_WAVES", "waves_per_launch")):
+            v = sq.get(c, {}).get(k)
+            if v:
+                # lsd_prep: two launches per batch (octaves), the mean of the first pair
+                entries[-1][field] = (v[0] + v[1]) / 2 if k == "lsd_prep_kernel" and len(v) > 1 else mean(v)
     dst.mkdir(parents=True, exist_ok=True)
     (dst / "pmc_traffic.json").write_text(json.dumps(entries, indent=1) + "\n")
     print(json.dumps(entries, indent=1))
