@@ -413,15 +413,9 @@ __device__ __forceinline__ s16x2 fast_S_ring2(const uint8_t (*rg)[kRingW], int y
     return __builtin_elementwise_max(A, -Bm);
 }
 
-#ifndef PLVI_BF_WPE
-#define PLVI_BF_WPE 1  // waves per EU blur + FAST is compiled for (1: no cap)
-#endif
-#ifdef PLVI_BF_VGPR  // hard VGPR cap (A/B builds)
-#define PLVI_BF_NUMVGPR __attribute__((amdgpu_num_vgpr(PLVI_BF_VGPR)))
-#else
-#define PLVI_BF_NUMVGPR
-#endif
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(PLVI_BF_WPE))) PLVI_BF_NUMVGPR void orb_blur_fast_kernel(const OrbLevelDev* __restrict__ lvs,
+// occupancy: 6 waves/SIMD, set by the 6.4 KB of LDS per wave (79 VGPRs fit
+// under that; a waves-per-EU or VGPR cap above 6 waves cannot take effect)
+__global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __restrict__ lvs,
                                                            const OrbStripDev* __restrict__ strips,
                                                            const uint8_t* __restrict__ frames, size_t f_frame,
                                                            size_t f_row, uint8_t* __restrict__ pyr,
