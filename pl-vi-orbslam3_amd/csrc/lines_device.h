@@ -8,6 +8,8 @@ namespace plvi {
 
 constexpr int kLineMaxOct = 2;      // Lineextractor nlevels (config: 2)
 constexpr int kLsdRawCap = 8192;    // LSD segments per (frame, octave)
+constexpr int kPrepBands = 8;       // row bands of the LSD prep for batches <= kPrepBandMax frames
+constexpr int kPrepBandMax = 256;
 
 
 struct LineOctDev {
@@ -26,6 +28,9 @@ struct LineOctDev {
     // lsd_prep2_kernel column strips (int4 {X0, X1, gx0, nc}, offset in the table buffer)
     long long tabStrips;
     int nstrips;
+    // lsd_prep_kernel row bands (int4 {dyA, dyB, ybase0, 0}): one band, or
+    // kPrepBands for small batches (offsets in the table buffer)
+    long long tabBands1, tabBandsK;
     // Sobel/LBD pyramid (computeGaussianPyramid): dims and offsets
     int lw, lh;
     long long loff, lplane;

@@ -91,6 +91,7 @@ __device__ __forceinline__ double dpp_from_right_d(double v) {
 
 __global__ __launch_bounds__(64) void lsd_prep_kernel(const uint8_t* __restrict__ src, size_t s_frame, size_t s_row,
                                                        int gw, int gh, int sw, int sh, const int4* __restrict__ strips,
+                                                       const int4* __restrict__ bands,
                                                        const int* __restrict__ xofs, const float* __restrict__ xa,
                                                        int xmax, const int* __restrict__ yrow,
                                                        const float* __restrict__ yb, double k0, double k1, double k2,
@@ -100,6 +101,12 @@ __global__ __launch_bounds__(64) void lsd_prep_kernel(const uint8_t* __restrict_
     __shared__ int hostdx[64];
     const int4 sd = strips[blockIdx.x];
     const int f = blockIdx.y;
+    // row band: scaled rows [dyA, dyB) from source rows ybase0.. (the band's
+    // first G row needs the 6 rows above it; earlier rows of the 7-slot
+    // window are never read)
+    const int4 bd = bands[blockIdx.z];
+    const int dyA = bd.x, dyB = bd.y, ybase0 = bd.z;
+    const int dyEnd = dyB < sh ? dyB + 1 : sh;  // scaled rows processed (one past the band: its Sc)
     const int X0 = sd.x, X1 = sd.y, gx0 = sd.z, nc = sd.w;
     const int lane = threadIdx.x;
     // compact lane t = lane takes scaled column X0 + t from lane Lt (the one
@@ -122,10 +129,10 @@ __global__ __launch_bounds__(64) void lsd_prep_kernel(const uint8_t* __restrict_
     const int yend = gh + 3;  // source rows -3 .. gh+2 (reflect-101)
     uint32_t pb[7];
 #pragma unroll
-    for (int k = 0; k < 7; ++k) pb[k] = S[(size_t)reflect101(k - 3, gh) * s_row];
+    for (int k = 0; k < 7; ++k) pb[k] = S[(size_t)reflect101(ybase0 + k, gh) * s_row];
     double Hw[7];
     double Gprev = 0.0, Gprevn = 0.0, Sp = 0.0, Spn = 0.0;
-    int dy = 0;
+    int dy = dyA;
     // gradient / angle / cos-sin of scaled row y from rows y (Sp, Spn) and y + 1 (Sc, Scn)
     auto emit = [&](int y, double Sc, double Scn) {
         if (lane >= nout) return;
@@ -148,11 +155,11 @@ __global__ __launch_bounds__(64) void lsd_prep_kernel(const uint8_t* __restrict_
             CS[o] = make_float2(pc, ps);
         }
     };
-    for (int ybase = -3; ybase < yend; ybase += 7) {
+    for (int ybase = ybase0; ybase < yend && dy < dyEnd; ybase += 7) {
 #pragma unroll
         for (int k = 0; k < 7; ++k) {
             const int y = ybase + k;
-            if (y >= yend) break;
+            if (y >= yend || dy >= dyEnd) break;
             const int v0 = (int)pb[k];
             if (y + 7 < yend) pb[k] = S[(size_t)reflect101(y + 7, gh) * s_row];
             // RowFilter: sequential sum over columns c-3 .. c+3
@@ -165,16 +172,16 @@ __global__ __launch_bounds__(64) void lsd_prep_kernel(const uint8_t* __restrict_
             s += k2 * (double)r1;
             s += k1 * (double)r2;
             s += k0 * (double)r3;
-            Hw[k] = s;  // slot k = source row ybase + k (ybase = -3 mod 7)
+            Hw[k] = s;  // slot k = source row ybase + k
             const int g = y - 3;
-            if (g < 0) continue;
+            if (g < ybase0 + 3) continue;  // rows g-3 .. g+3 not all streamed yet
             // SymmColumnFilter over rows g-3 .. g+3 (slots k+1 .. k+7 mod 7)
             double G = k3 * Hw[(k + 4) % 7] + 0.0;
             G += k2 * (Hw[(k + 5) % 7] + Hw[(k + 3) % 7]);
             G += k1 * (Hw[(k + 6) % 7] + Hw[(k + 2) % 7]);
             G += k0 * (Hw[k] + Hw[(k + 1) % 7]);
             const double Gn = dpp_from_right_d(G);
-            while (dy < sh && yrow[2 * dy + 1] == g) {
+            while (dy < dyEnd && yrow[2 * dy + 1] == g) {
                 const bool same = yrow[2 * dy] == g;  // else g - 1
                 const double G0 = same ? G : Gprev, G0n = same ? Gn : Gprevn;
                 const double b0 = (double)yb[2 * dy], b1 = (double)yb[2 * dy + 1];
@@ -189,7 +196,7 @@ __global__ __launch_bounds__(64) void lsd_prep_kernel(const uint8_t* __restrict_
                 const double Sv = H0 * b0 + H1 * b1;
                 const double Sc = shfl_d(Sv, Lt);
                 const double Scn = dpp_from_right_d(Sc);
-                if (dy > 0) emit(dy - 1, Sc, Scn);
+                if (dy > dyA) emit(dy - 1, Sc, Scn);
                 Sp = Sc;
                 Spn = Scn;
                 ++dy;
@@ -198,7 +205,7 @@ __global__ __launch_bounds__(64) void lsd_prep_kernel(const uint8_t* __restrict_
             Gprevn = Gn;
         }
     }
-    emit(sh - 1, 0.0, 0.0);  // last row: NOTDEF (ll_angle leaves row h-1 undefined)
+    if (dyB == sh) emit(sh - 1, 0.0, 0.0);  // last row: NOTDEF (ll_angle leaves row h-1 undefined)
 }
 
 // ---------------------------------------------------------------------------

@@ -345,6 +345,18 @@ struct LinePipeline {
                 }
                 d.nstrips = (int)strips.size() / 4;
                 d.tabStrips = put(strips.data(), strips.size() * 4);
+                // row bands: scaled rows [dyA, dyB) and the first source row
+                // a band streams (its first G row needs source rows from
+                // yrow[2 dyA] - 3); one band per strip for large batches,
+                // kPrepBands for small ones (latency: more waves per frame)
+                for (int nb : {1, kPrepBands}) {
+                    std::vector<int> bands;
+                    for (int b = 0; b < nb; ++b) {
+                        const int dyA = (int)((long long)d.sh * b / nb), dyB = (int)((long long)d.sh * (b + 1) / nb);
+                        bands.insert(bands.end(), {dyA, dyB, dyA == 0 ? -3 : yrow[2 * dyA] - 3, 0});
+                    }
+                    (nb == 1 ? d.tabBands1 : d.tabBandsK) = put(bands.data(), bands.size() * 4);
+                }
                 d.tabXofs = put(xofs.data(), xofs.size() * 4);
                 d.tabXa = put(xa.data(), xa.size() * 4);
                 d.tabYrow = put(yrow.data(), yrow.size() * 4);
@@ -515,8 +527,10 @@ struct LinePipeline {
             const size_t sr = l == 0 ? row_stride : (size_t)d.w;
             const bool kt = ktime && kn < kKRing;
             if (kt) (void)hipEventRecord(kev[2 * kn], st);
-            hipLaunchKernelGGL(lsd_prep_kernel, dim3(d.nstrips, nf), dim3(64), 0, st, s, sf, sr, d.w, d.h, d.sw,
-                               d.sh, (const int4*)(T + d.tabStrips), (const int*)(T + d.tabXofs),
+            const bool banded = nf <= kPrepBandMax;
+            hipLaunchKernelGGL(lsd_prep_kernel, dim3(d.nstrips, nf, banded ? kPrepBands : 1), dim3(64), 0, st, s, sf,
+                               sr, d.w, d.h, d.sw, d.sh, (const int4*)(T + d.tabStrips),
+                               (const int4*)(T + (banded ? d.tabBandsK : d.tabBands1)), (const int*)(T + d.tabXofs),
                                (const float*)(T + d.tabXa), d.xmax, (const int*)(T + d.tabYrow),
                                (const float*)(T + d.tabYb), gk[0], gk[1], gk[2], gk[3], rho,
                                pix.as<float>() + d.soff, modg.as<double>() + d.soff, seedcs.as<float2>() + d.soff,
