@@ -1095,15 +1095,13 @@ def extra_lines(args, torch, plvi, synth, lib, stream, W, H, seed0, orb, lx, ext
     lsc = torch.empty(4 * (b64 - 1) * 2 * lcap, **i32)
     lm = torch.empty((b64 - 1) * lcap, **i32)
     lnm = torch.empty(b64 - 1, **i32)
-
+    # the step's matching issued inside the frame schedule: the ORB kNN-2
+    # right behind the ORB chain, LineMatcher::match right behind the LBD
+    # descriptors (plvi_frame_extract_match_batch; same kernels and outputs as
+    # the calls after the schedule, minus the stream joins in between)
     def step64():
-        plvi.frame_extract_batch(o64, l64, seq.data_ptr(), b64, W * H, W, (0, 0), stream=st)
-        rc = lib.plvi_hamming_knn2_batch(de + cap * 32, co + 4, cap, de, co, cap, b64 - 1, *[o.data_ptr() for o in o4],
-                                         st)
-        rc |= lib.plvi_line_match_batch(lde + lcap * 32, lco + 4, lcap, lde, lco, lcap, b64 - 1, 0.9, lsc.data_ptr(),
-                                        lm.data_ptr(), lnm.data_ptr(), st)
-        if rc:
-            raise RuntimeError("b64 match")
+        plvi.frame_extract_match_batch(o64, l64, seq.data_ptr(), b64, W * H, W, [o.data_ptr() for o in o4], 0.9,
+                                       lsc.data_ptr(), lm.data_ptr(), lnm.data_ptr(), stream=st)
     for _ in range(3):
         step64()
     torch.cuda.synchronize()

@@ -897,6 +897,26 @@ int plvi_stereo_lines(const plvi_keyline* klL, const uint8_t* descL, int nL, con
 int plvi_frame_extract_batch(plvi_orb_extractor* orb, plvi_line_extractor* lines, const uint8_t* d_frames,
                              int n_frames, size_t frame_stride, size_t row_stride, int lap0, int lap1, void* stream);
 
+/* plvi_frame_extract_batch followed by the step's matching of every frame t
+ * in the batch against frame t-1: the ORB kNN-2 (plvi_hamming_knn2_batch of
+ * descriptor rows t vs t-1: outputs [n_frames-1][orb cap]) issued on the
+ * schedule's ORB stream as soon as the ORB extraction is done, and
+ * LineMatcher::match (plvi_line_match_batch, nnr, scratch as there: outputs
+ * [n_frames-1][line cap]) on the line path's stream right after the LBD
+ * descriptors -- no join of the schedule's streams in between.  Joins
+ * `stream` at the end.  n_frames >= 2. */
+int plvi_frame_extract_match_batch(plvi_orb_extractor* orb, plvi_line_extractor* lines, const uint8_t* d_frames,
+                                   int n_frames, size_t frame_stride, size_t row_stride, int lap0, int lap1,
+                                   int* d_idx0, int* d_d0, int* d_idx1, int* d_d1, float nnr, int* d_line_scratch,
+                                   int* d_line_matches, int* d_line_nmatch, void* stream);
+
+/* The event the last plvi_frame_extract_batch on `lines` recorded once its
+ * ORB extraction was complete (a hipEvent_t owned by the handle, re-recorded
+ * by the next call): work on the ORB tables -- kNN-2 against the previous
+ * frame -- can wait on it (plvi_stream_wait_event) and overlap the rest of
+ * the line path instead of waiting for the whole frame. */
+int plvi_frame_orb_event(plvi_line_extractor* lines, void** event);
+
 /* ------------------------------------------------------------ initialization
  * The monocular initializer's matchers, called on every frame until
  * Tracking::MonocularInitialization succeeds (src/Tracking.cc:3111-3113). */
@@ -966,6 +986,12 @@ int plvi_device_synchronize(void);
 int plvi_stream_create(void** stream);
 int plvi_stream_destroy(void* stream);
 int plvi_stream_synchronize(void* stream);
+/* Events for the same bindings (hipEventCreateWithFlags(hipEventDisableTiming),
+ * hipEventRecord, hipStreamWaitEvent, hipEventDestroy). */
+int plvi_event_create(void** event);
+int plvi_event_record(void* event, void* stream);
+int plvi_stream_wait_event(void* stream, void* event);
+int plvi_event_destroy(void* event);
 
 /* HIP graphs (no reference counterpart: a runtime facility of this
  * library).  plvi_graph_capture_begin starts capturing `stream` (a created

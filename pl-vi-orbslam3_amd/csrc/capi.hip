@@ -62,6 +62,32 @@ extern "C" int plvi_stream_synchronize(void* stream) {
     return PLVI_OK;
 }
 
+extern "C" int plvi_event_create(void** event) {
+    if (!event) return PLVI_E_BADARG;
+    hipEvent_t e = nullptr;
+    PLVI_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    *event = (void*)e;
+    return PLVI_OK;
+}
+
+extern "C" int plvi_event_record(void* event, void* stream) {
+    if (!event) return PLVI_E_BADARG;
+    PLVI_CHECK(hipEventRecord((hipEvent_t)event, (hipStream_t)stream));
+    return PLVI_OK;
+}
+
+extern "C" int plvi_stream_wait_event(void* stream, void* event) {
+    if (!event) return PLVI_E_BADARG;
+    PLVI_CHECK(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0));
+    return PLVI_OK;
+}
+
+extern "C" int plvi_event_destroy(void* event) {
+    if (!event) return PLVI_E_BADARG;
+    PLVI_CHECK(hipEventDestroy((hipEvent_t)event));
+    return PLVI_OK;
+}
+
 // HIP graphs: a batch step (any sequence of plvi_* calls on `stream`, their
 // internal streams joined by events) captured once and replayed with one
 // launch, which takes the per-call host work (~100 API calls per frame

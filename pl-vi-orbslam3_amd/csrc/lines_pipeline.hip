@@ -670,8 +670,14 @@ struct LinePipeline {
     // schedule: the latency-bound region growing runs while the ORB
     // extractor and the LBD Sobel pyramid fill the machine on two more
     // streams; everything joins back on `st`.
+    // the step's matching, issued inside the schedule (plvi_frame_extract_match_batch)
+    struct StepMatch {
+        int *idx0, *d0, *idx1, *d1;
+        float nnr;
+        int *lscratch, *lm12, *lnm;
+    };
     int run_with_orb(const uint8_t* d_frames, int nf, size_t frame_stride, size_t row_stride, hipStream_t st,
-                     plvi_orb_extractor* orb, int lap0, int lap1) {
+                     plvi_orb_extractor* orb, int lap0, int lap1, const StepMatch* sm = nullptr) {
         if (nf <= 0 || nf > Bcap) return PLVI_E_BADARG;
         if (!st) st = stream;
         lastFrames = nf;
@@ -707,6 +713,16 @@ struct LinePipeline {
         int rc = plvi_orb_extract_batch(orb, d_frames, nf, frame_stride, row_stride, lap0, lap1, aux[0]);
         if (waitBlur) plvi_orb_internal_blur_event(orb, nullptr);
         if (sobelLate) plvi_orb_internal_stage_event(orb, -1, nullptr);
+        if (sm && !rc) {
+            // ORB kNN-2 of frame t vs t-1 right behind the ORB chain
+            plvi_keypoint* kp = nullptr;
+            uint8_t* de = nullptr;
+            int *co = nullptr, *mo = nullptr, cap = 0;
+            rc = plvi_orb_outputs(orb, &kp, &de, &co, &mo, &cap);
+            if (!rc)
+                rc = plvi_hamming_knn2_batch(de + (size_t)cap * 32, co + 1, cap, de, co, cap, nf - 1, sm->idx0, sm->d0,
+                                             sm->idx1, sm->d1, aux[0]);
+        }
         PLVI_CHECK(hipEventRecord(evOrb, aux[0]));
         // split: octave 0 (the long waves, 3 per SIMD at 3072 frames) grows
         // right after the prep and leaves room for the ORB pyramid and blur +
@@ -744,6 +760,13 @@ struct LinePipeline {
             PLVI_CHECK(hipStreamWaitEvent(crit, evSobel, 0));
         }
         launch_describe(nf, crit);
+        if (sm && !rc) {
+            // LineMatcher::match of frame t vs t-1 right behind the LBD descriptors
+            uint8_t* ld = descOut.as<uint8_t>();
+            int* lc = cntOut.as<int>();
+            rc = plvi_line_match_batch(ld + (size_t)fcap * 32, lc + 1, fcap, ld, lc, fcap, nf - 1, sm->nnr,
+                                       sm->lscratch, sm->lm12, sm->lnm, crit);
+        }
         if (crit != st) {
             PLVI_CHECK(hipEventRecord(evCrit, crit));
             PLVI_CHECK(hipStreamWaitEvent(st, evCrit, 0));
@@ -822,6 +845,33 @@ extern "C" int plvi_frame_extract_batch(plvi_orb_extractor* orb, plvi_line_extra
         if (cs != hipStreamCaptureStatusNone && ver < 70200000) return PLVI_E_CAPTURE;
     }
     return lines->p().run_with_orb(d_frames, n_frames, frame_stride, row_stride, (hipStream_t)stream, orb, lap0, lap1);
+}
+
+extern "C" int plvi_frame_extract_match_batch(plvi_orb_extractor* orb, plvi_line_extractor* lines,
+                                              const uint8_t* d_frames, int n_frames, size_t frame_stride,
+                                              size_t row_stride, int lap0, int lap1, int* d_idx0, int* d_d0,
+                                              int* d_idx1, int* d_d1, float nnr, int* d_line_scratch,
+                                              int* d_line_matches, int* d_line_nmatch, void* stream) {
+    if (!orb || !lines || !d_frames || n_frames < 2 || !d_idx0 || !d_d0 || !d_idx1 || !d_d1 || !d_line_scratch ||
+        !d_line_matches || !d_line_nmatch)
+        return PLVI_E_BADARG;
+    PLVI_CHECK(hipSetDevice(lines->p().device));
+    if (stream) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        PLVI_CHECK(hipStreamIsCapturing((hipStream_t)stream, &cs));
+        int ver = 0;
+        PLVI_CHECK(hipRuntimeGetVersion(&ver));
+        if (cs != hipStreamCaptureStatusNone && ver < 70200000) return PLVI_E_CAPTURE;
+    }
+    const LinePipeline::StepMatch sm{d_idx0, d_d0, d_idx1, d_d1, nnr, d_line_scratch, d_line_matches, d_line_nmatch};
+    return lines->p().run_with_orb(d_frames, n_frames, frame_stride, row_stride, (hipStream_t)stream, orb, lap0,
+                                   lap1, &sm);
+}
+
+extern "C" int plvi_frame_orb_event(plvi_line_extractor* lines, void** event) {
+    if (!lines || !event) return PLVI_E_BADARG;
+    *event = (void*)lines->p().evOrb;
+    return PLVI_OK;
 }
 
 // The stereo-line Frame (src/Frame.cc:200-249): ORB left || right and lines

@@ -297,6 +297,12 @@ def _declare(lib):
         "plvi_search_by_projection_batch": ([I, V, V, V, V, I, V, V, V, V, V, V, V, V, V, V, I, V, V, V], I),
         "plvi_search_by_projection": ([V, V, V, I, V, V, V, V, V, V, V, I, V], I),
         "plvi_stereo_frame_extract_batch": ([V, V, V, V, V, V, I, S, S, I, I, V], I),
+        "plvi_event_create": ([c_void_pp], I),
+        "plvi_event_record": ([V, V], I),
+        "plvi_stream_wait_event": ([V, V], I),
+        "plvi_event_destroy": ([V], I),
+        "plvi_frame_orb_event": ([V, c_void_pp], I),
+        "plvi_frame_extract_match_batch": ([V, V, V, I, S, S, I, I, V, V, V, V, F, V, V, V, V], I),
         "plvi_stream_create": ([c_void_pp], I),
         "plvi_stream_destroy": ([V], I),
         "plvi_stream_synchronize": ([V], I),
@@ -1028,6 +1034,45 @@ def frame_extract_batch(orb, lines, d_frames_ptr, n_frames, frame_stride, row_st
     _check(load().plvi_frame_extract_batch(orb._h, lines._h, ctypes.c_void_p(d_frames_ptr), n_frames, frame_stride,
                                            row_stride, lap[0], lap[1], ctypes.c_void_p(stream or 0)),
            "plvi_frame_extract_batch")
+
+
+def frame_extract_match_batch(orb, lines, d_frames_ptr, n_frames, frame_stride, row_stride, knn_out, nnr,
+                              line_scratch, line_matches, line_nmatch, lap=(0, 0), stream=None):
+    """plvi_frame_extract_match_batch: the frame schedule plus the step's matching of frame t vs t-1 (ORB
+    kNN-2 into knn_out = (idx0, d0, idx1, d1) device pointers, LineMatcher::match into line_matches /
+    line_nmatch) issued inside the schedule's streams."""
+    V = ctypes.c_void_p
+    _check(load().plvi_frame_extract_match_batch(orb._h, lines._h, V(d_frames_ptr), n_frames, frame_stride, row_stride,
+                                                 lap[0], lap[1], *[V(p) for p in knn_out], ctypes.c_float(nnr),
+                                                 V(line_scratch), V(line_matches), V(line_nmatch), V(stream or 0)),
+           "plvi_frame_extract_match_batch")
+
+
+def frame_orb_event(lines):
+    """plvi_frame_orb_event: the hipEvent_t the last frame_extract_batch on `lines` recorded when its ORB
+    part completed (handle-owned)."""
+    e = ctypes.c_void_p()
+    _check(load().plvi_frame_orb_event(lines._h, ctypes.byref(e)), "plvi_frame_orb_event")
+    return e.value
+
+
+def event_create():
+    e = ctypes.c_void_p()
+    _check(load().plvi_event_create(ctypes.byref(e)), "plvi_event_create")
+    return e.value
+
+
+def event_record(event, stream=None):
+    _check(load().plvi_event_record(ctypes.c_void_p(event), ctypes.c_void_p(stream or 0)), "plvi_event_record")
+
+
+def stream_wait_event(stream, event):
+    _check(load().plvi_stream_wait_event(ctypes.c_void_p(stream or 0), ctypes.c_void_p(event)),
+           "plvi_stream_wait_event")
+
+
+def event_destroy(event):
+    _check(load().plvi_event_destroy(ctypes.c_void_p(event)), "plvi_event_destroy")
 
 
 def stereo_frame_extract_batch(orb_left, orb_right, lines_left, lines_right, d_left_ptr, d_right_ptr, n_frames,

@@ -201,3 +201,84 @@ def test_frame_step_hip_graph_replay():
         np.testing.assert_array_equal(a.view(np.uint8), b.view(np.uint8))
     for a, o in zip(ref_m, outs):
         np.testing.assert_array_equal(a, o.cpu().numpy())
+
+
+def test_orb_event_orders_knn_after_orb():
+    """plvi_frame_orb_event: a side stream that waits on it sees the finished ORB tables (the kNN-2 of
+    frame t against t-1 started there equals the one run after the whole schedule), while the line path
+    may still run; repeated calls re-record the handle's event."""
+    import ctypes
+    n = 12
+    frames = synth.batch(n, seed0=91)
+    buf = plvi.DeviceBuffer(frames.nbytes)
+    buf.upload(frames)
+    lib = plvi.load()
+    orb = plvi.ORBextractor(1000, 1.2, 8, 20, 7, 640, 480, max_batch=n)
+    lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 640, 480, max_batch=n)
+    kp, de, co, _, cap = orb.outputs()
+    st, side = ctypes.c_void_p(), ctypes.c_void_p()
+    assert lib.plvi_stream_create(ctypes.byref(st)) == 0 and lib.plvi_stream_create(ctypes.byref(side)) == 0
+    outs = [plvi.DeviceBuffer(4 * (n - 1) * cap) for _ in range(4)]
+    ev = plvi.event_create()
+    got = None
+    for rep in range(2):
+        plvi.frame_extract_batch(orb, lx, buf.ptr, n, 640 * 480, 640, stream=st.value)
+        plvi.stream_wait_event(side.value, plvi.frame_orb_event(lx))
+        assert lib.plvi_hamming_knn2_batch(de + cap * 32, co + 4, cap, de, co, cap, n - 1,
+                                           *[o.ptr for o in outs], side) == 0
+        plvi.event_record(ev, side.value)
+        plvi.stream_wait_event(st.value, ev)
+        assert lib.plvi_stream_synchronize(st) == 0
+        got = [o.download(np.zeros((n - 1) * cap, np.int32)) for o in outs]
+    # the reference: the same kNN after a full device synchronisation
+    lib.plvi_device_synchronize()
+    assert lib.plvi_hamming_knn2_batch(de + cap * 32, co + 4, cap, de, co, cap, n - 1, *[o.ptr for o in outs],
+                                       None) == 0
+    lib.plvi_device_synchronize()
+    ref = [o.download(np.zeros((n - 1) * cap, np.int32)) for o in outs]
+    for a, b in zip(got, ref):
+        np.testing.assert_array_equal(a, b)
+    plvi.event_destroy(ev)
+    lib.plvi_stream_destroy(st)
+    lib.plvi_stream_destroy(side)
+
+
+@pytest.mark.parametrize("n", [2, 9, 64])
+def test_frame_extract_match_equals_separate_calls(n):
+    """plvi_frame_extract_match_batch (matching issued inside the schedule's streams) = the frame schedule
+    followed by plvi_hamming_knn2_batch and plvi_line_match_batch on the caller's stream: identical tables."""
+    frames = synth.batch(n, seed0=301)
+    buf = plvi.DeviceBuffer(frames.nbytes)
+    buf.upload(frames)
+    lib = plvi.load()
+    orb = plvi.ORBextractor(1000, 1.2, 8, 20, 7, 640, 480, max_batch=n)
+    lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 640, 480, max_batch=n)
+    kp, de, co, _, cap = orb.outputs()
+    _, lde, _, lco, lcap = lx.outputs()
+    knn = [plvi.DeviceBuffer(4 * (n - 1) * cap) for _ in range(4)]
+    lsc = plvi.DeviceBuffer(4 * 4 * (n - 1) * 2 * lcap)
+    lm, lnm = plvi.DeviceBuffer(4 * (n - 1) * lcap), plvi.DeviceBuffer(4 * (n - 1))
+    sizes = [4 * (n - 1) * cap] * 4 + [4 * (n - 1) * lcap, 4 * (n - 1)]
+
+    def fill():  # the same stale contents before both runs (entries past a frame's count are not written)
+        for b, nb in zip(knn + [lm, lnm], sizes):
+            b.upload(np.full(nb, 0xAB, np.uint8))
+    fill()
+    plvi.frame_extract_batch(orb, lx, buf.ptr, n, 640 * 480, 640)
+    lib.plvi_device_synchronize()  # (the null stream does not order after the handles' non-blocking streams)
+    assert lib.plvi_hamming_knn2_batch(de + cap * 32, co + 4, cap, de, co, cap, n - 1, *[b.ptr for b in knn],
+                                       None) == 0
+    assert lib.plvi_line_match_batch(lde + lcap * 32, lco + 4, lcap, lde, lco, lcap, n - 1, 0.9, lsc.ptr, lm.ptr,
+                                     lnm.ptr, None) == 0
+    lib.plvi_device_synchronize()
+    ref = [b.download(np.zeros((n - 1) * cap, np.int32)) for b in knn] + \
+        [lm.download(np.zeros((n - 1) * lcap, np.int32)), lnm.download(np.zeros(n - 1, np.int32))]
+    fill()
+    plvi.frame_extract_match_batch(orb, lx, buf.ptr, n, 640 * 480, 640, [b.ptr for b in knn], 0.9, lsc.ptr, lm.ptr,
+                                   lnm.ptr)
+    lib.plvi_device_synchronize()
+    got = [b.download(np.zeros((n - 1) * cap, np.int32)) for b in knn] + \
+        [lm.download(np.zeros((n - 1) * lcap, np.int32)), lnm.download(np.zeros(n - 1, np.int32))]
+    for a, b in zip(ref, got):
+        np.testing.assert_array_equal(a, b)
+    assert (ref[-1] > 0).all()

@@ -41,11 +41,9 @@ st = s.cuda_stream
 
 
 def step():
-    plvi.frame_extract_batch(o, lx, seq.data_ptr(), B, W * H, W, (0, 0), stream=st)
-    rc = lib.plvi_hamming_knn2_batch(de + cap * 32, co + 4, cap, de, co, cap, B - 1, *[x.data_ptr() for x in o4], st)
-    rc |= lib.plvi_line_match_batch(lde + lcap * 32, lco + 4, lcap, lde, lco, lcap, B - 1, 0.9, lsc.data_ptr(),
-                                    lm.data_ptr(), lnm.data_ptr(), st)
-    assert rc == 0
+    # as bench.py's batch64 step: the matching issued inside the frame schedule
+    plvi.frame_extract_match_batch(o, lx, seq.data_ptr(), B, W * H, W, [x.data_ptr() for x in o4], 0.9,
+                                   lsc.data_ptr(), lm.data_ptr(), lnm.data_ptr(), stream=st)
 
 
 for _ in range(3):
