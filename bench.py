@@ -652,8 +652,12 @@ def run(args, world, rank):
         step_no[0] += 1
         sl = slots[k % len(slots)]
         lo = (k % nwin) * (B - 1)
-        extract(seq[lo].data_ptr(), sl=sl)
-        match(sl=sl)
+        # extract + match as one schedule (plvi_frame_extract_match_batch: the
+        # matching issued on the schedule's own streams, same kernels and
+        # tables as extract() + match())
+        plvi.frame_extract_match_batch(sl.orb, sl.lx, seq[lo].data_ptr(), B, W * H, W,
+                                       [o.data_ptr() for o in sl.outs], 0.9, sl.lscratch.data_ptr(),
+                                       sl.lm12.data_ptr(), sl.lnm.data_ptr(), stream=sl.st)
         if args.gather:
             gather(sl)
 
