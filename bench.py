@@ -618,8 +618,11 @@ def run(args, world, rank):
     # on one queue and serialise ORB || lines
     lat_handles = None
     if rank == 0 and world == 1 and not args.no_extra:
+        # (and the batch-64 line's pair, for the same reason)
         lat_handles = (plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, device=dev),
-                       plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, device=dev))
+                       plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, device=dev),
+                       plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=64, device=dev),
+                       plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=64, device=dev))
     orb, lx, stream, st = s0.orb, s0.lx, s0.stream, s0.st
     kp_p, de_p, co_p, kl_p, lde_p, lco_p = s0.kp_p, s0.de_p, s0.co_p, s0.kl_p, s0.lde_p, s0.lco_p
     outs, lscratch, lm12, lnm = s0.outs, s0.lscratch, s0.lm12, s0.lnm
@@ -1090,8 +1093,7 @@ def extra_lines(args, torch, plvi, synth, lib, stream, W, H, seed0, orb, lx, ext
     cuda = f"cuda:{dev}"
     # (1) batch 64
     b64 = 64
-    o64 = plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=b64, device=dev)
-    l64 = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=b64, device=dev)
+    o64, l64 = lat_handles[2], lat_handles[3]  # created at start-up
     kp, de, co, _, cap = o64.outputs()
     _, lde, _, lco, lcap = l64.outputs()
     i32 = dict(dtype=torch.int32, device=cuda)
@@ -1195,7 +1197,7 @@ def extra_lines(args, torch, plvi, synth, lib, stream, W, H, seed0, orb, lx, ext
             raise RuntimeError("pipelined batch-64 device error flags")
     del slots
     # (2) single-frame latency: host image -> host tables, ORB || lines on two threads
-    so, sl = lat_handles
+    so, sl = lat_handles[0], lat_handles[1]
     imgs = [seq[i].cpu().numpy() for i in range(24)]
     lat, lo_, ll_ = [], [], []
     for rep in range(len(imgs) + 4):

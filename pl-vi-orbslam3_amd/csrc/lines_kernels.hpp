@@ -916,7 +916,8 @@ __global__ __launch_bounds__(256) void line_assemble_kernel(const LineOctDev* __
                                                             const int* __restrict__ nlines, double min_length,
                                                             int nfeatures, int fcap, plvi_keyline* __restrict__ kl_out,
                                                             double* __restrict__ fn_out, int* __restrict__ count_out,
-                                                            plvi_keyline* __restrict__ kl_tmp, int* __restrict__ err) {
+                                                            plvi_keyline* __restrict__ kl_tmp, int* __restrict__ err,
+                                                            unsigned short* __restrict__ sort_pos) {
     __shared__ int s_scan[256];
     __shared__ int s_base;
     __shared__ __align__(8) SortItem s_items[kKlCap];
@@ -1029,8 +1030,11 @@ __global__ __launch_bounds__(256) void line_assemble_kernel(const LineOctDev* __
             for (int i = threadIdx.x; i < n; i += 256) s_items[i] = SortItem{tmp[i].response, i};
             __syncthreads();
             // the libstdc++ std::sort permutation, replayed by the whole block
-            // (std_sort.h: std_sort_block)
-            std_sort_block(s_items, n, s_rng[0], s_rng[1], s_seg, s_ctl);
+            // (std_sort.h: std_sort_block; long ranges partitioned by the
+            // block, their stop positions in this frame's global scratch so the
+            // LDS footprint -- and the kernel's occupancy -- stay as they were)
+            unsigned short* sp = sort_pos + (size_t)f * 2 * kKlCap;
+            std_sort_block(s_items, n, s_rng[0], s_rng[1], s_seg, s_ctl, sp, sp + kKlCap, s_scan);
         } else {
             for (int i = threadIdx.x; i < nfinal; i += 256) {
                 const unsigned long long v = K[i];

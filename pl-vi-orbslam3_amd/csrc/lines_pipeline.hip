@@ -87,7 +87,7 @@ struct LinePipeline {
     double gk[7]{};
     int lbdTaps[3] = {14, 62, 104};
     DevBuf d_oct, d_tabs, octImg, pix, modg, seedcs, gbits, qspill, regs, regpts, rawLines, nlines, klTmp, klOut, fnOut, cntOut, descOut, lbdBlur,
-        lbdG, err, staging, mwOwn, mwSlot, mwGrow;
+        lbdG, err, staging, mwOwn, mwSlot, mwGrow, sortPos;
     size_t qspillFrame = 0, gbitsFrame = 0, lbdPlaneTotal = 0;
     int lastFrames = 0;
     static constexpr int kStages = 5, kRing = 512;
@@ -396,6 +396,7 @@ struct LinePipeline {
             regs.alloc(sizeof(LsdRegion) * (size_t)kLsdRawCap * nOct * Bcap) ||
             regpts.alloc(sizeof(unsigned) * qspillFrame * nOct * Bcap) ||
             nlines.alloc(sizeof(int) * nOct * Bcap) || klTmp.alloc(sizeof(plvi_keyline) * (size_t)kKlCap * Bcap) ||
+            sortPos.alloc(sizeof(unsigned short) * 2 * (size_t)kKlCap * Bcap) ||
             klOut.alloc(sizeof(plvi_keyline) * (size_t)fcap * Bcap) || fnOut.alloc(sizeof(double) * 3 * fcap * Bcap) ||
             cntOut.alloc(sizeof(int) * Bcap) || descOut.alloc((size_t)32 * fcap * Bcap) ||
             lbdBlur.alloc((size_t)W * H * Bcap) || lbdG.alloc(sizeof(short2) * lbdPlaneTotal) ||
@@ -579,7 +580,7 @@ struct LinePipeline {
         hipLaunchKernelGGL(line_assemble_kernel, dim3(nf), dim3(256), 0, st, d_oct.as<LineOctDev>(), nOct,
                            (const LsdLine*)rawLines.as<LsdLine>(), (const int*)nlines.as<int>(), min_length,
                            prm.nfeatures, fcap, klOut.as<plvi_keyline>(), fnOut.as<double>(), cntOut.as<int>(),
-                           klTmp.as<plvi_keyline>(), err.as<int>());
+                           klTmp.as<plvi_keyline>(), err.as<int>(), sortPos.as<unsigned short>());
         mark(4, st);
     }
 

@@ -183,8 +183,62 @@ PLVI_SORT_HD inline void introsort_loop(SortItem* first, SortItem* last, int dep
 struct SortRange {
     int first, last, depth;
 };
+
+// unguarded_partition(a + f0 + 1, a + l0, a + f0) by the whole block.  The
+// sequential loop swaps its k-th left stop (k-th element, from the left, with
+// !comp(x, pivot)) with its k-th right stop (from the right, !comp(pivot, x))
+// for as long as the left one lies before the right one; the scans never read
+// a swapped element before they cross, so the stops are those of the
+// original range: rank them with a block scan, swap the first m pairs (m =
+// the pairs in order, a monotone test) and return min(L[m], R[m-1]) -- where
+// the sequential scans stop after their last swap (L[0] without a swap).
+// lpos / rpos: n entries each, scan: blockDim.x ints.
+constexpr int kCoopPartition = 128;  // ranges longer than this are partitioned by the block
+__device__ inline int block_partition(SortItem* a, int f0, int l0, unsigned short* lpos, unsigned short* rpos,
+                                      int* scan, int* ctl) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const SortItem P = a[f0];
+    const int b = f0 + 1, len = l0 - b, per = (len + nt - 1) / nt;
+    const int s0 = min(b + tid * per, l0), s1 = min(s0 + per, l0);
+    int cl = 0, cr = 0;
+    for (int i = s0; i < s1; ++i) {
+        cl += !sort_comp(a[i], P);
+        cr += !sort_comp(P, a[i]);
+    }
+    // inclusive scan of the packed counts (each < 2^16) over the threads
+    int v = cl | (cr << 16);
+    scan[tid] = v;
+    __syncthreads();
+    for (int o = 1; o < nt; o <<= 1) {
+        const int u = tid >= o ? scan[tid - o] : 0;
+        __syncthreads();
+        v += u;
+        scan[tid] = v;
+        __syncthreads();
+    }
+    const int tot = scan[nt - 1], nL = tot & 0xffff, nR = tot >> 16;
+    int lr = (v & 0xffff) - cl, rseen = (v >> 16) - cr;  // stops before this thread's chunk
+    for (int i = s0; i < s1; ++i) {
+        if (!sort_comp(a[i], P)) lpos[lr++] = (unsigned short)i;
+        if (!sort_comp(P, a[i])) rpos[nR - 1 - rseen++] = (unsigned short)i;  // rank from the right
+    }
+    if (tid == 0) ctl[2] = 0;
+    __syncthreads();
+    const int np = min(nL, nR);
+    int mc = 0;
+    for (int k = tid; k < np; k += nt) mc += lpos[k] < rpos[k];
+    if (mc) atomicAdd(&ctl[2], mc);
+    __syncthreads();
+    const int m = ctl[2];
+    for (int k = tid; k < m; k += nt) sort_swap(a + lpos[k], a + rpos[k]);
+    const int cut = m == 0 ? lpos[0] : min(m < nL ? (int)lpos[m] : 0x7fffffff, (int)rpos[m - 1]);
+    __syncthreads();
+    return cut;
+}
+
 __device__ inline void std_sort_block(SortItem* a, int n, SortRange* rng0, SortRange* rng1, unsigned* segbits,
-                                      int* ctl, int depth0 = -1) {  // depth0 >= 0: test override of 2 lg n
+                                      int* ctl, unsigned short* lpos, unsigned short* rpos, int* scan,
+                                      int depth0 = -1) {  // depth0 >= 0: test override of 2 lg n
     const int tid = threadIdx.x, nt = blockDim.x;
     for (int w = tid; w < (n + 31) / 32; w += nt) segbits[w] = 0u;
     if (tid == 0) {
@@ -203,8 +257,28 @@ __device__ inline void std_sort_block(SortItem* a, int n, SortRange* rng0, SortR
     while (nr > 0) {
         if (tid == 0) ctl[1] = 0;
         __syncthreads();
+        // long ranges: the whole block partitions them, one after another
+        for (int r = 0; r < nr; ++r) {
+            const SortRange R = cur[r];
+            if (R.depth == 0 || R.last - R.first <= kCoopPartition) continue;
+            if (tid == 0) {
+                SortItem* f = a + R.first;
+                move_median_to_first(f, f + 1, f + (R.last - R.first) / 2, a + R.last - 1);
+            }
+            __syncthreads();
+            const int c = block_partition(a, R.first, R.last, lpos, rpos, scan, ctl);
+            if (tid == 0) {
+                const SortRange kids[2] = {SortRange{R.first, c, R.depth - 1}, SortRange{c, R.last, R.depth - 1}};
+                for (const SortRange& k : kids) {
+                    if (k.last - k.first > 16) nxt[atomicAdd(&ctl[1], 1)] = k;
+                    else if (k.last > k.first) atomicOr(&segbits[k.first >> 5], 1u << (k.first & 31));
+                }
+            }
+            __syncthreads();
+        }
         for (int r = tid; r < nr; r += nt) {
             const SortRange R = cur[r];
+            if (R.depth != 0 && R.last - R.first > kCoopPartition) continue;  // done above
             SortItem* f = a + R.first;
             SortItem* l = a + R.last;
             if (R.depth == 0) {  // __partial_sort(first, last, last)

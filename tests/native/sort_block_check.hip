@@ -20,11 +20,13 @@ __global__ __launch_bounds__(256) void sort_kernel(SortItem* data, const int* of
     __shared__ SortRange r0[256], r1[256];
     __shared__ unsigned seg[4096 / 32];
     __shared__ int ctl[4];
+    __shared__ unsigned short lpos[4096], rpos[4096];
+    __shared__ int scan[256];
     const int c = blockIdx.x;
     const int o = off[c], n = off[c + 1] - off[c];
     for (int i = threadIdx.x; i < n; i += 256) s[i] = data[o + i];
     __syncthreads();
-    std_sort_block(s, n, r0, r1, seg, ctl, depth[c]);
+    std_sort_block(s, n, r0, r1, seg, ctl, lpos, rpos, scan, depth[c]);
     for (int i = threadIdx.x; i < n; i += 256) data[o + i] = s[i];
 }
 
