@@ -320,7 +320,13 @@ __device__ __forceinline__ bool is_aligned_fast(float deg, float tdeg, float pde
     const float dd = __builtin_fabsf(tdeg - deg);
     const bool near = __builtin_fabsf(dd - pdeg) < 1e-3f || __builtin_fabsf(dd - (360.f - pdeg)) < 1e-3f;
     bool r = deg != kNotdefF && (dd <= pdeg || dd >= 360.f - pdeg);
-    if (__builtin_expect(near, 0)) r = is_aligned_deg(deg, (double)tdeg * kD2R, prec);
+    if (__builtin_expect(near, 0)) {
+        // opaque inside the rare branch, so that its double conversions are not
+        // hoisted out of the caller's loops onto the common path
+        float dg = deg;
+        asm volatile("" : "+v"(dg));
+        r = is_aligned_deg(dg, (double)tdeg * kD2R, prec);
+    }
     return r;
 }
 
@@ -395,7 +401,9 @@ __device__ __forceinline__ void grow_wave_sync() {
     __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool STATS>
+constexpr int kGrowRB = 64, kGrowQL = 256;
+
+template <bool STATS, bool FIXED>
 __global__ __launch_bounds__(64 * kGrowWaves, PLVI_GROW_WPE) void lsd_grow_kernel(const LineOctDev* __restrict__ octs,
                                                       const float* __restrict__ pix,
                                                       const double* __restrict__ modgrad,
@@ -434,6 +442,11 @@ __global__ __launch_bounds__(64 * kGrowWaves, PLVI_GROW_WPE) void lsd_grow_kerne
     const int sw = od.sw, sh = od.sh;
     const int lane = threadIdx.x & 63;
     GrowCtx g;
+    if (FIXED) {  // the default windows as constants (no angle window, 64 USED rows, 256 queue entries in LDS)
+        R = 0;
+        RB = kGrowRB;
+        QL = kGrowQL;
+    }
     g.sw = sw; g.sh = sh; g.R = R; g.RB = RB; g.QL = QL;
     g.wpr = (sw + 31) >> 5;
     g.P = pix + od.soff + (size_t)f * od.splane;
@@ -584,7 +597,15 @@ __global__ __launch_bounds__(64 * kGrowWaves, PLVI_GROW_WPE) void lsd_grow_kerne
                     const unsigned long long t0 = do_stats ? __builtin_amdgcn_s_memtime() : 0;
                     const int nb = min(7, reg_size - i);
                     const bool active = lane < 9 * nb;
-                    const unsigned pv = active ? q_get(g, i + bp) : 0u;
+                    // the block's queue points: one LDS read (inactive lanes read entry i),
+                    // the global spill only once the queue has passed QL entries
+                    unsigned pv;
+                    if (i + 7 <= g.QL) {
+                        const unsigned v = g.qlds[i + (active ? bp : 0)];
+                        pv = active ? v : 0u;
+                    } else {
+                        pv = active ? q_get(g, i + bp) : 0u;
+                    }
                     const int px = (int)(pv & 0xffffu), py = (int)(pv >> 16);
                     const int nx = px + kdx, ny = py + kdy;
                     const bool valid = active && nx >= 0 && nx < sw && ny >= y && ny < sh;
@@ -610,8 +631,10 @@ __global__ __launch_bounds__(64 * kGrowWaves, PLVI_GROW_WPE) void lsd_grow_kerne
                     for (int p2 = 0; p2 < nb - 1; ++p2) {
                         const unsigned q2 = (unsigned)readlane_i((int)pv, 9 * p2);
                         const int ddx = nx - (int)(q2 & 0xffffu) + 1, ddy = ny - (int)(q2 >> 16) + 1;
-                        if (p2 < bp && ddx >= 0 && ddx <= 2 && ddy >= 0 && ddy <= 2)
-                            dup |= 1ull << (9 * p2 + ddy * 3 + ddx);
+                        const bool hit = p2 < bp && (unsigned)ddx <= 2u && (unsigned)ddy <= 2u;
+                        // as a mask, not a branch
+                        const unsigned long long hm = 0ull - (unsigned long long)hit;
+                        dup |= (1ull << ((9 * p2 + ddy * 3 + ddx) & 63)) & hm;
                     }
                     unsigned long long t1 = 0;
                     if (do_stats) {
@@ -620,7 +643,14 @@ __global__ __launch_bounds__(64 * kGrowWaves, PLVI_GROW_WPE) void lsd_grow_kerne
                     // USED is read once per block: within the block a lane's pixel
                     // only becomes USED through a commit of an earlier lane testing
                     // the same pixel (dup), tracked in Ccum
-                    const bool live0 = valid && deg != kNotdefF && !used_get(g, nx, ny);
+                    // (rows above the seed row are never valid lanes here)
+                    const int ux = valid ? nx : 0, uy = valid ? ny : y;
+                    unsigned uw = g.bits[(uy & (g.RB - 1)) * g.wpr + (ux >> 5)];
+                    const bool ufar = valid && uy >= g.wbb + g.RB;
+                    if (__builtin_expect(__ballot(ufar) != 0ull, 0)) {
+                        if (ufar) uw = gload_l2(g.gbits + (size_t)uy * g.wpr + (ux >> 5));
+                    }
+                    const bool live0 = valid & (deg != kNotdefF) & (((uw >> (ux & 31)) & 1u) == 0u);
                     unsigned long long Ccum = 0;
                     int start = 0;
                     while (start < 9 * nb) {
@@ -663,19 +693,28 @@ __global__ __launch_bounds__(64 * kGrowWaves, PLVI_GROW_WPE) void lsd_grow_kerne
                         if (nc > 0) {
                             Ccum |= C;
                             const bool mine = (C >> lane) & 1ull;
-                            if (mine) {
-                                used_set(g, nx, ny);
-                                q_put(g, reg_size + mbcnt64(C), (unsigned)nx | ((unsigned)ny << 16));
-                            }
-                            // global USED bits / queue spill must land before they are read back
-                            {
-                                const bool far = __ballot(mine && ny >= g.wbb + RB) != 0ull;
-                                const bool spill = reg_size + nc > QL;
-                                if (far || spill) vm_drain();
-                                if (do_stats) {
-                                    n_far += far;
-                                    n_spill += spill;
+                            const bool far = __ballot(mine && ny >= g.wbb + RB) != 0ull;
+                            const bool spill = reg_size + nc > QL;
+                            if (__builtin_expect(!far && !spill, 1)) {
+                                // USED bit and queue entry in LDS
+                                if (mine) {
+                                    __atomic_fetch_or(&g.bits[(ny & (g.RB - 1)) * g.wpr + (nx >> 5)], 1u << (nx & 31),
+                                                      __ATOMIC_RELAXED);
+                                    g.qlds[reg_size + mbcnt64(C)] = (unsigned)nx | ((unsigned)ny << 16);
                                 }
+                            } else {
+                                if (mine) {
+                                    int sx_ = nx, sy_ = ny;  // opaque: keep the slow path's addressing here
+                                    asm volatile("" : "+v"(sx_), "+v"(sy_));
+                                    used_set(g, sx_, sy_);
+                                    q_put(g, reg_size + mbcnt64(C), (unsigned)sx_ | ((unsigned)sy_ << 16));
+                                }
+                                // global USED bits / queue spill must land before they are read back
+                                vm_drain();
+                            }
+                            if (do_stats) {
+                                n_far += far;
+                                n_spill += spill;
                             }
                             reg_size += nc;
                             sumdx = readlane_f(pfx, ls);

@@ -434,7 +434,8 @@ struct LinePipeline {
         // tasks (waves) per workgroup: kGrowWaves, fewer when their LDS
         // partitions would not fit one CU (large PLVI_GROW_LDS budgets)
         growWPW = (int)std::max<size_t>(1, std::min<size_t>(kGrowWaves, (160 * 1024) / growSmem));
-        for (const void* k : {(const void*)lsd_grow_kernel<false>, (const void*)lsd_grow_kernel<true>})
+        for (const void* k : {(const void*)lsd_grow_kernel<false, false>, (const void*)lsd_grow_kernel<true, false>,
+                              (const void*)lsd_grow_kernel<false, true>, (const void*)lsd_grow_kernel<true, true>})
             PLVI_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(growSmem * growWPW)));
         // Small batches (latency): lsd_grow_mw_kernel, kMwWaves waves per
         // (frame, octave) growing regions of one frame concurrently.
@@ -556,7 +557,9 @@ struct LinePipeline {
                                qspillFrame, nlines.as<int>(), err.as<int>(), mwSlots, nOct, oBase, oCount, mwStats, nf);
             return;
         }
-        auto growK = growStats ? lsd_grow_kernel<true> : lsd_grow_kernel<false>;
+        const bool fixedWin = growR == 0 && growRB == kGrowRB && growQL == kGrowQL;
+        auto growK = growStats ? (fixedWin ? lsd_grow_kernel<true, true> : lsd_grow_kernel<true, false>)
+                               : (fixedWin ? lsd_grow_kernel<false, true> : lsd_grow_kernel<false, false>);
         hipLaunchKernelGGL(growK, dim3((oCount * nf + growWPW - 1) / growWPW), dim3(64 * growWPW),
                            growSmem * growWPW, st, d_oct.as<LineOctDev>(),
                            (const float*)pix.as<float>(), (const double*)modg.as<double>(),

@@ -224,7 +224,15 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
         const unsigned long long tb0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
         const int nb = min(7, reg_size - i);
         const bool active = lane < 9 * nb;
-        const unsigned pv = active ? mw_qget(Q, i + bp) : 0u;
+        // the block's queue points: one LDS read (inactive lanes read entry i),
+        // the global part only once the queue has passed its LDS entries
+        unsigned pv;
+        if (i + 7 <= Q.lcap) {
+            const unsigned v = Q.lq[i + (active ? bp : 0)];
+            pv = active ? v : 0u;
+        } else {
+            pv = active ? mw_qget(Q, i + bp) : 0u;
+        }
         const int px = (int)(pv & 0xffffu), py = (int)(pv >> 16);
         const int nx = px + kdx, ny = py + kdy;
         // pixels before the seed in raster order are USED when flsd reaches it
@@ -246,7 +254,9 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
         for (int p2 = 0; p2 < nb - 1; ++p2) {
             const unsigned q2 = (unsigned)readlane_i((int)pv, 9 * p2);
             const int ddx = nx - (int)(q2 & 0xffffu) + 1, ddy = ny - (int)(q2 >> 16) + 1;
-            if (p2 < bp && ddx >= 0 && ddx <= 2 && ddy >= 0 && ddy <= 2) dup |= 1ull << (9 * p2 + ddy * 3 + ddx);
+            const bool hit = p2 < bp && (unsigned)ddx <= 2u && (unsigned)ddy <= 2u;
+            const unsigned long long hm = 0ull - (unsigned long long)hit;  // a mask, not a branch
+            dup |= (1ull << ((9 * p2 + ddy * 3 + ddx) & 63)) & hm;
         }
         if (SPEC) {
             if (hd0 > seedb) {
@@ -262,7 +272,16 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
         // own marks and the committed bitmap, read once per block (within the
         // block a lane's pixel only changes through an earlier lane's commit
         // of the same pixel: dup / Ccum)
-        const bool live0 = valid && deg != kNotdefF && !mw_bit(E.C, E.wpr, nx, ny) && !mw_own_get(E, nx, ny, sy);
+        // committed bit and own mark, read for every lane (clamped), the own
+        // marks below the window from the global spill (rare, uniform branch)
+        const int ux = valid ? nx : sx, uy = valid ? ny : sy;
+        const unsigned cw = mw_word(E.C, E.wpr, ux, uy);
+        const bool ofar = uy >= sy + kMwRB;
+        unsigned ow = E.own[(ofar ? 0 : uy - sy) * E.wpr + (ux >> 5)];
+        if (__builtin_expect(__ballot(valid && ofar) != 0ull, 0)) {
+            if (ofar) ow = gload_l2(E.ownG + (size_t)uy * E.wpr + (ux >> 5));
+        }
+        const bool live0 = valid & (deg != kNotdefF) & ((((cw | ow) >> (ux & 31)) & 1u) == 0u);
         unsigned long long tb1 = 0;
         if (STATS) {
             tb1 = __builtin_amdgcn_s_memtime();
@@ -307,14 +326,26 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
                 }
                 Ccum |= Cm;
                 const bool mine = (Cm >> lane) & 1ull;
-                if (mine) {
-                    mw_own_set(E, nx, ny, sy);
-                    mw_or(E.H, E.wpr, nx, ny);
-                    mw_qput(Q, reg_size + mbcnt64(Cm), (unsigned)nx | ((unsigned)ny << 16));
-                }
                 const bool sp = __ballot(mine && ny >= sy + kMwRB) != 0ull;
                 spilled |= sp;
-                if (sp || reg_size + nc > Q.lcap) vm_drain();
+                if (__builtin_expect(!sp && reg_size + nc <= Q.lcap, 1)) {
+                    // own mark, claim hint and queue entry in LDS
+                    if (mine) {
+                        const unsigned b = 1u << (nx & 31);
+                        __atomic_fetch_or(&E.own[(ny - sy) * E.wpr + (nx >> 5)], b, __ATOMIC_RELAXED);
+                        __atomic_fetch_or(&E.H[ny * E.wpr + (nx >> 5)], b, __ATOMIC_RELAXED);
+                        Q.lq[reg_size + mbcnt64(Cm)] = (unsigned)nx | ((unsigned)ny << 16);
+                    }
+                } else {
+                    if (mine) {
+                        int sx_ = nx, sy_ = ny;  // opaque: keep the slow path's addressing here
+                        asm volatile("" : "+v"(sx_), "+v"(sy_));
+                        mw_own_set(E, sx_, sy_, sy);
+                        mw_or(E.H, E.wpr, sx_, sy_);
+                        mw_qput(Q, reg_size + mbcnt64(Cm), (unsigned)sx_ | ((unsigned)sy_ << 16));
+                    }
+                    vm_drain();
+                }
                 reg_size += nc;
                 sumdx = readlane_f(pfx, ls);
                 sumdy = readlane_f(pfy, ls);
