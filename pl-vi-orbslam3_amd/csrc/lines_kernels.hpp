@@ -244,6 +244,32 @@ struct GrowCtx {
     int sw, sh, R, RB, wpr, wb, wbb, QL, ys;  // window bases wb (angles) / wbb (bits); ys = seed row
 };
 
+// Lanes of earlier block points (p2 < this lane's point) testing the same
+// pixel: bit 9 * p2 + 3 * ddy + ddx of the block's 63 test lanes, where
+// (ddx, ddy) = (nx - qx + 1, ny - qy + 1) in [0, 2]^2 for point p2 = (qx, qy).
+// Both differences come from one packed 16-bit subtract, the range test from
+// one packed max; bit = 9 * p2 + (3 * ny + nx + 4) - (3 * qy + qx).
+typedef unsigned short plvi_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned long long dup_lanes(unsigned pv, int nb, int bp, int nx, int ny) {
+    const unsigned pn1 = (unsigned)(nx + 1) | ((unsigned)(ny + 1) << 16);
+    const int s = 3 * ny + nx + 4;
+    unsigned long long dup = 0;
+    for (int p2 = 0; p2 < nb - 1; ++p2) {
+        const unsigned q2 = (unsigned)__builtin_amdgcn_readlane((int)pv, 9 * p2);
+        const int t2 = 3 * (int)(q2 >> 16) + (int)(q2 & 0xffffu);
+        const plvi_u16x2 d = __builtin_bit_cast(plvi_u16x2, pn1) - __builtin_bit_cast(plvi_u16x2, q2);
+        const plvi_u16x2 m = __builtin_elementwise_max(d, (plvi_u16x2){2, 2});
+        const bool hit = (p2 < bp) & (__builtin_bit_cast(unsigned, m) == 0x00020002u);
+        const unsigned long long hm = 0ull - (unsigned long long)hit;  // a mask, not a branch
+        dup |= (1ull << ((9 * p2 - t2 + s) & 63)) & hm;
+    }
+    return dup;
+}
+
+// lane mask of a condition (the builtin on the bool itself; the multi-wave
+// growth uses it, the large-batch kernel keeps __ballot: measured either way
+// within noise there, profiles/r05/grow_ab_branchless.txt)
+__device__ __forceinline__ unsigned long long ballot(bool b) { return __builtin_amdgcn_ballot_w64(b); }
 // set bits of m below this lane (v_mbcnt_lo/hi: popcount(m & ((1 << lane) - 1)))
 __device__ __forceinline__ int mbcnt64(unsigned long long m) {
     return (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));

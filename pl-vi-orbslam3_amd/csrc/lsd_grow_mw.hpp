@@ -236,7 +236,8 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
         const int px = (int)(pv & 0xffffu), py = (int)(pv >> 16);
         const int nx = px + kdx, ny = py + kdy;
         // pixels before the seed in raster order are USED when flsd reaches it
-        const bool valid = active && nx >= 0 && nx < sw && ny < sh && (ny > sy || (ny == sy && nx >= sx));
+        // in the frame and at or after the seed in raster order
+        const bool valid = active & ((unsigned)nx < (unsigned)sw) & (ny < sh) & (ny * sw + nx >= sy * sw + sx);
         float deg = kNotdefF, cc = 0.f, ss = 0.f;
         if (valid) {
             const float2 cs2 = E.SC[(size_t)ny * sw + nx];
@@ -250,14 +251,7 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
             sumdx = (float)dc;
             sumdy = (float)ds;
         }
-        unsigned long long dup = 0;
-        for (int p2 = 0; p2 < nb - 1; ++p2) {
-            const unsigned q2 = (unsigned)readlane_i((int)pv, 9 * p2);
-            const int ddx = nx - (int)(q2 & 0xffffu) + 1, ddy = ny - (int)(q2 >> 16) + 1;
-            const bool hit = p2 < bp && (unsigned)ddx <= 2u && (unsigned)ddy <= 2u;
-            const unsigned long long hm = 0ull - (unsigned long long)hit;  // a mask, not a branch
-            dup |= (1ull << ((9 * p2 + ddy * 3 + ddx) & 63)) & hm;
-        }
+        const unsigned long long dup = dup_lanes(pv, nb, bp, nx, ny);
         if (SPEC) {
             if (hd0 > seedb) {
                 n_out = reg_size;
@@ -278,7 +272,7 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
         const unsigned cw = mw_word(E.C, E.wpr, ux, uy);
         const bool ofar = uy >= sy + kMwRB;
         unsigned ow = E.own[(ofar ? 0 : uy - sy) * E.wpr + (ux >> 5)];
-        if (__builtin_expect(__ballot(valid && ofar) != 0ull, 0)) {
+        if (__builtin_expect(ballot(valid && ofar) != 0ull, 0)) {
             if (ofar) ow = gload_l2(E.ownG + (size_t)uy * E.wpr + (ux >> 5));
         }
         const bool live0 = valid & (deg != kNotdefF) & ((((cw | ow) >> (ux & 31)) & 1u) == 0u);
@@ -292,10 +286,11 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
         int start = 0;
         while (start < 9 * nb) {
             const unsigned long long fromStart = ~0ull << start;
-            const bool candl = lane >= start && live0 && (dup & Ccum) == 0ull;
-            const bool al = candl && is_aligned_fast(deg, reg_deg, pdeg, prec);
-            const bool acc = al && (dup & fromStart) == 0ull;
-            const unsigned long long A = __ballot(acc);
+            const bool candl = (lane >= start) & live0 & ((dup & Ccum) == 0ull);
+            const bool alg = is_aligned_fast(deg, reg_deg, pdeg, prec);
+            const bool al = candl & alg;
+            const bool acc = al & ((dup & fromStart) == 0ull);
+            const unsigned long long A = ballot(acc);
             if (!A) break;
             const int cl = mbcnt64(A);
             float sx2 = sumdx, sy2 = sumdy, pfx = sumdx, pfy = sumdy;
@@ -312,8 +307,9 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
             }
             const float tha = plvi_fast_atan2(pfy, pfx);
             const float th = cl > 0 ? tha : reg_deg;
-            const bool al2 = candl && (dup & A) == 0ull && is_aligned_fast(deg, th, pdeg, prec);
-            const unsigned long long mism = __ballot(al2 != acc) & fromStart;
+            const bool alth = is_aligned_fast(deg, th, pdeg, prec);
+            const bool al2 = candl & ((dup & A) == 0ull) & alth;
+            const unsigned long long mism = ballot(al2 != acc) & fromStart;
             const int ls = mism ? __ffsll((long long)mism) - 1 : 63;
             const unsigned long long Cm = A & ((1ull << ls) - 1ull);
             const int nc = __popcll(Cm);
@@ -326,7 +322,7 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
                 }
                 Ccum |= Cm;
                 const bool mine = (Cm >> lane) & 1ull;
-                const bool sp = __ballot(mine && ny >= sy + kMwRB) != 0ull;
+                const bool sp = ballot(mine && ny >= sy + kMwRB) != 0ull;
                 spilled |= sp;
                 if (__builtin_expect(!sp && reg_size + nc <= Q.lcap, 1)) {
                     // own mark, claim hint and queue entry in LDS
@@ -414,7 +410,7 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
             for (int w0 = w + 1; w0 < nwords && found < 0; w0 += 64) {
                 const int ww = w0 + lane;
                 const bool nz = ww < nwords && ~mw_peek(E.C + ww) != 0u;
-                const unsigned long long b = __ballot(nz);
+                const unsigned long long b = ballot(nz);
                 if (b) found = w0 + __ffsll((long long)b) - 1;
             }
             if (found < 0) {
@@ -483,7 +479,7 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
                     const unsigned v = mw_qget(Q, j);
                     bad |= mw_bit(E.C, E.wpr, (int)(v & 0xffffu), (int)(v >> 16));
                 }
-                valid = __ballot(bad) == 0ull;
+                valid = ballot(bad) == 0ull;
             }
             if (valid) {
                 if (lane < n) mw_or(E.C, E.wpr, (int)(v0 & 0xffffu), (int)(v0 >> 16));
@@ -595,7 +591,7 @@ __device__ __forceinline__ int mw_dispatch(const MwEnv& E, lds_u8* pool, int nsl
             const int st = mw_lds_load(&S->state);
             ok = st == kMwFree || (st == kMwDone && S->seed < head);
         }
-        const unsigned long long b = __ballot(ok);
+        const unsigned long long b = ballot(ok);
         if (b) slot = b0 + __ffsll((long long)b) - 1;
     }
     if (slot < 0) return -1;
@@ -608,7 +604,7 @@ __device__ __forceinline__ int mw_dispatch(const MwEnv& E, lds_u8* pool, int nsl
         for (int w0 = w + 1; w0 < nwords && found < 0; w0 += 64) {
             const int ww = w0 + lane;
             const bool nz = ww < nwords && (mw_peek(E.C + ww) | E.T[ww] | mw_peek(E.H + ww)) != ~0u;
-            const unsigned long long b = __ballot(nz);
+            const unsigned long long b = ballot(nz);
             if (b) found = w0 + __ffsll((long long)b) - 1;
         }
         if (found < 0) {
@@ -643,7 +639,7 @@ __device__ __forceinline__ void mw_copy_points(const MwQueue& A, const MwQueue& 
         mw_qput(B, j, mw_qget(A, j));
         g |= j >= B.lcap;
     }
-    if (__ballot(g)) vm_drain();
+    if (ballot(g)) vm_drain();
 }
 
 
@@ -720,8 +716,8 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
         // none aligned with its angle -> region = {seed} (< min_reg_size)
         const bool grows = is_aligned_fast(dr, d0, pdeg, prec) || is_aligned_fast(dbl, d0, pdeg, prec) ||
                            is_aligned_fast(db, d0, pdeg, prec) || is_aligned_fast(dbr, d0, pdeg, prec);
-        const unsigned long long cm = __ballot(!def);
-        const unsigned long long tm = __ballot(def && !grows && min_reg > 1);
+        const unsigned long long cm = ballot(!def);
+        const unsigned long long tm = ballot(def && !grows && min_reg > 1);
         if (lane < 2 && (xb >> 5) + lane < wpr) {
             const int wi = y * wpr + (xb >> 5) + lane;
             C[wi] = lane == 0 ? (unsigned)cm : (unsigned)(cm >> 32);
@@ -768,7 +764,7 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
                 for (int b0 = 0; b0 < nslots && cs < 0; b0 += 64) {
                     const int si = b0 + lane;
                     const bool ok = si < nslots && mw_lds_load(&mw_slot(pool, si)->state) == kMwCommitted;
-                    const unsigned long long b = __ballot(ok);
+                    const unsigned long long b = ballot(ok);
                     if (b) cs = b0 + __ffsll((long long)b) - 1;
                 }
                 if (cs >= 0 && lane == 0) mw_lds_store(&mw_slot(pool, cs)->state, kMwCopying);
@@ -804,7 +800,7 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
                         ok = mw_lds_load(&S->state) == kMwDone && S->seed == dlog[2 * e] && S->seed >= head &&
                              S->chk < nc;
                     }
-                    const unsigned long long b = __ballot(ok);
+                    const unsigned long long b = ballot(ok);
                     if (b) {
                         const int cand = readlane_i(sj, __ffsll((long long)b) - 1);
                         int got = 0;
@@ -827,7 +823,7 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
                     int nst = kMwDone;
                     if (mw_bit(E.C, E.wpr, sx, sy)) {
                         nst = kMwFree;  // the seed itself was taken: the walk never visits it
-                    } else if (__ballot(bad) == 0ull) {
+                    } else if (ballot(bad) == 0ull) {
                         if (lane == 0) S->chk = nc0;
                     } else {
                         int n = 0;
