@@ -422,8 +422,9 @@ def dry_run(args, world, rank):
         pdist.init("gloo")
     W, H = (752, 480) if args.c4 else (args.width, args.height)
     B = args.batch
-    nwin = 2 if args.c4 else 1
-    seq = synth.device_sequence(B + (nwin - 1) * (B - 1), W, H, seed=pdist.shard_seed(rank))
+    nwin = 2 if args.c4 else max(1, args.inflight)  # the GPU run's windows (run())
+    wstride = (B - 1) if args.c4 else B
+    seq = synth.device_sequence(B + (nwin - 1) * wstride, W, H, seed=pdist.shard_seed(rank))
     digest = hashlib.sha256(seq[:B].numpy().tobytes()).hexdigest()[:16]
     gather = world > 1 if args.gather is None else args.gather
 
@@ -443,7 +444,7 @@ def dry_run(args, world, rank):
     t0 = time.perf_counter()
     sums = 0
     for k in range(args.steps):
-        lo = (k % nwin) * (B - 1)
+        lo = (k % nwin) * wstride
         sums += int(seq[lo:lo + B].to(torch.int64).sum())
         if tg is not None:
             tg.post(tables(lo))
@@ -461,7 +462,7 @@ def dry_run(args, world, rank):
     if tg is not None:
         # the last step's tables of every rank, as rank 0 received them, next
         # to each rank's own digest of the same tables
-        own = pdist.tables_digest(tables(((args.steps - 1) % nwin) * (B - 1)))
+        own = pdist.tables_digest(tables(((args.steps - 1) % nwin) * wstride))
         owns = [own]
         if world > 1:
             owns = [None] * world
@@ -570,10 +571,13 @@ def run(args, world, rank):
     seed0 = pdist.shard_seed(rank)
 
     # frames: C4 = one sequence per rank walked in windows [k(B-1), k(B-1)+B)
-    # (one-frame halo); default = one resident batch re-processed each step
-    # (C4: two windows per sequence, ~2B frames; the walk wraps to the start)
-    nwin = 2 if args.c4 else 1
-    seq = synth.device_sequence(B + (nwin - 1) * (B - 1), W, H, seed=seed0, device=cuda)
+    # (one-frame halo; two windows per sequence, ~2B frames; the walk wraps to
+    # the start); default = one resident batch of B distinct frames per batch
+    # in flight (consecutive windows [kB, kB+B) of one sequence), so the
+    # batches in flight never process the same frames
+    nwin = 2 if args.c4 else max(1, args.inflight)
+    wstride = (B - 1) if args.c4 else B
+    seq = synth.device_sequence(B + (nwin - 1) * wstride, W, H, seed=seed0, device=cuda)
     torch.cuda.synchronize()
     first_digest = hashlib.sha256(seq[:B].cpu().numpy().tobytes()).hexdigest()[:16]
 
@@ -654,7 +658,7 @@ def run(args, world, rank):
         k = step_no[0]
         step_no[0] += 1
         sl = slots[k % len(slots)]
-        lo = (k % nwin) * (B - 1)
+        lo = (k % nwin) * wstride
         # extract + match as one schedule (plvi_frame_extract_match_batch: the
         # matching issued on the schedule's own streams, same kernels and
         # tables as extract() + match())
@@ -765,7 +769,7 @@ def run(args, world, rank):
             sob[k][0] += t_
             sob[k][1] += n_
     # last timed batch's window (for the checks below)
-    lo_last = ((step_no[0] - 1) % nwin) * (B - 1)
+    lo_last = ((step_no[0] - 1) % nwin) * wstride
 
     # ---------------------------------------------------------- rooflines
     bf_bytes = blur_fast_bytes(W, H) * B
