@@ -399,19 +399,33 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
     int wp = ctl->wptr;
     int blocked = -1;
     while (true) {
-        // next unresolved pixel >= head: first zero bit of C
+        // next non-trivial unresolved pixel >= head.  The trivial seeds before
+        // it (one-pixel regions < min_reg_size; every earlier region is
+        // committed) are committed in place -- the words wholly before it in
+        // one wave-parallel pass, 64 words at a time.  Only the walker writes C.
         int w = head >> 5;
         if (w >= nwords) break;
         unsigned cw = mw_peek(E.C + w), tw = E.T[w];  // T is static after the set-up
         unsigned m = ~cw & (~0u << (head & 31));
-        if (!m) {
-            // wave-parallel scan of the following words
+        unsigned nt = m & ~tw;
+        if (!nt) {
+            if ((m & tw) && lane == 0) {
+                __atomic_fetch_or(&E.C[w], m & tw, __ATOMIC_RELAXED);
+                if (STATS) mw_stat(ctl, 4, __popc(m & tw));
+            }
             int found = -1;
             for (int w0 = w + 1; w0 < nwords && found < 0; w0 += 64) {
                 const int ww = w0 + lane;
-                const bool nz = ww < nwords && ~mw_peek(E.C + ww) != 0u;
-                const unsigned long long b = ballot(nz);
-                if (b) found = w0 + __ffsll((long long)b) - 1;
+                const bool in = ww < nwords;
+                const unsigned c = in ? mw_peek(E.C + ww) : ~0u, t = in ? E.T[ww] : 0u;
+                const unsigned long long b = ballot((~c & ~t) != 0u);
+                const int fl = b ? __ffsll((long long)b) - 1 : 64;
+                const unsigned triv = ~c & t;
+                if (lane < fl && triv) {
+                    __atomic_fetch_or(&E.C[ww], triv, __ATOMIC_RELAXED);
+                    if (STATS) mw_stat(ctl, 4, __popc(triv));
+                }
+                if (b) found = w0 + fl;
             }
             if (found < 0) {
                 head = nwords * 32;
@@ -421,17 +435,13 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
             cw = mw_peek(E.C + w);
             tw = E.T[w];
             m = ~cw;
+            nt = m & ~tw;
         }
-        // trivial seeds before the first non-trivial one are committed in place
-        const unsigned nt = m & ~tw;
-        const unsigned run = nt ? (m & tw & ((nt & (0u - nt)) - 1u)) : (m & tw);
+        // trivial seeds before the first non-trivial one of word w
+        const unsigned run = m & tw & ((nt & (0u - nt)) - 1u);
         if (run && lane == 0) {
             __atomic_fetch_or(&E.C[w], run, __ATOMIC_RELAXED);
             if (STATS) mw_stat(ctl, 4, __popc(run));
-        }
-        if (!nt) {
-            head = (w + 1) * 32;
-            continue;
         }
         const int q = w * 32 + (__ffs((int)nt) - 1);
         head = q;
