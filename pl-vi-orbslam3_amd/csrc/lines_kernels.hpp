@@ -816,8 +816,9 @@ __global__ __launch_bounds__(256) void lsd_rect_lanes_kernel(const LineOctDev* _
                                                              const unsigned* __restrict__ regpts,
                                                              size_t regpts_frame, const int* __restrict__ nlines,
                                                              double prec, double scale_lsd,
-                                                             LsdLine* __restrict__ lines) {
-    const int o = blockIdx.y, f = blockIdx.z, nOct = gridDim.y;
+                                                             LsdLine* __restrict__ lines, int oBase, int nOct) {
+    // octaves oBase .. oBase + gridDim.y - 1 of nOct
+    const int o = oBase + blockIdx.y, f = blockIdx.z;
     const int task = f * nOct + o;
     const int n = min(nlines[task], kLsdRawCap);
     const LineOctDev& od = octs[o];

@@ -568,17 +568,21 @@ struct LinePipeline {
                            qspillFrame, nlines.as<int>(), err.as<int>(), growR, growRB, growQL, nOct, oBase, oCount,
                            growStats, nf, (int)growSmem, growWPW);
     }
-    void launch_grow_assemble(int nf, hipStream_t st, bool grown = false) {
+    // region2rect (lane = region) of octaves [oBase, oBase + oCount); small
+    // batches spread a frame's regions over more workgroups (latency)
+    void launch_rect(int nf, int oBase, int oCount, hipStream_t st) {
+        const int bx = nf <= 16 ? 8 : kRectLaneBlocks;
+        hipLaunchKernelGGL(lsd_rect_lanes_kernel, dim3(bx, oCount, nf), dim3(256), 0, st, d_oct.as<LineOctDev>(),
+                           (const double*)modg.as<double>(), (const LsdRegion*)regs.as<LsdRegion>(),
+                           (const unsigned*)regpts.as<unsigned>(), qspillFrame, (const int*)nlines.as<int>(), prec,
+                           SCALE, rawLines.as<LsdLine>(), oBase, nOct);
+    }
+    // grown: region growing already launched; rect0: only octave 0's
+    // region2rect is left (the other octaves' ran behind their growth on
+    // the side stream, which the caller joined)
+    void launch_grow_assemble(int nf, hipStream_t st, bool grown = false, bool rect0 = false) {
         if (!grown) launch_grow(nf, 0, nOct, st);
-        {
-            // region2rect, lane = region; small batches spread a frame's
-            // regions over more workgroups (latency)
-            const int bx = nf <= 16 ? 8 : kRectLaneBlocks;
-            hipLaunchKernelGGL(lsd_rect_lanes_kernel, dim3(bx, nOct, nf), dim3(256), 0, st, d_oct.as<LineOctDev>(),
-                               (const double*)modg.as<double>(), (const LsdRegion*)regs.as<LsdRegion>(),
-                               (const unsigned*)regpts.as<unsigned>(), qspillFrame, (const int*)nlines.as<int>(),
-                               prec, SCALE, rawLines.as<LsdLine>());
-        }
+        launch_rect(nf, 0, rect0 ? 1 : nOct, st);
         mark(3, st);
         hipLaunchKernelGGL(line_assemble_kernel, dim3(nf), dim3(256), 0, st, d_oct.as<LineOctDev>(), nOct,
                            (const LsdLine*)rawLines.as<LsdLine>(), (const int*)nlines.as<int>(), min_length,
@@ -650,10 +654,11 @@ struct LinePipeline {
             PLVI_CHECK(hipStreamWaitEvent(aux[0], evPrep, 0));
             launch_prep(d_frames, nf, frame_stride, row_stride, aux[0], 1, nOct);
             launch_grow(nf, 1, nOct - 1, aux[0]);
+            launch_rect(nf, 1, nOct - 1, aux[0]);  // beside octave 0's growth
             PLVI_CHECK(hipEventRecord(evGrow2, aux[0]));
             launch_grow(nf, 0, 1, st);
             PLVI_CHECK(hipStreamWaitEvent(st, evGrow2, 0));
-            launch_grow_assemble(nf, st, true);
+            launch_grow_assemble(nf, st, true, true);
         } else {
             launch_prep(d_frames, nf, frame_stride, row_stride, st);
             launch_grow_assemble(nf, st);
@@ -703,6 +708,7 @@ struct LinePipeline {
             PLVI_CHECK(hipStreamWaitEvent(octStream, evPrep, 0));
             launch_prep(d_frames, nf, frame_stride, row_stride, octStream, 1, nOct);
             launch_grow(nf, 1, nOct - 1, octStream);
+            launch_rect(nf, 1, nOct - 1, octStream);  // beside octave 0's growth
             PLVI_CHECK(hipEventRecord(evGrow2, octStream));
         }
         hipEvent_t auxStart = (orbAfterPrep >= 2 || (orbAfterPrep == 1 && nf < 1024)) ? evPrep : evFork;
@@ -754,7 +760,7 @@ struct LinePipeline {
         if (octFirst) {
             launch_grow(nf, 0, 1, crit);
             PLVI_CHECK(hipStreamWaitEvent(crit, evGrow2, 0));
-            launch_grow_assemble(nf, crit, true);
+            launch_grow_assemble(nf, crit, true, true);
         } else {
             launch_grow_assemble(nf, crit, split);
         }
