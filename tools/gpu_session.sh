@@ -27,6 +27,9 @@ if [ "${SKIP_PROF:-0}" != 1 ]; then
   timeout -k 10 ${PROF_T:-400} rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py ${STATS_ARGS:-} > $OUT/prof.log 2>&1
   rc=$?; tail -3 $OUT/prof.log; fatal $rc rocprof hard
   python3 $R/tools/timed_stats.py $OUT/prof/run_kernel_trace.csv $OUT/kernel_stats_timed.csv
+  # the bench line of the profiled run: its roofline.avg_launch_ms times the
+  # same launches as kernel_stats_timed.csv (profiles/r05/prof_reps/README.md)
+  grep -h '^{"metric"' $OUT/prof.log > $OUT/bench_under_rocprof.json || true
 fi
 if [ "${SKIP_PMC:-0}" != 1 ]; then
   # calibrated HBM traffic of the roofline kernels (separate FETCH_SIZE / WRITE_SIZE passes)
