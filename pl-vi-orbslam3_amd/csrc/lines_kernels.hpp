@@ -609,9 +609,6 @@ __global__ __launch_bounds__(64 * kGrowWaves, PLVI_GROW_WPE) void lsd_grow_kerne
                 // seed direction sumdx / sumdy: computed in the first block, while
                 // its neighbourhood loads are in flight
                 float sumdx = 0.f, sumdy = 0.f;
-#if PLVI_SEED_DIR == 2
-                plvi_seed_dir(reg_deg, &sumdx, &sumdy);
-#endif
                 if (lane == 0) {
                     used_set(g, sx, y);
                     g.qlds[0] = (unsigned)sx | ((unsigned)y << 16);
@@ -650,15 +647,10 @@ __global__ __launch_bounds__(64 * kGrowWaves, PLVI_GROW_WPE) void lsd_grow_kerne
                     if (i == 0) {
                         // sumdx = (float)cos(reg_angle), sumdy = (float)sin(reg_angle)
                         // (lsd.cpp:648-649), double libm restated (plvi_math.h), wave-uniform
-#if PLVI_SEED_DIR == 1
-                        plvi_seed_dir(reg_deg, &sumdx, &sumdy);
-#elif PLVI_SEED_DIR == 2
-#else
                         double ds, dc;
                         plvi_sincos((double)reg_deg * kD2R, &ds, &dc);
                         sumdx = (float)dc;
                         sumdy = (float)ds;
-#endif
                     }
                     // lanes of earlier block points that test the same pixel
                     unsigned long long dup = 0;

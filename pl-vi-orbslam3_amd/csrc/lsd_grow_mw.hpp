@@ -206,9 +206,6 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
     // the seed direction (lsd.cpp:648-649) is computed in the first block,
     // while its neighbourhood loads are in flight
     float sumdx = 0.f, sumdy = 0.f;
-#if PLVI_SEED_DIR == 2
-    plvi_seed_dir(reg_deg, &sumdx, &sumdy);
-#endif
     if (lane == 0) {
         mw_own_set(E, sx, sy, sy);
         mw_or(E.H, E.wpr, sx, sy);
@@ -249,15 +246,10 @@ __device__ int mw_grow(const MwEnv& E, int sx, int sy, const MwQueue& Q, int& n_
             ss = cs2.y;
         }
         if (i == 0) {
-#if PLVI_SEED_DIR == 1
-            plvi_seed_dir(reg_deg, &sumdx, &sumdy);
-#elif PLVI_SEED_DIR == 2
-#else
             double ds, dc;
             plvi_sincos((double)reg_deg * kD2R, &ds, &dc);
             sumdx = (float)dc;
             sumdy = (float)ds;
-#endif
         }
         const unsigned long long dup = dup_lanes(pv, nb, bp, nx, ny);
         if (SPEC) {

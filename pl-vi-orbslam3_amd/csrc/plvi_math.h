@@ -397,76 +397,6 @@ PLVI_HD void plvi_sincos(double x, double* s, double* c) {
     *c = n == 0 ? kc : n == 1 ? -ks : n == 2 ? -kc : ks;
 }
 
-// True when (float)v is the float nearest to every double within 64 ulp of v:
-// v is zero, or a normal float magnitude and the 29 mantissa bits the float
-// conversion drops lie more than 64 away from the rounding midpoint.
-PLVI_HD bool plvi_f32_round_safe(double v) {
-    const uint64_t b = d2u(v);
-    const uint32_t t = (uint32_t)b & 0x1fffffffu;
-    const uint32_t dist = t > (1u << 28) ? t - (1u << 28) : (1u << 28) - t;
-    const uint32_t e = (uint32_t)(b >> 52) & 0x7ff;
-    return (b << 1) == 0 || (e >= 1023 - 125 && dist > 64u);
-}
-
-// A double constant materialised in an SGPR pair where it is used: a fused
-// multiply-add takes it as its scalar operand, instead of the compiler
-// hoisting it into a VGPR pair held across the caller's loops.
-PLVI_HD double plvi_sconst(double k) {
-#ifdef __HIP_DEVICE_COMPILE__
-    asm volatile("" : "+s"(k));
-#endif
-    return k;
-}
-
-// Seed direction of region_grow (lsd.cpp:648-649): *c = (float)cos(a),
-// *s = (float)sin(a), a = (double)deg * DEG_TO_RADS. A shorter evaluation than
-// plvi_sincos for the same float results: the first reduction step of
-// rem_pio2 only, the same minimax kernels as fused multiply-adds (both
-// within 2 ulp of the double). Its float rounding equals glibc's unless a
-// result lies within 64 ulp of a float rounding midpoint or the reduction
-// cancels (|a| within 2^-16 of a multiple of pi/2); those take plvi_sincos.
-// Checked for every float deg in [-360, 360] against the host glibc
-// (tests/native/libm_check.cpp and libm_device_check.hip, mode "seeddir").
-PLVI_HD void plvi_seed_dir(float deg, float* c, float* s) {
-    const double invpio2 = 6.36619772367581382433e-01, pio2_1 = 1.57079632673412561417e+00,
-                 pio2_1t = 6.07710050650619224932e-11;
-    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
-                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
-                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
-    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
-                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
-                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
-    const double x = (double)deg * (3.14159265358979323846 / 180);
-    const double fn = __builtin_rint(x * invpio2);
-    const double r = __builtin_fma(-fn, pio2_1, x);  // exact: fn * pio2_1 has 36 bits
-    const double w = fn * pio2_1t;
-    const double y0 = fn == 0.0 ? x : r - w, y1 = (r - y0) - w;  // x keeps the sign of a zero
-    const int gap = (int)((d2u(x) >> 52) & 0x7ff) - (int)((d2u(y0) >> 52) & 0x7ff);
-    const double z = y0 * y0, hz = 0.5 * z;
-    const double ps = __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, z * S6 + S5, plvi_sconst(S4)), plvi_sconst(S3)),
-                                       plvi_sconst(S2));
-    const double ks = y0 - __builtin_fma(-(y0 * z), __builtin_fma(z, ps, plvi_sconst(S1)), __builtin_fma(hz, y1, -y1));
-    const double pc = __builtin_fma(
-        z,
-        __builtin_fma(z, __builtin_fma(z, __builtin_fma(z, z * C6 + C5, plvi_sconst(C4)), plvi_sconst(C3)),
-                      plvi_sconst(C2)),
-        plvi_sconst(C1));
-    const double a = 1.0 - hz;
-    const double kc = a + (((1.0 - a) - hz) + __builtin_fma(z * z, pc, -(y0 * y1)));
-    const int n = (int)fn & 3;
-    const double sv = n == 0 ? ks : n == 1 ? kc : n == 2 ? -ks : -kc;
-    const double cv = n == 0 ? kc : n == 1 ? -ks : n == 2 ? -kc : ks;
-    const bool ok = gap <= 16 && plvi_f32_round_safe(sv) && plvi_f32_round_safe(cv);
-    *c = (float)cv;
-    *s = (float)sv;
-    if (__builtin_expect(!ok, 0)) {
-        double ds, dc;
-        plvi_sincos((double)deg * (3.14159265358979323846 / 180), &ds, &dc);
-        *c = (float)dc;
-        *s = (float)ds;
-    }
-}
-
 // cvRound (round half to even) and roundf (half away from zero).
 PLVI_HD int cv_round_f(float v) { return (int)__builtin_rintf(v); }
 PLVI_HD int cv_round_d(double v) { return (int)__builtin_rint(v); }

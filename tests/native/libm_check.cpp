@@ -9,7 +9,6 @@
 //   lsdangles   : every float deg in [0,360]: float(cos/sin((double)deg*pi/180))
 //   sincospos   : branch-free sincosf vs glibc, every float in [0,120)
 //   fastatan2 N : device cv::fastAtan2 vs the oracle's restatement, N pairs + grid
-//   seeddir     : every float deg in [-360,360]: plvi_seed_dir vs float(cos/sin(deg*pi/180))
 // Prints "mismatches=<k> checked=<n>" and exits non-zero on any mismatch.
 #include <cmath>
 #include <cstdio>
@@ -87,27 +86,6 @@ int main(int argc, char** argv) {
                     double na = -a;
                     if (!same((float)plvi::plvi_cos(na), (float)std::cos(na))) ++b;
                     if (!same((float)plvi::plvi_sin(na), (float)std::sin(na))) ++b;
-                    ++c;
-                }
-                bad += b; checked += c;
-            });
-    } else if (!strcmp(mode, "seeddir")) {
-        // region_grow's seed direction (lsd.cpp:648-649), both signs
-        const double D2R = M_PI / 180;
-        uint32_t hi = plvi::f2u(360.0f);
-        for (int t = 0; t < nt; ++t)
-            th.emplace_back([&, t] {
-                unsigned long long b = 0, c = 0;
-                for (uint32_t u = t; u <= hi; u += nt) {
-                    for (uint32_t sg = 0; sg < 2; ++sg) {
-                        float deg = plvi::u2f(u | (sg << 31)), fc, fs;
-                        double a = (double)deg * D2R;
-                        plvi::plvi_seed_dir(deg, &fc, &fs);
-                        if (!same(fc, (float)std::cos(a)) || !same(fs, (float)std::sin(a))) {
-                            if (b < 5) fprintf(stderr, "seeddir %a\n", deg);
-                            ++b;
-                        }
-                    }
                     ++c;
                 }
                 bad += b; checked += c;

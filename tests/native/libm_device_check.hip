@@ -13,7 +13,6 @@
 //   atan2f n    n seeded (y, x) pairs + grids: plvi_atan2f vs atan2f
 //   fastatan2 n n seeded pairs + grid: plvi_fast_atan2 vs the oracle's cv::fastAtan2
 //               (liboracle.so, oracle_fast_atan2)
-//   seeddir     every float deg in [0, 360], both signs: plvi_seed_dir vs float(cos / sin)
 // Prints "mismatches=<k> checked=<n>", exit 1 on any mismatch, 3 on a HIP error.
 #include <hip/hip_runtime.h>
 
@@ -41,7 +40,7 @@ extern "C" float oracle_fast_atan2(float y, float x);
 
 // mode 0: sinf/cosf of bit pattern base+i; 1: sincosf_pos of bit pattern i;
 // 2: float(cos/sin(+-deg*pi/180)) of bit pattern base+i (4 outputs);
-// 3: atan2f(y[i], x[i]); 4: fast_atan2(y[i], x[i]); 5: plvi_seed_dir(+-deg) (4 outputs)
+// 3: atan2f(y[i], x[i]); 4: fast_atan2(y[i], x[i])
 __global__ void eval_kernel(int mode, uint32_t base, long n, const float* ya, const float* xa, float* o0, float* o1,
                             float* o2, float* o3) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -61,10 +60,6 @@ __global__ void eval_kernel(int mode, uint32_t base, long n, const float* ya, co
         o1[i] = (float)plvi::plvi_sin(a);
         o2[i] = (float)plvi::plvi_cos(-a);
         o3[i] = (float)plvi::plvi_sin(-a);
-    } else if (mode == 5) {
-        const float deg = plvi::u2f(base + (uint32_t)i);
-        plvi::plvi_seed_dir(deg, &o0[i], &o1[i]);
-        plvi::plvi_seed_dir(-deg, &o2[i], &o3[i]);
     } else if (mode == 3) {
         o0[i] = plvi::plvi_atan2f(ya[i], xa[i]);
     } else {
@@ -83,7 +78,7 @@ static bool same(float a, float b) {
 int main(int argc, char** argv) {
     const char* m = argc > 1 ? argv[1] : "sincosf";
     const int mode = !strcmp(m, "sincosf") ? 0 : !strcmp(m, "sincospos") ? 1 : !strcmp(m, "lsdangles") ? 2
-                   : !strcmp(m, "atan2f") ? 3 : !strcmp(m, "fastatan2") ? 4 : !strcmp(m, "seeddir") ? 5 : -1;
+                   : !strcmp(m, "atan2f") ? 3 : !strcmp(m, "fastatan2") ? 4 : -1;
     if (mode < 0) {
         fprintf(stderr, "unknown mode\n");
         return 2;
@@ -91,10 +86,10 @@ int main(int argc, char** argv) {
     unsigned long long total;
     if (mode == 0) total = 1ull << 32;
     else if (mode == 1) total = plvi::f2u(120.0f);
-    else if (mode == 2 || mode == 5) total = (unsigned long long)plvi::f2u(360.0f) + 1;
+    else if (mode == 2) total = (unsigned long long)plvi::f2u(360.0f) + 1;
     else total = argc > 2 ? strtoull(argv[2], 0, 0) : 30000000ull;
     const long chunk = 1l << 26;
-    const int nout = mode == 2 || mode == 5 ? 4 : (mode <= 1 ? 2 : 1);
+    const int nout = mode == 2 ? 4 : (mode <= 1 ? 2 : 1);
     std::vector<float> h[4], ya, xa;
     float* d[4] = {nullptr, nullptr, nullptr, nullptr};
     float *dy = nullptr, *dx = nullptr;
@@ -102,7 +97,7 @@ int main(int argc, char** argv) {
         h[k].resize(chunk);
         CK(hipMalloc(&d[k], chunk * sizeof(float)));
     }
-    if (mode == 3 || mode == 4) {
+    if (mode >= 3) {
         ya.resize(chunk);
         xa.resize(chunk);
         CK(hipMalloc(&dy, chunk * sizeof(float)));
@@ -117,7 +112,7 @@ int main(int argc, char** argv) {
     std::uniform_real_distribution<float> ur(mode == 3 ? -800.f : -4.f, mode == 3 ? 800.f : 4.f);
     for (unsigned long long off = 0; off < total; off += chunk) {
         const long n = (long)std::min<unsigned long long>(chunk, total - off);
-        if (mode == 3 || mode == 4) {
+        if (mode >= 3) {
             for (long i = 0; i < n; ++i) {
                 const unsigned long long g = off + i;
                 if (g % 3 == 0) { ya[i] = plvi::u2f(bits(rng)); xa[i] = plvi::u2f(bits(rng)); }
@@ -141,7 +136,7 @@ int main(int argc, char** argv) {
                     const float x = plvi::u2f((uint32_t)(off + i));
                     if (mode == 0 || mode == 1) {
                         ok = same(h[0][i], sinf(x)) && same(h[1][i], cosf(x));
-                    } else if (mode == 2 || mode == 5) {
+                    } else if (mode == 2) {
                         const double a = (double)x * (M_PI / 180);
                         ok = same(h[0][i], (float)std::cos(a)) && same(h[1][i], (float)std::sin(a)) &&
                              same(h[2][i], (float)std::cos(-a)) && same(h[3][i], (float)std::sin(-a));

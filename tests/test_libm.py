@@ -40,10 +40,6 @@ def test_atan2f_sampled(libm_check):
     _run(libm_check, "atan2f", "30000000")
 
 
-def test_seed_direction_every_float_angle(libm_check):
-    _run(libm_check, "seeddir")                # plvi_seed_dir vs float(cos/sin(deg*pi/180)), every float deg in [-360, 360]
-
-
 def test_branch_free_sincosf_every_float(libm_check):
     _run(libm_check, "sincospos")              # plvi_sincosf_pos vs glibc sinf/cosf, every float in [0, 120)
 
@@ -81,7 +77,6 @@ def test_device_libm_check_builds():
     ("sincosf", (), 4294967296),          # every float bit pattern, sinf and cosf
     ("sincospos", (), None),              # branch-free sincosf, every float in [0, 120)
     ("lsdangles", (), None),              # float(cos/sin(+-deg*pi/180)), every float deg in [0, 360]
-    ("seeddir", (), None),                # region_grow seed direction fast path, every float deg in [-360, 360]
     ("atan2f", ("30000000",), 30000000),
     ("fastatan2", ("30000000",), 30000000),
 ])
