@@ -622,11 +622,12 @@ def run(args, world, rank):
     # on one queue and serialise ORB || lines
     lat_handles = None
     if rank == 0 and world == 1 and not args.no_extra:
-        # (and the batch-64 line's pair, for the same reason)
+        # (and the batch-64 line's pair and its stream, for the same reason)
         lat_handles = (plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, device=dev),
                        plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, device=dev),
                        plvi.ORBextractor(1000, 1.2, 8, 20, 7, W, H, max_batch=64, device=dev),
-                       plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=64, device=dev))
+                       plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, W, H, max_batch=64, device=dev),
+                       torch.cuda.Stream())
     orb, lx, stream, st = s0.orb, s0.lx, s0.stream, s0.st
     kp_p, de_p, co_p, kl_p, lde_p, lco_p = s0.kp_p, s0.de_p, s0.co_p, s0.kl_p, s0.lde_p, s0.lco_p
     outs, lscratch, lm12, lnm = s0.outs, s0.lscratch, s0.lm12, s0.lnm
@@ -1092,7 +1093,11 @@ def extra_lines(args, torch, plvi, synth, lib, stream, W, H, seed0, orb, lx, ext
     stream overlapped with batch k (two device frame buffers)."""
     import threading
     out = {}
-    st = stream.cuda_stream
+    # the batch-64 pair's own stream, created with its extractors at start-up
+    # (on slot 0's stream the step measured 8.46-8.53 ms instead of 7.90:
+    # that stream shares one of the runtime's few hardware queues with a
+    # stream of the pair's schedule; DESIGN.md §6)
+    st = lat_handles[4].cuda_stream
     dev = torch.cuda.current_device()
     cuda = f"cuda:{dev}"
     # (1) batch 64
@@ -1278,7 +1283,7 @@ def extra_lines(args, torch, plvi, synth, lib, stream, W, H, seed0, orb, lx, ext
     out["h2d_overlapped"] = {"value": B * nh / el, "unit": "frames/s", "ms_per_step": el / nh * 1e3,
                              "how": "frames from pinned host memory, H2D of batch k+1 on a copy stream overlapped "
                                     "with batch k's extract+match"}
-    if orb.errors(st) or lx.errors(st):
+    if orb.errors(stream.cuda_stream) or lx.errors(stream.cuda_stream):
         raise RuntimeError("h2d device error flags")
     return out
 
