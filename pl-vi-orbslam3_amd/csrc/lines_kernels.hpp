@@ -808,8 +808,15 @@ __global__ __launch_bounds__(64 * kGrowWaves, PLVI_GROW_WPE) void lsd_grow_kerne
 #define PLVI_RECT_LANE_BLOCKS 2
 #endif
 constexpr int kRectLaneBlocks = PLVI_RECT_LANE_BLOCKS;  // 4-wave workgroups per (octave, frame), 256 regions each
+// points fetched per group: 4 above kRectSmallNf frames (throughput, 64
+// VGPRs); 16 for small batches, where the longest region's three serial
+// passes are the launch (104 VGPRs; batch 64 7.97 -> 7.91 ms,
+// profiles/r05/latency_ab.txt)
 constexpr int kRectU = 4;
+constexpr int kRectUSmall = 16;
+constexpr int kRectSmallNf = 64;
 
+template <int U>
 __global__ __launch_bounds__(256) void lsd_rect_lanes_kernel(const LineOctDev* __restrict__ octs,
                                                              const double* __restrict__ modgrad,
                                                              const LsdRegion* __restrict__ regs,
@@ -833,15 +840,15 @@ __global__ __launch_bounds__(256) void lsd_rect_lanes_kernel(const LineOctDev* _
         // centroid (lsd.cpp:697-705)
         double xs = 0.0, ys = 0.0, sum = 0.0;
         int i = 0;
-        for (; i + kRectU <= rn; i += kRectU) {
-            unsigned v[kRectU];
-            double w[kRectU];
+        for (; i + U <= rn; i += U) {
+            unsigned v[U];
+            double w[U];
 #pragma unroll
-            for (int u = 0; u < kRectU; ++u) v[u] = q[i + u];
+            for (int u = 0; u < U; ++u) v[u] = q[i + u];
 #pragma unroll
-            for (int u = 0; u < kRectU; ++u) w[u] = M[(size_t)(v[u] >> 16) * sw + (v[u] & 0xffffu)];
+            for (int u = 0; u < U; ++u) w[u] = M[(size_t)(v[u] >> 16) * sw + (v[u] & 0xffffu)];
 #pragma unroll
-            for (int u = 0; u < kRectU; ++u) {
+            for (int u = 0; u < U; ++u) {
                 xs = rfma((double)(int)(v[u] & 0xffffu), w[u], xs);
                 ys = rfma((double)(int)(v[u] >> 16), w[u], ys);
                 sum += w[u];
@@ -859,15 +866,15 @@ __global__ __launch_bounds__(256) void lsd_rect_lanes_kernel(const LineOctDev* _
         // inertia (get_theta, lsd.cpp:755-763)
         double Ixx = 0.0, Iyy = 0.0, Ixy = 0.0;
         i = 0;
-        for (; i + kRectU <= rn; i += kRectU) {
-            unsigned v[kRectU];
-            double w[kRectU];
+        for (; i + U <= rn; i += U) {
+            unsigned v[U];
+            double w[U];
 #pragma unroll
-            for (int u = 0; u < kRectU; ++u) v[u] = q[i + u];
+            for (int u = 0; u < U; ++u) v[u] = q[i + u];
 #pragma unroll
-            for (int u = 0; u < kRectU; ++u) w[u] = M[(size_t)(v[u] >> 16) * sw + (v[u] & 0xffffu)];
+            for (int u = 0; u < U; ++u) w[u] = M[(size_t)(v[u] >> 16) * sw + (v[u] & 0xffffu)];
 #pragma unroll
-            for (int u = 0; u < kRectU; ++u) {
+            for (int u = 0; u < U; ++u) {
                 const double dx = (double)(int)(v[u] & 0xffffu) - xs, dy = (double)(int)(v[u] >> 16) - ys;
                 Ixx = rfma(dy * dy, w[u], Ixx);
                 Iyy = rfma(dx * dx, w[u], Iyy);
@@ -892,12 +899,12 @@ __global__ __launch_bounds__(256) void lsd_rect_lanes_kernel(const LineOctDev* _
         // l extents (lsd.cpp:722-735): order-free max(0, .) / min(0, .)
         double lmax = 0, lmin = 0;
         i = 0;
-        for (; i + kRectU <= rn; i += kRectU) {
-            unsigned v[kRectU];
+        for (; i + U <= rn; i += U) {
+            unsigned v[U];
 #pragma unroll
-            for (int u = 0; u < kRectU; ++u) v[u] = q[i + u];
+            for (int u = 0; u < U; ++u) v[u] = q[i + u];
 #pragma unroll
-            for (int u = 0; u < kRectU; ++u) {
+            for (int u = 0; u < U; ++u) {
                 const double l = rfma((double)(int)(v[u] & 0xffffu) - xs, dxv, ((double)(int)(v[u] >> 16) - ys) * dyv);
                 lmax = l > lmax ? l : lmax;
                 lmin = l < lmin ? l : lmin;
