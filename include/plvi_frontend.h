@@ -911,10 +911,14 @@ int plvi_frame_extract_match_batch(plvi_orb_extractor* orb, plvi_line_extractor*
                                    int* d_line_matches, int* d_line_nmatch, void* stream);
 
 /* The event the last plvi_frame_extract_batch on `lines` recorded once its
- * ORB extraction was complete (a hipEvent_t owned by the handle, re-recorded
- * by the next call): work on the ORB tables -- kNN-2 against the previous
- * frame -- can wait on it (plvi_stream_wait_event) and overlap the rest of
- * the line path instead of waiting for the whole frame. */
+ * ORB extraction was complete (a hipEvent_t owned by the handle): work on the
+ * ORB tables -- kNN-2 against the previous frame -- can wait on it
+ * (plvi_stream_wait_event) and overlap the rest of the line path instead of
+ * waiting for the whole frame.  After plvi_frame_extract_match_batch the same
+ * event is recorded after the ORB kNN-2 as well (it then covers extraction
+ * AND d_idx0/d_d0/d_idx1/d_d1).  The handle re-records it on its next
+ * extract call: issue every wait on it before the next extract call on the
+ * same handle, or the wait refers to the newer batch. */
 int plvi_frame_orb_event(plvi_line_extractor* lines, void** event);
 
 /* ------------------------------------------------------------ initialization

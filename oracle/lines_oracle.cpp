@@ -172,8 +172,10 @@ struct LSD {
         reg_angle = angles.px[addr];
         reg[0].angle = reg_angle;
         reg[0].modgrad = modgrad.px[addr];
-        float sumdx = (float)std::cos(reg_angle);
-        float sumdy = (float)std::sin(reg_angle);
+        double seed_s, seed_c;  // lsd.cpp:648-649, one sincos call as in the reference object
+        ::sincos(reg_angle, &seed_s, &seed_c);
+        float sumdx = (float)seed_c;
+        float sumdy = (float)seed_s;
         used[addr] = 1;
         for (int i = 0; i < reg_size; ++i) {
             const RegionPoint rp = reg[i];
@@ -235,7 +237,10 @@ struct LSD {
         x /= sum;
         y /= sum;
         double theta = get_theta(reg_size, x, y, reg_angle, prec);
-        double dx = std::cos(theta), dy = std::sin(theta);
+        // lsd.cpp:710-711: GCC merges the pair into one glibc sincos call (the
+        // reference object's `call sincos`; x86-64 sincos has no FMA ifunc)
+        double dx, dy;
+        ::sincos(theta, &dy, &dx);
         double l_min = 0, l_max = 0, w_min = 0, w_max = 0;
         for (int i = 0; i < reg_size; ++i) {
             double regdx = (double)reg[i].x - x, regdy = (double)reg[i].y - y;

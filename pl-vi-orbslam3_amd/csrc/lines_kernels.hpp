@@ -895,7 +895,10 @@ __global__ __launch_bounds__(256) void lsd_rect_lanes_kernel(const LineOctDev* _
                            : (double)plvi_fast_atan2((float)Ixy, (float)(lambda - Iyy));
         theta *= kD2R;
         if (angle_diff(theta, r.angle) > prec) theta += kPi;
-        const double dxv = plvi_cos(theta), dyv = plvi_sin(theta);
+        // dx = cos(theta), dy = sin(theta) (lsd.cpp:710-711): the reference
+        // object calls glibc's sincos; its doubles feed l and the endpoints
+        double dxv, dyv;
+        plvi_sincos_glibc(theta, &dyv, &dxv);
         // l extents (lsd.cpp:722-735): order-free max(0, .) / min(0, .)
         double lmax = 0, lmin = 0;
         i = 0;
@@ -983,6 +986,7 @@ __device__ inline int line_iter_count(int W, int H, float fx1, float fy1, float 
 }
 
 constexpr int kKlCap = 4096;  // keylines per frame before the top-k filter
+static_assert(kKlCap <= kSortBlockMax, "std_sort_block packs 16-bit counts and positions");
 
 __global__ __launch_bounds__(256) void line_assemble_kernel(const LineOctDev* __restrict__ octs, int nOct,
                                                             const LsdLine* __restrict__ lines,

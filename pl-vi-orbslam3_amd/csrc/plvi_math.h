@@ -11,11 +11,14 @@
 //       generic SSE2 build, no FMA).  KeyLine.angle
 //       (LSDDetector_custom.cpp:336).
 //   plvi_fast_atan2       : cv::fastAtan2 (OpenCV 4.2, degrees, no FMA).
-//   plvi_cos / plvi_sin   : double cos/sin for LSD region_grow's seed and
-//       region2rect (lsd.cpp:648-649, 710-711): fdlibm kernels with a
-//       3-part Cody-Waite reduction (< 1 ulp).  Their float conversions
-//       are checked exhaustively against glibc over every float angle LSD
-//       can produce; the double values themselves are not claimed bit-exact.
+//   plvi_cos / plvi_sin / plvi_sincos : double cos/sin for LSD region_grow's
+//       seed (lsd.cpp:648-649), which only uses their float conversions:
+//       fdlibm kernels with a 3-part Cody-Waite reduction (< 1 ulp), the
+//       float conversions checked exhaustively against glibc over every
+//       float angle LSD can produce (the doubles are not glibc's).
+//   plvi_sincos_glibc     : glibc 2.35's double sincos itself (s_sincos.c,
+//       SSE2 build), for region2rect (lsd.cpp:710-711), whose doubles feed
+//       the endpoints: bitwise equal to glibc over region2rect's whole domain.
 //
 // Every function is __host__ __device__ so tests/native/libm_check.cpp can
 // compare the very same code against the host glibc exhaustively.  All
@@ -395,6 +398,129 @@ PLVI_HD void plvi_sincos(double x, double* s, double* c) {
     const double ks = k_sin(y0, y1, 1), kc = k_cos(y0, y1);
     *s = n == 0 ? ks : n == 1 ? kc : n == 2 ? -ks : -kc;
     *c = n == 0 ? kc : n == 1 ? -ks : n == 2 ? -kc : ks;
+}
+
+// ------------------------------------------------------------ glibc sincos
+// glibc 2.35 sysdeps/ieee754/dbl-64/s_sincos.c with s_sin.c's do_sin, do_cos,
+// reduce_sincos and do_sincos (constants from usncs.h).  On x86-64 `sincos`
+// is NOT an ifunc (unlike sin / cos, whose __sin_fma / __cos_fma contract
+// multiply-adds): libm.so.6 exports one SSE2 build of it, no fused operation
+// in its disassembly, so every operation below is one IEEE operation
+// (callers build with -ffp-contract=off).  This is the call region2rect
+// makes (src/LSD/lsd.cpp:710-711; the reference object calls sincos,
+// tests/test_ref_objects.py), whose unrounded double results feed the l
+// extents and the endpoints (:719, :729-732).  Bitwise equal to glibc's
+// sincos over region2rect's domain (every θ = (double)T·π/180 for float T in
+// [0, 360], and θ + π) on the host and on the device
+// (tests/native/libm_check.cpp / libm_device_check.hip, mode r2rect) and on
+// sampled doubles (mode sincosd).  Domain: |x| < 105414350 (glibc's
+// __branred range is not restated).
+constexpr double kGlibcSinCosTab[440] = {
+#include "glibc_sincostab.inc"
+};
+
+PLVI_HD void glibc_tab(double u, double* sn, double* ssn, double* cs, double* ccs) {
+    const int k = (int)(uint32_t)d2u(u) << 2;  // SINCOS_TABLE_LOOKUP: u.i[LOW_HALF] << 2
+    *sn = kGlibcSinCosTab[k];
+    *ssn = kGlibcSinCosTab[k + 1];
+    *cs = kGlibcSinCosTab[k + 2];
+    *ccs = kGlibcSinCosTab[k + 3];
+}
+
+#define PLVI_G_SN3 -0x1.5555555555515p-3
+#define PLVI_G_SN5 0x1.11110e829872fp-7
+#define PLVI_G_CS2 0x1.0p-1
+#define PLVI_G_CS4 -0x1.5555555555535p-5
+#define PLVI_G_CS6 0x1.6c16bedd9e239p-10
+#define PLVI_G_BIG 0x1.8p+45
+
+// do_cos (s_sin.c)
+PLVI_HD double glibc_do_cos(double x, double dx) {
+    if (x < 0) dx = -dx;
+    const double u = PLVI_G_BIG + __builtin_fabs(x);
+    x = __builtin_fabs(x) - (u - PLVI_G_BIG) + dx;
+    const double xx = x * x;
+    const double s = x + x * xx * (PLVI_G_SN3 + xx * PLVI_G_SN5);
+    const double c = xx * (PLVI_G_CS2 + xx * (PLVI_G_CS4 + xx * PLVI_G_CS6));
+    double sn, ssn, cs, ccs;
+    glibc_tab(u, &sn, &ssn, &cs, &ccs);
+    const double cor = (ccs - s * ssn - cs * c) - sn * s;
+    return cs + cor;
+}
+
+// do_sin (s_sin.c), TAYLOR_SIN below 0.126
+PLVI_HD double glibc_do_sin(double x, double dx) {
+    const double xold = x;
+    if (__builtin_fabs(x) < 0.126) {
+        const double xx = x * x;
+        // POLYNOMIAL(xx) = ((((s5*xx + s4)*xx + s3)*xx + s2)*xx) + s1
+        const double p = ((((-0x1.addffc2fcdf59p-26 * xx + 0x1.71de27b9a7ed9p-19) * xx + -0x1.a01a019db08b8p-13) * xx +
+                           0x1.1111111110ecep-7) * xx) + -0x1.5555555555555p-3;
+        const double t = ((p * x - 0.5 * dx) * xx + dx);
+        return x + t;
+    }
+    if (x <= 0) dx = -dx;
+    const double u = PLVI_G_BIG + __builtin_fabs(x);
+    x = __builtin_fabs(x) - (u - PLVI_G_BIG);
+    const double xx = x * x;
+    const double s = x + (dx + x * xx * (PLVI_G_SN3 + xx * PLVI_G_SN5));
+    const double c = x * dx + xx * (PLVI_G_CS2 + xx * (PLVI_G_CS4 + xx * PLVI_G_CS6));
+    double sn, ssn, cs, ccs;
+    glibc_tab(u, &sn, &ssn, &cs, &ccs);
+    const double cor = (ssn + s * ccs - sn * c) + cs * s;
+    return __builtin_copysign(sn + cor, xold);
+}
+
+// reduce_sincos (s_sin.c): quadrant and a + da = x - n*pi/2
+PLVI_HD int glibc_reduce(double x, double* a, double* da) {
+    const double hpinv = 0x1.45f306dc9c883p-1, toint = 0x1.8p+52;
+    const double mp1 = 0x1.921fb58000000p+0, mp2 = -0x1.dde973c000000p-27;
+    const double pp3 = -0x1.cb3b398000000p-55, pp4 = -0x1.d747f23e32ed7p-83;
+    const double t = (x * hpinv + toint);
+    const double xn = t - toint;
+    const int n = (int)((uint32_t)d2u(t) & 3);
+    const double y = (x - xn * mp1) - xn * mp2;
+    double t1 = xn * pp3;
+    const double t2 = y - t1;
+    double db = (y - t2) - t1;
+    t1 = xn * pp4;
+    const double b = t2 - t1;
+    db += (t2 - b) - t1;
+    *a = b;
+    *da = db;
+    return n;
+}
+
+PLVI_HD double glibc_do_sincos(double a, double da, int n) {
+    const double r = (n & 1) ? glibc_do_cos(a, da) : glibc_do_sin(a, da);
+    return (n & 2) ? -r : r;
+}
+
+PLVI_HD void plvi_sincos_glibc(double x, double* sinx, double* cosx) {
+    const uint32_t k = (uint32_t)(d2u(x) >> 32) & 0x7fffffffu;
+    if (k < 0x400368fdu) {
+        if (k < 0x3e400000u) {
+            *sinx = x;
+            *cosx = 1.0;
+            return;
+        }
+        if (k < 0x3feb6000u) {
+            *sinx = glibc_do_sin(x, 0);
+            *cosx = glibc_do_cos(x, 0);
+            return;
+        }
+        const double hp0 = 0x1.921fb54442d18p+0, hp1 = 0x1.1a62633145c07p-54;
+        const double y = hp0 - __builtin_fabs(x);
+        const double a = y + hp1;
+        const double da = (y - a) + hp1;
+        *sinx = __builtin_copysign(glibc_do_cos(y, hp1), x);
+        *cosx = glibc_do_sin(a, da);
+        return;
+    }
+    double a, da;
+    const int n = glibc_reduce(x, &a, &da);
+    *sinx = glibc_do_sincos(a, da, n);
+    *cosx = glibc_do_sincos(a, da, n + 1);
 }
 
 // cvRound (round half to even) and roundf (half away from zero).

@@ -236,6 +236,11 @@ __device__ inline int block_partition(SortItem* a, int f0, int l0, unsigned shor
     return cut;
 }
 
+// Precondition: n <= kSortBlockMax.  block_partition packs a thread's two
+// counts into one int (cl | cr << 16, each < 2^15 keeps the scan's sum
+// positive) and keeps positions as unsigned short; callers size their arrays
+// with a compile-time cap and static_assert it against this limit.
+constexpr int kSortBlockMax = 32767;
 __device__ inline void std_sort_block(SortItem* a, int n, SortRange* rng0, SortRange* rng1, unsigned* segbits,
                                       int* ctl, unsigned short* lpos, unsigned short* rpos, int* scan,
                                       int depth0 = -1) {  // depth0 >= 0: test override of 2 lg n

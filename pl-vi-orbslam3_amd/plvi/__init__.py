@@ -159,6 +159,14 @@ class FrustumParams(ctypes.Structure):
 FRUSTUM_SEARCH, FRUSTUM_OBS, FRUSTUM_SEARCH_R, FRUSTUM_VISIBLE, FRUSTUM_TRACK = 1, 2, 4, 8, 16
 
 
+def _same_len(n, **arrays):
+    """The C entry points read n records from every host array: refuse a shorter (or longer) one
+    instead of letting hipMemcpy read past its end."""
+    for name, a in arrays.items():
+        if a is not None and len(a) != n:
+            raise ValueError(f"{name} has {len(a)} records, expected {n}")
+
+
 def frustum_params_init(p):
     """plvi_frustum_params_init: PredictScale's level_ratio table from nlevels / log_scale_factor."""
     _check(load().plvi_frustum_params_init(ctypes.byref(p)), "plvi_frustum_params_init")
@@ -182,6 +190,7 @@ def frustum_points(params, pos, normal, dist, in_flags, proj=None, level=None, d
     prr = (np.zeros((n, 4), np.float32) if proj_r is None else np.array(proj_r, np.float32).reshape(-1, 4)) \
         if two else None
     lvr = (np.zeros(n, np.int32) if level_r is None else np.array(level_r, np.int32)) if two else None
+    _same_len(n, normal=nr, dist=ds, in_flags=fi, proj=pr, level=lv, depth=de, proj_r=prr, level_r=lvr)
     fo = np.zeros(max(n, 1), np.uint8)
     nv = _check(load().plvi_frustum_points(ctypes.byref(params), _ptr(pos), _ptr(nr), _ptr(ds), _ptr(fi), n,
                                            _ptr(fo), _ptr(pr), _ptr(lv), None if prr is None else _ptr(prr),
@@ -201,6 +210,7 @@ def frustum_lines(params, sep, normal, dist, in_flags, desc=None, proj=None, ang
     de = None if desc is None else np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
     pr = np.zeros((n, 4), np.float32) if proj is None else np.array(proj, np.float32).reshape(-1, 4)
     an = np.zeros(n, np.float64) if angle is None else np.array(angle, np.float64)
+    _same_len(n, normal=nr, dist=ds, in_flags=fi, desc=de, proj=pr, angle=an)
     iv = np.zeros(max(n, 1), np.uint8)
     cp = np.zeros(max(n, 1), np.int32)
     cd = np.zeros((max(n, 1), 32), np.uint8)

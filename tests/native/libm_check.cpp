@@ -9,6 +9,9 @@
 //   lsdangles   : every float deg in [0,360]: float(cos/sin((double)deg*pi/180))
 //   sincospos   : branch-free sincosf vs glibc, every float in [0,120)
 //   fastatan2 N : device cv::fastAtan2 vs the oracle's restatement, N pairs + grid
+//   r2rect      : every float T in [0,360]: plvi_sincos_glibc(θ), θ = (double)T*pi/180
+//                 and θ + pi, bitwise (double) vs glibc sincos
+//   sincosd N   : plvi_sincos_glibc vs glibc sincos on N seeded doubles, |x| < 105414350
 // Prints "mismatches=<k> checked=<n>" and exits non-zero on any mismatch.
 #include <cmath>
 #include <cstdio>
@@ -21,6 +24,18 @@
 
 #include "../../pl-vi-orbslam3_amd/csrc/plvi_math.h"
 #include "../../oracle/cvprim.h"
+
+static bool samed(double a, double b) {
+    if (std::isnan(a) && std::isnan(b)) return true;
+    return plvi::d2u(a) == plvi::d2u(b);
+}
+
+static bool sincos_ok(double x) {
+    double s, c, gs, gc;
+    plvi::plvi_sincos_glibc(x, &s, &c);
+    sincos(x, &gs, &gc);
+    return samed(s, gs) && samed(c, gc);
+}
 
 static bool same(float a, float b) {
     if (std::isnan(a) && std::isnan(b)) return true;
@@ -100,6 +115,45 @@ int main(int argc, char** argv) {
                     float x = plvi::u2f(u), s, co;
                     plvi::plvi_sincosf_pos(x, &s, &co);
                     if (!same(s, sinf(x)) || !same(co, cosf(x))) { if (b < 5) fprintf(stderr, "sincospos %a\n", x); ++b; }
+                    ++c;
+                }
+                bad += b; checked += c;
+            });
+    } else if (!strcmp(mode, "r2rect")) {
+        // region2rect (lsd.cpp:707-711): theta = fastAtan2(...) * DEG_TO_RADS,
+        // + M_PI when it disagrees with the region angle, then sincos(theta)
+        const double D2R = M_PI / 180;
+        uint32_t hi = plvi::f2u(360.0f);
+        for (int t = 0; t < nt; ++t)
+            th.emplace_back([&, t] {
+                unsigned long long b = 0, c = 0;
+                for (uint32_t u = t; u <= hi; u += nt) {
+                    double a = (double)plvi::u2f(u) * D2R;
+                    if (!sincos_ok(a)) { if (b < 5) fprintf(stderr, "r2rect %a\n", a); ++b; }
+                    a += M_PI;
+                    if (!sincos_ok(a)) { if (b < 5) fprintf(stderr, "r2rect+pi %a\n", a); ++b; }
+                    c += 2;
+                }
+                bad += b; checked += c;
+            });
+    } else if (!strcmp(mode, "sincosd")) {
+        long n = argc > 2 ? atol(argv[2]) : 100000000L;
+        for (int t = 0; t < nt; ++t)
+            th.emplace_back([&, t] {
+                std::mt19937_64 rng(4321 + t);
+                std::uniform_real_distribution<double> u1(-10.0, 10.0), u2(-105414349.0, 105414349.0);
+                std::uniform_int_distribution<uint64_t> bits;
+                unsigned long long b = 0, c = 0;
+                for (long i = t; i < n; i += nt) {
+                    double x;
+                    if (i % 3 == 0) x = u1(rng);
+                    else if (i % 3 == 1) x = u2(rng);
+                    else {  // random bit patterns below 105414350 (all binades, denormals)
+                        x = plvi::u2d(bits(rng));
+                        if (!(std::fabs(x) < 105414349.0)) x = std::fmod(x, 105414349.0);
+                        if (std::isnan(x)) x = 0.5;
+                    }
+                    if (!sincos_ok(x)) { if (b < 5) fprintf(stderr, "sincosd %a\n", x); ++b; }
                     ++c;
                 }
                 bad += b; checked += c;

@@ -88,6 +88,29 @@ def test_frustum_params_init_arguments():
         assert oracle_lib.predict_scale(r, 1.0, 0.0, 8) == 0
 
 
+def test_frustum_wrappers_refuse_short_arrays():
+    """The C entry points copy n records from every host array: a shorter one raises ValueError in the
+    wrapper before any copy (no GPU needed)."""
+    import plvi
+    p = plvi.FrustumParams()
+    n = 5
+    pos, nrm, dst, fl = np.zeros((n, 3)), np.zeros((n, 3)), np.zeros((n, 2)), np.ones(n, np.uint8)
+    for kw in (dict(normal=nrm[:4]), dict(dist=dst[:3]), dict(in_flags=fl[:1]), dict(level=np.zeros(4)),
+               dict(depth=np.zeros(6)), dict(proj=np.zeros((2, 4)))):
+        args = dict(normal=nrm, dist=dst, in_flags=fl)
+        args.update(kw)
+        with pytest.raises(ValueError):
+            plvi.frustum_points(p, pos, args["normal"], args["dist"], args["in_flags"],
+                                **{k: v for k, v in kw.items() if k not in ("normal", "dist", "in_flags")})
+    sep = np.zeros((n, 6))
+    for kw in (dict(normal=nrm[:4]), dict(desc=np.zeros((3, 32), np.uint8)), dict(angle=np.zeros(2))):
+        args = dict(normal=nrm, dist=dst, in_flags=fl)
+        args.update(kw)
+        with pytest.raises(ValueError):
+            plvi.frustum_lines(p, sep, args["normal"], args["dist"], args["in_flags"],
+                               **{k: v for k, v in kw.items() if k not in ("normal", "dist", "in_flags")})
+
+
 def _numpy_is_in_frustum(p, case):
     """Frame.cc:760-835 (Pinhole, compat 0) in numpy float32 / float64: one IEEE op per operator, the
     Frame.cc.o fused mTrackProjXR via util.fmaf, PredictScale via the oracle's logf."""

@@ -36,6 +36,17 @@ def test_lsd_double_cos_sin_every_float_angle(libm_check):
     _run(libm_check, "lsdangles")              # float(cos/sin(deg*pi/180)) for every float deg in [0,360]
 
 
+def test_region2rect_sincos_double_bitwise(libm_check):
+    # region2rect's sincos(theta) (lsd.cpp:710-711) as DOUBLES, theta = T*pi/180
+    # for every float T in [0, 360] and theta + pi: 2 271 739 906 arguments
+    out = _run(libm_check, "r2rect")
+    assert "checked=2271739906" in out
+
+
+def test_glibc_sincos_sampled_doubles(libm_check):
+    _run(libm_check, "sincosd", "30000000")    # |x| < 105414350, all binades
+
+
 def test_atan2f_sampled(libm_check):
     _run(libm_check, "atan2f", "30000000")
 
@@ -77,6 +88,7 @@ def test_device_libm_check_builds():
     ("sincosf", (), 4294967296),          # every float bit pattern, sinf and cosf
     ("sincospos", (), None),              # branch-free sincosf, every float in [0, 120)
     ("lsdangles", (), None),              # float(cos/sin(+-deg*pi/180)), every float deg in [0, 360]
+    ("r2rect", (), None),                 # region2rect's double sincos(theta), theta + pi: every float deg
     ("atan2f", ("30000000",), 30000000),
     ("fastatan2", ("30000000",), 30000000),
 ])
