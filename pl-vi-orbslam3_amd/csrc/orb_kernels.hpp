@@ -261,6 +261,64 @@ __global__ __launch_bounds__(64 * (kPyrFrames + 1)) __attribute__((amdgpu_waves_
 }
 
 // ---------------------------------------------------------------------------
+// K1a', small batches: one launch per level (level l from level l-1 in HBM /
+// L2), thread = 4 consecutive output pixels of one row, the whole chip on
+// every level.  The streaming kernel above runs one resizer wave per frame
+// through all 7 chained levels: at one frame that is a 2.6 ms serial chain
+// for 1.6 MB.  Same arithmetic, same packed column table,
+// same 8U / generic switch.  Level 1 reads the caller's frames (level 0's
+// plane is written later by orb_blur_fast_kernel).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void orb_resize_level_kernel(const uint8_t* __restrict__ src, size_t s_frame,
+                                                               size_t s_row, int sw, int sh, uint8_t* __restrict__ dst,
+                                                               size_t d_frame, int w, int h, double scy,
+                                                               const uint32_t* __restrict__ T, int generic) {
+    PLVI_ORB_PRIO_SET();
+    const int qpr = (w + 3) >> 2;  // quads per row
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= qpr * h) return;
+    const int f = blockIdx.y;
+    const int y = i / qpr, x0 = (i - y * qpr) * 4;
+    float fy = (float)((y + 0.5) * scy - 0.5);
+    int sy = (int)fy;
+    sy -= (sy > fy);
+    fy -= (float)sy;
+    const int r0 = min(max(sy, 0), sh - 1), r1 = min(max(sy + 1, 0), sh - 1);
+    const unsigned b0 = (unsigned)__builtin_rintf((1.f - fy) * 2048), b1 = (unsigned)__builtin_rintf(fy * 2048);
+    const uint8_t* S0 = src + (size_t)f * s_frame + (size_t)r0 * s_row;
+    const uint8_t* S1 = src + (size_t)f * s_frame + (size_t)r1 * s_row;
+    uint8_t* D = dst + (size_t)f * d_frame + (size_t)y * w;
+    uint32_t e[4];
+    unsigned p00[4], p01[4], p10[4], p11[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) e[u] = x0 + u < w ? T[x0 + u] : T[x0];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int sx = e[u] & 1023;
+        const int sx1 = (e[u] >> 24) & 1 ? sx : sx + 1;
+        p00[u] = S0[sx];
+        p01[u] = S0[sx1];
+        p10[u] = S1[sx];
+        p11[u] = S1[sx1];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        if (x0 + u >= w) break;
+        const bool cr = (e[u] >> 24) & 1;
+        const unsigned a0 = cr ? 2048u : (e[u] >> 10) & 4095;
+        const unsigned a1 = cr ? 0u : 2047u - ((e[u] >> 10) & 4095) + ((e[u] >> 22) & 3);
+        const unsigned h0 = __umul24(p00[u], a0) + __umul24(p01[u], a1);
+        const unsigned h1 = __umul24(p10[u], a0) + __umul24(p11[u], a1);
+        int v;
+        if (!generic)
+            v = (int)(((__umul24(b0, h0 >> 4) >> 16) + (__umul24(b1, h1 >> 4) >> 16) + 2) >> 2);
+        else
+            v = min((int)((b0 * h0 + b1 * h1 + (1u << 21)) >> 22), 255);
+        D[x0 + u] = (uint8_t)v;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // K1b: 7x7 fixed-point Gaussian blur (ORBextractor.cc:1115; A.4) and FAST
 // score map (A.3) of every level in one launch.  One wave per strip of up to
 // kBfCols output columns x kBfRows rows: lane L holds the four columns

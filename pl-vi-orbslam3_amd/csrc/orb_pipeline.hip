@@ -95,6 +95,10 @@ struct OrbPipeline {
         odesc, ocount, omono, err, staging;
     size_t pyrSmem = 0;  // orb_pyramid_kernel LDS: column table + source-level row rings
     int xtabN = 0, pyrFrameLds = 0;
+    // batches of at most this many frames build the pyramid level by level
+    // (orb_resize_level_kernel, one launch per level) instead of streaming it
+    // (PLVI_PYR_LEVELWISE overrides)
+    int pyrLevelwiseMax = 1024;
     int lastFrames = 0;
     // Stage timing with HIP events on the launch stream (bench.py roofline).
     static constexpr int kStages = 7, kRing = 512;
@@ -181,6 +185,7 @@ struct OrbPipeline {
         prm = *p;
         W = width; H = height; Bcap = max_batch; device = dev; L = p->nlevels;
         if (const char* e = getenv("PLVI_GROW_GATE")) gateStage = std::min(3, std::max(0, atoi(e)));
+        if (const char* e = getenv("PLVI_PYR_LEVELWISE")) pyrLevelwiseMax = atoi(e);
         PLVI_CHECK(hipSetDevice(device));
         {
             // the handle's own stream (single-frame calls, batches without a
@@ -391,14 +396,28 @@ struct OrbPipeline {
             if (evStage && evStageAt == k) PLVI_CHECK(hipEventRecord(evStage, s_));
             return PLVI_OK;
         };
-        // K1a: the pyramid (ComputePyramid, chained resize: level l from l-1)
-        // of every frame in one streaming launch, one wave per frame
+        // K1a: the pyramid (ComputePyramid, chained resize: level l from l-1):
+        // small batches level by level over the whole chip, large ones in one
+        // streaming launch (a loader and a resizer wave per frame)
         if (L > 1) {
             const bool ktP = ktime && knP < kKRing;
             if (ktP) PLVI_CHECK(hipEventRecord(kevP[2 * knP], st));
-            hipLaunchKernelGGL(orb_pyramid_kernel, dim3((nf + kPyrFrames - 1) / kPyrFrames), dim3(64 * (kPyrFrames + 1)),
-                               pyrSmem, st, d_lv.as<OrbLevelDev>(), L, d_frames, frame_stride, row_stride, nf, P,
-                               (const uint32_t*)d_xtab.as<uint32_t>(), xtabN, pyrFrameLds, resizeGeneric);
+            if (nf <= pyrLevelwiseMax) {
+                for (int l = 1; l < L; ++l) {
+                    const OrbLevelDev& s = lv[l - 1];
+                    const OrbLevelDev& d = lv[l];
+                    const uint8_t* src = l == 1 ? d_frames : P + s.off;
+                    const size_t sfr = l == 1 ? frame_stride : (size_t)s.plane, srow = l == 1 ? row_stride : (size_t)s.w;
+                    const int items = ((d.w + 3) >> 2) * d.h;
+                    hipLaunchKernelGGL(orb_resize_level_kernel, dim3((items + 255) / 256, nf), dim3(256), 0, st, src, sfr,
+                                       srow, s.w, s.h, P + d.off, (size_t)d.plane, d.w, d.h, d.rsy,
+                                       (const uint32_t*)d_xtab.as<uint32_t>() + d.xtab, resizeGeneric);
+                }
+            } else {
+                hipLaunchKernelGGL(orb_pyramid_kernel, dim3((nf + kPyrFrames - 1) / kPyrFrames), dim3(64 * (kPyrFrames + 1)),
+                                   pyrSmem, st, d_lv.as<OrbLevelDev>(), L, d_frames, frame_stride, row_stride, nf, P,
+                                   (const uint32_t*)d_xtab.as<uint32_t>(), xtabN, pyrFrameLds, resizeGeneric);
+            }
             if (ktP) {
                 PLVI_CHECK(hipEventRecord(kevP[2 * knP + 1], st));
                 ++knP;

@@ -52,6 +52,41 @@ def test_orb_pyramid_matches_oracle(orb640):
         assert np.array_equal(got, exp["pyr"]), f"level {level}"
 
 
+@pytest.mark.parametrize("mode", ["0", "100000"])
+@pytest.mark.parametrize("wh", [(640, 480), (752, 480), (641, 479)])
+def test_orb_pyramid_builders_batch(plvi_lib, monkeypatch, mode, wh):
+    """Both pyramid builders -- the streaming kernel (PLVI_PYR_LEVELWISE=0: every batch) and the
+    level-by-level launches (PLVI_PYR_LEVELWISE=100000) -- give the oracle's levels for every frame of a
+    batch read from a row-padded device buffer, and the oracle's keypoints and descriptors."""
+    monkeypatch.setenv("PLVI_PYR_LEVELWISE", mode)
+    w, h = wh
+    imgs = [synth.frame(40 + k, w, h) for k in range(3)]
+    imgs.append(structured_frames(w, h)["checker"])
+    B, stride = len(imgs), w + 5  # rows padded: frames as a strided view
+    frames = np.zeros((B, h, stride), np.uint8)
+    for k, im in enumerate(imgs):
+        frames[k, :, :w] = im
+    buf = plvi.DeviceBuffer(frames.nbytes)
+    buf.upload(frames)
+    ext = plvi.ORBextractor(1000, 1.2, 8, 20, 7, w, h, max_batch=B)
+    ext.extract_batch(buf.ptr, B, h * stride, stride)
+    plvi_lib.plvi_device_synchronize()
+    assert ext.errors() == 0
+    for k, im in enumerate(imgs):
+        for level in range(8):
+            exp = ol.orb_stage(im, level)
+            assert np.array_equal(ext.pyramid_level(level, k), exp["pyr"]), f"mode {mode} frame {k} level {level}"
+    kp_p, de_p, co_p, mo_p, cap = ext.outputs()
+    cnt = plvi.download(co_p, np.zeros(B, np.int32))
+    mono = plvi.download(mo_p, np.zeros(B, np.int32))
+    kps = plvi.download(kp_p, np.zeros(B * cap, plvi.KEYPOINT_DTYPE))
+    desc = plvi.download(de_p, np.zeros((B * cap, 32), np.uint8))
+    for k, im in enumerate(imgs):
+        s = slice(k * cap, k * cap + cnt[k])
+        _assert_same((int(mono[k]), kps[s], desc[s]), ol.orb_extract(im), f"mode {mode} frame {k}")
+    ext.close()
+
+
 def test_orb_real_euroc_752(orb752):
     fr = real_frames()
     for k in ("euroc1", "euroc2"):
