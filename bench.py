@@ -655,17 +655,20 @@ def run(args, world, rank):
 
     step_no = [0]
 
+    def fused(sl, fptr):
+        # extract + match as one schedule (plvi_frame_extract_match_batch: the
+        # matching issued on the schedule's own streams, same kernels and
+        # tables as extract() + match())
+        plvi.frame_extract_match_batch(sl.orb, sl.lx, fptr, B, W * H, W,
+                                       [o.data_ptr() for o in sl.outs], 0.9, sl.lscratch.data_ptr(),
+                                       sl.lm12.data_ptr(), sl.lnm.data_ptr(), stream=sl.st)
+
     def step():
         k = step_no[0]
         step_no[0] += 1
         sl = slots[k % len(slots)]
         lo = (k % nwin) * wstride
-        # extract + match as one schedule (plvi_frame_extract_match_batch: the
-        # matching issued on the schedule's own streams, same kernels and
-        # tables as extract() + match())
-        plvi.frame_extract_match_batch(sl.orb, sl.lx, seq[lo].data_ptr(), B, W * H, W,
-                                       [o.data_ptr() for o in sl.outs], 0.9, sl.lscratch.data_ptr(),
-                                       sl.lm12.data_ptr(), sl.lnm.data_ptr(), stream=sl.st)
+        fused(sl, seq[lo].data_ptr())
         if args.gather:
             gather(sl)
 
@@ -875,7 +878,9 @@ def run(args, world, rank):
     extra = {}
     if rank == 0 and world == 1 and not args.no_extra:
         extra = extra_lines(args, torch, plvi, synth, lib, stream, W, H, seed0, orb, lx, extract, match, seq, B,
-                            lat_handles)
+                            lat_handles, slots, fused, nwin, wstride)
+        if "h2d_overlapped" in extra:
+            extra["h2d_overlapped"]["frac_of_resident"] = extra["h2d_overlapped"]["value"] / value
 
     result = {
         "metric": METRIC if (W, H) == (640, 480) else METRIC.replace("640×480", f"{W}×{H}"), "value": value,
@@ -913,6 +918,12 @@ def run(args, world, rank):
                                   "mismatches": bad}
         if bad:
             fail.append(f"oracle mismatch: {bad}")
+    b64c = result.pop("_b64_checks", None)
+    if b64c:
+        bad = oracle_verify(b64c[1])
+        result["batch64"]["oracle_check"] = {"frames": b64c[0], "items": len(b64c[1]), "mismatches": bad}
+        if bad:
+            fail.append(f"batch-64 oracle mismatch: {bad}")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         n = min(args.cpu_frames, B)
         result["cpu_baseline"] = cpu_baseline([seq[i].cpu().numpy() for i in range(n)])
@@ -1084,13 +1095,17 @@ def side_stages(args, torch, plvi, synth, lib, orb, st, stream, B, W, H, cap, kp
     return {k: round(v, 4) if isinstance(v, float) else v for k, v in out.items()}
 
 
-def extra_lines(args, torch, plvi, synth, lib, stream, W, H, seed0, orb, lx, extract, match, seq, B, lat_handles):
-    """Rank 0, N=1: (1) the same step at batch 64 (BASELINE C1/C2 as stated);
-    (2) single-frame latency of the drop-in entry points run the way Frame
-    runs them (plvi_orb_extract || plvi_lines_extract on two host threads,
-    host image in, host tables out; Frame.cc:558-561); (3) the step with the
-    frames streamed from pinned host memory: H2D of batch k+1 on a copy
-    stream overlapped with batch k (two device frame buffers)."""
+def extra_lines(args, torch, plvi, synth, lib, stream, W, H, seed0, orb, lx, extract, match, seq, B, lat_handles,
+                main_slots, fused, nwin, wstride):
+    """Rank 0, N=1: (1) the same step at batch 64 (BASELINE C1/C2 as stated),
+    on distinct frames every step, the last step's frames 0 / 31 / 32 / 63 and
+    pair (31, 32) checked against the oracle; (2) single-frame latency of the
+    drop-in entry points run the way Frame runs them (plvi_orb_extract ||
+    plvi_lines_extract on two host threads, host image in, host tables out;
+    Frame.cc:558-561); (3) the headline schedule (same slots, same fused
+    extract + match) with every batch's frames streamed from pinned host
+    memory: per slot a copy stream and two device frame buffers, the H2D of a
+    slot's next batch overlapped with the step in flight."""
     import threading
     out = {}
     # the batch-64 pair's own stream, created with its extractors at start-up
@@ -1114,22 +1129,39 @@ def extra_lines(args, torch, plvi, synth, lib, stream, W, H, seed0, orb, lx, ext
     # right behind the ORB chain, LineMatcher::match right behind the LBD
     # descriptors (plvi_frame_extract_match_batch; same kernels and outputs as
     # the calls after the schedule, minus the stream joins in between)
-    def step64():
-        plvi.frame_extract_match_batch(o64, l64, seq.data_ptr(), b64, W * H, W, [o.data_ptr() for o in o4], 0.9,
-                                       lsc.data_ptr(), lm.data_ptr(), lnm.data_ptr(), stream=st)
-    for _ in range(3):
-        step64()
+    # every step on its own 64 distinct resident frames (consecutive windows
+    # of the bench's sequence)
+    nwin64 = max(1, (seq.shape[0] - b64) // b64 + 1)
+
+    def step64(i):
+        lo64 = (i % nwin64) * b64
+        plvi.frame_extract_match_batch(o64, l64, seq[lo64].data_ptr(), b64, W * H, W, [o.data_ptr() for o in o4],
+                                       0.9, lsc.data_ptr(), lm.data_ptr(), lnm.data_ptr(), stream=st)
+        return lo64
+    for i in range(3):
+        step64(i)
     torch.cuda.synchronize()
     n64 = 50
     t0 = time.perf_counter()
-    for _ in range(n64):
-        step64()
+    for i in range(n64):
+        lo64 = step64(3 + i)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     out["batch64"] = {"value": b64 * n64 / el, "unit": "frames/s", "ms_per_step": el / n64 * 1e3,
-                      "config": "C1/C2/C3 at batch 64 (BASELINE.json configs[1..2]): same extract+match step"}
+                      "distinct_frames": min(n64, nwin64) * b64,
+                      "config": "C1/C2/C3 at batch 64 (BASELINE.json configs[1..2]): same extract+match step, "
+                                "distinct frames every step"}
     if o64.errors(st) or l64.errors(st):
         raise RuntimeError("batch-64 device error flags")
+    # the last timed step's tables against the oracle (outputs as the timed
+    # step left them: the re-run below writes the same tables)
+    if not args.no_check:
+        def ex64(fptr):
+            plvi.frame_extract_match_batch(o64, l64, fptr, b64, W * H, W, [o.data_ptr() for o in o4], 0.9,
+                                           lsc.data_ptr(), lm.data_ptr(), lnm.data_ptr(), stream=st)
+        out["_b64_checks"] = ([lo64, lo64 + b64 // 2 - 1, lo64 + b64 // 2, lo64 + b64 - 1],
+                              collect_checks(torch, plvi, seq, lo64, b64, W, H, o64, l64, o4, lm, lnm, cap, lcap,
+                                             ex64, lambda: None))
     del o64, l64
     # (1b) batch 64 with K batches in flight: K independent extractor slots
     # (own tables and streams), step i on slot i % K over its own 64 frames;
@@ -1250,41 +1282,75 @@ def extra_lines(args, torch, plvi, synth, lib, stream, W, H, seed0, orb, lx, ext
     except (subprocess.SubprocessError, ValueError, IndexError) as e:
         out["single_frame_latency"]["drop_in_process"] = {"error": str(e)[:200]}
     del so, sl
-    # (3) pinned-H2D overlapped step (the main handles, two device buffers)
-    host = torch.empty((B, H, W), dtype=torch.uint8, pin_memory=True)
-    host.copy_(seq[:B].cpu())
-    dbuf = [torch.empty((B, H, W), dtype=torch.uint8, device=cuda) for _ in range(2)]
-    cs = torch.cuda.Stream()
-    ev_copied = [torch.cuda.Event() for _ in range(2)]
-    ev_free = [torch.cuda.Event() for _ in range(2)]
-    for e in ev_free:
-        e.record(stream)
+    # (3) host-fed headline schedule: the timed step's slots and fused
+    # extract + match, each batch's frames copied from pinned host memory.
+    # Per slot: its own pinned host window, a copy stream and two device
+    # buffers; the copy of a slot's next batch waits only for the step that
+    # last used that buffer, so it overlaps the steps in flight.
+    nsl = len(main_slots)
+    hosts = []
+    for j in range(nsl):
+        lo_j = (j % nwin) * wstride
+        hb = torch.empty((B, H, W), dtype=torch.uint8, pin_memory=True)
+        hb.copy_(seq[lo_j:lo_j + B].cpu())
+        hosts.append(hb)
+    dbuf = [[torch.empty((B, H, W), dtype=torch.uint8, device=cuda) for _ in range(2)] for _ in range(nsl)]
+    cstreams = [torch.cuda.Stream() for _ in range(nsl)]
+    ev_copied = [[torch.cuda.Event() for _ in range(2)] for _ in range(nsl)]
+    ev_free = [[torch.cuda.Event() for _ in range(2)] for _ in range(nsl)]
+    for j in range(nsl):
+        for b in range(2):
+            ev_free[j][b].record(main_slots[j].stream)
 
     def h2d(k):
-        j = k % 2
-        cs.wait_event(ev_free[j])
-        with torch.cuda.stream(cs):
-            dbuf[j].copy_(host, non_blocking=True)
-        ev_copied[j].record(cs)
+        j, b = k % nsl, (k // nsl) % 2
+        cstreams[j].wait_event(ev_free[j][b])
+        with torch.cuda.stream(cstreams[j]):
+            dbuf[j][b].copy_(hosts[j], non_blocking=True)
+        ev_copied[j][b].record(cstreams[j])
 
-    nh = max(args.steps, 5)
-    h2d(0)
+    def hstep(k):
+        j, b = k % nsl, (k // nsl) % 2
+        sl_ = main_slots[j]
+        sl_.stream.wait_event(ev_copied[j][b])
+        fused(sl_, dbuf[j][b].data_ptr())
+        ev_free[j][b].record(sl_.stream)
+
+    # H2D alone (one batch, pinned), for the bandwidth the schedule can draw on
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(cstreams[0])
+    for _ in range(3):
+        with torch.cuda.stream(cstreams[0]):
+            dbuf[0][0].copy_(hosts[0], non_blocking=True)
+    e1.record(cstreams[0])
+    torch.cuda.synchronize()
+    h2d_alone = 3 * B * W * H / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    nh = max(args.steps, 6)
+    nw = 2 * nsl
+    for k in range(nsl):
+        h2d(k)
+    for k in range(nw):  # warm-up steps, copies kept nsl steps ahead
+        h2d(k + nsl)
+        hstep(k)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(nh):
-        h2d(k + 1)
-        j = k % 2
-        stream.wait_event(ev_copied[j])
-        extract(dbuf[j].data_ptr())
-        match()
-        ev_free[j].record(stream)
-    torch.cuda.synchronize()
+    for k in range(nw, nw + nh):
+        h2d(k + nsl)
+        hstep(k)
+    for sl_ in main_slots:
+        sl_.stream.synchronize()
     el = time.perf_counter() - t0
+    torch.cuda.synchronize()  # the copies issued ahead of the last steps
     out["h2d_overlapped"] = {"value": B * nh / el, "unit": "frames/s", "ms_per_step": el / nh * 1e3,
-                             "how": "frames from pinned host memory, H2D of batch k+1 on a copy stream overlapped "
-                                    "with batch k's extract+match"}
-    if orb.errors(stream.cuda_stream) or lx.errors(stream.cuda_stream):
-        raise RuntimeError("h2d device error flags")
+                             "pcie_gbs": B * W * H * nh / el / 1e9, "h2d_alone_gbs": h2d_alone,
+                             "inflight": nsl,
+                             "how": "the headline schedule (same slots, plvi_frame_extract_match_batch) with every "
+                                    "batch copied from pinned host memory: per slot a copy stream and two device "
+                                    "buffers, the copy of a slot's next batch overlapped with the steps in flight"}
+    for sl_ in main_slots:
+        if sl_.orb.errors(sl_.st) or sl_.lx.errors(sl_.st):
+            raise RuntimeError("h2d device error flags")
     return out
 
 
