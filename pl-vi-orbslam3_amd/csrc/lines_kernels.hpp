@@ -817,7 +817,7 @@ constexpr int kRectUSmall = 16;
 constexpr int kRectSmallNf = 64;
 
 template <int U>
-__global__ __launch_bounds__(256) void lsd_rect_lanes_kernel(const LineOctDev* __restrict__ octs,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 4 ? 8 : 1))) void lsd_rect_lanes_kernel(const LineOctDev* __restrict__ octs,
                                                              const double* __restrict__ modgrad,
                                                              const LsdRegion* __restrict__ regs,
                                                              const unsigned* __restrict__ regpts,

@@ -344,6 +344,11 @@ constexpr int kBfFlush = 1 ? 128 : 64;  // candidates scored per flush
 // any ring row are contiguous and a candidate's 17 taps are one base address
 // plus immediate offsets (no per-tap wrap arithmetic)
 constexpr int kRingMirror = 1 ? 6 : 0;
+// source rows loaded per batch, in flight while the previous batch is
+// filtered (4: 75 instead of 79 VGPRs, no faster; r06 also measured the 7-row
+// window read back from the LDS ring -- 64 VGPRs, 7 % slower alone, the step
+// unchanged: DESIGN.md §4)
+constexpr int kBfRB = 8;
 constexpr int kBfCols = 244, kBfRowsPlain = 128, kRingRows = 16, kRingW = 256,
               kBfQCap = kBfFlush - 1 + 256 + 1;  // a row adds <= 256 candidates to < kBfFlush queued
 
@@ -447,26 +452,38 @@ __device__ __forceinline__ s16x2 fast_S_ring2(const uint8_t (*rg)[kRingW], int y
     d[14] = v - RG2(2, -2);
     d[15] = v - RG2(3, -1);
 #undef RG2
-    s16x2 pa[8], pb[8], qa[8], qb[8];  // index i <-> odd start j = 2i + 1
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int j = 2 * i + 1;
-        pa[i] = __builtin_elementwise_min(d[j], d[(j + 1) & 15]);
-        pb[i] = __builtin_elementwise_max(d[j], d[(j + 1) & 15]);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {  // runs d[j..j+3]
-        qa[i] = __builtin_elementwise_min(pa[i], pa[(i + 1) & 7]);
-        qb[i] = __builtin_elementwise_max(pb[i], pb[(i + 1) & 7]);
-    }
+    // the brighter sense first, then the darker one, each with its pair and
+    // quad minima built in place: one sense's 8 partial runs live at a time
+    // (the r03 form kept pa / pb / qa / qb together, 16 more VGPRs at the
+    // kernel's register peak)
     s16x2 A = (s16x2){-1000, -1000}, Bm = (s16x2){1000, 1000};
+    {
+        s16x2 qa[8];  // index i <-> odd start j = 2i + 1: min(d[j], d[j+1]), then min over d[j..j+3]
 #pragma unroll
-    for (int k = 0; k < 16; k += 2) {
-        const int i = k / 2;  // inner run d[k+1..k+8] = quads at k+1 and k+5
-        const s16x2 ia = __builtin_elementwise_min(qa[i], qa[(i + 2) & 7]);
-        const s16x2 ib = __builtin_elementwise_max(qb[i], qb[(i + 2) & 7]);
-        A = __builtin_elementwise_max(A, __builtin_elementwise_min(ia, __builtin_elementwise_max(d[k], d[(k + 9) & 15])));
-        Bm = __builtin_elementwise_min(Bm, __builtin_elementwise_max(ib, __builtin_elementwise_min(d[k], d[(k + 9) & 15])));
+        for (int i = 0; i < 8; ++i) qa[i] = __builtin_elementwise_min(d[2 * i + 1], d[(2 * i + 2) & 15]);
+        const s16x2 p0 = qa[0];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) qa[i] = __builtin_elementwise_min(qa[i], i < 7 ? qa[i + 1] : p0);
+#pragma unroll
+        for (int k = 0; k < 16; k += 2) {
+            const int i = k / 2;  // inner run d[k+1..k+8] = quads at k+1 and k+5
+            const s16x2 ia = __builtin_elementwise_min(qa[i], qa[(i + 2) & 7]);
+            A = __builtin_elementwise_max(A, __builtin_elementwise_min(ia, __builtin_elementwise_max(d[k], d[(k + 9) & 15])));
+        }
+    }
+    {
+        s16x2 qb[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) qb[i] = __builtin_elementwise_max(d[2 * i + 1], d[(2 * i + 2) & 15]);
+        const s16x2 p0 = qb[0];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) qb[i] = __builtin_elementwise_max(qb[i], i < 7 ? qb[i + 1] : p0);
+#pragma unroll
+        for (int k = 0; k < 16; k += 2) {
+            const int i = k / 2;
+            const s16x2 ib = __builtin_elementwise_max(qb[i], qb[(i + 2) & 7]);
+            Bm = __builtin_elementwise_min(Bm, __builtin_elementwise_max(ib, __builtin_elementwise_min(d[k], d[(k + 9) & 15])));
+        }
     }
     return __builtin_elementwise_max(A, -Bm);
 }
@@ -562,16 +579,16 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
         wave_sync();
         oldest = rest > 0 ? ycur - (int)((((unsigned)ycur & 255u) - ((unsigned)q[0] >> 8)) & 255u) : 0;
     };
-    // rows rb..rb+7 of the source (reflected), four columns per lane
+    // rows rb..rb+kBfRB-1 of the source (reflected), four columns per lane
     auto load_rows = [&](int rb, uint32_t* pv) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < kBfRB; ++k) {
             const int r = rb + k;
             pv[k] = (inner && r < y1 + 3) ? ld_u32(src + (size_t)reflect1(r, h) * srow + c0) : 0u;
         }
         if (need && !inner) {  // image-edge lanes: reflected columns byte by byte
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
+            for (int k = 0; k < kBfRB; ++k) {
                 const int r = rb + k;
                 if (r < y1 + 3) {
                     const uint8_t* rp = src + (size_t)reflect1(r, h) * srow;
@@ -581,24 +598,24 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
             }
         }
     };
-    uint32_t pv[8];
+    uint32_t pv[kBfRB];
     load_rows(y0 - 3, pv);
-    for (int rb = y0 - 3; rb < y1 + 3; rb += 8) {
-        // writing rows rb..rb+7 replaces rows rb-kRingRows..rb-kRingRows+7
+    for (int rb = y0 - 3; rb < y1 + 3; rb += kBfRB) {
+        // writing rows rb..rb+kBfRB-1 replaces rows rb-kRingRows..rb-kRingRows+kBfRB-1
         // of the ring; a queued row yy needs rows yy-3..yy+3.  (The score ring
         // zeroes output rows up to rb+4, i.e. rows <= rb+4-kSRows: after this
         // every queued or NMS-pending row is >= rb-6.)
-        if (nq > 0 && oldest - 3 < rb - (kRingRows - 8)) flush(nq, ynew);
+        if (nq > 0 && oldest - 3 < rb - (kRingRows - kBfRB)) flush(nq, ynew);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < kBfRB; ++k) {
             const int rr = (rb + k) & (kRingRows - 1);
             *reinterpret_cast<uint32_t*>(&ring[rr][4 * lane]) = pv[k];
             if (rr < kRingMirror) *reinterpret_cast<uint32_t*>(&ring[rr + kRingRows][4 * lane]) = pv[k];
         }
         // next batch in flight while this one is filtered
-        if (rb + 8 < y1 + 3) load_rows(rb + 8, pv);
+        if (rb + kBfRB < y1 + 3) load_rows(rb + kBfRB, pv);
 #pragma unroll 1
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < kBfRB; ++k) {
             const int r = rb + k;
             if (r >= y1 + 3) break;
             const uint32_t V = *reinterpret_cast<const uint32_t*>(&ring[r & (kRingRows - 1)][4 * lane]);
@@ -618,6 +635,7 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
                 E += __umul24(kt[t], pe[t]);
                 O += __umul24(kt[t], po[t]);
             }
+            const uint32_t pe0 = pe[0], po0 = po[0], pe3 = pe[3], po3 = po[3], pe6 = pe[6], po6 = po[6];
             const uint32_t El = (uint32_t)lane_from_left((int)E), Ol = (uint32_t)lane_from_left((int)O);
             const uint32_t Er = (uint32_t)lane_from_right((int)E), Or = (uint32_t)lane_from_right((int)O);
             // El = (c0-4, c0-2), Ol = (c0-3, c0-1), Er = (c0+4, c0+6), Or = (c0+5, c0+7)
@@ -629,14 +647,14 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
             const unsigned h3 = udot2(E, pk(k0, k2), udot2(O, pk(k1, k3), udot2(Er, pk(k2, k0), udot2(Or, pk(k1, 0), 0u))));
             const uint32_t Bv = min((h0 + 32768u) >> 16, 255u) | min((h1 + 32768u) >> 16, 255u) << 8 |
                                 min((h2 + 32768u) >> 16, 255u) << 16 | min((h3 + 32768u) >> 16, 255u) << 24;
-            const uint32_t cvw = pe[3] | po[3] << 8;
+            const uint32_t cvw = pe3 | po3 << 8;
             const uint32_t L3 = __builtin_amdgcn_alignbyte(cvw, (uint32_t)lane_from_left((int)cvw), 1);   // column c-3
             const uint32_t R3 = __builtin_amdgcn_alignbyte((uint32_t)lane_from_right((int)cvw), cvw, 3);  // column c+3
             // compass pre-test on 16-bit fields (even pixels 0/2, odd pixels 1/3):
             // brighter-by-T / darker-by-T at two cyclically adjacent compass points
             // (0 = row+3, 4 = col+3, 8 = row-3, 12 = col-3)
-            const uint32_t ce[2] = {pe[3], po[3]};
-            const uint32_t p0[2] = {pe[6], po[6]}, p8[2] = {pe[0], po[0]};
+            const uint32_t ce[2] = {pe3, po3};
+            const uint32_t p0[2] = {pe6, po6}, p8[2] = {pe0, po0};
             const uint32_t p4[2] = {R3 & 0x00ff00ffu, (R3 >> 8) & 0x00ff00ffu};
             const uint32_t p12[2] = {L3 & 0x00ff00ffu, (L3 >> 8) & 0x00ff00ffu};
             unsigned candm = 0;  // bit j: pixel j passes the pre-test
@@ -1206,13 +1224,24 @@ constexpr int kDescR = 18, kDescP = 2 * kDescR + 1, kDescPitch = 40;
 constexpr int kAngR = 15, kAngRows = 2 * kAngR + 1, kAngPitch = 32;
 
 #ifndef PLVI_DESC_WPE
-#define PLVI_DESC_WPE 5
+#define PLVI_DESC_WPE 8
 #endif
 #ifndef PLVI_DESC_UNROLL
-#define PLVI_DESC_UNROLL 4  // rBRIEF loop unroll (1 or 2: 78 instead of 92 VGPRs)
+#define PLVI_DESC_UNROLL 1  // rBRIEF loop unroll (4: more VGPRs for no gain once the staging is lean)
 #endif
 #define PLVI_PRAGMA(x) _Pragma(#x)
 #define PLVI_UNROLL(n) PLVI_PRAGMA(unroll n)
+__device__ __forceinline__ float uniform_f(float v) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+// Register budget (r06): <= 64 VGPRs, so two describe waves fit a SIMD beside
+// six 64-VGPR region-growing waves of the other batch (one at 92 VGPRs, which
+// stretched every in-schedule launch to ~50 ms for 4 ms of work).  The
+// keypoint record is read once per wave into SGPRs, both boxes are addressed
+// from scalar bases with one 32-bit lane offset per load (no 64-bit VGPR
+// address pairs), and the LDS layouts are linear in the lane index (the IC box
+// is 8 dwords a row, the blur box 10), so every staging store is one base
+// register plus an immediate offset.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PLVI_DESC_WPE))) void orb_describe_kernel(const OrbLevelDev* __restrict__ lvs, int L,
                                                            const uint8_t* __restrict__ pyr,
                                                            const uint8_t* __restrict__ blur,
@@ -1250,14 +1279,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PLVI_DESC_W
         }
         return kpCapFrame;
     };
+    auto load_kp = [&](int s) {  // the wave's keypoint record, in SGPRs
+        const float4 v = lvkp[(size_t)f * kpCapFrame + s];
+        return make_float4(uniform_f(v.x), uniform_f(v.y), uniform_f(v.z), uniform_f(v.w));
+    };
     int lnext = 0;
     int snext = next_slot(blockIdx.x * 4 + wv, lnext);
-    float4 kpn = snext < kpCapFrame ? lvkp[(size_t)f * kpCapFrame + snext] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 kpn = snext < kpCapFrame ? load_kp(snext) : make_float4(0.f, 0.f, 0.f, 0.f);
     while (snext < kpCapFrame) {
         const int slot = snext, l = lnext;
         float4 kp = kpn;
         snext = next_slot(slot + stride, lnext);
-        if (snext < kpCapFrame) kpn = lvkp[(size_t)f * kpCapFrame + snext];
+        if (snext < kpCapFrame) kpn = load_kp(snext);
         const OrbLevelDev& lv = lvs[l];
         const int cx = (int)kp.x, cy = (int)kp.y;  // integer-valued level coords (>= 19 from every border)
         const int W = lv.w, BW = lv.bpitch;
@@ -1265,36 +1298,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PLVI_DESC_W
         const uint8_t* I0 = pyr + lv.off + (size_t)f * lv.plane + (size_t)(cy - kAngR) * W + (cx - kAngR);
         const uint8_t* B0 = blur + lv.boff + (size_t)f * lv.bplane + (size_t)(cy - kDescR) * BW + (cx - kDescR);
         uint32_t iv[4], bv[6];
-        uint8_t blast = 0;
         {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {  // 31 rows x 8 dwords (columns cx-15 .. cx+16)
                 const int i = lane + 64 * k;
-                iv[k] = i < kAngRows * 8 ? ld_u32(I0 + (size_t)(i >> 3) * W + 4 * (i & 7)) : 0u;
+                iv[k] = i < kAngRows * 8 ? ld_u32(I0 + (unsigned)((i >> 3) * W + 4 * (i & 7))) : 0u;
             }
         }
         {
 #pragma unroll
-            for (int k = 0; k < 6; ++k) {  // 37 rows x 9 dwords (columns cx-18 .. cx+17)
-                const int i = lane + 64 * k, r = i / 9;
-                bv[k] = i < kDescP * 9 ? ld_u32(B0 + (size_t)r * BW + 4 * (i - 9 * r)) : 0u;
-            }
-            if (lane < kDescP) blast = B0[(size_t)lane * BW + 36];  // column cx+18
-        }
-        {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int i = lane + 64 * k;
-                if (i < kAngRows * 8) *reinterpret_cast<uint32_t*>(IP + (i >> 3) * kAngPitch + 4 * (i & 7)) = iv[k];
+            for (int k = 0; k < 6; ++k) {  // 37 rows x 10 dwords (columns cx-18 .. cx+21; cx+19.. unused)
+                const int i = lane + 64 * k, r = i / 10;
+                bv[k] = i < kDescP * 10 ? ld_u32(B0 + (unsigned)(r * BW + 4 * (i - 10 * r))) : 0u;
             }
         }
         {
+            uint32_t* ip = reinterpret_cast<uint32_t*>(IP) + lane;  // dword i of the IC box = 4 i bytes
 #pragma unroll
-            for (int k = 0; k < 6; ++k) {
-                const int i = lane + 64 * k, r = i / 9;
-                if (i < kDescP * 9) *reinterpret_cast<uint32_t*>(P + r * kDescPitch + 4 * (i - 9 * r)) = bv[k];
-            }
-            if (lane < kDescP) P[lane * kDescPitch + 36] = blast;
+            for (int k = 0; k < 4; ++k)
+                if (lane + 64 * k < kAngRows * 8) ip[64 * k] = iv[k];
+            uint32_t* bp = reinterpret_cast<uint32_t*>(P) + lane;   // dword i of the blur box (pitch 10 dwords)
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+                if (lane + 64 * k < kDescP * 10) bp[64 * k] = bv[k];
         }
         wave_sync();
         // ---- IC_Angle (ORBextractor.cc:75-102)
