@@ -476,6 +476,7 @@ struct LinePipeline {
     int mwMaxFrames = 0, mwSlots = 0;
     size_t mwSmem = 0, mwOwnTask = 0;
     int* mwStats = nullptr;  // diagnostic counters (plvi_lines_debug_mw_stats)
+    DevBuf mwEpoch;          // PLVI_MW_DIAG variant: commit-epoch map per task
     size_t growSmem = 0;
     int growWPW = 1;  // region-growing tasks (waves) per workgroup
     int growR = 0, growRB = 0, growQL = 0;
@@ -554,7 +555,8 @@ struct LinePipeline {
                                (const float*)pix.as<float>(), (const float2*)seedcs.as<float2>(),
                                mwOwn.as<unsigned>(), mwOwnTask, mwGrow.as<unsigned>(), mwSlot.as<unsigned>(),
                                qspill.as<unsigned>(), qspillFrame, prec, regs.as<LsdRegion>(), regpts.as<unsigned>(),
-                               qspillFrame, nlines.as<int>(), err.as<int>(), mwSlots, nOct, oBase, oCount, mwStats, nf);
+                               qspillFrame, nlines.as<int>(), err.as<int>(), mwSlots, nOct, oBase, oCount, mwStats, nf,
+                               mwStats && PLVI_MW_DIAG ? mwEpoch.as<int>() : nullptr);
             return;
         }
         const bool fixedWin = growR == 0 && growRB == kGrowRB && growQL == kGrowQL;
@@ -1024,6 +1026,11 @@ extern "C" int plvi_lines_debug_stats(plvi_line_extractor* h, unsigned long long
 extern "C" int plvi_lines_debug_mw_stats(plvi_line_extractor* h, int* d_stats) {
     if (!h) return PLVI_E_BADARG;
     h->p().mwStats = d_stats;
+    // the diagnostic variant's commit-epoch map: one int per bit of every
+    // (frame, octave) task's bitmaps
+    if (PLVI_MW_DIAG && d_stats && !h->p().mwEpoch.p &&
+        h->p().mwEpoch.alloc(sizeof(int) * 32 * h->p().gbitsFrame * (size_t)h->p().mwMaxFrames * h->p().nOct))
+        return PLVI_E_HIP;
     return PLVI_OK;
 }
 

@@ -57,6 +57,12 @@ constexpr int kMwLog = 256;         // dispatch log entries (seed order)
 #define PLVI_MW_GROWER_PRIO 1
 #endif
 constexpr int kMwLook = PLVI_MW_LOOK;  // dispatch-log entries ahead of the walk that growers revalidate (0 = off)
+// diagnostic variant (tools/build_variant.sh ... -DPLVI_MW_DIAG=1): 32
+// counters per task instead of 16 and a commit-epoch map (see the stat list)
+#ifndef PLVI_MW_DIAG
+#define PLVI_MW_DIAG 0
+#endif
+constexpr int kMwStatN = PLVI_MW_DIAG ? 32 : 16;
 
 // slot states; COMMITTED: validated and committed, a grower still copies
 // its points out (regions of more than kMwSP points); WALKING: the walker
@@ -79,11 +85,17 @@ struct MwCtl {
     int lock, dlock, head, cursor, finished, npts, nout, overflow;
     int dlog_n, wptr, ncommit, pad1;  // dispatch log: entries appended / next entry the walk examines;
                                       // regions committed so far (revalidation epoch)
-    int stat[16];  // [0] dispatched [1] dropped [2] regrown [3] exact (undispatched) [4] trivial [5] committed
+    int stat[kMwStatN];  // [0] dispatched [1] dropped [2] regrown [3] exact (undispatched) [4] trivial [5] committed
                    // speculative [6] walk cycles [7] walker growth cycles [8] walk entries [9] blocked on a
                    // growing head [10] kernel cycles (wave 0) [11] speculative growth cycles (sum over waves)
                    // [12] unused [13] blocks (completed regions) [14] block setup cycles / 16
                    // [15] block round cycles / 16
+                   // PLVI_MW_DIAG: [16]/[17] walker waits on a revalidation regrowth (count / cycles)
+                   // [18]/[19] waits on a first growth [20..25] walker regrowths by distance (in commits)
+                   // from the commit that invalidated them: 1, 2, 3-4, 5-8, 9-16, >16 [26] sum of their
+                   // check lag (commits since last check) [27] of them last grown by a revalidation
+                   // [28] grower revalidation checks [29] grower regrowths [30] sum of waited-on region
+                   // sizes [31] sum of (dispatch log entries ahead of the walk) at its waits
 };
 
 typedef MwSlot __attribute__((address_space(3))) lds_slot;
@@ -105,6 +117,7 @@ struct MwEnv {
     lds_u32* own;      // this wave's own-mark window (RB rows x wpr)
     unsigned* ownG;    // this wave's own-mark spill (sh x wpr)
     lds_ctl* ctl;
+    int* epoch;  // PLVI_MW_DIAG: commit index of every committed pixel (bit index), else null
     int sw, sh, wpr, rowbits;  // rowbits = wpr * 32
     float pdeg;
     double prec;
@@ -465,6 +478,9 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
         }
         if (sst == kMwGrowing) {  // wait for it
             if (STATS && lane == 0) mw_stat(ctl, 9, 1);
+#if PLVI_MW_DIAG
+            if (STATS && lane == 0) mw_stat(ctl, 31, dn - wp);
+#endif
             blocked = si;
             break;
         }
@@ -490,6 +506,24 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
                     bad |= mw_bit(E.C, E.wpr, (int)(v & 0xffffu), (int)(v >> 16));
                 }
                 valid = ballot(bad) == 0ull;
+#if PLVI_MW_DIAG
+                if (STATS && !valid) {
+                    // the earliest commit that took one of its pixels
+                    int emin = 0x7fffffff;
+                    for (int j = lane; j < n; j += 64) {
+                        const unsigned v = mw_qget(Q, j);
+                        const int x = (int)(v & 0xffffu), y = (int)(v >> 16);
+                        if (mw_bit(E.C, E.wpr, x, y)) emin = min(emin, (int)gload_l2((unsigned*)E.epoch + y * rowbits + x));
+                    }
+                    for (int o = 32; o > 0; o >>= 1) emin = min(emin, __shfl_xor(emin, o));
+                    if (lane == 0) {
+                        const int nc = ctl->ncommit, d = nc - emin;
+                        mw_stat(ctl, d <= 1 ? 20 : d == 2 ? 21 : d <= 4 ? 22 : d <= 8 ? 23 : d <= 16 ? 24 : 25, 1);
+                        mw_stat(ctl, 26, nc - S->chk);
+                        if (S->out == -2) mw_stat(ctl, 27, 1);
+                    }
+                }
+#endif
             }
             if (valid) {
                 if (lane < n) mw_or(E.C, E.wpr, (int)(v0 & 0xffffu), (int)(v0 >> 16));
@@ -497,6 +531,13 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
                     const unsigned v = mw_qget(Q, j);
                     mw_or(E.C, E.wpr, (int)(v & 0xffffu), (int)(v >> 16));
                 }
+#if PLVI_MW_DIAG
+                if (STATS)
+                    for (int j = lane; j < n; j += 64) {
+                        const unsigned v = mw_qget(Q, j);
+                        E.epoch[(int)(v >> 16) * rowbits + (int)(v & 0xffffu)] = ctl->ncommit;
+                    }
+#endif
                 int st_next = kMwFree;
                 if (n >= min_reg) {
                     const int nout = ctl->nout, npts = ctl->npts;
@@ -545,6 +586,9 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
             for (int j = lane; j < n; j += 64) {
                 const unsigned v = mw_qget(XQ, j);
                 mw_or(E.C, E.wpr, (int)(v & 0xffffu), (int)(v >> 16));
+#if PLVI_MW_DIAG
+                if (STATS) E.epoch[(int)(v >> 16) * rowbits + (int)(v & 0xffffu)] = ctl->ncommit;
+#endif
             }
             mw_wave_sync();
             if (lane == 0) mw_lds_store(&ctl->ncommit, ctl->ncommit + 1);
@@ -632,6 +676,9 @@ __device__ __forceinline__ int mw_dispatch(const MwEnv& E, lds_u8* pool, int nsl
         S->seed = q;
         S->ovf = 0;
         S->chk = mw_peek(&ctl->ncommit);
+#if PLVI_MW_DIAG
+        S->out = -1;
+#endif
         mw_lds_store(&S->state, kMwGrowing);  // before the log entry that names it
         ctl->cursor = q + 1;
         dlog[2 * (dn & (kMwLog - 1))] = q;
@@ -659,7 +706,7 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
     unsigned* __restrict__ ownspill, size_t ownspill_task, unsigned* __restrict__ gspill, unsigned* __restrict__ slotspill,
     unsigned* __restrict__ xspill, size_t xspill_task, double prec, LsdRegion* __restrict__ regs,
     unsigned* __restrict__ regpts, size_t regpts_frame, int* __restrict__ nlines, int* __restrict__ err, int nslots,
-    int nOct, int oBase, int oCount, int* __restrict__ stats, int nf) {
+    int nOct, int oBase, int oCount, int* __restrict__ stats, int nf, int* __restrict__ epochs) {
     extern __shared__ __align__(16) unsigned lds_u[];
     __builtin_amdgcn_s_setprio(PLVI_GROW_SETPRIO);
     const int t = blockIdx.x;
@@ -689,6 +736,7 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
     E.own = ownAll + wv * kMwRB * wpr;
     E.ownG = ownspill + (size_t)task * ownspill_task + (size_t)wv * sh * wpr;
     E.ctl = ctl;
+    E.epoch = epochs ? epochs + (size_t)task * sh * (wpr * 32) : nullptr;
     E.sw = sw; E.sh = sh; E.wpr = wpr; E.rowbits = wpr * 32;
     E.pdeg = (float)(prec / kD2R);
     E.prec = prec;
@@ -746,7 +794,7 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
         ctl->lock = ctl->dlock = ctl->head = ctl->cursor = ctl->finished = 0;
         ctl->npts = ctl->nout = ctl->overflow = 0;
         ctl->dlog_n = ctl->wptr = ctl->ncommit = 0;
-        for (int i = 0; i < 16; ++i) ctl->stat[i] = 0;
+        for (int i = 0; i < kMwStatN; ++i) ctl->stat[i] = 0;
     }
     __syncthreads();
 
@@ -762,7 +810,18 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
                 mw_stat(ctl, 8, 1);
             }
             if (b < 0) break;  // every seed resolved
+#if PLVI_MW_DIAG
+            const unsigned long long twa = STATS ? __builtin_amdgcn_s_memtime() : 0;
+            const bool rg = STATS && mw_slot(pool, b)->out == -2;
+#endif
             while (mw_lds_load(&mw_slot(pool, b)->state) == kMwGrowing) __builtin_amdgcn_s_sleep(1);
+#if PLVI_MW_DIAG
+            if (STATS && lane == 0) {
+                mw_stat(ctl, rg ? 16 : 18, 1);
+                mw_stat(ctl, rg ? 17 : 19, (int)(__builtin_amdgcn_s_memtime() - twa));
+                mw_stat(ctl, 30, mw_slot(pool, b)->n);
+            }
+#endif
         }
     } else {
         // ---- growers
@@ -826,6 +885,9 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
                     const int sx = seed % E.rowbits, sy = seed / E.rowbits;
                     const MwQueue Q = mw_slot_queue(pool, sspill, rs);
                     bool bad = false;
+#if PLVI_MW_DIAG
+                    if (STATS && lane == 0) mw_stat(ctl, 28, 1);
+#endif
                     for (int k = lane; k < n0; k += 64) {
                         const unsigned v = mw_qget(Q, k);
                         bad |= mw_bit(E.C, E.wpr, (int)(v & 0xffffu), (int)(v >> 16));
@@ -840,6 +902,12 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
                         float deg = 0.f;
                         bool spilled = false;
                         const unsigned long long ts0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
+#if PLVI_MW_DIAG
+                        if (STATS && lane == 0) {
+                            mw_stat(ctl, 29, 1);
+                            S->out = -2;
+                        }
+#endif
                         int rc = mw_grow<true, STATS>(E, sx, sy, GQ, n, deg, spilled, lane);
                         mw_own_clear(E, sy, GQ, n, spilled, lane);
                         if (rc == 0) {
@@ -909,7 +977,7 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
         if (ctl->overflow) atomicOr(err + f, 4);
         if (STATS) {
             ctl->stat[10] = (int)(__builtin_amdgcn_s_memtime() - t_kernel);
-            for (int i = 0; i < 16; ++i) stats[(size_t)task * 16 + i] = ctl->stat[i];
+            for (int i = 0; i < kMwStatN; ++i) stats[(size_t)task * kMwStatN + i] = ctl->stat[i];
         }
     }
 }

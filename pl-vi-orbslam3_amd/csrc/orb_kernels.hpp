@@ -725,6 +725,10 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
 // One wave per (cell, frame), lane = window column (windows are < 64 wide),
 // each row's 8 neighbours from the rows above / below and DPP lane shifts.
 // ---------------------------------------------------------------------------
+#ifndef PLVI_NMS_ROWS
+#define PLVI_NMS_ROWS 8
+#endif
+constexpr int kNmsRows = PLVI_NMS_ROWS;  // rows loaded per round trip (8: eight in flight, the next eight prefetched)
 __device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, const OrbLevelDev* __restrict__ lvs,
                                              const uint8_t* __restrict__ score, uint8_t* __restrict__ cand, int t1,
                                              int t2) {
@@ -739,8 +743,38 @@ __device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, co
     // the kernel occupies no LDS next to the region-growing waves it runs
     // with; survivors are re-read from the (L2-resident) plane when written.
     unsigned long long ka = 0, kb = 0;
-    {
-        auto ld = [&](int r) -> int { return (incol && r < wh) ? (int)S[(size_t)r * w] : 0; };
+    auto ld = [&](int r) -> int { return (incol && r < wh) ? (int)S[(size_t)r * w] : 0; };
+    if (kNmsRows > 8) {
+        // kNmsRows rows per round trip (no prefetch of the next chunk): a
+        // detection window of up to kNmsRows + 1 rows is one load latency
+        int s = ld(0);
+        int hp = 0;
+        int lr = max(lane_from_left(s), lane_from_right(s));
+        int hc = max(s, lr);
+        for (int r0 = 0; r0 < wh; r0 += kNmsRows) {
+            int cur[kNmsRows];
+#pragma unroll
+            for (int k = 0; k < kNmsRows; ++k) cur[k] = ld(r0 + 1 + k);
+#pragma unroll
+            for (int k = 0; k < kNmsRows; ++k) {
+                const int r = r0 + k;
+                if (r < wh) {
+                    const int sn = cur[k];
+                    const int lrn = max(lane_from_left(sn), lane_from_right(sn));
+                    const int hn = max(sn, lrn);
+                    const int m = max(max(hp, hn), lr);
+                    if (s > m) {
+                        if (s >= t1) ka |= 1ull << r;
+                        if (s >= t2) kb |= 1ull << r;
+                    }
+                    hp = hc;
+                    hc = hn;
+                    lr = lrn;
+                    s = sn;
+                }
+            }
+        }
+    } else {
         int nx[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) nx[k] = ld(1 + k);
@@ -808,7 +842,10 @@ __global__ __launch_bounds__(64) void orb_cell_nms_kernel(const OrbCellDev* __re
 // candidates of the strips left of s.  One pass: read the candidate bytes
 // once, write 2 B per pixel (the two-pass int32 table moved 13 B per pixel).
 // ---------------------------------------------------------------------------
-constexpr int kSatRowsPerWave = 8;
+#ifndef PLVI_SAT_ROWS
+#define PLVI_SAT_ROWS 8
+#endif
+constexpr int kSatRowsPerWave = PLVI_SAT_ROWS;  // rows whose loads are in flight together
 
 // Rows top-down, 8 rows' loads in flight; per row ballots give the prefix
 // counts (v_mbcnt) and the row total (popcount) without any cross-lane scan;

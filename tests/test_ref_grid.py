@@ -21,6 +21,7 @@ C entry points only).  Compared here:
 Skips where /root/reference is absent (the GPU box).
 """
 import ctypes
+import os
 import pathlib
 import subprocess
 
@@ -34,7 +35,8 @@ ROOT = pathlib.Path(__file__).resolve().parent.parent
 REF_SRC = pathlib.Path("/root/reference/src")
 LIB = ROOT / "oracle" / "_ref" / "libref_grid.so"
 
-pytestmark = pytest.mark.skipif(not (REF_SRC / "gridStructure.cpp").exists(), reason="/root/reference absent")
+pytestmark = pytest.mark.skipif(not (REF_SRC / "gridStructure.cpp").exists() or os.environ.get("PLVI_SKIP_REF") == "1",
+                                reason="/root/reference absent (or PLVI_SKIP_REF=1)")
 
 
 @pytest.fixture(scope="module")

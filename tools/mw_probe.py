@@ -21,6 +21,11 @@ allf = synth.device_sequence(max(batches), W, H, 0, "cuda")
 lib = plvi.load()
 names = ["disp", "drop", "regrow", "exact", "trivial", "spec_ok", "walk_cyc", "wgrow_cyc", "walks", "blocked",
          "kern_cyc", "spec_cyc", "unused", "blocks", "setup16", "round16"]
+# MW_DIAG=1 with a -DPLVI_MW_DIAG=1 variant (PLVI_LIB): 32 counters per task
+NS = 32 if os.environ.get("MW_DIAG") == "1" else 16
+if NS == 32:
+    names += ["w_rg", "w_rg_cyc", "w_first", "w_first_cyc", "inv_d1", "inv_d2", "inv_d3_4", "inv_d5_8", "inv_d9_16",
+              "inv_d17p", "chk_lag", "inv_after_reval", "reval_chk", "reval_grow", "wait_n", "wait_ahead"]
 for B in batches:
     for mw in (0, 256):
         os.environ["PLVI_GROW_MW"] = str(mw)
@@ -34,12 +39,12 @@ for B in batches:
         lx.profile(False)
         line = f"B={B} mw={mw} " + " ".join(f"{k}={v / runs:.2f}" for k, v in st.items())
         if mw:
-            s = torch.zeros(B * 2 * 16, dtype=torch.int32, device="cuda")
+            s = torch.zeros(B * 2 * NS, dtype=torch.int32, device="cuda")
             lib.plvi_lines_debug_mw_stats(lx._h, ctypes.c_void_p(s.data_ptr()))
             lx.extract_batch(allf.data_ptr(), B, W * H, W)
             torch.cuda.synchronize()
             lib.plvi_lines_debug_mw_stats(lx._h, ctypes.c_void_p(0))
-            a = s.cpu().numpy().reshape(B, 2, 16).mean(axis=0)
+            a = s.cpu().numpy().reshape(B, 2, NS).mean(axis=0)
             for o in range(2):
                 line += f" | oct{o} " + " ".join(f"{n}={a[o, i]:.0f}" for i, n in enumerate(names))
                 line += f" setup/blk={16 * a[o, 14] / max(a[o, 13], 1):.0f} round/blk={16 * a[o, 15] / max(a[o, 13], 1):.0f}"
