@@ -80,12 +80,15 @@ def pyramid_bytes(w, h):
     return sum(planes[:-1]) + sum(planes[1:])
 
 
-def blur_fast_kernel_bytes(w, h):
+def blur_fast_kernel_bytes(w, h, copy0=False):
     """What orb_blur_fast_kernel itself materialises per frame (reported next
     to the SURVEY model, not used for frac): every level read once, its blur
-    and FAST score planes written once, and level 0's pyramid copy (u8)."""
+    and FAST score planes written once, and -- only when the frames' rows are
+    not packed (copy0) -- level 0's pyramid copy (u8).  Since r06 level 0 of
+    packed frames is a view of the frame (the bench's case): the kernel's
+    bytes are then the SURVEY model's."""
     planes = [a * b for a, b in level_dims(w, h)]
-    return sum(planes) + 2 * sum(planes) + planes[0]
+    return sum(planes) + 2 * sum(planes) + (planes[0] if copy0 else 0)
 
 
 def lsd_prep_bytes(w, h, scale=0.8, noct=2):

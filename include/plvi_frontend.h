@@ -145,15 +145,21 @@ int plvi_orb_outputs(plvi_orb_extractor* h, plvi_keypoint** d_kps, uint8_t** d_d
                      int* cap);
 
 /* mvImagePyramid[level] of frame `frame` of the last call (lazy D2H copy).
- * dst must hold w*h bytes; pass dst=NULL to query the size. */
+ * dst must hold w*h bytes; pass dst=NULL to query the size.  Level 0 is read
+ * from the last call's input frames when they were packed (see
+ * plvi_orb_pyramid_device), so call this before they are overwritten. */
 int plvi_orb_pyramid_level(plvi_orb_extractor* h, int frame, int level, uint8_t* dst, int* w, int* hgt);
 
 /* Device view of mvImagePyramid (include/ORBextractor.h:84, read by
  * Frame::ComputeStereoMatches, src/Frame.cc:1235,1325,1344): level `level`
  * of frame f is the w x hgt u8 image (row stride w) at
  * *d_frame0 + f * *frame_stride, valid after the last extraction on the
- * handle's stream.  level = -1 only reports *nlevels.  Any out pointer may
- * be NULL. */
+ * handle's stream.  Level 0 is the input image itself (ORBextractor.cc:1165
+ * copies it unchanged): when the last batch's rows were packed (row_stride ==
+ * width) it is returned as a view of the caller's frames (the batch pointer and
+ * its frame_stride; plvi_orb_extract's own staging copy for single frames),
+ * valid while that buffer is unchanged; otherwise the handle holds a copy.
+ * level = -1 only reports *nlevels.  Any out pointer may be NULL. */
 int plvi_orb_pyramid_device(plvi_orb_extractor* h, int level, const uint8_t** d_frame0, size_t* frame_stride, int* w,
                             int* hgt, int* nlevels);
 

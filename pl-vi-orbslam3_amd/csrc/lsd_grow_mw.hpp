@@ -56,6 +56,9 @@ constexpr int kMwLog = 256;         // dispatch log entries (seed order)
 #ifndef PLVI_MW_GROWER_PRIO
 #define PLVI_MW_GROWER_PRIO 1
 #endif
+#ifndef PLVI_MW_CHECKER_PRIO
+#define PLVI_MW_CHECKER_PRIO 2
+#endif
 constexpr int kMwLook = PLVI_MW_LOOK;  // dispatch-log entries ahead of the walk that growers revalidate (0 = off)
 // diagnostic variant (tools/build_variant.sh ... -DPLVI_MW_DIAG=1): 32
 // counters per task instead of 16 and a commit-epoch map (see the stat list)
@@ -68,7 +71,19 @@ constexpr int kMwStatN = PLVI_MW_DIAG ? 32 : 16;
 // its points out (regions of more than kMwSP points); WALKING: the walker
 // validates it (claimed from DONE by compare-and-swap, like a grower's
 // revalidation, which holds it as GROWING)
-enum : int { kMwFree = 0, kMwGrowing = 1, kMwDone = 2, kMwCommitted = 3, kMwCopying = 4, kMwWalking = 5 };
+// DIRTY: grown, and found invalid by the checker wave (a pixel of it has since
+// been committed); the walker regrows it without validating, a grower regrows
+// it ahead of the walk
+enum : int { kMwFree = 0, kMwGrowing = 1, kMwDone = 2, kMwCommitted = 3, kMwCopying = 4, kMwWalking = 5, kMwDirty = 6 };
+// commit-driven revalidation: wave 1 is a checker that, after every commit,
+// tests every grown region of the dispatch log ahead of the walk against the
+// committed bitmap and marks the invalid ones DIRTY; growers regrow DIRTY
+// regions (the earliest first) before growing new ones.  0: the r05 scheme
+// (idle growers recheck the first kMwLook log entries after the walk).
+#ifndef PLVI_MW_CHECKER
+#define PLVI_MW_CHECKER 1
+#endif
+constexpr bool kMwChecker = PLVI_MW_CHECKER != 0;
 
 struct MwSlot {
     int seed;   // bit index y * (wpr * 32) + x
@@ -94,7 +109,8 @@ struct MwCtl {
                    // [18]/[19] waits on a first growth [20..25] walker regrowths by distance (in commits)
                    // from the commit that invalidated them: 1, 2, 3-4, 5-8, 9-16, >16 [26] sum of their
                    // check lag (commits since last check) [27] of them last grown by a revalidation
-                   // [28] grower revalidation checks [29] grower regrowths [30] sum of waited-on region
+                   // [28] revalidation checks (r05 scheme) / regions the checker marked DIRTY [29] grower
+                   // regrowths [30] sum of waited-on region
                    // sizes [31] sum of (dispatch log entries ahead of the walk) at its waits
 };
 
@@ -469,12 +485,21 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
         }
         lds_slot* S = si >= 0 ? mw_slot(pool, si) : nullptr;
         int sst = si >= 0 ? mw_lds_load(&S->state) : kMwFree;
-        if (sst == kMwDone) {
-            // claim it against a grower's revalidation
+        bool dirty = false;  // found invalid by the checker: regrow without validating
+        if (sst == kMwDone || sst == kMwDirty) {
+            // claim it against a grower's revalidation / regrowth (and, for a
+            // DONE region, the checker marking it DIRTY meanwhile: one retry)
             int got = 0;
-                    if (lane == 0) got = mw_lds_cas(&S->state, kMwDone, kMwWalking) ? 1 : 0;
+            if (lane == 0) {
+                got = mw_lds_cas(&S->state, sst, kMwWalking) ? sst : 0;
+                if (!got && sst == kMwDone) got = mw_lds_cas(&S->state, kMwDirty, kMwWalking) ? kMwDirty : 0;
+            }
             got = __builtin_amdgcn_readfirstlane(got);
-                    if (!got) sst = kMwGrowing;
+            if (!got) sst = kMwGrowing;
+            else {
+                dirty = got == kMwDirty;
+                sst = kMwDone;
+            }
         }
         if (sst == kMwGrowing) {  // wait for it
             if (STATS && lane == 0) mw_stat(ctl, 9, 1);
@@ -493,7 +518,7 @@ __device__ int mw_walk(const MwEnv& E, lds_u8* pool, lds_i32* dlog, unsigned* sl
             n = S->n;
             const float deg = S->deg;
             const MwQueue Q = mw_slot_queue(pool, slotspill, si);
-            bool valid = S->ovf == 0;
+            bool valid = S->ovf == 0 && !dirty;
             unsigned v0 = 0u;
             if (valid) {
                 bool bad = false;
@@ -635,23 +660,39 @@ __device__ __forceinline__ int mw_dispatch(const MwEnv& E, lds_u8* pool, int nsl
     const int dn = mw_peek(&ctl->dlog_n);  // written under dlock only (held)
     if (dn - mw_lds_load(&ctl->wptr) >= kMwLog - 1) return -1;  // log full: the walk is far behind
     const int head = mw_lds_load(&ctl->head);
-    // a free slot (lanes scan the pool)
+    // a free slot (lanes scan the pool), claimed by compare-and-swap: growers
+    // claim DIRTY slots without the dispatch lock, and a dead DIRTY slot (seed
+    // passed by the walk) is also free here
     slot = -1;
+    int st0 = kMwFree;
     for (int b0 = 0; b0 < nslots && slot < 0; b0 += 64) {
         const int si = b0 + lane;
         bool ok = false;
+        int st = kMwFree;
         if (si < nslots) {
             lds_slot* S = mw_slot(pool, si);
-            const int st = mw_lds_load(&S->state);
-            ok = st == kMwFree || (st == kMwDone && S->seed < head);
+            st = mw_lds_load(&S->state);
+            ok = st == kMwFree || ((st == kMwDone || st == kMwDirty) && S->seed < head);
         }
-        const unsigned long long b = ballot(ok);
-        if (b) slot = b0 + __ffsll((long long)b) - 1;
+        for (unsigned long long b = ballot(ok); b && slot < 0; b &= b - 1) {
+            const int l = __ffsll((long long)b) - 1;
+            const int c = b0 + l, stc = readlane_i(st, l);
+            int got = 0;
+            if (lane == 0) got = mw_lds_cas(&mw_slot(pool, c)->state, stc, kMwGrowing) ? 1 : 0;
+            if (__builtin_amdgcn_readfirstlane(got)) {
+                slot = c;
+                st0 = stc;
+            }
+        }
     }
     if (slot < 0) return -1;
+    // (no seed: the claimed slot goes back as FREE -- it was free or held a dead region)
     int cur = max(ctl->cursor, head);
     int w = cur >> 5;
-    if (w >= nwords) return -1;
+    if (w >= nwords) {
+        if (lane == 0) mw_lds_store(&mw_slot(pool, slot)->state, kMwFree);
+        return -1;
+    }
     unsigned m = ~(mw_peek(E.C + w) | E.T[w] | mw_peek(E.H + w)) & (~0u << (cur & 31));
     if (!m) {
         int found = -1;
@@ -662,7 +703,10 @@ __device__ __forceinline__ int mw_dispatch(const MwEnv& E, lds_u8* pool, int nsl
             if (b) found = w0 + __ffsll((long long)b) - 1;
         }
         if (found < 0) {
-            if (lane == 0) ctl->cursor = nwords * 32;
+            if (lane == 0) {
+                ctl->cursor = nwords * 32;
+                mw_lds_store(&mw_slot(pool, slot)->state, kMwFree);
+            }
             return -1;
         }
         w = found;
@@ -671,15 +715,15 @@ __device__ __forceinline__ int mw_dispatch(const MwEnv& E, lds_u8* pool, int nsl
     const int q = w * 32 + (__ffs((int)m) - 1);
     if (lane == 0) {
         lds_slot* S = mw_slot(pool, slot);
-        const int st0 = mw_peek(&S->state);
-        if (STATS && st0 == kMwDone) mw_stat(ctl, 1, 1);  // a passed region, dropped
+        if (STATS && (st0 == kMwDone || st0 == kMwDirty)) mw_stat(ctl, 1, 1);  // a passed region, dropped
         S->seed = q;
         S->ovf = 0;
         S->chk = mw_peek(&ctl->ncommit);
 #if PLVI_MW_DIAG
         S->out = -1;
 #endif
-        mw_lds_store(&S->state, kMwGrowing);  // before the log entry that names it
+        // (GROWING since the claim) the slot record before the log entry that names it
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         ctl->cursor = q + 1;
         dlog[2 * (dn & (kMwLog - 1))] = q;
         dlog[2 * (dn & (kMwLog - 1)) + 1] = slot;
@@ -823,6 +867,75 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
             }
 #endif
         }
+    } else if (kMwChecker && wv == 1) {
+        // ---- the checker: after every commit, every grown region of the
+        // dispatch log ahead of the walk that was grown or checked before that
+        // commit is tested against C; an invalid one is marked DIRTY (a
+        // grower regrows it before the walk arrives).  Only a hint: the walker
+        // validates whatever it commits, and regrows what it finds DIRTY.
+        __builtin_amdgcn_s_setprio(PLVI_MW_CHECKER_PRIO);
+        int last = 0;
+        while (!mw_lds_load(&ctl->finished)) {
+            const int nc = mw_lds_load(&ctl->ncommit);
+            if (nc == last) {
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            last = nc;
+            const int wp = mw_lds_load(&ctl->wptr), dn = mw_lds_load(&ctl->dlog_n);
+            const int head = mw_lds_load(&ctl->head);
+            for (int b0 = wp; b0 < dn; b0 += 64) {
+                const int j = b0 + lane;
+                int sj = 0, n = 0;
+                bool cand = false;
+                if (j < dn) {
+                    const int e = j & (kMwLog - 1);
+                    sj = dlog[2 * e + 1];
+                    lds_slot* S = mw_slot(pool, sj);
+                    cand = mw_lds_load(&S->state) == kMwDone && S->seed == dlog[2 * e] && S->seed >= head &&
+                           S->chk < nc && S->ovf == 0;
+                    n = S->n;
+                }
+                // regions held in LDS: a lane each, first committed point ends the test
+                const bool small = cand && n <= kMwSP;
+                bool bad = false;
+                if (small) {
+                    const lds_u32* pts = (const lds_u32*)(pool + (size_t)sj * kMwSlotBytes + sizeof(MwSlot));
+                    for (int k = 0; k < n; ++k) {
+                        const unsigned v = pts[k];
+                        if (mw_bit(E.C, E.wpr, (int)(v & 0xffffu), (int)(v >> 16))) {
+                            bad = true;
+                            break;
+                        }
+                    }
+                }
+                // longer regions: the whole wave, one at a time
+                for (unsigned long long big = ballot(cand && !small); big; big &= big - 1) {
+                    const int lb = __ffsll((long long)big) - 1;
+                    const int sb = readlane_i(sj, lb), nb = readlane_i(n, lb);
+                    const MwQueue Q = mw_slot_queue(pool, sspill, sb);
+                    bool bb = false;
+                    for (int k = lane; k < nb; k += 64) {
+                        const unsigned v = mw_qget(Q, k);
+                        bb |= mw_bit(E.C, E.wpr, (int)(v & 0xffffu), (int)(v >> 16));
+                    }
+                    const bool isbad = ballot(bb) != 0ull;
+                    if (lane == lb) bad = isbad;
+                }
+                if (cand) {
+                    lds_slot* S = mw_slot(pool, sj);
+                    if (bad) {
+                        const bool marked = mw_lds_cas(&S->state, kMwDone, kMwDirty);
+#if PLVI_MW_DIAG
+                        if (STATS && marked) mw_stat(ctl, 28, 1);
+#endif
+                        (void)marked;
+                    } else {
+                        S->chk = nc;  // a hint (a racing re-dispatch rewrites it)
+                    }
+                }
+            }
+        }
     } else {
         // ---- growers
         __builtin_amdgcn_s_setprio(PLVI_MW_GROWER_PRIO);
@@ -849,14 +962,35 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
                 continue;
             }
             if (mw_lds_load(&ctl->finished)) break;
-            // revalidate one of the regions the walk reaches next (the first
-            // kMwLook dispatch-log entries after it) that was grown or checked
-            // before the latest commit: one whose pixels an earlier region has
-            // since taken is regrown here, off the walker's path (the walker
-            // still validates every region it commits)
-            if (kMwLook > 0) {
+            // regrow a region an earlier commit has invalidated, off the
+            // walker's path (the walker still validates every region it
+            // commits).  With the checker: the earliest DIRTY region of the log
+            // ahead of the walk (claimed by compare-and-swap, no lock).  r05
+            // scheme: recheck one of the first kMwLook log entries after the
+            // walk that was grown or checked before the latest commit.
+            if (kMwChecker || kMwLook > 0) {
                 int rs = -1;
-                if (mw_try_lock(&ctl->dlock, lane)) {
+                if (kMwChecker) {
+                    const int wp = mw_lds_load(&ctl->wptr), dn = mw_lds_load(&ctl->dlog_n);
+                    const int head = mw_lds_load(&ctl->head);
+                    for (int b0 = wp; b0 < dn && rs < 0; b0 += 64) {
+                        const int j = b0 + lane;
+                        int sj = -1;
+                        bool ok = false;
+                        if (j < dn) {
+                            const int e = j & (kMwLog - 1);
+                            sj = dlog[2 * e + 1];
+                            lds_slot* S = mw_slot(pool, sj);
+                            ok = mw_lds_load(&S->state) == kMwDirty && S->seed == dlog[2 * e] && S->seed >= head;
+                        }
+                        for (unsigned long long b = ballot(ok); b && rs < 0; b &= b - 1) {
+                            const int cand = readlane_i(sj, __ffsll((long long)b) - 1);
+                            int got = 0;
+                            if (lane == 0) got = mw_lds_cas(&mw_slot(pool, cand)->state, kMwDirty, kMwGrowing) ? 1 : 0;
+                            if (__builtin_amdgcn_readfirstlane(got)) rs = cand;
+                        }
+                    }
+                } else if (mw_try_lock(&ctl->dlock, lane)) {
                     const int wp = mw_lds_load(&ctl->wptr), dn = mw_peek(&ctl->dlog_n);
                     const int nc = mw_lds_load(&ctl->ncommit), head = mw_lds_load(&ctl->head);
                     const int j = wp + lane;
@@ -884,14 +1018,15 @@ __global__ __launch_bounds__(NW * 64) void lsd_grow_mw_kernel(
                     const int seed = S->seed, n0 = S->n;
                     const int sx = seed % E.rowbits, sy = seed / E.rowbits;
                     const MwQueue Q = mw_slot_queue(pool, sspill, rs);
-                    bool bad = false;
+                    bool bad = kMwChecker;  // a DIRTY region is known invalid
 #if PLVI_MW_DIAG
-                    if (STATS && lane == 0) mw_stat(ctl, 28, 1);
+                    if (STATS && lane == 0 && !kMwChecker) mw_stat(ctl, 28, 1);
 #endif
-                    for (int k = lane; k < n0; k += 64) {
-                        const unsigned v = mw_qget(Q, k);
-                        bad |= mw_bit(E.C, E.wpr, (int)(v & 0xffffu), (int)(v >> 16));
-                    }
+                    if (!kMwChecker)
+                        for (int k = lane; k < n0; k += 64) {
+                            const unsigned v = mw_qget(Q, k);
+                            bad |= mw_bit(E.C, E.wpr, (int)(v & 0xffffu), (int)(v >> 16));
+                        }
                     int nst = kMwDone;
                     if (mw_bit(E.C, E.wpr, sx, sy)) {
                         nst = kMwFree;  // the seed itself was taken: the walk never visits it

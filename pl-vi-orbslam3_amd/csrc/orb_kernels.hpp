@@ -497,7 +497,7 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
                                                            uint8_t* __restrict__ blur, uint8_t* __restrict__ score,
                                                            int k0, int k1,
                                                            int k2, int k3, int tmin, int t1, int t2, int nstrips,
-                                                           int nf) {
+                                                           int nf, int copy0) {
     if (PLVI_BF_SETPRIO) __builtin_amdgcn_s_setprio(PLVI_BF_SETPRIO);
     else PLVI_ORB_PRIO_SET();
     typedef unsigned short QT;
@@ -680,13 +680,13 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
             if (outl) {
                 const uint32_t o = (uint32_t)(y * w + c0), ob = (uint32_t)(y * bw + c0);
                 if (omask == 15u) {
-                    if (sd.level == 0) st_u32(Dp + o, cvw);
+                    if (sd.level == 0 && copy0) st_u32(Dp + o, cvw);
                     st_u32(Bp + ob, Bv);
                     st_u32(Sp + ob, 0u);  // candidates / survivors are overwritten later (wave-ordered)
                 } else {
                     for (int j = 0; j < 4; ++j)
                         if ((omask >> j) & 1u) {
-                            if (sd.level == 0) Dp[o + j] = (uint8_t)byte_of(cvw, j);
+                            if (sd.level == 0 && copy0) Dp[o + j] = (uint8_t)byte_of(cvw, j);
                             Bp[ob + j] = (uint8_t)byte_of(Bv, j);
                             Sp[ob + j] = 0;
                         }
@@ -1284,7 +1284,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PLVI_DESC_W
                                                            const uint8_t* __restrict__ blur,
                                                            const int* __restrict__ rect_cnt,
                                                            float4* __restrict__ lvkp, uint8_t* __restrict__ lvdesc,
-                                                           int kpCapFrame) {
+                                                           int kpCapFrame, const uint8_t* __restrict__ frames0,
+                                                           size_t f_frame, size_t f_row) {
     PLVI_ORB_PRIO_SET();
     __shared__ __align__(16) uint8_t patch[4][kDescP * kDescPitch];
     __shared__ __align__(16) uint8_t ipatch[4][kAngRows * kAngPitch];
@@ -1330,9 +1331,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PLVI_DESC_W
         if (snext < kpCapFrame) kpn = load_kp(snext);
         const OrbLevelDev& lv = lvs[l];
         const int cx = (int)kp.x, cy = (int)kp.y;  // integer-valued level coords (>= 19 from every border)
-        const int W = lv.w, BW = lv.bpitch;
+        // level 0's image is the caller's frame unless the pyramid holds a copy
+        // (frames0 != null: the batch's rows are not packed, or PLVI_ORB_L0_COPY)
+        const bool view0 = l == 0 && frames0;
+        const int W = view0 ? (int)f_row : lv.w, BW = lv.bpitch;
         // ---- stage both boxes: dword loads first, then LDS writes
-        const uint8_t* I0 = pyr + lv.off + (size_t)f * lv.plane + (size_t)(cy - kAngR) * W + (cx - kAngR);
+        const uint8_t* I0 = (view0 ? frames0 + (size_t)f * f_frame : pyr + lv.off + (size_t)f * lv.plane) +
+                            (size_t)(cy - kAngR) * W + (cx - kAngR);
         const uint8_t* B0 = blur + lv.boff + (size_t)f * lv.bplane + (size_t)(cy - kDescR) * BW + (cx - kDescR);
         uint32_t iv[4], bv[6];
         {

@@ -100,6 +100,14 @@ struct OrbPipeline {
     // (PLVI_PYR_LEVELWISE overrides)
     int pyrLevelwiseMax = 1024;
     int lastFrames = 0;
+    // Level 0 of the pyramid (mvImagePyramid[0]) is the input frame itself.
+    // When the batch's rows are packed (row stride = width) it stays a view of
+    // the caller's frames (no copy: 1 B/pixel of level-0 writes less in the
+    // blur + FAST pass); otherwise, or with PLVI_ORB_L0_COPY=1, blur + FAST
+    // copies it into the pyramid buffer as before.
+    const uint8_t* l0view = nullptr;  // the last run's frames when level 0 is a view
+    size_t l0fs = 0;
+    bool l0forceCopy = false;
     // Stage timing with HIP events on the launch stream (bench.py roofline).
     static constexpr int kStages = 7, kRing = 512;
     bool prof = false;
@@ -186,6 +194,7 @@ struct OrbPipeline {
         W = width; H = height; Bcap = max_batch; device = dev; L = p->nlevels;
         if (const char* e = getenv("PLVI_GROW_GATE")) gateStage = std::min(3, std::max(0, atoi(e)));
         if (const char* e = getenv("PLVI_PYR_LEVELWISE")) pyrLevelwiseMax = atoi(e);
+        if (const char* e = getenv("PLVI_ORB_L0_COPY")) l0forceCopy = atoi(e) != 0;
         PLVI_CHECK(hipSetDevice(device));
         {
             // the handle's own stream (single-frame calls, batches without a
@@ -378,6 +387,9 @@ struct OrbPipeline {
         if (nf <= 0 || nf > Bcap) return PLVI_E_BADARG;
         if (!st) st = stream;
         lastFrames = nf;
+        const bool copy0 = l0forceCopy || row_stride != (size_t)W;
+        l0view = copy0 ? nullptr : d_frames;
+        l0fs = frame_stride;
         const int tmin = std::max(0, std::min(std::min(prm.ini_th_fast, prm.min_th_fast), 255));
         const int t1 = std::max(0, std::min(prm.ini_th_fast, 255)), t2 = std::max(0, std::min(prm.min_th_fast, 255));
         uint8_t* P = pyr.as<uint8_t>();
@@ -430,7 +442,7 @@ struct OrbPipeline {
         hipLaunchKernelGGL(orb_blur_fast_kernel, dim3((unsigned)(strips.size() * 8 * ((nf + 7) / 8))), dim3(64), 0, st,
                            d_lv.as<OrbLevelDev>(), d_strips.as<OrbStripDev>(), d_frames, frame_stride, row_stride, P,
                            Bl, Sc, taps[0], taps[1], taps[2], taps[3], tmin, t1, t2, (int)strips.size(),
-                           nf);
+                           nf, copy0 ? 1 : 0);
         if (kt) {
             PLVI_CHECK(hipEventRecord(kev[2 * kn + 1], st));
             ++kn;
@@ -473,7 +485,8 @@ struct OrbPipeline {
         // K6 orientation + rBRIEF
         hipLaunchKernelGGL(orb_describe_kernel, dim3((kpCapFrame + 15) / 16, nf), dim3(256), 0, st,
                            d_lv.as<OrbLevelDev>(), L, (const uint8_t*)P, (const uint8_t*)Bl,
-                           (const int*)rectCnt.as<int>(), lvkp.as<float4>(), lvdesc.as<uint8_t>(), kpCapFrame);
+                           (const int*)rectCnt.as<int>(), lvkp.as<float4>(), lvdesc.as<uint8_t>(), kpCapFrame,
+                           copy0 ? nullptr : d_frames, frame_stride, row_stride);
         mark(6, st);
         // K7 assemble
         hipLaunchKernelGGL(orb_assemble_kernel, dim3(nf), dim3(256), 0, st, d_lv.as<OrbLevelDev>(), L,
@@ -609,8 +622,13 @@ extern "C" int plvi_orb_pyramid_level(plvi_orb_extractor* h, int frame, int leve
     if (!dst) return PLVI_OK;
     PLVI_CHECK(hipSetDevice(h->p().device));
     PLVI_CHECK(hipStreamSynchronize(h->p().stream));
-    PLVI_CHECK(hipMemcpy(dst, h->p().pyr.as<uint8_t>() + d.off + (size_t)frame * d.plane, (size_t)d.plane,
-                         hipMemcpyDeviceToHost));
+    const uint8_t* src = h->p().pyr.as<uint8_t>() + d.off;
+    size_t fs = (size_t)d.plane;
+    if (level == 0 && h->p().l0view) {  // level 0 is a view of the last run's frames
+        src = h->p().l0view;
+        fs = h->p().l0fs;
+    }
+    PLVI_CHECK(hipMemcpy(dst, src + (size_t)frame * fs, (size_t)d.plane, hipMemcpyDeviceToHost));
     return PLVI_OK;
 }
 
@@ -620,8 +638,9 @@ extern "C" int plvi_orb_pyramid_device(plvi_orb_extractor* h, int level, const u
     if (nlevels) *nlevels = h->p().L;
     if (level < 0) return PLVI_OK;
     const auto& d = h->p().lv[level];
-    if (d_frame0) *d_frame0 = h->p().pyr.as<uint8_t>() + d.off;
-    if (frame_stride) *frame_stride = (size_t)d.plane;
+    const bool view = level == 0 && h->p().l0view;
+    if (d_frame0) *d_frame0 = view ? h->p().l0view : h->p().pyr.as<uint8_t>() + d.off;
+    if (frame_stride) *frame_stride = view ? h->p().l0fs : (size_t)d.plane;
     if (w) *w = d.w;
     if (hgt) *hgt = d.h;
     return PLVI_OK;

@@ -38,9 +38,13 @@ constexpr int kThHigh = 100, kThLow = 50;          // ORBmatcher::TH_HIGH / TH_L
 constexpr int kLGridCols = 64, kLGridRows = 48;    // FRAME_GRID_COLS / ROWS (include/Frame.h:47-48)
 constexpr int kLGridCells = kLGridCols * kLGridRows;
 
+// per level and side: frame 0's image and the bytes between frames (level 0
+// may be a view of the caller's frames, the other levels the extractor's
+// pyramid buffer: plvi_orb_pyramid_device)
 struct StereoLv {
-    long long off[16];    // byte offset of level l, frame 0
-    long long plane[16];  // bytes per frame of level l
+    const uint8_t* pl[16];
+    const uint8_t* pr[16];
+    long long planeL[16], planeR[16];
     int w[16], h[16];
 };
 struct StereoPrm {
@@ -91,8 +95,7 @@ __device__ int block_scan_excl(int* s, int n, int* s_tmp) {
 __global__ __launch_bounds__(kStThreads) void stereo_orb_kernel(
     const plvi_keypoint* __restrict__ kL, const uint8_t* __restrict__ dL, const int* __restrict__ nLs, int capL,
     const plvi_keypoint* __restrict__ kR, const uint8_t* __restrict__ dR, const int* __restrict__ nRs, int capR,
-    const uint8_t* __restrict__ pyrL, const uint8_t* __restrict__ pyrR, StereoLv lv, StereoPrm prm,
-    float* __restrict__ uright, float* __restrict__ depth, int* __restrict__ nstereo, int* __restrict__ err) {
+    StereoLv lv, StereoPrm prm, float* __restrict__ uright, float* __restrict__ depth, int* __restrict__ nstereo, int* __restrict__ err) {
     extern __shared__ __align__(16) int lds_s[];
     __shared__ int s_tmp[kStThreads / 64], s_njob, s_nacc, s_fail, s_hist[256], s_sel[2];
     __shared__ int s_part[kStThreads / 64][121], s_dist[kStThreads / 64][11];
@@ -203,8 +206,8 @@ __global__ __launch_bounds__(kStThreads) void stereo_orb_kernel(
             if (crLo < 0 || (int)(scaleduR0 + L - w) + 2 * w + 1 > lw) {
                 if (lane == 0) atomicOr(err, 2);
             } else {
-                const uint8_t* PL = pyrL + lv.off[oct] + (size_t)f * lv.plane[oct];
-                const uint8_t* PR = pyrR + lv.off[oct] + (size_t)f * lv.plane[oct];
+                const uint8_t* PL = lv.pl[oct] + (size_t)f * lv.planeL[oct];
+                const uint8_t* PR = lv.pr[oct] + (size_t)f * lv.planeR[oct];
                 const int cL = PL[(size_t)(r0 + w) * lw + c0 + w];
 #pragma unroll
                 for (int pass = 0; pass < 2; ++pass) {
@@ -491,8 +494,8 @@ static size_t stereo_orb_lds(int nRows, int capL, int capR, int rowCap) {
 
 // Launch over raw device tables (shared by the handle and host entry points).
 static int launch_stereo_orb(int n, const plvi_keypoint* kL, const uint8_t* dL, const int* nL, int capL,
-                             const plvi_keypoint* kR, const uint8_t* dR, const int* nR, int capR, const uint8_t* pyrL,
-                             const uint8_t* pyrR, const StereoLv& lv, StereoPrm prm, float* ur, float* dp, int* ns,
+                             const plvi_keypoint* kR, const uint8_t* dR, const int* nR, int capR,
+                             const StereoLv& lv, StereoPrm prm, float* ur, float* dp, int* ns,
                              int* err, hipStream_t st) {
     if (n <= 0) return PLVI_OK;
     if (capL < 1 || capR < 1 || capR > 65535 || prm.nlevels < 1 || prm.nlevels > 16) return PLVI_E_BADARG;
@@ -501,7 +504,7 @@ static int launch_stereo_orb(int n, const plvi_keypoint* kL, const uint8_t* dL, 
     const size_t lds = stereo_orb_lds(lv.h[0], capL, capR, prm.rowCap);
     if (lds > 150 * 1024) return PLVI_E_BADARG;
     hipLaunchKernelGGL(stereo_orb_kernel, dim3(n), dim3(kStThreads), lds, st, kL, dL, nL, capL, kR, dR, nR, capR,
-                       pyrL, pyrR, lv, prm, ur, dp, ns, err);
+                       lv, prm, ur, dp, ns, err);
     PLVI_CHECK(hipGetLastError());
     return PLVI_OK;
 }
@@ -525,7 +528,6 @@ extern "C" int plvi_stereo_match_batch(plvi_orb_extractor* left, plvi_orb_extrac
     prm.mb = mb;
     prm.mbf = mbf;
     float inv[16], sc[16];
-    const uint8_t *bL = nullptr, *bR = nullptr;
     int nlev = 0;
     rc = plvi_orb_pyramid_device(left, -1, nullptr, nullptr, nullptr, nullptr, &nlev);
     if (rc) return rc;
@@ -536,18 +538,18 @@ extern "C" int plvi_stereo_match_batch(plvi_orb_extractor* left, plvi_orb_extrac
         int wl, hl, wr, hr;
         if ((rc = plvi_orb_pyramid_device(left, l, &pl, &fsl, &wl, &hl, nullptr))) return rc;
         if ((rc = plvi_orb_pyramid_device(right, l, &pr, &fsr, &wr, &hr, nullptr))) return rc;
-        if (wl != wr || hl != hr || fsl != fsr) return PLVI_E_BADARG;  // same extractor geometry both sides
-        if (l == 0) { bL = pl; bR = pr; }
-        lv.off[l] = (long long)(pl - bL);
-        if (pr - bR != pl - bL) return PLVI_E_BADARG;
-        lv.plane[l] = (long long)fsl;
+        if (wl != wr || hl != hr) return PLVI_E_BADARG;  // same extractor geometry both sides
+        lv.pl[l] = pl;
+        lv.pr[l] = pr;
+        lv.planeL[l] = (long long)fsl;
+        lv.planeR[l] = (long long)fsr;
         lv.w[l] = wl;
         lv.h[l] = hl;
     }
     if ((rc = plvi_orb_scale_tables(left, sc, inv, nullptr, nullptr))) return rc;
     prm.nlevels = nlev;
     for (int l = 0; l < nlev; ++l) { prm.scale[l] = sc[l]; prm.inv[l] = inv[l]; }
-    return launch_stereo_orb(n_frames, kL, dL, nL, capL, kR, dR, nR, capR, bL, bR, lv, prm, d_uright, d_depth,
+    return launch_stereo_orb(n_frames, kL, dL, nL, capL, kR, dR, nR, capR, lv, prm, d_uright, d_depth,
                              d_nstereo, d_err, (hipStream_t)stream);
 }
 
@@ -564,8 +566,7 @@ extern "C" int plvi_stereo_match(const plvi_keypoint* kpsL, const uint8_t* descL
     prm.nlevels = nlevels;
     size_t pyrBytes = 0;
     for (int l = 0; l < nlevels; ++l) {
-        lv.off[l] = lvl_off[l];
-        lv.plane[l] = 0;
+        lv.planeL[l] = lv.planeR[l] = 0;
         lv.w[l] = lvl_w[l];
         lv.h[l] = lvl_h[l];
         prm.scale[l] = scale[l];
@@ -590,9 +591,13 @@ extern "C" int plvi_stereo_match(const plvi_keypoint* kpsL, const uint8_t* descL
     PLVI_CHECK(hipMemcpy(b + oPL, pyrL, pyrBytes, hipMemcpyHostToDevice));
     PLVI_CHECK(hipMemcpy(b + oPR, pyrR, pyrBytes, hipMemcpyHostToDevice));
     PLVI_CHECK(hipMemcpy(I, counts, 16, hipMemcpyHostToDevice));
+    for (int l = 0; l < nlevels; ++l) {
+        lv.pl[l] = b + oPL + lvl_off[l];
+        lv.pr[l] = b + oPR + lvl_off[l];
+    }
     float* ur = reinterpret_cast<float*>(b + oO);
     int rc = launch_stereo_orb(1, reinterpret_cast<plvi_keypoint*>(b + oKL), b + oDL, I, nL,
-                               reinterpret_cast<plvi_keypoint*>(b + oKR), b + oDR, I + 1, capR, b + oPL, b + oPR, lv,
+                               reinterpret_cast<plvi_keypoint*>(b + oKR), b + oDR, I + 1, capR, lv,
                                prm, ur, ur + nL, I + 2, I + 3, nullptr);
     if (rc) return rc;
     int out[2];

@@ -21,8 +21,10 @@ def test_blur_fast_bytes_is_survey_blur_plus_fast_read():
     planes = sum(w * h for w, h in dims)
     assert planes == 950_532
     assert b.blur_fast_bytes(640, 480) == 2_851_596 == 1_901_064 + 950_532
-    # the kernel's own materialisation (score planes, level-0 copy) is reported beside it
-    assert b.blur_fast_kernel_bytes(640, 480) == 3_158_796 == planes + 2 * planes + 640 * 480
+    # the kernel's own materialisation (score planes; the level-0 copy only for row-padded
+    # frames since r06) is reported beside it
+    assert b.blur_fast_kernel_bytes(640, 480) == 2_851_596 == planes + 2 * planes
+    assert b.blur_fast_kernel_bytes(640, 480, copy0=True) == 3_158_796 == planes + 2 * planes + 640 * 480
 
 
 def test_roofline_frac_is_bytes_over_avg_launch_over_peak():
@@ -58,7 +60,7 @@ def test_committed_traffic_is_calibrated_and_near_algorithmic():
     b = _bench()
     t = b.committed_traffic(3072, "orb_blur_fast_kernel")
     assert t is not None
-    alg = b.blur_fast_kernel_bytes(640, 480) * 3072
+    alg = b.blur_fast_kernel_bytes(640, 480, copy0=True) * 3072
     assert 1.0 <= t / alg < 1.3  # measured 1.20
     assert 1.0 <= t / (b.blur_fast_bytes(640, 480) * 3072) < 1.45  # vs the SURVEY model: 1.36
     assert b.committed_traffic(3071, "orb_blur_fast_kernel") is None

@@ -124,3 +124,25 @@ def test_mw_consecutive_launches(plvi_lib, monkeypatch):
             for f in range(2):
                 assert _same(out[f], ol.line_extract(frames[i + f])), f"rep {rep} pair {i} frame {f}"
     lx.close()
+
+
+def test_mw_repeatable_against_sequential(plvi_lib, monkeypatch):
+    """The multi-wave kernel's result must not depend on how its waves
+    interleave: eight launches over the same 16 frames each equal the
+    sequential kernel bit for bit (r06: an unlocked slot claim between a
+    grower and the dispatcher once gave 2 differing frames in 480,
+    tools/mw_stress.py, profiles/r06/mw_stress_*.txt)."""
+    frames = synth.batch(16, seed0=5)
+    seq = _run(monkeypatch, frames, 0)
+    monkeypatch.setenv("PLVI_GROW_MW", "256")
+    lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 640, 480, max_batch=16)
+    buf = plvi.DeviceBuffer(frames.nbytes)
+    buf.upload(frames)
+    for rep in range(8):
+        lx.extract_batch(buf.ptr, 16, 640 * 480, 640)
+        plvi_lib.plvi_device_synchronize()
+        assert lx.errors() == 0
+        out = _tables(lx, 16)
+        bad = [f for f in range(16) if not _same(out[f], seq[f])]
+        assert not bad, f"launch {rep}: frames {bad} differ from the sequential kernel"
+    lx.close()

@@ -52,17 +52,19 @@ def test_orb_pyramid_matches_oracle(orb640):
         assert np.array_equal(got, exp["pyr"]), f"level {level}"
 
 
+@pytest.mark.parametrize("pad", [5, 0])
 @pytest.mark.parametrize("mode", ["0", "100000"])
 @pytest.mark.parametrize("wh", [(640, 480), (752, 480), (641, 479)])
-def test_orb_pyramid_builders_batch(plvi_lib, monkeypatch, mode, wh):
+def test_orb_pyramid_builders_batch(plvi_lib, monkeypatch, mode, wh, pad):
     """Both pyramid builders -- the streaming kernel (PLVI_PYR_LEVELWISE=0: every batch) and the
     level-by-level launches (PLVI_PYR_LEVELWISE=100000) -- give the oracle's levels for every frame of a
-    batch read from a row-padded device buffer, and the oracle's keypoints and descriptors."""
+    batch read from a row-padded (pad 5: level 0 copied into the pyramid) or packed (pad 0: level 0 is a
+    view of the caller's frames) device buffer, and the oracle's keypoints and descriptors."""
     monkeypatch.setenv("PLVI_PYR_LEVELWISE", mode)
     w, h = wh
     imgs = [synth.frame(40 + k, w, h) for k in range(3)]
     imgs.append(structured_frames(w, h)["checker"])
-    B, stride = len(imgs), w + 5  # rows padded: frames as a strided view
+    B, stride = len(imgs), w + pad  # padded rows: frames as a strided view
     frames = np.zeros((B, h, stride), np.uint8)
     for k, im in enumerate(imgs):
         frames[k, :, :w] = im
@@ -72,6 +74,12 @@ def test_orb_pyramid_builders_batch(plvi_lib, monkeypatch, mode, wh):
     ext.extract_batch(buf.ptr, B, h * stride, stride)
     plvi_lib.plvi_device_synchronize()
     assert ext.errors() == 0
+    p0, fs0, w0, h0 = ext.pyramid_device(0)
+    assert (w0, h0) == (w, h)
+    if pad == 0:
+        assert (p0, fs0) == (buf.ptr, h * stride), "packed frames: level 0 is a view of the batch"
+    else:
+        assert p0 != buf.ptr and fs0 == w * h
     for k, im in enumerate(imgs):
         for level in range(8):
             exp = ol.orb_stage(im, level)
@@ -85,6 +93,32 @@ def test_orb_pyramid_builders_batch(plvi_lib, monkeypatch, mode, wh):
         s = slice(k * cap, k * cap + cnt[k])
         _assert_same((int(mono[k]), kps[s], desc[s]), ol.orb_extract(im), f"mode {mode} frame {k}")
     ext.close()
+
+
+def test_orb_level0_copy_switch(plvi_lib, monkeypatch):
+    """PLVI_ORB_L0_COPY=1 keeps the r05 layout (level 0 copied into the pyramid buffer) for packed
+    frames too; both layouts give the oracle's outputs."""
+    frames = synth.batch(3, seed0=60)
+    buf = plvi.DeviceBuffer(frames.nbytes)
+    buf.upload(frames)
+    for copy in ("0", "1"):
+        monkeypatch.setenv("PLVI_ORB_L0_COPY", copy)
+        ext = plvi.ORBextractor(1000, 1.2, 8, 20, 7, 640, 480, max_batch=3)
+        ext.extract_batch(buf.ptr, 3, 640 * 480, 640)
+        plvi_lib.plvi_device_synchronize()
+        p0 = ext.pyramid_device(0)[0]
+        assert (p0 == buf.ptr) == (copy == "0")
+        for k in range(3):
+            assert np.array_equal(ext.pyramid_level(0, k), frames[k])
+        kp_p, de_p, co_p, mo_p, cap = ext.outputs()
+        cnt = plvi.download(co_p, np.zeros(3, np.int32))
+        mono = plvi.download(mo_p, np.zeros(3, np.int32))
+        kps = plvi.download(kp_p, np.zeros(3 * cap, plvi.KEYPOINT_DTYPE))
+        desc = plvi.download(de_p, np.zeros((3 * cap, 32), np.uint8))
+        for k in range(3):
+            s = slice(k * cap, k * cap + cnt[k])
+            _assert_same((int(mono[k]), kps[s], desc[s]), ol.orb_extract(frames[k]), f"copy {copy} frame {k}")
+        ext.close()
 
 
 def test_orb_real_euroc_752(orb752):
