@@ -60,9 +60,9 @@ def test_committed_traffic_is_calibrated_and_near_algorithmic():
     b = _bench()
     t = b.committed_traffic(3072, "orb_blur_fast_kernel")
     assert t is not None
-    alg = b.blur_fast_kernel_bytes(640, 480, copy0=True) * 3072
-    assert 1.0 <= t / alg < 1.3  # measured 1.20
-    assert 1.0 <= t / (b.blur_fast_bytes(640, 480) * 3072) < 1.45  # vs the SURVEY model: 1.36
+    alg = b.blur_fast_kernel_bytes(640, 480) * 3072  # r06: level 0 a view of the packed frames
+    assert 1.0 <= t / alg < 1.3  # measured 1.22 at r06 (1.20 at r05 with the level-0 copy counted)
+    assert 1.0 <= t / (b.blur_fast_bytes(640, 480) * 3072) < 1.3  # vs the SURVEY model: r05 1.35, r06 1.22
     assert b.committed_traffic(3071, "orb_blur_fast_kernel") is None
 
 
