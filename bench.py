@@ -501,7 +501,7 @@ def schedule_knobs(batch):
     return {"env": env,
             "orb_waits_for_lsd_prep": after_prep >= 2 or (after_prep == 1 and batch < 1024),
             "growth_waits_for_blur_fast": os.environ.get("PLVI_GROW_AFTER_BLUR", "1") != "0" and big,
-            "sobel_after_growth": os.environ.get("PLVI_SOBEL_AFTER_GROW", "1") != "0" and
+            "sobel_after_growth": os.environ.get("PLVI_SOBEL_AFTER_GROW", "0") != "0" and
             os.environ.get("PLVI_GROW_AFTER_BLUR", "1") != "0" and big}
 
 

@@ -76,7 +76,7 @@ struct LinePipeline {
                evBlur = nullptr, evGate = nullptr, evGrow2 = nullptr, evPair = nullptr;
     bool growAfterBlur = true, sobelWithGrow = false, growSplit = false;
     int sobelGate = -1;  // PLVI_SOBEL_GATE: ORB stage after which the Sobel pyramid starts (-1: with growth)
-    bool sobelAfterGrow = true;
+    bool sobelAfterGrow = false;
     hipStream_t critStream = nullptr;  // frame schedule: prep -> grow -> describe
     hipStream_t crit2 = nullptr;       // frame schedule: octave-1 region growing (split mode)
     hipStream_t octStream = nullptr;   // small batches: prep + growth of octaves >= 1 beside octave 0's
@@ -211,13 +211,15 @@ struct LinePipeline {
             // so it does not take wave slots from the ORB chain while that chain
             // runs beside region growing
             if (const char* e7 = getenv("PLVI_SOBEL_GATE")) sobelGate = std::min(5, std::max(-1, atoi(e7)));
-            // PLVI_SOBEL_AFTER_GROW (default 1, batches from 1024 frames): the
-            // Sobel pyramid runs on the critical stream after region growing +
-            // rect + assemble instead of beside growth on a low-priority
-            // stream.  With two batches in flight the step is the same (47.4K
-            // vs 47.6K FPS, within run-to-run noise) and lbd_sobel0 takes 3.0-3.3
-            // instead of 23-29 ms per launch (its waves no longer sit on the
-            // SIMDs beside the growth waves; profiles/r04/ab_sched_inflight2.txt)
+            // PLVI_SOBEL_AFTER_GROW=1 (batches from 1024 frames): the Sobel
+            // pyramid runs on the critical stream after region growing + rect +
+            // assemble instead of beside growth on a low-priority stream.  The
+            // r04 default (flat then: 47.4K vs 47.6K FPS, lbd_sobel0 3.0-3.3
+            // instead of 23-29 ms per launch); since r06, when the ORB chain and
+            // not region growing is the longest chain of the two-slot schedule,
+            // the line chain's extra work costs more than the Sobel waves beside
+            // growth: off by default, 52.6-52.8K -> 53.3-53.5K FPS
+            // (profiles/r06/ab_combo.txt)
             if (const char* e8 = getenv("PLVI_SOBEL_AFTER_GROW")) sobelAfterGrow = atoi(e8) != 0;
             if (prio) PLVI_CHECK(hipStreamCreateWithPriority(&critStream, hipStreamNonBlocking, greatest));
             // PLVI_GROW_SPLIT=1: octave 0 grows right after the prep, octave 1

@@ -349,6 +349,10 @@ constexpr int kRingMirror = 1 ? 6 : 0;
 // window read back from the LDS ring -- 64 VGPRs, 7 % slower alone, the step
 // unchanged: DESIGN.md §4)
 constexpr int kBfRB = 8;
+#ifndef PLVI_BF_WINLDS
+#define PLVI_BF_WINLDS 0
+#endif
+constexpr bool kBfWinLds = PLVI_BF_WINLDS != 0;  // blur's 7-row window from the LDS ring instead of registers
 constexpr int kBfCols = 244, kBfRowsPlain = 128, kRingRows = 16, kRingW = 256,
               kBfQCap = kBfFlush - 1 + 256 + 1;  // a row adds <= 256 candidates to < kBfFlush queued
 
@@ -618,16 +622,28 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
         for (int k = 0; k < kBfRB; ++k) {
             const int r = rb + k;
             if (r >= y1 + 3) break;
-            const uint32_t V = *reinterpret_cast<const uint32_t*>(&ring[r & (kRingRows - 1)][4 * lane]);
+            if constexpr (!kBfWinLds) {
+                const uint32_t V = *reinterpret_cast<const uint32_t*>(&ring[r & (kRingRows - 1)][4 * lane]);
 #pragma unroll
-            for (int rr = 0; rr < 6; ++rr) {
-                pe[rr] = pe[rr + 1];
-                po[rr] = po[rr + 1];
+                for (int rr = 0; rr < 6; ++rr) {
+                    pe[rr] = pe[rr + 1];
+                    po[rr] = po[rr + 1];
+                }
+                pe[6] = V & 0x00ff00ffu;
+                po[6] = (V >> 8) & 0x00ff00ffu;
             }
-            pe[6] = V & 0x00ff00ffu;
-            po[6] = (V >> 8) & 0x00ff00ffu;
             const int y = r - 3;
             if (y < y0) continue;
+            if constexpr (kBfWinLds) {
+                // the 7-row window read back from the LDS ring (rows y-3..y+3 =
+                // r-6..r are among its last 16): 18 fewer VGPRs than the register window
+#pragma unroll
+                for (int t = 0; t < 7; ++t) {
+                    const uint32_t Vt = *reinterpret_cast<const uint32_t*>(&ring[(r - 6 + t) & (kRingRows - 1)][4 * lane]);
+                    pe[t] = Vt & 0x00ff00ffu;
+                    po[t] = (Vt >> 8) & 0x00ff00ffu;
+                }
+            }
             // ---- output row y: rows y-3..y+3 are pe/po[0..6]
             uint32_t E = 0, O = 0;  // vertical sums: E = (c0, c0+2), O = (c0+1, c0+3)
 #pragma unroll
@@ -728,7 +744,7 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
 #ifndef PLVI_NMS_ROWS
 #define PLVI_NMS_ROWS 8
 #endif
-constexpr int kNmsRows = PLVI_NMS_ROWS;  // rows loaded per round trip (8: eight in flight, the next eight prefetched)
+constexpr int kNmsRows = PLVI_NMS_ROWS;  // rows loaded per round trip (<= 8: that many in flight, the next chunk prefetched)
 __device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, const OrbLevelDev* __restrict__ lvs,
                                              const uint8_t* __restrict__ score, uint8_t* __restrict__ cand, int t1,
                                              int t2) {
@@ -775,23 +791,25 @@ __device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, co
             }
         }
     } else {
-        int nx[8];
+        // kNmsRows (<= 8) rows in flight, the next chunk loaded while this one is swept
+        constexpr int R = kNmsRows;
+        int nx[R];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) nx[k] = ld(1 + k);
+        for (int k = 0; k < R; ++k) nx[k] = ld(1 + k);
         int s = ld(0);
         int hp = 0;
         int lr = max(lane_from_left(s), lane_from_right(s));
         int hc = max(s, lr);
-        for (int r0 = 0; r0 < wh; r0 += 8) {
-            int cur[8];
+        for (int r0 = 0; r0 < wh; r0 += R) {
+            int cur[R];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) cur[k] = nx[k];
-            if (r0 + 8 < wh) {
+            for (int k = 0; k < R; ++k) cur[k] = nx[k];
+            if (r0 + R < wh) {
 #pragma unroll
-                for (int k = 0; k < 8; ++k) nx[k] = ld(r0 + 9 + k);
+                for (int k = 0; k < R; ++k) nx[k] = ld(r0 + R + 1 + k);
             }
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
+            for (int k = 0; k < R; ++k) {
                 const int r = r0 + k;
                 if (r < wh) {
                     const int sn = cur[k];
@@ -1118,22 +1136,40 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
             while (!finish && !overflow) {
                 prevSize = size;
                 const int np = nv;
-                for (int i = 0; i < np; ++i) n.vprev[i] = n.vsz[i];
                 nv = 0;
-                // stable insertion sort by (cnt, seq) ascending
-                for (int i = 1; i < np; ++i) {
-                    const short v = n.vprev[i];
-                    const long long kv = ((long long)n.cnt[v] << 32) | (unsigned)n.seq[v];
-                    int j = i - 1;
-                    while (j >= 0) {
-                        const short u = n.vprev[j];
-                        const long long ku = ((long long)n.cnt[u] << 32) | (unsigned)n.seq[u];
-                        if (ku <= kv) break;
-                        n.vprev[j + 1] = u;
-                        --j;
-                    }
-                    n.vprev[j + 1] = v;
+                // sort(vPrevSizeAndPointerToNode) by (size, node) ascending, the
+                // node order being creation order (seq, unique): a rank sort with
+                // the whole wave -- lane i ranks entries i, i+64, ... against all
+                // np keys staged in ccnt (free until this phase's prefetch) -- into
+                // vprev.  (The r01-r05 lane-lockstep insertion sort was a chain of
+                // ~np^2/4 dependent LDS round trips: ~5.6K steps at level 0.)
+                wave_sync();
+                for (int i = lane; i < np; i += 64) {
+                    const int v = n.vsz[i];
+                    n.ccnt[i] = n.cnt[v];
+                    n.ccnt[C + i] = n.seq[v];
                 }
+                wave_sync();
+                for (int b0 = 0; b0 < np; b0 += 256) {
+                    int kh[4], kl[4], rk[4] = {0, 0, 0, 0};
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int i = b0 + lane + 64 * k;
+                        kh[k] = i < np ? n.ccnt[i] : 0x7fffffff;
+                        kl[k] = i < np ? n.ccnt[C + i] : 0x7fffffff;
+                    }
+                    for (int j = 0; j < np; ++j) {
+                        const int hj = n.ccnt[j], lj = n.ccnt[C + j];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) rk[k] += (hj < kh[k] || (hj == kh[k] && lj < kl[k])) ? 1 : 0;
+                    }
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const int i = b0 + lane + 64 * k;
+                        if (i < np) n.vprev[rk[k]] = n.vsz[i];
+                    }
+                }
+                wave_sync();
                 prefetch(n.vprev, np);
                 for (int j = np - 1; j >= 0; --j) {
                     const int p = n.vprev[j];
@@ -1177,6 +1213,10 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
 #define PLVI_BEST_NODES 1
 #endif
 constexpr int kBestNodes = PLVI_BEST_NODES;  // nodes per wave (the grid's x extent is nodeCapMax / kBestNodes)
+#ifndef PLVI_BEST_BATCH
+#define PLVI_BEST_BATCH 8
+#endif
+constexpr int kBestBatch = PLVI_BEST_BATCH;  // 64-pixel steps of a node rectangle loaded per round trip
 
 __device__ __forceinline__ void orb_node_best_one(const OrbLevelDev& lv, uint8_t* __restrict__ Cm, const short4 r,
                                                   float4* __restrict__ out);
@@ -1211,19 +1251,35 @@ __device__ __forceinline__ void orb_node_best_one(const OrbLevelDev& lv, uint8_t
     const int wd = max(wdt, 1);  // (an empty rectangle has total 0)
     const int q = 64 / wd, rr = 64 - q * wd;
     int yy = ry0 + lane / wd, xx = rx0 + lane % wd;
-    for (int i = lane; i < total; i += 64, yy += q, xx += rr) {
-        if (xx >= rx1) {
-            xx -= wdt;
-            ++yy;
+    uint8_t* const base = Cm + (size_t)lv.minB * lv.bpitch + lv.minB;
+    // kBestBatch steps of 64 pixels per round trip: every load of a batch is
+    // issued before any candidate is consumed (the consuming store would
+    // otherwise order each step's load behind the previous step's store)
+    for (int i0 = lane; i0 < total; i0 += 64 * kBestBatch) {
+        int off[kBestBatch], rv[kBestBatch];
+#pragma unroll
+        for (int k = 0; k < kBestBatch; ++k) {
+            if (xx >= rx1) {
+                xx -= wdt;
+                ++yy;
+            }
+            off[k] = yy * lv.bpitch + xx;
+            yy += q;
+            xx += rr;
         }
-        uint8_t* cp = Cm + (size_t)(lv.minB + yy) * lv.bpitch + lv.minB + xx;
-        const int resp = *cp;
-        if (!resp) continue;
-        *cp = 0;  // consumed: the next batch's NMS finds the plane zero
-        const unsigned ci = (unsigned)(yy - 3) / (unsigned)lv.hCell, cj = (unsigned)(xx - 3) / (unsigned)lv.wCell;
-        const unsigned key = ((ci * (unsigned)lv.nCols + cj) * (unsigned)lv.rh + (unsigned)yy) * (unsigned)lv.rw + (unsigned)xx;
-        const unsigned long long pk = ((unsigned long long)resp << 32) | (0xFFFFFFFFu - key);
-        best = pk > best ? pk : best;
+#pragma unroll
+        for (int k = 0; k < kBestBatch; ++k) rv[k] = i0 + 64 * k < total ? (int)base[off[k]] : 0;
+#pragma unroll
+        for (int k = 0; k < kBestBatch; ++k) {
+            const int resp = rv[k];
+            if (!resp) continue;
+            base[off[k]] = 0;  // consumed: the next batch's NMS finds the plane zero
+            const unsigned ys = (unsigned)off[k] / (unsigned)lv.bpitch, xs = (unsigned)off[k] - ys * (unsigned)lv.bpitch;
+            const unsigned ci = (ys - 3u) / (unsigned)lv.hCell, cj = (xs - 3u) / (unsigned)lv.wCell;
+            const unsigned key = ((ci * (unsigned)lv.nCols + cj) * (unsigned)lv.rh + ys) * (unsigned)lv.rw + xs;
+            const unsigned long long pk = ((unsigned long long)resp << 32) | (0xFFFFFFFFu - key);
+            best = pk > best ? pk : best;
+        }
     }
     for (int o = 32; o > 0; o >>= 1) {
         const unsigned long long other = __shfl_xor(best, o);
