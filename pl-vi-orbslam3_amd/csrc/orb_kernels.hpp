@@ -346,13 +346,9 @@ constexpr int kBfFlush = 1 ? 128 : 64;  // candidates scored per flush
 constexpr int kRingMirror = 1 ? 6 : 0;
 // source rows loaded per batch, in flight while the previous batch is
 // filtered (4: 75 instead of 79 VGPRs, no faster; r06 also measured the 7-row
-// window read back from the LDS ring -- 64 VGPRs, 7 % slower alone, the step
-// unchanged: DESIGN.md §4)
+// window read back from the LDS ring -- 64 VGPRs, two waves beside six
+// growth waves, yet the step 52.3-52.4K vs 52.6-52.8K FPS: profiles/r06/ab_combo.txt)
 constexpr int kBfRB = 8;
-#ifndef PLVI_BF_WINLDS
-#define PLVI_BF_WINLDS 0
-#endif
-constexpr bool kBfWinLds = PLVI_BF_WINLDS != 0;  // blur's 7-row window from the LDS ring instead of registers
 constexpr int kBfCols = 244, kBfRowsPlain = 128, kRingRows = 16, kRingW = 256,
               kBfQCap = kBfFlush - 1 + 256 + 1;  // a row adds <= 256 candidates to < kBfFlush queued
 
@@ -622,28 +618,16 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
         for (int k = 0; k < kBfRB; ++k) {
             const int r = rb + k;
             if (r >= y1 + 3) break;
-            if constexpr (!kBfWinLds) {
-                const uint32_t V = *reinterpret_cast<const uint32_t*>(&ring[r & (kRingRows - 1)][4 * lane]);
+            const uint32_t V = *reinterpret_cast<const uint32_t*>(&ring[r & (kRingRows - 1)][4 * lane]);
 #pragma unroll
-                for (int rr = 0; rr < 6; ++rr) {
-                    pe[rr] = pe[rr + 1];
-                    po[rr] = po[rr + 1];
-                }
-                pe[6] = V & 0x00ff00ffu;
-                po[6] = (V >> 8) & 0x00ff00ffu;
+            for (int rr = 0; rr < 6; ++rr) {
+                pe[rr] = pe[rr + 1];
+                po[rr] = po[rr + 1];
             }
+            pe[6] = V & 0x00ff00ffu;
+            po[6] = (V >> 8) & 0x00ff00ffu;
             const int y = r - 3;
             if (y < y0) continue;
-            if constexpr (kBfWinLds) {
-                // the 7-row window read back from the LDS ring (rows y-3..y+3 =
-                // r-6..r are among its last 16): 18 fewer VGPRs than the register window
-#pragma unroll
-                for (int t = 0; t < 7; ++t) {
-                    const uint32_t Vt = *reinterpret_cast<const uint32_t*>(&ring[(r - 6 + t) & (kRingRows - 1)][4 * lane]);
-                    pe[t] = Vt & 0x00ff00ffu;
-                    po[t] = (Vt >> 8) & 0x00ff00ffu;
-                }
-            }
             // ---- output row y: rows y-3..y+3 are pe/po[0..6]
             uint32_t E = 0, O = 0;  // vertical sums: E = (c0, c0+2), O = (c0+1, c0+3)
 #pragma unroll
@@ -741,10 +725,10 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
 // One wave per (cell, frame), lane = window column (windows are < 64 wide),
 // each row's 8 neighbours from the rows above / below and DPP lane shifts.
 // ---------------------------------------------------------------------------
-#ifndef PLVI_NMS_ROWS
-#define PLVI_NMS_ROWS 8
-#endif
-constexpr int kNmsRows = PLVI_NMS_ROWS;  // rows loaded per round trip (<= 8: that many in flight, the next chunk prefetched)
+// rows loaded per round trip, the next chunk prefetched while one is swept
+// (r06: a whole 40-row window per round trip, 61 VGPRs, made the step 4 %
+// slower, profiles/r06/ab_nms_sat.txt)
+constexpr int kNmsRows = 8;
 __device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, const OrbLevelDev* __restrict__ lvs,
                                              const uint8_t* __restrict__ score, uint8_t* __restrict__ cand, int t1,
                                              int t2) {
@@ -760,38 +744,8 @@ __device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, co
     // with; survivors are re-read from the (L2-resident) plane when written.
     unsigned long long ka = 0, kb = 0;
     auto ld = [&](int r) -> int { return (incol && r < wh) ? (int)S[(size_t)r * w] : 0; };
-    if (kNmsRows > 8) {
-        // kNmsRows rows per round trip (no prefetch of the next chunk): a
-        // detection window of up to kNmsRows + 1 rows is one load latency
-        int s = ld(0);
-        int hp = 0;
-        int lr = max(lane_from_left(s), lane_from_right(s));
-        int hc = max(s, lr);
-        for (int r0 = 0; r0 < wh; r0 += kNmsRows) {
-            int cur[kNmsRows];
-#pragma unroll
-            for (int k = 0; k < kNmsRows; ++k) cur[k] = ld(r0 + 1 + k);
-#pragma unroll
-            for (int k = 0; k < kNmsRows; ++k) {
-                const int r = r0 + k;
-                if (r < wh) {
-                    const int sn = cur[k];
-                    const int lrn = max(lane_from_left(sn), lane_from_right(sn));
-                    const int hn = max(sn, lrn);
-                    const int m = max(max(hp, hn), lr);
-                    if (s > m) {
-                        if (s >= t1) ka |= 1ull << r;
-                        if (s >= t2) kb |= 1ull << r;
-                    }
-                    hp = hc;
-                    hc = hn;
-                    lr = lrn;
-                    s = sn;
-                }
-            }
-        }
-    } else {
-        // kNmsRows (<= 8) rows in flight, the next chunk loaded while this one is swept
+    {
+        // kNmsRows rows in flight, the next chunk loaded while this one is swept
         constexpr int R = kNmsRows;
         int nx[R];
 #pragma unroll
