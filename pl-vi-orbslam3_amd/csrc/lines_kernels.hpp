@@ -429,7 +429,7 @@ __device__ __forceinline__ void grow_wave_sync() {
 
 constexpr int kGrowRB = 64, kGrowQL = 256;
 
-template <bool STATS, bool FIXED>
+template <bool STATS, bool FIXED, bool LOOP = false>
 __global__ __launch_bounds__(64 * kGrowWaves, PLVI_GROW_WPE) void lsd_grow_kernel(const LineOctDev* __restrict__ octs,
                                                       const float* __restrict__ pix,
                                                       const double* __restrict__ modgrad,
@@ -454,8 +454,12 @@ __global__ __launch_bounds__(64 * kGrowWaves, PLVI_GROW_WPE) void lsd_grow_kerne
     // tasks per workgroup; the wave index is read uniformly (readfirstlane)
     // so that everything derived from the task stays scalar
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int task = blockIdx.x * wpw + wv;
-    if (task >= nf * oCount) return;  // no workgroup barrier below: the other waves go on
+    // a grid of fewer waves than tasks (PLVI_GROW_TPW) walks them in a
+    // grid-stride loop: with two tasks per wave, wave w grows octave 0 and then
+    // octave 1 of frame w (no workgroup barrier below: the other waves go on)
+    const int ntask = nf * oCount, tstride = LOOP ? (int)gridDim.x * wpw : ntask;
+    for (int task0 = blockIdx.x * wpw + wv; task0 < ntask; task0 += tstride) {
+    const int task = __builtin_amdgcn_readfirstlane(task0);
     // consecutive frames per workgroup (spreading frames over the workgroups
     // by a stride permutation was slower: 35.3 vs 33.2 ms per 3072 frames)
     const int o = oBase + task / nf, f = task - (o - oBase) * nf;
@@ -791,6 +795,8 @@ __global__ __launch_bounds__(64 * kGrowWaves, PLVI_GROW_WPE) void lsd_grow_kerne
         S[21] = t_real0;                                 // start and end on the chip-wide 100 MHz clock
         S[22] = __builtin_amdgcn_s_memrealtime();
     }
+    if (!LOOP) break;  // one task per wave: the loop is a single trip
+    }  // task
 }
 
 // ---------------------------------------------------------------------------

@@ -437,13 +437,15 @@ struct LinePipeline {
         // partitions would not fit one CU (large PLVI_GROW_LDS budgets)
         growWPW = (int)std::max<size_t>(1, std::min<size_t>(kGrowWaves, (160 * 1024) / growSmem));
         for (const void* k : {(const void*)lsd_grow_kernel<false, false>, (const void*)lsd_grow_kernel<true, false>,
-                              (const void*)lsd_grow_kernel<false, true>, (const void*)lsd_grow_kernel<true, true>})
+                              (const void*)lsd_grow_kernel<false, true>, (const void*)lsd_grow_kernel<true, true>,
+                              (const void*)lsd_grow_kernel<false, true, true>})
             PLVI_CHECK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)(growSmem * growWPW)));
         // Small batches (latency): lsd_grow_mw_kernel, kMwWaves waves per
         // (frame, octave) growing regions of one frame concurrently.
         // PLVI_GROW_MW = largest batch that takes it (default 256; 0 = off).
         mwMaxFrames = 256;
         if (const char* e = getenv("PLVI_GROW_MW")) mwMaxFrames = atoi(e);
+        if (const char* e = getenv("PLVI_GROW_TPW")) growTPW = std::max(1, atoi(e));
         mwMaxFrames = std::min(mwMaxFrames, Bcap);
         if (mwMaxFrames > 0) {
             // LDS: ctl + dispatch log + C/T/H bitmaps + own windows + growth
@@ -481,6 +483,15 @@ struct LinePipeline {
     DevBuf mwEpoch;          // PLVI_MW_DIAG variant: commit-epoch map per task
     size_t growSmem = 0;
     int growWPW = 1;  // region-growing tasks (waves) per workgroup
+    // region-growing tasks per wave of the large-batch kernel: 2 = octave 0
+    // and octave 1 of a frame in one wave, half the resident growth waves
+    // (3 per SIMD at 3072 frames instead of 6, so the two batches in flight
+    // can grow at once and blur + FAST shares a SIMD with 3 growth waves
+    // instead of 6).  Default 2 from 2048 frames (at least two waves per SIMD
+    // remain), else 1; PLVI_GROW_TPW forces a value.  Step 52.9-53.0K ->
+    // 53.0-53.3K FPS, blur + FAST in the timed window 15-17 -> 10-12 ms
+    // (profiles/r06/ab_knn_tpw.txt)
+    int growTPW = 0;  // 0: the batch-size rule
     int growR = 0, growRB = 0, growQL = 0;
     unsigned long long* growStats = nullptr;  // diagnostic cycle counters (plvi_lines_debug_stats)
 
@@ -562,9 +573,14 @@ struct LinePipeline {
             return;
         }
         const bool fixedWin = growR == 0 && growRB == kGrowRB && growQL == kGrowQL;
+        // (the multi-task loop is built for the default windows only)
+        const int tpwWant = growTPW > 0 ? growTPW : (nf >= 2048 ? 2 : 1);
+        const int tpw = tpwWant > 1 && !growStats && fixedWin ? tpwWant : 1;
         auto growK = growStats ? (fixedWin ? lsd_grow_kernel<true, true> : lsd_grow_kernel<true, false>)
-                               : (fixedWin ? lsd_grow_kernel<false, true> : lsd_grow_kernel<false, false>);
-        hipLaunchKernelGGL(growK, dim3((oCount * nf + growWPW - 1) / growWPW), dim3(64 * growWPW),
+                               : (fixedWin ? (tpw > 1 ? lsd_grow_kernel<false, true, true> : lsd_grow_kernel<false, true>)
+                                           : lsd_grow_kernel<false, false>);
+        const int waves = (oCount * nf + tpw - 1) / tpw;
+        hipLaunchKernelGGL(growK, dim3((waves + growWPW - 1) / growWPW), dim3(64 * growWPW),
                            growSmem * growWPW, st, d_oct.as<LineOctDev>(),
                            (const float*)pix.as<float>(), (const double*)modg.as<double>(),
                            (const float2*)seedcs.as<float2>(), gbits.as<unsigned>(), gbitsFrame,
