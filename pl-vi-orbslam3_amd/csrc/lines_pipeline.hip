@@ -487,11 +487,14 @@ struct LinePipeline {
     // and octave 1 of a frame in one wave, half the resident growth waves
     // (3 per SIMD at 3072 frames instead of 6, so the two batches in flight
     // can grow at once and blur + FAST shares a SIMD with 3 growth waves
-    // instead of 6).  Default 2 from 2048 frames (at least two waves per SIMD
-    // remain), else 1; PLVI_GROW_TPW forces a value.  Step 52.9-53.0K ->
-    // 53.0-53.3K FPS, blur + FAST in the timed window 15-17 -> 10-12 ms
-    // (profiles/r06/ab_knn_tpw.txt)
-    int growTPW = 0;  // 0: the batch-size rule
+    // instead of 6).  Default 2 in the frame schedule (run_with_orb) from
+    // 2048 frames (at least two waves per SIMD remain), else 1 -- a lines-only
+    // batch alone on the chip grows faster with every task in its own wave
+    // (30 vs 40 ms at 3072 frames); PLVI_GROW_TPW forces a value.  Step
+    // 52.9-53.0K -> 53.0-53.3K FPS, blur + FAST in the timed window 15-17 ->
+    // 10-12 ms (profiles/r06/ab_knn_tpw.txt)
+    int growTPW = 0;  // 0: the rule above
+    bool inSchedule = false;  // run_with_orb is issuing
     int growR = 0, growRB = 0, growQL = 0;
     unsigned long long* growStats = nullptr;  // diagnostic cycle counters (plvi_lines_debug_stats)
 
@@ -574,7 +577,7 @@ struct LinePipeline {
         }
         const bool fixedWin = growR == 0 && growRB == kGrowRB && growQL == kGrowQL;
         // (the multi-task loop is built for the default windows only)
-        const int tpwWant = growTPW > 0 ? growTPW : (nf >= 2048 ? 2 : 1);
+        const int tpwWant = growTPW > 0 ? growTPW : (inSchedule && nf >= 2048 ? 2 : 1);
         const int tpw = tpwWant > 1 && !growStats && fixedWin ? tpwWant : 1;
         auto growK = growStats ? (fixedWin ? lsd_grow_kernel<true, true> : lsd_grow_kernel<true, false>)
                                : (fixedWin ? (tpw > 1 ? lsd_grow_kernel<false, true, true> : lsd_grow_kernel<false, true>)
@@ -713,6 +716,7 @@ struct LinePipeline {
         lastFrames = nf;
         const bool p0 = prof;
         prof = false;  // stage events are meaningless across streams
+        inSchedule = true;
         // the critical path (prep -> region growing -> LBD describe) runs on
         // the high-priority stream `crit`; ORB and the Sobel pyramid on the
         // low-priority aux streams, started after prep (orbAfterPrep) or at once
@@ -804,6 +808,7 @@ struct LinePipeline {
         }
         PLVI_CHECK(hipStreamWaitEvent(st, evOrb, 0));
         prof = p0;
+        inSchedule = false;
         PLVI_CHECK(hipGetLastError());
         return rc;
     }
