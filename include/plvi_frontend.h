@@ -189,7 +189,7 @@ int plvi_orb_kernel_timing_read_kind(plvi_orb_extractor* h, int kind, float* tot
 /* Diagnostic: cap every level's octree node capacity at `cap` (<= 0 restores
  * the planned capacities).  A level whose DistributeOctTree needs more nodes
  * flags its frame (plvi_orb_errors bit 1) and yields no keypoints; the test
- * hook for that path (the candidate plane it must leave zero). */
+ * hook for that path. */
 int plvi_orb_debug_node_cap(plvi_orb_extractor* h, int cap);
 
 /* ------------------------------------------------------------------ Lines

@@ -12,24 +12,21 @@ constexpr int kOrbCellMax = 64;  // max detection-window side (wCell+2 < 64)
 #ifndef PLVI_BF_ALIGN
 #define PLVI_BF_ALIGN 32
 #endif
-constexpr int kBfAlign = PLVI_BF_ALIGN;  // byte alignment of the blur / score / candidate rows and strips
+constexpr int kBfAlign = PLVI_BF_ALIGN;  // byte alignment of the blur / score rows and strips
 
 struct OrbLevelDev {
     int w, h;
-    long long off;    // byte offset of this level's frame-0 plane in pyr/blur/score/cand
+    long long off;    // byte offset of this level's frame-0 plane in pyr
     long long plane;  // bytes per frame plane (w*h) of the pyramid
-    // blur / FAST score / candidate planes: rows padded to bpitch (a multiple
+    // blur / FAST score planes: rows padded to bpitch (a multiple
     // of kBfAlign) so that every blur+FAST strip writes whole aligned segments
     int bpitch;
     long long boff, bplane;
     int minB;         // EDGE_THRESHOLD-3 = 16
     int rw, rh;       // relative region (maxBorder-minBorder)
     int nCols, nRows, wCell, hCell;
-    long long satOff;    // ushort offset of this level's frame-0 strip-local SAT
-    long long satPlane;  // ushorts per frame ((rh+1) x satStrips*64)
-    long long carryOff;  // int offset of this level's frame-0 strip carry table
-    long long carryPlane;  // ints per frame ((rh+1) x (satStrips+1))
-    int satStrips;       // 64-column strips covering SAT columns 0..rw
+    int listOff;         // offset (entries) of this level's candidate list in a frame's block
+    int listCap;         // its capacity: no two NMS survivors of a cell window are 8-adjacent
     int quota;           // mnFeaturesPerLevel
     int nodeCap;         // octree output capacity (>= quota+3)
     int kpOff;           // offset of this level in the per-frame level-keypoint table

@@ -724,24 +724,38 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
 // greater than all 8 (A.3).
 // One wave per (cell, frame), lane = window column (windows are < 64 wide),
 // each row's 8 neighbours from the rows above / below and DPP lane shifts.
+// Survivors are appended to the (frame, level) candidate list -- one 32-bit
+// entry (x, y relative to the octree region, response) each, a block of the
+// list reserved per cell with one atomic (r06: the list replaces the
+// candidate plane, its summed-area table and the per-node plane scans; the
+// consumers, node counts and per-node maxima, do not depend on list order).
 // ---------------------------------------------------------------------------
 // rows loaded per round trip, the next chunk prefetched while one is swept
 // (r06: a whole 40-row window per round trip, 61 VGPRs, made the step 4 %
 // slower, profiles/r06/ab_nms_sat.txt)
 constexpr int kNmsRows = 8;
+// a candidate: .x = x | y << 11 | response << 21 (x < 2048, y < 1024 relative to
+// the octree region), .y = its rank in the reference's candidate order
+// (cell-row-major, raster within a cell; the node maximum's tie-break)
+__device__ __forceinline__ uint2 orb_cand_pack(int x, int y, int resp, const OrbLevelDev& lv) {
+    const unsigned ci = (unsigned)(y - 3) / (unsigned)lv.hCell, cj = (unsigned)(x - 3) / (unsigned)lv.wCell;
+    const unsigned key = ((ci * (unsigned)lv.nCols + cj) * (unsigned)lv.rh + (unsigned)y) * (unsigned)lv.rw + (unsigned)x;
+    return make_uint2((uint32_t)x | (uint32_t)y << 11 | (uint32_t)resp << 21, key);
+}
 __device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, const OrbLevelDev* __restrict__ lvs,
-                                             const uint8_t* __restrict__ score, uint8_t* __restrict__ cand, int t1,
-                                             int t2) {
-    const OrbLevelDev& L = lvs[c.level];
-    const int ww = c.x1 - c.x0, wh = c.y1 - c.y0, w = L.bpitch;
+                                             const uint8_t* __restrict__ score, uint2* __restrict__ clist,
+                                             int listFrame, int* __restrict__ ccount, int L, int* __restrict__ err,
+                                             int t1, int t2) {
+    const OrbLevelDev& Lv = lvs[c.level];
+    const int ww = c.x1 - c.x0, wh = c.y1 - c.y0, w = Lv.bpitch;
     const int lane = threadIdx.x;
     const bool incol = lane < ww;
-    const size_t base = L.boff + (size_t)f * L.bplane + (size_t)c.y0 * w + c.x0 + lane;
+    const size_t base = Lv.boff + (size_t)f * Lv.bplane + (size_t)c.y0 * w + c.x0 + lane;
     const uint8_t* S = score + base;
     // Register streaming, no LDS: rows come straight from the score plane,
     // eight in flight (the next chunk is loaded while this one is swept), so
     // the kernel occupies no LDS next to the region-growing waves it runs
-    // with; survivors are re-read from the (L2-resident) plane when written.
+    // with; survivors' responses are re-read from the (L2-resident) plane.
     unsigned long long ka = 0, kb = 0;
     auto ld = [&](int r) -> int { return (incol && r < wh) ? (int)S[(size_t)r * w] : 0; };
     {
@@ -783,140 +797,55 @@ __device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, co
         }
     }
     const unsigned long long keep = __ballot(ka != 0ull) != 0ull ? ka : kb;
-    if (!incol) return;
-    uint8_t* C = cand + base;
-    for (unsigned long long kk = keep; kk; kk &= kk - 1) {
+    // reserve the cell's block of the list: wave prefix of the per-lane counts
+    const int nk = incol ? __popcll(keep) : 0;
+    int pre = nk;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(pre, o);
+        if (lane >= o) pre += t;
+    }
+    const int tot = __shfl(pre, 63);
+    if (tot == 0) return;
+    int b0 = 0;
+    if (lane == 0) b0 = atomicAdd(ccount + (size_t)f * L + c.level, tot);
+    b0 = __shfl(b0, 0);
+    if (lane == 0 && b0 + tot > Lv.listCap) atomicOr(err + f, 1);  // cannot happen: listCap bounds the survivors
+    int pos = b0 + pre - nk;
+    uint2* out = clist + (size_t)f * listFrame + Lv.listOff;
+    const int xr = c.x0 + lane - Lv.minB, yr0 = c.y0 - Lv.minB;
+    for (unsigned long long kk = keep; incol && kk; kk &= kk - 1, ++pos) {
         const int r = __ffsll((long long)kk) - 1;
-        C[(size_t)r * w] = S[(size_t)r * w];
+        if (pos < Lv.listCap) out[pos] = orb_cand_pack(xr, yr0 + r, S[(size_t)r * w], Lv);
     }
 }
-
-#ifndef PLVI_NMS_CELLS
-#define PLVI_NMS_CELLS 1
-#endif
-constexpr int kNmsCells = PLVI_NMS_CELLS;  // cells per wave (the launch grid's x extent is ncells / kNmsCells)
 
 __global__ __launch_bounds__(64) void orb_cell_nms_kernel(const OrbCellDev* __restrict__ cells, int ncells,
                                                           const OrbLevelDev* __restrict__ lvs,
                                                           const uint8_t* __restrict__ score,
-                                                          uint8_t* __restrict__ cand, int t1, int t2) {
+                                                          uint2* __restrict__ clist, int listFrame,
+                                                          int* __restrict__ ccount, int L, int* __restrict__ err,
+                                                          int t1, int t2) {
     PLVI_ORB_PRIO_SET();
     const int f = blockIdx.y;
-    for (int ci = blockIdx.x; ci < ncells; ci += gridDim.x) orb_nms_cell(cells[ci], f, lvs, score, cand, t1, t2);
+    for (int ci = blockIdx.x; ci < ncells; ci += gridDim.x)
+        orb_nms_cell(cells[ci], f, lvs, score, clist, listFrame, ccount, L, err, t1, t2);
 }
 
 // ---------------------------------------------------------------------------
-// K3: summed-area table of the candidate indicator over each level's octree
-// region [minB, minB+rw) x [minB, minB+rh): SAT(x, y) = #candidates in
-// [0,x) x [0,y) (relative coords), x in [0, rw], y in [0, rh].  Stored per
-// 64-column strip s: SAT(64s + j, y) = Carry(s, y) + Local(s, j, y), Local
-// the strip's own counts (< 64 * rh < 2^16: ushort), Carry(s, y) the
-// candidates of the strips left of s.  One pass: read the candidate bytes
-// once, write 2 B per pixel (the two-pass int32 table moved 13 B per pixel).
-// ---------------------------------------------------------------------------
-#ifndef PLVI_SAT_ROWS
-#define PLVI_SAT_ROWS 8
-#endif
-constexpr int kSatRowsPerWave = PLVI_SAT_ROWS;  // rows whose loads are in flight together
-
-// Rows top-down, 8 rows' loads in flight; per row ballots give the prefix
-// counts (v_mbcnt) and the row total (popcount) without any cross-lane scan;
-// running column sums.  Four columns per lane: one wave covers four 64-column
-// strips (lanes 16g..16g+15 = strip 4w+g), one dword load per row and lane,
-// the strip-local prefix counts from four ballots masked to the lane's
-// 16-lane group, the four ushort entries of a lane stored as one 8-byte
-// store.  A quarter of the waves and load / store instructions.
-__global__ __launch_bounds__(64) void orb_sat_quad_kernel(const OrbLevelDev* __restrict__ lvs,
-                                                          const uint8_t* __restrict__ cand,
-                                                          unsigned short* __restrict__ lsat, int* __restrict__ carry) {
-    PLVI_ORB_PRIO_SET();
-    const int w = blockIdx.x, l = blockIdx.y, f = blockIdx.z;
-    const OrbLevelDev& L = lvs[l];
-    const int nS = L.satStrips;
-    if (4 * w >= nS) return;
-    const int lane = threadIdx.x, g = lane >> 4, s = 4 * w + g, xb = 256 * w + 4 * lane, pitch = 64 * nS;
-    const bool live = s < nS;
-    unsigned short* base = lsat + L.satOff + (size_t)f * L.satPlane;
-    int* T = carry + L.carryOff + (size_t)f * L.carryPlane;
-    const uint8_t* C0 = cand + L.boff + (size_t)f * L.bplane + (size_t)L.minB * L.bpitch + L.minB;
-    if (live) *reinterpret_cast<unsigned long long*>(base + xb) = 0ull;
-    if (live && (lane & 15) == 0) T[s + 1] = 0;
-    const unsigned long long below = ((1ull << lane) - 1ull) & ~((1ull << (16 * g)) - 1ull);
-    const unsigned long long group = 0xffffull << (16 * g);
-    const bool full = xb + 4 <= L.rw;
-    unsigned acc[4] = {0u, 0u, 0u, 0u};
-    int tot = 0;
-    for (int y0 = 1; y0 <= L.rh; y0 += kSatRowsPerWave) {
-        uint32_t v[kSatRowsPerWave];
-#pragma unroll
-        for (int k = 0; k < kSatRowsPerWave; ++k) {
-            const int y = y0 + k;  // SAT row y counts image row y-1 of the region
-            uint32_t u = 0u;
-            if (y <= L.rh && live && xb < L.rw) {
-                const uint8_t* r = C0 + (size_t)(y - 1) * L.bpitch + xb;
-                if (full) {
-                    u = ld_u32(r);
-                } else {
-                    for (int j = 0; j < 4; ++j)
-                        if (xb + j < L.rw) u |= (uint32_t)r[j] << (8 * j);
-                }
-            }
-            v[k] = u;
-        }
-#pragma unroll
-        for (int k = 0; k < kSatRowsPerWave; ++k) {
-            const uint32_t u = v[k];
-            const bool i0 = (u & 0xffu) != 0u, i1 = (u & 0xff00u) != 0u, i2 = (u & 0xff0000u) != 0u,
-                       i3 = (u & 0xff000000u) != 0u;
-            const unsigned long long m0 = __ballot(i0), m1 = __ballot(i1), m2 = __ballot(i2), m3 = __ballot(i3);
-            const unsigned cb = (unsigned)(__popcll(m0 & below) + __popcll(m1 & below) + __popcll(m2 & below) +
-                                           __popcll(m3 & below));
-            acc[0] += cb;
-            acc[1] += cb + (i0 ? 1u : 0u);
-            acc[2] += cb + (i0 ? 1u : 0u) + (i1 ? 1u : 0u);
-            acc[3] += cb + (i0 ? 1u : 0u) + (i1 ? 1u : 0u) + (i2 ? 1u : 0u);
-            tot += __popcll(m0 & group) + __popcll(m1 & group) + __popcll(m2 & group) + __popcll(m3 & group);
-            const int y = y0 + k;
-            if (y <= L.rh && live) {
-                const unsigned long long e = (unsigned long long)(acc[0] & 0xffffu) |
-                                             (unsigned long long)(acc[1] & 0xffffu) << 16 |
-                                             (unsigned long long)(acc[2] & 0xffffu) << 32 |
-                                             (unsigned long long)(acc[3] & 0xffffu) << 48;
-                *reinterpret_cast<unsigned long long*>(base + (size_t)y * pitch + xb) = e;
-                if ((lane & 15) == 0) T[(size_t)y * (nS + 1) + s + 1] = tot;
-            }
-        }
-    }
-}
-
-// Carry(s, y) = sum of the strip totals left of s (in place), one thread per row.
-__global__ __launch_bounds__(256) void orb_sat_carry_kernel(const OrbLevelDev* __restrict__ lvs,
-                                                            int* __restrict__ carry) {
-    const int l = blockIdx.y, f = blockIdx.z;
-    const OrbLevelDev& L = lvs[l];
-    const int y = blockIdx.x * 256 + threadIdx.x;
-    if (y > L.rh) return;
-    const int nS = L.satStrips;
-    int* row = carry + L.carryOff + (size_t)f * L.carryPlane + (size_t)y * (nS + 1);
-    // row[k] (k >= 1) holds strip k-1's total; Carry(s) = row[1] + ... + row[s]
-    int acc = 0;
-    row[0] = 0;
-    for (int k = 1; k <= nS; ++k) {
-        acc += row[k];
-        row[k] = acc;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// K4: ORBextractor::DistributeOctTree (ORBextractor.cc:537-761) as a list
-// emulation over node rectangles.  A node's key set is the set of candidates
-// inside its membership rectangle, so DivideNode's vKeys copies are replaced
-// by O(1) SAT counts; the std::list order (children pushed to the FRONT in
-// n1..n4 order, parent erased), the bNoMore flags, both termination tests
-// and the phase-2 (size, node*) sort are reproduced exactly, with the
-// canonical creation-order tie-break of SURVEY.md B.1.
-// One wave per (level, frame); lane 0 runs the list algorithm.
-// Output: per node (list order) its membership rectangle.
+// K3: ORBextractor::DistributeOctTree (ORBextractor.cc:537-761) as a list
+// emulation over node rectangles, then "retain the best point in each node"
+// (:739-758).  A node's key set is the set of candidates inside its
+// membership rectangle, so DivideNode's vKeys copies are replaced by counts
+// over the (frame, level) candidate list; the std::list order (children
+// pushed to the FRONT in n1..n4 order, parent erased), the bNoMore flags,
+// both termination tests and the phase-2 (size, node*) sort are reproduced
+// exactly, with the canonical creation-order tie-break of SURVEY.md B.1.
+// Each final node keeps its maximum-response candidate, ties to the first in
+// the reference's candidate order (cell-row-major, raster within a cell: a
+// key of the coordinates).  One wave per (level, frame); the list emulation
+// runs in lockstep on every lane, the counts and maxima over the candidates
+// with the whole wave.  Output: the level keypoints in node list order.
 // ---------------------------------------------------------------------------
 struct OctNodes {
     short *gx0, *gy0, *gx1, *gy1;  // geometry UL=(gx0,gy0) BR=(gx1,gy1)
@@ -925,18 +854,20 @@ struct OctNodes {
     short *nxt, *prv, *freel;
     short *vsz, *vprev, *todo;
     int* ccnt;                     // [C][4] key counts of the four children (prefetched)
+    int* beg;                      // [C] first entry of the node's range in the partitioned list
+    int* cbeg;                     // [C][4] first entries of the four children's ranges
     unsigned char* nomore;
 };
+constexpr int kOctListLds = 1536;  // candidates of a (frame, level) staged in LDS (more: read from the list in memory)
+// dynamic LDS of orb_octree_kernel: the node arrays, then the staged candidates
+__host__ __device__ inline size_t orb_octree_lds_nodes(int nodeCap) { return ((size_t)nodeCap * (11 * 4 + 14 * 2 + 1) + 15) & ~(size_t)15; }
+__host__ __device__ inline size_t orb_octree_lds(int nodeCap, int lcap) { return orb_octree_lds_nodes(nodeCap) + 8 * (size_t)lcap; }
 
-// The whole wave executes the list algorithm in lockstep (identical values in
-// every lane, identical LDS writes), so that the SAT counts of every split a
-// phase will perform are gathered first by all lanes in parallel: the
-// children of a node depend only on the node, not on the list order.
 __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __restrict__ lvs,
-                                                        const unsigned short* __restrict__ lsat,
-                                                        const int* __restrict__ carry, short4* __restrict__ out_rect,
-                                                        int* __restrict__ out_cnt, int nodeCapMax, int L,
-                                                        int* __restrict__ err, uint8_t* __restrict__ cand) {
+                                                        const uint2* __restrict__ clist, int listFrame,
+                                                        const int* __restrict__ ccount, float4* __restrict__ lvkp,
+                                                        int kpCapFrame, int* __restrict__ out_cnt, int nodeCapMax,
+                                                        int L, int* __restrict__ err, int lcap) {
     PLVI_ORB_PRIO_SET();
     extern __shared__ __align__(16) unsigned char smem[];
     // blocks are dealt round-robin over the 8 XCDs: with l = blockIdx.x every
@@ -946,58 +877,114 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
     const OrbLevelDev& lv = lvs[l];
     const int C = nodeCapMax;
     OctNodes n;
+    uint2* lcache;
     {
         int* ip = reinterpret_cast<int*>(smem);
         n.cnt = ip; ip += C;
         n.seq = ip; ip += C;
         n.ccnt = ip; ip += 4 * C;
+        n.beg = ip; ip += C;
+        n.cbeg = ip; ip += 4 * C;
         short* sp = reinterpret_cast<short*>(ip);
         n.gx0 = sp; sp += C; n.gy0 = sp; sp += C; n.gx1 = sp; sp += C; n.gy1 = sp; sp += C;
         n.mx0 = sp; sp += C; n.my0 = sp; sp += C; n.mx1 = sp; sp += C; n.my1 = sp; sp += C;
         n.nxt = sp; sp += C; n.prv = sp; sp += C; n.freel = sp; sp += C;
         n.vsz = sp; sp += C; n.vprev = sp; sp += C; n.todo = sp; sp += C;
         n.nomore = reinterpret_cast<unsigned char*>(sp);
+        lcache = reinterpret_cast<uint2*>(smem + orb_octree_lds_nodes(C));
     }
-    const unsigned short* S = lsat + lv.satOff + (size_t)f * lv.satPlane;
-    const int* T = carry + lv.carryOff + (size_t)f * lv.carryPlane;
-    const int st = 64 * lv.satStrips, ct = lv.satStrips + 1, RW = lv.rw, RH = lv.rh;
-    auto sat_raw = [&](int x, int y) -> int { return T[y * ct + (x >> 6)] + (int)S[y * st + x]; };
-    auto sat_at = [&](int x, int y) -> int {
-        x = max(0, min(x, RW));
-        y = max(0, min(y, RH));
-        return sat_raw(x, y);
+    const int RW = lv.rw, RH = lv.rh;
+    // the level's candidates: in LDS when they fit (the usual case), else read from memory
+    const int K = min(ccount[(size_t)f * L + l], lv.listCap);
+    const uint2* G = clist + (size_t)f * listFrame + lv.listOff;
+    const bool inLds = K <= lcap;
+    // In LDS the candidates are kept partitioned like the reference's vKeys
+    // (ORBextractor.cc:616-641 hands each child its own keys): every node owns
+    // a range [beg, beg + cnt) of A, children are split off stably (T is the
+    // scatter buffer), so a node's counts read only its own range.  The key
+    // (candidate order) is recomputed from (x, y) where it is needed.
+    uint32_t* A = reinterpret_cast<uint32_t*>(lcache);
+    uint32_t* T = A + lcap;
+    if (inLds)
+        for (int i = lane; i < K; i += 64) A[i] = G[i].x;
+    wave_sync();
+    // stable split of [b, b + m) into groups 0..ng-1 (ng <= 8) of cls(entry);
+    // group counts to cnt[], group starts to st[] (LDS)
+    auto partition = [&](int b, int m, int ng, auto cls, int* cnt, int* st) {
+        int c[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) c[q] = 0;
+        for (int j = 0; j < m; j += 64) {
+            const int g = j + lane < m ? cls(A[b + j + lane]) : -1;
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (q < ng) c[q] += __popcll(__ballot(g == q));
+        }
+        int o[8], acc = b;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            o[q] = acc;
+            if (q < ng) { cnt[q] = c[q]; st[q] = acc; acc += c[q]; }
+        }
+        for (int j = 0; j < m; j += 64) {
+            const uint32_t e = j + lane < m ? A[b + j + lane] : 0u;
+            const int g = j + lane < m ? cls(e) : -1;
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (q < ng) {
+                    const unsigned long long bal = __ballot(g == q);
+                    if (g == q) T[o[q] + orb_mbcnt(bal)] = e;
+                    o[q] += __popcll(bal);
+                }
+        }
+        wave_sync();
+        for (int j = b + lane; j < acc; j += 64) A[j] = T[j];
+        wave_sync();
     };
+    // candidates in [x0, x1) x [y0, y1), with the whole wave
     auto count = [&](int x0, int y0, int x1, int y1) -> int {
-        x0 = max(0, min(x0, RW)); x1 = max(0, min(x1, RW));
-        y0 = max(0, min(y0, RH)); y1 = max(0, min(y1, RH));
-        if (x0 >= x1 || y0 >= y1) return 0;
-        return sat_raw(x1, y1) - sat_raw(x1, y0) - sat_raw(x0, y1) + sat_raw(x0, y0);
+        int c = 0;
+        for (int b = 0; b < K; b += 64) {
+            const int i = b + lane;
+            const uint32_t e = i < K ? G[i].x : 0xFFFFFFFFu;
+            const int x = (int)(e & 2047u), y = (int)((e >> 11) & 1023u);
+            c += __popcll(__ballot(i < K && x >= x0 && x < x1 && y >= y0 && y < y1));
+        }
+        return c;
     };
-    // children counts of nodes ids[0..k): lanes in parallel, 16 SAT loads each in flight
+    // the four children's counts of nodes ids[0..k): every candidate chunk
+    // against each node, one ballot per child
     auto prefetch = [&](const short* ids, int k) {
         wave_sync();  // one wave per block
-        for (int i = lane; i < k; i += 64) {
-            const int p = ids[i];
+        for (int t = 0; t < k; ++t) {
+            const int p = ids[t];
             const int x0 = n.gx0[p], y0 = n.gy0[p], x1 = n.gx1[p], y1 = n.gy1[p];
             const int midX = x0 + (int)ceilf((float)(x1 - x0) / 2), midY = y0 + (int)ceilf((float)(y1 - y0) / 2);
-            const int mx0 = n.mx0[p], my0 = n.my0[p], mx1 = n.mx1[p], my1 = n.my1[p];
-            const int xs[4] = {mx0, min(mx1, midX), max(mx0, midX), mx1};
-            const int ys[4] = {my0, min(my1, midY), max(my0, midY), my1};
-            int v[4][4];
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-                for (int b = 0; b < 4; ++b) v[a][b] = sat_at(xs[b], ys[a]);
-            // child q: x range (xs[0],xs[1]) or (xs[2],xs[3]); y range likewise
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int xa = (q & 1) ? 2 : 0, ya = (q & 2) ? 2 : 0;
-                const int cx0 = max(0, min(xs[xa], RW)), cx1 = max(0, min(xs[xa + 1], RW));
-                const int cy0 = max(0, min(ys[ya], RH)), cy1 = max(0, min(ys[ya + 1], RH));
-                n.ccnt[4 * p + q] = (cx0 >= cx1 || cy0 >= cy1)
-                                        ? 0
-                                        : v[ya + 1][xa + 1] - v[ya][xa + 1] - v[ya + 1][xa] + v[ya][xa];
+            if (inLds) {
+                // the node's range holds exactly its members: quadrant = (x >= midX) + 2 (y >= midY)
+                partition(n.beg[p], n.cnt[p], 4, [&](uint32_t e) {
+                    return (int)((e & 2047u) >= (unsigned)midX) + 2 * (int)(((e >> 11) & 1023u) >= (unsigned)midY);
+                }, n.ccnt + 4 * p, n.cbeg + 4 * p);
+                continue;
             }
+            const int mx0 = n.mx0[p], my0 = n.my0[p], mx1 = n.mx1[p], my1 = n.my1[p];
+            const int xa = min(mx1, midX), xb = max(mx0, midX), ya = min(my1, midY), yb = max(my0, midY);
+            int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+            for (int b = 0; b < K; b += 64) {
+                const int i = b + lane;
+                const uint32_t e = i < K ? G[i].x : 0xFFFFFFFFu;
+                const int x = (int)(e & 2047u), y = (int)((e >> 11) & 1023u);
+                const bool in = i < K && x >= mx0 && x < mx1 && y >= my0 && y < my1;
+                const bool left = x < xa, right = x >= xb, top = y < ya, bottom = y >= yb;
+                c0 += __popcll(__ballot(in && left && top));
+                c1 += __popcll(__ballot(in && right && top));
+                c2 += __popcll(__ballot(in && left && bottom));
+                c3 += __popcll(__ballot(in && right && bottom));
+            }
+            n.ccnt[4 * p + 0] = c0;
+            n.ccnt[4 * p + 1] = c1;
+            n.ccnt[4 * p + 2] = c2;
+            n.ccnt[4 * p + 3] = c3;
         }
         wave_sync();
     };
@@ -1024,14 +1011,26 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
         ++size;
     };
     // Initial nodes (ORBextractor.cc:541-583): push_back in order; empty erased.
+    // Partitioned: the roots' counts and starts are staged in ccnt / cbeg
+    // (free until the first prefetch).
+    if (inLds)
+        partition(0, K, lv.nIni, [&](uint32_t e) {
+            const int x = (int)(e & 2047u);
+            int g = -1;
+#pragma unroll
+            for (int q = 0; q < kOrbMaxRoots; ++q)
+                if (q < lv.nIni && x >= lv.rootB[q] && x < lv.rootB[q + 1]) g = q;
+            return g;
+        }, n.ccnt, n.cbeg);
     for (int i = 0; i < lv.nIni; ++i) {
-        const int c = count(lv.rootB[i], 0, lv.rootB[i + 1], RH);
+        const int c = inLds ? n.ccnt[i] : count(lv.rootB[i], 0, lv.rootB[i + 1], RH);
+        const int rb = inLds ? n.cbeg[i] : 0;
         if (c == 0) continue;
         const int k = alloc();
         if (k < 0) break;
         n.gx0[k] = (short)lv.rootGx[i]; n.gy0[k] = 0; n.gx1[k] = (short)lv.rootGx[i + 1]; n.gy1[k] = (short)RH;
         n.mx0[k] = (short)lv.rootB[i]; n.my0[k] = 0; n.mx1[k] = (short)lv.rootB[i + 1]; n.my1[k] = (short)RH;
-        n.cnt[k] = c; n.seq[k] = seqc++; n.nomore[k] = (c == 1);
+        n.cnt[k] = c; n.seq[k] = seqc++; n.nomore[k] = (c == 1); n.beg[k] = rb;
         n.prv[k] = (short)tail; n.nxt[k] = -1;
         if (tail >= 0) n.nxt[tail] = (short)k; else head = k;
         tail = k;
@@ -1059,7 +1058,7 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
             if (k < 0) return;
             n.gx0[k] = (short)cx0; n.gy0[k] = (short)cy0; n.gx1[k] = (short)cx1; n.gy1[k] = (short)cy1;
             n.mx0[k] = (short)bx0; n.my0[k] = (short)by0; n.mx1[k] = (short)bx1; n.my1[k] = (short)by1;
-            n.cnt[k] = c; n.seq[k] = seqc++; n.nomore[k] = (c == 1);
+            n.cnt[k] = c; n.seq[k] = seqc++; n.nomore[k] = (c == 1); n.beg[k] = n.cbeg[4 * p + q];
             push_front(k);
             if (c > 1) {
                 if (nToExpand) ++*nToExpand;
@@ -1136,114 +1135,74 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
             }
         }
     }
-    short4* R = out_rect + ((size_t)f * L + l) * nodeCapMax;
+    // "Retain the best point in each node" (ORBextractor.cc:739-758): lane
+    // j keeps the maximum of (response, first in candidate order) over nodes
+    // j, j + 64, ... of the list; every candidate is read once per 64 nodes
     int cntOut = 0;
     if (!overflow) {
-        for (int it = head; it >= 0 && cntOut < lv.nodeCap; it = n.nxt[it]) {
-            if (lane == 0) R[cntOut] = make_short4(n.mx0[it], n.my0[it], n.mx1[it], n.my1[it]);
-            ++cntOut;
-        }
+        for (int it = head; it >= 0 && cntOut < lv.nodeCap; it = n.nxt[it]) n.todo[cntOut++] = (short)it;
         if (size > lv.nodeCap) overflow = true;
+    }
+    wave_sync();
+    if (!overflow && inLds) {
+        // lane j: node j's own range (the key -- candidate order -- from (x, y))
+        float4* out = lvkp + (size_t)f * kpCapFrame + lv.kpOff;
+        for (int j = lane; j < cntOut; j += 64) {
+            const int p = n.todo[j];
+            const int b = n.beg[p], m = n.cnt[p];
+            unsigned long long best = 0;
+            for (int i = b; i < b + m; ++i) {
+                const uint32_t e = A[i];
+                const int x = (int)(e & 2047u), y = (int)((e >> 11) & 1023u), resp = (int)(e >> 21);
+                const unsigned key = orb_cand_pack(x, y, 0, lv).y;
+                const unsigned long long pk = ((unsigned long long)resp << 32) | (0xFFFFFFFFu - key);
+                if (pk > best) best = pk;
+            }
+            const unsigned key = 0xFFFFFFFFu - (unsigned)(best & 0xFFFFFFFFu);
+            const unsigned xx = key % (unsigned)RW;
+            const unsigned yy = (key / (unsigned)RW) % (unsigned)RH;
+            out[j] = make_float4((float)(xx + lv.minB), (float)(yy + lv.minB), (float)(best >> 32), 0.f);
+        }
+    } else if (!overflow) {
+        float4* out = lvkp + (size_t)f * kpCapFrame + lv.kpOff;
+        for (int j0 = 0; j0 < cntOut; j0 += 4 * 64) {
+            // nodes j0 + lane + 64 k, k < 4, in registers; one pass over the candidates
+            int bx0[4], by0[4], bx1[4], by1[4];
+            unsigned long long best[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int j = j0 + lane + 64 * k;
+                bx0[k] = by0[k] = bx1[k] = by1[k] = 0;
+                best[k] = 0;
+                if (j < cntOut) {
+                    const int p = n.todo[j];
+                    bx0[k] = n.mx0[p]; by0[k] = n.my0[p]; bx1[k] = n.mx1[p]; by1[k] = n.my1[p];
+                }
+            }
+            for (int i = 0; i < K; ++i) {
+                const uint2 e2 = G[i];
+                const uint32_t e = e2.x;
+                const int x = (int)(e & 2047u), y = (int)((e >> 11) & 1023u), resp = (int)(e >> 21);
+                const unsigned long long pk = ((unsigned long long)resp << 32) | (0xFFFFFFFFu - e2.y);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (x >= bx0[k] && x < bx1[k] && y >= by0[k] && y < by1[k] && pk > best[k]) best[k] = pk;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int j = j0 + lane + 64 * k;
+                if (j < cntOut) {
+                    const unsigned key = 0xFFFFFFFFu - (unsigned)(best[k] & 0xFFFFFFFFu);
+                    const unsigned xx = key % (unsigned)RW;
+                    const unsigned yy = (key / (unsigned)RW) % (unsigned)RH;
+                    out[j] = make_float4((float)(xx + lv.minB), (float)(yy + lv.minB), (float)(best[k] >> 32), 0.f);
+                }
+            }
+        }
     }
     if (lane == 0) {
         out_cnt[(size_t)f * L + l] = overflow ? 0 : cntOut;
         if (overflow) atomicOr(err + f, 1);
-    }
-    if (overflow) {
-        // no node list for orb_node_best_kernel to clear from: zero the region here
-        uint8_t* Cm = cand + lv.boff + (size_t)f * lv.bplane + (size_t)lv.minB * lv.bpitch + lv.minB;
-        for (int y = 0; y < RH; ++y)
-            for (int x = lane; x < RW; x += 64) Cm[(size_t)y * lv.bpitch + x] = 0;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// K5: "Retain the best point in each node" (ORBextractor.cc:739-758): max
-// response, ties -> first in the candidate list order (cell-row-major,
-// raster within a cell).  One wave per (node, level, frame).  Output level
-// keypoint (x, y, response) in level coordinates.
-// ---------------------------------------------------------------------------
-#ifndef PLVI_BEST_NODES
-#define PLVI_BEST_NODES 1
-#endif
-constexpr int kBestNodes = PLVI_BEST_NODES;  // nodes per wave (the grid's x extent is nodeCapMax / kBestNodes)
-#ifndef PLVI_BEST_BATCH
-#define PLVI_BEST_BATCH 8
-#endif
-constexpr int kBestBatch = PLVI_BEST_BATCH;  // 64-pixel steps of a node rectangle loaded per round trip
-
-__device__ __forceinline__ void orb_node_best_one(const OrbLevelDev& lv, uint8_t* __restrict__ Cm, const short4 r,
-                                                  float4* __restrict__ out);
-
-__global__ __launch_bounds__(64) void orb_node_best_kernel(const OrbLevelDev* __restrict__ lvs,
-                                                           uint8_t* __restrict__ cand,
-                                                           const short4* __restrict__ rects,
-                                                           const int* __restrict__ rect_cnt, int nodeCapMax, int L,
-                                                           float4* __restrict__ lvkp, int kpCapFrame) {
-    PLVI_ORB_PRIO_SET();
-    const int l = blockIdx.y, f = blockIdx.z;
-    const int ncnt = rect_cnt[(size_t)f * L + l];
-    const OrbLevelDev& lv = lvs[l];
-    uint8_t* Cm = cand + lv.boff + (size_t)f * lv.bplane;
-    for (int k = 0; k < kBestNodes; ++k) {
-        const int node = blockIdx.x * kBestNodes + k;
-        if (node >= ncnt) return;
-        orb_node_best_one(lv, Cm, rects[((size_t)f * L + l) * nodeCapMax + node],
-                          lvkp + (size_t)f * kpCapFrame + lv.kpOff + node);
-    }
-}
-
-__device__ __forceinline__ void orb_node_best_one(const OrbLevelDev& lv, uint8_t* __restrict__ Cm, const short4 r,
-                                                  float4* __restrict__ out) {
-    const int lane = threadIdx.x;
-    const int rx0 = r.x, ry0 = r.y, rx1 = r.z, ry1 = r.w;
-    const int wdt = rx1 - rx0;
-    unsigned long long best = 0;
-    const int total = wdt * (ry1 - ry0);
-    // i = lane + 64 t walks the rectangle row-major; (yy, xx) advance by
-    // 64 = q rows + rr columns per step (no division in the loop)
-    const int wd = max(wdt, 1);  // (an empty rectangle has total 0)
-    const int q = 64 / wd, rr = 64 - q * wd;
-    int yy = ry0 + lane / wd, xx = rx0 + lane % wd;
-    uint8_t* const base = Cm + (size_t)lv.minB * lv.bpitch + lv.minB;
-    // kBestBatch steps of 64 pixels per round trip: every load of a batch is
-    // issued before any candidate is consumed (the consuming store would
-    // otherwise order each step's load behind the previous step's store)
-    for (int i0 = lane; i0 < total; i0 += 64 * kBestBatch) {
-        int off[kBestBatch], rv[kBestBatch];
-#pragma unroll
-        for (int k = 0; k < kBestBatch; ++k) {
-            if (xx >= rx1) {
-                xx -= wdt;
-                ++yy;
-            }
-            off[k] = yy * lv.bpitch + xx;
-            yy += q;
-            xx += rr;
-        }
-#pragma unroll
-        for (int k = 0; k < kBestBatch; ++k) rv[k] = i0 + 64 * k < total ? (int)base[off[k]] : 0;
-#pragma unroll
-        for (int k = 0; k < kBestBatch; ++k) {
-            const int resp = rv[k];
-            if (!resp) continue;
-            base[off[k]] = 0;  // consumed: the next batch's NMS finds the plane zero
-            const unsigned ys = (unsigned)off[k] / (unsigned)lv.bpitch, xs = (unsigned)off[k] - ys * (unsigned)lv.bpitch;
-            const unsigned ci = (ys - 3u) / (unsigned)lv.hCell, cj = (xs - 3u) / (unsigned)lv.wCell;
-            const unsigned key = ((ci * (unsigned)lv.nCols + cj) * (unsigned)lv.rh + ys) * (unsigned)lv.rw + xs;
-            const unsigned long long pk = ((unsigned long long)resp << 32) | (0xFFFFFFFFu - key);
-            best = pk > best ? pk : best;
-        }
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long other = __shfl_xor(best, o);
-        best = other > best ? other : best;
-    }
-    if (lane == 0) {
-        const unsigned key = 0xFFFFFFFFu - (unsigned)(best & 0xFFFFFFFFu);
-        const unsigned xx = key % (unsigned)lv.rw;
-        const unsigned yy = (key / (unsigned)lv.rw) % (unsigned)lv.rh;
-        *out = make_float4((float)(xx + lv.minB), (float)(yy + lv.minB), (float)(best >> 32), 0.f);
     }
 }
 

@@ -88,13 +88,15 @@ struct OrbPipeline {
     int taps[7]{};
     int resizeGeneric = 0;  // A.1 vertical-pass switch (PLVI_COMPAT_RESIZE_V_GENERIC)
     int kpCapFrame = 0, nodeCapMax = 0;
-    size_t pyrBytesFrameTotal = 0, candBytesTotal = 0, satIntsFrameTotal = 0;
-    size_t lvOff0 = 0;  // (unused)
-    bool candDirty = false;  // survivors of an aborted run() may still be in the candidate plane
-    DevBuf d_lv, d_cells, d_strips, d_xtab, pyr, blur, score, cand, sat, carry, rects, rectCnt, lvkp, lvdesc, okp,
-        odesc, ocount, omono, err, staging;
+    size_t pyrBytesFrameTotal = 0, blurBytesTotal = 0;
+    int listFrame = 0, listMax = 0;  // NMS candidate lists: entries per frame, largest level
+    DevBuf d_lv, d_cells, d_strips, d_xtab, pyr, blur, score, clist, ccount, rectCnt, lvkp, lvdesc, okp, odesc, ocount,
+        omono, err, staging;
     size_t pyrSmem = 0;  // orb_pyramid_kernel LDS: column table + source-level row rings
     int xtabN = 0, pyrFrameLds = 0;
+    int octLcap = 0;      // candidates a (frame, level) octree wave stages in LDS
+    int octLdsMax = kOctListLds;  // PLVI_ORB_OCT_LDS (0: every level's octree scans its list in memory)
+    size_t octSmem = 0;   // orb_octree_kernel dynamic LDS
     // batches of at most this many frames build the pyramid level by level
     // (orb_resize_level_kernel, one launch per level) instead of streaming it
     // (PLVI_PYR_LEVELWISE overrides)
@@ -195,6 +197,7 @@ struct OrbPipeline {
         if (const char* e = getenv("PLVI_GROW_GATE")) gateStage = std::min(3, std::max(0, atoi(e)));
         if (const char* e = getenv("PLVI_PYR_LEVELWISE")) pyrLevelwiseMax = atoi(e);
         if (const char* e = getenv("PLVI_ORB_L0_COPY")) l0forceCopy = atoi(e) != 0;
+        if (const char* e = getenv("PLVI_ORB_OCT_LDS")) octLdsMax = std::max(0, std::min(kOctListLds, atoi(e)));
         PLVI_CHECK(hipSetDevice(device));
         {
             // the handle's own stream (single-frame calls, batches without a
@@ -247,7 +250,8 @@ struct OrbPipeline {
         resizeGeneric = (p->compat & PLVI_COMPAT_RESIZE_V_GENERIC) ? 1 : 0;
         // Levels
         lv.resize(L);
-        size_t off = 0, boffAll = 0, satOff = 0, carryOff = 0;
+        size_t off = 0, boffAll = 0;
+        long long listOff = 0;
         std::vector<uint32_t> xtab;
         int kpOff = 0;
         nodeCapMax = 0;
@@ -271,18 +275,13 @@ struct OrbPipeline {
             d.nCols = (int)(width / 30.f);
             d.nRows = (int)(height / 30.f);
             if (d.nCols <= 0 || d.nRows <= 0) return PLVI_E_BADARG;
+            // the node maximum's tie-break key (cell, row, column) must fit 32 bits
+            if ((double)d.nRows * d.nCols * d.rh * d.rw >= 4294967296.0) return PLVI_E_BADARG;
             d.wCell = (int)std::ceil(width / d.nCols);
             d.hCell = (int)std::ceil(height / d.nRows);
             if (d.wCell + 6 > kOrbCellMax || d.hCell + 6 > kOrbCellMax) return PLVI_E_BADARG;
-            // strip-local SAT (K3): Local counts < 64 * rh must fit a ushort
-            if (64LL * d.rh >= 65536) return PLVI_E_BADARG;
-            d.satStrips = d.rw / 64 + 1;  // covers SAT columns 0..rw
-            d.satPlane = (long long)(d.rh + 1) * 64 * d.satStrips;
-            d.satOff = (long long)satOff;
-            satOff += (size_t)d.satPlane * Bcap;
-            d.carryPlane = (long long)(d.rh + 1) * (d.satStrips + 1);
-            d.carryOff = (long long)carryOff;
-            carryOff += (size_t)d.carryPlane * Bcap;
+            // candidate entries pack x (11 bits) and y (10 bits) relative to the region
+            if (d.rw >= 2048 || d.rh >= 1024) return PLVI_E_BADARG;
             d.quota = quota[l];
             d.scale = scale[l];
             d.size = (float)(int)(31 * scale[l]);
@@ -319,7 +318,12 @@ struct OrbPipeline {
                     c.level = l;
                     c.x0 = (int)iniX + 3; c.y0 = (int)iniY + 3;
                     c.x1 = (int)maxX - 3; c.y1 = (int)maxY - 3;
-                    if (c.x1 > c.x0 && c.y1 > c.y0) cells.push_back(c);
+                    if (c.x1 > c.x0 && c.y1 > c.y0) {
+                        cells.push_back(c);
+                        // survivors are strict maxima over their 8 neighbours
+                        // inside the window: at most one per 2 x 2 block
+                        d.listCap += ((c.x1 - c.x0 + 1) / 2) * ((c.y1 - c.y0 + 1) / 2);
+                    }
                 }
             }
             // cv::resize scale from level l-1 (resize.cpp: scale_x = 1 / inv_scale_x)
@@ -351,8 +355,14 @@ struct OrbPipeline {
         }
         kpCapFrame = kpOff;
         pyrBytesFrameTotal = off;
-        candBytesTotal = boffAll;
-        satIntsFrameTotal = satOff;
+        blurBytesTotal = boffAll;
+        for (auto& d : lv) {
+            d.listOff = (int)listOff;
+            listOff += d.listCap;
+            listMax = std::max(listMax, d.listCap);
+        }
+        if (listOff >= (1LL << 31) / 8) return PLVI_E_BADARG;
+        listFrame = (int)listOff;
         // device tables
         if (d_lv.alloc(sizeof(OrbLevelDev) * L) || d_cells.alloc(sizeof(OrbCellDev) * cells.size()) ||
             d_strips.alloc(sizeof(OrbStripDev) * strips.size()))
@@ -369,15 +379,19 @@ struct OrbPipeline {
         PLVI_CHECK(hipMemcpy(d_xtab.p, xtab.data(), 4 * xtab.size(), hipMemcpyHostToDevice));
         PLVI_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax.data(), 16 * sizeof(int)));
         // work buffers
-        if (pyr.alloc(off) || blur.alloc(boffAll) || score.alloc(boffAll) || cand.alloc(boffAll) ||
-            sat.alloc(satOff * sizeof(unsigned short)) || carry.alloc(carryOff * sizeof(int)) || rects.alloc(sizeof(short4) * (size_t)nodeCapMax * L * Bcap) ||
+        if (pyr.alloc(off) || blur.alloc(boffAll) || score.alloc(boffAll) ||
+            clist.alloc(sizeof(uint2) * (size_t)listFrame * Bcap) || ccount.alloc(sizeof(int) * L * Bcap) ||
             rectCnt.alloc(sizeof(int) * L * Bcap) || lvkp.alloc(sizeof(float4) * (size_t)kpCapFrame * Bcap) ||
             lvdesc.alloc((size_t)32 * kpCapFrame * Bcap) || okp.alloc(sizeof(plvi_keypoint) * (size_t)kpCapFrame * Bcap) ||
             odesc.alloc((size_t)32 * kpCapFrame * Bcap) || ocount.alloc(sizeof(int) * Bcap) ||
             omono.alloc(sizeof(int) * Bcap) || err.alloc(sizeof(int) * Bcap) || staging.alloc((size_t)W * H))
             return PLVI_E_HIP;
         PLVI_CHECK(hipMemset(err.p, 0, sizeof(int) * Bcap));
-        PLVI_CHECK(hipMemset(cand.p, 0, cand.bytes));  // outside the detection windows it stays 0
+        octLcap = std::min(listMax, octLdsMax);
+        octSmem = orb_octree_lds(nodeCapMax, octLcap);
+        if (octSmem > 160 * 1024) return PLVI_E_BADARG;
+        PLVI_CHECK(hipFuncSetAttribute((const void*)orb_octree_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)octSmem));
         return PLVI_OK;
     }
 
@@ -394,14 +408,9 @@ struct OrbPipeline {
         const int t1 = std::max(0, std::min(prm.ini_th_fast, 255)), t2 = std::max(0, std::min(prm.min_th_fast, 255));
         uint8_t* P = pyr.as<uint8_t>();
         uint8_t* Bl = blur.as<uint8_t>();
-        uint8_t* Cd = cand.as<uint8_t>();
         uint8_t* Sc = score.as<uint8_t>();
-        // The candidate plane must be zero when the NMS writes its survivors:
-        // orb_node_best_kernel clears every candidate it reads (the octree
-        // kernel the region of a level that overflowed).  A run that returned
-        // between the two launches left survivors behind: clear it once.
-        if (candDirty) PLVI_CHECK(hipMemsetAsync(Cd, 0, candBytesTotal, st));
-        candDirty = false;
+        // the NMS appends to the (frame, level) candidate lists from zero
+        PLVI_CHECK(hipMemsetAsync(ccount.p, 0, sizeof(int) * (size_t)L * nf, st));
         mark(0, st);
         auto hook = [&](int k, hipStream_t s_) {
             if (evAfterBlur && gateStage == k) PLVI_CHECK(hipEventRecord(evAfterBlur, s_));
@@ -449,37 +458,22 @@ struct OrbPipeline {
         }
         if (const int hrc = hook(1, st)) return hrc;
         mark(1, st);
-        // K2 cell NMS -> candidate map: only survivors are written, onto the
-        // zero plane (no fill per launch: see candDirty above)
-        candDirty = true;
-        hipLaunchKernelGGL(orb_cell_nms_kernel, dim3((unsigned)((cells.size() + kNmsCells - 1) / kNmsCells), nf),
-                           dim3(64), 0, st, d_cells.as<OrbCellDev>(), (int)cells.size(), d_lv.as<OrbLevelDev>(),
-                           (const uint8_t*)Sc, Cd, t1, t2);
+        // K2 cell NMS -> the (frame, level) candidate lists
+        hipLaunchKernelGGL(orb_cell_nms_kernel, dim3((unsigned)cells.size(), nf), dim3(64), 0, st,
+                           d_cells.as<OrbCellDev>(), (int)cells.size(), d_lv.as<OrbLevelDev>(), (const uint8_t*)Sc,
+                           clist.as<uint2>(), listFrame, ccount.as<int>(), L, err.as<int>(), t1, t2);
         mark(2, st);
         if (const int hrc = hook(2, st)) return hrc;
-        // K3 SAT
-        int maxRh = 0, maxStrips = 0;
-        for (auto& d : lv) { maxRh = std::max(maxRh, d.rh); maxStrips = std::max(maxStrips, d.satStrips); }
-        hipLaunchKernelGGL(orb_sat_quad_kernel, dim3((maxStrips + 3) / 4, L, nf), dim3(64), 0, st,
-                           d_lv.as<OrbLevelDev>(), (const uint8_t*)Cd, sat.as<unsigned short>(), carry.as<int>());
-        hipLaunchKernelGGL(orb_sat_carry_kernel, dim3((maxRh + 1 + 255) / 256, L, nf), dim3(256), 0, st,
-                           d_lv.as<OrbLevelDev>(), carry.as<int>());
+        // (K3, the r01-r05 summed-area table of the candidate plane, is gone:
+        // stage 3 stays as an empty profiling slot)
         mark(3, st);
         if (const int hrc = hook(3, st)) return hrc;
-        // K4 octree
-        const size_t smem = (size_t)nodeCapMax * (6 * 4 + 14 * 2 + 1) + 16;
-        hipLaunchKernelGGL(orb_octree_kernel, dim3(L, nf), dim3(64), smem, st, d_lv.as<OrbLevelDev>(),
-                           (const unsigned short*)sat.as<unsigned short>(), (const int*)carry.as<int>(),
-                           rects.as<short4>(), rectCnt.as<int>(), nodeCapMax, L,
-                           err.as<int>(), Cd);
+        // K4 octree + the best candidate of every node (K5 in r01-r05)
+        hipLaunchKernelGGL(orb_octree_kernel, dim3(L, nf), dim3(64), octSmem, st, d_lv.as<OrbLevelDev>(),
+                           (const uint2*)clist.as<uint2>(), listFrame, (const int*)ccount.as<int>(), lvkp.as<float4>(),
+                           kpCapFrame, rectCnt.as<int>(), nodeCapMax, L, err.as<int>(), octLcap);
         mark(4, st);
         if (const int hrc = hook(4, st)) return hrc;
-        // K5 best per node
-        hipLaunchKernelGGL(orb_node_best_kernel, dim3((nodeCapMax + kBestNodes - 1) / kBestNodes, L, nf), dim3(64), 0, st,
-                           d_lv.as<OrbLevelDev>(),
-                           Cd, (const short4*)rects.as<short4>(), (const int*)rectCnt.as<int>(),
-                           nodeCapMax, L, lvkp.as<float4>(), kpCapFrame);
-        candDirty = false;  // node-best (or the octree on overflow) consumed every survivor
         mark(5, st);
         if (const int hrc = hook(5, st)) return hrc;
         // K6 orientation + rBRIEF

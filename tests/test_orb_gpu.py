@@ -121,6 +121,31 @@ def test_orb_level0_copy_switch(plvi_lib, monkeypatch):
         ext.close()
 
 
+def test_orb_octree_memory_scan_path(plvi_lib, monkeypatch):
+    """PLVI_ORB_OCT_LDS=0 sends every level's octree down the path used when a
+    level's candidate list exceeds the LDS stage (counts and node maxima by
+    scanning the list in memory instead of partitioned per-node ranges); both
+    paths give the oracle's outputs, on smooth frames and on binary noise."""
+    frames = np.concatenate([synth.batch(2, seed0=70),
+                             np.random.default_rng(9).integers(0, 256, size=(1, 480, 640), dtype=np.uint8)])
+    buf = plvi.DeviceBuffer(frames.nbytes)
+    buf.upload(frames)
+    for lds in ("0", "1536"):
+        monkeypatch.setenv("PLVI_ORB_OCT_LDS", lds)
+        ext = plvi.ORBextractor(1000, 1.2, 8, 20, 7, 640, 480, max_batch=3)
+        ext.extract_batch(buf.ptr, 3, 640 * 480, 640)
+        plvi_lib.plvi_device_synchronize()
+        kp_p, de_p, co_p, mo_p, cap = ext.outputs()
+        cnt = plvi.download(co_p, np.zeros(3, np.int32))
+        mono = plvi.download(mo_p, np.zeros(3, np.int32))
+        kps = plvi.download(kp_p, np.zeros(3 * cap, plvi.KEYPOINT_DTYPE))
+        desc = plvi.download(de_p, np.zeros((3 * cap, 32), np.uint8))
+        for k in range(3):
+            s = slice(k * cap, k * cap + cnt[k])
+            _assert_same((int(mono[k]), kps[s], desc[s]), ol.orb_extract(frames[k]), f"oct lds {lds} frame {k}")
+        ext.close()
+
+
 def test_orb_real_euroc_752(orb752):
     fr = real_frames()
     for k in ("euroc1", "euroc2"):
@@ -194,11 +219,11 @@ def _batch_tables(orb, batch):
     return [(int(mono[f]), kps[f * cap:f * cap + cnt[f]], desc[f * cap:f * cap + cnt[f]]) for f in range(n)]
 
 
-def test_orb_octree_overflow_leaves_candidate_plane_clean(plvi_lib):
+def test_orb_octree_overflow_then_normal_batch(plvi_lib):
     """An octree overflow (forced with the plvi_orb_debug_node_cap hook) flags
-    its frames and has no node list for orb_node_best_kernel to clear the
-    candidate plane from: the octree kernel zeroes the level's region itself.
-    The next normal batch through the same handle is the oracle's bit for bit."""
+    its frames and writes no level keypoints; the next normal batch through
+    the same handle (its candidate lists restart from zero) is the oracle's
+    bit for bit."""
     orb = plvi.ORBextractor(1000, 1.2, 8, 20, 7, 640, 480, max_batch=4)
     lib = plvi.load()
     noise = np.random.default_rng(5).integers(0, 256, size=(4, 480, 640), dtype=np.uint8)
@@ -214,9 +239,12 @@ def test_orb_octree_overflow_leaves_candidate_plane_clean(plvi_lib):
     orb.close()
 
 
-def test_orb_candidate_plane_reuse_across_batches(orb640):
-    """The candidate plane is cleared by the node-best pass that reads it, not filled per launch: a batch after a larger, candidate-dense one (binary noise) and a shorter batch after it must
-    still match the oracle frame by frame."""
+def test_orb_candidate_lists_reuse_across_batches(orb640):
+    """The NMS candidate lists (appended in arbitrary cell order, counted and
+    maximised per octree node, lists of the dense levels beyond the octree
+    wave's LDS read from memory) are reused across batches: a batch after a
+    larger, candidate-dense one (binary noise) and a shorter batch after it
+    must still match the oracle frame by frame."""
     noise = np.random.default_rng(3).integers(0, 256, size=(8, 480, 640), dtype=np.uint8)
     frames = synth.batch(8, seed0=40)
     for batch in (noise, frames[:3], frames[3:8], noise[:1], frames[:8]):
