@@ -734,16 +734,19 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
 // (r06: a whole 40-row window per round trip, 61 VGPRs, made the step 4 %
 // slower, profiles/r06/ab_nms_sat.txt)
 constexpr int kNmsRows = 8;
-// a candidate: .x = x | y << 11 | response << 21 (x < 2048, y < 1024 relative to
-// the octree region), .y = its rank in the reference's candidate order
-// (cell-row-major, raster within a cell; the node maximum's tie-break)
-__device__ __forceinline__ uint2 orb_cand_pack(int x, int y, int resp, const OrbLevelDev& lv) {
+// a candidate: x | y << 11 | response << 21 (x < 2048, y < 1024 relative to
+// the octree region)
+__device__ __forceinline__ uint32_t orb_cand_pack(int x, int y, int resp) {
+    return (uint32_t)x | (uint32_t)y << 11 | (uint32_t)resp << 21;
+}
+// its rank in the reference's candidate order (cell-row-major, raster within
+// a cell): the node maximum's tie-break, recomputed where it is needed
+__device__ __forceinline__ unsigned orb_cand_key(int x, int y, const OrbLevelDev& lv) {
     const unsigned ci = (unsigned)(y - 3) / (unsigned)lv.hCell, cj = (unsigned)(x - 3) / (unsigned)lv.wCell;
-    const unsigned key = ((ci * (unsigned)lv.nCols + cj) * (unsigned)lv.rh + (unsigned)y) * (unsigned)lv.rw + (unsigned)x;
-    return make_uint2((uint32_t)x | (uint32_t)y << 11 | (uint32_t)resp << 21, key);
+    return ((ci * (unsigned)lv.nCols + cj) * (unsigned)lv.rh + (unsigned)y) * (unsigned)lv.rw + (unsigned)x;
 }
 __device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, const OrbLevelDev* __restrict__ lvs,
-                                             const uint8_t* __restrict__ score, uint2* __restrict__ clist,
+                                             const uint8_t* __restrict__ score, uint32_t* __restrict__ clist,
                                              int listFrame, int* __restrict__ ccount, int L, int* __restrict__ err,
                                              int t1, int t2) {
     const OrbLevelDev& Lv = lvs[c.level];
@@ -812,18 +815,18 @@ __device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, co
     b0 = __shfl(b0, 0);
     if (lane == 0 && b0 + tot > Lv.listCap) atomicOr(err + f, 1);  // cannot happen: listCap bounds the survivors
     int pos = b0 + pre - nk;
-    uint2* out = clist + (size_t)f * listFrame + Lv.listOff;
+    uint32_t* out = clist + (size_t)f * listFrame + Lv.listOff;
     const int xr = c.x0 + lane - Lv.minB, yr0 = c.y0 - Lv.minB;
     for (unsigned long long kk = keep; incol && kk; kk &= kk - 1, ++pos) {
         const int r = __ffsll((long long)kk) - 1;
-        if (pos < Lv.listCap) out[pos] = orb_cand_pack(xr, yr0 + r, S[(size_t)r * w], Lv);
+        if (pos < Lv.listCap) out[pos] = orb_cand_pack(xr, yr0 + r, S[(size_t)r * w]);
     }
 }
 
 __global__ __launch_bounds__(64) void orb_cell_nms_kernel(const OrbCellDev* __restrict__ cells, int ncells,
                                                           const OrbLevelDev* __restrict__ lvs,
                                                           const uint8_t* __restrict__ score,
-                                                          uint2* __restrict__ clist, int listFrame,
+                                                          uint32_t* __restrict__ clist, int listFrame,
                                                           int* __restrict__ ccount, int L, int* __restrict__ err,
                                                           int t1, int t2) {
     PLVI_ORB_PRIO_SET();
@@ -864,7 +867,7 @@ __host__ __device__ inline size_t orb_octree_lds_nodes(int nodeCap) { return ((s
 __host__ __device__ inline size_t orb_octree_lds(int nodeCap, int lcap) { return orb_octree_lds_nodes(nodeCap) + 8 * (size_t)lcap; }
 
 __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __restrict__ lvs,
-                                                        const uint2* __restrict__ clist, int listFrame,
+                                                        const uint32_t* __restrict__ clist, int listFrame,
                                                         const int* __restrict__ ccount, float4* __restrict__ lvkp,
                                                         int kpCapFrame, int* __restrict__ out_cnt, int nodeCapMax,
                                                         int L, int* __restrict__ err, int lcap) {
@@ -877,7 +880,7 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
     const OrbLevelDev& lv = lvs[l];
     const int C = nodeCapMax;
     OctNodes n;
-    uint2* lcache;
+    uint32_t* lcache;
     {
         int* ip = reinterpret_cast<int*>(smem);
         n.cnt = ip; ip += C;
@@ -891,22 +894,22 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
         n.nxt = sp; sp += C; n.prv = sp; sp += C; n.freel = sp; sp += C;
         n.vsz = sp; sp += C; n.vprev = sp; sp += C; n.todo = sp; sp += C;
         n.nomore = reinterpret_cast<unsigned char*>(sp);
-        lcache = reinterpret_cast<uint2*>(smem + orb_octree_lds_nodes(C));
+        lcache = reinterpret_cast<uint32_t*>(smem + orb_octree_lds_nodes(C));
     }
     const int RW = lv.rw, RH = lv.rh;
     // the level's candidates: in LDS when they fit (the usual case), else read from memory
     const int K = min(ccount[(size_t)f * L + l], lv.listCap);
-    const uint2* G = clist + (size_t)f * listFrame + lv.listOff;
+    const uint32_t* G = clist + (size_t)f * listFrame + lv.listOff;
     const bool inLds = K <= lcap;
     // In LDS the candidates are kept partitioned like the reference's vKeys
     // (ORBextractor.cc:616-641 hands each child its own keys): every node owns
     // a range [beg, beg + cnt) of A, children are split off stably (T is the
     // scatter buffer), so a node's counts read only its own range.  The key
     // (candidate order) is recomputed from (x, y) where it is needed.
-    uint32_t* A = reinterpret_cast<uint32_t*>(lcache);
+    uint32_t* A = lcache;
     uint32_t* T = A + lcap;
     if (inLds)
-        for (int i = lane; i < K; i += 64) A[i] = G[i].x;
+        for (int i = lane; i < K; i += 64) A[i] = G[i];
     wave_sync();
     // stable split of [b, b + m) into groups 0..ng-1 (ng <= 8) of cls(entry);
     // group counts to cnt[], group starts to st[] (LDS)
@@ -946,7 +949,7 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
         int c = 0;
         for (int b = 0; b < K; b += 64) {
             const int i = b + lane;
-            const uint32_t e = i < K ? G[i].x : 0xFFFFFFFFu;
+            const uint32_t e = i < K ? G[i] : 0xFFFFFFFFu;
             const int x = (int)(e & 2047u), y = (int)((e >> 11) & 1023u);
             c += __popcll(__ballot(i < K && x >= x0 && x < x1 && y >= y0 && y < y1));
         }
@@ -972,7 +975,7 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
             int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
             for (int b = 0; b < K; b += 64) {
                 const int i = b + lane;
-                const uint32_t e = i < K ? G[i].x : 0xFFFFFFFFu;
+                const uint32_t e = i < K ? G[i] : 0xFFFFFFFFu;
                 const int x = (int)(e & 2047u), y = (int)((e >> 11) & 1023u);
                 const bool in = i < K && x >= mx0 && x < mx1 && y >= my0 && y < my1;
                 const bool left = x < xa, right = x >= xb, top = y < ya, bottom = y >= yb;
@@ -1154,7 +1157,7 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
             for (int i = b; i < b + m; ++i) {
                 const uint32_t e = A[i];
                 const int x = (int)(e & 2047u), y = (int)((e >> 11) & 1023u), resp = (int)(e >> 21);
-                const unsigned key = orb_cand_pack(x, y, 0, lv).y;
+                const unsigned key = orb_cand_key(x, y, lv);
                 const unsigned long long pk = ((unsigned long long)resp << 32) | (0xFFFFFFFFu - key);
                 if (pk > best) best = pk;
             }
@@ -1180,10 +1183,9 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
                 }
             }
             for (int i = 0; i < K; ++i) {
-                const uint2 e2 = G[i];
-                const uint32_t e = e2.x;
+                const uint32_t e = G[i];
                 const int x = (int)(e & 2047u), y = (int)((e >> 11) & 1023u), resp = (int)(e >> 21);
-                const unsigned long long pk = ((unsigned long long)resp << 32) | (0xFFFFFFFFu - e2.y);
+                const unsigned long long pk = ((unsigned long long)resp << 32) | (0xFFFFFFFFu - orb_cand_key(x, y, lv));
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
                     if (x >= bx0[k] && x < bx1[k] && y >= by0[k] && y < by1[k] && pk > best[k]) best[k] = pk;

@@ -380,7 +380,7 @@ struct OrbPipeline {
         PLVI_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax.data(), 16 * sizeof(int)));
         // work buffers
         if (pyr.alloc(off) || blur.alloc(boffAll) || score.alloc(boffAll) ||
-            clist.alloc(sizeof(uint2) * (size_t)listFrame * Bcap) || ccount.alloc(sizeof(int) * L * Bcap) ||
+            clist.alloc(sizeof(uint32_t) * (size_t)listFrame * Bcap) || ccount.alloc(sizeof(int) * L * Bcap) ||
             rectCnt.alloc(sizeof(int) * L * Bcap) || lvkp.alloc(sizeof(float4) * (size_t)kpCapFrame * Bcap) ||
             lvdesc.alloc((size_t)32 * kpCapFrame * Bcap) || okp.alloc(sizeof(plvi_keypoint) * (size_t)kpCapFrame * Bcap) ||
             odesc.alloc((size_t)32 * kpCapFrame * Bcap) || ocount.alloc(sizeof(int) * Bcap) ||
@@ -461,7 +461,7 @@ struct OrbPipeline {
         // K2 cell NMS -> the (frame, level) candidate lists
         hipLaunchKernelGGL(orb_cell_nms_kernel, dim3((unsigned)cells.size(), nf), dim3(64), 0, st,
                            d_cells.as<OrbCellDev>(), (int)cells.size(), d_lv.as<OrbLevelDev>(), (const uint8_t*)Sc,
-                           clist.as<uint2>(), listFrame, ccount.as<int>(), L, err.as<int>(), t1, t2);
+                           clist.as<uint32_t>(), listFrame, ccount.as<int>(), L, err.as<int>(), t1, t2);
         mark(2, st);
         if (const int hrc = hook(2, st)) return hrc;
         // (K3, the r01-r05 summed-area table of the candidate plane, is gone:
@@ -470,7 +470,7 @@ struct OrbPipeline {
         if (const int hrc = hook(3, st)) return hrc;
         // K4 octree + the best candidate of every node (K5 in r01-r05)
         hipLaunchKernelGGL(orb_octree_kernel, dim3(L, nf), dim3(64), octSmem, st, d_lv.as<OrbLevelDev>(),
-                           (const uint2*)clist.as<uint2>(), listFrame, (const int*)ccount.as<int>(), lvkp.as<float4>(),
+                           (const uint32_t*)clist.as<uint32_t>(), listFrame, (const int*)ccount.as<int>(), lvkp.as<float4>(),
                            kpCapFrame, rectCnt.as<int>(), nodeCapMax, L, err.as<int>(), octLcap);
         mark(4, st);
         if (const int hrc = hook(4, st)) return hrc;
