@@ -858,12 +858,11 @@ struct OctNodes {
     short *vsz, *vprev, *todo;
     int* ccnt;                     // [C][4] key counts of the four children (prefetched)
     int* beg;                      // [C] first entry of the node's range in the partitioned list
-    int* cbeg;                     // [C][4] first entries of the four children's ranges
     unsigned char* nomore;
 };
 constexpr int kOctListLds = 1536;  // candidates of a (frame, level) staged in LDS (more: read from the list in memory)
 // dynamic LDS of orb_octree_kernel: the node arrays, then the staged candidates
-__host__ __device__ inline size_t orb_octree_lds_nodes(int nodeCap) { return ((size_t)nodeCap * (11 * 4 + 14 * 2 + 1) + 15) & ~(size_t)15; }
+__host__ __device__ inline size_t orb_octree_lds_nodes(int nodeCap) { return ((size_t)nodeCap * (7 * 4 + 14 * 2 + 1) + 15) & ~(size_t)15; }
 __host__ __device__ inline size_t orb_octree_lds(int nodeCap, int lcap) { return orb_octree_lds_nodes(nodeCap) + 8 * (size_t)lcap; }
 
 __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __restrict__ lvs,
@@ -887,7 +886,6 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
         n.seq = ip; ip += C;
         n.ccnt = ip; ip += 4 * C;
         n.beg = ip; ip += C;
-        n.cbeg = ip; ip += 4 * C;
         short* sp = reinterpret_cast<short*>(ip);
         n.gx0 = sp; sp += C; n.gy0 = sp; sp += C; n.gx1 = sp; sp += C; n.gy1 = sp; sp += C;
         n.mx0 = sp; sp += C; n.my0 = sp; sp += C; n.mx1 = sp; sp += C; n.my1 = sp; sp += C;
@@ -912,8 +910,8 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
         for (int i = lane; i < K; i += 64) A[i] = G[i];
     wave_sync();
     // stable split of [b, b + m) into groups 0..ng-1 (ng <= 8) of cls(entry);
-    // group counts to cnt[], group starts to st[] (LDS)
-    auto partition = [&](int b, int m, int ng, auto cls, int* cnt, int* st) {
+    // group counts to cnt[] (LDS); group q starts at b + cnt[0] + ... + cnt[q-1]
+    auto partition = [&](int b, int m, int ng, auto cls, int* cnt) {
         int c[8];
 #pragma unroll
         for (int q = 0; q < 8; ++q) c[q] = 0;
@@ -927,7 +925,7 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             o[q] = acc;
-            if (q < ng) { cnt[q] = c[q]; st[q] = acc; acc += c[q]; }
+            if (q < ng) { cnt[q] = c[q]; acc += c[q]; }
         }
         for (int j = 0; j < m; j += 64) {
             const uint32_t e = j + lane < m ? A[b + j + lane] : 0u;
@@ -967,7 +965,7 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
                 // the node's range holds exactly its members: quadrant = (x >= midX) + 2 (y >= midY)
                 partition(n.beg[p], n.cnt[p], 4, [&](uint32_t e) {
                     return (int)((e & 2047u) >= (unsigned)midX) + 2 * (int)(((e >> 11) & 1023u) >= (unsigned)midY);
-                }, n.ccnt + 4 * p, n.cbeg + 4 * p);
+                }, n.ccnt + 4 * p);
                 continue;
             }
             const int mx0 = n.mx0[p], my0 = n.my0[p], mx1 = n.mx1[p], my1 = n.my1[p];
@@ -1014,8 +1012,8 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
         ++size;
     };
     // Initial nodes (ORBextractor.cc:541-583): push_back in order; empty erased.
-    // Partitioned: the roots' counts and starts are staged in ccnt / cbeg
-    // (free until the first prefetch).
+    // Partitioned: the roots' counts are staged in ccnt (free until the first
+    // prefetch).
     if (inLds)
         partition(0, K, lv.nIni, [&](uint32_t e) {
             const int x = (int)(e & 2047u);
@@ -1024,16 +1022,18 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
             for (int q = 0; q < kOrbMaxRoots; ++q)
                 if (q < lv.nIni && x >= lv.rootB[q] && x < lv.rootB[q + 1]) g = q;
             return g;
-        }, n.ccnt, n.cbeg);
+        }, n.ccnt);
+    int rb = 0;
     for (int i = 0; i < lv.nIni; ++i) {
         const int c = inLds ? n.ccnt[i] : count(lv.rootB[i], 0, lv.rootB[i + 1], RH);
-        const int rb = inLds ? n.cbeg[i] : 0;
+        const int cb = rb;
+        rb += c;
         if (c == 0) continue;
         const int k = alloc();
         if (k < 0) break;
         n.gx0[k] = (short)lv.rootGx[i]; n.gy0[k] = 0; n.gx1[k] = (short)lv.rootGx[i + 1]; n.gy1[k] = (short)RH;
         n.mx0[k] = (short)lv.rootB[i]; n.my0[k] = 0; n.mx1[k] = (short)lv.rootB[i + 1]; n.my1[k] = (short)RH;
-        n.cnt[k] = c; n.seq[k] = seqc++; n.nomore[k] = (c == 1); n.beg[k] = rb;
+        n.cnt[k] = c; n.seq[k] = seqc++; n.nomore[k] = (c == 1); n.beg[k] = cb;
         n.prv[k] = (short)tail; n.nxt[k] = -1;
         if (tail >= 0) n.nxt[tail] = (short)k; else head = k;
         tail = k;
@@ -1049,6 +1049,7 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
         int cc[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) cc[q] = n.ccnt[4 * p + q];
+        int cb = n.beg[p];  // the children's ranges follow each other in quadrant order
         for (int q = 0; q < 4; ++q) {
             int cx0, cy0, cx1, cy1, bx0, by0, bx1, by1;
             if (q == 0) { cx0 = x0; cy0 = y0; cx1 = midX; cy1 = midY; bx0 = mx0; by0 = my0; bx1 = min(mx1, midX); by1 = min(my1, midY); }
@@ -1056,12 +1057,13 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
             else if (q == 2) { cx0 = x0; cy0 = midY; cx1 = midX; cy1 = y1; bx0 = mx0; by0 = max(my0, midY); bx1 = min(mx1, midX); by1 = my1; }
             else { cx0 = midX; cy0 = midY; cx1 = x1; cy1 = y1; bx0 = max(mx0, midX); by0 = max(my0, midY); bx1 = mx1; by1 = my1; }
             const int c = cc[q];
+            cb += c;
             if (c == 0) continue;
             const int k = alloc();
             if (k < 0) return;
             n.gx0[k] = (short)cx0; n.gy0[k] = (short)cy0; n.gx1[k] = (short)cx1; n.gy1[k] = (short)cy1;
             n.mx0[k] = (short)bx0; n.my0[k] = (short)by0; n.mx1[k] = (short)bx1; n.my1[k] = (short)by1;
-            n.cnt[k] = c; n.seq[k] = seqc++; n.nomore[k] = (c == 1); n.beg[k] = n.cbeg[4 * p + q];
+            n.cnt[k] = c; n.seq[k] = seqc++; n.nomore[k] = (c == 1); n.beg[k] = cb - c;
             push_front(k);
             if (c > 1) {
                 if (nToExpand) ++*nToExpand;
