@@ -445,7 +445,7 @@ struct LinePipeline {
         // PLVI_GROW_MW = largest batch that takes it (default 256; 0 = off).
         mwMaxFrames = 256;
         if (const char* e = getenv("PLVI_GROW_MW")) mwMaxFrames = atoi(e);
-        if (const char* e = getenv("PLVI_GROW_TPW")) growTPW = std::max(1, atoi(e));
+        if (const char* e = getenv("PLVI_GROW_TPW")) growTPW = std::max(0, atoi(e));
         mwMaxFrames = std::min(mwMaxFrames, Bcap);
         if (mwMaxFrames > 0) {
             // LDS: ctl + dispatch log + C/T/H bitmaps + own windows + growth
@@ -487,13 +487,16 @@ struct LinePipeline {
     // and octave 1 of a frame in one wave, half the resident growth waves
     // (3 per SIMD at 3072 frames instead of 6, so the two batches in flight
     // can grow at once and blur + FAST shares a SIMD with 3 growth waves
-    // instead of 6).  Default 2 in the frame schedule (run_with_orb) from
-    // 2048 frames (at least two waves per SIMD remain), else 1 -- a lines-only
-    // batch alone on the chip grows faster with every task in its own wave
-    // (30 vs 40 ms at 3072 frames); PLVI_GROW_TPW forces a value.  Step
-    // 52.9-53.0K -> 53.0-53.3K FPS, blur + FAST in the timed window 15-17 ->
-    // 10-12 ms (profiles/r06/ab_knn_tpw.txt)
-    int growTPW = 0;  // 0: the rule above
+    // instead of 6).  PLVI_GROW_TPW=0 selects the rule: 2 in the frame
+    // schedule (run_with_orb) from 2048 frames, else 1 -- a lines-only batch
+    // alone on the chip grows faster with every task in its own wave (30 vs
+    // 40 ms at 3072 frames).  The rule was the default while the ORB chain
+    // was the longer chain of a slot (52.9-53.0K -> 53.0-53.3K FPS, blur +
+    // FAST in the timed window 15-17 -> 10-12 ms, profiles/r06/ab_knn_tpw.txt);
+    // after the candidate-list ORB middle the line chain is the longer one
+    // and one task per wave is faster again (54.9K -> 55.9K FPS, blur + FAST
+    // in the window 12 -> 16-17 ms, profiles/r06/ab_resweep.txt): default 1
+    int growTPW = 1;  // 0: the rule above
     bool inSchedule = false;  // run_with_orb is issuing
     int growR = 0, growRB = 0, growQL = 0;
     unsigned long long* growStats = nullptr;  // diagnostic cycle counters (plvi_lines_debug_stats)

@@ -126,3 +126,28 @@ def test_lines_grow_window_budgets(plvi_lib, monkeypatch, lds, rb, rd):
 def test_lines_structured_extremes(lx640, name):
     img = structured_frames()[name]
     _assert_same(lx640(img), ol.line_extract(img), name)
+
+
+@pytest.mark.parametrize("tpw", ["2", "0"])
+def test_lines_grow_tasks_per_wave(plvi_lib, monkeypatch, tpw):
+    """PLVI_GROW_TPW=2 runs two growth tasks per wave of the large-batch kernel
+    (octave 0 then octave 1 of a frame, the LOOP form); 0 selects the r06
+    in-schedule rule.  Either gives the oracle's lines (odd batch: the last
+    wave holds one task)."""
+    monkeypatch.setenv("PLVI_GROW_MW", "0")
+    monkeypatch.setenv("PLVI_GROW_TPW", tpw)
+    lx = plvi.Lineextractor(200, 0, 0.8, 2, 2.0, 0, 640, 480, max_batch=3)
+    frames = synth.batch(3, seed0=80)
+    buf = plvi.DeviceBuffer(frames.nbytes)
+    buf.upload(frames)
+    lx.extract_batch(buf.ptr, 3, 640 * 480, 640)
+    plvi.load().plvi_device_synchronize()
+    klp, dep, fnp, cop, cap = lx.outputs()
+    cnt = plvi.download(cop, np.zeros(3, np.int32))
+    kl = plvi.download(klp, np.zeros(3 * cap, plvi.KEYLINE_DTYPE))
+    de = plvi.download(dep, np.zeros((3 * cap, 32), np.uint8))
+    fn = plvi.download(fnp, np.zeros((3 * cap, 3), np.float64))
+    for f in range(3):
+        s = slice(f * cap, f * cap + cnt[f])
+        _assert_same((kl[s], de[s], fn[s]), ol.line_extract(frames[f]), f"tpw {tpw} frame {f}")
+    assert lx.errors() == 0
