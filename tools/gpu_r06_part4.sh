@@ -1,0 +1,12 @@
+#!/bin/bash
+# r06: octree quadrant split of ranges <= 256 entries in registers, in place
+# (in-tree) vs HEAD (variants/head): ORB parity subset, ORB-only chain, headline A/B
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests -m gpu -q -x --timeout 240 --timeout-method thread -k "orb or frame or stereo" > gpurun_out/r06_part4_tests.log 2>&1; rc=$?; tail -1 gpurun_out/r06_part4_tests.log; [ $rc -eq 0 ] || { grep -E "^E |FAILED" gpurun_out/r06_part4_tests.log | head -20; exit $rc; }
+for v in head -; do
+  if [ $v = - ]; then unset PLVI_LIB; else export PLVI_LIB=$R/pl-vi-orbslam3_amd/variants/$v/libplvi_frontend.so; fi
+  echo "== $v"; timeout -k 10 200 python -u tools/pyr_probe.py 3072 0 2>&1 | grep -v amdgpu.ids | head -1 || exit 1
+done
+unset PLVI_LIB
+CONFIGS="head|head|-;part4|-|-" REPS=3 bash tools/ab_mix.sh
