@@ -178,26 +178,30 @@ struct LinePipeline {
             PLVI_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
             const char* e1 = getenv("PLVI_STREAM_PRIO");
             const bool prio = !e1 || atoi(e1) != 0;
-            // PLVI_ORB_AFTER_PREP: ORB waits for the LSD prep -- 1 (default) in
-            // batches below 1024 frames, 2 in every batch, 0 never.  With one
-            // 3072-frame batch in flight waiting is ~1 % faster (the pyramid
-            // otherwise ends while the prep still runs and blur + FAST shares
-            // the CUs with it); with two in flight (bench default) starting ORB
-            // at once is 2-3 % faster (47.9K vs 46.6K FPS, 47.3K vs 46.2K,
-            // profiles/r04/ab_sched_inflight2.txt): the next batch's pyramid and
-            // blur + FAST no longer wait for its prep while the other batch grows
+            // PLVI_ORB_AFTER_PREP: ORB waits for the LSD prep -- 1 in batches
+            // below 1024 frames, 2 (default since late r06) in every batch, 0
+            // never.  In r04, with two 3072-frame batches in flight, starting
+            // ORB at once was 2-3 % faster (profiles/r04/ab_sched_inflight2.txt);
+            // since the ORB chain is the busier one (one growth task per wave,
+            // r06) waiting is level on the step and, with the ORB stream at the
+            // least priority (below), blur + FAST runs 2x shorter in the window
+            // (profiles/r06/ab_sched_orbprio.txt)
             const char* e2 = getenv("PLVI_ORB_AFTER_PREP");
-            orbAfterPrep = e2 ? atoi(e2) : 1;
+            orbAfterPrep = e2 ? atoi(e2) : 2;
             // PLVI_GROW_AFTER_BLUR=0: region growing starts right after the prep
             // (default 1: it waits for the ORB blur + FAST launch, whose 81-VGPR /
             // 9 KB-LDS waves cannot share a CU with the region-growing waves; the
             // rest of the ORB chain then runs alongside region growing)
             const char* e3 = getenv("PLVI_GROW_AFTER_BLUR");
             growAfterBlur = !e3 || atoi(e3) != 0;
-            // PLVI_ORB_PRIO (default 1): the ORB stream at the greatest priority as
-            // well (its pyramid + blur gate region growing from 1024 frames on)
+            // PLVI_ORB_PRIO=1: the ORB stream at the greatest priority as well
+            // (its pyramid + blur gate region growing from 1024 frames on; the
+            // default until late r06).  Default 0 (least priority) with ORB
+            // after the prep: same step (56.8K vs 56.5K FPS over 3 pairs), blur +
+            // FAST 8-10 instead of 16-22 ms in the window
+            // (profiles/r06/ab_sched_orbprio.txt)
             const char* e4 = getenv("PLVI_ORB_PRIO");
-            const bool orbHigh = !e4 || atoi(e4) != 0;
+            const bool orbHigh = e4 && atoi(e4) != 0;
             for (int a = 0; a < 2; ++a)
                 PLVI_CHECK(hipStreamCreateWithPriority(&aux[a], hipStreamNonBlocking,
                                                        prio ? (a == 0 && orbHigh ? greatest : least) : 0));
