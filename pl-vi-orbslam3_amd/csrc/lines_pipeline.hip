@@ -195,13 +195,14 @@ struct LinePipeline {
             const char* e3 = getenv("PLVI_GROW_AFTER_BLUR");
             growAfterBlur = !e3 || atoi(e3) != 0;
             // PLVI_ORB_PRIO=1: the ORB stream at the greatest priority as well
-            // (its pyramid + blur gate region growing from 1024 frames on; the
-            // default until late r06).  Default 0 (least priority) with ORB
-            // after the prep: same step (56.8K vs 56.5K FPS over 3 pairs), blur +
-            // FAST 8-10 instead of 16-22 ms in the window
-            // (profiles/r06/ab_sched_orbprio.txt)
+            // (its pyramid + blur gate region growing from 1024 frames on).
+            // Default: greatest for handles of fewer than 1024 frames (batch 64:
+            // 8.2K FPS at the least priority against 8.6K), least for the large
+            // ones -- with ORB after the prep the same step (56.8K vs 56.5K FPS
+            // over 3 pairs) and blur + FAST 8-10 instead of 16-22 ms in the
+            // window (profiles/r06/ab_sched_orbprio.txt)
             const char* e4 = getenv("PLVI_ORB_PRIO");
-            const bool orbHigh = e4 && atoi(e4) != 0;
+            const bool orbHigh = e4 ? atoi(e4) != 0 : Bcap < 1024;
             for (int a = 0; a < 2; ++a)
                 PLVI_CHECK(hipStreamCreateWithPriority(&aux[a], hipStreamNonBlocking,
                                                        prio ? (a == 0 && orbHigh ? greatest : least) : 0));
