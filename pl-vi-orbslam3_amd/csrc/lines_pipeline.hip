@@ -178,31 +178,29 @@ struct LinePipeline {
             PLVI_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
             const char* e1 = getenv("PLVI_STREAM_PRIO");
             const bool prio = !e1 || atoi(e1) != 0;
-            // PLVI_ORB_AFTER_PREP: ORB waits for the LSD prep -- 1 in batches
-            // below 1024 frames, 2 (default since late r06) in every batch, 0
-            // never.  In r04, with two 3072-frame batches in flight, starting
-            // ORB at once was 2-3 % faster (profiles/r04/ab_sched_inflight2.txt);
-            // since the ORB chain is the busier one (one growth task per wave,
-            // r06) waiting is level on the step and, with the ORB stream at the
-            // least priority (below), blur + FAST runs 2x shorter in the window
+            // PLVI_ORB_AFTER_PREP: ORB waits for the LSD prep -- 1 (default) in
+            // batches below 1024 frames, 2 in every batch, 0 never.  In r04,
+            // with two 3072-frame batches in flight, starting ORB at once was
+            // 2-3 % faster (profiles/r04/ab_sched_inflight2.txt); in late r06
+            // (one growth task per wave) 2 was level on the step
             // (profiles/r06/ab_sched_orbprio.txt)
             const char* e2 = getenv("PLVI_ORB_AFTER_PREP");
-            orbAfterPrep = e2 ? atoi(e2) : 2;
+            orbAfterPrep = e2 ? atoi(e2) : 1;
             // PLVI_GROW_AFTER_BLUR=0: region growing starts right after the prep
             // (default 1: it waits for the ORB blur + FAST launch, whose 81-VGPR /
             // 9 KB-LDS waves cannot share a CU with the region-growing waves; the
             // rest of the ORB chain then runs alongside region growing)
             const char* e3 = getenv("PLVI_GROW_AFTER_BLUR");
             growAfterBlur = !e3 || atoi(e3) != 0;
-            // PLVI_ORB_PRIO=1: the ORB stream at the greatest priority as well
-            // (its pyramid + blur gate region growing from 1024 frames on).
-            // Default: greatest for handles of fewer than 1024 frames (batch 64:
-            // 8.2K FPS at the least priority against 8.6K), least for the large
-            // ones -- with ORB after the prep the same step (56.8K vs 56.5K FPS
-            // over 3 pairs) and blur + FAST 8-10 instead of 16-22 ms in the
-            // window (profiles/r06/ab_sched_orbprio.txt)
+            // PLVI_ORB_PRIO (default 1): the ORB stream at the greatest priority as
+            // well (its pyramid + blur gate region growing from 1024 frames on).
+            // r06: 0 (least) with ORB after the prep gives the same headline
+            // step and blur + FAST 8-10 instead of 16-22 ms in the window, but
+            // a batch-64 pair created later in the same process then steps in
+            // 7.9 instead of 7.45 ms -- even with its own ORB stream at the
+            // greatest priority (profiles/r06/ab_sched_orbprio.txt); kept at 1
             const char* e4 = getenv("PLVI_ORB_PRIO");
-            const bool orbHigh = e4 ? atoi(e4) != 0 : Bcap < 1024;
+            const bool orbHigh = !e4 || atoi(e4) != 0;
             for (int a = 0; a < 2; ++a)
                 PLVI_CHECK(hipStreamCreateWithPriority(&aux[a], hipStreamNonBlocking,
                                                        prio ? (a == 0 && orbHigh ? greatest : least) : 0));
