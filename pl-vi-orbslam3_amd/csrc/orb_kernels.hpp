@@ -734,6 +734,13 @@ __global__ __launch_bounds__(64) void orb_blur_fast_kernel(const OrbLevelDev* __
 // (r06: a whole 40-row window per round trip, 61 VGPRs, made the step 4 %
 // slower, profiles/r06/ab_nms_sat.txt)
 constexpr int kNmsRows = 8;
+// the (frame, level) candidate counters, one per 128-byte line: the NMS waves
+// of a level (~300 at level 0) all add to theirs, and packed counters put two
+// frames' levels on one line, whose atomics the L2 serialises
+#ifndef PLVI_COUNT_PAD
+#define PLVI_COUNT_PAD 32
+#endif
+constexpr int kOrbCountPad = PLVI_COUNT_PAD;
 // a candidate: x | y << 11 | response << 21 (x < 2048, y < 1024 relative to
 // the octree region)
 __device__ __forceinline__ uint32_t orb_cand_pack(int x, int y, int resp) {
@@ -811,7 +818,7 @@ __device__ __forceinline__ void orb_nms_cell(const OrbCellDev c, const int f, co
     const int tot = __shfl(pre, 63);
     if (tot == 0) return;
     int b0 = 0;
-    if (lane == 0) b0 = atomicAdd(ccount + (size_t)f * L + c.level, tot);
+    if (lane == 0) b0 = atomicAdd(ccount + ((size_t)f * L + c.level) * kOrbCountPad, tot);
     b0 = __shfl(b0, 0);
     if (lane == 0 && b0 + tot > Lv.listCap) atomicOr(err + f, 1);  // cannot happen: listCap bounds the survivors
     int pos = b0 + pre - nk;
@@ -896,7 +903,7 @@ __global__ __launch_bounds__(64) void orb_octree_kernel(const OrbLevelDev* __res
     }
     const int RW = lv.rw, RH = lv.rh;
     // the level's candidates: in LDS when they fit (the usual case), else read from memory
-    const int K = min(ccount[(size_t)f * L + l], lv.listCap);
+    const int K = min(ccount[((size_t)f * L + l) * kOrbCountPad], lv.listCap);
     const uint32_t* G = clist + (size_t)f * listFrame + lv.listOff;
     const bool inLds = K <= lcap;
     // In LDS the candidates are kept partitioned like the reference's vKeys

@@ -380,7 +380,7 @@ struct OrbPipeline {
         PLVI_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_umax), umax.data(), 16 * sizeof(int)));
         // work buffers
         if (pyr.alloc(off) || blur.alloc(boffAll) || score.alloc(boffAll) ||
-            clist.alloc(sizeof(uint32_t) * (size_t)listFrame * Bcap) || ccount.alloc(sizeof(int) * L * Bcap) ||
+            clist.alloc(sizeof(uint32_t) * (size_t)listFrame * Bcap) || ccount.alloc(sizeof(int) * kOrbCountPad * L * Bcap) ||
             rectCnt.alloc(sizeof(int) * L * Bcap) || lvkp.alloc(sizeof(float4) * (size_t)kpCapFrame * Bcap) ||
             lvdesc.alloc((size_t)32 * kpCapFrame * Bcap) || okp.alloc(sizeof(plvi_keypoint) * (size_t)kpCapFrame * Bcap) ||
             odesc.alloc((size_t)32 * kpCapFrame * Bcap) || ocount.alloc(sizeof(int) * Bcap) ||
@@ -410,7 +410,7 @@ struct OrbPipeline {
         uint8_t* Bl = blur.as<uint8_t>();
         uint8_t* Sc = score.as<uint8_t>();
         // the NMS appends to the (frame, level) candidate lists from zero
-        PLVI_CHECK(hipMemsetAsync(ccount.p, 0, sizeof(int) * (size_t)L * nf, st));
+        PLVI_CHECK(hipMemsetAsync(ccount.p, 0, sizeof(int) * kOrbCountPad * (size_t)L * nf, st));
         mark(0, st);
         auto hook = [&](int k, hipStream_t s_) {
             if (evAfterBlur && gateStage == k) PLVI_CHECK(hipEventRecord(evAfterBlur, s_));
