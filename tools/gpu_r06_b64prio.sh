@@ -3,7 +3,7 @@
 # (default: least for >= 1024-frame handles; PLVI_ORB_PRIO=1: greatest for all)
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
-for rep in 1 2; do
+for rep in ${B64_REPS:-1 2}; do
   for c in ${B64_CONFIGS:-"-" "PLVI_ORB_PRIO=1"}; do
     e=$c; [ "$e" = "-" ] && e=""
     env $e timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/b64p.json 2> gpurun_out/b64p.err || { tail -3 gpurun_out/b64p.err; exit 1; }
