@@ -469,7 +469,7 @@ struct OrbPipeline {
         mark(3, st);
         if (const int hrc = hook(3, st)) return hrc;
         // K4 octree + the best candidate of every node (K5 in r01-r05)
-        hipLaunchKernelGGL(orb_octree_kernel, dim3(L, nf), dim3(64), octSmem, st, d_lv.as<OrbLevelDev>(),
+        hipLaunchKernelGGL(orb_octree_kernel, dim3(nf, L), dim3(64), octSmem, st, d_lv.as<OrbLevelDev>(),
                            (const uint32_t*)clist.as<uint32_t>(), listFrame, (const int*)ccount.as<int>(), lvkp.as<float4>(),
                            kpCapFrame, rectCnt.as<int>(), nodeCapMax, L, err.as<int>(), octLcap);
         mark(4, st);
