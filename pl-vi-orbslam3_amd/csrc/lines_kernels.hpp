@@ -830,8 +830,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(U <= 4 ? 8 
                                                              size_t regpts_frame, const int* __restrict__ nlines,
                                                              double prec, double scale_lsd,
                                                              LsdLine* __restrict__ lines, int oBase, int nOct) {
-    // octaves oBase .. oBase + gridDim.y - 1 of nOct
-    const int o = oBase + blockIdx.y, f = blockIdx.z;
+    // octaves oBase .. oBase + gridDim.z - 1 of nOct; grid (blocks, frames,
+    // octaves): every frame's octave 0 (the most regions) is dispatched
+    // before the octave-1 blocks, which fill the tail
+    const int o = oBase + blockIdx.z, f = blockIdx.y;
     const int task = f * nOct + o;
     const int n = min(nlines[task], kLsdRawCap);
     const LineOctDev& od = octs[o];

@@ -602,7 +602,7 @@ struct LinePipeline {
     void launch_rect(int nf, int oBase, int oCount, hipStream_t st) {
         const int bx = nf <= 16 ? 8 : kRectLaneBlocks;
         auto rectK = nf <= kRectSmallNf ? lsd_rect_lanes_kernel<kRectUSmall> : lsd_rect_lanes_kernel<kRectU>;
-        hipLaunchKernelGGL(rectK, dim3(bx, oCount, nf), dim3(256), 0, st, d_oct.as<LineOctDev>(),
+        hipLaunchKernelGGL(rectK, dim3(bx, nf, oCount), dim3(256), 0, st, d_oct.as<LineOctDev>(),
                            (const double*)modg.as<double>(), (const LsdRegion*)regs.as<LsdRegion>(),
                            (const unsigned*)regpts.as<unsigned>(), qspillFrame, (const int*)nlines.as<int>(), prec,
                            SCALE, rawLines.as<LsdLine>(), oBase, nOct);
