@@ -8,7 +8,11 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 marks = [i for i, r in enumerate(rows) if "spin_kernel" in r["Kernel_Name"]]
 timed = rows[marks[0] + 1:marks[1]]
-starts = [i for i, r in enumerate(timed) if "lsd_half_kernel" in r["Kernel_Name"]]
+# one slot's period: from one of its lsd_half launches to its next (the
+# other slot's launches fall in between with two batches in flight)
+halves = [i for i, r in enumerate(timed) if "lsd_half_kernel" in r["Kernel_Name"]]
+q0 = timed[halves[0]]["Queue_Id"]
+starts = [i for i in halves if timed[i]["Queue_Id"] == q0]
 k = int(sys.argv[2]) if len(sys.argv) > 2 else len(starts) // 2
 i0, i1 = starts[k], starts[k + 1] if k + 1 < len(starts) else len(timed)
 t0 = int(timed[i0]["Start_Timestamp"])
