@@ -496,7 +496,7 @@ SCHEDULE_ENV = ("PLVI_STREAM_PRIO", "PLVI_ORB_AFTER_PREP", "PLVI_GROW_AFTER_BLUR
 
 def schedule_knobs(batch):
     env = {k: os.environ[k] for k in SCHEDULE_ENV if k in os.environ}
-    after_prep = int(os.environ.get("PLVI_ORB_AFTER_PREP", "1"))
+    after_prep = int(os.environ.get("PLVI_ORB_AFTER_PREP", "2"))
     big = batch >= 1024
     return {"env": env,
             "orb_waits_for_lsd_prep": after_prep >= 2 or (after_prep == 1 and batch < 1024),

@@ -178,14 +178,15 @@ struct LinePipeline {
             PLVI_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
             const char* e1 = getenv("PLVI_STREAM_PRIO");
             const bool prio = !e1 || atoi(e1) != 0;
-            // PLVI_ORB_AFTER_PREP: ORB waits for the LSD prep -- 1 (default) in
-            // batches below 1024 frames, 2 in every batch, 0 never.  In r04,
-            // with two 3072-frame batches in flight, starting ORB at once was
-            // 2-3 % faster (profiles/r04/ab_sched_inflight2.txt); in late r06
-            // (one growth task per wave) 2 was level on the step
-            // (profiles/r06/ab_sched_orbprio.txt)
+            // PLVI_ORB_AFTER_PREP: ORB waits for the LSD prep -- 1 in batches
+            // below 1024 frames, 2 (default since late r06) in every batch, 0
+            // never.  In r04, with two 3072-frame batches in flight, starting
+            // ORB at once was 2-3 % faster (profiles/r04/ab_sched_inflight2.txt);
+            // at the end of r06 (one growth task per wave, ORB the busier chain)
+            // waiting is +0.2-0.6 % over two A/Bs and blur + FAST's in-window
+            // time steadier (profiles/r06/ab_sched_orbprio.txt, ab_final_knobs.txt)
             const char* e2 = getenv("PLVI_ORB_AFTER_PREP");
-            orbAfterPrep = e2 ? atoi(e2) : 1;
+            orbAfterPrep = e2 ? atoi(e2) : 2;
             // PLVI_GROW_AFTER_BLUR=0: region growing starts right after the prep
             // (default 1: it waits for the ORB blur + FAST launch, whose 81-VGPR /
             // 9 KB-LDS waves cannot share a CU with the region-growing waves; the
